@@ -1,0 +1,171 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself
+(tools/goldens/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import graph as og
+from oracle import layers as ol
+from oracle import model as om
+from oracle import ops
+
+C = 0.01
+
+
+def close(a, b, tol=1e-4):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    err = np.abs(a - b) / np.maximum(1.0, np.abs(b))
+    assert err.max() <= tol, err.max()
+
+
+@pytest.mark.parametrize("tag", ["small", "mid", "empty_rel"])
+def test_graph_indexing(golden, tag):
+    z = golden("graph_indexing.npz")
+    V, R = z[tag + "_meta"]
+    g = og.build_sub_graph(int(V), int(R), z[tag + "_triples"])
+    for k in ("src", "dst", "type", "in_deg", "uniq_r", "r_len"):
+        np.testing.assert_array_equal(g[k], z[tag + "_" + k], err_msg=k)
+    np.testing.assert_array_equal(g["norm"], z[tag + "_norm"])
+    np.testing.assert_array_equal(g["enorm"], z[tag + "_enorm"])
+    for a, b in g["r_len"]:
+        assert set(g["r_to_e"][a:b].tolist()) == set(z[tag + "_r_to_e"][a:b].tolist())
+
+
+@pytest.mark.parametrize("cname,c", [("c01", 0.01), ("c05", 0.05)])
+def test_ops(golden, cname, c):
+    z = golden("ops.npz")
+    x, v, y, rad = (torch.from_numpy(z[cname + k]) for k in ("_x", "_v", "_y", "_rad"))
+    close(ops.project(x, c), z[cname + "_project"])
+    close(ops.log0(x, c), z[cname + "_log0"])
+    close(ops.exp0(v, c), z[cname + "_exp0"])
+    xb = ops.project(x, c)
+    close(ops.mobius_add(xb, y, c), z[cname + "_mobius"])
+    close(ops.hyperbolic_distance(xb, y, c), z[cname + "_dist"])
+    close(ops.get_radius(x), z[cname + "_radius"])
+    close(ops.apply_radius(y, rad, c), z[cname + "_apply_radius"])
+    L = ops.to_lorentz(y, c)
+    close(L, z[cname + "_to_lorentz"])
+    close(ops.to_poincare(L, c), z[cname + "_to_poincare"])
+    close(ops.lorentz_centroid(L, torch.from_numpy(z[cname + "_w"]), c), z[cname + "_centroid"])
+
+
+def _graph(z, prefix=""):
+    V, R = int(z[prefix + "meta"][0]), int(z[prefix + "meta"][1])
+    return og.build_sub_graph(V, R, z[prefix + "triples"])
+
+
+@pytest.mark.parametrize("gname,gamma", [("g0", 0.0), ("g15", 0.15)])
+@pytest.mark.parametrize("skip", [False, True])
+def test_union_layer(golden, gname, gamma, skip):
+    z = golden("layer_union.npz")
+    g = _graph(z)
+    t = lambda k: torch.from_numpy(z[k])  # noqa: E731
+    sk = (t("w_skip_weight"), t("w_skip_bias"), t("prev_h")) if skip else None
+    y = ol.union_layer(g, t("h"), t("rel"), t("w_weight_neighbor"), t("w_loop_weight"),
+                       t("w_evolve_loop_weight"), C, gamma, skip=sk)
+    close(y, z["%s_%s_out" % (gname, "skip" if skip else "noskip")])
+
+
+def test_euclid_layer(golden):
+    z = golden("layer_euclid.npz")
+    g = _graph(z)
+    t = lambda k: torch.from_numpy(z[k])  # noqa: E731
+    y = ol.euclid_union_layer(g, t("h"), t("rel"), t("w_weight_neighbor"), t("w_loop_weight"),
+                              t("w_evolve_loop_weight"))
+    close(y, z["out"])
+
+
+@pytest.mark.parametrize("tag,skip", [("s2", False), ("s2", True), ("s4", False), ("s1", False),
+                                      ("s20", False)])
+def test_lorentz_layer(golden, tag, skip):
+    z = golden("layer_lorentz.npz")
+    g = _graph(z, tag + "_")
+    t = lambda k: torch.from_numpy(z[tag + "_" + k])  # noqa: E731
+    V, R, d, nb = (int(v) for v in z[tag + "_meta"])
+    nb = min(nb, 2 * R)
+    sk = (t("w_skip_weight"), t("w_skip_bias"), t("prev_h")) if skip else None
+    y = ol.lorentz_layer(g, t("h"), t("rel"), t("w_weight"), t("w_loop_weight"),
+                         t("w_evolve_loop_weight"), C, nb, skip=sk)
+    close(y, z[tag + ("_skip" if skip else "_noskip") + "_out"])
+
+
+MODEL_CASES = {
+    "uvrgcn_roth": dict(encoder="hyperbolic_uvrgcn", decoder="roth", layer_norm=False),
+    "uvrgcn_roth_ln": dict(encoder="hyperbolic_uvrgcn", decoder="roth", layer_norm=True),
+    "lgcn_roth": dict(encoder="lgcn", decoder="roth", layer_norm=False),
+    "lgcn_roth_ln": dict(encoder="lgcn", decoder="roth", layer_norm=True),
+    "uvrgcn_murp_nores": dict(encoder="hyperbolic_uvrgcn", decoder="murp", layer_norm=False,
+                              use_residual_evolution=False),
+    "uvrgcn_atth_beta": dict(encoder="hyperbolic_uvrgcn", decoder="atth", layer_norm=True,
+                             radius_anchor_beta=0.5),
+    "lgcn_roth_bias_crel": dict(encoder="lgcn", decoder="roth", layer_norm=False),
+    "uvrgcn_convtranse": dict(encoder="hyperbolic_uvrgcn", decoder="hyperbolic_convtranse",
+                              layer_norm=True),
+}
+
+
+def model_cfg(tag, d):
+    cfg = dict(c=C, n_layers=2, n_bases=d // 2, radius_min=0.5, radius_max=3.0, radius_epsilon=0.1,
+               radius_anchor_beta=1.0, radius_msg_gamma=0.15, use_residual_evolution=True)
+    cfg.update(MODEL_CASES[tag])
+    return cfg
+
+
+def load_model_case(z):
+    sd = {k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("sd_")}
+    V, R, d, T = (int(v) for v in z["meta"])
+    glist = [og.build_sub_graph(V, R, z["snap%d" % t]) for t in range(T)]
+    return sd, glist, torch.from_numpy(z["test"]), (V, R, d, T)
+
+
+@pytest.mark.parametrize("tag", list(MODEL_CASES))
+def test_hyperbolic_model(golden, tag):
+    z = golden("model_%s.npz" % tag)
+    sd, glist, test, (V, R, d, T) = load_model_case(z)
+    all_tr, score, score_rel, embs, h0 = om.hyperbolic_predict(sd, model_cfg(tag, d), glist, test)
+    np.testing.assert_array_equal(all_tr.numpy(), z["all_triples"])
+    close(torch.stack(embs), z["embs"])
+    close(h0, z["h0"])
+    close(score, z["score"])
+    close(score_rel, z["score_rel"])
+
+
+@pytest.mark.parametrize("tag", ["noln", "ln"])
+def test_euclid_model(golden, tag):
+    z = golden("rrgcn_%s.npz" % tag)
+    sd, glist, test, (V, R, d, T) = load_model_case(z)
+    cfg = dict(layer_norm=(tag == "ln"), n_layers=2)
+    all_tr, score, score_rel, embs, h0 = om.euclid_predict(sd, cfg, glist, test)
+    close(torch.stack(embs), z["embs"])
+    close(h0, z["h0"])
+    close(score, z["score"])
+    close(score_rel, z["score_rel"])
+
+
+def test_score_and_ce(golden):
+    z = golden("score.npz")
+    t = lambda k: torch.from_numpy(z[k])  # noqa: E731
+    q, e, bias, scale, margin = t("q"), t("e"), t("bias"), t("scale"), t("margin")
+    close(om.dist_score(q, e, None, C), z["score_plain"])
+    close(om.dist_score(q, e, bias, C, scale, margin), z["score_bias"])
+    close(om.dist_score(q, e, bias, C, scale, margin, t("c_r"), True), z["score_crel"])
+    close(om.dist_score(q, e, None, C, scale, margin, None, True), z["score_dist"])
+    close(om.ce_loss(q, e, t("target"), C, bias, scale, margin), z["ce_bias"])
+    close(om.ce_loss(q, e, t("target"), C, bias, scale, margin, t("c_r"), True), z["ce_crel"])
+
+
+def test_rank(golden):
+    z = golden("rank.npz")
+    V, R = (int(v) for v in z["meta"])
+    tr = torch.from_numpy(z["all_triples"])
+    ans_e = om.answers_for_filter(z["snap"], R, False)
+    ans_r = om.answers_for_filter(z["snap"], R, True)
+    mf, m, rank, frank = om.total_rank(tr, torch.from_numpy(z["score"]), ans_e)
+    np.testing.assert_array_equal(rank.numpy(), z["rank"])
+    np.testing.assert_array_equal(frank.numpy(), z["frank"])
+    mfr, mr, rank_r, frank_r = om.total_rank(tr, torch.from_numpy(z["score_rel"]), ans_r, True)
+    np.testing.assert_array_equal(rank_r.numpy(), z["rank_r"])
+    np.testing.assert_array_equal(frank_r.numpy(), z["frank_r"])
+    np.testing.assert_allclose([m, mf, mr, mfr], z["mrr"], rtol=1e-6)

@@ -1,0 +1,410 @@
+"""Generate golden input/output vectors by running the REFERENCE code on CPU.
+
+CONTAINER ONLY.  This script imports the read-only reference tree at
+/root/reference (through the test-only DGL stand-in in ./standin) and writes
+small .npz fixtures into tests/golden/.  The fixtures are data (inputs and the
+reference's outputs); no reference source travels with them.  Nothing on the
+GPU box runs this script.
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tools/goldens/make_golden.py
+
+Each fixture pins one row of SURVEY.md §8(a):
+  graph_indexing.npz   a1  build_sub_graph + r2e           rgcn/utils.py:78-134
+  ops.npz              a3  HyperbolicOps / LorentzOps        hyperbolic_ops.py:37-233, 476-581
+  layer_union.npz      a4  HyperbolicUnionRGCNLayer          hyperbolic_layers.py:164-323
+  layer_euclid.npz     a5  UnionRGCNLayer                    rgcn/layers.py:182-279
+  layer_lorentz.npz    a6  LorentzRGCNLayer                  hyperbolic_layers.py:524-694
+  model_*.npz          a9  HyperbolicRecurrentRGCN.predict / get_loss   hyperbolic_model.py:722-1088
+  rrgcn_*.npz          a9  RecurrentRGCN.predict             src/rrgcn.py:142-194
+  score.npz            a11/a12 chunked dist score / CE       hyperbolic_decoder.py:89-307
+  rank.npz             f2  get_total_rank / filter_score     rgcn/utils.py:21-166
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+sys.dont_write_bytecode = True
+sys.path.insert(0, os.path.join(HERE, "standin"))
+sys.path.insert(0, REF)
+
+# rgcn/layers.py:229-231 calls .cuda() unconditionally; make it a no-op on CPU.
+torch.Tensor.cuda = lambda self, *a, **k: self  # noqa: E731
+
+from rgcn import utils as rutils  # noqa: E402
+from rgcn.layers import UnionRGCNLayer  # noqa: E402
+from hyperbolic_src.hyperbolic_ops import HyperbolicOps, LorentzOps  # noqa: E402
+from hyperbolic_src.hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNLayer  # noqa: E402
+from hyperbolic_src import hyperbolic_decoder as hdec  # noqa: E402
+from hyperbolic_src.hyperbolic_model import HyperbolicRecurrentRGCN  # noqa: E402
+from src.rrgcn import RecurrentRGCN  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+C = 0.01
+
+
+def zipf_triples(rng, V, R, T, alpha=1.1, self_loops=0, dups=0):
+    perm = rng.permutation(V)
+    p = 1.0 / np.arange(1, V + 1) ** alpha
+    p /= p.sum()
+    s = perm[rng.choice(V, size=T, p=p)]
+    o = perm[rng.choice(V, size=T, p=p)]
+    r = rng.integers(0, R, size=T)
+    tr = np.stack([s, r, o], 1).astype(np.int64)
+    if self_loops:
+        tr[:self_loops, 2] = tr[:self_loops, 0]
+    if dups:
+        tr[-dups:] = tr[self_loops:self_loops + dups]
+    return tr
+
+
+def ball_points(gen, n, d, rmin=0.5, rmax=3.0):
+    x = HyperbolicOps.exp_map_zero(torch.randn(n, d, generator=gen), C)
+    rad = rmin + (rmax - rmin) * torch.rand(n, generator=gen)
+    return HyperbolicOps.apply_radius(x, rad, C)
+
+
+def graph_arrays(g, prefix=""):
+    return {
+        prefix + "src": g._src.numpy(), prefix + "dst": g._dst.numpy(),
+        prefix + "type": g.edata["type"].numpy(),
+        prefix + "in_deg": g.in_degrees(range(g.number_of_nodes())).numpy(),
+        prefix + "norm": g.ndata["norm"].numpy().reshape(-1),
+        prefix + "enorm": g.edata["norm"].numpy().reshape(-1),
+        prefix + "uniq_r": np.asarray(g.uniq_r), prefix + "r_len": np.asarray(g.r_len).reshape(-1, 2),
+        prefix + "r_to_e": np.asarray(g.r_to_e, dtype=np.int64),
+    }
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print("wrote", path, "%.0f KB" % (os.path.getsize(path) / 1024))
+
+
+def gen_graph_indexing():
+    rng = np.random.default_rng(1)
+    out = {}
+    cases = [("small", 64, 8, 200, 6, 10), ("mid", 500, 40, 3000, 20, 50), ("empty_rel", 30, 12, 40, 2, 3)]
+    for tag, V, R, T, sl, dup in cases:
+        tr = zipf_triples(rng, V, R, T, self_loops=sl, dups=dup)
+        if tag == "empty_rel":
+            tr[:, 1] = tr[:, 1] % 5 * 2  # only even relation ids < 10 present
+        g = rutils.build_sub_graph(V, R, tr, False, "cpu")
+        out[tag + "_triples"] = tr
+        out[tag + "_meta"] = np.array([V, R])
+        out.update(graph_arrays(g, tag + "_"))
+    save("graph_indexing.npz", **out)
+
+
+def gen_ops():
+    gen = torch.Generator().manual_seed(2)
+    d = 200
+    out = {}
+    for cname, c in (("c01", 0.01), ("c05", 0.05)):
+        base = torch.randn(16, d, generator=gen)
+        unit = base / base.norm(dim=-1, keepdim=True)
+        bound = 1.0 / np.sqrt(c)
+        norms = torch.tensor([0.0, 1e-9, 1e-5, 1e-3, 0.1, 1.0, 3.0, 0.5 * bound, 0.9 * bound,
+                              0.99 * bound, 0.9999 * bound, bound - 1e-6, bound, bound + 1e-3,
+                              1.5 * bound, 0.2])
+        x = unit * norms[:, None]
+        x[0] = 0.0
+        v = unit * torch.tensor([0.0, 1e-8, 1e-4, 0.01, 1.0, 5.0, 10.0, 20.0, 50.0, 80.0, 100.0,
+                                 200.0, 1e3, 1e4, 3.0, 0.3])[:, None]
+        y = ball_points(gen, 16, d) * (1.0 if c == 0.01 else 0.4)
+        rad = torch.tensor([1e-8, 0.5, 1.0, 2.0, 3.0, 5.0, 9.0, 9.999999, 10.0, 11.0, 20.0, 0.7,
+                            1.3, 2.2, 4.4, 6.0])
+        out[cname + "_x"] = x.numpy()
+        out[cname + "_v"] = v.numpy()
+        out[cname + "_y"] = y.numpy()
+        out[cname + "_rad"] = rad.numpy()
+        out[cname + "_project"] = HyperbolicOps.project_to_ball(x, c).numpy()
+        out[cname + "_log0"] = HyperbolicOps.log_map_zero(x, c).numpy()
+        out[cname + "_exp0"] = HyperbolicOps.exp_map_zero(v, c).numpy()
+        xb = HyperbolicOps.project_to_ball(x, c)
+        out[cname + "_mobius"] = HyperbolicOps.mobius_add(xb, y, c).numpy()
+        out[cname + "_dist"] = HyperbolicOps.hyperbolic_distance(xb, y, c).numpy()
+        out[cname + "_radius"] = HyperbolicOps.get_radius(x).numpy()
+        out[cname + "_apply_radius"] = HyperbolicOps.apply_radius(y, rad, c).numpy()
+        L = LorentzOps.to_lorentz(y, c)
+        out[cname + "_to_lorentz"] = L.numpy()
+        out[cname + "_to_poincare"] = LorentzOps.to_poincare(L, c).numpy()
+        w = torch.rand(16, generator=gen)
+        out[cname + "_w"] = w.numpy()
+        out[cname + "_centroid"] = LorentzOps.lorentz_centroid(L, w, c).numpy()
+    save("ops.npz", **out)
+
+
+def layer_graph(seed, V=300, R=256, T=1000, d=200, zero_deg_min=40):
+    rng = np.random.default_rng(seed)
+    tr = zipf_triples(rng, V, R, T, self_loops=5, dups=20)
+    g = rutils.build_sub_graph(V, R, tr, False, "cpu")
+    deg = g.in_degrees(range(V)).numpy()
+    assert (deg == 0).sum() >= zero_deg_min, (deg == 0).sum()
+    return tr, g
+
+
+def gen_layer_union():
+    torch.manual_seed(3)
+    gen = torch.Generator().manual_seed(3)
+    V, R, d = 300, 128, 200
+    tr, g = layer_graph(3, V, R, 1000, d)
+    h = ball_points(gen, V, d)
+    prev = ball_points(gen, V, d)
+    rel = torch.randn(2 * R, d, generator=gen) * 0.3
+    out = {"triples": tr, "meta": np.array([V, R, d]), "h": h.numpy(), "prev_h": prev.numpy(),
+           "rel": rel.numpy()}
+    shared = None
+    for gname, gamma in (("g0", 0.0), ("g15", 0.15)):
+        for skip in (False, True):
+            lay = HyperbolicUnionRGCNLayer(d, d, 2 * R, -1, c=C, activation=F.rrelu, self_loop=True,
+                                           dropout=0.2, skip_connect=skip, radius_msg_gamma=gamma)
+            if shared is None:
+                shared = {k: v.clone() for k, v in lay.state_dict().items()}
+                for k, v in shared.items():
+                    out["w_" + k] = v.numpy()
+            if skip and "w_skip_weight" not in out:
+                out["w_skip_weight"] = lay.skip_weight.detach().numpy()
+                out["w_skip_bias"] = (torch.randn(d, generator=gen) * 0.1).numpy()
+            sd = {k: torch.from_numpy(out["w_" + k]) for k in lay.state_dict()}
+            lay.load_state_dict(sd)
+            lay.eval()
+            with torch.no_grad():
+                y = lay(g, h, rel, prev_h=prev if skip else None)
+            out["%s_%s_out" % (gname, "skip" if skip else "noskip")] = y.numpy()
+    save("layer_union.npz", **out)
+
+
+def gen_layer_euclid():
+    torch.manual_seed(4)
+    gen = torch.Generator().manual_seed(4)
+    V, R, d = 300, 256, 200
+    tr, g = layer_graph(4, V, R, 1000, d)
+    h = torch.randn(V, d, generator=gen) * 0.5
+    rel = torch.randn(2 * R, d, generator=gen) * 0.3
+    out = {"triples": tr, "meta": np.array([V, R, d]), "h": h.numpy(), "rel": rel.numpy()}
+    lay = UnionRGCNLayer(d, d, 2 * R, -1, activation=F.rrelu, self_loop=True, dropout=0.2)
+    lay.eval()
+    g.ndata["h"] = h
+    with torch.no_grad():
+        y = lay(g, [], rel)
+    out["out"] = y.numpy()
+    for k, v in lay.state_dict().items():
+        out["w_" + k] = v.numpy()
+    save("layer_euclid.npz", **out)
+
+
+def gen_layer_lorentz():
+    out = {}
+    # (tag, d, R, n_bases) -> submatrix s = d / min(n_bases, 2R)
+    cases = [("s2", 200, 64, 100), ("s4", 64, 32, 16), ("s1", 64, 32, 64), ("s20", 60, 16, 3)]
+    for i, (tag, d, R, nb) in enumerate(cases):
+        torch.manual_seed(10 + i)
+        gen = torch.Generator().manual_seed(10 + i)
+        V = 300
+        tr, g = layer_graph(10 + i, V, R, 1000, d)
+        h = ball_points(gen, V, d)
+        prev = ball_points(gen, V, d)
+        rel = torch.randn(2 * R, d, generator=gen) * 0.3
+        out[tag + "_triples"] = tr
+        out[tag + "_meta"] = np.array([V, R, d, nb])
+        out[tag + "_h"] = h.numpy()
+        out[tag + "_prev_h"] = prev.numpy()
+        out[tag + "_rel"] = rel.numpy()
+        for skip in ((False, True) if tag == "s2" else (False,)):
+            lay = LorentzRGCNLayer(d, d, 2 * R, nb, c=C, activation=F.rrelu, self_loop=True,
+                                   dropout=0.2, skip_connect=skip)
+            for k, v in lay.state_dict().items():
+                if tag + "_w_" + k not in out:
+                    out[tag + "_w_" + k] = v.numpy()
+            if skip:
+                out[tag + "_w_skip_bias"] = (torch.randn(d, generator=gen) * 0.1).numpy()
+            lay.load_state_dict({k: torch.from_numpy(out[tag + "_w_" + k]) for k in lay.state_dict()})
+            lay.eval()
+            with torch.no_grad():
+                y = lay(g, h, rel, prev_h=prev if skip else None)
+            out[tag + ("_skip" if skip else "_noskip") + "_out"] = y.numpy()
+    save("layer_lorentz.npz", **out)
+
+
+def snapshot_series(seed, V, R, n_snap, per_snap):
+    """Synthetic TKG snapshots with temporal recurrence."""
+    rng = np.random.default_rng(seed)
+    snaps = []
+    for t in range(n_snap):
+        tr = zipf_triples(rng, V, R, per_snap)
+        if snaps:
+            k = int(0.6 * per_snap)
+            pool = np.concatenate(snaps[-3:])
+            tr[:k] = pool[rng.integers(0, len(pool), size=k)]
+        snaps.append(tr)
+    return snaps
+
+
+def gen_models():
+    V, R, T = 256, 64, 3
+    snaps = snapshot_series(20, V, R, T + 1, 120)
+    rng = np.random.default_rng(21)
+    radius_target = rng.uniform(0.5, 3.0, size=V).astype(np.float32)
+    cases = [
+        ("uvrgcn_roth", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False)),
+        ("uvrgcn_roth_ln", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=True)),
+        ("lgcn_roth", dict(encoder_name="lgcn", decoder_name="roth", layer_norm=False)),
+        ("lgcn_roth_ln", dict(encoder_name="lgcn", decoder_name="roth", layer_norm=True)),
+        ("uvrgcn_murp_nores", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="murp", layer_norm=False,
+                                   use_residual_evolution=False)),
+        ("uvrgcn_atth_beta", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="atth", layer_norm=True,
+                                  radius_anchor_beta=0.5)),
+        ("lgcn_roth_bias_crel", dict(encoder_name="lgcn", decoder_name="roth", layer_norm=False,
+                                     use_entity_euclidean_bias=True, use_relation_specific_curvature=True)),
+        ("uvrgcn_convtranse", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="hyperbolic_convtranse",
+                                   layer_norm=True)),
+    ]
+    glist = [rutils.build_sub_graph(V, R, s, False, "cpu") for s in snaps[:T]]
+    test = torch.from_numpy(snaps[T])
+    for i, (tag, kw) in enumerate(cases):
+        torch.manual_seed(100 + i)
+        # d=200 (the north-star width) for the configs[1] encoder/decoder pair, d=64 elsewhere to keep the
+        # fixtures small; n_bases gives 2x2 Lorentz blocks in both.
+        d = 200 if tag == "lgcn_roth" else 64
+        base = dict(num_ents=V, num_rels=R, num_static_rels=0, num_words=0, h_dim=d, opn="sub",
+                    sequence_len=T, num_bases=d // 2, num_hidden_layers=2, dropout=0.2, c=C,
+                    self_loop=True, skip_connect=False, input_dropout=0.2, hidden_dropout=0.2,
+                    feat_dropout=0.2, entity_prediction=True, relation_prediction=True,
+                    use_cuda=False, gpu="cpu", radius_target=radius_target, radius_msg_gamma=0.15)
+        base.update(kw)
+        m = HyperbolicRecurrentRGCN(**base)
+        with torch.no_grad():
+            # make the decoder scales/biases non-trivial so the epilogue is exercised
+            for mod in (m.decoder_ob, m.rdecoder):
+                if hasattr(mod, "score_margin"):
+                    mod.score_margin.fill_(0.7)
+                    mod.score_scale_raw.fill_(0.4)
+                if getattr(mod, "entity_bias", None) is not None:
+                    mod.entity_bias.normal_(0, 0.1)
+                if getattr(mod, "rel_bias", None) is not None:
+                    mod.rel_bias.normal_(0, 0.1)
+            m.radius_static.add_(torch.randn(V) * 0.2)
+        m.eval()
+        with torch.no_grad():
+            embs, _, h0, _, _ = m.forward(glist, None, False)
+            all_tr, score, score_rel = m.predict(glist, R, None, test.clone(), False)
+        out = {"meta": np.array([V, R, d, T]), "test": snaps[T], "all_triples": all_tr.numpy(),
+               "score": score.numpy(), "score_rel": score_rel.numpy(), "h0": h0.numpy(),
+               "embs": torch.stack(embs).numpy(), "radius_target": radius_target}
+        for t in range(T):
+            out["snap%d" % t] = snaps[t]
+        for k, v in m.state_dict().items():
+            out["sd_" + k] = v.numpy().copy()
+        # deterministic loss: model.train() but every dropout p=0 and BatchNorm frozen
+        m.train()
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.Dropout):
+                mod.p = 0.0
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.eval()
+        losses = m.get_loss(glist, test.clone(), None, False)
+        out["losses"] = np.array([x.item() for x in losses])
+        save("model_%s.npz" % tag, **out)
+
+
+def gen_rrgcn():
+    V, R, d, T = 256, 64, 64, 3
+    snaps = snapshot_series(30, V, R, T + 1, 120)
+    glist = [rutils.build_sub_graph(V, R, s, False, "cpu") for s in snaps[:T]]
+    test = torch.from_numpy(snaps[T])
+    for i, ln in enumerate((False, True)):
+        torch.manual_seed(200 + i)
+        m = RecurrentRGCN("convtranse", "uvrgcn", V, R, 0, 0, d, "sub", T, num_bases=100,
+                          num_basis=100, num_hidden_layers=2, dropout=0.2, self_loop=True,
+                          skip_connect=False, layer_norm=ln, input_dropout=0.2, hidden_dropout=0.2,
+                          feat_dropout=0.2, entity_prediction=True, relation_prediction=True,
+                          use_cuda=False, gpu="cpu")
+        m.eval()
+        with torch.no_grad():
+            embs, _, h0, _, _ = m.forward(glist, None, False)
+            all_tr, score, score_rel = m.predict(glist, R, None, test.clone(), False)
+        out = {"meta": np.array([V, R, d, T]), "test": snaps[T], "all_triples": all_tr.numpy(),
+               "score": score.numpy(), "score_rel": score_rel.numpy(), "h0": h0.numpy(),
+               "embs": torch.stack(embs).numpy()}
+        for t in range(T):
+            out["snap%d" % t] = snaps[t]
+        for k, v in m.state_dict().items():
+            out["sd_" + k] = v.numpy().copy()
+        save("rrgcn_%s.npz" % ("ln" if ln else "noln"), **out)
+
+
+def gen_score():
+    gen = torch.Generator().manual_seed(5)
+    B, N, d = 64, 1000, 200
+    q = ball_points(gen, B, d)
+    e = ball_points(gen, N, d)
+    # near-duplicate queries (cancellation stress) and a boundary query
+    q[0] = e[17] + 1e-4 * torch.randn(d, generator=gen)
+    q[1] = e[500]
+    q[2] = q[2] / q[2].norm() * 9.99
+    bias = torch.randn(N, generator=gen) * 0.1
+    tgt = torch.randint(0, N, (B,), generator=gen)
+    c_r = 0.002 + 0.008 * torch.rand(B, generator=gen)
+    scale = torch.tensor(1.3)
+    margin = torch.tensor(0.7)
+    out = {"q": q.numpy(), "e": e.numpy(), "bias": bias.numpy(), "target": tgt.numpy(),
+           "c_r": c_r.numpy(), "scale": scale.numpy(), "margin": margin.numpy()}
+    with torch.no_grad():
+        out["score_plain"] = hdec._chunked_hyperbolic_dist_score(q, e, None, C, 128, 256).numpy()
+        out["score_bias"] = hdec._chunked_hyperbolic_dist_score(
+            q, e, bias, C, 128, 256, score_scale=scale, score_margin=margin).numpy()
+        out["score_crel"] = hdec._chunked_hyperbolic_dist_score(
+            q, e, bias, C, 128, 256, score_scale=scale, score_margin=margin, query_curvature=c_r,
+            use_hyperbolic_distance=True).numpy()
+        out["score_dist"] = hdec._chunked_hyperbolic_dist_score(
+            q, e, None, C, 128, 256, score_scale=scale, score_margin=margin,
+            use_hyperbolic_distance=True).numpy()
+        out["ce_bias"] = hdec._chunked_hyperbolic_ce_loss(
+            q, e, tgt, C, 256, candidate_bias=bias, q_chunk_size=128, score_scale=scale,
+            score_margin=margin).numpy()
+        out["ce_crel"] = hdec._chunked_hyperbolic_ce_loss(
+            q, e, tgt, C, 256, candidate_bias=bias, q_chunk_size=128, score_scale=scale,
+            score_margin=margin, query_curvature=c_r, use_hyperbolic_distance=True).numpy()
+    save("score.npz", **out)
+
+
+def gen_rank():
+    rng = np.random.default_rng(6)
+    V, R, B = 120, 10, 80
+    snap = zipf_triples(rng, V, R, B, alpha=0.8)
+    snap[40:50] = snap[0:10]
+    snap[50:55, 2] = (snap[50:55, 2] + 1) % V  # same (s, r), another object
+    snap[50:55, :2] = snap[0:5, :2]
+    tr = torch.from_numpy(snap)
+    inv = tr[:, [2, 1, 0]].clone()
+    inv[:, 1] += R
+    all_tr = torch.cat([tr, inv])
+    score = torch.from_numpy(rng.standard_normal((2 * B, V)).astype(np.float32))
+    score_rel = torch.from_numpy(rng.standard_normal((2 * B, 2 * R)).astype(np.float32))
+    data = np.concatenate([snap, np.zeros((B, 1), np.int64)], 1)
+    ans_e = rutils.load_all_answers_for_time_filter(data, R, V, False)[0]
+    ans_r = rutils.load_all_answers_for_time_filter(data, R, V, True)[0]
+    mrr_f, mrr, rank, frank = rutils.get_total_rank(all_tr, score.clone(), ans_e, 1000, 0)
+    mrr_fr, mrr_r, rank_r, frank_r = rutils.get_total_rank(all_tr, score_rel.clone(), ans_r, 1000, 1)
+    save("rank.npz", snap=snap, all_triples=all_tr.numpy(), score=score.numpy(),
+         score_rel=score_rel.numpy(), rank=rank.numpy(), frank=frank.numpy(),
+         rank_r=rank_r.numpy(), frank_r=frank_r.numpy(),
+         mrr=np.array([mrr, mrr_f, mrr_r, mrr_fr]), meta=np.array([V, R]))
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    which = sys.argv[1:] or ["graph", "ops", "union", "euclid", "lorentz", "models", "rrgcn",
+                             "score", "rank"]
+    table = {"graph": gen_graph_indexing, "ops": gen_ops, "union": gen_layer_union,
+             "euclid": gen_layer_euclid, "lorentz": gen_layer_lorentz, "models": gen_models,
+             "rrgcn": gen_rrgcn, "score": gen_score, "rank": gen_rank}
+    for w in which:
+        table[w]()
