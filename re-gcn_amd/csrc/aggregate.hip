@@ -1,0 +1,330 @@
+// CSR gather / segment-reduce kernels.
+//
+// Work decomposition.  The host (regcn_amd/graph.py) sorts a snapshot's edges by
+// destination (stable, so ties keep the reference's edge order) and cuts every
+// destination's edge list into chunks of at most `chunk_edges` edges:
+//     chunk = {row, e_begin, e_end, slot}
+// slot < 0: the row fits one chunk and the wave writes the finished row.
+// slot >= 0: the wave writes a raw partial sum into partial[slot]; a fix-up
+// kernel then sums each long row's partials in chunk order and finishes it.
+// No atomics: results are bitwise reproducible run to run.
+//
+// One 64-lane wave per chunk; lane l owns columns [4l, 4l+4) (float4), so each
+// gathered 800-B row (d = 200) is one coalesced wave load.  Edge indices of up
+// to 64 edges are fetched cooperatively (one per lane) and broadcast with
+// readlane; the row loads of 4 edges are issued before they are consumed.
+//
+// HBM roofline (Union, per layer): E*(4d + 12) + V*(4d + 12) algorithmic bytes
+// (src row + col_src + col_type + radius_src per edge; output row + row
+// metadata per node); relation rows and Lorentz blocks are L2-resident.
+#include "common.h"
+#include "regcn_internal.h"
+
+namespace regcn {
+
+struct Chunk {
+  int row, beg, end, slot;
+};
+
+struct Fixup {
+  int row, sbeg, send, pad;
+};
+
+enum AggMode : int { AGG_UNION = 0, AGG_MEAN = 1, AGG_EUCLID = 2 };
+
+__device__ __forceinline__ int rl(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
+__device__ __forceinline__ float rlf(float v, int j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+}
+
+// ------------------------------------------------------------------------ Union / mean
+// UNION : acc = sum_e w_e (x[src_e] + rel[type_e]),  w_e = exp(-gamma |r_src - r_dst|)
+//         out = norm[row] * acc          (hyperbolic_layers.py:222-240, linearity of W_n)
+// EUCLID: same with w_e = 1              (rgcn/layers.py:257-279)
+// MEAN  : acc = sum_e x[idx_e];  out = acc / count  (hyperbolic_model.py:802-812)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_gather_sum(
+    const float* __restrict__ x, const float* __restrict__ radius, const float* __restrict__ rel,
+    const int* __restrict__ col_src, const int* __restrict__ col_type, const float* __restrict__ rowscale,
+    const Chunk* __restrict__ chunks, int n_chunks, float gamma, int d, float* __restrict__ partial,
+    int pstride, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane * 4;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int ci = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ci < n_chunks; ci += nw) {
+    const Chunk ch = chunks[ci];
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float r_dst = (MODE == AGG_UNION) ? radius[ch.row] : 0.f;
+    for (int e0 = ch.beg; e0 < ch.end; e0 += 64) {
+      const int n = min(64, ch.end - e0);
+      int my_s = 0, my_t = 0;
+      float my_w = 1.f;
+      if (lane < n) {
+        my_s = col_src[e0 + lane];
+        if (MODE != AGG_MEAN) my_t = col_type[e0 + lane];
+        if (MODE == AGG_UNION) my_w = expf(-gamma * fabsf(radius[my_s] - r_dst));
+      }
+      int j = 0;
+      for (; j + 4 <= n; j += 4) {
+        f4 xs[4], rr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          xs[u] = load4(x + (int64_t)rl(my_s, j + u) * d, col, d);
+          if (MODE != AGG_MEAN) rr[u] = load4(rel + (int64_t)rl(my_t, j + u) * d, col, d);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (MODE == AGG_MEAN) acc += xs[u];
+          else if (MODE == AGG_EUCLID) acc += xs[u] + rr[u];
+          else acc += rlf(my_w, j + u) * (xs[u] + rr[u]);
+        }
+      }
+      for (; j < n; ++j) {
+        f4 xs = load4(x + (int64_t)rl(my_s, j) * d, col, d);
+        if (MODE == AGG_MEAN) acc += xs;
+        else {
+          f4 rr = load4(rel + (int64_t)rl(my_t, j) * d, col, d);
+          if (MODE == AGG_EUCLID) acc += xs + rr;
+          else acc += rlf(my_w, j) * (xs + rr);
+        }
+      }
+    }
+    if (ch.slot < 0) {
+      f4 v = (MODE == AGG_MEAN) ? acc / rowscale[ch.row] : acc * rowscale[ch.row];
+      store4(out + (int64_t)ch.row * d, col, d, v);
+    } else {
+      store4(partial + (int64_t)ch.slot * pstride, col, d, acc);
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_gather_fixup(const float* __restrict__ partial, int pstride,
+                                                      const Fixup* __restrict__ fx, int n_fix,
+                                                      const float* __restrict__ rowscale, int d,
+                                                      float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane * 4;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n_fix; i += nw) {
+    const Fixup f = fx[i];
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = f.sbeg; s < f.send; ++s) acc += load4(partial + (int64_t)s * pstride, col, d);
+    f4 v = (MODE == AGG_MEAN) ? acc / rowscale[f.row] : acc * rowscale[f.row];
+    store4(out + (int64_t)f.row * d, col, d, v);
+  }
+}
+
+// ------------------------------------------------------------------------------ Lorentz
+// Per edge (hyperbolic_layers.py:589-611):
+//   m = blockdiag_k(W[type]_k (s x s)) . x_src + rel[type];  p = exp0(m);
+//   L = (x0 = (1 + c|p|^2) / (sqrt_c den), xi = 2 p / den),  den = max(1 - c|p|^2, eps)
+// Per destination (hyperbolic_layers.py:613-625, hyperbolic_ops.py:562-581): the
+// mailbox weights are uniform, so the weighted centroid equals S / sqrt(-<S,S>_L c)
+// with S = sum_e L_e; then to_poincare -> log0 (hyperbolic_layers.py:669-671).
+template <int S>
+__device__ __forceinline__ f4 block_matvec(f4 xs, const float* __restrict__ Wt, int lane, int d,
+                                           const float* xsh) {
+  const int col = lane * 4;
+  if (col >= d) return f4{0.f, 0.f, 0.f, 0.f};
+  if (S == 1) {
+    f4 w = *reinterpret_cast<const f4*>(Wt + col);
+    return xs * w;
+  } else if (S == 2) {
+    f4 w0 = *reinterpret_cast<const f4*>(Wt + 2 * col);
+    f4 w1 = *reinterpret_cast<const f4*>(Wt + 2 * col + 4);
+    return f4{xs.x * w0.x + xs.y * w0.z, xs.x * w0.y + xs.y * w0.w, xs.z * w1.x + xs.w * w1.z,
+              xs.z * w1.y + xs.w * w1.w};
+  } else if (S == 4) {
+    const float* b = Wt + 4 * col;
+    f4 w0 = *reinterpret_cast<const f4*>(b);
+    f4 w1 = *reinterpret_cast<const f4*>(b + 4);
+    f4 w2 = *reinterpret_cast<const f4*>(b + 8);
+    f4 w3 = *reinterpret_cast<const f4*>(b + 12);
+    return xs.x * w0 + xs.y * w1 + xs.z * w2 + xs.w * w3;
+  } else {
+    // general s: x row staged in this wave's LDS slice (xsh), W read from L2
+    return f4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+__device__ __forceinline__ float block_general(const float* xsh, const float* __restrict__ Wt, int s, int c) {
+  const int blk = c / s, jj = c - blk * s;
+  const float* w = Wt + (int64_t)blk * s * s + jj;
+  const float* xb = xsh + blk * s;
+  float m = 0.f;
+  for (int i = 0; i < s; ++i) m += xb[i] * w[i * s];
+  return m;
+}
+
+template <int S>
+__global__ __launch_bounds__(256) void k_lorentz_sum(
+    const float* __restrict__ x, const float* __restrict__ rel, const float* __restrict__ W,
+    const int* __restrict__ col_src, const int* __restrict__ col_type, const Chunk* __restrict__ chunks,
+    int n_chunks, int nb, int s_gen, Curv k, int d, float* __restrict__ partial, int pstride,
+    float* __restrict__ out) {
+  __shared__ float xsh_all[4][256];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  float* xsh = xsh_all[wv];
+  const int col = lane * 4;
+  const int wstride = nb * (d / nb) * (d / nb);
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int ci = blockIdx.x * (blockDim.x >> 6) + wv; ci < n_chunks; ci += nw) {
+    const Chunk ch = chunks[ci];
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    float acc0 = 0.f;
+    for (int e0 = ch.beg; e0 < ch.end; e0 += 64) {
+      const int n = min(64, ch.end - e0);
+      int my_s = 0, my_t = 0;
+      if (lane < n) {
+        my_s = col_src[e0 + lane];
+        my_t = col_type[e0 + lane];
+      }
+      for (int j = 0; j < n; ++j) {
+        const int src = rl(my_s, j), typ = rl(my_t, j);
+        const float* Wt = W + (int64_t)typ * wstride;
+        f4 xs = load4(x + (int64_t)src * d, col, d);
+        f4 m;
+        if (S > 0) {
+          m = block_matvec<S>(xs, Wt, lane, d, nullptr);
+        } else {
+          if (col < d) *reinterpret_cast<f4*>(xsh + col) = xs;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          m = f4{0.f, 0.f, 0.f, 0.f};
+          if (col < d) {
+            m.x = block_general(xsh, Wt, s_gen, col);
+            m.y = block_general(xsh, Wt, s_gen, col + 1);
+            m.z = block_general(xsh, Wt, s_gen, col + 2);
+            m.w = block_general(xsh, Wt, s_gen, col + 3);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+        }
+        m += load4(rel + (int64_t)typ * d, col, d);
+        float p2;
+        const float f = exp0_factor(wave_sum(dot4(m, m)), k, &p2);
+        const float den = fmaxf(1.f - k.c * p2, REGCN_EPS);
+        acc0 += (1.f + k.c * p2) / (k.sqrt_c * den);
+        acc += m * (2.f * f / den);
+      }
+    }
+    if (ch.slot < 0) {
+      const float ip = -acc0 * acc0 + wave_sum(dot4(acc, acc));
+      const float sc = sqrtf(fmaxf(-ip * k.c, REGCN_EPS));
+      const float c0 = acc0 / sc;
+      f4 y = (acc / sc) / fmaxf(1.f + c0 * k.sqrt_c, REGCN_EPS);
+      store4(out + (int64_t)ch.row * d, col, d, row_log0(y, k));
+    } else {
+      float* p = partial + (int64_t)ch.slot * pstride;
+      store4(p, col, d, acc);
+      if (lane == 0) p[d] = acc0;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lorentz_fixup(const float* __restrict__ partial, int pstride,
+                                                       const Fixup* __restrict__ fx, int n_fix, Curv k,
+                                                       int d, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane * 4;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n_fix; i += nw) {
+    const Fixup f = fx[i];
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    float acc0 = 0.f;
+    for (int s = f.sbeg; s < f.send; ++s) {
+      const float* p = partial + (int64_t)s * pstride;
+      acc += load4(p, col, d);
+      acc0 += p[d];
+    }
+    const float ip = -acc0 * acc0 + wave_sum(dot4(acc, acc));
+    const float sc = sqrtf(fmaxf(-ip * k.c, REGCN_EPS));
+    const float c0 = acc0 / sc;
+    f4 y = (acc / sc) / fmaxf(1.f + c0 * k.sqrt_c, REGCN_EPS);
+    store4(out + (int64_t)f.row * d, col, d, row_log0(y, k));
+  }
+}
+
+static inline unsigned grid_for(int n_items) {
+  long b = ((long)n_items + 3) / 4;
+  if (b > 16384) b = 16384;
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+int gather_sum(int mode, const float* x, const float* radius, const float* rel, const int* col_src,
+               const int* col_type, const float* rowscale, const void* chunks, int n_chunks,
+               const void* fixups, int n_fix, float gamma, int d, float* partial, int pstride, float* out,
+               hipStream_t st) {
+  if (d <= 0 || d > 256 || (d & 3)) return set_error(REGCN_EINVAL, "aggregation needs d %% 4 == 0 and d <= 256 (d=%d)", d);
+  if (!x || !col_src || !rowscale || !out) return set_error(REGCN_EINVAL, "null pointer");
+  if (mode != AGG_MEAN && (!col_type || !rel)) return set_error(REGCN_EINVAL, "null pointer");
+  if (mode == AGG_UNION && !radius) return set_error(REGCN_EINVAL, "union aggregation needs radius");
+  if (n_fix > 0 && !partial) return set_error(REGCN_EINVAL, "partial workspace required");
+  const Chunk* ch = (const Chunk*)chunks;
+  const Fixup* fx = (const Fixup*)fixups;
+  if (n_chunks > 0) {
+    dim3 g(grid_for(n_chunks)), b(256);
+    if (mode == AGG_UNION)
+      hipLaunchKernelGGL(k_gather_sum<AGG_UNION>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,
+                         n_chunks, gamma, d, partial, pstride, out);
+    else if (mode == AGG_EUCLID)
+      hipLaunchKernelGGL(k_gather_sum<AGG_EUCLID>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,
+                         n_chunks, gamma, d, partial, pstride, out);
+    else if (mode == AGG_MEAN)
+      hipLaunchKernelGGL(k_gather_sum<AGG_MEAN>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,
+                         n_chunks, gamma, d, partial, pstride, out);
+    else
+      return set_error(REGCN_EINVAL, "unknown aggregation mode %d", mode);
+    int rc = check_launch("k_gather_sum");
+    if (rc) return rc;
+  }
+  if (n_fix > 0) {
+    dim3 g(grid_for(n_fix)), b(256);
+    if (mode == AGG_MEAN)
+      hipLaunchKernelGGL(k_gather_fixup<AGG_MEAN>, g, b, 0, st, partial, pstride, fx, n_fix, rowscale, d, out);
+    else
+      hipLaunchKernelGGL(k_gather_fixup<AGG_UNION>, g, b, 0, st, partial, pstride, fx, n_fix, rowscale, d, out);
+    return check_launch("k_gather_fixup");
+  }
+  return 0;
+}
+
+int lorentz_sum(const float* x, const float* rel, const float* W, const int* col_src, const int* col_type,
+                const void* chunks, int n_chunks, const void* fixups, int n_fix, int nb, float c, int d,
+                float* partial, int pstride, float* out, hipStream_t st) {
+  if (d <= 0 || d > 256 || (d & 3)) return set_error(REGCN_EINVAL, "aggregation needs d %% 4 == 0 and d <= 256 (d=%d)", d);
+  if (nb <= 0 || d % nb) return set_error(REGCN_EINVAL, "d=%d not divisible by num_bases=%d", d, nb);
+  if (!x || !rel || !W || !col_src || !col_type || !out) return set_error(REGCN_EINVAL, "null pointer");
+  if (n_fix > 0 && (!partial || pstride < d + 1)) return set_error(REGCN_EINVAL, "partial workspace required");
+  const int s = d / nb;
+  Curv k = make_curv(c);
+  const Chunk* ch = (const Chunk*)chunks;
+  if (n_chunks > 0) {
+    dim3 g(grid_for(n_chunks)), b(256);
+    if (s == 1)
+      hipLaunchKernelGGL(k_lorentz_sum<1>, g, b, 0, st, x, rel, W, col_src, col_type, ch, n_chunks, nb, s, k, d,
+                         partial, pstride, out);
+    else if (s == 2)
+      hipLaunchKernelGGL(k_lorentz_sum<2>, g, b, 0, st, x, rel, W, col_src, col_type, ch, n_chunks, nb, s, k, d,
+                         partial, pstride, out);
+    else if (s == 4)
+      hipLaunchKernelGGL(k_lorentz_sum<4>, g, b, 0, st, x, rel, W, col_src, col_type, ch, n_chunks, nb, s, k, d,
+                         partial, pstride, out);
+    else
+      hipLaunchKernelGGL(k_lorentz_sum<0>, g, b, 0, st, x, rel, W, col_src, col_type, ch, n_chunks, nb, s, k, d,
+                         partial, pstride, out);
+    int rc = check_launch("k_lorentz_sum");
+    if (rc) return rc;
+  }
+  if (n_fix > 0) {
+    dim3 g(grid_for(n_fix)), b(256);
+    hipLaunchKernelGGL(k_lorentz_fixup, g, b, 0, st, partial, pstride, (const Fixup*)fixups, n_fix, k, d, out);
+    return check_launch("k_lorentz_fixup");
+  }
+  return 0;
+}
+
+}  // namespace regcn

@@ -1,0 +1,165 @@
+// extern "C" entry points of libregcn_hip.so (declared in include/regcn_hip.h).
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "regcn_internal.h"
+
+namespace regcn {
+
+static thread_local char g_err[512] = "";
+
+int set_error(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error((int)e, "%s: %s", what, hipGetErrorString(e));
+  return 0;
+}
+
+}  // namespace regcn
+
+using namespace regcn;
+
+#define ST(s) ((hipStream_t)(s))
+
+extern "C" {
+
+int regcn_version(void) { return REGCN_ABI_VERSION; }
+const char* regcn_last_error_string(void) { return g_err; }
+
+int regcn_log0_f32(const float* x, int64_t rows, int32_t d, float c, float* out, void* s) {
+  return rowmap(0, x, nullptr, nullptr, rows, d, c, out, nullptr, nullptr, ST(s));
+}
+int regcn_exp0_f32(const float* v, int64_t rows, int32_t d, float c, float* out, void* s) {
+  return rowmap(1, v, nullptr, nullptr, rows, d, c, out, nullptr, nullptr, ST(s));
+}
+int regcn_project_f32(const float* x, int64_t rows, int32_t d, float c, float* out, void* s) {
+  return rowmap(2, x, nullptr, nullptr, rows, d, c, out, nullptr, nullptr, ST(s));
+}
+int regcn_apply_radius_f32(const float* x, const float* radius, int64_t rows, int32_t d, float c, float* out,
+                           void* s) {
+  return rowmap(3, x, nullptr, radius, rows, d, c, out, nullptr, nullptr, ST(s));
+}
+int regcn_radius_f32(const float* x, int64_t rows, int32_t d, float* out, void* s) {
+  return rowmap(4, x, nullptr, nullptr, rows, d, 0.01f, out, nullptr, nullptr, ST(s));
+}
+int regcn_sumsq_f32(const float* x, int64_t rows, int32_t d, float* out, void* s) {
+  return rowmap(9, x, nullptr, nullptr, rows, d, 0.01f, out, nullptr, nullptr, ST(s));
+}
+int regcn_mobius_add_f32(const float* x, const float* y, int64_t rows, int32_t d, float c, float* out, void* s) {
+  return rowmap(5, x, y, nullptr, rows, d, c, out, nullptr, nullptr, ST(s));
+}
+int regcn_to_lorentz_f32(const float* x, int64_t rows, int32_t d, float c, float* out, void* s) {
+  return rowmap(6, x, nullptr, nullptr, rows, d, c, out, nullptr, nullptr, ST(s));
+}
+int regcn_to_poincare_f32(const float* y, int64_t rows, int32_t d, float c, float* out, void* s) {
+  return rowmap(7, y, nullptr, nullptr, rows, d, c, out, nullptr, nullptr, ST(s));
+}
+int regcn_prologue_f32(const float* h, int64_t rows, int32_t d, float c, float* x_out, float* r_out, void* s) {
+  return rowmap(8, h, nullptr, nullptr, rows, d, c, x_out, r_out, nullptr, ST(s));
+}
+int regcn_ln_roundtrip_f32(const float* x, int64_t rows, int32_t d, float c, float* out, void* s) {
+  return rowmap(10, x, nullptr, nullptr, rows, d, c, out, nullptr, nullptr, ST(s));
+}
+int regcn_init_entities_f32(const float* dyn, const float* r_static, int64_t rows, int32_t d, float c,
+                            int32_t layer_norm, float* h_out, float* x_out, float* r_out, void* s) {
+  return rowmap(layer_norm ? 12 : 11, dyn, nullptr, r_static, rows, d, c, h_out, x_out, r_out, ST(s));
+}
+
+int regcn_union_aggregate_f32(const float* x, const float* radius, const float* rel, const int32_t* col_src,
+                              const int32_t* col_type, const float* norm, const int32_t* chunks, int32_t n_chunks,
+                              const int32_t* fixups, int32_t n_fix, float gamma, int32_t d, float* partial,
+                              int32_t partial_stride, float* out, void* s) {
+  return gather_sum(0, x, radius, rel, col_src, col_type, norm, chunks, n_chunks, fixups, n_fix, gamma, d, partial,
+                    partial_stride, out, ST(s));
+}
+int regcn_euclid_aggregate_f32(const float* h, const float* rel, const int32_t* col_src, const int32_t* col_type,
+                               const float* norm, const int32_t* chunks, int32_t n_chunks, const int32_t* fixups,
+                               int32_t n_fix, int32_t d, float* partial, int32_t partial_stride, float* out,
+                               void* s) {
+  return gather_sum(2, h, nullptr, rel, col_src, col_type, norm, chunks, n_chunks, fixups, n_fix, 0.f, d, partial,
+                    partial_stride, out, ST(s));
+}
+int regcn_segment_mean_f32(const float* x, const int32_t* idx, const float* count, const int32_t* chunks,
+                           int32_t n_chunks, const int32_t* fixups, int32_t n_fix, int32_t d, float* partial,
+                           int32_t partial_stride, float* out, void* s) {
+  return gather_sum(1, x, nullptr, nullptr, idx, nullptr, count, chunks, n_chunks, fixups, n_fix, 0.f, d, partial,
+                    partial_stride, out, ST(s));
+}
+int regcn_lorentz_aggregate_f32(const float* x, const float* rel, const float* weight, const int32_t* col_src,
+                                const int32_t* col_type, const int32_t* chunks, int32_t n_chunks,
+                                const int32_t* fixups, int32_t n_fix, int32_t num_bases, float c, int32_t d,
+                                float* partial, int32_t partial_stride, float* out, void* s) {
+  return lorentz_sum(x, rel, weight, col_src, col_type, chunks, n_chunks, fixups, n_fix, num_bases, c, d, partial,
+                     partial_stride, out, ST(s));
+}
+
+int regcn_layer_tail_f32(const float* agg, const float* w_n, const float* x, const float* w_loop,
+                         const float* w_evolve, const float* prev_t, const float* w_skip, const float* b_skip,
+                         const float* drop_mask, const int32_t* rows, int32_t n_pos, int32_t V, int32_t d,
+                         int32_t euclid, float c, float* h_out, float* x_next, float* r_next, void* s) {
+  LayerArgs a{agg, w_n, x, w_loop, w_evolve, prev_t, w_skip, b_skip, drop_mask, rows, n_pos, V, d, euclid,
+              make_curv(c), h_out, x_next, r_next};
+  return layer_tail(a, ST(s));
+}
+
+int regcn_timestep_f32(const float* hc, const float* x_prev, const float* w_g, const float* b_g,
+                       const float* r_static, const float* w_r, const float* b_r, float eps_r, float beta,
+                       int32_t layer_norm, int32_t residual, int32_t V, int32_t d, float c, float c_radius,
+                       float* h_out, float* x_out, float* r_out, void* s) {
+  if (residual && !b_r) return set_error(REGCN_EINVAL, "residual radius needs b_r");
+  StepArgs a{hc, x_prev, w_g, b_g, r_static, w_r, b_r, eps_r, beta, layer_norm, residual, V, d,
+             make_curv(c), make_curv(c_radius), h_out, x_out, r_out};
+  return timestep(a, ST(s));
+}
+
+static ScoreArgs score_args(const float* q, const float* cand, const float* bias, const float* c_rel, const float* scale, const float* margin,
+                            int32_t B, int32_t N, int32_t d, float c, int32_t use_dist) {
+  ScoreArgs a{};
+  Curv k = make_curv(c);
+  a.q = q; a.e = cand; a.bias = bias; a.c_r = c_rel;
+  a.B = B; a.N = N; a.d = d; a.use_dist = use_dist;
+  a.c = k.c; a.sqrt_c = k.sqrt_c; a.mx = k.mx;
+  a.dist_mx = (float)(1.0 / (sqrt((double)c) + 1e-6) - 1e-6);
+  a.scale_p = scale; a.margin_p = margin;
+  return a;
+}
+
+int regcn_hyp_score_f32(const float* q, const float* cand, const float* bias, const float* c_rel, const float* scale, const float* margin, int32_t B,
+                        int32_t N, int32_t d, float c, int32_t use_dist, float* out, void* s) {
+  if (c_rel && !use_dist) return set_error(REGCN_EINVAL, "per-query curvature requires use_dist");
+  ScoreArgs a = score_args(q, cand, bias, c_rel, scale, margin, B, N, d, c, use_dist);
+  a.out = out;
+  return score(a, 0, nullptr, ST(s));
+}
+
+size_t regcn_hyp_ce_workspace_bytes(int32_t B, int32_t N) {
+  const size_t nblk = ((size_t)N + 63) / 64;
+  return ((size_t)B * nblk * 2 + (size_t)B) * sizeof(float);
+}
+
+int regcn_hyp_ce_f32(const float* q, const float* cand, const float* bias, const float* c_rel, const float* scale, const float* margin,
+                     const int32_t* target, int32_t B, int32_t N, int32_t d, float c, int32_t use_dist,
+                     void* workspace, float* loss_per_query, void* s) {
+  if (c_rel && !use_dist) return set_error(REGCN_EINVAL, "per-query curvature requires use_dist");
+  if (!workspace) return set_error(REGCN_EINVAL, "null workspace");
+  ScoreArgs a = score_args(q, cand, bias, c_rel, scale, margin, B, N, d, c, use_dist);
+  const size_t nblk = ((size_t)N + 63) / 64;
+  a.target = target;
+  a.part = (float*)workspace;
+  a.tgt_logit = a.part + (size_t)B * nblk * 2;
+  return score(a, 1, loss_per_query, ST(s));
+}
+
+int regcn_rank_f32(const float* score_m, int32_t B, int32_t N, const int32_t* target, const int32_t* filt_ptr,
+                   const int32_t* filt_idx, int32_t* rank_raw, int32_t* rank_filt, void* s) {
+  return rank(score_m, B, N, target, filt_ptr, filt_idx, rank_raw, rank_filt, ST(s));
+}
+
+}  // extern "C"

@@ -1,0 +1,121 @@
+// Shared device helpers for the RE-GCN MI355X (gfx950) kernels.
+//
+// Row layout: a node/relation row of width d (d % 4 == 0, d <= 256) is held by ONE
+// 64-lane wavefront, lane l owning columns [4l, 4l+4) as a float4 (lanes with
+// 4l >= d hold zeros).  Row norms are wave reductions.  All arithmetic is fp32,
+// matching the reference (hyperbolic_src/hyperbolic_ops.py) to ~1 ulp per op.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define REGCN_EPS 1e-6f
+#define WAVE 64
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+namespace regcn {
+
+// Curvature-derived constants, computed on the host in double and rounded
+// once to fp32 exactly as torch rounds a python-float clamp bound.
+struct Curv {
+  float c;        // curvature
+  float sqrt_c;   // sqrt(c)
+  float mx;       // project bound: 1/sqrt(c) - 2e-6  (hyperbolic_ops.py:73 + :52)
+  float rmax;     // apply_radius bound: 1/sqrt(c) - 1e-6 (hyperbolic_ops.py:229)
+  float atanh_mx; // log0 clamp: 1 - 1e-6 (hyperbolic_ops.py:115)
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Reduction over the 16 lanes that share (lane >> 4): the row group of an
+// MFMA 16x16 C/D fragment (col = lane & 15).
+__device__ __forceinline__ float group16_sum(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+
+__device__ __forceinline__ float dot4(f4 a, f4 b) {
+  return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+}
+
+__device__ __forceinline__ f4 clamp4(f4 v, float lo, float hi) {
+  return f4{fminf(fmaxf(v.x, lo), hi), fminf(fmaxf(v.y, lo), hi), fminf(fmaxf(v.z, lo), hi),
+            fminf(fmaxf(v.w, lo), hi)};
+}
+
+// F.rrelu(x) with training=False: slope (1/8 + 1/3) / 2 = 11/48.
+__device__ __forceinline__ float leaky(float x) {
+  const float slope = (1.0f / 8.0f + 1.0f / 3.0f) * 0.5f;
+  return x >= 0.f ? x : x * slope;
+}
+
+__device__ __forceinline__ f4 leaky4(f4 v) { return f4{leaky(v.x), leaky(v.y), leaky(v.z), leaky(v.w)}; }
+
+__device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ---- scalar factors of the row maps, given the row's squared norm n2 ------------------
+
+// log0: x * atanh(min(sqrt_c |x|, 1-eps)) / (sqrt_c |x|), |x| clamped to eps
+// (hyperbolic_ops.py:97-116).
+__device__ __forceinline__ float log0_factor(float n2, const Curv& k) {
+  float n = fmaxf(sqrtf(n2), REGCN_EPS);
+  float s = fminf(k.sqrt_c * n, k.atanh_mx);
+  return atanhf(s) / (k.sqrt_c * n);
+}
+
+// project_to_ball factor (hyperbolic_ops.py:37-74): min(|x|c, mx)/|x|c, |x|c = max(|x|, eps).
+__device__ __forceinline__ float project_factor(float n2, const Curv& k) {
+  float n = fmaxf(sqrtf(n2), REGCN_EPS);
+  return fminf(n, k.mx) / n;
+}
+
+// exp0 then project (hyperbolic_ops.py:76-95).  Returns the factor f with
+// exp0(v) = f * v; *out_n2 receives |exp0(v)|^2 (analytic).
+__device__ __forceinline__ float exp0_factor(float n2, const Curv& k, float* out_n2 = nullptr) {
+  float rn = sqrtf(n2);
+  float n = fmaxf(rn, REGCN_EPS);
+  float t = tanhf(k.sqrt_c * n);
+  float f = t / (n * k.sqrt_c);
+  float pn = f * rn;                 // |tanh(..) v / (n sqrt_c)|
+  float pf = project_factor(pn * pn, k);
+  if (out_n2) {
+    float q = pn * pf;
+    *out_n2 = q * q;
+  }
+  return f * pf;
+}
+
+// ---- wave-per-row maps on a float4 fragment ---------------------------------------------
+__device__ __forceinline__ f4 row_log0(f4 v, const Curv& k) { return v * log0_factor(wave_sum(dot4(v, v)), k); }
+__device__ __forceinline__ f4 row_exp0(f4 v, const Curv& k) { return v * exp0_factor(wave_sum(dot4(v, v)), k); }
+__device__ __forceinline__ f4 row_project(f4 v, const Curv& k) { return v * project_factor(wave_sum(dot4(v, v)), k); }
+
+// apply_radius (hyperbolic_ops.py:208-233): direction * clamp(r, eps, rmax).
+__device__ __forceinline__ f4 row_apply_radius(f4 v, float r, const Curv& k) {
+  float n = fmaxf(sqrtf(wave_sum(dot4(v, v))), REGCN_EPS);
+  float rr = fminf(fmaxf(r, REGCN_EPS), k.rmax);
+  return (v / n) * rr;
+}
+
+__device__ __forceinline__ f4 load4(const float* p, int col, int d) {
+  return col < d ? *reinterpret_cast<const f4*>(p + col) : f4{0.f, 0.f, 0.f, 0.f};
+}
+
+__device__ __forceinline__ void store4(float* p, int col, int d, f4 v) {
+  if (col < d) *reinterpret_cast<f4*>(p + col) = v;
+}
+
+}  // namespace regcn

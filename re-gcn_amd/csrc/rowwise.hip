@@ -1,0 +1,199 @@
+// Row-wise Poincaré / Lorentz maps.
+//
+// HBM-bound: each op reads and writes whole rows once.  One 64-lane wave per
+// row; lane l holds elements l, l+64, ... (EPL = ceil(d/64) per lane), so every
+// wave-instruction touches 256 contiguous bytes for any d.  Row norms are
+// wave reductions.  Reference: hyperbolic_src/hyperbolic_ops.py.
+#include "common.h"
+#include "regcn_internal.h"
+
+namespace regcn {
+
+enum RowOp : int {
+  OP_LOG0 = 0,
+  OP_EXP0 = 1,
+  OP_PROJECT = 2,
+  OP_APPLY_RADIUS = 3,
+  OP_RADIUS = 4,
+  OP_MOBIUS_ADD = 5,
+  OP_TO_LORENTZ = 6,
+  OP_TO_POINCARE = 7,
+  OP_PROLOGUE = 8,      // x = log0(h), r = max(|h|, eps) in one pass
+  OP_SUMSQ = 9,         // |x|^2 (scorer row norms)
+  OP_LN_ROUNDTRIP = 10, // exp0(normalize(log0(x)))  (hyperbolic_model.py:926-929)
+  OP_INIT = 11,         // h = apply_radius(exp0(x), r_s); also log0(h), |h|  (:779-782)
+  OP_INIT_LN = 12,      // same with exp0(normalize(x))
+};
+
+template <int EPL>
+struct Frag {
+  float v[EPL];
+  __device__ __forceinline__ void load(const float* row, int d, int lane, int off = 0) {
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      int col = lane + j * WAVE;
+      v[j] = col < d ? row[col + off] : 0.f;
+    }
+  }
+  __device__ __forceinline__ void store(float* row, int d, int lane, int off = 0) const {
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      int col = lane + j * WAVE;
+      if (col < d) row[col + off] = v[j];
+    }
+  }
+  __device__ __forceinline__ float sumsq() const {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) s += v[j] * v[j];
+    return wave_sum(s);
+  }
+  __device__ __forceinline__ float dot(const Frag& o) const {
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) s += v[j] * o.v[j];
+    return wave_sum(s);
+  }
+  __device__ __forceinline__ void scale(float f) {
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) v[j] *= f;
+  }
+};
+
+template <int EPL, int OP>
+__global__ __launch_bounds__(256) void k_rowmap(const float* __restrict__ a, const float* __restrict__ b,
+                                                const float* __restrict__ vec, int64_t rows, int d,
+                                                Curv k, float* __restrict__ out, float* __restrict__ out2,
+                                                float* __restrict__ out3) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += nwaves) {
+    Frag<EPL> x;
+    if (OP == OP_TO_POINCARE) {
+      x.load(a + r * (d + 1), d, lane, 1);
+      float y0 = a[r * (d + 1)];
+      x.scale(1.0f / fmaxf(1.0f + y0 * k.sqrt_c, REGCN_EPS));        // hyperbolic_ops.py:516-518
+      x.store(out + r * d, d, lane);
+      continue;
+    }
+    x.load(a + r * d, d, lane);
+    float n2 = x.sumsq();
+    if (OP == OP_LOG0) {
+      x.scale(log0_factor(n2, k));
+      x.store(out + r * d, d, lane);
+    } else if (OP == OP_PROLOGUE) {
+      float rad = fmaxf(sqrtf(n2), REGCN_EPS);
+      x.scale(log0_factor(n2, k));
+      x.store(out + r * d, d, lane);
+      if (lane == 0) out2[r] = rad;
+    } else if (OP == OP_EXP0) {
+      x.scale(exp0_factor(n2, k));
+      x.store(out + r * d, d, lane);
+    } else if (OP == OP_PROJECT) {
+      x.scale(project_factor(n2, k));
+      x.store(out + r * d, d, lane);
+    } else if (OP == OP_APPLY_RADIUS) {
+      float n = fmaxf(sqrtf(n2), REGCN_EPS);
+      float rr = fminf(fmaxf(vec[r], REGCN_EPS), k.rmax);
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) x.v[j] = (x.v[j] / n) * rr;
+      x.store(out + r * d, d, lane);
+    } else if (OP == OP_RADIUS) {
+      if (lane == 0) out[r] = fmaxf(sqrtf(n2), REGCN_EPS);
+    } else if (OP == OP_SUMSQ) {
+      if (lane == 0) out[r] = n2;
+    } else if (OP == OP_LN_ROUNDTRIP) {
+      x.scale(log0_factor(n2, k));
+      x.scale(1.0f / fmaxf(sqrtf(x.sumsq()), 1e-12f));
+      x.scale(exp0_factor(x.sumsq(), k));
+      x.store(out + r * d, d, lane);
+    } else if (OP == OP_INIT || OP == OP_INIT_LN) {
+      if (OP == OP_INIT_LN) {
+        x.scale(1.0f / fmaxf(sqrtf(n2), 1e-12f));
+        n2 = x.sumsq();
+      }
+      x.scale(exp0_factor(n2, k));
+      {
+        const float n = fmaxf(sqrtf(x.sumsq()), REGCN_EPS);
+        const float rr = fminf(fmaxf(vec[r], REGCN_EPS), k.rmax);
+#pragma unroll
+        for (int j = 0; j < EPL; ++j) x.v[j] = (x.v[j] / n) * rr;
+      }
+      x.store(out + r * d, d, lane);
+      const float h2 = x.sumsq();
+      if (lane == 0 && out3) out3[r] = fmaxf(sqrtf(h2), REGCN_EPS);
+      if (out2) {
+        x.scale(log0_factor(h2, k));
+        x.store(out2 + r * d, d, lane);
+      }
+    } else if (OP == OP_MOBIUS_ADD) {                                   // hyperbolic_ops.py:118-143
+      Frag<EPL> y;
+      y.load(b + r * d, d, lane);
+      float y2 = y.sumsq(), xy = x.dot(y);
+      float A = 1.f + 2.f * k.c * xy + k.c * y2;
+      float B = 1.f - k.c * n2;
+      float den = 1.f + 2.f * k.c * xy + k.c * k.c * n2 * y2 + REGCN_EPS;
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) x.v[j] = (A * x.v[j] + B * y.v[j]) / den;
+      x.scale(project_factor(x.sumsq(), k));
+      x.store(out + r * d, d, lane);
+    } else if (OP == OP_TO_LORENTZ) {                                   // hyperbolic_ops.py:476-499
+      float den = fmaxf(1.f - k.c * n2, REGCN_EPS);
+      if (lane == 0) out[r * (d + 1)] = (1.f + k.c * n2) / (k.sqrt_c * den);
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) x.v[j] = 2.f * x.v[j] / den;
+      x.store(out + r * (d + 1), d, lane, 1);
+    }
+  }
+}
+
+template <int OP>
+static int launch_rowmap(const float* a, const float* b, const float* vec, int64_t rows, int d,
+                         const Curv& k, float* out, float* out2, float* out3, hipStream_t st) {
+  if (rows == 0) return 0;
+  int64_t blocks = (rows + 3) / 4;
+  if (blocks > 8192) blocks = 8192;                      // grid-stride beyond 8 blocks/CU
+  dim3 g((unsigned)blocks), blk(256);
+  int epl = (d + 63) / 64;
+  if (epl <= 1) hipLaunchKernelGGL((k_rowmap<1, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3);
+  else if (epl <= 2) hipLaunchKernelGGL((k_rowmap<2, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3);
+  else if (epl <= 4) hipLaunchKernelGGL((k_rowmap<4, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3);
+  else if (epl <= 8) hipLaunchKernelGGL((k_rowmap<8, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3);
+  else if (epl <= 16) hipLaunchKernelGGL((k_rowmap<16, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3);
+  else return set_error(REGCN_EINVAL, "row width d=%d exceeds 1024", d);
+  return check_launch("k_rowmap");
+}
+
+int rowmap(int op, const float* a, const float* b, const float* vec, int64_t rows, int d, float c,
+           float* out, float* out2, float* out3, hipStream_t st) {
+  if (d <= 0) return set_error(REGCN_EINVAL, "d must be positive");
+  if (!a || !out) return set_error(REGCN_EINVAL, "null pointer");
+  Curv k = make_curv(c);
+  switch (op) {
+    case OP_LOG0: return launch_rowmap<OP_LOG0>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_EXP0: return launch_rowmap<OP_EXP0>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_PROJECT: return launch_rowmap<OP_PROJECT>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_APPLY_RADIUS:
+      if (!vec) return set_error(REGCN_EINVAL, "apply_radius needs a radius vector");
+      return launch_rowmap<OP_APPLY_RADIUS>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_RADIUS: return launch_rowmap<OP_RADIUS>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_MOBIUS_ADD:
+      if (!b) return set_error(REGCN_EINVAL, "mobius_add needs y");
+      return launch_rowmap<OP_MOBIUS_ADD>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_TO_LORENTZ: return launch_rowmap<OP_TO_LORENTZ>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_TO_POINCARE: return launch_rowmap<OP_TO_POINCARE>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_PROLOGUE:
+      if (!out2) return set_error(REGCN_EINVAL, "prologue needs a radius output");
+      return launch_rowmap<OP_PROLOGUE>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_SUMSQ: return launch_rowmap<OP_SUMSQ>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_LN_ROUNDTRIP: return launch_rowmap<OP_LN_ROUNDTRIP>(a, b, vec, rows, d, k, out, out2, out3, st);
+    case OP_INIT:
+    case OP_INIT_LN:
+      if (!vec) return set_error(REGCN_EINVAL, "init needs the static radius");
+      if (op == OP_INIT) return launch_rowmap<OP_INIT>(a, b, vec, rows, d, k, out, out2, out3, st);
+      return launch_rowmap<OP_INIT_LN>(a, b, vec, rows, d, k, out, out2, out3, st);
+  }
+  return set_error(REGCN_EINVAL, "unknown row op %d", op);
+}
+
+}  // namespace regcn

@@ -1,0 +1,283 @@
+// All-entity hyperbolic distance scoring on MFMA (f2).
+//
+// The reference expands every (query, candidate) pair and runs mobius_add(-q, e)
+// per pair (hyperbolic_decoder.py:89-179).  With x = -q, y = e everything the
+// distance needs is three scalars per pair:
+//     xy = <q, e>   (the only d-length contraction: a GEMM Q E^T on MFMA)
+//     x2 = |q|^2, y2 = |e|^2   (per-row, accumulated while the tiles are staged)
+//   A = 1 - 2c xy + c y2,  B = 1 - c x2,  |num|^2 = A^2 x2 - 2AB xy + B^2 y2
+//   den = 1 - 2c xy + c^2 x2 y2 (+eps);  |mobius| = min(|num| / den, mx)
+//   proxy score  = scale (margin - |mobius|^2) + bias[n]
+//   true distance (use_hyperbolic_distance): 2/sqrt_c atanh(sqrt_c |.|) with the
+//   reference's clamps, optionally with a per-query curvature c_r (:145-164).
+//
+// Tile: 256 threads, 64 queries x 64 candidates; wave w computes 16 queries x 64
+// candidates as four 16x16 v_mfma_f32_16x16x4_f32 accumulators; K streamed through
+// LDS in 16-deep chunks.  Epilogues: write S (score), or per-tile (max, sum exp)
+// partials + target logit for a fused cross entropy (never materialising B x N).
+#include "common.h"
+#include "regcn_internal.h"
+
+namespace regcn {
+
+constexpr int SQ = 64, SN = 64, SKC = 16, SLD = SKC + 1;
+
+
+
+template <typename T>
+__device__ __forceinline__ T pair_score(T xy, T x2, T y2, T bias_n, T cr, const ScoreArgs& p) {
+  const T eps = (T)REGCN_EPS;
+  if (!p.use_dist) {
+    const T c = (T)p.c;
+    const T A = (T)1 - (T)2 * c * xy + c * y2;
+    const T Bq = (T)1 - c * x2;
+    const T num2 = fmax(A * A * x2 - (T)2 * A * Bq * xy + Bq * Bq * y2, (T)0);
+    const T den = (T)1 - (T)2 * c * xy + c * c * x2 * y2 + eps;
+    const T n = fmin(sqrt(num2) / den, (T)p.mx);
+    return (T)p.scale * ((T)p.margin - n * n) + bias_n;
+  }
+  if (p.c_r) {  // hyperbolic_decoder.py:146-161
+    const T c = cr;
+    const T sc = sqrt(c + eps);
+    const T A = (T)1 - (T)2 * c * xy + c * y2, Bq = (T)1 - c * x2;
+    const T num2 = fmax(A * A * x2 - (T)2 * A * Bq * xy + Bq * Bq * y2, (T)0);
+    const T den = (T)1 - (T)2 * c * xy + c * c * x2 * y2 + eps;
+    T n = fmax(sqrt(num2) / den, eps);
+    n = fmin(n, (T)1 / (sc + eps) - eps);
+    const T dist = ((T)2 / (sc + eps)) * atanh(fmin(sc * n, (T)1 - eps));
+    return (T)p.scale * ((T)p.margin - dist) + bias_n;
+  }
+  // HyperbolicOps.hyperbolic_distance (hyperbolic_ops.py:168-191): mobius_add projects
+  // to |.| <= mx, then the norm is clamped to [eps, 1/(sqrt_c + eps) - eps].
+  const T c = (T)p.c, sc = (T)p.sqrt_c;
+  const T A = (T)1 - (T)2 * c * xy + c * y2, Bq = (T)1 - c * x2;
+  const T num2 = fmax(A * A * x2 - (T)2 * A * Bq * xy + Bq * Bq * y2, (T)0);
+  const T den = (T)1 - (T)2 * c * xy + c * c * x2 * y2 + eps;
+  T n = fmin(sqrt(num2) / den, (T)p.mx);
+  n = fmin(fmax(n, eps), (T)p.dist_mx);
+  const T dist = ((T)2 / sc) * atanh(sc * n);
+  return (T)p.scale * ((T)p.margin - dist) + bias_n;
+}
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+template <bool F64>
+struct ScoreT;
+template <>
+struct ScoreT<false> {
+  typedef float T;
+  typedef f4 V;
+  static __device__ __forceinline__ V mfma(T a, T b, V c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+  // C/D layout of v_mfma_f32_16x16x4_f32: row 4*(lane>>4) + r
+  static __device__ __forceinline__ int row(int lane, int r) { return 4 * (lane >> 4) + r; }
+};
+template <>
+struct ScoreT<true> {
+  typedef double T;
+  typedef d4 V;
+  static __device__ __forceinline__ V mfma(T a, T b, V c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
+  // C/D layout of v_mfma_f64_16x16x4_f64: row (lane>>4) + 4 r
+  static __device__ __forceinline__ int row(int lane, int r) { return (lane >> 4) + 4 * r; }
+};
+
+// MODE 0 = write scores, 1 = CE partials.  F64: fp64 MFMA + fp64 epilogue, used for the
+// true-distance mode where the arctanh distance is linear in |num| and the fp32 expansion
+// would lose ~3 digits on near-duplicate pairs (the per-pair fp32 reference does not).
+template <int MODE, bool F64>
+__global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
+  typedef ScoreT<F64> S;
+  typedef typename S::T T;
+  p.scale = p.scale_p ? *p.scale_p : 1.f;
+  p.margin = p.margin_p ? *p.margin_p : 0.f;
+  __shared__ T Qs[SQ * SLD];
+  __shared__ T Es[SN * SLD];
+  __shared__ T q2s[SQ], e2s[SN];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // consecutive blocks share a query tile (the candidate stream is the large operand)
+  const int nbn = (p.N + SN - 1) / SN;
+  const int bq = blockIdx.x / nbn, bn = blockIdx.x - bq * nbn;
+  const int q0 = bq * SQ, n0 = bn * SN;
+  typename S::V acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = typename S::V{0, 0, 0, 0};
+  const int i = tid >> 2, kq = (tid & 3) * 4;
+  T sq_q = 0, sq_e = 0;  // row |.|^2, accumulated by the 4 staging threads of row i
+  for (int k0 = 0; k0 < p.d; k0 += SKC) {
+    __syncthreads();
+    f4 vq = {0.f, 0.f, 0.f, 0.f}, ve = {0.f, 0.f, 0.f, 0.f};
+    if (q0 + i < p.B && k0 + kq < p.d) vq = *reinterpret_cast<const f4*>(p.q + (int64_t)(q0 + i) * p.d + k0 + kq);
+    if (n0 + i < p.N && k0 + kq < p.d) ve = *reinterpret_cast<const f4*>(p.e + (int64_t)(n0 + i) * p.d + k0 + kq);
+    T* dq = Qs + i * SLD + kq;
+    T* de = Es + i * SLD + kq;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const T a = (T)vq[u], b = (T)ve[u];
+      dq[u] = a;
+      de[u] = b;
+      sq_q += a * a;
+      sq_e += b * b;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < SKC; kk += 4) {
+      const T a = Qs[(16 * wv + (lane & 15)) * SLD + kk + (lane >> 4)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const T b = Es[(16 * j + (lane & 15)) * SLD + kk + (lane >> 4)];
+        acc[j] = S::mfma(a, b, acc[j]);
+      }
+    }
+  }
+  sq_q += __shfl_xor(sq_q, 1);
+  sq_q += __shfl_xor(sq_q, 2);
+  sq_e += __shfl_xor(sq_e, 1);
+  sq_e += __shfl_xor(sq_e, 2);
+  if ((tid & 3) == 0) {
+    q2s[i] = sq_q;
+    e2s[i] = sq_e;
+  }
+  __syncthreads();
+  // epilogue: lane holds queries q0 + 16 wv + S::row(lane, r), candidates n0 + 16 j + (lane & 15)
+  T x2[4], cr[4];
+  int qi[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int li = 16 * wv + S::row(lane, r);
+    qi[r] = q0 + li;
+    const bool ok = qi[r] < p.B;
+    x2[r] = q2s[li];
+    cr[r] = (ok && p.c_r) ? (T)p.c_r[qi[r]] : (T)0;
+  }
+  T y2[4], bn_[4];
+  int ni[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ni[j] = n0 + 16 * j + (lane & 15);
+    const bool ok = ni[j] < p.N;
+    y2[j] = e2s[16 * j + (lane & 15)];
+    bn_[j] = (ok && p.bias) ? (T)p.bias[ni[j]] : (T)0;
+  }
+  if (MODE == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (qi[r] >= p.B) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ni[j] < p.N)
+          p.out[(int64_t)qi[r] * p.N + ni[j]] = (float)pair_score<T>(acc[j][r], x2[r], y2[j], bn_[j], cr[r], p);
+    }
+  } else {
+    const int nblk = (p.N + SN - 1) / SN;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float s[4], m = -INFINITY;
+      const int t = qi[r] < p.B ? p.target[qi[r]] : -1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[j] = ni[j] < p.N ? (float)pair_score<T>(acc[j][r], x2[r], y2[j], bn_[j], cr[r], p) : -INFINITY;
+        m = fmaxf(m, s[j]);
+        if (ni[j] == t) p.tgt_logit[qi[r]] = s[j];
+      }
+      // reduce over the 16 lanes of this row group
+      m = fmaxf(m, __shfl_xor(m, 1));
+      m = fmaxf(m, __shfl_xor(m, 2));
+      m = fmaxf(m, __shfl_xor(m, 4));
+      m = fmaxf(m, __shfl_xor(m, 8));
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) se += ni[j] < p.N ? expf(s[j] - m) : 0.f;
+      se = group16_sum(se);
+      if ((lane & 15) == 0 && qi[r] < p.B) {
+        float* o = p.part + ((int64_t)qi[r] * nblk + bn) * 2;
+        o[0] = m;
+        o[1] = se;
+      }
+    }
+  }
+}
+
+// Combine per-tile (max, sumexp) into per-query loss = lse - target logit (one wave per query).
+__global__ __launch_bounds__(256) void k_ce_combine(const float* __restrict__ part, const float* __restrict__ tgt,
+                                                    int B, int nblk, float* __restrict__ loss) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float* pb = part + (int64_t)b * nblk * 2;
+  float m = -INFINITY;
+  for (int i = lane; i < nblk; i += 64) m = fmaxf(m, pb[2 * i]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int i = lane; i < nblk; i += 64) s += pb[2 * i + 1] * expf(pb[2 * i] - m);
+  s = wave_sum(s);
+  if (lane == 0) loss[b] = (m + logf(s)) - tgt[b];
+}
+
+// Rank of the target under a descending sort, as 1 + #{n : S[b,n] > S[b,t]} (raw)
+// and the same count excluding the other true answers of the snapshot (time-aware
+// filter, rgcn/utils.py:51-75 sets them to -1e7).  filt_ptr/filt_idx: CSR of the
+// entities to exclude per query (target itself excluded by the host).
+__global__ __launch_bounds__(256) void k_rank(const float* __restrict__ S, int B, int N, const int* __restrict__ target,
+                                              const int* __restrict__ filt_ptr, const int* __restrict__ filt_idx,
+                                              int* __restrict__ rank_raw, int* __restrict__ rank_filt) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float* row = S + (int64_t)b * N;
+  const float ts = row[target[b]];
+  int cnt = 0;
+  for (int n = lane * 4; n < N; n += 256) {
+    if (n + 3 < N && ((reinterpret_cast<uintptr_t>(row + n) & 15) == 0)) {
+      f4 v = *reinterpret_cast<const f4*>(row + n);
+      cnt += (v.x > ts) + (v.y > ts) + (v.z > ts) + (v.w > ts);
+    } else {
+      for (int u = 0; u < 4 && n + u < N; ++u) cnt += row[n + u] > ts;
+    }
+  }
+  int f = 0;
+  if (filt_ptr) {
+    for (int i = filt_ptr[b] + lane; i < filt_ptr[b + 1]; i += 64) f += row[filt_idx[i]] > ts;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o);
+    f += __shfl_xor(f, o);
+  }
+  if (lane == 0) {
+    rank_raw[b] = cnt + 1;
+    if (rank_filt) rank_filt[b] = cnt - f + 1;
+  }
+}
+
+int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
+  if (a.d <= 0 || (a.d & 3)) return set_error(REGCN_EINVAL, "score needs d %% 4 == 0");
+  if (!a.q || !a.e) return set_error(REGCN_EINVAL, "null pointer");
+  if (a.B == 0 || a.N == 0) return 0;
+  const int nbq = (a.B + SQ - 1) / SQ, nbn = (a.N + SN - 1) / SN;
+  const long blocks = (long)nbq * nbn;
+  if (blocks > 0x7fffffffL) return set_error(REGCN_EINVAL, "score grid too large");
+  dim3 g((unsigned)blocks), b(256);
+  if (mode == 0) {
+    if (!a.out) return set_error(REGCN_EINVAL, "null output");
+    if (a.use_dist) hipLaunchKernelGGL((k_score<0, true>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((k_score<0, false>), g, b, 0, st, a);
+    return check_launch("k_score");
+  }
+  if (!a.target || !a.part || !a.tgt_logit || !loss) return set_error(REGCN_EINVAL, "CE needs target/workspace/loss");
+  if (a.use_dist) hipLaunchKernelGGL((k_score<1, true>), g, b, 0, st, a);
+  else hipLaunchKernelGGL((k_score<1, false>), g, b, 0, st, a);
+  int rc = check_launch("k_score_ce");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_ce_combine, dim3((a.B + 3) / 4), b, 0, st, a.part, a.tgt_logit, a.B, nbn, loss);
+  return check_launch("k_ce_combine");
+}
+
+int rank(const float* S, int B, int N, const int* target, const int* filt_ptr, const int* filt_idx, int* rank_raw,
+         int* rank_filt, hipStream_t st) {
+  if (!S || !target || !rank_raw) return set_error(REGCN_EINVAL, "null pointer");
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(k_rank, dim3((B + 3) / 4), dim3(256), 0, st, S, B, N, target, filt_ptr, filt_idx, rank_raw,
+                     rank_filt);
+  return check_launch("k_rank");
+}
+
+}  // namespace regcn

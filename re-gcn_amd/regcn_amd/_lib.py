@@ -1,0 +1,117 @@
+"""ctypes binding to libregcn_hip.so (the C-ABI declared in include/regcn_hip.h).
+
+The library is built in-tree by `__graft_entry__.build()` (hipcc --offload-arch=gfx950)
+and loaded from this directory.  There is no fallback: if the library is missing or a
+tensor is not a contiguous fp32/int32 HIP tensor, the call raises.
+
+torch is imported before the library so that libregcn_hip.so binds to the same
+libamdhip64 instance (same soname) that torch already loaded: one HIP runtime, one
+set of streams.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libregcn_hip.so")
+ABI_VERSION = 1
+
+_c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+P = _c_vp
+
+# name -> argtypes (restype int32 unless listed in _RESTYPE)
+_SIGS = {
+    "regcn_version": [],
+    "regcn_last_error_string": [],
+    "regcn_log0_f32": [P, _c_i64, _c_int, _c_f, P, P],
+    "regcn_exp0_f32": [P, _c_i64, _c_int, _c_f, P, P],
+    "regcn_project_f32": [P, _c_i64, _c_int, _c_f, P, P],
+    "regcn_apply_radius_f32": [P, P, _c_i64, _c_int, _c_f, P, P],
+    "regcn_radius_f32": [P, _c_i64, _c_int, P, P],
+    "regcn_sumsq_f32": [P, _c_i64, _c_int, P, P],
+    "regcn_mobius_add_f32": [P, P, _c_i64, _c_int, _c_f, P, P],
+    "regcn_to_lorentz_f32": [P, _c_i64, _c_int, _c_f, P, P],
+    "regcn_to_poincare_f32": [P, _c_i64, _c_int, _c_f, P, P],
+    "regcn_prologue_f32": [P, _c_i64, _c_int, _c_f, P, P, P],
+    "regcn_ln_roundtrip_f32": [P, _c_i64, _c_int, _c_f, P, P],
+    "regcn_init_entities_f32": [P, P, _c_i64, _c_int, _c_f, _c_int, P, P, P, P],
+    "regcn_union_aggregate_f32": [P, P, P, P, P, P, P, _c_int, P, _c_int, _c_f, _c_int, P, _c_int, P, P],
+    "regcn_euclid_aggregate_f32": [P, P, P, P, P, P, _c_int, P, _c_int, _c_int, P, _c_int, P, P],
+    "regcn_segment_mean_f32": [P, P, P, P, _c_int, P, _c_int, _c_int, P, _c_int, P, P],
+    "regcn_lorentz_aggregate_f32": [P, P, P, P, P, P, _c_int, P, _c_int, _c_int, _c_f, _c_int, P, _c_int, P, P],
+    "regcn_layer_tail_f32": [P, P, P, P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_int, _c_f, P, P, P, P],
+    "regcn_timestep_f32": [P, P, P, P, P, P, P, _c_f, _c_f, _c_int, _c_int, _c_int, _c_int, _c_f, _c_f, P, P, P, P],
+    "regcn_hyp_score_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P],
+    "regcn_hyp_ce_workspace_bytes": [_c_int, _c_int],
+    "regcn_hyp_ce_f32": [P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P, P],
+    "regcn_rank_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
+}
+_RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz}
+
+_lib = None
+
+
+class HipLibraryError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raise if the HIP library is unavailable."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipLibraryError(
+                "libregcn_hip.so not found at %s; build it with `python -c \"import __graft_entry__ as g; "
+                "g.build()\"`" % LIB_PATH)
+        h = ctypes.CDLL(LIB_PATH)
+        for name, args in _SIGS.items():
+            fn = getattr(h, name)
+            fn.argtypes = args
+            fn.restype = _RESTYPE.get(name, _c_int)
+        v = h.regcn_version()
+        if v != ABI_VERSION:
+            raise HipLibraryError("libregcn_hip.so ABI %d != expected %d" % (v, ABI_VERSION))
+        _lib = h
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc, name):
+    if rc != 0:
+        msg = lib().regcn_last_error_string().decode(errors="replace")
+        raise RuntimeError("%s failed (rc=%d): %s" % (name, rc, msg))
+
+
+def call(name, *args):
+    check(getattr(lib(), name)(*args), name)
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dptr(t, dtype=torch.float32, what="tensor"):
+    """Device pointer of a contiguous HIP tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not isinstance(t, torch.Tensor):
+        raise TypeError("%s must be a torch.Tensor" % what)
+    if not t.is_cuda:
+        raise ValueError("%s must live on a HIP device (got %s); the HIP path has no CPU fallback" % (what, t.device))
+    if t.dtype != dtype:
+        raise TypeError("%s must be %s (got %s)" % (what, dtype, t.dtype))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % what)
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def fptr(t, what="tensor"):
+    return dptr(t, torch.float32, what)
+
+
+def iptr(t, what="index tensor"):
+    return dptr(t, torch.int32, what)

@@ -1,0 +1,219 @@
+"""Snapshot graph: the DGL-free replacement of the object built by rgcn/utils.py:100-134.
+
+`build_sub_graph(num_nodes, num_rels, triples, use_cuda, gpu)` keeps the reference
+signature and edge semantics bit-exactly:
+  * edges in the reference order: src = cat(s, o), dst = cat(o, s), type = cat(r, r + R)
+    (rgcn/utils.py:116-118, :125);
+  * in-degree over the doubled graph, norm = 1/in_deg with 0 -> 1, fp32 (:110-114);
+  * edge norm = norm[dst] * norm[src] (:124); node id = arange(V) (:122);
+  * uniq_r / r_len / r_to_e as in r2e (:78-97); each r_to_e span holds the same entity
+    SET as the reference (its order there is Python set-iteration order).
+
+On top of the DGL-visible surface (ndata/edata/in_degrees/number_of_nodes/to) the
+object carries the device-side work lists the HIP kernels consume:
+  * a destination-sorted CSR (stable, so equal destinations keep edge-id order):
+    col_src / col_type int32;
+  * `chunks` int32[n][4] = {row, edge_begin, edge_end, slot} with at most
+    `chunk_edges` edges per chunk, and `fixups` int32[m][4] = {row, slot_begin,
+    slot_end, 0} for rows split over several chunks (see csrc/aggregate.hip);
+  * `rows` int32[V]: rows with in-degree > 0 first, then the rest (`n_pos` of the
+    former), so every 64-row tile of the layer GEMM uses one self-loop weight;
+  * the same chunking over r_to_e for the relation-context mean.
+Built once per snapshot on the host and cached across epochs.
+"""
+import numpy as np
+import torch
+
+DEFAULT_CHUNK_EDGES = 512
+
+
+def r2e(triplets, num_rels):
+    """rgcn/utils.py:78-97.  Returns (uniq_r, r_len list of (start, end), r_to_e list)."""
+    triplets = np.asarray(triplets, dtype=np.int64).reshape(-1, 3)
+    src, rel, dst = triplets[:, 0], triplets[:, 1], triplets[:, 2]
+    uniq = np.unique(rel)
+    uniq_r = np.concatenate((uniq, uniq + num_rels))
+    if len(triplets) == 0:
+        return uniq_r, [], []
+    order = np.argsort(rel, kind="stable")
+    rel_sorted = rel[order]
+    starts = np.searchsorted(rel_sorted, uniq, side="left")
+    ends = np.searchsorted(rel_sorted, uniq, side="right")
+    per_rel = []
+    for a, b in zip(starts, ends):
+        idx = order[a:b]
+        per_rel.append(np.unique(np.concatenate((src[idx], dst[idx]))))
+    r_len, e_idx, pos = [], [], 0
+    for ents in per_rel + per_rel:  # inverse ids share the forward set (:88-89)
+        r_len.append((pos, pos + len(ents)))
+        e_idx.append(ents)
+        pos += len(ents)
+    return uniq_r, r_len, np.concatenate(e_idx).tolist()
+
+
+def _chunk_rows(seg_ptr, seg_rows, chunk_edges):
+    """Cut segments [seg_ptr[i], seg_ptr[i+1]) of row seg_rows[i] into chunks."""
+    lens = np.diff(seg_ptr)
+    nz = lens > 0
+    rows, beg, lens = seg_rows[nz], seg_ptr[:-1][nz], lens[nz]
+    nchunk = (lens + chunk_edges - 1) // chunk_edges
+    total = int(nchunk.sum())
+    rep_rows = np.repeat(rows, nchunk)
+    rep_beg = np.repeat(beg, nchunk)
+    first = np.repeat(np.cumsum(nchunk) - nchunk, nchunk)
+    k = np.arange(total) - first
+    c_beg = rep_beg + k * chunk_edges
+    c_end = np.minimum(c_beg + chunk_edges, np.repeat(beg + lens, nchunk))
+    multi = np.repeat(nchunk > 1, nchunk)
+    slot = np.full(total, -1, dtype=np.int64)
+    slot[multi] = np.arange(int(multi.sum()))
+    chunks = np.stack([rep_rows, c_beg, c_end, slot], 1).astype(np.int32)
+    long_rows = rows[nchunk > 1]
+    ncl = nchunk[nchunk > 1]
+    sb = np.cumsum(ncl) - ncl
+    fixups = np.stack([long_rows, sb, sb + ncl, np.zeros_like(ncl)], 1).astype(np.int32)
+    return chunks.reshape(-1, 4), fixups.reshape(-1, 4), int(multi.sum())
+
+
+class _Frame(dict):
+    """dict with DGL's `ndata`/`edata` feel (get/pop/update/[])."""
+
+
+class SnapshotGraph:
+    """One temporal snapshot (see module docstring)."""
+
+    def __init__(self, num_nodes, num_rels, src, dst, etype, uniq_r, r_len, r_to_e,
+                 chunk_edges=DEFAULT_CHUNK_EDGES):
+        V = int(num_nodes)
+        self.num_nodes_, self.num_rels = V, int(num_rels)
+        self.device = torch.device("cpu")
+        E = len(src)
+        if V >= 2 ** 31 - 1 or E >= 2 ** 31 - 1:
+            raise ValueError("snapshot too large for int32 indices")
+        in_deg = np.bincount(dst, minlength=V).astype(np.int64)
+        deg_f = in_deg.astype(np.float32)
+        deg_f[deg_f == 0] = 1.0
+        norm = (np.float32(1.0) / deg_f).astype(np.float32)
+        self.src_np, self.dst_np, self.type_np = src, dst, etype
+        self.in_deg_np = in_deg
+        self.uniq_r = uniq_r
+        self.r_len = r_len
+        self.r_to_e = r_to_e
+        self.ndata = _Frame(id=torch.arange(V, dtype=torch.long).view(-1, 1),
+                            norm=torch.from_numpy(norm).view(-1, 1))
+        self.edata = _Frame(type=torch.from_numpy(etype.astype(np.int64)),
+                            norm=torch.from_numpy((norm[dst] * norm[src]).astype(np.float32)).view(-1, 1))
+        # ---- kernel work lists (int32, host) ----
+        order = np.argsort(dst, kind="stable")
+        rowptr = np.zeros(V + 1, dtype=np.int64)
+        np.cumsum(in_deg, out=rowptr[1:])
+        self.chunk_edges = int(chunk_edges)
+        chunks, fixups, nslot = _chunk_rows(rowptr, np.arange(V), self.chunk_edges)
+        pos = np.nonzero(in_deg > 0)[0]
+        zero = np.nonzero(in_deg == 0)[0]
+        R2 = 2 * self.num_rels
+        rel_ptr = np.zeros(R2 + 1, dtype=np.int64)
+        rel_count = np.zeros(R2, dtype=np.float32)
+        if len(r_len):
+            lens = np.array([b - a for a, b in r_len], dtype=np.int64)
+            ur = np.asarray(uniq_r, dtype=np.int64)
+            rel_count[ur] = lens
+            # spans are laid out in uniq_r order; re-express them per relation id
+            starts = np.array([a for a, _ in r_len], dtype=np.int64)
+            rel_start = np.zeros(R2, dtype=np.int64)
+            rel_start[ur] = starts
+            rel_len = np.zeros(R2, dtype=np.int64)
+            rel_len[ur] = lens
+            rchunks, rfix, rslot = _chunk_rows_spans(rel_start, rel_len, self.chunk_edges)
+        else:
+            rchunks, rfix, rslot = np.zeros((0, 4), np.int32), np.zeros((0, 4), np.int32), 0
+        del rel_ptr
+        self._host = {
+            "col_src": src[order].astype(np.int32), "col_type": etype[order].astype(np.int32),
+            "chunks": chunks, "fixups": fixups, "norm": norm,
+            "rows": np.concatenate([pos, zero]).astype(np.int32),
+            "rel_idx": np.asarray(r_to_e, dtype=np.int32).reshape(-1),
+            "rel_count": rel_count, "rel_chunks": rchunks, "rel_fixups": rfix,
+        }
+        self.n_pos = int(len(pos))
+        self.n_slots = nslot
+        self.rel_slots = rslot
+        self.dev = None
+
+    # ---------------------------------------------------------------- DGL-visible surface
+    def number_of_nodes(self):
+        return self.num_nodes_
+
+    def number_of_edges(self):
+        return int(len(self.src_np))
+
+    def in_degrees(self, v=None):
+        deg = torch.from_numpy(self.in_deg_np).to(self.device)
+        if v is None:
+            return deg
+        idx = torch.as_tensor(list(v) if isinstance(v, range) else v, dtype=torch.long, device=self.device)
+        return deg[idx]
+
+    def edges(self):
+        return torch.from_numpy(self.src_np), torch.from_numpy(self.dst_np)
+
+    def to(self, device):
+        """Move the graph (node/edge data and kernel work lists) to `device`.
+        Accepts the reference's gpu ids (int), strings or torch.device."""
+        if isinstance(device, int):
+            device = torch.device("cuda", device) if device >= 0 else torch.device("cpu")
+        device = torch.device(device)
+        if device == self.device:
+            return self
+        g = object.__new__(SnapshotGraph)
+        g.__dict__.update(self.__dict__)
+        g.device = device
+        g.ndata = _Frame({k: v.to(device) for k, v in self.ndata.items()})
+        g.edata = _Frame({k: v.to(device) for k, v in self.edata.items()})
+        g.dev = {k: torch.from_numpy(v).to(device) for k, v in self._host.items()} if device.type == "cuda" else None
+        return g
+
+    def work(self):
+        """Device work lists (raises on a CPU graph: the HIP path has no CPU fallback)."""
+        if self.dev is None:
+            raise ValueError("SnapshotGraph must be moved to a HIP device (g.to('cuda')) before message passing")
+        return self.dev
+
+
+def _chunk_rows_spans(start, length, chunk_edges):
+    """Chunk per-relation spans [start[r], start[r]+length[r]) of the r_to_e list."""
+    R = len(start)
+    order = np.arange(R)
+    nz = length > 0
+    rows, beg, lens = order[nz], start[nz], length[nz]
+    ptr = np.zeros(len(rows) + 1, dtype=np.int64)
+    # re-use _chunk_rows by building a synthetic pointer per relation
+    chunks_l, fix_l, nslot = [], [], 0
+    nchunk = (lens + chunk_edges - 1) // chunk_edges
+    for r, b, n, k in zip(rows, beg, lens, nchunk):
+        if k == 1:
+            chunks_l.append((r, b, b + n, -1))
+        else:
+            for i in range(k):
+                chunks_l.append((r, b + i * chunk_edges, min(b + (i + 1) * chunk_edges, b + n), nslot + i))
+            fix_l.append((r, nslot, nslot + k, 0))
+            nslot += k
+    del ptr
+    chunks = np.array(chunks_l, dtype=np.int32).reshape(-1, 4)
+    fixups = np.array(fix_l, dtype=np.int32).reshape(-1, 4)
+    return chunks, fixups, nslot
+
+
+def build_sub_graph(num_nodes, num_rels, triples, use_cuda=False, gpu=0, chunk_edges=DEFAULT_CHUNK_EDGES):
+    """rgcn/utils.py:100-134 (same signature; returns a SnapshotGraph)."""
+    triples = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+    s, r, o = triples[:, 0], triples[:, 1], triples[:, 2]
+    src = np.concatenate((s, o))
+    dst = np.concatenate((o, s))
+    etype = np.concatenate((r, r + num_rels))
+    uniq_r, r_len, r_to_e = r2e(triples, num_rels)
+    g = SnapshotGraph(num_nodes, num_rels, src, dst, etype, uniq_r, r_len, r_to_e, chunk_edges=chunk_edges)
+    if use_cuda:
+        g = g.to(gpu)
+        g.r_to_e = torch.from_numpy(np.array(r_to_e, dtype=np.int64))  # :133
+    return g

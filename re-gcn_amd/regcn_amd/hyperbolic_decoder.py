@@ -1,0 +1,464 @@
+"""Hyperbolic decoders with HIP scoring (mirror of hyperbolic_src/hyperbolic_decoder.py).
+
+The scoring half — `_chunked_hyperbolic_dist_score` and `_chunked_hyperbolic_ce_loss`,
+same signatures — runs on the fp32-MFMA scorer (csrc/score.hip): one GEMM Q E^T plus a
+per-pair epilogue that reproduces mobius_add(-q, e) / the arctanh distance without
+expanding B x N x d.  The chunk sizes are accepted as tiling hints and do not change the
+math (hyperbolic_decoder.py:104-106).  Query prologues (MuRP / RotH / AttH and their
+relation variants) keep the reference's parameters and state_dict keys; their row maps
+run on the HIP row kernels, their small projections on torch.  Forward only.
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.nn.parameter import Parameter
+
+from . import _lib
+from .hyperbolic_ops import HyperbolicOps
+
+SCORE_SCALE_EPSILON = 1e-6
+REL_CURVATURE_EPSILON = 1e-5
+REL_CURVATURE_SAFETY_MARGIN = 0.999
+REL_CURVATURE_INIT_RATIO = 0.95
+
+
+def _softplus_inverse(x, eps=1e-12):
+    return math.log(max(math.exp(float(x)) - 1.0, eps))
+
+
+def _relation_curvature_theta_init(global_c):
+    """hyperbolic_decoder.py:46-63."""
+    if torch.is_tensor(global_c):
+        global_c = global_c.detach().item()
+    return _softplus_inverse(max(float(global_c) * REL_CURVATURE_INIT_RATIO, REL_CURVATURE_EPSILON))
+
+
+def _clamp_relation_curvature(rel_c_raw, global_c, warmup_max=None):
+    """hyperbolic_decoder.py:66-86."""
+    g = global_c if torch.is_tensor(global_c) else rel_c_raw.new_tensor(float(global_c))
+    upper = REL_CURVATURE_SAFETY_MARGIN * g.to(rel_c_raw.device, rel_c_raw.dtype)
+    if warmup_max is not None:
+        upper = torch.min(upper, rel_c_raw.new_tensor(float(warmup_max)))
+    return torch.max(torch.min(rel_c_raw, upper), rel_c_raw.new_tensor(REL_CURVATURE_EPSILON))
+
+
+def _cf(c):
+    return float(c.item()) if torch.is_tensor(c) else float(c)
+
+
+def _scalar(v, like):
+    """Device fp32 scalar tensor for the kernel (None -> None)."""
+    if v is None:
+        return None
+    if torch.is_tensor(v):
+        return v.detach().reshape(1).to(device=like.device, dtype=torch.float32).contiguous()
+    return torch.full((1,), float(v), device=like.device, dtype=torch.float32)
+
+
+def _score_operands(query, candidates, bias, score_scale, score_margin, query_curvature):
+    q = query.detach().contiguous().float()
+    e = candidates.detach().contiguous().float()
+    b = bias.detach().contiguous().float() if bias is not None else None
+    cr = query_curvature.detach().reshape(-1).contiguous().float() if query_curvature is not None else None
+    return q, e, b, cr, _scalar(score_scale, q), _scalar(score_margin, q)
+
+
+def _chunked_hyperbolic_dist_score(query, candidates, bias, c, q_chunk_size, c_chunk_size, score_scale=None,
+                                   score_margin=0.0, query_curvature=None, use_hyperbolic_distance=False):
+    """hyperbolic_decoder.py:89-179 -> regcn_hyp_score_f32.  Returns (B, N)."""
+    B, d = query.shape
+    N = candidates.shape[0]
+    q, e, b, cr, sc, mg = _score_operands(query, candidates, bias, score_scale, score_margin,
+                                                    query_curvature if use_hyperbolic_distance else None)
+    out = torch.empty(B, N, device=q.device, dtype=torch.float32)
+    f = _lib.fptr
+    _lib.call("regcn_hyp_score_f32", f(q, "query"), f(e, "candidates"), f(b), f(cr), f(sc), f(mg),
+              B, N, d, _cf(c), int(bool(use_hyperbolic_distance)), f(out), _lib.stream())
+    return out
+
+
+def _chunked_hyperbolic_ce_loss(query, candidates, target, c, c_chunk_size, candidate_bias=None, query_bias=None,
+                                q_chunk_size=None, score_scale=None, score_margin=0.0, query_curvature=None,
+                                use_hyperbolic_distance=False):
+    """hyperbolic_decoder.py:182-307 -> regcn_hyp_ce_f32 (fused scores + log-sum-exp; the
+    B x N logits are never materialised).  query_bias cancels in CE and is ignored (:204-205)."""
+    B, d = query.shape
+    N = candidates.shape[0]
+    q, e, b, cr, sc, mg = _score_operands(query, candidates, candidate_bias, score_scale, score_margin,
+                                                    query_curvature if use_hyperbolic_distance else None)
+    tgt = target.to(device=q.device, dtype=torch.int32).contiguous()
+    ws_bytes = _lib.lib().regcn_hyp_ce_workspace_bytes(B, N)
+    ws = torch.empty((ws_bytes + 3) // 4, device=q.device, dtype=torch.float32)
+    loss = torch.empty(B, device=q.device, dtype=torch.float32)
+    f = _lib.fptr
+    _lib.call("regcn_hyp_ce_f32", f(q, "query"), f(e, "candidates"), f(b), f(cr), f(sc), f(mg),
+              _lib.iptr(tgt, "target"), B, N, d, _cf(c), int(bool(use_hyperbolic_distance)), f(ws), f(loss),
+              _lib.stream())
+    return loss.mean()
+
+
+def givens_rotation(x, angles):
+    """hyperbolic_decoder.py:1032-1051 (interleaved pairs)."""
+    if angles.dim() == 1:
+        angles = angles.unsqueeze(0).expand(x.shape[0], -1)
+    x1, x2 = x[:, 0::2], x[:, 1::2]
+    co, si = torch.cos(angles), torch.sin(angles)
+    return torch.stack([co * x1 - si * x2, si * x1 + co * x2], dim=2).reshape(x.shape[0], x.shape[1])
+
+
+def givens_reflection(x, angles):
+    """hyperbolic_decoder.py:1392-1401."""
+    if angles.dim() == 1:
+        angles = angles.unsqueeze(0).expand(x.shape[0], -1)
+    x1, x2 = x[:, 0::2], x[:, 1::2]
+    co, si = torch.cos(angles), torch.sin(angles)
+    return torch.stack([co * x1 + si * x2, si * x1 - co * x2], dim=2).reshape(x.shape[0], x.shape[1])
+
+
+class _EntityDecoderBase(nn.Module):
+    """Shared state of MuRP/RotH/AttH entity decoders (hyperbolic_decoder.py:662-731)."""
+
+    def _init_common(self, num_entities, num_relations, embedding_dim, c, dropout, query_chunk_size,
+                     candidate_chunk_size, score_scale_init, score_margin_init, use_entity_euclidean_bias,
+                     use_relation_specific_curvature):
+        self.num_entities, self.embedding_dim, self.c = num_entities, embedding_dim, c
+        self.query_chunk_size, self.candidate_chunk_size = query_chunk_size, candidate_chunk_size
+        self.num_relations = num_relations
+        self.use_entity_euclidean_bias = use_entity_euclidean_bias
+        self.use_relation_specific_curvature = use_relation_specific_curvature
+
+    def _init_tail(self, num_entities, num_relations, c, score_scale_init, score_margin_init, dropout,
+                   use_entity_euclidean_bias, use_relation_specific_curvature):
+        if use_entity_euclidean_bias:
+            self.entity_bias = nn.Parameter(torch.zeros(num_entities))
+        else:
+            self.register_parameter("entity_bias", None)
+        if use_relation_specific_curvature:
+            self.rel_curvature_raw = nn.Parameter(torch.full((num_relations,), _relation_curvature_theta_init(c)))
+            self.rel_curvature_max = float(c)
+        else:
+            self.register_parameter("rel_curvature_raw", None)
+            self.rel_curvature_max = None
+        self.score_scale_raw = nn.Parameter(torch.tensor(float(score_scale_init)))
+        self.score_margin = nn.Parameter(torch.tensor(float(score_margin_init)))
+        self.dropout = nn.Dropout(dropout)
+
+    def _score_scale(self):
+        return F.softplus(self.score_scale_raw) + SCORE_SCALE_EPSILON
+
+    def _relation_curvature(self, r_idx):
+        if self.rel_curvature_raw is None:
+            return None
+        raw = F.softplus(self.rel_curvature_raw[torch.remainder(r_idx, self.num_relations)])
+        return _clamp_relation_curvature(raw, self.c, self.rel_curvature_max)
+
+    def set_relation_curvature_bounds(self, curvature_max=None):
+        if curvature_max is not None:
+            self.rel_curvature_max = float(curvature_max)
+
+    def _query(self, entity_embedding, rel_embedding, triplets):
+        raise NotImplementedError
+
+    def forward(self, entity_embedding, rel_embedding, triplets, mode="train"):
+        q = self._query(entity_embedding, rel_embedding, triplets)
+        rel_c = self._relation_curvature(triplets[:, 1])
+        scores = _chunked_hyperbolic_dist_score(
+            q, entity_embedding, self.entity_bias, self.c, self.query_chunk_size, self.candidate_chunk_size,
+            score_scale=self._score_scale(), score_margin=self.score_margin, query_curvature=rel_c,
+            use_hyperbolic_distance=self.use_relation_specific_curvature)
+        if self.entity_bias is not None:
+            scores = scores + self.entity_bias[triplets[:, 0]].unsqueeze(1)
+        return scores
+
+    def loss(self, entity_embedding, rel_embedding, triplets):
+        q = self._query(entity_embedding, rel_embedding, triplets)
+        rel_c = self._relation_curvature(triplets[:, 1])
+        return _chunked_hyperbolic_ce_loss(
+            q, entity_embedding, triplets[:, 2], self.c, self.candidate_chunk_size, candidate_bias=self.entity_bias,
+            q_chunk_size=self.query_chunk_size, score_scale=self._score_scale(), score_margin=self.score_margin,
+            query_curvature=rel_c, use_hyperbolic_distance=self.use_relation_specific_curvature)
+
+
+class HyperbolicMuRP(_EntityDecoderBase):
+    """hyperbolic_decoder.py:647-817."""
+
+    def __init__(self, num_entities, num_relations, embedding_dim, c=0.01, dropout=0.0, query_chunk_size=128,
+                 candidate_chunk_size=256, init_scale=1e-3, score_scale_init=1.0, score_margin_init=1.0,
+                 use_entity_euclidean_bias=False, use_relation_specific_curvature=False):
+        super().__init__()
+        self._init_common(num_entities, num_relations, embedding_dim, c, dropout, query_chunk_size,
+                          candidate_chunk_size, score_scale_init, score_margin_init, use_entity_euclidean_bias,
+                          use_relation_specific_curvature)
+        self.rot_proj = nn.Linear(embedding_dim, embedding_dim)
+        self.trans_proj = nn.Linear(embedding_dim, embedding_dim)
+        for lin in (self.rot_proj, self.trans_proj):
+            nn.init.uniform_(lin.weight, -init_scale, init_scale)
+            nn.init.zeros_(lin.bias)
+        self._init_tail(num_entities, num_relations, c, score_scale_init, score_margin_init, dropout,
+                        use_entity_euclidean_bias, use_relation_specific_curvature)
+
+    def _query(self, ent, rel, trip):
+        """hyperbolic_decoder.py:745-764."""
+        c = self.c
+        r_idx = trip[:, 1]
+        s_emb = HyperbolicOps.project_to_ball(ent[trip[:, 0]], c)
+        s_tan = self.dropout(HyperbolicOps.log_map_zero(s_emb, c))
+        rot_s = HyperbolicOps.exp_map_zero((self.rot_proj(rel[r_idx]) * s_tan).contiguous(), c)
+        t_r = HyperbolicOps.exp_map_zero(self.trans_proj(rel[r_idx]).contiguous(), c)
+        return HyperbolicOps.mobius_add(HyperbolicOps.project_to_ball(rot_s, c),
+                                        HyperbolicOps.project_to_ball(t_r, c), c)
+
+
+class HyperbolicRotH(_EntityDecoderBase):
+    """hyperbolic_decoder.py:931-1138."""
+
+    def __init__(self, num_entities, num_relations, embedding_dim, c=0.01, dropout=0.0, query_chunk_size=128,
+                 candidate_chunk_size=256, init_scale=1e-3, score_scale_init=1.0, score_margin_init=1.0,
+                 use_entity_euclidean_bias=False, use_relation_specific_curvature=False):
+        super().__init__()
+        assert embedding_dim % 2 == 0, "embedding_dim must be even (required for Givens rotation)"
+        self._init_common(num_entities, num_relations, embedding_dim, c, dropout, query_chunk_size,
+                          candidate_chunk_size, score_scale_init, score_margin_init, use_entity_euclidean_bias,
+                          use_relation_specific_curvature)
+        self.half_dim = embedding_dim // 2
+        self.rot_proj = nn.Linear(embedding_dim, self.half_dim)
+        self.trans_proj = nn.Linear(embedding_dim, embedding_dim)
+        self.reshape_fc1 = nn.Linear(embedding_dim, embedding_dim)
+        self.reshape_fc2 = nn.Linear(embedding_dim, embedding_dim)
+        for lin in (self.rot_proj, self.trans_proj, self.reshape_fc1, self.reshape_fc2):
+            nn.init.uniform_(lin.weight, -init_scale, init_scale)
+            nn.init.zeros_(lin.bias)
+        self._init_tail(num_entities, num_relations, c, score_scale_init, score_margin_init, dropout,
+                        use_entity_euclidean_bias, use_relation_specific_curvature)
+
+    givens_rotation = staticmethod(givens_rotation)
+
+    def _reshape_tangent(self, x):
+        return x + self.reshape_fc2(F.relu(self.reshape_fc1(x)))
+
+    def _query(self, ent, rel, trip):
+        """hyperbolic_decoder.py:1065-1085."""
+        c = self.c
+        r_idx = trip[:, 1]
+        s_emb = HyperbolicOps.project_to_ball(ent[trip[:, 0]], c)
+        s_tan = self._reshape_tangent(self.dropout(HyperbolicOps.log_map_zero(s_emb, c)))
+        rot_s = HyperbolicOps.exp_map_zero(givens_rotation(s_tan, self.rot_proj(rel[r_idx])).contiguous(), c)
+        t_r = HyperbolicOps.exp_map_zero(self.trans_proj(rel[r_idx]).contiguous(), c)
+        return HyperbolicOps.mobius_add(HyperbolicOps.project_to_ball(rot_s, c),
+                                        HyperbolicOps.project_to_ball(t_r, c), c)
+
+
+class HyperbolicAttH(_EntityDecoderBase):
+    """hyperbolic_decoder.py:1283-1512."""
+
+    def __init__(self, num_entities, num_relations, embedding_dim, c=0.01, dropout=0.0, query_chunk_size=128,
+                 candidate_chunk_size=256, init_scale=1e-3, score_scale_init=1.0, score_margin_init=1.0,
+                 use_entity_euclidean_bias=False, use_relation_specific_curvature=False):
+        super().__init__()
+        assert embedding_dim % 2 == 0, "embedding_dim must be even"
+        self._init_common(num_entities, num_relations, embedding_dim, c, dropout, query_chunk_size,
+                          candidate_chunk_size, score_scale_init, score_margin_init, use_entity_euclidean_bias,
+                          use_relation_specific_curvature)
+        self.half_dim = embedding_dim // 2
+        self.rot_proj = nn.Linear(embedding_dim, self.half_dim)
+        self.ref_proj = nn.Linear(embedding_dim, self.half_dim)
+        self.trans_proj = nn.Linear(embedding_dim, embedding_dim)
+        self.attn_proj = nn.Linear(embedding_dim, 2 * embedding_dim)
+        for lin in (self.rot_proj, self.ref_proj, self.trans_proj, self.attn_proj):
+            nn.init.uniform_(lin.weight, -init_scale, init_scale)
+            nn.init.zeros_(lin.bias)
+        self._init_tail(num_entities, num_relations, c, score_scale_init, score_margin_init, dropout,
+                        use_entity_euclidean_bias, use_relation_specific_curvature)
+
+    givens_rotation = staticmethod(givens_rotation)
+    givens_reflection = staticmethod(givens_reflection)
+
+    def _query(self, ent, rel, trip):
+        """hyperbolic_decoder.py:1414-1448."""
+        c = self.c
+        r_idx = trip[:, 1]
+        s_emb = HyperbolicOps.project_to_ball(ent[trip[:, 0]], c)
+        s_tan = self.dropout(HyperbolicOps.log_map_zero(s_emb, c))
+        rr = rel[r_idx]
+        rot_s = givens_rotation(s_tan, self.rot_proj(rr))
+        ref_s = givens_reflection(s_tan, self.ref_proj(rr))
+        a_r = torch.sigmoid(torch.sum(self.attn_proj(rr) * torch.cat([s_tan, rr], dim=-1), dim=-1, keepdim=True))
+        mixed = HyperbolicOps.exp_map_zero((a_r * rot_s + (1.0 - a_r) * ref_s).contiguous(), c)
+        t_r = HyperbolicOps.exp_map_zero(self.trans_proj(rr).contiguous(), c)
+        return HyperbolicOps.mobius_add(HyperbolicOps.project_to_ball(mixed, c),
+                                        HyperbolicOps.project_to_ball(t_r, c), c)
+
+
+class _RelDecoderBase(nn.Module):
+    def _score_scale(self):
+        return F.softplus(self.score_scale_raw) + SCORE_SCALE_EPSILON
+
+    def forward(self, entity_embedding, rel_embedding, triplets, mode="train"):
+        q = self._query(entity_embedding, triplets)
+        rel_hyp = HyperbolicOps.exp_map_zero(rel_embedding.contiguous(), self.c)
+        return _chunked_hyperbolic_dist_score(q, rel_hyp, self.rel_bias, self.c, self.query_chunk_size,
+                                              self.candidate_chunk_size, **self._score_kw())
+
+    def loss(self, entity_embedding, rel_embedding, triplets):
+        q = self._query(entity_embedding, triplets)
+        rel_hyp = HyperbolicOps.exp_map_zero(rel_embedding.contiguous(), self.c)
+        return _chunked_hyperbolic_ce_loss(q, rel_hyp, triplets[:, 1], self.c, self.candidate_chunk_size,
+                                           candidate_bias=self.rel_bias, q_chunk_size=self.query_chunk_size,
+                                           **self._score_kw())
+
+    def _score_kw(self):
+        return dict(score_scale=self._score_scale(), score_margin=self.score_margin)
+
+
+class HyperbolicMuRPRel(_RelDecoderBase):
+    """hyperbolic_decoder.py:820-928 (no score scale/margin in the reference)."""
+
+    def __init__(self, num_relations, embedding_dim, c=0.01, dropout=0.0, query_chunk_size=128,
+                 candidate_chunk_size=256):
+        super().__init__()
+        self.num_relations, self.embedding_dim, self.c = num_relations, embedding_dim, c
+        self.query_chunk_size, self.candidate_chunk_size = query_chunk_size, candidate_chunk_size
+        self.W_s = nn.Parameter(torch.Tensor(embedding_dim, embedding_dim))
+        nn.init.xavier_uniform_(self.W_s)
+        self.W_o = nn.Parameter(torch.Tensor(embedding_dim, embedding_dim))
+        nn.init.xavier_uniform_(self.W_o)
+        self.rel_bias = nn.Parameter(torch.zeros(num_relations * 2))
+        self.dropout = nn.Dropout(dropout)
+
+    def _score_kw(self):
+        return {}
+
+    def _query(self, ent, trip):
+        c = self.c
+        s_tan = self.dropout(HyperbolicOps.log_map_zero(ent[trip[:, 0]], c))
+        o_tan = self.dropout(HyperbolicOps.log_map_zero(ent[trip[:, 2]], c))
+        return HyperbolicOps.exp_map_zero((torch.mm(s_tan, self.W_s) + torch.mm(o_tan, self.W_o)).contiguous(), c)
+
+
+class HyperbolicRotHRel(_RelDecoderBase):
+    """hyperbolic_decoder.py:1141-1280."""
+
+    def __init__(self, num_relations, embedding_dim, c=0.01, dropout=0.0, query_chunk_size=128,
+                 candidate_chunk_size=256, init_scale=1e-3, score_scale_init=1.0, score_margin_init=1.0):
+        super().__init__()
+        assert embedding_dim % 2 == 0, "embedding_dim must be even"
+        self.num_relations, self.embedding_dim, self.half_dim, self.c = num_relations, embedding_dim, \
+            embedding_dim // 2, c
+        self.query_chunk_size, self.candidate_chunk_size = query_chunk_size, candidate_chunk_size
+        self.global_rot = nn.Parameter(torch.Tensor(self.half_dim))
+        nn.init.uniform_(self.global_rot, -math.pi, math.pi)
+        self.reshape_fc1 = nn.Linear(embedding_dim, embedding_dim)
+        self.reshape_fc2 = nn.Linear(embedding_dim, embedding_dim)
+        for lin in (self.reshape_fc1, self.reshape_fc2):
+            nn.init.uniform_(lin.weight, -init_scale, init_scale)
+            nn.init.zeros_(lin.bias)
+        self.rel_bias = nn.Parameter(torch.zeros(num_relations * 2))
+        self.score_scale_raw = nn.Parameter(torch.tensor(float(score_scale_init)))
+        self.score_margin = nn.Parameter(torch.tensor(float(score_margin_init)))
+        self.dropout = nn.Dropout(dropout)
+
+    givens_rotation = staticmethod(givens_rotation)
+
+    def _query(self, ent, trip):
+        """hyperbolic_decoder.py:1223-1234."""
+        c = self.c
+        o_emb = ent[trip[:, 2]].contiguous()
+        s_tan = self.dropout(HyperbolicOps.log_map_zero(ent[trip[:, 0]], c))
+        s_tan = s_tan + self.reshape_fc2(F.relu(self.reshape_fc1(s_tan)))
+        rot_s = HyperbolicOps.exp_map_zero(givens_rotation(s_tan, self.global_rot).contiguous(), c)
+        return HyperbolicOps.mobius_add(-rot_s, o_emb, c)
+
+
+class HyperbolicAttHRel(_RelDecoderBase):
+    """hyperbolic_decoder.py:1515-1679."""
+
+    def __init__(self, num_relations, embedding_dim, c=0.01, dropout=0.0, query_chunk_size=128,
+                 candidate_chunk_size=256, init_scale=1e-3, score_scale_init=1.0, score_margin_init=1.0):
+        super().__init__()
+        assert embedding_dim % 2 == 0, "embedding_dim must be even"
+        self.num_relations, self.embedding_dim, self.half_dim, self.c = num_relations, embedding_dim, \
+            embedding_dim // 2, c
+        self.query_chunk_size, self.candidate_chunk_size = query_chunk_size, candidate_chunk_size
+        self.global_rot = nn.Parameter(torch.Tensor(self.half_dim))
+        nn.init.uniform_(self.global_rot, -math.pi, math.pi)
+        self.global_ref = nn.Parameter(torch.Tensor(self.half_dim))
+        nn.init.uniform_(self.global_ref, -math.pi, math.pi)
+        self.attn_weight = nn.Parameter(torch.Tensor(2 * embedding_dim))
+        nn.init.uniform_(self.attn_weight, -init_scale, init_scale)
+        self.rel_bias = nn.Parameter(torch.zeros(num_relations * 2))
+        self.score_scale_raw = nn.Parameter(torch.tensor(float(score_scale_init)))
+        self.score_margin = nn.Parameter(torch.tensor(float(score_margin_init)))
+        self.dropout = nn.Dropout(dropout)
+
+    givens_rotation = staticmethod(givens_rotation)
+    givens_reflection = staticmethod(givens_reflection)
+
+    def _query(self, ent, trip):
+        """hyperbolic_decoder.py:1605-1628."""
+        c = self.c
+        o_emb = ent[trip[:, 2]].contiguous()
+        s_tan = self.dropout(HyperbolicOps.log_map_zero(ent[trip[:, 0]], c))
+        o_tan = HyperbolicOps.log_map_zero(o_emb, c)
+        a = torch.sigmoid(torch.mv(torch.cat([s_tan, o_tan], dim=-1), self.attn_weight)).unsqueeze(1)
+        mixed = a * givens_rotation(s_tan, self.global_rot) + (1.0 - a) * givens_reflection(s_tan, self.global_ref)
+        rot = HyperbolicOps.exp_map_zero(mixed.contiguous(), c)
+        return HyperbolicOps.mobius_add(-rot, o_emb, c)
+
+
+class HyperbolicConvTransE(nn.Module):
+    """hyperbolic_decoder.py:310-413 (tangent-space ConvTransE; host torch convolution,
+    HIP log0; the all-entity product is a plain GEMM)."""
+
+    def __init__(self, num_entities, embedding_dim, c=0.01, input_dropout=0.0, hidden_dropout=0.0,
+                 feature_map_dropout=0.0, channels=50, kernel_size=3):
+        super().__init__()
+        self.num_entities, self.embedding_dim, self.c = num_entities, embedding_dim, c
+        self.inp_drop = nn.Dropout(input_dropout)
+        self.hidden_drop = nn.Dropout(hidden_dropout)
+        self.feature_map_drop = nn.Dropout(feature_map_dropout)
+        self.conv1 = nn.Conv1d(2, channels, kernel_size, stride=1, padding=int(math.floor(kernel_size / 2)))
+        self.bn0 = nn.BatchNorm1d(2)
+        self.bn1 = nn.BatchNorm1d(channels)
+        self.bn2 = nn.BatchNorm1d(embedding_dim)
+        self.fc = nn.Linear(embedding_dim * channels, embedding_dim)
+        self.register_parameter("b", Parameter(torch.zeros(num_entities)))
+
+    def forward(self, entity_embedding, rel_embedding, triplets, mode="train"):
+        et = HyperbolicOps.log_map_zero(entity_embedding.contiguous(), self.c)
+        et = 0.9 * torch.tanh(et) + 0.1 * et
+        B = len(triplets)
+        x = torch.cat([et[triplets[:, 0]].unsqueeze(1), rel_embedding[triplets[:, 1]].unsqueeze(1)], 1)
+        x = self.feature_map_drop(F.relu(self.bn1(self.conv1(self.inp_drop(self.bn0(x))))))
+        x = self.hidden_drop(self.fc(x.view(B, -1)))
+        if B > 1:
+            x = self.bn2(x)
+        return torch.mm(F.relu(x), et.transpose(1, 0)) + self.b
+
+
+class HyperbolicConvTransR(nn.Module):
+    """hyperbolic_decoder.py:416-510."""
+
+    def __init__(self, num_relations, embedding_dim, c=0.01, input_dropout=0.0, hidden_dropout=0.0,
+                 feature_map_dropout=0.0, channels=50, kernel_size=3):
+        super().__init__()
+        self.num_relations, self.embedding_dim, self.c = num_relations, embedding_dim, c
+        self.inp_drop = nn.Dropout(input_dropout)
+        self.hidden_drop = nn.Dropout(hidden_dropout)
+        self.feature_map_drop = nn.Dropout(feature_map_dropout)
+        self.conv1 = nn.Conv1d(2, channels, kernel_size, stride=1, padding=int(math.floor(kernel_size / 2)))
+        self.bn0 = nn.BatchNorm1d(2)
+        self.bn1 = nn.BatchNorm1d(channels)
+        self.bn2 = nn.BatchNorm1d(embedding_dim)
+        self.fc = nn.Linear(embedding_dim * channels, embedding_dim)
+        self.register_parameter("b", Parameter(torch.zeros(num_relations * 2)))
+
+    def forward(self, entity_embedding, rel_embedding, triplets, mode="train"):
+        et = HyperbolicOps.log_map_zero(entity_embedding.contiguous(), self.c)
+        et = 0.9 * torch.tanh(et) + 0.1 * et
+        B = len(triplets)
+        x = torch.cat([et[triplets[:, 0]].unsqueeze(1), et[triplets[:, 2]].unsqueeze(1)], 1)
+        x = self.feature_map_drop(F.relu(self.bn1(self.conv1(self.inp_drop(self.bn0(x))))))
+        x = self.bn2(self.hidden_drop(self.fc(x.view(B, -1))))
+        return torch.mm(F.relu(x), rel_embedding.transpose(1, 0)) + self.b

@@ -1,0 +1,312 @@
+"""HyperbolicRecurrentRGCN on HIP (mirror of hyperbolic_src/hyperbolic_model.py).
+
+Same constructor arguments, state_dict keys and the drop-in
+signatures `forward(g_list, static_graph, use_cuda)` -> (history_embs, static_emb, h_0,
+gate_list, degree_list), `predict(...)` and `get_loss(...)`.
+
+Per timestep (hyperbolic_model.py:797-884) the path is:
+  relation context mean        regcn_segment_mean_f32     (HIP)
+  relation GRU + normalize     torch.nn.GRUCell           (R2 x 2d -> d, host GEMM)
+  encoder cell (L layers)      prologue/aggregate/layer-tail kernels (HIP)
+  project/LN/time gate/radius  regcn_timestep_f32         (HIP, MFMA gate GEMM + fused epilogue)
+The initial entity state is one fused row kernel (regcn_init_entities_f32).
+
+Scope: eval/forward.  Static graph (--add-static-graph), EST components, FHNN/HGAT
+encoders and geoopt manifold parameters are out of scope and raise.
+"""
+import logging
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from .hyperbolic_decoder import (HyperbolicAttH, HyperbolicAttHRel, HyperbolicConvTransE, HyperbolicConvTransR,
+                                 HyperbolicMuRP, HyperbolicMuRPRel, HyperbolicRotH, HyperbolicRotHRel)
+from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell
+from .hyperbolic_ops import HyperbolicOps, TemporalRadiusEvolution
+from .tangent import attach, tangent_of
+
+logger = logging.getLogger("hyperbolic_model")
+GEOOPT_AVAILABLE = False
+
+
+class HyperbolicBaseRGCN(nn.Module):
+    """hyperbolic_model.py:74-111."""
+
+    def __init__(self, num_nodes, h_dim, out_dim, num_rels, num_bases=-1, num_hidden_layers=1, dropout=0, c=0.01,
+                 self_loop=False, skip_connect=False, encoder_name="hyperbolic_uvrgcn", rel_emb=None, use_cuda=False,
+                 analysis=False, radius_msg_gamma=1.0):
+        super().__init__()
+        self.num_nodes, self.h_dim, self.out_dim, self.num_rels = num_nodes, h_dim, out_dim, num_rels
+        self.num_bases, self.num_hidden_layers, self.dropout, self.c = num_bases, num_hidden_layers, dropout, c
+        self.self_loop, self.skip_connect, self.encoder_name = self_loop, skip_connect, encoder_name
+        self.rel_emb = rel_emb
+        self.use_cuda, self.run_analysis, self.radius_msg_gamma = use_cuda, analysis, radius_msg_gamma
+        self.layers = nn.ModuleList([self.build_hidden_layer(i) for i in range(num_hidden_layers)])
+
+    def build_hidden_layer(self, idx):
+        raise NotImplementedError
+
+
+class HyperbolicRGCNCell(HyperbolicBaseRGCN):
+    """hyperbolic_model.py:114-154."""
+
+    def build_hidden_layer(self, idx):
+        sc = False if idx == 0 or not self.skip_connect else True
+        return HyperbolicUnionRGCNLayer(self.h_dim, self.h_dim, self.num_rels, self.num_bases, c=self.c,
+                                        activation=F.rrelu, self_loop=self.self_loop, dropout=self.dropout,
+                                        skip_connect=sc, radius_msg_gamma=self.radius_msg_gamma)
+
+    def forward(self, g, init_ent_emb, init_rel_emb):
+        h = init_ent_emb  # node ids are arange(V): the reference gather is the identity
+        rel_embs = init_rel_emb if isinstance(init_rel_emb, list) else [init_rel_emb] * len(self.layers)
+        for i, layer in enumerate(self.layers):
+            h = layer(g, h, rel_embs[i])  # prev_h is never passed (hyperbolic_model.py:152)
+        return h
+
+
+def relation_context(x, g, num_rels2):
+    """x_input[r] = mean_{e in r_to_e span} x[e] (hyperbolic_model.py:802-812), HIP."""
+    wk = g.work()
+    V, d = x.shape
+    out = torch.zeros(num_rels2, d, device=x.device, dtype=torch.float32)
+    ch, fx = wk["rel_chunks"], wk["rel_fixups"]
+    part = torch.empty(g.rel_slots, d, device=x.device, dtype=torch.float32) if g.rel_slots else None
+    _lib.call("regcn_segment_mean_f32", _lib.fptr(x, "x"), _lib.iptr(wk["rel_idx"]), _lib.fptr(wk["rel_count"]),
+              _lib.iptr(ch), ch.shape[0], _lib.iptr(fx), fx.shape[0], d, _lib.fptr(part), d, _lib.fptr(out),
+              _lib.stream())
+    return out
+
+
+class HyperbolicRecurrentRGCN(nn.Module):
+    """hyperbolic_model.py:157-1128."""
+
+    def __init__(self, decoder_name, encoder_name, num_ents, num_rels, num_static_rels, num_words, h_dim, opn,
+                 sequence_len, num_bases=-1, num_hidden_layers=1, dropout=0, c=0.01, self_loop=False,
+                 skip_connect=False, layer_norm=False, input_dropout=0, hidden_dropout=0, feat_dropout=0, weight=1,
+                 discount=0, angle=0, use_static=False, entity_prediction=False, relation_prediction=False,
+                 use_cuda=False, gpu=0, analysis=False, learn_curvature=False, use_residual_evolution=True,
+                 radius_target=None, radius_lambda=0.02, radius_min=0.5, radius_max=3.0, radius_epsilon=0.1,
+                 radius_anchor_beta=1.0, curvature_min=1e-4, curvature_max=1e-1, num_heads=4, query_chunk_size=128,
+                 candidate_chunk_size=256, hyp_init_scale=1e-3, hyp_score_scale_init=1.0, hyp_score_margin_init=1.0,
+                 use_entity_euclidean_bias=False, use_relation_specific_curvature=False, use_est=False,
+                 est_state_alpha=0.2, est_encoder="gru", use_time_aware_negative=False, radius_msg_gamma=1.0):
+        super().__init__()
+        if use_static:
+            raise NotImplementedError("--add-static-graph is outside this build's scope (SURVEY.md §2 row 1)")
+        if use_est:
+            raise NotImplementedError("EST components are outside this build's scope (SURVEY.md §2 row 8)")
+        if encoder_name not in ("hyperbolic_uvrgcn", "lgcn"):
+            raise NotImplementedError("encoder %r is outside this build's scope (hyperbolic_uvrgcn, lgcn)"
+                                      % encoder_name)
+        self.decoder_name, self.encoder_name = decoder_name, encoder_name
+        self.num_rels, self.num_ents, self.opn, self.num_words = num_rels, num_ents, opn, num_words
+        self.num_static_rels, self.sequence_len, self.h_dim = num_static_rels, sequence_len, h_dim
+        self.layer_norm, self.h, self.run_analysis = layer_norm, None, analysis
+        self.weight, self.discount, self.use_static, self.angle = weight, discount, use_static, angle
+        self.relation_prediction, self.entity_prediction, self.gpu = relation_prediction, entity_prediction, gpu
+        self.learn_curvature, self.use_residual_evolution = learn_curvature, use_residual_evolution
+        self.radius_lambda, self.radius_min, self.radius_max = radius_lambda, radius_min, radius_max
+        self.radius_anchor_beta, self.curvature_min, self.curvature_max = radius_anchor_beta, curvature_min, \
+            curvature_max
+        self.num_heads, self.query_chunk_size, self.candidate_chunk_size = num_heads, query_chunk_size, \
+            candidate_chunk_size
+        self.use_entity_euclidean_bias = use_entity_euclidean_bias
+        self.use_relation_specific_curvature = use_relation_specific_curvature
+        self.radius_msg_gamma, self.use_est = radius_msg_gamma, use_est
+        self.est_state_alpha, self.use_time_aware_negative = est_state_alpha, use_time_aware_negative
+        self.temporal_index, self.true_tails_by_hr = None, None
+        if learn_curvature:
+            self.log_c = nn.Parameter(torch.tensor(math.log(c)))
+        else:
+            self.register_buffer("c", torch.tensor(c))
+        self.training_stats = {"embedding_norms": [], "gradient_norms": [], "loss_components": [],
+                               "time_gate_values": []}
+        self.dynamic_emb = nn.Parameter(torch.Tensor(num_ents, h_dim))
+        nn.init.normal_(self.dynamic_emb, std=1.0)
+        self.emb_rel = nn.Parameter(torch.Tensor(num_rels * 2, h_dim))
+        nn.init.xavier_normal_(self.emb_rel)
+        self.temporal_radius_evolution = TemporalRadiusEvolution(h_dim, c=c, epsilon=radius_epsilon,
+                                                                 anchor_beta=radius_anchor_beta)
+        self.w1 = nn.Parameter(torch.Tensor(h_dim, h_dim))
+        nn.init.xavier_normal_(self.w1)
+        self.w2 = nn.Parameter(torch.Tensor(h_dim, h_dim))
+        nn.init.xavier_normal_(self.w2)
+        self.loss_r = nn.CrossEntropyLoss()
+        self.loss_e = nn.CrossEntropyLoss()
+        if encoder_name == "hyperbolic_uvrgcn":
+            self.rgcn = HyperbolicRGCNCell(num_ents, h_dim, h_dim, num_rels * 2, num_bases, num_hidden_layers,
+                                           dropout, c=c, self_loop=self_loop, skip_connect=skip_connect,
+                                           encoder_name=encoder_name, rel_emb=self.emb_rel, use_cuda=use_cuda,
+                                           analysis=analysis, radius_msg_gamma=radius_msg_gamma)
+        else:
+            self.rgcn = LorentzRGCNCell(num_ents, h_dim, h_dim, num_rels * 2, num_bases, num_hidden_layers, dropout,
+                                        c=c, self_loop=self_loop, skip_connect=skip_connect,
+                                        encoder_name=encoder_name, rel_emb=self.emb_rel, use_cuda=use_cuda,
+                                        analysis=analysis)
+        self.time_gate_weight = nn.Parameter(torch.Tensor(h_dim, h_dim))
+        nn.init.xavier_uniform_(self.time_gate_weight, gain=nn.init.calculate_gain("relu"))
+        self.time_gate_bias = nn.Parameter(torch.zeros(h_dim))
+        self.relation_gru = nn.GRUCell(h_dim * 2, h_dim)
+        dk = dict(query_chunk_size=query_chunk_size, candidate_chunk_size=candidate_chunk_size)
+        hk = dict(init_scale=hyp_init_scale, score_scale_init=hyp_score_scale_init,
+                  score_margin_init=hyp_score_margin_init)
+        ek = dict(use_entity_euclidean_bias=use_entity_euclidean_bias,
+                  use_relation_specific_curvature=use_relation_specific_curvature)
+        if decoder_name == "hyperbolic_convtranse":
+            self.decoder_ob = HyperbolicConvTransE(num_ents, h_dim, c=c, input_dropout=input_dropout,
+                                                   hidden_dropout=hidden_dropout, feature_map_dropout=feat_dropout)
+            self.rdecoder = HyperbolicConvTransR(num_rels, h_dim, c=c, input_dropout=input_dropout,
+                                                 hidden_dropout=hidden_dropout, feature_map_dropout=feat_dropout)
+        elif decoder_name == "murp":
+            self.decoder_ob = HyperbolicMuRP(num_ents, num_rels * 2, h_dim, c=c, dropout=input_dropout, **dk, **hk,
+                                             **ek)
+            self.rdecoder = HyperbolicMuRPRel(num_rels, h_dim, c=c, dropout=input_dropout, **dk)
+        elif decoder_name == "roth":
+            self.decoder_ob = HyperbolicRotH(num_ents, num_rels * 2, h_dim, c=c, dropout=input_dropout, **dk, **hk,
+                                             **ek)
+            self.rdecoder = HyperbolicRotHRel(num_rels, h_dim, c=c, dropout=input_dropout, **dk, **hk)
+        elif decoder_name == "atth":
+            self.decoder_ob = HyperbolicAttH(num_ents, num_rels * 2, h_dim, c=c, dropout=input_dropout, **dk, **hk,
+                                             **ek)
+            self.rdecoder = HyperbolicAttHRel(num_rels, h_dim, c=c, dropout=input_dropout, **dk, **hk)
+        else:
+            raise NotImplementedError("Decoder '%s' not implemented. Choose from: hyperbolic_convtranse, murp, "
+                                      "roth, atth" % decoder_name)
+        target = torch.full((num_ents,), 0.5 * (radius_min + radius_max)) if radius_target is None else \
+            torch.as_tensor(radius_target, dtype=torch.float)
+        self.register_buffer("radius_target", target)
+        self.radius_static = nn.Parameter(self.radius_target.clone())
+
+    # ---------------------------------------------------------------------------- helpers
+    def get_curvature(self):
+        """hyperbolic_model.py:673-679."""
+        if self.learn_curvature:
+            return torch.clamp(torch.exp(self.log_c), min=self.curvature_min, max=self.curvature_max)
+        return self.c
+
+    def set_curvature_bounds(self, curvature_min=None, curvature_max=None):
+        if curvature_min is not None:
+            self.curvature_min = curvature_min
+        if curvature_max is not None:
+            self.curvature_max = curvature_max
+
+    def set_relation_curvature_bounds(self, curvature_max=None):
+        dec = getattr(self, "decoder_ob", None)
+        if dec is not None and hasattr(dec, "set_relation_curvature_bounds"):
+            dec.set_relation_curvature_bounds(curvature_max=curvature_max)
+
+    def _static_radius(self, c_val=None):
+        """hyperbolic_model.py:715-720."""
+        if c_val is None:
+            c_val = float(self.get_curvature().detach().item())
+        radius = torch.clamp(self.radius_static, min=self.radius_min, max=self.radius_max)
+        return torch.clamp(radius, max=1.0 / math.sqrt(c_val) - 1e-6)
+
+    def _guard_autograd(self):
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                "the HIP path is forward-only in this build (backward kernels are SURVEY.md §8(f) row f1); "
+                "wrap the call in torch.no_grad()")
+
+    # ---------------------------------------------------------------------------- forward
+    def forward(self, g_list, static_graph, use_cuda):
+        """hyperbolic_model.py:722-890."""
+        self._guard_autograd()
+        c = self.get_curvature()
+        c_val = float(c.item()) if isinstance(c, torch.Tensor) else float(c)
+        dev = self.dynamic_emb.device
+        V, d = self.dynamic_emb.shape
+        r_static = self._static_radius(c_val).contiguous()
+        dyn = self.dynamic_emb.detach().contiguous()
+        h = torch.empty_like(dyn)
+        x = torch.empty_like(dyn)
+        r = torch.empty(V, device=dev, dtype=torch.float32)
+        _lib.call("regcn_init_entities_f32", _lib.fptr(dyn, "dynamic_emb"), _lib.fptr(r_static), V, d, c_val,
+                  int(bool(self.layer_norm)), _lib.fptr(h), _lib.fptr(x), _lib.fptr(r), _lib.stream())
+        attach(h, x, r, c_val)
+        self.h = h
+        R2 = self.num_rels * 2
+        history_embs = []
+        trev = self.temporal_radius_evolution
+        w_r = trev.radius_mlp.weight.detach().reshape(-1).contiguous()
+        b_r = trev.radius_mlp.bias.detach().reshape(-1).contiguous()
+        wg = self.time_gate_weight.detach().contiguous()
+        bg = self.time_gate_bias.detach().contiguous()
+        for i, g in enumerate(g_list):
+            g = g.to(dev)
+            x_prev, _ = tangent_of(self.h, c_val)
+            x_input = relation_context(x_prev, g, R2)
+            x_input = torch.cat((self.emb_rel, x_input), dim=1)
+            self.h_0 = self.relation_gru(x_input, self.emb_rel if i == 0 else self.h_0)
+            self.h_0 = F.normalize(self.h_0) if self.layer_norm else self.h_0
+            current_h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0])
+            h_new = torch.empty_like(x_prev)
+            x_new = torch.empty_like(x_prev)
+            r_new = torch.empty(V, device=dev, dtype=torch.float32)
+            _lib.call("regcn_timestep_f32", _lib.fptr(current_h.contiguous(), "current_h"), _lib.fptr(x_prev),
+                      _lib.fptr(wg), _lib.fptr(bg), _lib.fptr(r_static), _lib.fptr(w_r), _lib.fptr(b_r),
+                      float(trev.epsilon), float(trev.anchor_beta), int(bool(self.layer_norm)),
+                      int(bool(self.use_residual_evolution)), V, d, c_val, float(trev.c), _lib.fptr(h_new),
+                      _lib.fptr(x_new), _lib.fptr(r_new), _lib.stream())
+            self.h = attach(h_new, x_new, r_new, c_val)
+            history_embs.append(self.h)
+        return history_embs, None, self.h_0, [], []
+
+    def _final_embedding(self, emb, c_val):
+        if self.layer_norm:
+            return HyperbolicOps.layer_norm_roundtrip(emb, c_val)  # :926-929 / :992-995
+        return emb
+
+    def predict(self, test_graph, num_rels, static_graph, test_triplets, use_cuda):
+        """hyperbolic_model.py:892-939."""
+        with torch.no_grad():
+            c = self.get_curvature()
+            c_val = float(c.item()) if isinstance(c, torch.Tensor) else float(c)
+            inverse_test_triplets = test_triplets[:, [2, 1, 0]]
+            inverse_test_triplets[:, 1] = inverse_test_triplets[:, 1] + num_rels
+            all_triples = torch.cat((test_triplets, inverse_test_triplets))
+            evolve_embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
+            embedding = self._final_embedding(evolve_embs[-1], c_val)
+            at = all_triples.to(embedding.device)
+            score = self.decoder_ob.forward(embedding, r_emb, at, mode="test")
+            score_rel = self.rdecoder.forward(embedding, r_emb, at, mode="test")
+            return all_triples, score, score_rel
+
+    def get_loss(self, glist, triples, static_graph, use_cuda, query_time=None):
+        """hyperbolic_model.py:941-1088 (forward value of the four losses)."""
+        c = self.get_curvature()
+        c_val = c.item() if isinstance(c, torch.Tensor) else c
+        self.decoder_ob.c = c_val
+        self.rdecoder.c = c_val
+        dev = self.dynamic_emb.device
+        loss_ent = torch.zeros(1, device=dev)
+        loss_rel = torch.zeros(1, device=dev)
+        loss_static = torch.zeros(1, device=dev)
+        inverse_triples = triples[:, [2, 1, 0]]
+        inverse_triples[:, 1] = inverse_triples[:, 1] + self.num_rels
+        all_triples = torch.cat([triples, inverse_triples]).to(dev)
+        evolve_embs, static_emb, r_emb, _, _ = self.forward(glist, static_graph, use_cuda)
+        pre_emb = self._final_embedding(evolve_embs[-1], c_val)
+        if self.entity_prediction:
+            if hasattr(self.decoder_ob, "loss"):
+                loss_ent = self.decoder_ob.loss(pre_emb, r_emb, all_triples)
+            else:
+                scores_ob = self.decoder_ob.forward(pre_emb, r_emb, all_triples).view(-1, self.num_ents)
+                loss_ent = self.loss_e(scores_ob, all_triples[:, 2])
+        if self.relation_prediction:
+            if hasattr(self.rdecoder, "loss"):
+                loss_rel = self.rdecoder.loss(pre_emb, r_emb, all_triples)
+            else:
+                score_rel = self.rdecoder.forward(pre_emb, r_emb, all_triples, mode="train").view(-1, 2 * self.num_rels)
+                loss_rel = self.loss_r(score_rel, all_triples[:, 1])
+        entity_ids = torch.unique(all_triples[:, [0, 2]].reshape(-1))
+        radius_static = self._static_radius(float(c_val)).index_select(0, entity_ids)
+        radius_target = self.radius_target.to(dev).index_select(0, entity_ids)
+        loss_radius = self.radius_lambda * F.mse_loss(radius_static, radius_target)
+        return loss_ent, loss_rel, loss_static, loss_radius
+
+    def get_training_summary(self):
+        return {"curvature": float(self.get_curvature())}

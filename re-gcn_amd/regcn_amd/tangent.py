@@ -1,0 +1,33 @@
+"""Tangent-space cache riding on Poincaré tensors.
+
+Every HIP kernel that produces Poincaré rows h also writes x = log0(h) and r = |h|
+(the next consumer's prologue) from registers.  They are attached to the output tensor
+object so the next layer / timestep / relation-context mean reuses them instead of
+re-reading h: the reference recomputes log0(h) at every consumer
+(hyperbolic_layers.py:268-270, hyperbolic_model.py:802, :842).  A cache entry is keyed
+by the curvature it was computed with and by the tensor's version counter, so an
+in-place edit of h invalidates it.
+"""
+import torch
+
+from . import _lib
+
+
+def attach(h, x, r, c):
+    h._regcn_xr = (x, r, float(c), h._version)
+    return h
+
+
+def tangent_of(h, c):
+    """(log0(h), max(|h|, eps)) for fp32 HIP rows h, from the cache or one prologue kernel."""
+    c = float(c)
+    cached = getattr(h, "_regcn_xr", None)
+    if cached is not None and cached[2] == c and cached[3] == h._version:
+        return cached[0], cached[1]
+    hc = h.contiguous()
+    V, d = hc.shape
+    x = torch.empty_like(hc)
+    r = torch.empty(V, device=hc.device, dtype=torch.float32)
+    _lib.call("regcn_prologue_f32", _lib.fptr(hc, "h"), V, d, c, _lib.fptr(x), _lib.fptr(r), _lib.stream())
+    attach(h, x, r, c)
+    return x, r

@@ -1,0 +1,183 @@
+"""HIP path vs the reference's golden vectors and the CPU oracle (-m gpu).
+
+Tolerance: |delta| <= 1e-4 * max(1, |ref|) elementwise; indices exact."""
+import numpy as np
+import pytest
+import torch
+
+from gpu_helpers import C, MODEL_CASES, assert_close, build_hyperbolic_model
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def t(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+@pytest.mark.parametrize("cname,c", [("c01", 0.01), ("c05", 0.05)])
+def test_row_ops_vs_golden(golden, cname, c):
+    from regcn_amd.hyperbolic_ops import HyperbolicOps as H, LorentzOps as L
+    z = golden("ops.npz")
+    x, v, y, rad = (t(z[cname + k]) for k in ("_x", "_v", "_y", "_rad"))
+    assert_close(H.project_to_ball(x, c), z[cname + "_project"], what="project")
+    assert_close(H.log_map_zero(x, c), z[cname + "_log0"], what="log0")
+    assert_close(H.exp_map_zero(v, c), z[cname + "_exp0"], what="exp0")
+    xb = H.project_to_ball(x, c)
+    assert_close(H.mobius_add(xb, y, c), z[cname + "_mobius"], what="mobius")
+    assert_close(H.hyperbolic_distance(xb, y, c), z[cname + "_dist"], what="dist")
+    assert_close(H.get_radius(x), z[cname + "_radius"], what="radius")
+    assert_close(H.apply_radius(y, rad, c), z[cname + "_apply_radius"], what="apply_radius")
+    Lz = L.to_lorentz(y, c)
+    assert_close(Lz, z[cname + "_to_lorentz"], what="to_lorentz")
+    assert_close(L.to_poincare(Lz, c), z[cname + "_to_poincare"], what="to_poincare")
+
+
+@pytest.mark.parametrize("d", [3, 64, 200, 256, 300])
+def test_row_ops_any_width_vs_oracle(d):
+    from oracle import ops as O
+    from regcn_amd.hyperbolic_ops import HyperbolicOps as H
+    g = torch.Generator().manual_seed(d)
+    x = torch.randn(37, d, generator=g) * 0.3
+    assert_close(H.log_map_zero(H.exp_map_zero(x.to(DEV), C), C), O.log0(O.exp0(x, C), C), what="roundtrip")
+    assert_close(H.layer_norm_roundtrip(x.to(DEV), C), O.exp0(torch.nn.functional.normalize(O.log0(x, C)), C))
+
+
+def _graph(z, prefix="", chunk=512):
+    from regcn_amd import graph as G
+    V, R = int(z[prefix + "meta"][0]), int(z[prefix + "meta"][1])
+    return G.build_sub_graph(V, R, z[prefix + "triples"], True, DEV, chunk_edges=chunk)
+
+
+@pytest.mark.parametrize("gamma,gname", [(0.0, "g0"), (0.15, "g15")])
+@pytest.mark.parametrize("skip", [False, True])
+@pytest.mark.parametrize("chunk", [512, 3])
+def test_union_layer_vs_golden(golden, gamma, gname, skip, chunk):
+    import torch.nn.functional as F
+    from regcn_amd.hyperbolic_layers import HyperbolicUnionRGCNLayer
+    z = golden("layer_union.npz")
+    V, R, d = (int(v) for v in z["meta"])
+    lay = HyperbolicUnionRGCNLayer(d, d, 2 * R, -1, c=C, activation=F.rrelu, self_loop=True, dropout=0.2,
+                                   skip_connect=skip, radius_msg_gamma=gamma)
+    lay.load_state_dict({k: torch.from_numpy(z["w_" + k]) for k in lay.state_dict()})
+    lay = lay.to(DEV).eval()
+    g = _graph(z, chunk=chunk)
+    with torch.no_grad():
+        y = lay(g, t(z["h"]), t(z["rel"]), prev_h=t(z["prev_h"]) if skip else None)
+    assert_close(y, z["%s_%s_out" % (gname, "skip" if skip else "noskip")], what="union layer")
+
+
+@pytest.mark.parametrize("chunk", [512, 2])
+def test_euclid_layer_vs_golden(golden, chunk):
+    import torch.nn.functional as F
+    from regcn_amd.layers import UnionRGCNLayer
+    z = golden("layer_euclid.npz")
+    V, R, d = (int(v) for v in z["meta"])
+    lay = UnionRGCNLayer(d, d, 2 * R, -1, activation=F.rrelu, self_loop=True, dropout=0.2)
+    lay.load_state_dict({k: torch.from_numpy(z["w_" + k]) for k in lay.state_dict()})
+    lay = lay.to(DEV).eval()
+    g = _graph(z, chunk=chunk)
+    g.ndata["h"] = t(z["h"])
+    with torch.no_grad():
+        y = lay(g, [], t(z["rel"]))
+    assert_close(y, z["out"], what="euclid layer")
+
+
+@pytest.mark.parametrize("tag,skip", [("s2", False), ("s2", True), ("s4", False), ("s1", False), ("s20", False)])
+@pytest.mark.parametrize("chunk", [512, 5])
+def test_lorentz_layer_vs_golden(golden, tag, skip, chunk):
+    import torch.nn.functional as F
+    from regcn_amd.hyperbolic_layers import LorentzRGCNLayer
+    z = golden("layer_lorentz.npz")
+    V, R, d, nb = (int(v) for v in z[tag + "_meta"])
+    lay = LorentzRGCNLayer(d, d, 2 * R, nb, c=C, activation=F.rrelu, self_loop=True, dropout=0.2,
+                           skip_connect=skip)
+    sd = {k: torch.from_numpy(z[tag + "_w_" + k]) for k in lay.state_dict()}
+    lay.load_state_dict(sd)
+    lay = lay.to(DEV).eval()
+    g = _graph(z, tag + "_", chunk=chunk)
+    with torch.no_grad():
+        y = lay(g, t(z[tag + "_h"]), t(z[tag + "_rel"]), prev_h=t(z[tag + "_prev_h"]) if skip else None)
+    assert_close(y, z[tag + ("_skip" if skip else "_noskip") + "_out"], what="lorentz layer")
+
+
+@pytest.mark.parametrize("tag", list(MODEL_CASES))
+def test_hyperbolic_model_predict_vs_golden(golden, tag):
+    z = golden("model_%s.npz" % tag)
+    m, glist, (V, R, d, T) = build_hyperbolic_model(z, tag, DEV)
+    with torch.no_grad():
+        embs, _, h0, _, _ = m.forward(glist, None, True)
+        all_tr, score, score_rel = m.predict(glist, R, None, torch.from_numpy(z["test"]).to(DEV), True)
+    np.testing.assert_array_equal(all_tr.cpu().numpy(), z["all_triples"])
+    assert_close(torch.stack(embs), z["embs"], what="history_embs")
+    assert_close(h0, z["h0"], what="h_0")
+    assert_close(score, z["score"], what="entity score")
+    assert_close(score_rel, z["score_rel"], what="relation score")
+
+
+@pytest.mark.parametrize("tag", ["uvrgcn_roth", "lgcn_roth", "uvrgcn_murp_nores", "uvrgcn_atth_beta",
+                                 "lgcn_roth_bias_crel"])
+def test_get_loss_vs_golden(golden, tag):
+    z = golden("model_%s.npz" % tag)
+    m, glist, (V, R, d, T) = build_hyperbolic_model(z, tag, DEV)
+    with torch.no_grad():
+        losses = m.get_loss(glist, torch.from_numpy(z["test"]).to(DEV), None, True)
+    got = np.array([float(x) for x in losses])
+    assert_close(got, z["losses"], what="losses")
+
+
+@pytest.mark.parametrize("tag", ["noln", "ln"])
+def test_euclid_model_vs_golden(golden, tag):
+    from regcn_amd import graph as G
+    from regcn_amd.rrgcn import RecurrentRGCN
+    z = golden("rrgcn_%s.npz" % tag)
+    V, R, d, T = (int(v) for v in z["meta"])
+    m = RecurrentRGCN("convtranse", "uvrgcn", V, R, 0, 0, d, "sub", T, num_bases=100, num_basis=100,
+                      num_hidden_layers=2, dropout=0.2, self_loop=True, layer_norm=(tag == "ln"),
+                      input_dropout=0.2, hidden_dropout=0.2, feat_dropout=0.2, entity_prediction=True,
+                      relation_prediction=True, use_cuda=True, gpu=0)
+    m.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("sd_")})
+    m = m.to(DEV).eval()
+    glist = [G.build_sub_graph(V, R, z["snap%d" % i], True, DEV) for i in range(T)]
+    with torch.no_grad():
+        embs, _, h0, _, _ = m.forward(glist, None, True)
+        _, score, score_rel = m.predict(glist, R, None, torch.from_numpy(z["test"]).to(DEV), True)
+    assert_close(torch.stack(embs), z["embs"], what="embs")
+    assert_close(h0, z["h0"], what="h0")
+    assert_close(score, z["score"], what="score")
+    assert_close(score_rel, z["score_rel"], what="score_rel")
+
+
+def test_score_and_ce_vs_golden(golden):
+    from regcn_amd.hyperbolic_decoder import _chunked_hyperbolic_ce_loss as ce
+    from regcn_amd.hyperbolic_decoder import _chunked_hyperbolic_dist_score as sc
+    z = golden("score.npz")
+    q, e, bias, scale, margin, cr, tgt = (t(z[k]) for k in ("q", "e", "bias", "scale", "margin", "c_r", "target"))
+    assert_close(sc(q, e, None, C, 128, 256), z["score_plain"], what="plain")
+    assert_close(sc(q, e, bias, C, 128, 256, score_scale=scale, score_margin=margin), z["score_bias"], what="bias")
+    assert_close(sc(q, e, bias, C, 128, 256, score_scale=scale, score_margin=margin, query_curvature=cr,
+                    use_hyperbolic_distance=True), z["score_crel"], what="crel")
+    assert_close(sc(q, e, None, C, 128, 256, score_scale=scale, score_margin=margin, use_hyperbolic_distance=True),
+                 z["score_dist"], what="dist")
+    assert_close(ce(q, e, tgt, C, 256, candidate_bias=bias, score_scale=scale, score_margin=margin).reshape(1),
+                 z["ce_bias"].reshape(1), what="ce")
+    assert_close(ce(q, e, tgt, C, 256, candidate_bias=bias, score_scale=scale, score_margin=margin,
+                    query_curvature=cr, use_hyperbolic_distance=True).reshape(1), z["ce_crel"].reshape(1),
+                 what="ce crel")
+
+
+@pytest.mark.parametrize("B,N,d", [(1, 1, 4), (5, 7, 12), (130, 1000, 200), (64, 64, 256)])
+def test_score_shapes_vs_oracle(B, N, d):
+    from oracle import model as OM
+    from oracle import ops as O
+    from regcn_amd.hyperbolic_decoder import _chunked_hyperbolic_dist_score as sc
+    g = torch.Generator().manual_seed(B * 1000 + N)
+    q = O.exp0(torch.randn(B, d, generator=g), C)
+    e = O.exp0(torch.randn(N, d, generator=g), C)
+    assert_close(sc(q.to(DEV), e.to(DEV), None, C, 128, 256), OM.dist_score(q, e, None, C), what="score")

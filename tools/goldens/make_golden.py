@@ -112,14 +112,14 @@ def gen_ops():
         bound = 1.0 / np.sqrt(c)
         norms = torch.tensor([0.0, 1e-9, 1e-5, 1e-3, 0.1, 1.0, 3.0, 0.5 * bound, 0.9 * bound,
                               0.99 * bound, 0.9999 * bound, bound - 1e-6, bound, bound + 1e-3,
-                              1.5 * bound, 0.2])
+                              1.5 * bound, 0.2], dtype=torch.float32)
         x = unit * norms[:, None]
         x[0] = 0.0
         v = unit * torch.tensor([0.0, 1e-8, 1e-4, 0.01, 1.0, 5.0, 10.0, 20.0, 50.0, 80.0, 100.0,
-                                 200.0, 1e3, 1e4, 3.0, 0.3])[:, None]
+                                 200.0, 1e3, 1e4, 3.0, 0.3], dtype=torch.float32)[:, None]
         y = ball_points(gen, 16, d) * (1.0 if c == 0.01 else 0.4)
         rad = torch.tensor([1e-8, 0.5, 1.0, 2.0, 3.0, 5.0, 9.0, 9.999999, 10.0, 11.0, 20.0, 0.7,
-                            1.3, 2.2, 4.4, 6.0])
+                            1.3, 2.2, 4.4, 6.0], dtype=torch.float32)
         out[cname + "_x"] = x.numpy()
         out[cname + "_v"] = v.numpy()
         out[cname + "_y"] = y.numpy()
