@@ -102,6 +102,13 @@ int regcn_lorentz_aggregate_f32(const float* x, const float* rel, const float* w
                                 float* partial, int32_t partial_stride, float* out, void* stream);
 
 /* ---- a4/a5/a6: layer tail (MFMA GEMMs + fused epilogue) ----------------------------- */
+/* Weight prepacking for the MFMA tails: a d_in x d_out row-major weight W (x @ W) becomes
+ * packed[s][jq][lane][e] = W[4s + lane/16][16(4jq + e) + lane%16] (zero-padded), i.e. the
+ * B-operand fragments of v_mfma_f32_16x16x4_f32 in k-step order.  d_out <= 256.
+ * regcn_packed_weight_floats(d_in) floats; every w_* / b-matrix argument of
+ * regcn_layer_tail_f32 and regcn_timestep_f32 is such a packed matrix. */
+size_t regcn_packed_weight_floats(int32_t d_in);
+int regcn_pack_weight_f32(const float* w, int32_t d_in, int32_t d_out, float* packed, void* stream);
 /* rows: permutation of 0..V-1 with the n_pos in-degree>0 rows first.
  * hyperbolic (euclid=0): v = clamp(agg @ w_n | agg, +-10) + x @ (w_loop | w_evolve)
  *   [skip: g = sigmoid(prev_t @ w_skip + b_skip); v = g v + (1-g) prev_t]

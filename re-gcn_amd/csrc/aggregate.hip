@@ -122,31 +122,24 @@ __global__ __launch_bounds__(256) void k_gather_fixup(const float* __restrict__ 
 // Per destination (hyperbolic_layers.py:613-625, hyperbolic_ops.py:562-581): the
 // mailbox weights are uniform, so the weighted centroid equals S / sqrt(-<S,S>_L c)
 // with S = sum_e L_e; then to_poincare -> log0 (hyperbolic_layers.py:669-671).
+// Relation block fragment of one lane: the s x s blocks covering columns [4l, 4l+4).
 template <int S>
-__device__ __forceinline__ f4 block_matvec(f4 xs, const float* __restrict__ Wt, int lane, int d,
-                                           const float* xsh) {
-  const int col = lane * 4;
-  if (col >= d) return f4{0.f, 0.f, 0.f, 0.f};
-  if (S == 1) {
-    f4 w = *reinterpret_cast<const f4*>(Wt + col);
-    return xs * w;
-  } else if (S == 2) {
-    f4 w0 = *reinterpret_cast<const f4*>(Wt + 2 * col);
-    f4 w1 = *reinterpret_cast<const f4*>(Wt + 2 * col + 4);
-    return f4{xs.x * w0.x + xs.y * w0.z, xs.x * w0.y + xs.y * w0.w, xs.z * w1.x + xs.w * w1.z,
-              xs.z * w1.y + xs.w * w1.w};
-  } else if (S == 4) {
-    const float* b = Wt + 4 * col;
-    f4 w0 = *reinterpret_cast<const f4*>(b);
-    f4 w1 = *reinterpret_cast<const f4*>(b + 4);
-    f4 w2 = *reinterpret_cast<const f4*>(b + 8);
-    f4 w3 = *reinterpret_cast<const f4*>(b + 12);
-    return xs.x * w0 + xs.y * w1 + xs.z * w2 + xs.w * w3;
-  } else {
-    // general s: x row staged in this wave's LDS slice (xsh), W read from L2
-    return f4{0.f, 0.f, 0.f, 0.f};
+struct WFrag {
+  static constexpr int NV = S == 4 ? 4 : (S == 2 ? 2 : 1);
+  f4 w[NV];
+  __device__ __forceinline__ void load(const float* __restrict__ Wt, int col) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) w[i] = *reinterpret_cast<const f4*>(Wt + S * col + 4 * i);
   }
-}
+  // m[j] = sum_i x[blk*s + i] W[blk][i][j]  (bmm(node (1 x s), weight (s x s)), :593-598)
+  __device__ __forceinline__ f4 apply(f4 xs) const {
+    if constexpr (S == 1) return xs * w[0];
+    else if constexpr (S == 2)
+      return f4{xs.x * w[0].x + xs.y * w[0].z, xs.x * w[0].y + xs.y * w[0].w, xs.z * w[1].x + xs.w * w[1].z,
+                xs.z * w[1].y + xs.w * w[1].w};
+    else return xs.x * w[0] + xs.y * w[1 % NV] + xs.z * w[2 % NV] + xs.w * w[3 % NV];
+  }
+};
 
 __device__ __forceinline__ float block_general(const float* xsh, const float* __restrict__ Wt, int s, int c) {
   const int blk = c / s, jj = c - blk * s;
@@ -157,17 +150,28 @@ __device__ __forceinline__ float block_general(const float* xsh, const float* __
   return m;
 }
 
+// Lorentz point of exp0(m), accumulated into (acc0, acc).
+__device__ __forceinline__ void lorentz_accum(f4 m, float n2, const Curv& k, float& acc0, f4& acc) {
+  float p2;
+  const float f = exp0_factor(n2, k, &p2);
+  const float den = fmaxf(1.f - k.c * p2, REGCN_EPS);
+  acc0 += (1.f + k.c * p2) / (k.sqrt_c * den);
+  acc += m * (2.f * f / den);
+}
+
+// S in {1, 2, 4}: blocks held in registers, 4 edges in flight per wave (independent
+// loads and reductions, accumulation in edge order).  S == 0: any s, x row staged in LDS.
 template <int S>
 __global__ __launch_bounds__(256) void k_lorentz_sum(
     const float* __restrict__ x, const float* __restrict__ rel, const float* __restrict__ W,
     const int* __restrict__ col_src, const int* __restrict__ col_type, const Chunk* __restrict__ chunks,
     int n_chunks, int nb, int s_gen, Curv k, int d, float* __restrict__ partial, int pstride,
     float* __restrict__ out) {
-  __shared__ float xsh_all[4][256];
+  __shared__ float xsh_all[S == 0 ? 4 : 1][S == 0 ? 256 : 1];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  float* xsh = xsh_all[wv];
   const int col = lane * 4;
+  const bool active = col < d;
   const int wstride = nb * (d / nb) * (d / nb);
   const int nw = gridDim.x * (blockDim.x >> 6);
   for (int ci = blockIdx.x * (blockDim.x >> 6) + wv; ci < n_chunks; ci += nw) {
@@ -181,20 +185,49 @@ __global__ __launch_bounds__(256) void k_lorentz_sum(
         my_s = col_src[e0 + lane];
         my_t = col_type[e0 + lane];
       }
-      for (int j = 0; j < n; ++j) {
+      int j = 0;
+      if constexpr (S > 0) {
+        for (; j + 4 <= n; j += 4) {
+          f4 xs[4], rr[4], m[4];
+          WFrag<S> wf[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int src = rl(my_s, j + u), typ = rl(my_t, j + u);
+            xs[u] = load4(x + (int64_t)src * d, col, d);
+            rr[u] = load4(rel + (int64_t)typ * d, col, d);
+            if (active) wf[u].load(W + (int64_t)typ * wstride, col);
+          }
+          float n2[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            m[u] = active ? wf[u].apply(xs[u]) + rr[u] : f4{0.f, 0.f, 0.f, 0.f};
+            n2[u] = row16_sum(dot4(m[u], m[u]));
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float t = (rlane(n2[u], 0) + rlane(n2[u], 16)) + (rlane(n2[u], 32) + rlane(n2[u], 48));
+            lorentz_accum(m[u], t, k, acc0, acc);
+          }
+        }
+      }
+      for (; j < n; ++j) {
         const int src = rl(my_s, j), typ = rl(my_t, j);
         const float* Wt = W + (int64_t)typ * wstride;
         f4 xs = load4(x + (int64_t)src * d, col, d);
-        f4 m;
-        if (S > 0) {
-          m = block_matvec<S>(xs, Wt, lane, d, nullptr);
+        f4 m = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (S > 0) {
+          if (active) {
+            WFrag<S> wf;
+            wf.load(Wt, col);
+            m = wf.apply(xs);
+          }
         } else {
-          if (col < d) *reinterpret_cast<f4*>(xsh + col) = xs;
+          float* xsh = xsh_all[S == 0 ? wv : 0];
+          if (active) *reinterpret_cast<f4*>(xsh + col) = xs;
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          m = f4{0.f, 0.f, 0.f, 0.f};
-          if (col < d) {
+          if (active) {
             m.x = block_general(xsh, Wt, s_gen, col);
             m.y = block_general(xsh, Wt, s_gen, col + 1);
             m.z = block_general(xsh, Wt, s_gen, col + 2);
@@ -204,11 +237,7 @@ __global__ __launch_bounds__(256) void k_lorentz_sum(
           __builtin_amdgcn_wave_barrier();
         }
         m += load4(rel + (int64_t)typ * d, col, d);
-        float p2;
-        const float f = exp0_factor(wave_sum(dot4(m, m)), k, &p2);
-        const float den = fmaxf(1.f - k.c * p2, REGCN_EPS);
-        acc0 += (1.f + k.c * p2) / (k.sqrt_c * den);
-        acc += m * (2.f * f / den);
+        lorentz_accum(m, wave_sum(dot4(m, m)), k, acc0, acc);
       }
     }
     if (ch.slot < 0) {

@@ -100,6 +100,12 @@ int regcn_lorentz_aggregate_f32(const float* x, const float* rel, const float* w
                      partial_stride, out, ST(s));
 }
 
+size_t regcn_packed_weight_floats(int32_t d_in) { return packed_weight_floats(d_in); }
+
+int regcn_pack_weight_f32(const float* w, int32_t d_in, int32_t d_out, float* packed, void* s) {
+  return pack_weight(w, d_in, d_out, packed, ST(s));
+}
+
 int regcn_layer_tail_f32(const float* agg, const float* w_n, const float* x, const float* w_loop,
                          const float* w_evolve, const float* prev_t, const float* w_skip, const float* b_skip,
                          const float* drop_mask, const int32_t* rows, int32_t n_pos, int32_t V, int32_t d,

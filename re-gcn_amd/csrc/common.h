@@ -25,10 +25,24 @@ struct Curv {
   float atanh_mx; // log0 clamp: 1 - 1e-6 (hyperbolic_ops.py:115)
 };
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+// Sum over each DPP row of 16 lanes, result in every lane of the row: two quad_perm
+// swaps and two row rotations (VALU DPP; no LDS crossbar like ds_bpermute/__shfl).
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false)); // row_ror:4
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false)); // row_ror:8
   return v;
+}
+
+__device__ __forceinline__ float rlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// Full 64-lane sum, broadcast (wave-uniform) to every lane.
+__device__ __forceinline__ float wave_sum(float v) {
+  v = row16_sum(v);
+  return (rlane(v, 0) + rlane(v, 16)) + (rlane(v, 32) + rlane(v, 48));
 }
 
 __device__ __forceinline__ float wave_max(float v) {
@@ -39,13 +53,7 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // Reduction over the 16 lanes that share (lane >> 4): the row group of an
 // MFMA 16x16 C/D fragment (col = lane & 15).
-__device__ __forceinline__ float group16_sum(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 8);
-  return v;
-}
+__device__ __forceinline__ float group16_sum(float v) { return row16_sum(v); }
 
 __device__ __forceinline__ float dot4(f4 a, f4 b) {
   return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;

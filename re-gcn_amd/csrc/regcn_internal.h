@@ -89,6 +89,8 @@ struct ScoreArgs {
   float* tgt_logit;      // [B] (CE mode)
 };
 
+size_t packed_weight_floats(int d_in);
+int pack_weight(const float* W, int d_in, int d_out, float* Wp, hipStream_t st);
 int layer_tail(const LayerArgs& a, hipStream_t st);
 int timestep(const StepArgs& a, hipStream_t st);
 int score(ScoreArgs& a, int mode, float* loss, hipStream_t st);

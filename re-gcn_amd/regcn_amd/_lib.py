@@ -40,6 +40,8 @@ _SIGS = {
     "regcn_euclid_aggregate_f32": [P, P, P, P, P, P, _c_int, P, _c_int, _c_int, P, _c_int, P, P],
     "regcn_segment_mean_f32": [P, P, P, P, _c_int, P, _c_int, _c_int, P, _c_int, P, P],
     "regcn_lorentz_aggregate_f32": [P, P, P, P, P, P, _c_int, P, _c_int, _c_int, _c_f, _c_int, P, _c_int, P, P],
+    "regcn_packed_weight_floats": [_c_int],
+    "regcn_pack_weight_f32": [P, _c_int, _c_int, P, P],
     "regcn_layer_tail_f32": [P, P, P, P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_int, _c_f, P, P, P, P],
     "regcn_timestep_f32": [P, P, P, P, P, P, P, _c_f, _c_f, _c_int, _c_int, _c_int, _c_int, _c_f, _c_f, P, P, P, P],
     "regcn_hyp_score_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P],
@@ -47,7 +49,8 @@ _SIGS = {
     "regcn_hyp_ce_f32": [P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P, P],
     "regcn_rank_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
 }
-_RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz}
+_RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz,
+            "regcn_packed_weight_floats": _c_sz}
 
 _lib = None
 

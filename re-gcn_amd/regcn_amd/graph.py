@@ -24,7 +24,14 @@ Built once per snapshot on the host and cached across epochs (SURVEY.md §8(f) f
 import numpy as np
 import torch
 
-DEFAULT_CHUNK_EDGES = 512
+DEFAULT_CHUNK_EDGES = None  # adaptive, see chunk_size_for()
+
+
+def chunk_size_for(num_edges):
+    """Edges per work chunk: small snapshots (ICEWS/GDELT: 0.5-3k edges, Zipf in-degrees
+    with hubs of hundreds of edges) are latency-bound, so chunks are cut short (16) to
+    spread a hub over many waves; large snapshots get up to 1024 edges per wave."""
+    return int(min(1024, max(16, num_edges // 4096)))
 
 
 def r2e(triplets, num_rels):
@@ -107,7 +114,7 @@ class SnapshotGraph:
         order = np.argsort(dst, kind="stable")
         rowptr = np.zeros(V + 1, dtype=np.int64)
         np.cumsum(in_deg, out=rowptr[1:])
-        self.chunk_edges = int(chunk_edges)
+        self.chunk_edges = int(chunk_edges) if chunk_edges else chunk_size_for(E)
         chunks, fixups, nslot = _chunk_rows(rowptr, np.arange(V), self.chunk_edges)
         pos = np.nonzero(in_deg > 0)[0]
         zero = np.nonzero(in_deg == 0)[0]

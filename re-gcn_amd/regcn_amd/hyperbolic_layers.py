@@ -14,6 +14,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from .tangent import attach, tangent_of
+from .weights import packed
 
 EPS = 1e-6
 
@@ -26,13 +27,15 @@ def _drop_mask(layer, like):
 
 
 def layer_tail(agg, w_n, x, w_loop, w_evolve, prev_t, w_skip, b_skip, drop_mask, g, c, euclid):
-    """regcn_layer_tail_f32 wrapper; returns (h, x_next, r_next)."""
+    """regcn_layer_tail_f32 wrapper (weights as (d, d) tensors, packed on first use);
+    returns (h, x_next, r_next)."""
     wk = g.work()
     V, d = x.shape
     h = torch.empty_like(x)
     xn = torch.empty_like(x)
     rn = torch.empty(V, device=x.device, dtype=torch.float32)
     f = _lib.fptr
+    w_n, w_loop, w_evolve, w_skip = packed(w_n), packed(w_loop), packed(w_evolve), packed(w_skip)
     _lib.call("regcn_layer_tail_f32", f(agg), f(w_n), f(x, "x"), f(w_loop), f(w_evolve), f(prev_t), f(w_skip),
               f(b_skip), f(drop_mask), _lib.iptr(wk["rows"]), g.n_pos, V, d, int(euclid), float(c), f(h), f(xn),
               f(rn), _lib.stream())

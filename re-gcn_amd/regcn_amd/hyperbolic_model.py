@@ -27,6 +27,7 @@ from .hyperbolic_decoder import (HyperbolicAttH, HyperbolicAttHRel, HyperbolicCo
 from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell
 from .hyperbolic_ops import HyperbolicOps, TemporalRadiusEvolution
 from .tangent import attach, tangent_of
+from .weights import packed
 
 logger = logging.getLogger("hyperbolic_model")
 GEOOPT_AVAILABLE = False
@@ -198,10 +199,23 @@ class HyperbolicRecurrentRGCN(nn.Module):
         if dec is not None and hasattr(dec, "set_relation_curvature_bounds"):
             dec.set_relation_curvature_bounds(curvature_max=curvature_max)
 
+    def _c_float(self):
+        """The curvature as a python float.  A fixed curvature is a buffer that only
+        changes through load_state_dict/in-place edits, so its value is cached against
+        the buffer's version counter: no device->host sync per forward, which keeps the
+        forward capturable into a HIP graph.  A learned curvature is read each call, as
+        the reference does (hyperbolic_model.py:755)."""
+        if self.learn_curvature:
+            return float(self.get_curvature().detach().item())
+        key = (self.c.data_ptr(), self.c._version)
+        if getattr(self, "_c_cache", (None, None))[0] != key:
+            self._c_cache = (key, float(self.c.item()))
+        return self._c_cache[1]
+
     def _static_radius(self, c_val=None):
         """hyperbolic_model.py:715-720."""
         if c_val is None:
-            c_val = float(self.get_curvature().detach().item())
+            c_val = self._c_float()
         radius = torch.clamp(self.radius_static, min=self.radius_min, max=self.radius_max)
         return torch.clamp(radius, max=1.0 / math.sqrt(c_val) - 1e-6)
 
@@ -215,8 +229,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
     def forward(self, g_list, static_graph, use_cuda):
         """hyperbolic_model.py:722-890."""
         self._guard_autograd()
-        c = self.get_curvature()
-        c_val = float(c.item()) if isinstance(c, torch.Tensor) else float(c)
+        c_val = self._c_float()
         dev = self.dynamic_emb.device
         V, d = self.dynamic_emb.shape
         r_static = self._static_radius(c_val).contiguous()
@@ -233,7 +246,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
         trev = self.temporal_radius_evolution
         w_r = trev.radius_mlp.weight.detach().reshape(-1).contiguous()
         b_r = trev.radius_mlp.bias.detach().reshape(-1).contiguous()
-        wg = self.time_gate_weight.detach().contiguous()
+        wg = packed(self.time_gate_weight)
         bg = self.time_gate_bias.detach().contiguous()
         for i, g in enumerate(g_list):
             g = g.to(dev)
@@ -263,9 +276,9 @@ class HyperbolicRecurrentRGCN(nn.Module):
     def predict(self, test_graph, num_rels, static_graph, test_triplets, use_cuda):
         """hyperbolic_model.py:892-939."""
         with torch.no_grad():
-            c = self.get_curvature()
-            c_val = float(c.item()) if isinstance(c, torch.Tensor) else float(c)
-            inverse_test_triplets = test_triplets[:, [2, 1, 0]]
+            c_val = self._c_float()
+            # [o, r, s] (hyperbolic_model.py:917); flip() keeps the index on the device
+            inverse_test_triplets = test_triplets.flip(1)
             inverse_test_triplets[:, 1] = inverse_test_triplets[:, 1] + num_rels
             all_triples = torch.cat((test_triplets, inverse_test_triplets))
             evolve_embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
@@ -277,15 +290,14 @@ class HyperbolicRecurrentRGCN(nn.Module):
 
     def get_loss(self, glist, triples, static_graph, use_cuda, query_time=None):
         """hyperbolic_model.py:941-1088 (forward value of the four losses)."""
-        c = self.get_curvature()
-        c_val = c.item() if isinstance(c, torch.Tensor) else c
+        c_val = self._c_float()
         self.decoder_ob.c = c_val
         self.rdecoder.c = c_val
         dev = self.dynamic_emb.device
         loss_ent = torch.zeros(1, device=dev)
         loss_rel = torch.zeros(1, device=dev)
         loss_static = torch.zeros(1, device=dev)
-        inverse_triples = triples[:, [2, 1, 0]]
+        inverse_triples = triples.flip(1)
         inverse_triples[:, 1] = inverse_triples[:, 1] + self.num_rels
         all_triples = torch.cat([triples, inverse_triples]).to(dev)
         evolve_embs, static_emb, r_emb, _, _ = self.forward(glist, static_graph, use_cuda)

@@ -174,7 +174,7 @@ class RecurrentRGCN(nn.Module):
     def predict(self, test_graph, num_rels, static_graph, test_triplets, use_cuda):
         """src/rrgcn.py:183-194."""
         with torch.no_grad():
-            inv = test_triplets[:, [2, 1, 0]]
+            inv = test_triplets.flip(1)
             inv[:, 1] = inv[:, 1] + num_rels
             all_triples = torch.cat((test_triplets, inv))
             evolve_embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)

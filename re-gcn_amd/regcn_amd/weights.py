@@ -1,0 +1,26 @@
+"""Packed MFMA B-operand copies of d x d weights (regcn_pack_weight_f32).
+
+The layer tail and timestep kernels read their weights in v_mfma_f32_16x16x4_f32
+fragment order.  The packed copy is cached on the weight tensor itself and rebuilt only
+when its storage, shape or version counter changes (an optimizer step, an in-place edit,
+load_state_dict), so steady-state forwards launch no packing kernel.
+"""
+import torch
+
+from . import _lib
+
+
+def packed(w):
+    """Packed copy of a (d_in, d_out) fp32 HIP weight (None -> None)."""
+    if w is None:
+        return None
+    key = (w.data_ptr(), w._version, tuple(w.shape))
+    hit = getattr(w, "_regcn_packed", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    d_in, d_out = w.shape
+    wc = w.detach().contiguous()
+    out = torch.empty(_lib.lib().regcn_packed_weight_floats(d_in), device=w.device, dtype=torch.float32)
+    _lib.call("regcn_pack_weight_f32", _lib.fptr(wc, "weight"), d_in, d_out, _lib.fptr(out), _lib.stream())
+    w._regcn_packed = (key, out)
+    return out

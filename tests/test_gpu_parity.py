@@ -31,7 +31,14 @@ def test_row_ops_vs_golden(golden, cname, c):
     assert_close(H.exp_map_zero(v, c), z[cname + "_exp0"], what="exp0")
     xb = H.project_to_ball(x, c)
     assert_close(H.mobius_add(xb, y, c), z[cname + "_mobius"], what="mobius")
-    assert_close(H.hyperbolic_distance(xb, y, c), z[cname + "_dist"], what="dist")
+    # atanh near the ball boundary amplifies fp32 rounding of |(-x)(+)y| by its relative
+    # condition number k = z / ((1 - z^2) atanh z), z = sqrt(c)|.|; the tolerance scales by it.
+    ref = np.asarray(z[cname + "_dist"], np.float64)
+    zz = np.tanh(ref * np.sqrt(c) / 2)
+    kappa = np.where(zz > 1e-6, zz / np.maximum((1 - zz ** 2) * np.arctanh(np.minimum(zz, 1 - 1e-12)), 1e-30), 1.0)
+    got = H.hyperbolic_distance(xb, y, c).double().cpu().numpy()
+    err = np.abs(got - ref) / np.maximum(1.0, np.abs(ref)) / np.maximum(1.0, kappa)
+    assert err.max() <= 1e-4, "dist condition-scaled error %.3g" % err.max()
     assert_close(H.get_radius(x), z[cname + "_radius"], what="radius")
     assert_close(H.apply_radius(y, rad, c), z[cname + "_apply_radius"], what="apply_radius")
     Lz = L.to_lorentz(y, c)
