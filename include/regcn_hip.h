@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 1
+#define REGCN_ABI_VERSION 2
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -122,6 +122,80 @@ int regcn_layer_tail_f32(const float* agg, const float* w_n, const float* x, con
                          const float* drop_mask, const int32_t* rows, int32_t n_pos, int32_t V, int32_t d,
                          int32_t euclid, float c, float* h_out, float* x_next, float* r_next, void* stream);
 
+/* ---- a2-a8 fused: one whole layer per launch (gather + GEMMs + epilogue [+ timestep]) -- */
+#define REGCN_AGG_UNION 0   /* HyperbolicUnionRGCNLayer, hyperbolic_layers.py:164-323 */
+#define REGCN_AGG_EUCLID 2  /* UnionRGCNLayer, rgcn/layers.py:189-279 */
+#define REGCN_AGG_LORENTZ 3 /* LorentzRGCNLayer, hyperbolic_layers.py:524-694 */
+#define REGCN_AGG_NONE 4    /* aggregation supplied in `agg` (regcn_layer_tail_f32) */
+
+/* Destination tiles (graph.py): `tiles` int32[n_pos_tiles][2] = {start, count} over
+ * rows[0, n_pos), each count <= 16; `rowptr` int32[V+1] is the destination-sorted CSR
+ * whose col_src/col_type the gather reads.  Rows with in-degree > `budget` are not
+ * gathered inline: their finished aggregation must already be in `agg` (chunked
+ * regcn_*_aggregate_f32 over those rows only).  All w_* matrices are packed
+ * (regcn_pack_weight_f32).  With fuse_step != 0 the layer output is not stored: the
+ * timestep (regcn_timestep_f32 semantics; step_* fields) runs on it in registers. */
+typedef struct regcn_layer_desc {
+  int32_t agg_mode;
+  const float* x;        /* V x d layer input: log0(h) (hyperbolic) or h (euclid) */
+  const float* radius;   /* V, |h| (union message weights) */
+  const float* rel;      /* R2 x d relation rows */
+  const float* w_rel;    /* R2 x nb*s*s Lorentz block weights */
+  int32_t num_bases;
+  float gamma;           /* radius_msg_gamma */
+  const int32_t* rowptr;
+  const int32_t* col_src;
+  const int32_t* col_type;
+  const float* norm;     /* V: 1 / in-degree (0 -> 1) */
+  int32_t budget;
+  const int32_t* tiles;
+  int32_t n_pos_tiles;
+  const float* agg;
+  const float* w_n;
+  const float* w_loop;
+  const float* w_evolve;
+  const float* prev_t;
+  const float* w_skip;
+  const float* b_skip;
+  const float* drop_mask;
+  const int32_t* rows;
+  int32_t n_pos, V, d, euclid;
+  float c;
+  float* h_out;
+  float* x_next;
+  float* r_next;
+  int32_t fuse_step;
+  const float* step_x_prev;   /* log0(h_prev) */
+  const float* step_w_g;
+  const float* step_b_g;
+  const float* step_r_static;
+  const float* step_w_r;
+  const float* step_b_r;
+  float step_eps_r, step_beta;
+  int32_t step_layer_norm, step_residual;
+  float step_c_radius;
+  float* step_h_out;
+  float* step_x_out;
+  float* step_r_out;
+} regcn_layer_desc;
+int regcn_layer_f32(const regcn_layer_desc* desc, void* stream);
+
+/* ---- a7: relation evolution (segment mean + GRUCell in one launch) ------------------- */
+/* nn.Linear-layout packing for the relation GRU: W is (n_gates * n_out) x n_in row-major
+ * (GRUCell weight_ih: 3d x 2d, weight_hh: 3d x d); packed[g][s][jt][lane] =
+ * W[g*n_out + 16 jt + lane%16][4 s + lane/16], zero padded. */
+size_t regcn_packed_linear_floats(int32_t n_gates, int32_t n_out, int32_t n_in);
+int regcn_pack_linear_f32(const float* w, int32_t n_gates, int32_t n_out, int32_t n_in, float* packed,
+                          void* stream);
+/* hyperbolic_model.py:797-818 (rrgcn.py:161-174): x_mean[r] = mean of x[rel_idx[rel_start[r] ..
+ * + rel_count[r]]] (0 for absent relations; or x_mean given precomputed, rel_* unused), then
+ * h_out = GRUCell([emb_rel | x_mean], h_prev) with packed w_ih / w_hh and biases b_ih / b_hh
+ * (3d each, gate order r, z, n). */
+int regcn_relation_gru_f32(const float* x, const int32_t* rel_idx, const int32_t* rel_start, const float* rel_count,
+                           const float* x_mean, const float* emb_rel, const float* h_prev, const float* w_ih,
+                           const float* w_hh, const float* b_ih, const float* b_hh, int32_t R2, int32_t d,
+                           float* h_out, void* stream);
+
 /* ---- a8: per-timestep entity evolution (MFMA time gate + fused row epilogue) --------- */
 /* hyperbolic_model.py:829-869 + TemporalRadiusEvolution.forward (hyperbolic_ops.py:395-435):
  * hc = cell output, x_prev = log0(h_prev), r_static = clamped static radius (:715-720),
@@ -132,19 +206,40 @@ int regcn_timestep_f32(const float* hc, const float* x_prev, const float* w_g, c
                        int32_t layer_norm, int32_t residual, int32_t V, int32_t d, float c, float c_radius,
                        float* h_out, float* x_out, float* r_out, void* stream);
 
+/* ---- a9/a10: decoder queries (one launch each) -------------------------------------- */
+/* Queries b < n_test use trip[b] = (s, r, o) (int64, n_test x 3); b >= n_test the inverse
+ * (o, r + num_rels, s) of trip[b - n_test] (hyperbolic_model.py:915-919).  B <= 2 n_test.
+ * All w_* are nn.Linear weights packed transposed: regcn_pack_weight_f32 of W^T (in x out).
+ * RotH (HyperbolicRotH._query, hyperbolic_decoder.py:1065-1085): w1/b1, w2/b2 reshape_fc1/2,
+ * w_rot/b_rot rot_proj (d -> d/2), w_trans/b_trans trans_proj; rel = relation embedding. */
+int regcn_roth_query_f32(const float* ent, const float* rel, const int64_t* trip, int32_t n_test, int32_t B,
+                         int32_t num_rels, const float* w1, const float* b1, const float* w2, const float* b2,
+                         const float* w_rot, const float* b_rot, const float* w_trans, const float* b_trans, int32_t d,
+                         float c, float* q_out, void* stream);
+/* RotHRel (HyperbolicRotHRel._query + candidates, hyperbolic_decoder.py:1223-1243):
+ * q = mobius_add(-exp0(givens(s_tan, global_rot)), E[o]); also cand_out = exp0(rel) for the
+ * n_cand relation rows (the relation scorer's candidates). */
+int regcn_roth_rel_query_f32(const float* ent, const int64_t* trip, int32_t n_test, int32_t B, int32_t num_rels,
+                             const float* w1, const float* b1, const float* w2, const float* b2,
+                             const float* global_rot, const float* rel, int32_t n_cand, int32_t d, float c,
+                             float* q_out, float* cand_out, void* stream);
+
 /* ---- a11/a12/f2: all-entity hyperbolic scoring ------------------------------------- */
+#define REGCN_SCORE_DIST 1       /* flags: true hyperbolic distance (fp64 MFMA) */
+#define REGCN_SCORE_RAW_SCALE 2  /* flags: `scale` is score_scale_raw; softplus(raw) + 1e-6 in-kernel */
 /* _chunked_hyperbolic_dist_score, hyperbolic_decoder.py:89-179.  scale/margin: device
- * scalars or NULL (1, 0).  bias [N] or NULL.  use_dist=1 selects the true hyperbolic
- * distance (computed with fp64 MFMA: the arctanh distance is linear in |(-q)(+)e| and an
- * fp32 expansion would lose ~3 digits on near-duplicate pairs); c_rel [B] (or NULL) the
- * per-query curvature of --plus-relation-specific-curvature.  out: [B][N] fp32. */
+ * scalars or NULL (1, 0).  bias [N] or NULL.  flags: REGCN_SCORE_DIST selects the true
+ * hyperbolic distance (computed with fp64 MFMA: the arctanh distance is linear in
+ * |(-q)(+)e| and an fp32 expansion would lose ~3 digits on near-duplicate pairs);
+ * REGCN_SCORE_RAW_SCALE applies softplus + 1e-6 to *scale on the device (:717).  c_rel [B]
+ * (or NULL) the per-query curvature of --plus-relation-specific-curvature.  out: [B][N]. */
 int regcn_hyp_score_f32(const float* q, const float* cand, const float* bias, const float* c_rel, const float* scale, const float* margin, int32_t B,
-                        int32_t N, int32_t d, float c, int32_t use_dist, float* out, void* stream);
+                        int32_t N, int32_t d, float c, int32_t flags, float* out, void* stream);
 /* _chunked_hyperbolic_ce_loss, hyperbolic_decoder.py:182-307: per-query lse - target logit
  * (the caller takes the mean).  workspace: regcn_hyp_ce_workspace_bytes(B, N) bytes. */
 size_t regcn_hyp_ce_workspace_bytes(int32_t B, int32_t N);
 int regcn_hyp_ce_f32(const float* q, const float* cand, const float* bias, const float* c_rel, const float* scale, const float* margin,
-                     const int32_t* target, int32_t B, int32_t N, int32_t d, float c, int32_t use_dist,
+                     const int32_t* target, int32_t B, int32_t N, int32_t d, float c, int32_t flags,
                      void* workspace, float* loss_per_query, void* stream);
 /* get_total_rank / sort_and_rank / filter_score, rgcn/utils.py:21-166: 1 + count of
  * candidates scoring strictly above the target, raw and excluding the CSR list of other

@@ -18,24 +18,10 @@
 // (src row + col_src + col_type + radius_src per edge; output row + row
 // metadata per node); relation rows and Lorentz blocks are L2-resident.
 #include "common.h"
+#include "gather.h"
 #include "regcn_internal.h"
 
 namespace regcn {
-
-struct Chunk {
-  int row, beg, end, slot;
-};
-
-struct Fixup {
-  int row, sbeg, send, pad;
-};
-
-enum AggMode : int { AGG_UNION = 0, AGG_MEAN = 1, AGG_EUCLID = 2 };
-
-__device__ __forceinline__ int rl(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
-__device__ __forceinline__ float rlf(float v, int j) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
-}
 
 // ------------------------------------------------------------------------ Union / mean
 // UNION : acc = sum_e w_e (x[src_e] + rel[type_e]),  w_e = exp(-gamma |r_src - r_dst|)
@@ -116,49 +102,7 @@ __global__ __launch_bounds__(256) void k_gather_fixup(const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------ Lorentz
-// Per edge (hyperbolic_layers.py:589-611):
-//   m = blockdiag_k(W[type]_k (s x s)) . x_src + rel[type];  p = exp0(m);
-//   L = (x0 = (1 + c|p|^2) / (sqrt_c den), xi = 2 p / den),  den = max(1 - c|p|^2, eps)
-// Per destination (hyperbolic_layers.py:613-625, hyperbolic_ops.py:562-581): the
-// mailbox weights are uniform, so the weighted centroid equals S / sqrt(-<S,S>_L c)
-// with S = sum_e L_e; then to_poincare -> log0 (hyperbolic_layers.py:669-671).
-// Relation block fragment of one lane: the s x s blocks covering columns [4l, 4l+4).
-template <int S>
-struct WFrag {
-  static constexpr int NV = S == 4 ? 4 : (S == 2 ? 2 : 1);
-  f4 w[NV];
-  __device__ __forceinline__ void load(const float* __restrict__ Wt, int col) {
-#pragma unroll
-    for (int i = 0; i < NV; ++i) w[i] = *reinterpret_cast<const f4*>(Wt + S * col + 4 * i);
-  }
-  // m[j] = sum_i x[blk*s + i] W[blk][i][j]  (bmm(node (1 x s), weight (s x s)), :593-598)
-  __device__ __forceinline__ f4 apply(f4 xs) const {
-    if constexpr (S == 1) return xs * w[0];
-    else if constexpr (S == 2)
-      return f4{xs.x * w[0].x + xs.y * w[0].z, xs.x * w[0].y + xs.y * w[0].w, xs.z * w[1].x + xs.w * w[1].z,
-                xs.z * w[1].y + xs.w * w[1].w};
-    else return xs.x * w[0] + xs.y * w[1 % NV] + xs.z * w[2 % NV] + xs.w * w[3 % NV];
-  }
-};
-
-__device__ __forceinline__ float block_general(const float* xsh, const float* __restrict__ Wt, int s, int c) {
-  const int blk = c / s, jj = c - blk * s;
-  const float* w = Wt + (int64_t)blk * s * s + jj;
-  const float* xb = xsh + blk * s;
-  float m = 0.f;
-  for (int i = 0; i < s; ++i) m += xb[i] * w[i * s];
-  return m;
-}
-
-// Lorentz point of exp0(m), accumulated into (acc0, acc).
-__device__ __forceinline__ void lorentz_accum(f4 m, float n2, const Curv& k, float& acc0, f4& acc) {
-  float p2;
-  const float f = exp0_factor(n2, k, &p2);
-  const float den = fmaxf(1.f - k.c * p2, REGCN_EPS);
-  acc0 += (1.f + k.c * p2) / (k.sqrt_c * den);
-  acc += m * (2.f * f / den);
-}
-
+// Messages and centroid: gather.h (hyperbolic_layers.py:589-625).
 // S in {1, 2, 4}: blocks held in registers, 4 edges in flight per wave (independent
 // loads and reductions, accumulation in edge order).  S == 0: any s, x row staged in LDS.
 template <int S>
@@ -222,30 +166,14 @@ __global__ __launch_bounds__(256) void k_lorentz_sum(
             m = wf.apply(xs);
           }
         } else {
-          float* xsh = xsh_all[S == 0 ? wv : 0];
-          if (active) *reinterpret_cast<f4*>(xsh + col) = xs;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          if (active) {
-            m.x = block_general(xsh, Wt, s_gen, col);
-            m.y = block_general(xsh, Wt, s_gen, col + 1);
-            m.z = block_general(xsh, Wt, s_gen, col + 2);
-            m.w = block_general(xsh, Wt, s_gen, col + 3);
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
+          m = block_general4(xsh_all[S == 0 ? wv : 0], xs, Wt, s_gen, col, active);
         }
         m += load4(rel + (int64_t)typ * d, col, d);
         lorentz_accum(m, wave_sum(dot4(m, m)), k, acc0, acc);
       }
     }
     if (ch.slot < 0) {
-      const float ip = -acc0 * acc0 + wave_sum(dot4(acc, acc));
-      const float sc = sqrtf(fmaxf(-ip * k.c, REGCN_EPS));
-      const float c0 = acc0 / sc;
-      f4 y = (acc / sc) / fmaxf(1.f + c0 * k.sqrt_c, REGCN_EPS);
-      store4(out + (int64_t)ch.row * d, col, d, row_log0(y, k));
+      store4(out + (int64_t)ch.row * d, col, d, lorentz_finish(acc0, acc, k));
     } else {
       float* p = partial + (int64_t)ch.slot * pstride;
       store4(p, col, d, acc);
@@ -269,11 +197,7 @@ __global__ __launch_bounds__(256) void k_lorentz_fixup(const float* __restrict__
       acc += load4(p, col, d);
       acc0 += p[d];
     }
-    const float ip = -acc0 * acc0 + wave_sum(dot4(acc, acc));
-    const float sc = sqrtf(fmaxf(-ip * k.c, REGCN_EPS));
-    const float c0 = acc0 / sc;
-    f4 y = (acc / sc) / fmaxf(1.f + c0 * k.sqrt_c, REGCN_EPS);
-    store4(out + (int64_t)f.row * d, col, d, row_log0(y, k));
+    store4(out + (int64_t)f.row * d, col, d, lorentz_finish(acc0, acc, k));
   }
 }
 

@@ -110,9 +110,101 @@ int regcn_layer_tail_f32(const float* agg, const float* w_n, const float* x, con
                          const float* w_evolve, const float* prev_t, const float* w_skip, const float* b_skip,
                          const float* drop_mask, const int32_t* rows, int32_t n_pos, int32_t V, int32_t d,
                          int32_t euclid, float c, float* h_out, float* x_next, float* r_next, void* s) {
-  LayerArgs a{agg, w_n, x, w_loop, w_evolve, prev_t, w_skip, b_skip, drop_mask, rows, n_pos, V, d, euclid,
-              make_curv(c), h_out, x_next, r_next};
-  return layer_tail(a, ST(s));
+  LayerArgs a{};
+  a.agg_mode = 4;  // AGG_NONE
+  a.agg = agg;
+  a.w_n = w_n;
+  a.x = x;
+  a.w_loop = w_loop;
+  a.w_evolve = w_evolve;
+  a.prev_t = prev_t;
+  a.w_skip = w_skip;
+  a.b_skip = b_skip;
+  a.drop_mask = drop_mask;
+  a.rows = rows;
+  a.n_pos = agg ? n_pos : 0;  // no neighbour term: every row takes the pos/zero weight split below
+  a.V = V;
+  a.d = d;
+  a.euclid = euclid;
+  a.k = make_curv(c);
+  a.h_out = h_out;
+  a.x_next = x_next;
+  a.r_next = r_next;
+  if (!agg && n_pos > 0) {
+    // no neighbour term, but rows still choose W_loop (in-degree > 0) or W_evolve: two
+    // launches over the two row ranges, each as "zero in-degree" tiles
+    LayerArgs z = a;
+    z.n_pos = 0;
+    z.rows = rows;
+    z.V = n_pos;
+    z.w_evolve = w_loop;
+    int rc = layer(z, ST(s));
+    if (rc) return rc;
+    z.rows = rows + n_pos;
+    z.V = V - n_pos;
+    z.w_evolve = w_evolve;
+    return layer(z, ST(s));
+  }
+  return layer(a, ST(s));
+}
+
+int regcn_layer_f32(const regcn_layer_desc* g, void* s) {
+  if (!g) return set_error(REGCN_EINVAL, "null descriptor");
+  LayerArgs a{};
+  a.agg_mode = g->agg_mode;
+  a.x = g->x;
+  a.radius = g->radius;
+  a.rel = g->rel;
+  a.w_rel = g->w_rel;
+  a.nb = g->num_bases;
+  a.gamma = g->gamma;
+  a.rowptr = g->rowptr;
+  a.col_src = g->col_src;
+  a.col_type = g->col_type;
+  a.norm = g->norm;
+  a.budget = g->budget;
+  a.tiles = g->tiles;
+  a.n_pos_tiles = g->n_pos_tiles;
+  a.agg = g->agg;
+  a.w_n = g->w_n;
+  a.w_loop = g->w_loop;
+  a.w_evolve = g->w_evolve;
+  a.prev_t = g->prev_t;
+  a.w_skip = g->w_skip;
+  a.b_skip = g->b_skip;
+  a.drop_mask = g->drop_mask;
+  a.rows = g->rows;
+  a.n_pos = g->n_pos;
+  a.V = g->V;
+  a.d = g->d;
+  a.euclid = g->euclid;
+  a.k = make_curv(g->c);
+  a.h_out = g->h_out;
+  a.x_next = g->x_next;
+  a.r_next = g->r_next;
+  a.fuse_step = g->fuse_step;
+  if (g->fuse_step) {
+    StepArgs& t = a.step;
+    t.hc = nullptr;
+    t.x_prev = g->step_x_prev;
+    t.w_g = g->step_w_g;
+    t.b_g = g->step_b_g;
+    t.r_static = g->step_r_static;
+    t.w_r = g->step_w_r;
+    t.b_r = g->step_b_r;
+    t.eps_r = g->step_eps_r;
+    t.beta = g->step_beta;
+    t.layer_norm = g->step_layer_norm;
+    t.residual = g->step_residual;
+    t.V = g->V;
+    t.d = g->d;
+    t.k = a.k;
+    t.k_rad = make_curv(g->step_c_radius);
+    t.h_out = g->step_h_out;
+    t.x_out = g->step_x_out;
+    t.r_out = g->step_r_out;
+  }
+  return layer(a, ST(s));
 }
 
 int regcn_timestep_f32(const float* hc, const float* x_prev, const float* w_g, const float* b_g,
@@ -125,12 +217,77 @@ int regcn_timestep_f32(const float* hc, const float* x_prev, const float* w_g, c
   return timestep(a, ST(s));
 }
 
+size_t regcn_packed_linear_floats(int32_t n_gates, int32_t n_out, int32_t n_in) {
+  return packed_linear_floats(n_gates, n_out, n_in);
+}
+
+int regcn_pack_linear_f32(const float* w, int32_t n_gates, int32_t n_out, int32_t n_in, float* packed, void* s) {
+  return pack_linear(w, n_gates, n_out, n_in, packed, ST(s));
+}
+
+int regcn_relation_gru_f32(const float* x, const int32_t* rel_idx, const int32_t* rel_start, const float* rel_count,
+                           const float* x_mean, const float* emb_rel, const float* h_prev, const float* w_ih,
+                           const float* w_hh, const float* b_ih, const float* b_hh, int32_t R2, int32_t d,
+                           float* h_out, void* s) {
+  RelGruArgs a{x, rel_idx, rel_start, rel_count, x_mean, emb_rel, h_prev, w_ih, w_hh, b_ih, b_hh, R2, d, h_out};
+  return rel_gru(a, ST(s));
+}
+
+int regcn_roth_query_f32(const float* ent, const float* rel, const int64_t* trip, int32_t n_test, int32_t B,
+                         int32_t num_rels, const float* w1, const float* b1, const float* w2, const float* b2,
+                         const float* w_rot, const float* b_rot, const float* w_trans, const float* b_trans, int32_t d,
+                         float c, float* q_out, void* s) {
+  QueryArgs a{};
+  a.ent = ent;
+  a.rel = rel;
+  a.trip = trip;
+  a.n_test = n_test;
+  a.B = B;
+  a.num_rels = num_rels;
+  a.w1 = w1;
+  a.b1 = b1;
+  a.w2 = w2;
+  a.b2 = b2;
+  a.wrot = w_rot;
+  a.brot = b_rot;
+  a.wtr = w_trans;
+  a.btr = b_trans;
+  a.d = d;
+  a.k = make_curv(c);
+  a.q_out = q_out;
+  return query(a, 0, ST(s));
+}
+
+int regcn_roth_rel_query_f32(const float* ent, const int64_t* trip, int32_t n_test, int32_t B, int32_t num_rels,
+                             const float* w1, const float* b1, const float* w2, const float* b2,
+                             const float* global_rot, const float* rel, int32_t n_cand, int32_t d, float c,
+                             float* q_out, float* cand_out, void* s) {
+  QueryArgs a{};
+  a.ent = ent;
+  a.rel = rel;
+  a.trip = trip;
+  a.n_test = n_test;
+  a.B = B;
+  a.num_rels = num_rels;
+  a.w1 = w1;
+  a.b1 = b1;
+  a.w2 = w2;
+  a.b2 = b2;
+  a.global_rot = global_rot;
+  a.n_cand = n_cand;
+  a.d = d;
+  a.k = make_curv(c);
+  a.q_out = q_out;
+  a.cand_out = cand_out;
+  return query(a, 1, ST(s));
+}
+
 static ScoreArgs score_args(const float* q, const float* cand, const float* bias, const float* c_rel, const float* scale, const float* margin,
                             int32_t B, int32_t N, int32_t d, float c, int32_t use_dist) {
   ScoreArgs a{};
   Curv k = make_curv(c);
   a.q = q; a.e = cand; a.bias = bias; a.c_r = c_rel;
-  a.B = B; a.N = N; a.d = d; a.use_dist = use_dist;
+  a.B = B; a.N = N; a.d = d; a.use_dist = use_dist & 1; a.scale_raw = (use_dist >> 1) & 1;
   a.c = k.c; a.sqrt_c = k.sqrt_c; a.mx = k.mx;
   a.dist_mx = (float)(1.0 / (sqrt((double)c) + 1e-6) - 1e-6);
   a.scale_p = scale; a.margin_p = margin;
@@ -139,7 +296,7 @@ static ScoreArgs score_args(const float* q, const float* cand, const float* bias
 
 int regcn_hyp_score_f32(const float* q, const float* cand, const float* bias, const float* c_rel, const float* scale, const float* margin, int32_t B,
                         int32_t N, int32_t d, float c, int32_t use_dist, float* out, void* s) {
-  if (c_rel && !use_dist) return set_error(REGCN_EINVAL, "per-query curvature requires use_dist");
+  if (c_rel && !(use_dist & 1)) return set_error(REGCN_EINVAL, "per-query curvature requires use_dist");
   ScoreArgs a = score_args(q, cand, bias, c_rel, scale, margin, B, N, d, c, use_dist);
   a.out = out;
   return score(a, 0, nullptr, ST(s));
@@ -153,7 +310,7 @@ size_t regcn_hyp_ce_workspace_bytes(int32_t B, int32_t N) {
 int regcn_hyp_ce_f32(const float* q, const float* cand, const float* bias, const float* c_rel, const float* scale, const float* margin,
                      const int32_t* target, int32_t B, int32_t N, int32_t d, float c, int32_t use_dist,
                      void* workspace, float* loss_per_query, void* s) {
-  if (c_rel && !use_dist) return set_error(REGCN_EINVAL, "per-query curvature requires use_dist");
+  if (c_rel && !(use_dist & 1)) return set_error(REGCN_EINVAL, "per-query curvature requires use_dist");
   if (!workspace) return set_error(REGCN_EINVAL, "null workspace");
   ScoreArgs a = score_args(q, cand, bias, c_rel, scale, margin, B, N, d, c, use_dist);
   const size_t nblk = ((size_t)N + 63) / 64;

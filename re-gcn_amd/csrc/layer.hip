@@ -1,0 +1,537 @@
+// Fused message-passing layer (+ timestep) kernels.
+//
+// One workgroup = 4 waves = one tile of up to 16 destination rows with all d columns:
+//   1. CSR gather: the tile's in-edges are flattened into one item list and split into 4
+//      contiguous ranges, one per wave; each wave keeps 4 edges in flight and does a
+//      segmented (per-row) reduction into its own LDS partial row, so a tile's hub and its
+//      single-edge rows cost the same wall time.  Partials are combined in wave order
+//      (deterministic, no atomics).  Rows with in-degree > budget were pre-aggregated by
+//      the chunked kernels (aggregate.hip) and are read back instead.
+//   2. Self-loop / neighbour GEMMs on fp32 MFMA (rowtile.h) from LDS tiles.
+//   3. Epilogue in registers: clamp, rrelu, dropout mask, exp0 -> h; then either the next
+//      layer's prologue (x = log0 h, r = |h|) or the whole timestep (time gate GEMM, radius
+//      evolution) -- the layer output never round-trips through HBM.
+// Tiles come from the host (graph.py): in-degree-sorted rows packed greedily under an
+// edge budget, so no tile's gather is much longer than another's; zero in-degree rows
+// follow in plain 16-row tiles (self-evolve weight only).
+//
+// Reference: UnionRGCNLayer / LorentzRGCNLayer forward (hyperbolic_layers.py:242-323,
+// :627-694), rgcn/layers.py:226-279 (euclid), timestep hyperbolic_model.py:829-869.
+#include "common.h"
+#include "gather.h"
+#include "regcn_internal.h"
+#include "rowtile.h"
+
+namespace regcn {
+
+struct LdsLayout {
+  int lda;
+  int part, X, red, ints, xsh, total_bytes;  // float offsets; total in bytes
+};
+
+__host__ __device__ inline LdsLayout lds_layout(int d, bool gen_s) {
+  LdsLayout L;
+  L.lda = tile_lda(d);
+  L.part = 0;
+  L.X = NWAVE * TM * L.lda;
+  L.red = L.X + TM * L.lda;
+  L.ints = L.red + 2 * NWAVE * TM;
+  L.xsh = L.ints + 48;  // trow[16], toff[17], tmask[4] (+pad)
+  L.total_bytes = (L.xsh + (gen_s ? NWAVE * MAX_D : 0)) * 4;
+  return L;
+}
+
+// ---------------------------------------------------------------------- timestep epilogue
+// ct: current_h rows (Poincare) in fragments; P: clamp(x_prev) tile in LDS.
+//   cur = project(ct); [LN: exp0(normalize(log0(cur)))]; ct = clamp(log0(cur))
+//   tw = sigmoid(P @ W_g + b_g);  h = project(exp0(tw * ct + (1 - tw) * P))
+//   residual: r = beta r_s + (1 - beta)|h| + clamp(log0(h) . w_r + b_r, +-eps_r); else r = r_s
+//   h = apply_radius(h, r); outputs h, x = log0(h), r = max(|h|, eps).
+__device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, const float* P, int lda, const int* trow,
+                                              int n_valid, const StepArgs& p) {
+  Frag tw;
+  tw.zero();
+  mfma_tile(tw, P, lda, p.w_g, p.d);
+  frag_project(rr, ct, p.k);
+  if (p.layer_norm) {
+    frag_log0(rr, ct, p.k);
+    frag_normalize(rr, ct);
+    frag_exp0(rr, ct, p.k);
+  }
+  frag_log0(rr, ct, p.k);
+  Frag pt;
+  frag_from_tile(pt, P, lda, p.d);
+  float bg[4];
+  col_load(bg, p.b_g, p.d);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f4 c4 = clamp4(ct.t[j], -10.f, 10.f);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float g = sigmoidf(tw.t[j][r] + bg[j]);
+      ct.t[j][r] = g * c4[r] + (1.f - g) * pt.t[j][r];
+    }
+  }
+  frag_exp0(rr, ct, p.k);
+  frag_project(rr, ct, p.k);  // hyperbolic_model.py:860
+  float n2[4], rs[4], newr[4];
+  rr.sumsq(ct, n2);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = frag_row(r);
+    rs[r] = p.r_static[trow[i < n_valid ? i : 0]];
+  }
+  if (p.residual) {
+    float wr[4], dl[4];
+    col_load(wr, p.w_r, p.d);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float f = log0_factor(n2[r], p.k_rad);
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += wr[j] * (ct.t[j][r] * f);
+      dl[r] = s;
+    }
+    rr.allreduce(dl);
+    const float br = *p.b_r;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float delta = fminf(fmaxf(dl[r] + br, -p.eps_r), p.eps_r);
+      const float dyn = fmaxf(sqrtf(n2[r]), REGCN_EPS);
+      newr[r] = (p.beta * rs[r] + (1.f - p.beta) * dyn) + delta;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) newr[r] = rs[r];
+  }
+  float f[4];
+  const Curv& kr = p.residual ? p.k_rad : p.k;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float n = fmaxf(sqrtf(n2[r]), REGCN_EPS);
+    f[r] = fminf(fmaxf(newr[r], REGCN_EPS), kr.rmax) / n;
+  }
+  row_scale(ct, f);
+  frag_store(ct, p.h_out, trow, n_valid, p.d);
+  if (p.r_out || p.x_out) {
+    float h2[4];
+    rr.sumsq(ct, h2);
+    if (p.r_out) store_radius(h2, p.r_out, trow, n_valid);
+    if (p.x_out) {
+      float g[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g[r] = log0_factor(h2[r], p.k);
+      row_scale(ct, g);
+      frag_store(ct, p.x_out, trow, n_valid, p.d);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------- inline gather
+// Flattened, segmented gather of the tile's in-edges (see file header).  Wave w reduces
+// items [ib, ie); each row it touches gets one partial row in part[w][i] (+ the Lorentz
+// time coordinate at column d) and a bit in tmask[w].
+template <int AGG, int S>
+__device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int lda, const int* trow,
+                                            const int* toff, int count, int* tmask, float* xsh) {
+  const int lane = threadIdx.x & 63, w = wave_id();
+  const int col = lane * 4, d = p.d;
+  const bool active = col < d;
+  const int n_items = toff[count];
+  const int ib = (n_items * w) / NWAVE, ie = (n_items * (w + 1)) / NWAVE;
+  const int s_gen = (AGG == AGG_LORENTZ) ? d / p.nb : 1;
+  const int wstride = (AGG == AGG_LORENTZ) ? p.nb * s_gen * s_gen : 0;
+  const Curv k = p.k;
+  int cur = -1;
+  unsigned mask = 0;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  float acc0 = 0.f;
+  auto flush = [&]() {
+    if (cur >= 0) {
+      float* dst = part + (w * TM + cur) * lda;
+      if (active) {
+        dst[col] = acc.x;
+        dst[col + 1] = acc.y;
+        dst[col + 2] = acc.z;
+        dst[col + 3] = acc.w;
+      }
+      if (AGG == AGG_LORENTZ && lane == 0) dst[d] = acc0;
+      mask |= 1u << cur;
+    }
+  };
+  auto take = [&](int li) {
+    if (li != cur) {
+      flush();
+      cur = li;
+      acc = f4{0.f, 0.f, 0.f, 0.f};
+      acc0 = 0.f;
+    }
+  };
+  for (int t0 = ib; t0 < ie; t0 += 64) {
+    const int n = min(64, ie - t0);
+    int my_s = 0, my_t = 0, my_i = 0;
+    float my_w = 1.f;
+    if (lane < n) {
+      const int t = t0 + lane;
+      int i = 0;
+      while (i + 1 < count && toff[i + 1] <= t) ++i;
+      const int row = trow[i];
+      const int e = p.rowptr[row] + (t - toff[i]);
+      my_s = p.col_src[e];
+      my_t = p.col_type[e];
+      my_i = i;
+      if (AGG == AGG_UNION) my_w = expf(-p.gamma * fabsf(p.radius[my_s] - p.radius[row]));
+    }
+    int j = 0;
+    if constexpr (AGG == AGG_UNION || AGG == AGG_EUCLID) {
+      for (; j + 4 <= n; j += 4) {
+        f4 xs[4], rv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          xs[u] = load4(p.x + (int64_t)rl(my_s, j + u) * d, col, d);
+          rv[u] = load4(p.rel + (int64_t)rl(my_t, j + u) * d, col, d);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          take(rl(my_i, j + u));
+          if (AGG == AGG_EUCLID) acc += xs[u] + rv[u];
+          else acc += rlf(my_w, j + u) * (xs[u] + rv[u]);
+        }
+      }
+      for (; j < n; ++j) {
+        f4 xs = load4(p.x + (int64_t)rl(my_s, j) * d, col, d);
+        f4 rv = load4(p.rel + (int64_t)rl(my_t, j) * d, col, d);
+        take(rl(my_i, j));
+        if (AGG == AGG_EUCLID) acc += xs + rv;
+        else acc += rlf(my_w, j) * (xs + rv);
+      }
+    } else if constexpr (AGG == AGG_LORENTZ) {
+      if constexpr (S > 0) {
+        for (; j + 4 <= n; j += 4) {
+          f4 xs[4], rv[4], m[4];
+          WFrag<S> wf[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int src = rl(my_s, j + u), typ = rl(my_t, j + u);
+            xs[u] = load4(p.x + (int64_t)src * d, col, d);
+            rv[u] = load4(p.rel + (int64_t)typ * d, col, d);
+            if (active) wf[u].load(p.w_rel + (int64_t)typ * wstride, col);
+          }
+          float n2[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            m[u] = active ? wf[u].apply(xs[u]) + rv[u] : f4{0.f, 0.f, 0.f, 0.f};
+            n2[u] = row16_sum(dot4(m[u], m[u]));
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float t = (rlane(n2[u], 0) + rlane(n2[u], 16)) + (rlane(n2[u], 32) + rlane(n2[u], 48));
+            take(rl(my_i, j + u));
+            lorentz_accum(m[u], t, k, acc0, acc);
+          }
+        }
+      }
+      for (; j < n; ++j) {
+        const int src = rl(my_s, j), typ = rl(my_t, j);
+        const float* Wt = p.w_rel + (int64_t)typ * wstride;
+        f4 xs = load4(p.x + (int64_t)src * d, col, d);
+        f4 m = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (S > 0) {
+          if (active) {
+            WFrag<S> wf;
+            wf.load(Wt, col);
+            m = wf.apply(xs);
+          }
+        } else {
+          m = block_general4(xsh + w * MAX_D, xs, Wt, s_gen, col, active);
+        }
+        m += load4(p.rel + (int64_t)typ * d, col, d);
+        take(rl(my_i, j));
+        lorentz_accum(m, wave_sum(dot4(m, m)), k, acc0, acc);
+      }
+    }
+  }
+  flush();
+  if (lane == 0) tmask[w] = (int)mask;
+}
+
+// Combine the wave partials of row i (wave i % 4 does rows i, i+4, ...) and finish it:
+// Lorentz centroid -> log0, or norm-scaled sum; rows over budget read the pre-aggregated
+// row.  The result overwrites part[0][i] (the A operand / agg fragment source).
+template <int AGG>
+__device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int lda, const int* trow, int count,
+                                            const int* tmask) {
+  const int lane = threadIdx.x & 63, w = wave_id();
+  const int col = lane * 4, d = p.d;
+  for (int i = w; i < TM; i += NWAVE) {
+    f4 a = {0.f, 0.f, 0.f, 0.f};
+    if (i < count) {
+      const int row = trow[i];
+      const int deg = p.rowptr[row + 1] - p.rowptr[row];
+      if (deg > p.budget) {
+        a = load4(p.agg + (int64_t)row * d, col, d);
+      } else {
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
+        float acc0 = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < NWAVE; ++w2) {
+          if ((tmask[w2] >> i) & 1) {
+            const float* src = part + (w2 * TM + i) * lda;
+            if (col < d) acc += f4{src[col], src[col + 1], src[col + 2], src[col + 3]};
+            if (AGG == AGG_LORENTZ) acc0 += src[d];
+          }
+        }
+        if constexpr (AGG == AGG_LORENTZ) a = lorentz_finish(acc0, acc, p.k);
+        else a = acc * p.norm[row];
+      }
+    }
+    float* dst = part + i * lda;
+    if (col < d) {
+      dst[col] = a.x;
+      dst[col + 1] = a.y;
+      dst[col + 2] = a.z;
+      dst[col + 3] = a.w;
+    }
+  }
+}
+
+// ==================================================================================== layer
+template <int AGG, int S, bool STEP>
+__global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
+  extern __shared__ float lds[];
+  const LdsLayout L = lds_layout(p.d, AGG == AGG_LORENTZ && S == 0);
+  const int lda = L.lda;
+  float* part = lds + L.part;
+  float* X = lds + L.X;
+  int* trow = reinterpret_cast<int*>(lds + L.ints);
+  int* toff = trow + TM;
+  int* tmask = toff + TM + 1;
+  RowRed rr{lds + L.red, 0};
+  float* P1 = part + TM * lda;      // skip-connection operand
+  float* P2 = part + 2 * TM * lda;  // timestep: clamp(x_prev)
+
+  const int n_pos_tiles = p.tiles ? p.n_pos_tiles : (p.n_pos + TM - 1) / TM;
+  const bool pos = (int)blockIdx.x < n_pos_tiles;
+  int start, count;
+  if (pos) {
+    if (p.tiles) {
+      start = p.tiles[2 * blockIdx.x];
+      count = p.tiles[2 * blockIdx.x + 1];
+    } else {
+      start = blockIdx.x * TM;
+      count = min(TM, p.n_pos - start);
+    }
+  } else {
+    start = p.n_pos + (blockIdx.x - n_pos_tiles) * TM;
+    count = min(TM, p.V - start);
+  }
+  const bool inline_gather = pos && AGG != AGG_NONE;
+  if (threadIdx.x < 64) {
+    const int t = threadIdx.x;
+    const int row = p.rows[start + (t < count ? t : 0)];
+    if (t < TM) trow[t] = row;
+    if (inline_gather) {  // exclusive scan of the inline item counts over the 16 rows
+      int v = 0;
+      if (t < count) {
+        const int deg = p.rowptr[row + 1] - p.rowptr[row];
+        v = deg <= p.budget ? deg : 0;
+      }
+#pragma unroll
+      for (int o = 1; o < TM; o <<= 1) {
+        const int y = __shfl_up(v, o, TM);
+        if ((t & (TM - 1)) >= o) v += y;
+      }
+      if (t < TM) toff[t + 1] = v;
+      if (t == 0) toff[0] = 0;
+    }
+  }
+  __syncthreads();
+
+  // ---- operands: self-loop rows; pre-aggregated rows (AGG_NONE); gather
+  stage_rows<false>(X, lda, p.x, trow, p.d, count);
+  if (pos && AGG == AGG_NONE) stage_rows<false>(part, lda, p.agg, trow, p.d, count);
+  if (!inline_gather) {
+    if (STEP) stage_rows<true>(P2, lda, p.step.x_prev, trow, p.d, count);
+    if (p.prev_t) stage_rows<false>(P1, lda, p.prev_t, trow, p.d, count);
+  }
+  if (inline_gather) {
+    if constexpr (AGG != AGG_NONE) {
+      tile_gather<AGG, S>(p, part, lda, trow, toff, count, tmask, lds + L.xsh);
+      __syncthreads();
+      tile_finish<AGG>(p, part, lda, trow, count, tmask);
+    }
+    if (STEP) stage_rows<true>(P2, lda, p.step.x_prev, trow, p.d, count);
+    if (p.prev_t) stage_rows<false>(P1, lda, p.prev_t, trow, p.d, count);
+  }
+  __syncthreads();
+
+  // ---- v = clamp(agg [@ W_n]) + x @ (W_loop | W_evolve)
+  Frag v;
+  v.zero();
+  if (pos) {
+    if (p.w_n) mfma_tile(v, part, lda, p.w_n, p.d);
+    else frag_from_tile(v, part, lda, p.d);
+    if (!p.euclid) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v.t[j] = clamp4(v.t[j], -10.f, 10.f);
+    }
+  }
+  const float* wsel = pos ? p.w_loop : p.w_evolve;
+  if (wsel) mfma_tile(v, X, lda, wsel, p.d);
+  if (p.prev_t) {  // v = g v + (1 - g) prev_t, g = sigmoid(prev_t @ W_skip + b)
+    Frag g;
+    g.zero();
+    mfma_tile(g, P1, lda, p.w_skip, p.d);
+    Frag pt;
+    frag_from_tile(pt, P1, lda, p.d);
+    float b[4];
+    col_load(b, p.b_skip, p.d);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float gt = sigmoidf(g.t[j][r] + b[j]);
+        v.t[j][r] = gt * v.t[j][r] + (1.f - gt) * pt.t[j][r];
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (!p.euclid) v.t[j] = clamp4(v.t[j], -10.f, 10.f);
+    v.t[j] = leaky4(v.t[j]);
+  }
+  if (p.drop_mask) {
+    Frag m;
+    frag_load(m, p.drop_mask, trow, count, p.d);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v.t[j] *= m.t[j];
+  }
+  if (!p.euclid) frag_exp0(rr, v, p.k);
+
+  if constexpr (STEP) {
+    step_epilogue(rr, v, P2, lda, trow, count, p.step);
+  } else {
+    frag_store(v, p.h_out, trow, count, p.d);
+    if (p.r_next || (p.x_next && !p.euclid)) {
+      float n2[4];
+      rr.sumsq(v, n2);
+      if (p.r_next) store_radius(n2, p.r_next, trow, count);
+      if (p.x_next && !p.euclid) {
+        float f[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) f[r] = log0_factor(n2[r], p.k);
+        row_scale(v, f);
+      }
+    }
+    if (p.x_next) frag_store(v, p.x_next, trow, count, p.d);
+  }
+}
+
+// ================================================================================ timestep
+__global__ __launch_bounds__(NTHR) void k_timestep(StepArgs p) {
+  extern __shared__ float lds[];
+  const int lda = tile_lda(p.d);
+  float* P = lds;
+  RowRed rr{lds + TM * lda, 0};
+  int* trow = reinterpret_cast<int*>(lds + TM * lda + 2 * NWAVE * TM);
+  const int r0 = blockIdx.x * TM;
+  const int n_valid = min(TM, p.V - r0);
+  if (threadIdx.x < TM) trow[threadIdx.x] = r0 + (threadIdx.x < n_valid ? threadIdx.x : 0);
+  __syncthreads();
+  stage_rows<true>(P, lda, p.x_prev, trow, p.d, n_valid);
+  Frag ct;
+  frag_load(ct, p.hc, trow, n_valid, p.d);
+  __syncthreads();
+  step_epilogue(rr, ct, P, lda, trow, n_valid, p);
+}
+
+// ============================================================================ pack weights
+// Wp[s][jq][lane][e] = W[4s + lane/16][16(4jq + e) + lane%16] (zero outside d_in x d_out).
+__global__ void k_pack_weight(const float* __restrict__ W, int d_in, int d_out, float* __restrict__ Wp) {
+  const int S = (d_in + 3) >> 2;
+  const int total = S * 4 * 64 * 4;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int e = idx & 3, lane = (idx >> 2) & 63, jq = (idx >> 8) & 3, s = idx >> 10;
+    const int k = 4 * s + (lane >> 4), n = 16 * (4 * jq + e) + (lane & 15);
+    Wp[idx] = (k < d_in && n < d_out) ? W[(int64_t)k * d_out + n] : 0.f;
+  }
+}
+
+// ============================================================================ launchers
+template <int AGG, int S>
+static void launch_layer(const LayerArgs& a, dim3 grid, size_t lds, hipStream_t st) {
+  if (a.fuse_step)
+    hipLaunchKernelGGL((k_layer<AGG, S, true>), grid, dim3(NTHR), lds, st, a);
+  else
+    hipLaunchKernelGGL((k_layer<AGG, S, false>), grid, dim3(NTHR), lds, st, a);
+}
+
+int layer(const LayerArgs& a, hipStream_t st) {
+  if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "layer needs d %% 4 == 0, d <= 256 (d=%d)", a.d);
+  if (!a.x || !a.rows || (!a.h_out && !a.fuse_step)) return set_error(REGCN_EINVAL, "null pointer");
+  if ((a.w_loop == nullptr) != (a.w_evolve == nullptr)) return set_error(REGCN_EINVAL, "self-loop weights must come in pairs");
+  if (a.prev_t && (!a.w_skip || !a.b_skip)) return set_error(REGCN_EINVAL, "skip needs weight and bias");
+  if (a.n_pos < 0 || a.n_pos > a.V) return set_error(REGCN_EINVAL, "bad n_pos");
+  const int mode = a.agg_mode;
+  if (mode != AGG_NONE && mode != AGG_UNION && mode != AGG_EUCLID && mode != AGG_LORENTZ)
+    return set_error(REGCN_EINVAL, "unknown aggregation mode %d", mode);
+  if (mode == AGG_NONE && a.n_pos > 0 && !a.agg) return set_error(REGCN_EINVAL, "AGG_NONE needs agg rows");
+  if (mode != AGG_NONE) {
+    if (!a.rowptr || !a.col_src || !a.col_type || !a.rel) return set_error(REGCN_EINVAL, "gather needs CSR + rel");
+    if (mode == AGG_UNION && !a.radius) return set_error(REGCN_EINVAL, "union gather needs radius");
+    if (mode != AGG_LORENTZ && !a.norm) return set_error(REGCN_EINVAL, "gather needs norm");
+    if (mode == AGG_LORENTZ && (!a.w_rel || a.nb <= 0 || a.d % a.nb))
+      return set_error(REGCN_EINVAL, "lorentz gather needs weights and d %% num_bases == 0");
+    if (a.tiles && a.n_pos_tiles < 0) return set_error(REGCN_EINVAL, "bad tile count");
+  }
+  if ((mode == AGG_UNION || mode == AGG_LORENTZ) && a.euclid) return set_error(REGCN_EINVAL, "hyperbolic gather with euclid tail");
+  if (a.fuse_step) {
+    const StepArgs& s = a.step;
+    if (a.euclid) return set_error(REGCN_EINVAL, "the fused timestep is hyperbolic only");
+    if (!s.x_prev || !s.w_g || !s.b_g || !s.r_static || !s.h_out) return set_error(REGCN_EINVAL, "null timestep pointer");
+    if (s.residual && (!s.w_r || !s.b_r)) return set_error(REGCN_EINVAL, "residual radius needs w_r and b_r");
+    if (s.d != a.d || s.V != a.V) return set_error(REGCN_EINVAL, "timestep shape mismatch");
+  }
+  if (a.V == 0) return 0;
+  const int n_pos_tiles = (a.tiles && mode != AGG_NONE) ? a.n_pos_tiles : (a.n_pos + TM - 1) / TM;
+  LayerArgs b = a;
+  if (mode == AGG_NONE) b.tiles = nullptr;
+  b.n_pos_tiles = n_pos_tiles;
+  const unsigned grid = (unsigned)(n_pos_tiles + (a.V - a.n_pos + TM - 1) / TM);
+  const int s = mode == AGG_LORENTZ ? a.d / a.nb : 1;
+  const bool gen = mode == AGG_LORENTZ && s != 1 && s != 2 && s != 4;
+  const size_t lds = (size_t)lds_layout(a.d, gen).total_bytes;
+  switch (mode) {
+    case AGG_NONE: launch_layer<AGG_NONE, 1>(b, dim3(grid), lds, st); break;
+    case AGG_UNION: launch_layer<AGG_UNION, 1>(b, dim3(grid), lds, st); break;
+    case AGG_EUCLID: launch_layer<AGG_EUCLID, 1>(b, dim3(grid), lds, st); break;
+    default:
+      if (s == 1) launch_layer<AGG_LORENTZ, 1>(b, dim3(grid), lds, st);
+      else if (s == 2) launch_layer<AGG_LORENTZ, 2>(b, dim3(grid), lds, st);
+      else if (s == 4) launch_layer<AGG_LORENTZ, 4>(b, dim3(grid), lds, st);
+      else launch_layer<AGG_LORENTZ, 0>(b, dim3(grid), lds, st);
+  }
+  return check_launch("k_layer");
+}
+
+int timestep(const StepArgs& a, hipStream_t st) {
+  if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "timestep needs d %% 4 == 0, d <= 256");
+  if (!a.hc || !a.x_prev || !a.w_g || !a.b_g || !a.r_static || !a.h_out) return set_error(REGCN_EINVAL, "null pointer");
+  if (a.residual && (!a.w_r || !a.b_r)) return set_error(REGCN_EINVAL, "residual radius needs w_r and b_r");
+  if (a.V == 0) return 0;
+  const unsigned grid = (unsigned)((a.V + TM - 1) / TM);
+  const size_t lds = (size_t)(TM * tile_lda(a.d) + 2 * NWAVE * TM + TM) * 4;
+  hipLaunchKernelGGL(k_timestep, dim3(grid), dim3(NTHR), lds, st, a);
+  return check_launch("k_timestep");
+}
+
+size_t packed_weight_floats(int d_in) { return (size_t)((d_in + 3) / 4) * 4 * 64 * 4; }
+
+int pack_weight(const float* W, int d_in, int d_out, float* Wp, hipStream_t st) {
+  if (!W || !Wp) return set_error(REGCN_EINVAL, "null pointer");
+  if (d_in <= 0 || d_out <= 0 || d_out > MAX_D) return set_error(REGCN_EINVAL, "pack_weight needs d_out <= 256");
+  const int total = (int)packed_weight_floats(d_in);
+  hipLaunchKernelGGL(k_pack_weight, dim3((total + 255) / 256), dim3(256), 0, st, W, d_in, d_out, Wp);
+  return check_launch("k_pack_weight");
+}
+
+}  // namespace regcn

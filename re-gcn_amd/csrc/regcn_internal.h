@@ -36,25 +36,7 @@ int lorentz_sum(const float* x, const float* rel, const float* W, const int* col
                 const void* chunks, int n_chunks, const void* fixups, int n_fix, int nb, float c, int d,
                 float* partial, int pstride, float* out, hipStream_t st);
 
-// ---- argument blocks of the fused kernels (rowgemm.hip, score.hip) ----
-struct LayerArgs {
-  const float* agg;
-  const float* w_n;
-  const float* x;
-  const float* w_loop;
-  const float* w_evolve;
-  const float* prev_t;
-  const float* w_skip;
-  const float* b_skip;
-  const float* drop_mask;
-  const int* rows;
-  int n_pos, V, d, euclid;
-  Curv k;
-  float* h_out;
-  float* x_next;
-  float* r_next;
-};
-
+// ---- argument blocks of the fused kernels (layer.hip, score.hip) ----
 struct StepArgs {
   const float* hc;
   const float* x_prev;
@@ -72,6 +54,41 @@ struct StepArgs {
   float* r_out;
 };
 
+// One message-passing layer: inline CSR gather + self-loop/neighbour GEMMs + epilogue,
+// optionally followed by the timestep (layer.hip).  Weights are prepacked.
+struct LayerArgs {
+  int agg_mode;             // AGG_UNION / AGG_EUCLID / AGG_LORENTZ (inline gather) or AGG_NONE
+  const float* x;           // V x d layer input (tangent rows; raw rows for euclid)
+  const float* radius;      // V, union message weights
+  const float* rel;         // R2 x d relation rows
+  const float* w_rel;       // R2 x nb*s*s Lorentz block weights
+  int nb;
+  float gamma;
+  const int* rowptr;        // V + 1, destination-sorted CSR
+  const int* col_src;
+  const int* col_type;
+  const float* norm;        // V, union / euclid row scale
+  int budget;               // rows with in-degree > budget read `agg` (pre-aggregated)
+  const int* tiles;         // n_pos_tiles x {start, count} over rows[0, n_pos); null: 16-row tiles
+  int n_pos_tiles;
+  const float* agg;         // V x d pre-aggregated rows (heavy rows; every pos row for AGG_NONE)
+  const float* w_n;
+  const float* w_loop;
+  const float* w_evolve;
+  const float* prev_t;
+  const float* w_skip;
+  const float* b_skip;
+  const float* drop_mask;
+  const int* rows;          // V: rows with in-degree > 0 first (n_pos), then the rest
+  int n_pos, V, d, euclid;
+  Curv k;
+  float* h_out;
+  float* x_next;
+  float* r_next;
+  int fuse_step;            // run the timestep on the layer output (step.hc unused)
+  StepArgs step;
+};
+
 struct ScoreArgs {
   const float* q;
   const float* e;
@@ -83,15 +100,60 @@ struct ScoreArgs {
   float c, sqrt_c, mx, dist_mx;
   const float* scale_p;  // device scalar or null (1.0): softplus(raw) + 1e-6, hyperbolic_decoder.py:717
   const float* margin_p; // device scalar or null (0.0)
+  int scale_raw;         // scale_p holds the raw parameter: softplus(raw) + 1e-6 in-kernel
   float scale, margin;   // filled in-kernel from the pointers
   float* out;            // [B, N] score (SCORE mode)
   float* part;           // [B, nblk, 2] (CE mode): running max, sum exp
   float* tgt_logit;      // [B] (CE mode)
 };
 
+// Relation GRU of one timestep (relgru.hip).
+struct RelGruArgs {
+  const float* x;          // V x d entity tangent rows (x_mean source)
+  const int* rel_idx;      // r_to_e entity ids
+  const int* rel_start;    // R2 span starts into rel_idx
+  const float* rel_count;  // R2 span lengths (0: relation absent)
+  const float* x_mean;     // R2 x d precomputed means, or null (gather in-kernel)
+  const float* emb_rel;    // R2 x d
+  const float* h_prev;     // R2 x d GRU state
+  const float* w_ih;       // packed (pack_linear, 3 gates, d x 2d)
+  const float* w_hh;       // packed (3 gates, d x d)
+  const float* b_ih;
+  const float* b_hh;
+  int R2, d;
+  float* h_out;
+};
+
+// RotH decoder queries (query.hip).  Linear weights are packed transposed (x @ W^T).
+struct QueryArgs {
+  const float* ent;         // V x d final entity embedding
+  const float* rel;         // R2 x d relation embedding (RotH: query rows; RotHRel: candidates)
+  const int64_t* trip;      // n_test x 3 test triples (s, r, o)
+  int n_test, B, num_rels;  // B <= 2 n_test queries: forward then inverse
+  const float* w1;          // reshape_fc1 / fc2
+  const float* b1;
+  const float* w2;
+  const float* b2;
+  const float* wrot;        // RotH rot_proj (d -> d/2)
+  const float* brot;
+  const float* wtr;         // RotH trans_proj
+  const float* btr;
+  const float* global_rot;  // RotHRel (d/2)
+  int n_cand;               // RotHRel: rows of exp0(rel) written to cand_out
+  int d;
+  Curv k;
+  float* q_out;             // B x d
+  float* cand_out;
+};
+int query(const QueryArgs& a, int mode, hipStream_t st);
+
+size_t packed_linear_floats(int n_gates, int n_out, int n_in);
+int pack_linear(const float* W, int n_gates, int n_out, int n_in, float* Wp, hipStream_t st);
+int rel_gru(const RelGruArgs& a, hipStream_t st);
+
 size_t packed_weight_floats(int d_in);
 int pack_weight(const float* W, int d_in, int d_out, float* Wp, hipStream_t st);
-int layer_tail(const LayerArgs& a, hipStream_t st);
+int layer(const LayerArgs& a, hipStream_t st);
 int timestep(const StepArgs& a, hipStream_t st);
 int score(ScoreArgs& a, int mode, float* loss, hipStream_t st);
 int rank(const float* S, int B, int N, const int* target, const int* filt_ptr, const int* filt_idx, int* rank_raw,

@@ -88,6 +88,8 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
   typedef ScoreT<F64> S;
   typedef typename S::T T;
   p.scale = p.scale_p ? *p.scale_p : 1.f;
+  if (p.scale_raw && p.scale_p)  // softplus(raw) + 1e-6 (hyperbolic_decoder.py:717; torch threshold 20)
+    p.scale = (p.scale > 20.f ? p.scale : log1pf(expf(p.scale))) + 1e-6f;
   p.margin = p.margin_p ? *p.margin_p : 0.f;
   __shared__ T Qs[SQ * SLD];
   __shared__ T Es[SN * SLD];

@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libregcn_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -48,11 +48,36 @@ _SIGS = {
     "regcn_hyp_ce_workspace_bytes": [_c_int, _c_int],
     "regcn_hyp_ce_f32": [P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P, P],
     "regcn_rank_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
+    "regcn_layer_f32": [P, P],
+    "regcn_packed_linear_floats": [_c_int, _c_int, _c_int],
+    "regcn_pack_linear_f32": [P, _c_int, _c_int, _c_int, P, P],
+    "regcn_relation_gru_f32": [P, P, P, P, P, P, P, P, P, P, P, _c_int, _c_int, P, P],
+    "regcn_roth_query_f32": [P, P, P, _c_int, _c_int, _c_int, P, P, P, P, P, P, P, P, _c_int, _c_f, P, P],
+    "regcn_roth_rel_query_f32": [P, P, _c_int, _c_int, _c_int, P, P, P, P, P, P, _c_int, _c_int, _c_f, P, P, P],
 }
+
+SCORE_DIST, SCORE_RAW_SCALE = 1, 2
 _RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz,
-            "regcn_packed_weight_floats": _c_sz}
+            "regcn_packed_weight_floats": _c_sz, "regcn_packed_linear_floats": _c_sz}
 
 _lib = None
+
+AGG_UNION, AGG_EUCLID, AGG_LORENTZ, AGG_NONE = 0, 2, 3, 4
+
+
+class LayerDesc(ctypes.Structure):
+    """regcn_layer_desc (include/regcn_hip.h); pointer fields take dptr()/None."""
+    _fields_ = [
+        ("agg_mode", _c_int), ("x", P), ("radius", P), ("rel", P), ("w_rel", P), ("num_bases", _c_int),
+        ("gamma", _c_f), ("rowptr", P), ("col_src", P), ("col_type", P), ("norm", P), ("budget", _c_int),
+        ("tiles", P), ("n_pos_tiles", _c_int), ("agg", P), ("w_n", P), ("w_loop", P), ("w_evolve", P),
+        ("prev_t", P), ("w_skip", P), ("b_skip", P), ("drop_mask", P), ("rows", P), ("n_pos", _c_int),
+        ("V", _c_int), ("d", _c_int), ("euclid", _c_int), ("c", _c_f), ("h_out", P), ("x_next", P),
+        ("r_next", P), ("fuse_step", _c_int), ("step_x_prev", P), ("step_w_g", P), ("step_b_g", P),
+        ("step_r_static", P), ("step_w_r", P), ("step_b_r", P), ("step_eps_r", _c_f), ("step_beta", _c_f),
+        ("step_layer_norm", _c_int), ("step_residual", _c_int), ("step_c_radius", _c_f), ("step_h_out", P),
+        ("step_x_out", P), ("step_r_out", P),
+    ]
 
 
 class HipLibraryError(RuntimeError):
@@ -93,12 +118,16 @@ def call(name, *args):
     check(getattr(lib(), name)(*args), name)
 
 
+def call_layer(desc):
+    check(lib().regcn_layer_f32(ctypes.byref(desc), stream()), "regcn_layer_f32")
+
+
 def stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-def dptr(t, dtype=torch.float32, what="tensor"):
-    """Device pointer of a contiguous HIP tensor (None -> NULL)."""
+def addr(t, dtype=torch.float32, what="tensor"):
+    """Device address (int) of a contiguous HIP tensor (None -> None)."""
     if t is None:
         return None
     if not isinstance(t, torch.Tensor):
@@ -109,7 +138,13 @@ def dptr(t, dtype=torch.float32, what="tensor"):
         raise TypeError("%s must be %s (got %s)" % (what, dtype, t.dtype))
     if not t.is_contiguous():
         raise ValueError("%s must be contiguous" % what)
-    return ctypes.c_void_p(t.data_ptr())
+    return t.data_ptr()
+
+
+def dptr(t, dtype=torch.float32, what="tensor"):
+    """Device pointer of a contiguous HIP tensor (None -> NULL)."""
+    a = addr(t, dtype, what)
+    return None if a is None else ctypes.c_void_p(a)
 
 
 def fptr(t, what="tensor"):

@@ -90,7 +90,7 @@ class SnapshotGraph:
     """One temporal snapshot (see module docstring)."""
 
     def __init__(self, num_nodes, num_rels, src, dst, etype, uniq_r, r_len, r_to_e,
-                 chunk_edges=DEFAULT_CHUNK_EDGES):
+                 chunk_edges=DEFAULT_CHUNK_EDGES, tile_budget=None):
         V = int(num_nodes)
         self.num_nodes_, self.num_rels = V, int(num_rels)
         self.device = torch.device("cpu")
@@ -117,34 +117,46 @@ class SnapshotGraph:
         self.chunk_edges = int(chunk_edges) if chunk_edges else chunk_size_for(E)
         chunks, fixups, nslot = _chunk_rows(rowptr, np.arange(V), self.chunk_edges)
         pos = np.nonzero(in_deg > 0)[0]
+        pos = pos[np.argsort(-in_deg[pos], kind="stable")]  # in-degree descending (tile packing)
         zero = np.nonzero(in_deg == 0)[0]
+        # fused-layer tiles (csrc/layer.hip): rows over the edge budget are pre-aggregated
+        self.budget = int(tile_budget) if tile_budget else tile_budget_for(E, self.chunk_edges)
+        heavy = pos[in_deg[pos] > self.budget]
+        tiles = _pack_tiles(np.where(in_deg[pos] > self.budget, 0, in_deg[pos]), self.budget)
+        hchunks, hfixups, hslot = _chunk_spans(rowptr[heavy], in_deg[heavy], heavy, self.chunk_edges)
         R2 = 2 * self.num_rels
-        rel_ptr = np.zeros(R2 + 1, dtype=np.int64)
         rel_count = np.zeros(R2, dtype=np.float32)
+        rel_start = np.zeros(R2, dtype=np.int64)
         if len(r_len):
             lens = np.array([b - a for a, b in r_len], dtype=np.int64)
             ur = np.asarray(uniq_r, dtype=np.int64)
             rel_count[ur] = lens
             # spans are laid out in uniq_r order; re-express them per relation id
             starts = np.array([a for a, _ in r_len], dtype=np.int64)
-            rel_start = np.zeros(R2, dtype=np.int64)
             rel_start[ur] = starts
             rel_len = np.zeros(R2, dtype=np.int64)
             rel_len[ur] = lens
             rchunks, rfix, rslot = _chunk_rows_spans(rel_start, rel_len, self.chunk_edges)
         else:
             rchunks, rfix, rslot = np.zeros((0, 4), np.int32), np.zeros((0, 4), np.int32), 0
-        del rel_ptr
         self._host = {
             "col_src": src[order].astype(np.int32), "col_type": etype[order].astype(np.int32),
             "chunks": chunks, "fixups": fixups, "norm": norm,
             "rows": np.concatenate([pos, zero]).astype(np.int32),
             "rel_idx": np.asarray(r_to_e, dtype=np.int32).reshape(-1),
             "rel_count": rel_count, "rel_chunks": rchunks, "rel_fixups": rfix,
+            "rel_start": rel_start.astype(np.int32),
+            "rowptr": rowptr.astype(np.int32), "tiles": tiles,
+            "heavy_chunks": hchunks, "heavy_fixups": hfixups,
         }
         self.n_pos = int(len(pos))
+        self.n_pos_tiles = int(len(tiles))
+        self.n_heavy = int(len(heavy))
+        self.heavy_slots = hslot
         self.n_slots = nslot
         self.rel_slots = rslot
+        # relation spans short enough for the GRU kernel's in-kernel mean (csrc/relgru.hip)
+        self.rel_max_span = int(rel_count.max()) if R2 else 0
         self.dev = None
 
     # ---------------------------------------------------------------- DGL-visible surface
@@ -187,6 +199,50 @@ class SnapshotGraph:
         return self.dev
 
 
+def tile_budget_for(num_edges, chunk_edges):
+    """In-edges one fused-layer tile gathers inline (4 waves share them).  Small snapshots
+    keep it at 64 (16 edges = 4 batches of 4 per wave) so no tile outlasts the rest by
+    much; large ones raise it with the chunk size (many tiles per CU hide the spread)."""
+    return int(max(64, 4 * chunk_edges)) if num_edges > 65536 else 64
+
+
+def _pack_tiles(inline_deg, budget):
+    """Greedy tiles over the in-degree-sorted positive rows: up to 16 rows per tile while
+    the tile's inline edges stay within `budget` (a row over budget contributes 0).
+    Returns int32[n][2] = {start, count}."""
+    n = len(inline_deg)
+    if n == 0:
+        return np.zeros((0, 2), np.int32)
+    cs = np.concatenate([[0], np.cumsum(inline_deg, dtype=np.int64)])
+    out = []
+    a = 0
+    while a < n:
+        if cs[min(a + 16, n)] - cs[a] <= budget:  # the common case once past the hubs
+            cnt = min(16, n - a)
+        else:
+            cnt = int(np.searchsorted(cs, cs[a] + budget, side="right")) - 1 - a
+            cnt = max(1, min(16, cnt))
+        out.append((a, cnt))
+        a += cnt
+    return np.asarray(out, dtype=np.int32).reshape(-1, 2)
+
+
+def _chunk_spans(starts, lens, rows, chunk_edges):
+    """Chunks {row, beg, end, slot} + fixups over explicit per-row CSR spans."""
+    chunks_l, fix_l, nslot = [], [], 0
+    for r, b, n in zip(rows, starts, lens):
+        k = (int(n) + chunk_edges - 1) // chunk_edges
+        if k == 1:
+            chunks_l.append((r, b, b + n, -1))
+            continue
+        for i in range(k):
+            chunks_l.append((r, b + i * chunk_edges, min(b + (i + 1) * chunk_edges, b + n), nslot + i))
+        fix_l.append((r, nslot, nslot + k, 0))
+        nslot += k
+    return (np.array(chunks_l, dtype=np.int32).reshape(-1, 4), np.array(fix_l, dtype=np.int32).reshape(-1, 4),
+            nslot)
+
+
 def _chunk_rows_spans(start, length, chunk_edges):
     """Chunk per-relation spans [start[r], start[r]+length[r]) of the r_to_e list."""
     R = len(start)
@@ -211,15 +267,18 @@ def _chunk_rows_spans(start, length, chunk_edges):
     return chunks, fixups, nslot
 
 
-def build_sub_graph(num_nodes, num_rels, triples, use_cuda=False, gpu=0, chunk_edges=DEFAULT_CHUNK_EDGES):
-    """rgcn/utils.py:100-134 (same signature; returns a SnapshotGraph)."""
+def build_sub_graph(num_nodes, num_rels, triples, use_cuda=False, gpu=0, chunk_edges=DEFAULT_CHUNK_EDGES,
+                    tile_budget=None):
+    """rgcn/utils.py:100-134 (same signature; returns a SnapshotGraph).  chunk_edges /
+    tile_budget override the work-list heuristics (tests use them to force split rows)."""
     triples = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
     s, r, o = triples[:, 0], triples[:, 1], triples[:, 2]
     src = np.concatenate((s, o))
     dst = np.concatenate((o, s))
     etype = np.concatenate((r, r + num_rels))
     uniq_r, r_len, r_to_e = r2e(triples, num_rels)
-    g = SnapshotGraph(num_nodes, num_rels, src, dst, etype, uniq_r, r_len, r_to_e, chunk_edges=chunk_edges)
+    g = SnapshotGraph(num_nodes, num_rels, src, dst, etype, uniq_r, r_len, r_to_e, chunk_edges=chunk_edges,
+                      tile_budget=tile_budget)
     if use_cuda:
         g = g.to(gpu)
         g.r_to_e = torch.from_numpy(np.array(r_to_e, dtype=np.int64))  # :133

@@ -17,6 +17,7 @@ from torch.nn.parameter import Parameter
 
 from . import _lib
 from .hyperbolic_ops import HyperbolicOps
+from .weights import packed_t
 
 SCORE_SCALE_EPSILON = 1e-6
 REL_CURVATURE_EPSILON = 1e-5
@@ -66,16 +67,19 @@ def _score_operands(query, candidates, bias, score_scale, score_margin, query_cu
 
 
 def _chunked_hyperbolic_dist_score(query, candidates, bias, c, q_chunk_size, c_chunk_size, score_scale=None,
-                                   score_margin=0.0, query_curvature=None, use_hyperbolic_distance=False):
-    """hyperbolic_decoder.py:89-179 -> regcn_hyp_score_f32.  Returns (B, N)."""
+                                   score_margin=0.0, query_curvature=None, use_hyperbolic_distance=False,
+                                   _raw_scale=False):
+    """hyperbolic_decoder.py:89-179 -> regcn_hyp_score_f32.  Returns (B, N).
+    _raw_scale: score_scale is score_scale_raw; softplus + eps is applied on the device."""
     B, d = query.shape
     N = candidates.shape[0]
     q, e, b, cr, sc, mg = _score_operands(query, candidates, bias, score_scale, score_margin,
                                                     query_curvature if use_hyperbolic_distance else None)
     out = torch.empty(B, N, device=q.device, dtype=torch.float32)
     f = _lib.fptr
+    flags = (_lib.SCORE_DIST if use_hyperbolic_distance else 0) | (_lib.SCORE_RAW_SCALE if _raw_scale else 0)
     _lib.call("regcn_hyp_score_f32", f(q, "query"), f(e, "candidates"), f(b), f(cr), f(sc), f(mg),
-              B, N, d, _cf(c), int(bool(use_hyperbolic_distance)), f(out), _lib.stream())
+              B, N, d, _cf(c), flags, f(out), _lib.stream())
     return out
 
 
@@ -166,8 +170,8 @@ class _EntityDecoderBase(nn.Module):
         rel_c = self._relation_curvature(triplets[:, 1])
         scores = _chunked_hyperbolic_dist_score(
             q, entity_embedding, self.entity_bias, self.c, self.query_chunk_size, self.candidate_chunk_size,
-            score_scale=self._score_scale(), score_margin=self.score_margin, query_curvature=rel_c,
-            use_hyperbolic_distance=self.use_relation_specific_curvature)
+            score_scale=self.score_scale_raw, score_margin=self.score_margin, query_curvature=rel_c,
+            use_hyperbolic_distance=self.use_relation_specific_curvature, _raw_scale=True)
         if self.entity_bias is not None:
             scores = scores + self.entity_bias[triplets[:, 0]].unsqueeze(1)
         return scores
@@ -239,7 +243,20 @@ class HyperbolicRotH(_EntityDecoderBase):
         return x + self.reshape_fc2(F.relu(self.reshape_fc1(x)))
 
     def _query(self, ent, rel, trip):
-        """hyperbolic_decoder.py:1065-1085."""
+        """hyperbolic_decoder.py:1065-1085.  In eval mode (dropout = identity) one HIP launch
+        (regcn_roth_query_f32); with active dropout the same op sequence on torch."""
+        if not (self.training and self.dropout.p > 0) and not getattr(self, "_torch_query", False):
+            d = ent.shape[1]
+            q = torch.empty(trip.shape[0], d, device=ent.device, dtype=torch.float32)
+            f = _lib.fptr
+            lins = (self.reshape_fc1, self.reshape_fc2, self.rot_proj, self.trans_proj)
+            ws = [packed_t(l.weight) for l in lins]
+            bs = [l.bias.detach() for l in lins]
+            _lib.call("regcn_roth_query_f32", f(ent.contiguous(), "entity_embedding"),
+                      f(rel.detach().contiguous(), "rel_embedding"), _lib.dptr(trip.contiguous(), torch.int64),
+                      trip.shape[0], trip.shape[0], 0, f(ws[0]), f(bs[0]), f(ws[1]), f(bs[1]), f(ws[2]), f(bs[2]),
+                      f(ws[3]), f(bs[3]), d, _cf(self.c), f(q), _lib.stream())
+            return q
         c = self.c
         r_idx = trip[:, 1]
         s_emb = HyperbolicOps.project_to_ball(ent[trip[:, 0]], c)
@@ -360,6 +377,26 @@ class HyperbolicRotHRel(_RelDecoderBase):
         self.dropout = nn.Dropout(dropout)
 
     givens_rotation = staticmethod(givens_rotation)
+
+    def forward(self, entity_embedding, rel_embedding, triplets, mode="train"):
+        """Eval mode: queries and the exp0 candidates in one launch (regcn_roth_rel_query_f32),
+        then the scorer with softplus(score_scale_raw) applied on the device."""
+        if self.training and self.dropout.p > 0:
+            return super().forward(entity_embedding, rel_embedding, triplets, mode)
+        B, d = triplets.shape[0], entity_embedding.shape[1]
+        R2 = rel_embedding.shape[0]
+        q = torch.empty(B, d, device=entity_embedding.device, dtype=torch.float32)
+        cand = torch.empty(R2, d, device=entity_embedding.device, dtype=torch.float32)
+        f = _lib.fptr
+        _lib.call("regcn_roth_rel_query_f32", f(entity_embedding.contiguous(), "entity_embedding"),
+                  _lib.dptr(triplets.contiguous(), torch.int64), B, B, 0, f(packed_t(self.reshape_fc1.weight)),
+                  f(self.reshape_fc1.bias.detach()), f(packed_t(self.reshape_fc2.weight)),
+                  f(self.reshape_fc2.bias.detach()), f(self.global_rot.detach()),
+                  f(rel_embedding.detach().contiguous(), "rel_embedding"), R2, d, _cf(self.c), f(q), f(cand),
+                  _lib.stream())
+        return _chunked_hyperbolic_dist_score(q, cand, self.rel_bias, self.c, self.query_chunk_size,
+                                              self.candidate_chunk_size, score_scale=self.score_scale_raw,
+                                              score_margin=self.score_margin, _raw_scale=True)
 
     def _query(self, ent, trip):
         """hyperbolic_decoder.py:1223-1234."""

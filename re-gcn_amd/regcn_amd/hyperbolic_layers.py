@@ -42,6 +42,90 @@ def layer_tail(agg, w_n, x, w_loop, w_evolve, prev_t, w_skip, b_skip, drop_mask,
     return h, xn, rn
 
 
+def _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c):
+    """Pre-aggregate the rows over the fused kernel's edge budget (chunked kernels);
+    returns the V x d buffer holding them, or None when the snapshot has none."""
+    if not g.n_heavy:
+        return None
+    wk = g.work()
+    V, d = x.shape
+    agg = torch.empty_like(x)
+    hc, hf = wk["heavy_chunks"], wk["heavy_fixups"]
+    stride = d + 4
+    part = torch.empty(max(g.heavy_slots, 1), stride, device=x.device, dtype=torch.float32)
+    f, i = _lib.fptr, _lib.iptr
+    if mode == _lib.AGG_LORENTZ:
+        _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(wk["col_src"]), i(wk["col_type"]), i(hc),
+                  hc.shape[0], i(hf), hf.shape[0], nb, float(c), d, f(part), stride, f(agg), _lib.stream())
+    elif mode == _lib.AGG_UNION:
+        _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(wk["col_src"]), i(wk["col_type"]),
+                  f(wk["norm"]), i(hc), hc.shape[0], i(hf), hf.shape[0], float(gamma), d, f(part), stride, f(agg),
+                  _lib.stream())
+    else:
+        _lib.call("regcn_euclid_aggregate_f32", f(x), f(rel), i(wk["col_src"]), i(wk["col_type"]), f(wk["norm"]),
+                  i(hc), hc.shape[0], i(hf), hf.shape[0], d, f(part), stride, f(agg), _lib.stream())
+    return agg
+
+
+class StepSpec:
+    """Timestep operands fused behind the last layer (regcn_layer_desc step_* fields)."""
+
+    def __init__(self, x_prev, w_g, b_g, r_static, w_r, b_r, eps_r, beta, layer_norm, residual, c_radius):
+        self.x_prev, self.w_g, self.b_g, self.r_static = x_prev, w_g, b_g, r_static
+        self.w_r, self.b_r, self.eps_r, self.beta = w_r, b_r, eps_r, beta
+        self.layer_norm, self.residual, self.c_radius = layer_norm, residual, c_radius
+
+
+def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip, drop_mask, c,
+              euclid=False, step=None):
+    """One fused layer launch (regcn_layer_f32): inline gather + GEMMs + epilogue, or with
+    `step` the timestep too.  Returns (h, x_next, r_next) of the layer (or of the step)."""
+    wk = g.work()
+    V, d = x.shape
+    a = _lib.addr
+    agg = _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c)
+    h = torch.empty_like(x)
+    xn = torch.empty_like(x)
+    rn = torch.empty(V, device=x.device, dtype=torch.float32)
+    pk = [packed(w) for w in (w_n, w_loop, w_evolve, w_skip)]
+    desc = _lib.LayerDesc()
+    desc.agg_mode = mode
+    desc.x = a(x, what="x")
+    desc.radius = a(r, what="radius")
+    desc.rel = a(rel, what="rel_emb")
+    desc.w_rel = a(w_rel, what="weight")
+    desc.num_bases = int(nb)
+    desc.gamma = float(gamma)
+    desc.rowptr = a(wk["rowptr"], torch.int32)
+    desc.col_src = a(wk["col_src"], torch.int32)
+    desc.col_type = a(wk["col_type"], torch.int32)
+    desc.norm = a(wk["norm"])
+    desc.budget = g.budget
+    desc.tiles = a(wk["tiles"], torch.int32)
+    desc.n_pos_tiles = g.n_pos_tiles
+    desc.agg = a(agg)
+    desc.w_n, desc.w_loop, desc.w_evolve, desc.w_skip = (a(w) for w in pk)
+    desc.prev_t = a(prev_t, what="prev_h")
+    desc.b_skip = a(b_skip)
+    desc.drop_mask = a(drop_mask)
+    desc.rows = a(wk["rows"], torch.int32)
+    desc.n_pos, desc.V, desc.d, desc.euclid = g.n_pos, V, d, int(bool(euclid))
+    desc.c = float(c)
+    if step is None:
+        desc.h_out, desc.x_next, desc.r_next = a(h), a(xn), a(rn)
+    else:
+        desc.fuse_step = 1
+        desc.step_x_prev = a(step.x_prev, what="x_prev")
+        desc.step_w_g, desc.step_b_g = a(step.w_g), a(step.b_g)
+        desc.step_r_static, desc.step_w_r, desc.step_b_r = a(step.r_static), a(step.w_r), a(step.b_r)
+        desc.step_eps_r, desc.step_beta = float(step.eps_r), float(step.beta)
+        desc.step_layer_norm, desc.step_residual = int(bool(step.layer_norm)), int(bool(step.residual))
+        desc.step_c_radius = float(step.c_radius)
+        desc.step_h_out, desc.step_x_out, desc.step_r_out = a(h), a(xn), a(rn)
+    _lib.call_layer(desc)
+    return h, xn, rn
+
+
 def _partial(g, d, device, lorentz=False):
     if g.n_slots == 0:
         return None, 0
@@ -76,31 +160,23 @@ class HyperbolicUnionRGCNLayer(nn.Module):
             self.skip_bias = nn.Parameter(torch.zeros(out_feat))
         self.dropout = nn.Dropout(dropout) if dropout > 0 else None
 
-    def forward(self, g, h_hyper, rel_emb, prev_h=None):
-        """hyperbolic_layers.py:242-323."""
+    def forward(self, g, h_hyper, rel_emb, prev_h=None, step=None):
+        """hyperbolic_layers.py:242-323 (one fused launch; `step` fuses the timestep)."""
         if self.activation is None:
             raise NotImplementedError("the fused tail applies rrelu; activation=None is not supported")
         self.rel_emb = rel_emb
         c = float(self.c)
         x, r = tangent_of(h_hyper, c)
-        wk = g.work()
-        V, d = x.shape
-        agg = torch.empty_like(x)
-        part, stride = _partial(g, d, x.device)
-        ch, fx = wk["chunks"], wk["fixups"]
-        _lib.call("regcn_union_aggregate_f32", _lib.fptr(x), _lib.fptr(r), _lib.fptr(rel_emb.contiguous(), "rel_emb"),
-                  _lib.iptr(wk["col_src"]), _lib.iptr(wk["col_type"]), _lib.fptr(wk["norm"]), _lib.iptr(ch),
-                  ch.shape[0], _lib.iptr(fx), fx.shape[0], float(self.radius_msg_gamma), d, _lib.fptr(part), stride,
-                  _lib.fptr(agg), _lib.stream())
         prev_t = None
         if self.skip_connect and prev_h is not None:
             prev_t = tangent_of(prev_h, c)[0]
         wl = self.loop_weight if self.self_loop else None
         we = self.evolve_loop_weight if self.self_loop else None
-        h, xn, rn = layer_tail(agg, self.weight_neighbor, x, wl, we, prev_t,
-                               self.skip_weight if prev_t is not None else None,
-                               self.skip_bias if prev_t is not None else None,
-                               _drop_mask(self, x), g, c, euclid=False)
+        h, xn, rn = run_layer(_lib.AGG_UNION, g, x, r, rel_emb.contiguous(), None, 0, self.radius_msg_gamma,
+                              self.weight_neighbor, wl, we, prev_t,
+                              self.skip_weight if prev_t is not None else None,
+                              self.skip_bias.detach() if prev_t is not None else None,
+                              _drop_mask(self, x), c, step=step)
         return attach(h, xn, rn, c)
 
 
@@ -135,8 +211,8 @@ class LorentzRGCNLayer(nn.Module):
         self.dropout = nn.Dropout(dropout) if dropout > 0 else None
         self.rel_emb = None
 
-    def forward(self, g, h_hyper, rel_emb=None, prev_h=None):
-        """hyperbolic_layers.py:627-694."""
+    def forward(self, g, h_hyper, rel_emb=None, prev_h=None, step=None):
+        """hyperbolic_layers.py:627-694 (one fused launch; `step` fuses the timestep)."""
         if self.activation is None:
             raise NotImplementedError("the fused tail applies rrelu; activation=None is not supported")
         if self.submat_in * self.num_bases != self.in_feat:
@@ -144,27 +220,23 @@ class LorentzRGCNLayer(nn.Module):
             raise RuntimeError("in_feat=%d is not divisible by num_bases=%d" % (self.in_feat, self.num_bases))
         self.rel_emb = rel_emb
         c = float(self.c)
-        x, _ = tangent_of(h_hyper, c)
-        wk = g.work()
+        x, r = tangent_of(h_hyper, c)
         V, d = x.shape
-        rel = rel_emb[:, :d].contiguous() if rel_emb is not None else \
-            torch.zeros(self.num_rels, d, device=x.device, dtype=torch.float32)
-        agg = torch.empty_like(x)
-        part, stride = _partial(g, d, x.device, lorentz=True)
-        ch, fx = wk["chunks"], wk["fixups"]
-        _lib.call("regcn_lorentz_aggregate_f32", _lib.fptr(x), _lib.fptr(rel, "rel_emb"),
-                  _lib.fptr(self.weight.contiguous(), "weight"), _lib.iptr(wk["col_src"]), _lib.iptr(wk["col_type"]),
-                  _lib.iptr(ch), ch.shape[0], _lib.iptr(fx), fx.shape[0], self.num_bases, c, d, _lib.fptr(part),
-                  stride, _lib.fptr(agg), _lib.stream())
+        if rel_emb is None:
+            rel = torch.zeros(self.num_rels, d, device=x.device, dtype=torch.float32)
+        else:
+            rel = rel_emb if rel_emb.shape[1] == d else rel_emb[:, :d]
+            rel = rel.contiguous()
         prev_t = None
         if self.skip_connect and prev_h is not None:
             prev_t = tangent_of(prev_h, c)[0]
         wl = self.loop_weight if self.self_loop else None
         we = self.evolve_loop_weight if self.self_loop else None
-        h, xn, rn = layer_tail(agg, None, x, wl, we, prev_t,
-                               self.skip_weight if prev_t is not None else None,
-                               self.skip_bias if prev_t is not None else None,
-                               _drop_mask(self, x), g, c, euclid=False)
+        h, xn, rn = run_layer(_lib.AGG_LORENTZ, g, x, r, rel, self.weight.detach().contiguous(), self.num_bases, 0.0,
+                              None, wl, we, prev_t,
+                              self.skip_weight if prev_t is not None else None,
+                              self.skip_bias.detach() if prev_t is not None else None,
+                              _drop_mask(self, x), c, step=step)
         return attach(h, xn, rn, c)
 
 
@@ -182,12 +254,15 @@ class LorentzRGCNCell(nn.Module):
             self.layers.append(LorentzRGCNLayer(h_dim, h_dim, num_rels, num_bases, c=c, activation=F.rrelu,
                                                 self_loop=self_loop, dropout=dropout, skip_connect=sc))
 
-    def forward(self, g, init_ent_emb, init_rel_emb):
+    def forward(self, g, init_ent_emb, init_rel_emb, step=None):
+        """`step` (StepSpec): run the timestep fused into the last layer's launch and
+        return its output instead of the cell output."""
         h = init_ent_emb  # node ids are arange(V) (rgcn/utils.py:122): the gather is the identity
         rel_embs = init_rel_emb if isinstance(init_rel_emb, list) else [init_rel_emb] * len(self.layers)
         prev_h = None
+        n = len(self.layers)
         for i, layer in enumerate(self.layers):
-            h_new = layer(g, h, rel_embs[i], prev_h=prev_h)
+            h_new = layer(g, h, rel_embs[i], prev_h=prev_h, step=step if i == n - 1 else None)
             prev_h = h
             h = h_new
         return h

@@ -5,10 +5,9 @@ signatures `forward(g_list, static_graph, use_cuda)` -> (history_embs, static_em
 gate_list, degree_list), `predict(...)` and `get_loss(...)`.
 
 Per timestep (hyperbolic_model.py:797-884) the path is:
-  relation context mean        regcn_segment_mean_f32     (HIP)
-  relation GRU + normalize     torch.nn.GRUCell           (R2 x 2d -> d, host GEMM)
-  encoder cell (L layers)      prologue/aggregate/layer-tail kernels (HIP)
-  project/LN/time gate/radius  regcn_timestep_f32         (HIP, MFMA gate GEMM + fused epilogue)
+  relation context mean + GRU  regcn_relation_gru_f32     (one launch, MFMA)
+  encoder cell (L layers)      regcn_layer_f32            (one launch per layer: gather + MFMA tail)
+  project/LN/time gate/radius  fused into the last layer's launch (regcn_layer_f32 fuse_step)
 The initial entity state is one fused row kernel (regcn_init_entities_f32).
 
 Scope: eval/forward.  Static graph (--add-static-graph), EST components, FHNN/HGAT
@@ -24,7 +23,7 @@ import torch.nn.functional as F
 from . import _lib
 from .hyperbolic_decoder import (HyperbolicAttH, HyperbolicAttHRel, HyperbolicConvTransE, HyperbolicConvTransR,
                                  HyperbolicMuRP, HyperbolicMuRPRel, HyperbolicRotH, HyperbolicRotHRel)
-from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell
+from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell, StepSpec
 from .hyperbolic_ops import HyperbolicOps, TemporalRadiusEvolution
 from .tangent import attach, tangent_of
 from .weights import packed
@@ -60,11 +59,14 @@ class HyperbolicRGCNCell(HyperbolicBaseRGCN):
                                         activation=F.rrelu, self_loop=self.self_loop, dropout=self.dropout,
                                         skip_connect=sc, radius_msg_gamma=self.radius_msg_gamma)
 
-    def forward(self, g, init_ent_emb, init_rel_emb):
+    def forward(self, g, init_ent_emb, init_rel_emb, step=None):
+        """`step` (StepSpec): the timestep runs fused into the last layer's launch."""
         h = init_ent_emb  # node ids are arange(V): the reference gather is the identity
         rel_embs = init_rel_emb if isinstance(init_rel_emb, list) else [init_rel_emb] * len(self.layers)
+        n = len(self.layers)
         for i, layer in enumerate(self.layers):
-            h = layer(g, h, rel_embs[i])  # prev_h is never passed (hyperbolic_model.py:152)
+            # prev_h is never passed (hyperbolic_model.py:152)
+            h = layer(g, h, rel_embs[i], step=step if i == n - 1 else None)
         return h
 
 
@@ -78,6 +80,30 @@ def relation_context(x, g, num_rels2):
     _lib.call("regcn_segment_mean_f32", _lib.fptr(x, "x"), _lib.iptr(wk["rel_idx"]), _lib.fptr(wk["rel_count"]),
               _lib.iptr(ch), ch.shape[0], _lib.iptr(fx), fx.shape[0], d, _lib.fptr(part), d, _lib.fptr(out),
               _lib.stream())
+    return out
+
+
+REL_INLINE_MAX_SPAN = 64  # longer r_to_e spans are averaged by the chunked segment-mean kernel first
+
+
+def relation_gru_step(gru, emb_rel, x, g, h_prev):
+    """h_0' = GRUCell([emb_rel | mean_{r_to_e} x], h_prev) in one launch
+    (regcn_relation_gru_f32; hyperbolic_model.py:797-818, src/rrgcn.py:161-174)."""
+    from .weights import packed_linear
+    wk = g.work()
+    R2, d = emb_rel.shape
+    x_mean = relation_context(x, g, R2) if g.rel_max_span > REL_INLINE_MAX_SPAN else None
+    zeros = None
+    if gru.bias_ih is None:
+        zeros = torch.zeros(3 * d, device=emb_rel.device, dtype=torch.float32)
+    b_ih = gru.bias_ih.detach() if gru.bias_ih is not None else zeros
+    b_hh = gru.bias_hh.detach() if gru.bias_hh is not None else zeros
+    out = torch.empty(R2, d, device=emb_rel.device, dtype=torch.float32)
+    f = _lib.fptr
+    _lib.call("regcn_relation_gru_f32", f(x, "x"), _lib.iptr(wk["rel_idx"]) if wk["rel_idx"].numel() else None,
+              _lib.iptr(wk["rel_start"]), f(wk["rel_count"]), f(x_mean), f(emb_rel.detach(), "emb_rel"),
+              f(h_prev.detach().contiguous(), "h_0"), f(packed_linear(gru.weight_ih, 3)),
+              f(packed_linear(gru.weight_hh, 3)), f(b_ih), f(b_hh), R2, d, f(out), _lib.stream())
     return out
 
 
@@ -216,8 +242,16 @@ class HyperbolicRecurrentRGCN(nn.Module):
         """hyperbolic_model.py:715-720."""
         if c_val is None:
             c_val = self._c_float()
-        radius = torch.clamp(self.radius_static, min=self.radius_min, max=self.radius_max)
-        return torch.clamp(radius, max=1.0 / math.sqrt(c_val) - 1e-6)
+        p = self.radius_static
+        key = (p.data_ptr(), p._version, float(c_val), self.radius_min, self.radius_max)
+        hit = getattr(self, "_r_static_cache", None)
+        if hit is not None and hit[0] == key and not torch.is_grad_enabled():
+            return hit[1]  # parameter-only value: computed once per parameter version
+        radius = torch.clamp(p, min=self.radius_min, max=self.radius_max)
+        radius = torch.clamp(radius, max=1.0 / math.sqrt(c_val) - 1e-6)
+        if not torch.is_grad_enabled():
+            self._r_static_cache = (key, radius.detach().contiguous())
+        return radius
 
     def _guard_autograd(self):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
@@ -251,20 +285,25 @@ class HyperbolicRecurrentRGCN(nn.Module):
         for i, g in enumerate(g_list):
             g = g.to(dev)
             x_prev, _ = tangent_of(self.h, c_val)
-            x_input = relation_context(x_prev, g, R2)
-            x_input = torch.cat((self.emb_rel, x_input), dim=1)
-            self.h_0 = self.relation_gru(x_input, self.emb_rel if i == 0 else self.h_0)
+            self.h_0 = relation_gru_step(self.relation_gru, self.emb_rel, x_prev, g,
+                                         self.emb_rel if i == 0 else self.h_0)
             self.h_0 = F.normalize(self.h_0) if self.layer_norm else self.h_0
-            current_h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0])
-            h_new = torch.empty_like(x_prev)
-            x_new = torch.empty_like(x_prev)
-            r_new = torch.empty(V, device=dev, dtype=torch.float32)
-            _lib.call("regcn_timestep_f32", _lib.fptr(current_h.contiguous(), "current_h"), _lib.fptr(x_prev),
-                      _lib.fptr(wg), _lib.fptr(bg), _lib.fptr(r_static), _lib.fptr(w_r), _lib.fptr(b_r),
-                      float(trev.epsilon), float(trev.anchor_beta), int(bool(self.layer_norm)),
-                      int(bool(self.use_residual_evolution)), V, d, c_val, float(trev.c), _lib.fptr(h_new),
-                      _lib.fptr(x_new), _lib.fptr(r_new), _lib.stream())
-            self.h = attach(h_new, x_new, r_new, c_val)
+            if len(self.rgcn.layers) and not self.run_analysis:
+                # cell + timestep: the last layer's launch runs the timestep on its output
+                step = StepSpec(x_prev, wg, bg, r_static, w_r, b_r, trev.epsilon, trev.anchor_beta,
+                                self.layer_norm, self.use_residual_evolution, trev.c)
+                self.h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0], step=step)
+            else:
+                current_h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0])
+                h_new = torch.empty_like(x_prev)
+                x_new = torch.empty_like(x_prev)
+                r_new = torch.empty(V, device=dev, dtype=torch.float32)
+                _lib.call("regcn_timestep_f32", _lib.fptr(current_h.contiguous(), "current_h"), _lib.fptr(x_prev),
+                          _lib.fptr(wg), _lib.fptr(bg), _lib.fptr(r_static), _lib.fptr(w_r), _lib.fptr(b_r),
+                          float(trev.epsilon), float(trev.anchor_beta), int(bool(self.layer_norm)),
+                          int(bool(self.use_residual_evolution)), V, d, c_val, float(trev.c), _lib.fptr(h_new),
+                          _lib.fptr(x_new), _lib.fptr(r_new), _lib.stream())
+                self.h = attach(h_new, x_new, r_new, c_val)
             history_embs.append(self.h)
         return history_embs, None, self.h_0, [], []
 

@@ -2,8 +2,8 @@
 
 `UnionRGCNLayer.forward(g, prev_h, emb_rel)` reads g.ndata['h'], writes the new node
 representation back to g.ndata['h'] and returns it, as the reference does (:222-255).
-Two kernels: the CSR gather-sum of (h_src + rel[type]) (regcn_euclid_aggregate_f32)
-and the MFMA tail leaky(agg @ W_n + h @ W_loop|W_evolve) (regcn_layer_tail_f32).
+One fused launch (regcn_layer_f32, AGG_EUCLID): the CSR gather-sum of (h_src + rel[type])
+and the MFMA tail leaky(agg @ W_n + h @ W_loop|W_evolve).
 Unlike the reference, it runs without CUDA (`.cuda()` at :230 is not needed).
 """
 import torch
@@ -11,7 +11,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
-from .hyperbolic_layers import _drop_mask, _partial, layer_tail
+from .hyperbolic_layers import _drop_mask, run_layer
 
 
 class UnionRGCNLayer(nn.Module):
@@ -44,20 +44,13 @@ class UnionRGCNLayer(nn.Module):
             raise NotImplementedError("the fused tail applies rrelu; activation=None is not supported")
         self.rel_emb = emb_rel
         h = g.ndata["h"].contiguous()
-        wk = g.work()
-        V, d = h.shape
-        agg = torch.empty_like(h)
-        part, stride = _partial(g, d, h.device)
-        ch, fx = wk["chunks"], wk["fixups"]
-        _lib.call("regcn_euclid_aggregate_f32", _lib.fptr(h, "h"), _lib.fptr(emb_rel.contiguous(), "emb_rel"),
-                  _lib.iptr(wk["col_src"]), _lib.iptr(wk["col_type"]), _lib.fptr(wk["norm"]), _lib.iptr(ch),
-                  ch.shape[0], _lib.iptr(fx), fx.shape[0], d, _lib.fptr(part), stride, _lib.fptr(agg),
-                  _lib.stream())
         skip = len(prev_h) != 0 and self.skip_connect
-        out, _, _ = layer_tail(agg, self.weight_neighbor, h, self.loop_weight if self.self_loop else None,
-                               self.evolve_loop_weight if self.self_loop else None,
-                               prev_h.contiguous() if skip else None,
-                               self.skip_connect_weight if skip else None,
-                               self.skip_connect_bias if skip else None, _drop_mask(self, h), g, 0.01, euclid=True)
+        out, _, _ = run_layer(_lib.AGG_EUCLID, g, h, None, emb_rel.contiguous(), None, 0, 0.0, self.weight_neighbor,
+                              self.loop_weight if self.self_loop else None,
+                              self.evolve_loop_weight if self.self_loop else None,
+                              prev_h.contiguous() if skip else None,
+                              self.skip_connect_weight if skip else None,
+                              self.skip_connect_bias.detach() if skip else None, _drop_mask(self, h), 0.01,
+                              euclid=True)
         g.ndata["h"] = out
         return out

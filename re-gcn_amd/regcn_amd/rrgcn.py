@@ -12,7 +12,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.nn.parameter import Parameter
 
-from .hyperbolic_model import relation_context
+from .hyperbolic_model import relation_gru_step
 from .layers import UnionRGCNLayer
 
 
@@ -161,8 +161,8 @@ class RecurrentRGCN(nn.Module):
         R2 = self.num_rels * 2
         for i, g in enumerate(g_list):
             g = g.to(dev)
-            x_input = torch.cat((self.emb_rel, relation_context(self.h, g, R2)), dim=1)
-            self.h_0 = self.relation_cell_1(x_input, self.emb_rel if i == 0 else self.h_0)
+            self.h_0 = relation_gru_step(self.relation_cell_1, self.emb_rel, self.h, g,
+                                         self.emb_rel if i == 0 else self.h_0)
             self.h_0 = F.normalize(self.h_0) if self.layer_norm else self.h_0
             current_h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0])
             current_h = F.normalize(current_h) if self.layer_norm else current_h

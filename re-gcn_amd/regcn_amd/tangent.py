@@ -8,19 +8,27 @@ re-reading h: the reference recomputes log0(h) at every consumer
 by the curvature it was computed with and by the tensor's version counter, so an
 in-place edit of h invalidates it.
 """
+import struct
+
 import torch
 
 from . import _lib
 
 
+def _c32(c):
+    """The curvature as the kernels see it (an fp32 argument): 0.01 and the fp32 buffer
+    value 0.00999999977648 are the same key."""
+    return struct.unpack("f", struct.pack("f", float(c)))[0]
+
+
 def attach(h, x, r, c):
-    h._regcn_xr = (x, r, float(c), h._version)
+    h._regcn_xr = (x, r, _c32(c), h._version)
     return h
 
 
 def tangent_of(h, c):
     """(log0(h), max(|h|, eps)) for fp32 HIP rows h, from the cache or one prologue kernel."""
-    c = float(c)
+    c = _c32(c)
     cached = getattr(h, "_regcn_xr", None)
     if cached is not None and cached[2] == c and cached[3] == h._version:
         return cached[0], cached[1]

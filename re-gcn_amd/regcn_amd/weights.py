@@ -24,3 +24,35 @@ def packed(w):
     _lib.call("regcn_pack_weight_f32", _lib.fptr(wc, "weight"), d_in, d_out, _lib.fptr(out), _lib.stream())
     w._regcn_packed = (key, out)
     return out
+
+
+def packed_linear(w, n_gates=1):
+    """Per-16-column-tile packing of an nn.Linear-layout weight ((n_gates*n_out) x n_in,
+    regcn_pack_linear_f32), cached like `packed`."""
+    key = (w.data_ptr(), w._version, tuple(w.shape), n_gates)
+    hit = getattr(w, "_regcn_packed_lin", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    rows, n_in = w.shape
+    n_out = rows // n_gates
+    wc = w.detach().contiguous()
+    out = torch.empty(_lib.lib().regcn_packed_linear_floats(n_gates, n_out, n_in), device=w.device,
+                      dtype=torch.float32)
+    _lib.call("regcn_pack_linear_f32", _lib.fptr(wc, "weight"), n_gates, n_out, n_in, _lib.fptr(out), _lib.stream())
+    w._regcn_packed_lin = (key, out)
+    return out
+
+
+def packed_t(w):
+    """`packed` of the transpose of an nn.Linear weight (out x in): the B operand of
+    x @ W^T, cached on the weight itself."""
+    key = (w.data_ptr(), w._version, tuple(w.shape))
+    hit = getattr(w, "_regcn_packed_t", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    n_out, n_in = w.shape
+    wt = w.detach().t().contiguous()
+    out = torch.empty(_lib.lib().regcn_packed_weight_floats(n_in), device=w.device, dtype=torch.float32)
+    _lib.call("regcn_pack_weight_f32", _lib.fptr(wt, "weight"), n_in, n_out, _lib.fptr(out), _lib.stream())
+    w._regcn_packed_t = (key, out, wt)  # keep wt alive until the packing kernel has run
+    return out

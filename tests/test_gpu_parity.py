@@ -56,16 +56,21 @@ def test_row_ops_any_width_vs_oracle(d):
     assert_close(H.layer_norm_roundtrip(x.to(DEV), C), O.exp0(torch.nn.functional.normalize(O.log0(x, C)), C))
 
 
-def _graph(z, prefix="", chunk=512):
+def _graph(z, prefix="", chunk=512, budget=None):
+    """budget=1 sends every row with 2+ in-edges through the chunked pre-aggregation
+    (and, with a small chunk, its fix-up pass) instead of the fused kernel's inline gather."""
     from regcn_amd import graph as G
     V, R = int(z[prefix + "meta"][0]), int(z[prefix + "meta"][1])
-    return G.build_sub_graph(V, R, z[prefix + "triples"], True, DEV, chunk_edges=chunk)
+    g = G.build_sub_graph(V, R, z[prefix + "triples"], True, DEV, chunk_edges=chunk, tile_budget=budget)
+    if budget == 1:
+        assert g.n_heavy > 0
+    return g
 
 
 @pytest.mark.parametrize("gamma,gname", [(0.0, "g0"), (0.15, "g15")])
 @pytest.mark.parametrize("skip", [False, True])
-@pytest.mark.parametrize("chunk", [512, 3])
-def test_union_layer_vs_golden(golden, gamma, gname, skip, chunk):
+@pytest.mark.parametrize("chunk,budget", [(512, None), (3, 1), (512, 1)])
+def test_union_layer_vs_golden(golden, gamma, gname, skip, chunk, budget):
     import torch.nn.functional as F
     from regcn_amd.hyperbolic_layers import HyperbolicUnionRGCNLayer
     z = golden("layer_union.npz")
@@ -74,14 +79,14 @@ def test_union_layer_vs_golden(golden, gamma, gname, skip, chunk):
                                    skip_connect=skip, radius_msg_gamma=gamma)
     lay.load_state_dict({k: torch.from_numpy(z["w_" + k]) for k in lay.state_dict()})
     lay = lay.to(DEV).eval()
-    g = _graph(z, chunk=chunk)
+    g = _graph(z, chunk=chunk, budget=budget)
     with torch.no_grad():
         y = lay(g, t(z["h"]), t(z["rel"]), prev_h=t(z["prev_h"]) if skip else None)
     assert_close(y, z["%s_%s_out" % (gname, "skip" if skip else "noskip")], what="union layer")
 
 
-@pytest.mark.parametrize("chunk", [512, 2])
-def test_euclid_layer_vs_golden(golden, chunk):
+@pytest.mark.parametrize("chunk,budget", [(512, None), (2, 1)])
+def test_euclid_layer_vs_golden(golden, chunk, budget):
     import torch.nn.functional as F
     from regcn_amd.layers import UnionRGCNLayer
     z = golden("layer_euclid.npz")
@@ -89,7 +94,7 @@ def test_euclid_layer_vs_golden(golden, chunk):
     lay = UnionRGCNLayer(d, d, 2 * R, -1, activation=F.rrelu, self_loop=True, dropout=0.2)
     lay.load_state_dict({k: torch.from_numpy(z["w_" + k]) for k in lay.state_dict()})
     lay = lay.to(DEV).eval()
-    g = _graph(z, chunk=chunk)
+    g = _graph(z, chunk=chunk, budget=budget)
     g.ndata["h"] = t(z["h"])
     with torch.no_grad():
         y = lay(g, [], t(z["rel"]))
@@ -97,8 +102,8 @@ def test_euclid_layer_vs_golden(golden, chunk):
 
 
 @pytest.mark.parametrize("tag,skip", [("s2", False), ("s2", True), ("s4", False), ("s1", False), ("s20", False)])
-@pytest.mark.parametrize("chunk", [512, 5])
-def test_lorentz_layer_vs_golden(golden, tag, skip, chunk):
+@pytest.mark.parametrize("chunk,budget", [(512, None), (5, 1), (512, 3)])
+def test_lorentz_layer_vs_golden(golden, tag, skip, chunk, budget):
     import torch.nn.functional as F
     from regcn_amd.hyperbolic_layers import LorentzRGCNLayer
     z = golden("layer_lorentz.npz")
@@ -108,7 +113,7 @@ def test_lorentz_layer_vs_golden(golden, tag, skip, chunk):
     sd = {k: torch.from_numpy(z[tag + "_w_" + k]) for k in lay.state_dict()}
     lay.load_state_dict(sd)
     lay = lay.to(DEV).eval()
-    g = _graph(z, tag + "_", chunk=chunk)
+    g = _graph(z, tag + "_", chunk=chunk, budget=budget)
     with torch.no_grad():
         y = lay(g, t(z[tag + "_h"]), t(z[tag + "_rel"]), prev_h=t(z[tag + "_prev_h"]) if skip else None)
     assert_close(y, z[tag + ("_skip" if skip else "_noskip") + "_out"], what="lorentz layer")
@@ -188,3 +193,94 @@ def test_score_shapes_vs_oracle(B, N, d):
     q = O.exp0(torch.randn(B, d, generator=g), C)
     e = O.exp0(torch.randn(N, d, generator=g), C)
     assert_close(sc(q.to(DEV), e.to(DEV), None, C, 128, 256), OM.dist_score(q, e, None, C), what="score")
+
+
+def _zipf_snapshot(V, R, T, seed):
+    rng = np.random.default_rng(seed)
+    p = 1.0 / np.arange(1, V + 1) ** 1.1
+    p /= p.sum()
+    perm = rng.permutation(V)
+    return np.stack([perm[rng.choice(V, T, p=p)], rng.integers(0, R, T), perm[rng.choice(V, T, p=p)]], 1)
+
+
+@pytest.mark.parametrize("kind", ["union", "lorentz", "euclid"])
+def test_layers_with_hubs_vs_oracle(kind):
+    """Zipf snapshot with hubs over the tile budget (pre-aggregated + fixups) next to
+    inline-gathered rows, at d = 200 / num_bases = 100 (the bench shape)."""
+    import torch.nn.functional as F
+    from oracle import graph as OG
+    from oracle import layers as OL
+    from oracle import ops as O
+    from regcn_amd import graph as G
+    from regcn_amd.hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNLayer
+    from regcn_amd.layers import UnionRGCNLayer
+    V, R, T, d = 3000, 60, 20000, 200  # 2R >= num_bases = 100 (else the reference clamps num_bases)
+    tr = _zipf_snapshot(V, R, T, 7)
+    g = G.build_sub_graph(V, R, tr, True, DEV)
+    assert g.n_heavy > 0 and g.heavy_slots > 0
+    og = OG.build_sub_graph(V, R, tr)
+    gen = torch.Generator().manual_seed(3)
+    h = O.exp0(torch.randn(V, d, generator=gen) * 0.5, C)
+    rel = torch.randn(2 * R, d, generator=gen) * 0.1
+    torch.manual_seed(0)
+    if kind == "union":
+        lay = HyperbolicUnionRGCNLayer(d, d, 2 * R, -1, c=C, activation=F.rrelu, self_loop=True, dropout=0.2,
+                                       radius_msg_gamma=0.15).eval()
+        ref = OL.union_layer(og, h, rel, lay.weight_neighbor.detach(), lay.loop_weight.detach(),
+                             lay.evolve_loop_weight.detach(), C, 0.15)
+        with torch.no_grad():
+            y = lay.to(DEV)(g, h.to(DEV), rel.to(DEV))
+    elif kind == "lorentz":
+        lay = LorentzRGCNLayer(d, d, 2 * R, 100, c=C, activation=F.rrelu, self_loop=True, dropout=0.2).eval()
+        ref = OL.lorentz_layer(og, h, rel, lay.weight.detach(), lay.loop_weight.detach(),
+                               lay.evolve_loop_weight.detach(), C, 100)
+        with torch.no_grad():
+            y = lay.to(DEV)(g, h.to(DEV), rel.to(DEV))
+    else:
+        lay = UnionRGCNLayer(d, d, 2 * R, -1, activation=F.rrelu, self_loop=True, dropout=0.2).eval()
+        hx = torch.randn(V, d, generator=gen) * 0.1
+        ref = OL.euclid_union_layer(og, hx, rel, lay.weight_neighbor.detach(), lay.loop_weight.detach(),
+                                    lay.evolve_loop_weight.detach())
+        g.ndata["h"] = hx.to(DEV)
+        with torch.no_grad():
+            y = lay.to(DEV)(g, [], rel.to(DEV))
+    assert_close(y, ref, what=kind + " layer with hubs")
+
+
+@pytest.mark.parametrize("tag", ["lgcn_roth_bias_crel", "uvrgcn_roth", "lgcn_roth"])
+def test_predict_is_deterministic(golden, tag):
+    """Bitwise-identical reruns (no atomics, no uninitialised reads): the fused kernels
+    combine partial sums in a fixed order."""
+    z = golden("model_%s.npz" % tag)
+    m, glist, (V, R, d, T) = build_hyperbolic_model(z, tag, DEV)
+    test = torch.from_numpy(z["test"]).to(DEV)
+    with torch.no_grad():
+        runs = [m.predict(glist, R, None, test, True) for _ in range(3)]
+    for _, s, sr in runs:
+        assert torch.isfinite(s).all() and torch.isfinite(sr).all()
+        assert torch.equal(s, runs[0][1]) and torch.equal(sr, runs[0][2])
+
+
+@pytest.mark.parametrize("tag", ["uvrgcn_roth", "lgcn_roth"])
+def test_roth_query_kernel_matches_torch_sequence(golden, tag):
+    """regcn_roth_query_f32 / regcn_roth_rel_query_f32 against the same decoders run op by
+    op on torch (hyperbolic_decoder.py:1065-1085, :1223-1243)."""
+    from regcn_amd.hyperbolic_decoder import _RelDecoderBase
+    z = golden("model_%s.npz" % tag)
+    m, glist, (V, R, d, T) = build_hyperbolic_model(z, tag, DEV)
+    test = torch.from_numpy(z["test"]).to(DEV)
+    with torch.no_grad():
+        emb_l, _, r_emb, _, _ = m.forward(glist, None, True)
+        emb = emb_l[-1]
+        inv = test.flip(1)
+        inv[:, 1] += R
+        at = torch.cat([test, inv])
+        dec, rdec = m.decoder_ob, m.rdecoder
+        q = dec._query(emb, r_emb, at)
+        s_rel = rdec.forward(emb, r_emb, at)
+        dec._torch_query = True
+        q_t = dec._query(emb, r_emb, at)
+        dec._torch_query = False
+        s_rel_t = _RelDecoderBase.forward(rdec, emb, r_emb, at)
+    assert_close(q, q_t, what="RotH query")
+    assert_close(s_rel, s_rel_t, what="RotHRel scores")

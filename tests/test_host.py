@@ -96,6 +96,42 @@ def test_work_lists_cover_every_edge_once(chunk):
     assert (cov == 1).all()
 
 
+@pytest.mark.parametrize("V,T", [(200, 1500), (50, 40), (3000, 70000)])
+def test_fused_layer_tiles(V, T):
+    """Tiles of the fused layer kernel (csrc/layer.hip): each positive row in exactly one
+    tile, <= 16 rows, inline edges within budget (a lone row may exceed only if heavy),
+    heavy rows pre-aggregated by chunks covering exactly their CSR spans."""
+    rng = np.random.default_rng(V)
+    p = 1.0 / np.arange(1, V + 1) ** 1.3
+    p /= p.sum()
+    tr = np.stack([rng.choice(V, T, p=p), rng.integers(0, 9, T), rng.choice(V, T, p=p)], 1)
+    g = G.build_sub_graph(V, 9, tr, False, 0)
+    h = g._host
+    deg = g.in_deg_np
+    rows = h["rows"]
+    np.testing.assert_array_equal(h["rowptr"], np.concatenate([[0], np.cumsum(deg)]))
+    assert (np.diff(deg[rows[:g.n_pos]]) <= 0).all()  # in-degree descending
+    tiles = h["tiles"]
+    assert len(tiles) == g.n_pos_tiles
+    assert tiles[0, 0] == 0 and (tiles[1:, 0] == tiles[:-1, 0] + tiles[:-1, 1]).all()
+    assert tiles[-1, 0] + tiles[-1, 1] == g.n_pos
+    assert ((tiles[:, 1] >= 1) & (tiles[:, 1] <= 16)).all()
+    heavy = set()
+    for s, c in tiles:
+        d = deg[rows[s:s + c]]
+        inl = np.where(d > g.budget, 0, d)
+        assert inl.sum() <= g.budget
+        heavy.update(rows[s:s + c][d > g.budget].tolist())
+    assert len(heavy) == g.n_heavy
+    cov = np.zeros(len(h["col_src"]), dtype=np.int64)
+    for row, b, e, s in h["heavy_chunks"]:
+        assert row in heavy and h["rowptr"][row] <= b < e <= h["rowptr"][row + 1]
+        cov[b:e] += 1
+    for row in heavy:
+        assert (cov[h["rowptr"][row]:h["rowptr"][row + 1]] == 1).all()
+    assert cov.sum() == sum(deg[r] for r in heavy)
+
+
 def test_empty_snapshot():
     g = G.build_sub_graph(10, 3, np.zeros((0, 3), dtype=np.int64), False, 0)
     assert g.number_of_edges() == 0 and g.n_pos == 0
