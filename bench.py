@@ -103,87 +103,99 @@ def event_time(fn, reps, stream, replays=5):
     return s.elapsed_time(e) / (reps * replays)
 
 
+def pmc_traffic(kernel, config, d):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this same bench
+    command (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes).  (None, reason) if absent."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, "no profiles/pmc_traffic.json"
+    with open(path) as f:
+        pm = json.load(f)
+    if pm.get("config") != config or int(pm.get("d", -1)) != d:
+        return None, "pmc_traffic.json is for another workload"
+    k = pm["kernels"].get(kernel.split(" ")[0] if kernel.startswith("k_query<1>") else kernel)
+    if k is None:
+        return None, "kernel not in pmc_traffic.json"
+    return k["hbm_bytes"], "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, %d launches)" % \
+        k["launches"]
+
+
+def _work(flops, nbytes, ms):
+    """Roofline bound of a launch: whichever of its MFMA flops / HBM bytes takes longer at
+    peak.  Returns dict(bound, unit, work, achieved, frac)."""
+    t_mfma = flops / (FP32_MFMA_PEAK_TFLOPS * 1e12)
+    t_hbm = nbytes / (HBM_PEAK_GBS * 1e9)
+    if t_mfma >= t_hbm:
+        ach = flops / (ms * 1e-3) / 1e12
+        return dict(bound="mfma", unit="TFLOP/s", work=flops, achieved=ach, peak=FP32_MFMA_PEAK_TFLOPS,
+                    frac=ach / FP32_MFMA_PEAK_TFLOPS)
+    ach = nbytes / (ms * 1e-3) / 1e9
+    return dict(bound="hbm", unit="GB/s", work=nbytes, achieved=ach, peak=HBM_PEAK_GBS, frac=ach / HBM_PEAK_GBS)
+
+
 def kernel_profile(model, sample, d, device):
-    """Live HIP-event timing of each hot-path kernel on the bench workload (first history
-    snapshot of sample 0 for the per-layer kernels, the sample's queries for the scorer).
-    Returns {name: dict(ms, launches_per_step, work, unit, bound)}."""
-    from regcn_amd import _lib
+    """Live HIP-event timing of each launch of the hot path on the bench workload: every
+    stage of one timestep on the sample's last history snapshot, and the two decoders on
+    its queries.  Each stage is captured `reps` times into a HIP graph on its own stream and
+    replayed between HIP events on that stream.  Returns {kernel: dict(ms, per_step, ...)}."""
     from regcn_amd.hyperbolic_decoder import _chunked_hyperbolic_dist_score
+    from regcn_amd.hyperbolic_layers import StepSpec
+    from regcn_amd.hyperbolic_model import relation_gru_step
     from regcn_amd.tangent import tangent_of
+    from regcn_amd.weights import packed
     hist, glist, test, _ = sample
-    g = glist[0]
-    wk = g.work()
+    g = glist[-1]
     V = g.number_of_nodes()
+    E = g.number_of_edges()
     T = len(glist)
+    n_pos = g.n_pos
     st = torch.cuda.Stream(device)
     res = {}
+    c = model._c_float()
     with torch.no_grad(), torch.cuda.stream(st):
         embs, _, h0, _, _ = model.forward(glist, None, True)
-        h = embs[-1]
-        x, r = tangent_of(h, 0.01)
-        rel = h0.contiguous()
-        agg = torch.empty_like(x)
-        lay = model.rgcn.layers[0]
-        ch, fx = wk["chunks"], wk["fixups"]
-        E = g.number_of_edges()
-        n_rows = int(ch.shape[0])  # single-chunk rows written (no long rows at this size)
-        agg_bytes = E * (4 * d + 12) + n_rows * (4 * d + 12)
-        if model.encoder_name == "lgcn":
-            part = torch.empty(max(g.n_slots, 1), d + 4, device=device)
-            W = lay.weight.detach().contiguous()
-            name = "k_lorentz_sum"
-
-            def agg_fn():
-                _lib.call("regcn_lorentz_aggregate_f32", _lib.fptr(x), _lib.fptr(rel), _lib.fptr(W),
-                          _lib.iptr(wk["col_src"]), _lib.iptr(wk["col_type"]), _lib.iptr(ch), ch.shape[0],
-                          _lib.iptr(fx), fx.shape[0], lay.num_bases, 0.01, d, _lib.fptr(part), d + 4,
-                          _lib.fptr(agg), _lib.stream())
-        else:
-            part = torch.empty(max(g.n_slots, 1), d, device=device)
-            name = "k_gather_sum"
-
-            def agg_fn():
-                _lib.call("regcn_union_aggregate_f32", _lib.fptr(x), _lib.fptr(r), _lib.fptr(rel),
-                          _lib.iptr(wk["col_src"]), _lib.iptr(wk["col_type"]), _lib.fptr(wk["norm"]),
-                          _lib.iptr(ch), ch.shape[0], _lib.iptr(fx), fx.shape[0], 0.15, d, _lib.fptr(part), d,
-                          _lib.fptr(agg), _lib.stream())
-        res[name] = dict(ms=event_time(agg_fn, 200, st), launches_per_step=2 * T, work=agg_bytes, unit="GB/s",
-                         bound="hbm", what="E*(4d+12) + rows*(4d+12) bytes, E=%d, rows=%d" % (E, n_rows))
-        from regcn_amd.hyperbolic_layers import layer_tail
-        wl, we = lay.loop_weight.detach(), lay.evolve_loop_weight.detach()
-        wn = getattr(lay, "weight_neighbor", None)
-        wn = wn.detach() if wn is not None else None
-
-        def tail_fn():
-            layer_tail(agg, wn, x, wl, we, None, None, None, None, g, 0.01, False)
-        tail_flops = 2.0 * d * d * (V + (g.n_pos if wn is not None else 0))
-        res["k_layer_tail"] = dict(ms=event_time(tail_fn, 200, st), launches_per_step=2 * T, work=tail_flops,
-                                   unit="TFLOP/s", bound="mfma",
-                                   what="2*d*d*(V%s) flops" % (" + n_pos" if wn is not None else ""))
+        h = embs[-2] if len(embs) > 1 else embs[-1]
+        x, r = tangent_of(h, c)
+        lay0, lay1 = model.rgcn.layers[0], model.rgcn.layers[-1]
         trev = model.temporal_radius_evolution
-        from regcn_amd.weights import packed
-        wg, bg = packed(model.time_gate_weight), model.time_gate_bias.detach().contiguous()
-        w_r = trev.radius_mlp.weight.detach().reshape(-1).contiguous()
-        b_r = trev.radius_mlp.bias.detach().reshape(-1).contiguous()
-        rs = model._static_radius(0.01).contiguous()
-        hn, xn, rn = torch.empty_like(x), torch.empty_like(x), torch.empty_like(r)
-        hc = h.contiguous()
+        step = StepSpec(x, packed(model.time_gate_weight), model.time_gate_bias.detach(),
+                        model._static_radius(c), trev.radius_mlp.weight.detach().reshape(-1).contiguous(),
+                        trev.radius_mlp.bias.detach().reshape(-1).contiguous(), trev.epsilon, trev.anchor_beta,
+                        model.layer_norm, model.use_residual_evolution, trev.c)
+        h1 = lay0(g, h, h0)
+        lorentz = model.encoder_name == "lgcn"
+        tag = "3, %d" % (d // lay0.num_bases if d // lay0.num_bases in (1, 2, 4) else 0) if lorentz else "0, 1"
+        gather_b = E * (4 * d + 8 + (0 if lorentz else 4)) + V * 4 * 2
+        wn_flops = 0 if lorentz else 2.0 * d * d * n_pos
+        R2 = model.emb_rel.shape[0]
 
-        def step_fn():
-            _lib.call("regcn_timestep_f32", _lib.fptr(hc), _lib.fptr(x), _lib.fptr(wg), _lib.fptr(bg), _lib.fptr(rs),
-                      _lib.fptr(w_r), _lib.fptr(b_r), 0.1, 1.0, 0, 1, V, d, 0.01, 0.01, _lib.fptr(hn), _lib.fptr(xn),
-                      _lib.fptr(rn), _lib.stream())
-        res["k_timestep"] = dict(ms=event_time(step_fn, 200, st), launches_per_step=T, work=2.0 * d * d * V,
-                                 unit="TFLOP/s", bound="mfma", what="2*d*d*V flops")
-        B = 2 * test.shape[0]
-        q = torch.randn(B, d, device=device) * 0.05
-        cand = h.contiguous()
-        sc = torch.ones(1, device=device)
-
-        def score_fn():
-            _chunked_hyperbolic_dist_score(q, cand, None, 0.01, 128, 256, score_scale=sc, score_margin=sc)
-        res["k_score"] = dict(ms=event_time(score_fn, 200, st), launches_per_step=1, work=2.0 * B * V * d,
-                              unit="TFLOP/s", bound="mfma", what="2*B*N*d flops, B=%d, N=%d" % (B, V))
+        stages = [
+            ("k_rel_gru", lambda: relation_gru_step(model.relation_gru, model.emb_rel, x, g, h0), 1,
+             2.0 * R2 * 9 * d * d, 4.0 * R2 * d * 3 + 4.0 * 9 * d * d + 4.0 * R2 * d),
+            ("k_layer<%s, false>" % tag, lambda: lay0(g, h, h0), 1,
+             2.0 * d * d * V + wn_flops, gather_b + 4.0 * V * d + 4.0 * V * (2 * d + 1)),
+            ("k_layer<%s, true>" % tag, lambda: lay1(g, h1, h0, step=step), 1,
+             4.0 * d * d * V + wn_flops, gather_b + 8.0 * V * d + 4.0 * V * (2 * d + 2)),
+        ]
+        at = torch.cat([test, torch.stack([test[:, 2], test[:, 1] + model.num_rels, test[:, 0]], 1)])
+        B = at.shape[0]
+        emb = model._final_embedding(embs[-1], c)
+        dec, rdec = model.decoder_ob, model.rdecoder
+        q = dec._query(emb, h0, at)
+        if type(dec).__name__ == "HyperbolicRotH":
+            stages.append(("k_query<0>", lambda: dec._query(emb, h0, at), 1, 2.0 * B * 3.5 * d * d,
+                           4.0 * B * d * 3))
+        stages.append(("k_score<0, false>", lambda: _chunked_hyperbolic_dist_score(
+            q, emb, dec.entity_bias, dec.c, 128, 256, score_scale=dec.score_scale_raw,
+            score_margin=dec.score_margin, _raw_scale=True), 1, 2.0 * B * V * d, 4.0 * (B * d + V * d + B * V)))
+        if type(rdec).__name__ == "HyperbolicRotHRel":
+            stages.append(("k_query<1> + k_score (relations)", lambda: rdec.forward(emb, h0, at), 1,
+                           2.0 * B * 2 * d * d + 2.0 * B * R2 * d, 4.0 * (B * d * 3 + B * R2)))
+        for name, fn, per_layer_step, flops, nbytes in stages:
+            ms = event_time(fn, 100, st)
+            per_step = T if name.startswith(("k_rel_gru", "k_layer")) else 1
+            res[name] = dict(ms=ms, per_step=per_step, flops=flops, bytes=nbytes, **_work(flops, nbytes, ms))
     torch.cuda.synchronize()
     return res
 
@@ -292,19 +304,17 @@ def main():
     kern = kernel_profile(model, samples[0], d, device) if rank == 0 else {}
     out = None
     if rank == 0:
-        shares = {k: v["ms"] * v["launches_per_step"] for k, v in kern.items()}
+        shares = {k: v["ms"] * v["per_step"] for k, v in kern.items()}
         dom = max(shares, key=shares.get)
         kd = kern[dom]
-        if kd["unit"] == "GB/s":
-            ach, peak = kd["work"] / (kd["ms"] * 1e-3) / 1e9, HBM_PEAK_GBS
-        else:
-            ach, peak = kd["work"] / (kd["ms"] * 1e-3) / 1e12, FP32_MFMA_PEAK_TFLOPS
-        roof = dict(bound=kd["bound"], kernel=dom, achieved=round(ach, 3), peak=peak, unit=kd["unit"],
-                    frac=round(ach / peak, 4), traffic=None, work_per_launch=kd["what"],
+        traffic, tsrc = pmc_traffic(dom, args.config, d)
+        roof = dict(bound=kd["bound"], kernel=dom, achieved=round(kd["achieved"], 3), peak=kd["peak"],
+                    unit=kd["unit"], frac=round(kd["frac"], 4), traffic=traffic, traffic_source=tsrc,
+                    flops_per_launch=kd["flops"], algorithmic_bytes_per_launch=kd["bytes"],
                     avg_launch_us=round(kd["ms"] * 1e3, 3))
-        kernels = {k: dict(avg_us=round(v["ms"] * 1e3, 3), per_step=v["launches_per_step"],
-                           achieved=round(v["work"] / (v["ms"] * 1e-3) / (1e9 if v["unit"] == "GB/s" else 1e12), 3),
-                           unit=v["unit"]) for k, v in kern.items()}
+        kernels = {k: dict(avg_us=round(v["ms"] * 1e3, 3), per_step=v["per_step"], bound=v["bound"],
+                           achieved=round(v["achieved"], 3), unit=v["unit"], frac=round(v["frac"], 4))
+                   for k, v in kern.items()}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg, d, model, samples[0], args.cpu_budget)

@@ -130,7 +130,8 @@ int regcn_layer_tail_f32(const float* agg, const float* w_n, const float* x, con
 
 /* Destination tiles (graph.py): `tiles` int32[n_pos_tiles][2] = {start, count} over
  * rows[0, n_pos), each count <= 16; `rowptr` int32[V+1] is the destination-sorted CSR
- * whose col_src/col_type the gather reads.  Rows with in-degree > `budget` are not
+ * (in-degrees); the inline in-edges of tile t are items [item_ptr[t], item_ptr[t+1]),
+ * in CSR order per row, rows in tile order.  Rows with in-degree > `budget` are not
  * gathered inline: their finished aggregation must already be in `agg` (chunked
  * regcn_*_aggregate_f32 over those rows only).  All w_* matrices are packed
  * (regcn_pack_weight_f32).  With fuse_step != 0 the layer output is not stored: the
@@ -150,6 +151,9 @@ typedef struct regcn_layer_desc {
   int32_t budget;
   const int32_t* tiles;
   int32_t n_pos_tiles;
+  const int32_t* item_ptr;  /* n_pos_tiles + 1: tile t gathers items [item_ptr[t], item_ptr[t+1]) */
+  const int32_t* item_src;  /* per item: source entity */
+  const int32_t* item_tl;   /* per item: relation type << 4 | tile-local destination row */
   const float* agg;
   const float* w_n;
   const float* w_loop;
@@ -177,6 +181,8 @@ typedef struct regcn_layer_desc {
   float* step_h_out;
   float* step_x_out;
   float* step_r_out;
+  int64_t* trace;  /* optional: per-workgroup phase timestamps (s_memrealtime, 8 per
+                      workgroup) for profiling; NULL in production */
 } regcn_layer_desc;
 int regcn_layer_f32(const regcn_layer_desc* desc, void* stream);
 

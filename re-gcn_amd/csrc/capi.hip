@@ -165,6 +165,9 @@ int regcn_layer_f32(const regcn_layer_desc* g, void* s) {
   a.budget = g->budget;
   a.tiles = g->tiles;
   a.n_pos_tiles = g->n_pos_tiles;
+  a.item_ptr = g->item_ptr;
+  a.item_src = g->item_src;
+  a.item_tl = g->item_tl;
   a.agg = g->agg;
   a.w_n = g->w_n;
   a.w_loop = g->w_loop;
@@ -204,6 +207,7 @@ int regcn_layer_f32(const regcn_layer_desc* g, void* s) {
     t.x_out = g->step_x_out;
     t.r_out = g->step_r_out;
   }
+  a.trace = g->trace;
   return layer(a, ST(s));
 }
 

@@ -36,7 +36,7 @@ __host__ __device__ inline LdsLayout lds_layout(int d, bool gen_s) {
   L.X = NWAVE * TM * L.lda;
   L.red = L.X + TM * L.lda;
   L.ints = L.red + 2 * NWAVE * TM;
-  L.xsh = L.ints + 48;  // trow[16], toff[17], tmask[4] (+pad)
+  L.xsh = L.ints + 32;  // trow[16], tmask[4] (+pad)
   L.total_bytes = (L.xsh + (gen_s ? NWAVE * MAX_D : 0)) * 4;
   return L;
 }
@@ -127,24 +127,35 @@ __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, const float*
   }
 }
 
+// Profiling hook: wall-clock phase stamps (100 MHz) of wave 0, 16 slots per workgroup.
+__device__ __forceinline__ void trace_mark(const LayerArgs& p, int k) {
+  if (p.trace && threadIdx.x == 0) p.trace[blockIdx.x * 16 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+}
+
 // --------------------------------------------------------------------------- inline gather
-// Flattened, segmented gather of the tile's in-edges (see file header).  Wave w reduces
-// items [ib, ie); each row it touches gets one partial row in part[w][i] (+ the Lorentz
-// time coordinate at column d) and a bit in tmask[w].
+// Flattened, segmented gather of the tile's in-edges (see file header).  Items come from
+// the host-built per-tile list (item_src, item_tl = type << 4 | local row), so an edge's
+// row loads depend on one coalesced index load only.  Wave w reduces items [ib, ie), EB
+// edges in flight (all loads unconditional, clamped addresses); each row it touches gets
+// one partial row in part[w][i] (+ the Lorentz time coordinate at column d) and a bit in
+// tmask[w].
 template <int AGG, int S>
-__device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int lda, const int* trow,
-                                            const int* toff, int count, int* tmask, float* xsh) {
+__device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int lda, const int* trow, int tile,
+                                            int* tmask, float* xsh) {
+  constexpr int EB = (AGG == AGG_LORENTZ && (S == 4 || S == 0)) ? 4 : 8;
   const int lane = threadIdx.x & 63, w = wave_id();
-  const int col = lane * 4, d = p.d;
+  const int d = p.d;
+  const int col = lane * 4, colc = min(col, d - 4);
   const bool active = col < d;
-  const int n_items = toff[count];
-  const int ib = (n_items * w) / NWAVE, ie = (n_items * (w + 1)) / NWAVE;
+  const int i0 = p.item_ptr[tile], n_items = p.item_ptr[tile + 1] - i0;
+  const int ib = i0 + (n_items * w) / NWAVE, ie = i0 + (n_items * (w + 1)) / NWAVE;
   const int s_gen = (AGG == AGG_LORENTZ) ? d / p.nb : 1;
   const int wstride = (AGG == AGG_LORENTZ) ? p.nb * s_gen * s_gen : 0;
   const Curv k = p.k;
+  const f4 zero = {0.f, 0.f, 0.f, 0.f};
   int cur = -1;
   unsigned mask = 0;
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  f4 acc = zero;
   float acc0 = 0.f;
   auto flush = [&]() {
     if (cur >= 0) {
@@ -163,94 +174,105 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
     if (li != cur) {
       flush();
       cur = li;
-      acc = f4{0.f, 0.f, 0.f, 0.f};
+      acc = zero;
       acc0 = 0.f;
     }
   };
+  auto row4 = [&](const float* base, int row) {  // unconditional clamped row fragment
+    const f4 v = *reinterpret_cast<const f4*>(base + (int64_t)row * d + colc);
+    return active ? v : zero;
+  };
+  trace_mark(p, 8);
   for (int t0 = ib; t0 < ie; t0 += 64) {
     const int n = min(64, ie - t0);
-    int my_s = 0, my_t = 0, my_i = 0;
+    const int t = t0 + min(lane, n - 1);
+    const int my_s = p.item_src[t];
+    const int tl = p.item_tl[t];
+    const int my_t = tl >> 4, my_i = tl & 15;
     float my_w = 1.f;
-    if (lane < n) {
-      const int t = t0 + lane;
-      int i = 0;
-      while (i + 1 < count && toff[i + 1] <= t) ++i;
-      const int row = trow[i];
-      const int e = p.rowptr[row] + (t - toff[i]);
-      my_s = p.col_src[e];
-      my_t = p.col_type[e];
-      my_i = i;
-      if (AGG == AGG_UNION) my_w = expf(-p.gamma * fabsf(p.radius[my_s] - p.radius[row]));
+    if (AGG == AGG_UNION) my_w = expf(-p.gamma * fabsf(p.radius[my_s] - p.radius[trow[my_i]]));
+    if (t0 == ib) {
+      __builtin_amdgcn_s_waitcnt(0);
+      trace_mark(p, 9);
     }
     int j = 0;
     if constexpr (AGG == AGG_UNION || AGG == AGG_EUCLID) {
-      for (; j + 4 <= n; j += 4) {
-        f4 xs[4], rv[4];
+      for (; j + EB <= n; j += EB) {
+        f4 xs[EB], rv[EB];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          xs[u] = load4(p.x + (int64_t)rl(my_s, j + u) * d, col, d);
-          rv[u] = load4(p.rel + (int64_t)rl(my_t, j + u) * d, col, d);
+        for (int u = 0; u < EB; ++u) {
+          xs[u] = row4(p.x, rl(my_s, j + u));
+          rv[u] = row4(p.rel, rl(my_t, j + u));
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < EB; ++u) {
           take(rl(my_i, j + u));
           if (AGG == AGG_EUCLID) acc += xs[u] + rv[u];
           else acc += rlf(my_w, j + u) * (xs[u] + rv[u]);
         }
       }
       for (; j < n; ++j) {
-        f4 xs = load4(p.x + (int64_t)rl(my_s, j) * d, col, d);
-        f4 rv = load4(p.rel + (int64_t)rl(my_t, j) * d, col, d);
+        const f4 xs = row4(p.x, rl(my_s, j));
+        const f4 rv = row4(p.rel, rl(my_t, j));
         take(rl(my_i, j));
         if (AGG == AGG_EUCLID) acc += xs + rv;
         else acc += rlf(my_w, j) * (xs + rv);
       }
     } else if constexpr (AGG == AGG_LORENTZ) {
       if constexpr (S > 0) {
-        for (; j + 4 <= n; j += 4) {
-          f4 xs[4], rv[4], m[4];
-          WFrag<S> wf[4];
+        for (; j + EB <= n; j += EB) {
+          f4 xs[EB], rv[EB];
+          WFrag<S> wf[EB];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < EB; ++u) {
             const int src = rl(my_s, j + u), typ = rl(my_t, j + u);
-            xs[u] = load4(p.x + (int64_t)src * d, col, d);
-            rv[u] = load4(p.rel + (int64_t)typ * d, col, d);
-            if (active) wf[u].load(p.w_rel + (int64_t)typ * wstride, col);
+            xs[u] = row4(p.x, src);
+            rv[u] = row4(p.rel, typ);
+            wf[u].load(p.w_rel + (int64_t)typ * wstride, colc);
           }
-          float n2[4];
+          f4 m[EB];
+          float n2l = 0.f;  // lane u < EB holds |m_u|^2
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            m[u] = active ? wf[u].apply(xs[u]) + rv[u] : f4{0.f, 0.f, 0.f, 0.f};
-            n2[u] = row16_sum(dot4(m[u], m[u]));
+          for (int u = 0; u < EB; ++u) {
+            m[u] = active ? wf[u].apply(xs[u]) + rv[u] : zero;
+            const float q = row16_sum(dot4(m[u], m[u]));
+            const float tt = (rlane(q, 0) + rlane(q, 16)) + (rlane(q, 32) + rlane(q, 48));
+            n2l = lane == u ? tt : n2l;
           }
+          // the per-edge scalars of the Lorentz point, once per batch with lane = edge
+          float p2;
+          const float f = exp0_factor(n2l, k, &p2);
+          const float den = fmaxf(1.f - k.c * p2, REGCN_EPS);
+          const float a0 = (1.f + k.c * p2) / (k.sqrt_c * den);
+          const float sc = 2.f * f / den;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float t = (rlane(n2[u], 0) + rlane(n2[u], 16)) + (rlane(n2[u], 32) + rlane(n2[u], 48));
+          for (int u = 0; u < EB; ++u) {
             take(rl(my_i, j + u));
-            lorentz_accum(m[u], t, k, acc0, acc);
+            acc0 += rlane(a0, u);
+            acc += m[u] * rlane(sc, u);
           }
+          if (j == 0 && t0 == ib) trace_mark(p, 10);
         }
       }
       for (; j < n; ++j) {
         const int src = rl(my_s, j), typ = rl(my_t, j);
         const float* Wt = p.w_rel + (int64_t)typ * wstride;
-        f4 xs = load4(p.x + (int64_t)src * d, col, d);
-        f4 m = {0.f, 0.f, 0.f, 0.f};
+        const f4 xs = row4(p.x, src);
+        f4 m = zero;
         if constexpr (S > 0) {
-          if (active) {
-            WFrag<S> wf;
-            wf.load(Wt, col);
-            m = wf.apply(xs);
-          }
+          WFrag<S> wf;
+          wf.load(Wt, colc);
+          m = active ? wf.apply(xs) : zero;
         } else {
           m = block_general4(xsh + w * MAX_D, xs, Wt, s_gen, col, active);
         }
-        m += load4(p.rel + (int64_t)typ * d, col, d);
+        m += row4(p.rel, typ);
         take(rl(my_i, j));
         lorentz_accum(m, wave_sum(dot4(m, m)), k, acc0, acc);
       }
     }
   }
+  trace_mark(p, 11);
   flush();
   if (lane == 0) tmask[w] = (int)mask;
 }
@@ -262,31 +284,69 @@ template <int AGG>
 __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int lda, const int* trow, int count,
                                             const int* tmask) {
   const int lane = threadIdx.x & 63, w = wave_id();
-  const int col = lane * 4, d = p.d;
-  for (int i = w; i < TM; i += NWAVE) {
-    f4 a = {0.f, 0.f, 0.f, 0.f};
-    if (i < count) {
-      const int row = trow[i];
-      const int deg = p.rowptr[row + 1] - p.rowptr[row];
-      if (deg > p.budget) {
-        a = load4(p.agg + (int64_t)row * d, col, d);
-      } else {
-        f4 acc = {0.f, 0.f, 0.f, 0.f};
-        float acc0 = 0.f;
+  const int d = p.d;
+  const int col = lane * 4, colc = min(col, d - 4);
+  const bool active = col < d;
+  const f4 zero = {0.f, 0.f, 0.f, 0.f};
+  // the wave's 4 rows side by side: independent loads and reductions (ILP 4)
+  f4 acc[4], pre[4];
+  float acc0[4];
+  bool heavy[4];
 #pragma unroll
-        for (int w2 = 0; w2 < NWAVE; ++w2) {
-          if ((tmask[w2] >> i) & 1) {
-            const float* src = part + (w2 * TM + i) * lda;
-            if (col < d) acc += f4{src[col], src[col + 1], src[col + 2], src[col + 3]};
-            if (AGG == AGG_LORENTZ) acc0 += src[d];
-          }
-        }
-        if constexpr (AGG == AGG_LORENTZ) a = lorentz_finish(acc0, acc, p.k);
-        else a = acc * p.norm[row];
-      }
+  for (int q = 0; q < 4; ++q) {
+    const int i = w + NWAVE * q;
+    const int row = trow[i < count ? i : 0];
+    heavy[q] = i < count && p.rowptr[row + 1] - p.rowptr[row] > p.budget;
+    pre[q] = zero;
+    if (heavy[q]) {  // pre-aggregated by the chunked kernels
+      const f4 v = *reinterpret_cast<const f4*>(p.agg + (int64_t)row * d + colc);
+      pre[q] = active ? v : zero;
     }
+    acc[q] = zero;
+    acc0[q] = 0.f;
+#pragma unroll
+    for (int w2 = 0; w2 < NWAVE; ++w2) {
+      const bool on = (tmask[w2] >> i) & 1;  // slot written by wave w2 (else stale LDS)
+      const float* src = part + (w2 * TM + i) * lda;
+      const f4 v = {src[colc], src[colc + 1], src[colc + 2], src[colc + 3]};
+      acc[q] += (on && active) ? v : zero;
+      if (AGG == AGG_LORENTZ) acc0[q] += on ? src[d] : 0.f;
+    }
+  }
+  f4 out[4];
+  if constexpr (AGG == AGG_LORENTZ) {
+    float ss[4], yy[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ss[q] = row16_sum(dot4(acc[q], acc[q]));
+    f4 y[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float s2 = (rlane(ss[q], 0) + rlane(ss[q], 16)) + (rlane(ss[q], 32) + rlane(ss[q], 48));
+      const float ip = -acc0[q] * acc0[q] + s2;
+      const float sc = sqrtf(fmaxf(-ip * p.k.c, REGCN_EPS));
+      const float c0 = acc0[q] / sc;
+      y[q] = (acc[q] / sc) / fmaxf(1.f + c0 * p.k.sqrt_c, REGCN_EPS);
+      yy[q] = row16_sum(dot4(y[q], y[q]));
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float n2 = (rlane(yy[q], 0) + rlane(yy[q], 16)) + (rlane(yy[q], 32) + rlane(yy[q], 48));
+      out[q] = y[q] * log0_factor(n2, p.k);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = w + NWAVE * q;
+      out[q] = acc[q] * p.norm[trow[i < count ? i : 0]];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = w + NWAVE * q;
+    f4 a = heavy[q] ? pre[q] : out[q];
+    if (i >= count) a = zero;
     float* dst = part + i * lda;
-    if (col < d) {
+    if (active) {
       dst[col] = a.x;
       dst[col + 1] = a.y;
       dst[col + 2] = a.z;
@@ -304,12 +364,16 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
   float* part = lds + L.part;
   float* X = lds + L.X;
   int* trow = reinterpret_cast<int*>(lds + L.ints);
-  int* toff = trow + TM;
-  int* tmask = toff + TM + 1;
+  int* tmask = trow + TM;
   RowRed rr{lds + L.red, 0};
   float* P1 = part + TM * lda;      // skip-connection operand
   float* P2 = part + 2 * TM * lda;  // timestep: clamp(x_prev)
 
+  auto mark = [&](int k) {
+    trace_mark(p, k);
+  };
+  mark(0);
+  if (p.trace && threadIdx.x == 0) p.trace[blockIdx.x * 16 + 6] = (int64_t)__builtin_amdgcn_s_memtime();
   const int n_pos_tiles = p.tiles ? p.n_pos_tiles : (p.n_pos + TM - 1) / TM;
   const bool pos = (int)blockIdx.x < n_pos_tiles;
   int start, count;
@@ -326,28 +390,17 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
     count = min(TM, p.V - start);
   }
   const bool inline_gather = pos && AGG != AGG_NONE;
-  if (threadIdx.x < 64) {
-    const int t = threadIdx.x;
-    const int row = p.rows[start + (t < count ? t : 0)];
-    if (t < TM) trow[t] = row;
-    if (inline_gather) {  // exclusive scan of the inline item counts over the 16 rows
-      int v = 0;
-      if (t < count) {
-        const int deg = p.rowptr[row + 1] - p.rowptr[row];
-        v = deg <= p.budget ? deg : 0;
-      }
-#pragma unroll
-      for (int o = 1; o < TM; o <<= 1) {
-        const int y = __shfl_up(v, o, TM);
-        if ((t & (TM - 1)) >= o) v += y;
-      }
-      if (t < TM) toff[t + 1] = v;
-      if (t == 0) toff[0] = 0;
-    }
-  }
+  if (threadIdx.x < TM) trow[threadIdx.x] = p.rows[start + ((int)threadIdx.x < count ? threadIdx.x : 0)];
   __syncthreads();
+  mark(1);
 
-  // ---- operands: self-loop rows; pre-aggregated rows (AGG_NONE); gather
+  // ---- operands: self-loop rows; pre-aggregated rows (AGG_NONE); gather.  The first
+  // GEMM's B ring is issued before the A tiles (it depends on nothing), except on tiles
+  // that gather inline, where it would sit in registers across the gather.
+  const float* wsel = pos ? p.w_loop : p.w_evolve;
+  const float* wfirst = (pos && p.w_n) ? p.w_n : wsel;
+  BRing br;
+  if (!inline_gather && wfirst) br.load(wfirst, p.d);
   stage_rows<false>(X, lda, p.x, trow, p.d, count);
   if (pos && AGG == AGG_NONE) stage_rows<false>(part, lda, p.agg, trow, p.d, count);
   if (!inline_gather) {
@@ -356,28 +409,35 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
   }
   if (inline_gather) {
     if constexpr (AGG != AGG_NONE) {
-      tile_gather<AGG, S>(p, part, lda, trow, toff, count, tmask, lds + L.xsh);
+      tile_gather<AGG, S>(p, part, lda, trow, blockIdx.x, tmask, lds + L.xsh);
       __syncthreads();
+      trace_mark(p, 12);
       tile_finish<AGG>(p, part, lda, trow, count, tmask);
+      trace_mark(p, 13);
     }
     if (STEP) stage_rows<true>(P2, lda, p.step.x_prev, trow, p.d, count);
     if (p.prev_t) stage_rows<false>(P1, lda, p.prev_t, trow, p.d, count);
+    if (wfirst) br.load(wfirst, p.d);
   }
   __syncthreads();
+  mark(2);
 
   // ---- v = clamp(agg [@ W_n]) + x @ (W_loop | W_evolve)
   Frag v;
   v.zero();
   if (pos) {
-    if (p.w_n) mfma_tile(v, part, lda, p.w_n, p.d);
+    if (p.w_n) mfma_tile_pf(v, part, lda, p.w_n, p.d, br);
     else frag_from_tile(v, part, lda, p.d);
     if (!p.euclid) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) v.t[j] = clamp4(v.t[j], -10.f, 10.f);
     }
   }
-  const float* wsel = pos ? p.w_loop : p.w_evolve;
-  if (wsel) mfma_tile(v, X, lda, wsel, p.d);
+  if (wsel) {
+    if (wfirst == wsel && !(pos && p.w_n)) mfma_tile_pf(v, X, lda, wsel, p.d, br);
+    else mfma_tile(v, X, lda, wsel, p.d);
+  }
+  mark(3);
   if (p.prev_t) {  // v = g v + (1 - g) prev_t, g = sigmoid(prev_t @ W_skip + b)
     Frag g;
     g.zero();
@@ -406,6 +466,7 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
     for (int j = 0; j < 4; ++j) v.t[j] *= m.t[j];
   }
   if (!p.euclid) frag_exp0(rr, v, p.k);
+  mark(4);
 
   if constexpr (STEP) {
     step_epilogue(rr, v, P2, lda, trow, count, p.step);
@@ -424,6 +485,8 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
     }
     if (p.x_next) frag_store(v, p.x_next, trow, count, p.d);
   }
+  mark(5);
+  if (p.trace && threadIdx.x == 0) p.trace[blockIdx.x * 16 + 7] = (int64_t)__builtin_amdgcn_s_memtime();
 }
 
 // ================================================================================ timestep
@@ -481,7 +544,8 @@ int layer(const LayerArgs& a, hipStream_t st) {
     if (mode != AGG_LORENTZ && !a.norm) return set_error(REGCN_EINVAL, "gather needs norm");
     if (mode == AGG_LORENTZ && (!a.w_rel || a.nb <= 0 || a.d % a.nb))
       return set_error(REGCN_EINVAL, "lorentz gather needs weights and d %% num_bases == 0");
-    if (a.tiles && a.n_pos_tiles < 0) return set_error(REGCN_EINVAL, "bad tile count");
+    if (!a.tiles || !a.item_ptr || a.n_pos_tiles < 0)
+      return set_error(REGCN_EINVAL, "inline gather needs tiles and item lists");
   }
   if ((mode == AGG_UNION || mode == AGG_LORENTZ) && a.euclid) return set_error(REGCN_EINVAL, "hyperbolic gather with euclid tail");
   if (a.fuse_step) {

@@ -71,6 +71,9 @@ struct LayerArgs {
   int budget;               // rows with in-degree > budget read `agg` (pre-aggregated)
   const int* tiles;         // n_pos_tiles x {start, count} over rows[0, n_pos); null: 16-row tiles
   int n_pos_tiles;
+  const int* item_ptr;      // n_pos_tiles + 1: each tile's in-edge items
+  const int* item_src;      // source entity of each item
+  const int* item_tl;       // relation type << 4 | tile-local destination row
   const float* agg;         // V x d pre-aggregated rows (heavy rows; every pos row for AGG_NONE)
   const float* w_n;
   const float* w_loop;
@@ -87,6 +90,7 @@ struct LayerArgs {
   float* r_next;
   int fuse_step;            // run the timestep on the layer output (step.hc unused)
   StepArgs step;
+  int64_t* trace;           // debug: 8 phase timestamps per workgroup, or null
 };
 
 struct ScoreArgs {

@@ -87,23 +87,44 @@ __global__ __launch_bounds__(NTHR) void k_rel_gru(RelGruArgs p) {
   f4 ar = {0.f, 0.f, 0.f, 0.f}, az = ar, ai = ar, ah = ar;
   const float* arow = A + (lane & 15) * lda + (lane >> 4);
   const int gs_in = S_in * NT * 64, gs_h = S_h * NT * 64;  // per-gate stride of the packs
-  int s = sb;
-  for (; s < se && s < S_in; ++s) {
-    const float a = arow[4 * s];
-    const float* b = p.w_ih + ((int64_t)s * NT + jt) * 64 + lane;
-    const float br = b[0], bz = b[gs_in], bn = b[2 * gs_in];
-    ar = __builtin_amdgcn_mfma_f32_16x16x4f32(a, br, ar, 0, 0, 0);
-    az = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bz, az, 0, 0, 0);
-    ai = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bn, ai, 0, 0, 0);
+  // B (3 gates) and A operands ride in rings GR k-steps ahead of their MFMAs; every load
+  // is unconditional (clamped step) so the waits are counted, not drained.
+  constexpr int GR = 8;
+  auto bptr = [&](int st) {
+    return st < S_in ? p.w_ih + ((int64_t)st * NT + jt) * 64 + lane
+                     : p.w_hh + ((int64_t)(st - S_in) * NT + jt) * 64 + lane;
+  };
+  float ra[GR], rr_[GR], rz[GR], rn[GR];
+#pragma unroll
+  for (int i = 0; i < GR; ++i) {
+    const int st = min(sb + i, S - 1);
+    const float* b = bptr(st);
+    const int gs = st < S_in ? gs_in : gs_h;
+    rr_[i] = b[0];
+    rz[i] = b[gs];
+    rn[i] = b[2 * gs];
+    ra[i] = arow[4 * st];
   }
-  for (; s < se; ++s) {
-    const int sh = s - S_in;
-    const float a = arow[4 * s];
-    const float* b = p.w_hh + ((int64_t)sh * NT + jt) * 64 + lane;
-    const float br = b[0], bz = b[gs_h], bn = b[2 * gs_h];
-    ar = __builtin_amdgcn_mfma_f32_16x16x4f32(a, br, ar, 0, 0, 0);
-    az = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bz, az, 0, 0, 0);
-    ah = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bn, ah, 0, 0, 0);
+  for (int s0 = sb; s0 < se; s0 += GR) {
+#pragma unroll
+    for (int i = 0; i < GR; ++i) {
+      const int s = s0 + i;
+      if (s < se) {  // wave-uniform
+        ar = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rr_[i], ar, 0, 0, 0);
+        az = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rz[i], az, 0, 0, 0);
+        if (s < S_in) ai = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rn[i], ai, 0, 0, 0);
+        else ah = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rn[i], ah, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const int st = min(s + GR, S - 1);
+      const float* b = bptr(st);
+      const int gs = st < S_in ? gs_in : gs_h;
+      rr_[i] = b[0];
+      rz[i] = b[gs];
+      rn[i] = b[2 * gs];
+      ra[i] = arow[4 * st];
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   red[(w * 4 + 0) * 64 + lane] = ar;
   red[(w * 4 + 1) * 64 + lane] = az;

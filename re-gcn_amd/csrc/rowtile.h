@@ -74,28 +74,53 @@ __device__ __forceinline__ void mfma4(Frag& acc, float a, f4 b) {
   acc.t[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b.w, acc.t[3], 0, 0, 0);
 }
 
-// acc += T[16 x d] @ W (T in LDS, W packed with d_in = d).  No barriers inside.
-__device__ __forceinline__ void mfma_tile(Frag& acc, const float* T, int lda, const float* __restrict__ Wp, int d) {
+// The first RING B fragments of a packed weight, loaded ahead of the A tile (they do not
+// depend on it), so the MFMA chain starts without a load latency.
+struct BRing {
+  f4 ring[RING];
+  __device__ __forceinline__ void load(const float* __restrict__ Wp, int d) {
+    const f4* bsrc = reinterpret_cast<const f4*>(Wp) + wave_id() * 64 + (threadIdx.x & 63);
+    const int S = d >> 2;
+#pragma unroll
+    for (int i = 0; i < RING; ++i) ring[i] = bsrc[(int64_t)min(i, S - 1) * 256];
+  }
+};
+
+// acc += T[16 x d] @ W (T in LDS, W packed with d_in = d), ring pre-filled by BRing::load.
+__device__ __forceinline__ void mfma_tile_pf(Frag& acc, const float* T, int lda, const float* __restrict__ Wp, int d,
+                                             BRing& br) {
   const int lane = threadIdx.x & 63, w = wave_id();
   const int S = d >> 2;
   const f4* bsrc = reinterpret_cast<const f4*>(Wp) + w * 64 + lane;  // + s * 256
   const float* arow = T + (lane & 15) * lda + (lane >> 4);
-  f4 ring[RING];
+  f4* ring = br.ring;
+  // A operands ride in their own ring, RING k-steps ahead: an LDS read right before its
+  // MFMA would expose the ds_read latency on every step (the sched barriers keep order).
+  float aring[RING];
 #pragma unroll
-  for (int i = 0; i < RING; ++i) ring[i] = bsrc[(int64_t)min(i, S - 1) * 256];
+  for (int i = 0; i < RING; ++i) aring[i] = arow[4 * min(i, S - 1)];
   int s = 0;
   for (; s + RING <= S; s += RING) {
 #pragma unroll
     for (int i = 0; i < RING; ++i) {
-      mfma4(acc, arow[4 * (s + i)], ring[i]);
+      mfma4(acc, aring[i], ring[i]);
       __builtin_amdgcn_sched_barrier(0);
-      ring[i] = bsrc[(int64_t)min(s + i + RING, S - 1) * 256];  // unconditional: hipcc can count it
+      const int nx = min(s + i + RING, S - 1);
+      ring[i] = bsrc[(int64_t)nx * 256];  // unconditional: hipcc can count it
+      aring[i] = arow[4 * nx];
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 #pragma unroll
   for (int i = 0; i < RING; ++i)
-    if (s + i < S) mfma4(acc, arow[4 * (s + i)], ring[i]);
+    if (s + i < S) mfma4(acc, aring[i], ring[i]);
+}
+
+// acc += T[16 x d] @ W.  No barriers inside.
+__device__ __forceinline__ void mfma_tile(Frag& acc, const float* T, int lda, const float* __restrict__ Wp, int d) {
+  BRing br;
+  br.load(Wp, d);
+  mfma_tile_pf(acc, T, lda, Wp, d, br);
 }
 
 // Cross-wave row reductions: per-wave partials -> LDS red[buf][wave][row] -> sum.

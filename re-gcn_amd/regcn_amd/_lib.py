@@ -70,13 +70,13 @@ class LayerDesc(ctypes.Structure):
     _fields_ = [
         ("agg_mode", _c_int), ("x", P), ("radius", P), ("rel", P), ("w_rel", P), ("num_bases", _c_int),
         ("gamma", _c_f), ("rowptr", P), ("col_src", P), ("col_type", P), ("norm", P), ("budget", _c_int),
-        ("tiles", P), ("n_pos_tiles", _c_int), ("agg", P), ("w_n", P), ("w_loop", P), ("w_evolve", P),
+        ("tiles", P), ("n_pos_tiles", _c_int), ("item_ptr", P), ("item_src", P), ("item_tl", P), ("agg", P), ("w_n", P), ("w_loop", P), ("w_evolve", P),
         ("prev_t", P), ("w_skip", P), ("b_skip", P), ("drop_mask", P), ("rows", P), ("n_pos", _c_int),
         ("V", _c_int), ("d", _c_int), ("euclid", _c_int), ("c", _c_f), ("h_out", P), ("x_next", P),
         ("r_next", P), ("fuse_step", _c_int), ("step_x_prev", P), ("step_w_g", P), ("step_b_g", P),
         ("step_r_static", P), ("step_w_r", P), ("step_b_r", P), ("step_eps_r", _c_f), ("step_beta", _c_f),
         ("step_layer_norm", _c_int), ("step_residual", _c_int), ("step_c_radius", _c_f), ("step_h_out", P),
-        ("step_x_out", P), ("step_r_out", P),
+        ("step_x_out", P), ("step_r_out", P), ("trace", P),
     ]
 
 

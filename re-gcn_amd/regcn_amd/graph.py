@@ -120,10 +120,31 @@ class SnapshotGraph:
         pos = pos[np.argsort(-in_deg[pos], kind="stable")]  # in-degree descending (tile packing)
         zero = np.nonzero(in_deg == 0)[0]
         # fused-layer tiles (csrc/layer.hip): rows over the edge budget are pre-aggregated
-        self.budget = int(tile_budget) if tile_budget else tile_budget_for(E, self.chunk_edges)
+        self.budget = int(tile_budget) if tile_budget else tile_budget_for(
+            E, self.chunk_edges, int(in_deg.max()) if V else 0)
         heavy = pos[in_deg[pos] > self.budget]
-        tiles = _pack_tiles(np.where(in_deg[pos] > self.budget, 0, in_deg[pos]), self.budget)
+        # small snapshots pack ~32 inline edges per tile (8 per wave = one batch in flight);
+        # a row up to the budget still sits alone in its own tile
+        self.pack_items = min(32, self.budget) if E <= 65536 else self.budget
+        tiles = _pack_tiles(np.where(in_deg[pos] > self.budget, 0, in_deg[pos]), self.pack_items)
         hchunks, hfixups, hslot = _chunk_spans(rowptr[heavy], in_deg[heavy], heavy, self.chunk_edges)
+        # per-tile flattened in-edge lists of the inline rows (tile order = rows order):
+        # item_src, item_tl = type << 4 | tile-local row, item_ptr[t] = first item of tile t
+        inl = np.where(in_deg[pos] > self.budget, 0, in_deg[pos])
+        n_items = int(inl.sum())
+        first = np.cumsum(inl) - inl
+        perm = np.arange(n_items, dtype=np.int64) + np.repeat(rowptr[pos] - first, inl)
+        counts = tiles[:, 1].astype(np.int64) if len(tiles) else np.zeros(0, np.int64)
+        local = np.arange(len(pos)) - np.repeat(tiles[:, 0].astype(np.int64), counts) if len(tiles) else \
+            np.zeros(0, np.int64)
+        col_src_s, col_type_s = src[order], etype[order]
+        if len(etype) and int(etype.max()) >= 2 ** 27:
+            raise ValueError("relation ids must be < 2^27")
+        item_src = col_src_s[perm].astype(np.int32)
+        item_tl = ((col_type_s[perm].astype(np.int64) << 4) | np.repeat(local, inl)).astype(np.int32)
+        item_ptr = np.zeros(len(tiles) + 1, dtype=np.int64)
+        if len(tiles):
+            item_ptr[1:] = np.cumsum(np.add.reduceat(inl, tiles[:, 0]))
         R2 = 2 * self.num_rels
         rel_count = np.zeros(R2, dtype=np.float32)
         rel_start = np.zeros(R2, dtype=np.int64)
@@ -148,6 +169,7 @@ class SnapshotGraph:
             "rel_start": rel_start.astype(np.int32),
             "rowptr": rowptr.astype(np.int32), "tiles": tiles,
             "heavy_chunks": hchunks, "heavy_fixups": hfixups,
+            "item_src": item_src, "item_tl": item_tl, "item_ptr": item_ptr.astype(np.int32),
         }
         self.n_pos = int(len(pos))
         self.n_pos_tiles = int(len(tiles))
@@ -199,11 +221,15 @@ class SnapshotGraph:
         return self.dev
 
 
-def tile_budget_for(num_edges, chunk_edges):
-    """In-edges one fused-layer tile gathers inline (4 waves share them).  Small snapshots
-    keep it at 64 (16 edges = 4 batches of 4 per wave) so no tile outlasts the rest by
-    much; large ones raise it with the chunk size (many tiles per CU hide the spread)."""
-    return int(max(64, 4 * chunk_edges)) if num_edges > 65536 else 64
+def tile_budget_for(num_edges, chunk_edges, max_deg=0):
+    """In-edges one fused-layer tile gathers inline (4 waves share them, 8 in flight per
+    wave).  Small snapshots take every row up to 256 in-edges inline: a hub tile then runs
+    a few more batches than the rest, cheaper than the two extra launches of the chunked
+    pre-aggregation.  Large snapshots scale it with the chunk size (many tiles per CU hide
+    the spread)."""
+    if num_edges > 65536:
+        return int(max(64, 4 * chunk_edges))
+    return int(min(256, max(64, max_deg)))
 
 
 def _pack_tiles(inline_deg, budget):

@@ -17,6 +17,7 @@ from .tangent import attach, tangent_of
 from .weights import packed
 
 EPS = 1e-6
+TRACE = None  # int64 HIP tensor (>= 8 x workgroups) to record k_layer phase timestamps (profiling)
 
 
 def _drop_mask(layer, like):
@@ -103,6 +104,9 @@ def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_
     desc.budget = g.budget
     desc.tiles = a(wk["tiles"], torch.int32)
     desc.n_pos_tiles = g.n_pos_tiles
+    desc.item_ptr = a(wk["item_ptr"], torch.int32)
+    desc.item_src = a(wk["item_src"], torch.int32) if wk["item_src"].numel() else None
+    desc.item_tl = a(wk["item_tl"], torch.int32) if wk["item_tl"].numel() else None
     desc.agg = a(agg)
     desc.w_n, desc.w_loop, desc.w_evolve, desc.w_skip = (a(w) for w in pk)
     desc.prev_t = a(prev_t, what="prev_h")
@@ -122,6 +126,8 @@ def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_
         desc.step_layer_norm, desc.step_residual = int(bool(step.layer_norm)), int(bool(step.residual))
         desc.step_c_radius = float(step.c_radius)
         desc.step_h_out, desc.step_x_out, desc.step_r_out = a(h), a(xn), a(rn)
+    if TRACE is not None:  # profiling hook: per-workgroup phase timestamps
+        desc.trace = a(TRACE, torch.int64)
     _lib.call_layer(desc)
     return h, xn, rn
 

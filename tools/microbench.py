@@ -1,91 +1,60 @@
-"""Kernel microbenchmarks on the GPU box (graph-replayed launches timed with HIP events)."""
+"""Kernel microbenchmarks on the GPU box: the fused per-layer kernel (Lorentz and Union,
+with and without the fused timestep) and the relation GRU at four snapshot sizes, timed
+as graph-replayed launches between HIP events (bench.event_time)."""
 import os
 import sys
-import time
 
-import numpy as np
 import torch
+import torch.nn.functional as F
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "re-gcn_amd"))
-from regcn_amd import _lib, graph as G  # noqa: E402
+sys.path.insert(0, REPO)
+from bench import FP32_MFMA_PEAK_TFLOPS, HBM_PEAK_GBS, event_time  # noqa: E402
+from regcn_amd import graph as G  # noqa: E402
+from regcn_amd.hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNLayer, StepSpec  # noqa: E402
+from regcn_amd.hyperbolic_model import relation_gru_step  # noqa: E402
+from regcn_amd.hyperbolic_ops import HyperbolicOps as H  # noqa: E402
 from regcn_amd.synthetic import snapshot_series  # noqa: E402
+from regcn_amd.weights import packed  # noqa: E402
 
 dev = torch.device("cuda", 0)
+C = 0.01
 
 
-def timeit(fn, reps=50):
-    st = torch.cuda.Stream()
-    with torch.cuda.stream(st):
-        fn()
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=st):
-            for _ in range(reps):
-                fn()
-        g.replay()
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record(st)
-        for _ in range(5):
-            g.replay()
-        e.record(st)
-        e.synchronize()
-    return s.elapsed_time(e) / (5 * reps) * 1e3  # us per launch
-
-
-def run(V, R, per_snap, d=200, nb=100, chunk=None):
+def run(V, R, per_snap, d=200, nb=100):
     snaps = snapshot_series(0, V, R, 1, per_snap)
-    g = G.build_sub_graph(V, R, snaps[0], True, dev, chunk_edges=chunk)
-    wk = g.work()
+    g = G.build_sub_graph(V, R, snaps[0], True, dev)
     E = g.number_of_edges()
-    x = torch.randn(V, d, device=dev) * 0.1
-    r = x.norm(dim=1).contiguous()
+    torch.manual_seed(0)
+    h = H.exp_map_zero(torch.randn(V, d, device=dev) * 0.3, C)
     rel = torch.randn(2 * R, d, device=dev) * 0.1
-    W = torch.randn(2 * R, nb * (d // nb) ** 2, device=dev) * 0.1
-    out = torch.empty_like(x)
-    ch, fx = wk["chunks"], wk["fixups"]
-    part = torch.empty(max(g.n_slots, 1), d + 4, device=dev)
-    f, i = _lib.fptr, _lib.iptr
-
-    def lor():
-        _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(W), i(wk["col_src"]), i(wk["col_type"]), i(ch),
-                  ch.shape[0], i(fx), fx.shape[0], nb, 0.01, d, f(part), d + 4, f(out), _lib.stream())
-
-    def uni():
-        _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(wk["col_src"]), i(wk["col_type"]),
-                  f(wk["norm"]), i(ch), ch.shape[0], i(fx), fx.shape[0], 0.15, d, f(part), d + 4, f(out),
-                  _lib.stream())
-
-    def pro():
-        _lib.call("regcn_prologue_f32", f(x), V, d, 0.01, f(out), f(r), _lib.stream())
-    from regcn_amd.hyperbolic_layers import layer_tail
-    from regcn_amd.weights import packed
-    Wl = torch.randn(d, d, device=dev) * 0.05
-    We = torch.randn(d, d, device=dev) * 0.05
-    Wn = torch.randn(d, d, device=dev) * 0.05
-
-    def tail():
-        layer_tail(out, Wn, x, Wl, We, None, None, None, None, g, 0.01, False)
-    Wg = packed(torch.randn(d, d, device=dev) * 0.05)
-    bg = torch.zeros(d, device=dev)
-    rs = torch.rand(V, device=dev) + 0.5
-    wr = torch.randn(d, device=dev) * 0.01
-    br = torch.zeros(1, device=dev)
-    hn, xn, rn = torch.empty_like(x), torch.empty_like(x), torch.empty_like(r)
-
-    def step():
-        _lib.call("regcn_timestep_f32", f(x), f(x), f(Wg), f(bg), f(rs), f(wr), f(br), 0.1, 1.0, 0, 1, V, d, 0.01,
-                  0.01, f(hn), f(xn), f(rn), _lib.stream())
-    tl, tu, tp, tt, ts = timeit(lor), timeit(uni), timeit(pro), timeit(tail), timeit(step)
-    byts = E * (4 * d + 12) + ch.shape[0] * (4 * d + 12)
-    fl_tail = 2.0 * d * d * (V + g.n_pos)
-    print("V=%d E=%d chunks=%d (chunk_edges=%d) lorentz %.1f us (%.1f GB/s)  union %.1f us (%.1f GB/s)  "
-          "prologue %.1f us  layer_tail %.1f us (%.1f TF)  timestep %.1f us (%.1f TF)"
-          % (V, E, ch.shape[0], g.chunk_edges, tl, byts / tl / 1e3, tu, byts / tu / 1e3, tp, tt,
-             fl_tail / tt / 1e6, ts, 2.0 * d * d * V / ts / 1e6), flush=True)
+    lor = LorentzRGCNLayer(d, d, 2 * R, nb, c=C, activation=F.rrelu, self_loop=True).to(dev).eval()
+    uni = HyperbolicUnionRGCNLayer(d, d, 2 * R, c=C, activation=F.rrelu, self_loop=True,
+                                   radius_msg_gamma=0.15).to(dev).eval()
+    gru = torch.nn.GRUCell(2 * d, d).to(dev)
+    xp = torch.randn(V, d, device=dev) * 0.1
+    step = StepSpec(xp, packed(torch.randn(d, d, device=dev) * 0.05), torch.zeros(d, device=dev),
+                    torch.rand(V, device=dev) + 0.5, torch.randn(d, device=dev) * 0.01, torch.zeros(1, device=dev),
+                    0.1, 1.0, False, True, C)
+    x = H.log_map_zero(h, C)
+    st = torch.cuda.Stream(dev)
+    with torch.no_grad():
+        t_lor = event_time(lambda: lor(g, h, rel), 20, st)
+        t_lors = event_time(lambda: lor(g, h, rel, step=step), 20, st)
+        t_uni = event_time(lambda: uni(g, h, rel), 20, st)
+        t_gru = event_time(lambda: relation_gru_step(gru, rel, x, g, rel), 20, st)
+    gather = E * (4 * d + 8) + 8 * V
+    io = 4.0 * V * d * 3 + 4 * V
+    fl = 2.0 * d * d * V
+    print("V=%d E=%d pos=%d tiles=%d heavy=%d | lorentz layer %.1f us (%.1f TF, %.0f GB/s) | +step %.1f us "
+          "(%.1f TF) | union layer %.1f us (%.1f TF) | rel GRU %.1f us"
+          % (V, E, g.n_pos, g.n_pos_tiles, g.n_heavy, t_lor * 1e3, fl / t_lor / 1e9, (gather + io) / t_lor / 1e6,
+             t_lors * 1e3, 2 * fl / t_lors / 1e9, t_uni * 1e3, (fl + 2.0 * d * d * g.n_pos) / t_uni / 1e9,
+             t_gru * 1e3), flush=True)
 
 
 if __name__ == "__main__":
+    print("peaks: %.1f TF fp32 MFMA, %.0f GB/s HBM" % (FP32_MFMA_PEAK_TFLOPS, HBM_PEAK_GBS))
     for V, R, ps in [(7128, 230, 246), (23033, 256, 1540), (100000, 256, 250000), (1000000, 256, 2500000)]:
         run(V, R, ps)
