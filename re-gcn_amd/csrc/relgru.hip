@@ -90,42 +90,42 @@ __global__ __launch_bounds__(NTHR) void k_rel_gru(RelGruArgs p) {
   // B (3 gates) and A operands ride in rings GR k-steps ahead of their MFMAs; every load
   // is unconditional (clamped step) so the waits are counted, not drained.
   constexpr int GR = 8;
-  auto bptr = [&](int st) {
-    return st < S_in ? p.w_ih + ((int64_t)st * NT + jt) * 64 + lane
-                     : p.w_hh + ((int64_t)(st - S_in) * NT + jt) * 64 + lane;
-  };
-  float ra[GR], rr_[GR], rz[GR], rn[GR];
-#pragma unroll
-  for (int i = 0; i < GR; ++i) {
-    const int st = min(sb + i, S - 1);
-    const float* b = bptr(st);
-    const int gs = st < S_in ? gs_in : gs_h;
-    rr_[i] = b[0];
-    rz[i] = b[gs];
-    rn[i] = b[2 * gs];
-    ra[i] = arow[4 * st];
-  }
-  for (int s0 = sb; s0 < se; s0 += GR) {
+  // steps [beg, end) of one weight (W: packed base, off: its first global step, gs: gate
+  // stride); the n gate accumulates into accn (n_in for W_ih, n_h for W_hh)
+  auto segment = [&](int beg, int end, const float* W, int off, int gs, f4& accn) {
+    if (beg >= end) return;
+    const float* bb = W + (int64_t)jt * 64 + lane;
+    float ra[GR], rr_[GR], rz[GR], rn[GR];
 #pragma unroll
     for (int i = 0; i < GR; ++i) {
-      const int s = s0 + i;
-      if (s < se) {  // wave-uniform
-        ar = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rr_[i], ar, 0, 0, 0);
-        az = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rz[i], az, 0, 0, 0);
-        if (s < S_in) ai = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rn[i], ai, 0, 0, 0);
-        else ah = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rn[i], ah, 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      const int st = min(s + GR, S - 1);
-      const float* b = bptr(st);
-      const int gs = st < S_in ? gs_in : gs_h;
+      const int st = min(beg + i, end - 1);
+      const float* b = bb + (int64_t)(st - off) * NT * 64;
       rr_[i] = b[0];
       rz[i] = b[gs];
       rn[i] = b[2 * gs];
       ra[i] = arow[4 * st];
-      __builtin_amdgcn_sched_barrier(0);
     }
-  }
+    for (int s0 = beg; s0 < end; s0 += GR) {
+#pragma unroll
+      for (int i = 0; i < GR; ++i) {
+        if (s0 + i < end) {  // wave-uniform
+          ar = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rr_[i], ar, 0, 0, 0);
+          az = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rz[i], az, 0, 0, 0);
+          accn = __builtin_amdgcn_mfma_f32_16x16x4f32(ra[i], rn[i], accn, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const int st = min(s0 + i + GR, end - 1);
+        const float* b = bb + (int64_t)(st - off) * NT * 64;
+        rr_[i] = b[0];
+        rz[i] = b[gs];
+        rn[i] = b[2 * gs];
+        ra[i] = arow[4 * st];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  segment(sb, min(se, S_in), p.w_ih, 0, gs_in, ai);
+  segment(max(sb, S_in), se, p.w_hh, S_in, gs_h, ah);
   red[(w * 4 + 0) * 64 + lane] = ar;
   red[(w * 4 + 1) * 64 + lane] = az;
   red[(w * 4 + 2) * 64 + lane] = ai;

@@ -20,7 +20,15 @@
 
 namespace regcn {
 
-constexpr int SQ = 64, SN = 64, SKC = 16, SLD = SKC + 1;
+constexpr int SQ = 64, SN = 64;
+// K chunk: 16 * NF columns (NF float4 per staging thread and row); fp32 64, fp64 32,
+// double-buffered in LDS (4 chunks at d = 200: few barriers, loads one chunk ahead).
+template <bool F64>
+struct Chunking {
+  static constexpr int NF = F64 ? 2 : 4;
+  static constexpr int SKC = 16 * NF;
+  static constexpr int SLD = SKC + 1;
+};
 
 
 
@@ -91,8 +99,9 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
   if (p.scale_raw && p.scale_p)  // softplus(raw) + 1e-6 (hyperbolic_decoder.py:717; torch threshold 20)
     p.scale = (p.scale > 20.f ? p.scale : log1pf(expf(p.scale))) + 1e-6f;
   p.margin = p.margin_p ? *p.margin_p : 0.f;
-  __shared__ T Qs[SQ * SLD];
-  __shared__ T Es[SN * SLD];
+  constexpr int NF = Chunking<F64>::NF, SKC = Chunking<F64>::SKC, SLD = Chunking<F64>::SLD;
+  __shared__ T Qs2[2][SQ * SLD];  // double-buffered K chunks
+  __shared__ T Es2[2][SN * SLD];
   __shared__ T q2s[SQ], e2s[SN];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // consecutive blocks share a query tile (the candidate stream is the large operand)
@@ -104,24 +113,49 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
   for (int j = 0; j < 4; ++j) acc[j] = typename S::V{0, 0, 0, 0};
   const int i = tid >> 2, kq = (tid & 3) * 4;
   T sq_q = 0, sq_e = 0;  // row |.|^2, accumulated by the 4 staging threads of row i
-  for (int k0 = 0; k0 < p.d; k0 += SKC) {
-    __syncthreads();
-    f4 vq = {0.f, 0.f, 0.f, 0.f}, ve = {0.f, 0.f, 0.f, 0.f};
-    if (q0 + i < p.B && k0 + kq < p.d) vq = *reinterpret_cast<const f4*>(p.q + (int64_t)(q0 + i) * p.d + k0 + kq);
-    if (n0 + i < p.N && k0 + kq < p.d) ve = *reinterpret_cast<const f4*>(p.e + (int64_t)(n0 + i) * p.d + k0 + kq);
-    T* dq = Qs + i * SLD + kq;
-    T* de = Es + i * SLD + kq;
+  // Software pipeline: chunk c + 1 is loaded into registers (unconditional, clamped
+  // addresses) while chunk c is multiplied out of the other LDS buffer.
+  const float* qrow = p.q + (int64_t)min(q0 + i, p.B - 1) * p.d;
+  const float* erow = p.e + (int64_t)min(n0 + i, p.N - 1) * p.d;
+  const bool q_ok = q0 + i < p.B, e_ok = n0 + i < p.N;
+  const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  auto fetch = [&](int k0, f4* vq, f4* ve) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const T a = (T)vq[u], b = (T)ve[u];
-      dq[u] = a;
-      de[u] = b;
-      sq_q += a * a;
-      sq_e += b * b;
+    for (int f = 0; f < NF; ++f) {
+      const int k = k0 + kq + 16 * f;
+      const int c = min(k, p.d - 4);
+      const bool k_ok = k < p.d;
+      const f4 a = *reinterpret_cast<const f4*>(qrow + c);
+      const f4 b = *reinterpret_cast<const f4*>(erow + c);
+      vq[f] = (q_ok && k_ok) ? a : z4;
+      ve[f] = (e_ok && k_ok) ? b : z4;
     }
-    __syncthreads();
+  };
+  f4 vq[NF], ve[NF];
+  fetch(0, vq, ve);
+  int buf = 0;
+  for (int k0 = 0; k0 < p.d; k0 += SKC, buf ^= 1) {
 #pragma unroll
-    for (int kk = 0; kk < SKC; kk += 4) {
+    for (int f = 0; f < NF; ++f) {
+      T* dq = Qs2[buf] + i * SLD + kq + 16 * f;
+      T* de = Es2[buf] + i * SLD + kq + 16 * f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const T a = (T)vq[f][u], b = (T)ve[f][u];
+        dq[u] = a;
+        de[u] = b;
+        sq_q += a * a;
+        sq_e += b * b;
+      }
+    }
+    fetch(k0 + SKC, vq, ve);  // unconditional (past the end it reads a clamped chunk it never
+                              // stores): a conditional load would be drained right here
+    __syncthreads();  // chunk k0 staged; the other buffer's readers (chunk k0 - SKC) are done
+    const T* Qs = Qs2[buf];
+    const T* Es = Es2[buf];
+    const int kn = min(SKC, p.d - k0);
+#pragma unroll 4
+    for (int kk = 0; kk < kn; kk += 4) {
       const T a = Qs[(16 * wv + (lane & 15)) * SLD + kk + (lane >> 4)];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
