@@ -35,7 +35,7 @@ __host__ __device__ inline LdsLayout lds_layout(int d, bool gen_s) {
   L.part = 0;
   L.X = NWAVE * TM * L.lda;
   L.red = L.X + TM * L.lda;
-  L.ints = L.red + 2 * NWAVE * TM;
+  L.ints = L.red + RED_FLOATS;
   L.xsh = L.ints + 32;  // trow[16], tmask[4] (+pad)
   L.total_bytes = (L.xsh + (gen_s ? NWAVE * MAX_D : 0)) * 4;
   return L;
@@ -47,18 +47,20 @@ __host__ __device__ inline LdsLayout lds_layout(int d, bool gen_s) {
 //   tw = sigmoid(P @ W_g + b_g);  h = project(exp0(tw * ct + (1 - tw) * P))
 //   residual: r = beta r_s + (1 - beta)|h| + clamp(log0(h) . w_r + b_r, +-eps_r); else r = r_s
 //   h = apply_radius(h, r); outputs h, x = log0(h), r = max(|h|, eps).
-__device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, const float* P, int lda, const int* trow,
-                                              int n_valid, const StepArgs& p) {
+// n2: |ct row|^2 on entry (known from the producer's row maps); the chain below needs
+// only two cross-wave reductions (the exp0 of the gated mix, the radius-MLP dot).
+__device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4], const float* P, int lda,
+                                              const int* trow, int n_valid, const StepArgs& p) {
   Frag tw;
   tw.zero();
   mfma_tile(tw, P, lda, p.w_g, p.d);
-  frag_project(rr, ct, p.k);
+  project_known(ct, n2, p.k);
   if (p.layer_norm) {
-    frag_log0(rr, ct, p.k);
-    frag_normalize(rr, ct);
-    frag_exp0(rr, ct, p.k);
+    log0_known(ct, n2, p.k);
+    normalize_known(ct, n2);
+    exp0_known(ct, n2, p.k);
   }
-  frag_log0(rr, ct, p.k);
+  log0_known(ct, n2, p.k);
   Frag pt;
   frag_from_tile(pt, P, lda, p.d);
   float bg[4];
@@ -72,10 +74,10 @@ __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, const float*
       ct.t[j][r] = g * c4[r] + (1.f - g) * pt.t[j][r];
     }
   }
-  frag_exp0(rr, ct, p.k);
-  frag_project(rr, ct, p.k);  // hyperbolic_model.py:860
-  float n2[4], rs[4], newr[4];
   rr.sumsq(ct, n2);
+  exp0_known(ct, n2, p.k);
+  project_known(ct, n2, p.k);  // hyperbolic_model.py:860
+  float rs[4], newr[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = frag_row(r);
@@ -111,19 +113,12 @@ __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, const float*
     const float n = fmaxf(sqrtf(n2[r]), REGCN_EPS);
     f[r] = fminf(fmaxf(newr[r], REGCN_EPS), kr.rmax) / n;
   }
-  row_scale(ct, f);
+  scale_known(ct, n2, f);
   frag_store(ct, p.h_out, trow, n_valid, p.d);
-  if (p.r_out || p.x_out) {
-    float h2[4];
-    rr.sumsq(ct, h2);
-    if (p.r_out) store_radius(h2, p.r_out, trow, n_valid);
-    if (p.x_out) {
-      float g[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) g[r] = log0_factor(h2[r], p.k);
-      row_scale(ct, g);
-      frag_store(ct, p.x_out, trow, n_valid, p.d);
-    }
+  if (p.r_out) store_radius(n2, p.r_out, trow, n_valid);
+  if (p.x_out) {
+    log0_known(ct, n2, p.k);
+    frag_store(ct, p.x_out, trow, n_valid, p.d);
   }
 }
 
@@ -465,24 +460,17 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) v.t[j] *= m.t[j];
   }
-  if (!p.euclid) frag_exp0(rr, v, p.k);
+  float n2[4];  // |row|^2 of v, carried through the row maps (rowtile.h)
+  if (!p.euclid || p.r_next) rr.sumsq(v, n2);
+  if (!p.euclid) exp0_known(v, n2, p.k);
   mark(4);
 
   if constexpr (STEP) {
-    step_epilogue(rr, v, P2, lda, trow, count, p.step);
+    step_epilogue(rr, v, n2, P2, lda, trow, count, p.step);
   } else {
     frag_store(v, p.h_out, trow, count, p.d);
-    if (p.r_next || (p.x_next && !p.euclid)) {
-      float n2[4];
-      rr.sumsq(v, n2);
-      if (p.r_next) store_radius(n2, p.r_next, trow, count);
-      if (p.x_next && !p.euclid) {
-        float f[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) f[r] = log0_factor(n2[r], p.k);
-        row_scale(v, f);
-      }
-    }
+    if (p.r_next) store_radius(n2, p.r_next, trow, count);
+    if (p.x_next && !p.euclid) log0_known(v, n2, p.k);
     if (p.x_next) frag_store(v, p.x_next, trow, count, p.d);
   }
   mark(5);
@@ -495,7 +483,7 @@ __global__ __launch_bounds__(NTHR) void k_timestep(StepArgs p) {
   const int lda = tile_lda(p.d);
   float* P = lds;
   RowRed rr{lds + TM * lda, 0};
-  int* trow = reinterpret_cast<int*>(lds + TM * lda + 2 * NWAVE * TM);
+  int* trow = reinterpret_cast<int*>(lds + TM * lda + RED_FLOATS);
   const int r0 = blockIdx.x * TM;
   const int n_valid = min(TM, p.V - r0);
   if (threadIdx.x < TM) trow[threadIdx.x] = r0 + (threadIdx.x < n_valid ? threadIdx.x : 0);
@@ -504,7 +492,9 @@ __global__ __launch_bounds__(NTHR) void k_timestep(StepArgs p) {
   Frag ct;
   frag_load(ct, p.hc, trow, n_valid, p.d);
   __syncthreads();
-  step_epilogue(rr, ct, P, lda, trow, n_valid, p);
+  float n2[4];
+  rr.sumsq(ct, n2);
+  step_epilogue(rr, ct, n2, P, lda, trow, n_valid, p);
 }
 
 // ============================================================================ pack weights
@@ -583,7 +573,7 @@ int timestep(const StepArgs& a, hipStream_t st) {
   if (a.residual && (!a.w_r || !a.b_r)) return set_error(REGCN_EINVAL, "residual radius needs w_r and b_r");
   if (a.V == 0) return 0;
   const unsigned grid = (unsigned)((a.V + TM - 1) / TM);
-  const size_t lds = (size_t)(TM * tile_lda(a.d) + 2 * NWAVE * TM + TM) * 4;
+  const size_t lds = (size_t)(TM * tile_lda(a.d) + RED_FLOATS + TM) * 4;
   hipLaunchKernelGGL(k_timestep, dim3(grid), dim3(NTHR), lds, st, a);
   return check_launch("k_timestep");
 }

@@ -69,11 +69,11 @@ __device__ __forceinline__ void givens(Frag& x, int d, AngleFn angle) {
   }
 }
 
-// HyperbolicOps.mobius_add (hyperbolic_ops.py:118-143) + its final project.
-__device__ __forceinline__ void frag_mobius(RowRed& rr, Frag& x, const Frag& y, const Curv& k) {
-  float x2[4], y2[4], xy[4];
-  rr.sumsq(x, x2);
-  rr.sumsq(y, y2);
+// HyperbolicOps.mobius_add (hyperbolic_ops.py:118-143) + its final project, with the row
+// norms x2 / y2 known: one reduction (<x, y>); the result's norm follows from them.
+__device__ __forceinline__ void mobius_known(RowRed& rr, Frag& x, const float x2[4], const Frag& y, const float y2[4],
+                                             const Curv& k) {
+  float xy[4], n2[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float s = 0.f;
@@ -89,8 +89,9 @@ __device__ __forceinline__ void frag_mobius(RowRed& rr, Frag& x, const Frag& y, 
     const float den = 1.f + 2.f * k.c * xy[r] + k.c * k.c * x2[r] * y2[r] + REGCN_EPS;
 #pragma unroll
     for (int j = 0; j < 4; ++j) x.t[j][r] = (A * x.t[j][r] + B * y.t[j][r]) / den;
+    n2[r] = fmaxf(A * A * x2[r] + 2.f * A * B * xy[r] + B * B * y2[r], 0.f) / (den * den);
   }
-  frag_project(rr, x, k);
+  project_known(x, n2, k);
 }
 
 template <int MODE>  // 0: RotH entity query, 1: RotH relation query (+ exp0 candidates)
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(NTHR) void k_query(QueryArgs p) {
   float* T1 = T0 + TM * lda;
   float* T2 = T1 + TM * lda;
   RowRed rr{T2 + TM * lda, 0};
-  int* ids = reinterpret_cast<int*>(T2 + TM * lda + 2 * NWAVE * TM);  // s[16], r[16], o[16]
+  int* ids = reinterpret_cast<int*>(T2 + TM * lda + RED_FLOATS);  // s[16], r[16], o[16]
   const int n_qt = (p.B + TM - 1) / TM;
 
   if (MODE == 1 && (int)blockIdx.x >= n_qt) {  // candidate tiles: exp0(R)
@@ -130,10 +131,28 @@ __global__ __launch_bounds__(NTHR) void k_query(QueryArgs p) {
   const int* rid = ids + TM;
   const int* oid = ids + 2 * TM;
 
-  Frag s;
+  Frag s, o;
+  float n2s[4], n2o[4];
   frag_load(s, p.ent, sid, nq, d);
-  if (MODE == 0) frag_project(rr, s, p.k);
-  frag_log0(rr, s, p.k);
+  if (MODE == 1) {  // |E[s]|^2 and |E[o]|^2 in one barrier
+    frag_load(o, p.ent, oid, nq, d);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a += s.t[j][r] * s.t[j][r];
+        b += o.t[j][r] * o.t[j][r];
+      }
+      n2s[r] = a;
+      n2o[r] = b;
+    }
+    rr.allreduce2(n2s, n2o);
+  } else {
+    rr.sumsq(s, n2s);
+    project_known(s, n2s, p.k);
+  }
+  log0_known(s, n2s, p.k);
   frag_to_tile(s, T0, lda, d);
   if (MODE == 0) stage_rows<false>(T1, lda, p.rel, rid, d, nq);
   __syncthreads();
@@ -159,19 +178,31 @@ __global__ __launch_bounds__(NTHR) void k_query(QueryArgs p) {
 
   if (MODE == 0) {
     givens(s, d, [&](int r, int k2) { return T2[frag_row(r) * lda + k2]; });
-    frag_exp0(rr, s, p.k);
-    frag_project(rr, s, p.k);
-    frag_exp0(rr, tr, p.k);
-    frag_project(rr, tr, p.k);
-    frag_mobius(rr, s, tr, p.k);
+    float n2t[4];  // |rot|^2 and |trans|^2 in one barrier (a rotation keeps the norm)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a += s.t[j][r] * s.t[j][r];
+        b += tr.t[j][r] * tr.t[j][r];
+      }
+      n2s[r] = a;
+      n2t[r] = b;
+    }
+    rr.allreduce2(n2s, n2t);
+    exp0_known(s, n2s, p.k);
+    project_known(s, n2s, p.k);
+    exp0_known(tr, n2t, p.k);
+    project_known(tr, n2t, p.k);
+    mobius_known(rr, s, n2s, tr, n2t, p.k);
   } else {
     givens(s, d, [&](int, int k2) { return p.global_rot[k2]; });
-    frag_exp0(rr, s, p.k);
+    rr.sumsq(s, n2s);
+    exp0_known(s, n2s, p.k);
 #pragma unroll
     for (int j = 0; j < 4; ++j) s.t[j] = -s.t[j];
-    Frag o;
-    frag_load(o, p.ent, oid, nq, d);
-    frag_mobius(rr, s, o, p.k);
+    mobius_known(rr, s, n2s, o, n2o, p.k);
   }
   // store rows b0 .. b0 + nq - 1 (query order, not entity ids)
 #pragma unroll
@@ -197,7 +228,7 @@ int query(const QueryArgs& a, int mode, hipStream_t st) {
   const int n_qt = (a.B + TM - 1) / TM;
   const int n_ct = mode == 1 ? (a.n_cand + TM - 1) / TM : 0;
   if (n_qt + n_ct == 0) return 0;
-  const size_t lds = (size_t)(3 * TM * tile_lda(a.d) + 2 * NWAVE * TM + 3 * TM) * 4;
+  const size_t lds = (size_t)(3 * TM * tile_lda(a.d) + RED_FLOATS + 3 * TM) * 4;
   if (mode == 0)
     hipLaunchKernelGGL(k_query<0>, dim3(n_qt), dim3(NTHR), lds, st, a);
   else

@@ -21,6 +21,7 @@ constexpr int TM = 16;         // rows per workgroup
 constexpr int NWAVE = 4;       // waves per workgroup (= 64-column groups)
 constexpr int NTHR = 64 * NWAVE;
 constexpr int RING = 8;        // k-steps of B fragments in flight per wave
+constexpr int RED_FLOATS = 4 * NWAVE * TM;  // RowRed scratch (2 buffers x 2 quantities)
 
 // LDS row stride for width d: smallest value >= d + 2 that is 2 (mod 32).
 __host__ __device__ constexpr int tile_lda(int d) { return d + 2 + ((32 - (d + 2) % 32) % 32); }
@@ -126,11 +127,11 @@ __device__ __forceinline__ void mfma_tile(Frag& acc, const float* T, int lda, co
 // Cross-wave row reductions: per-wave partials -> LDS red[buf][wave][row] -> sum.
 // Two buffers alternate so one barrier per reduction suffices.
 struct RowRed {
-  float* red;  // LDS, 2 * NWAVE * TM floats
+  float* red;  // LDS, RED_FLOATS: 2 buffers x (2 quantities x NWAVE x TM)
   int buf;
   __device__ __forceinline__ void allreduce(float part[4]) {
     const int lane = threadIdx.x & 63, w = wave_id();
-    float* b = red + buf * NWAVE * TM;
+    float* b = red + buf * 2 * NWAVE * TM;
 #pragma unroll
     for (int r = 0; r < 4; ++r) part[r] = row16_sum(part[r]);
     if ((lane & 15) == 0) {
@@ -145,6 +146,32 @@ struct RowRed {
     }
     buf ^= 1;
   }
+  // two independent per-row sums in one barrier (uses both halves of the buffer pair)
+  __device__ __forceinline__ void allreduce2(float pa[4], float pb[4]) {
+    const int lane = threadIdx.x & 63, w = wave_id();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pa[r] = row16_sum(pa[r]);
+      pb[r] = row16_sum(pb[r]);
+    }
+    float* ba = red + buf * 2 * NWAVE * TM;
+    float* bb = ba + NWAVE * TM;
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ba[w * TM + frag_row(r)] = pa[r];
+        bb[w * TM + frag_row(r)] = pb[r];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = frag_row(r);
+      pa[r] = (ba[i] + ba[TM + i]) + (ba[2 * TM + i] + ba[3 * TM + i]);
+      pb[r] = (bb[i] + bb[TM + i]) + (bb[2 * TM + i] + bb[3 * TM + i]);
+    }
+    buf ^= 1;
+  }
   __device__ __forceinline__ void sumsq(const Frag& a, float out[4]) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -156,6 +183,48 @@ struct RowRed {
     allreduce(out);
   }
 };
+
+// ---- row maps with the row norms carried along ------------------------------------------
+// A row map scales each row by a factor of its norm, so the norm after the map follows
+// analytically (|f x| = f |x|): chains of maps need one cross-wave reduction, not one per
+// map.  n2[r] is |row|^2 of fragment row r, updated in place.
+__device__ __forceinline__ void row_scale(Frag& a, const float f[4]);
+
+__device__ __forceinline__ void scale_known(Frag& a, float n2[4], const float f[4]) {
+  row_scale(a, f);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) n2[r] *= f[r] * f[r];
+}
+
+__device__ __forceinline__ void project_known(Frag& a, float n2[4], const Curv& k) {
+  float f[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) f[r] = project_factor(n2[r], k);
+  scale_known(a, n2, f);
+}
+
+__device__ __forceinline__ void log0_known(Frag& a, float n2[4], const Curv& k) {
+  float f[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) f[r] = log0_factor(n2[r], k);
+  scale_known(a, n2, f);
+}
+
+__device__ __forceinline__ void exp0_known(Frag& a, float n2[4], const Curv& k) {  // exp0 + project
+  float f[4], o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) f[r] = exp0_factor(n2[r], k, &o[r]);
+  row_scale(a, f);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) n2[r] = o[r];
+}
+
+__device__ __forceinline__ void normalize_known(Frag& a, float n2[4]) {  // F.normalize, eps 1e-12
+  float f[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) f[r] = 1.0f / fmaxf(sqrtf(n2[r]), 1e-12f);
+  scale_known(a, n2, f);
+}
 
 __device__ __forceinline__ void row_scale(Frag& a, const float f[4]) {
 #pragma unroll

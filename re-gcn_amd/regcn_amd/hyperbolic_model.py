@@ -323,9 +323,27 @@ class HyperbolicRecurrentRGCN(nn.Module):
             evolve_embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
             embedding = self._final_embedding(evolve_embs[-1], c_val)
             at = all_triples.to(embedding.device)
-            score = self.decoder_ob.forward(embedding, r_emb, at, mode="test")
-            score_rel = self.rdecoder.forward(embedding, r_emb, at, mode="test")
+            score, score_rel = self._decode_both(embedding, r_emb, at)
             return all_triples, score, score_rel
+
+    def _decode_both(self, embedding, r_emb, at):
+        """Entity and relation decoders are independent: on a HIP device the relation
+        decoder runs on a side stream, so each uses the CUs the other's ~30-workgroup
+        launches leave idle (also inside a captured HIP graph: a fork/join)."""
+        if embedding.device.type != "cuda":
+            return (self.decoder_ob.forward(embedding, r_emb, at, mode="test"),
+                    self.rdecoder.forward(embedding, r_emb, at, mode="test"))
+        main = torch.cuda.current_stream(embedding.device)
+        side = getattr(self, "_side_stream", None)
+        if side is None or side.device != embedding.device:
+            side = self._side_stream = torch.cuda.Stream(embedding.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            score_rel = self.rdecoder.forward(embedding, r_emb, at, mode="test")
+        score = self.decoder_ob.forward(embedding, r_emb, at, mode="test")
+        main.wait_stream(side)
+        score_rel.record_stream(main)
+        return score, score_rel
 
     def get_loss(self, glist, triples, static_graph, use_cuda, query_time=None):
         """hyperbolic_model.py:941-1088 (forward value of the four losses)."""
