@@ -101,6 +101,16 @@ int regcn_lorentz_aggregate_f32(const float* x, const float* rel, const float* w
                                 const int32_t* fixups, int32_t n_fix, int32_t num_bases, float c, int32_t d,
                                 float* partial, int32_t partial_stride, float* out, void* stream);
 
+/* ---- e: multi-GPU edge partition ------------------------------------------------------
+ * A rank aggregates only its slice of the edge list: the regcn_*_aggregate_f32 calls above
+ * with every chunk slotted and n_fix = 0 leave raw per-chunk sums in `partial`; this call
+ * sums each row's slots into out[row] (width columns: d, or d + 1 with the Lorentz time
+ * coordinate at column d), unfinished, so the cross-rank all-reduce of `out` is a plain
+ * sum (SURVEY.md §8(e) partitioning 1).  The all-reduced rows are then finished by the
+ * same aggregate call with n_chunks = 0, partial = out and fixups {row, row, row + 1}. */
+int regcn_partial_sum_f32(const float* partial, int32_t partial_stride, const int32_t* fixups, int32_t n_fix,
+                          int32_t width, float* out, int32_t out_stride, void* stream);
+
 /* ---- a4/a5/a6: layer tail (MFMA GEMMs + fused epilogue) ----------------------------- */
 /* Weight prepacking for the MFMA tails: a d_in x d_out row-major weight W (x @ W) becomes
  * packed[s][jq][lane][e] = W[4s + lane/16][16(4jq + e) + lane%16] (zero-padded), i.e. the

@@ -101,6 +101,24 @@ __global__ __launch_bounds__(256) void k_gather_fixup(const float* __restrict__ 
   }
 }
 
+// Raw partial sums of a shard (multi-GPU, edge partition): out[row] = sum of its chunk
+// partials, all `width` columns (d, or d + 1 with the Lorentz time coordinate), unfinished,
+// so the all-reduce of out across ranks is a plain sum.
+__global__ __launch_bounds__(256) void k_partial_sum(const float* __restrict__ partial, int pstride,
+                                                     const Fixup* __restrict__ fx, int n_fix, int width,
+                                                     float* __restrict__ out, int ostride) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n_fix; i += nw) {
+    const Fixup f = fx[i];
+    for (int c = lane; c < width; c += 64) {
+      float acc = 0.f;
+      for (int s = f.sbeg; s < f.send; ++s) acc += partial[(int64_t)s * pstride + c];
+      out[(int64_t)f.row * ostride + c] = acc;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ Lorentz
 // Messages and centroid: gather.h (hyperbolic_layers.py:589-625).
 // S in {1, 2, 4}: blocks held in registers, 4 edges in flight per wave (independent
@@ -243,6 +261,16 @@ int gather_sum(int mode, const float* x, const float* radius, const float* rel, 
     return check_launch("k_gather_fixup");
   }
   return 0;
+}
+
+int partial_sum(const float* partial, int pstride, const void* fixups, int n_fix, int width, float* out, int ostride,
+                hipStream_t st) {
+  if (n_fix == 0) return 0;
+  if (!partial || !fixups || !out) return set_error(REGCN_EINVAL, "null pointer");
+  if (width <= 0 || width > pstride || width > ostride) return set_error(REGCN_EINVAL, "bad partial-sum width");
+  dim3 g(grid_for(n_fix)), b(256);
+  hipLaunchKernelGGL(k_partial_sum, g, b, 0, st, partial, pstride, (const Fixup*)fixups, n_fix, width, out, ostride);
+  return check_launch("k_partial_sum");
 }
 
 int lorentz_sum(const float* x, const float* rel, const float* W, const int* col_src, const int* col_type,

@@ -100,6 +100,11 @@ int regcn_lorentz_aggregate_f32(const float* x, const float* rel, const float* w
                      partial_stride, out, ST(s));
 }
 
+int regcn_partial_sum_f32(const float* partial, int32_t partial_stride, const int32_t* fixups, int32_t n_fix,
+                          int32_t width, float* out, int32_t out_stride, void* s) {
+  return partial_sum(partial, partial_stride, fixups, n_fix, width, out, out_stride, ST(s));
+}
+
 size_t regcn_packed_weight_floats(int32_t d_in) { return packed_weight_floats(d_in); }
 
 int regcn_pack_weight_f32(const float* w, int32_t d_in, int32_t d_out, float* packed, void* s) {

@@ -116,35 +116,17 @@ class SnapshotGraph:
         np.cumsum(in_deg, out=rowptr[1:])
         self.chunk_edges = int(chunk_edges) if chunk_edges else chunk_size_for(E)
         chunks, fixups, nslot = _chunk_rows(rowptr, np.arange(V), self.chunk_edges)
-        pos = np.nonzero(in_deg > 0)[0]
-        pos = pos[np.argsort(-in_deg[pos], kind="stable")]  # in-degree descending (tile packing)
-        zero = np.nonzero(in_deg == 0)[0]
-        # fused-layer tiles (csrc/layer.hip): rows over the edge budget are pre-aggregated
-        self.budget = int(tile_budget) if tile_budget else tile_budget_for(
-            E, self.chunk_edges, int(in_deg.max()) if V else 0)
-        heavy = pos[in_deg[pos] > self.budget]
-        # small snapshots pack ~32 inline edges per tile (8 per wave = one batch in flight);
-        # a row up to the budget still sits alone in its own tile
-        self.pack_items = min(32, self.budget) if E <= 65536 else self.budget
-        tiles = _pack_tiles(np.where(in_deg[pos] > self.budget, 0, in_deg[pos]), self.pack_items)
-        hchunks, hfixups, hslot = _chunk_spans(rowptr[heavy], in_deg[heavy], heavy, self.chunk_edges)
-        # per-tile flattened in-edge lists of the inline rows (tile order = rows order):
-        # item_src, item_tl = type << 4 | tile-local row, item_ptr[t] = first item of tile t
-        inl = np.where(in_deg[pos] > self.budget, 0, in_deg[pos])
-        n_items = int(inl.sum())
-        first = np.cumsum(inl) - inl
-        perm = np.arange(n_items, dtype=np.int64) + np.repeat(rowptr[pos] - first, inl)
-        counts = tiles[:, 1].astype(np.int64) if len(tiles) else np.zeros(0, np.int64)
-        local = np.arange(len(pos)) - np.repeat(tiles[:, 0].astype(np.int64), counts) if len(tiles) else \
-            np.zeros(0, np.int64)
         col_src_s, col_type_s = src[order], etype[order]
         if len(etype) and int(etype.max()) >= 2 ** 27:
             raise ValueError("relation ids must be < 2^27")
-        item_src = col_src_s[perm].astype(np.int32)
-        item_tl = ((col_type_s[perm].astype(np.int64) << 4) | np.repeat(local, inl)).astype(np.int32)
-        item_ptr = np.zeros(len(tiles) + 1, dtype=np.int64)
-        if len(tiles):
-            item_ptr[1:] = np.cumsum(np.add.reduceat(inl, tiles[:, 0]))
+        # fused-layer work (csrc/layer.hip) over all nodes
+        self.budget = int(tile_budget) if tile_budget else tile_budget_for(
+            E, self.chunk_edges, int(in_deg.max()) if V else 0)
+        # small snapshots pack ~32 inline edges per tile (8 per wave = one batch in flight);
+        # a row up to the budget still sits alone in its own tile
+        self.pack_items = min(32, self.budget) if E <= 65536 else self.budget
+        fw = fused_work(np.arange(V), in_deg, rowptr, col_src_s, col_type_s, self.budget, self.pack_items,
+                        self.chunk_edges)
         R2 = 2 * self.num_rels
         rel_count = np.zeros(R2, dtype=np.float32)
         rel_start = np.zeros(R2, dtype=np.int64)
@@ -161,20 +143,16 @@ class SnapshotGraph:
         else:
             rchunks, rfix, rslot = np.zeros((0, 4), np.int32), np.zeros((0, 4), np.int32), 0
         self._host = {
-            "col_src": src[order].astype(np.int32), "col_type": etype[order].astype(np.int32),
+            "col_src": col_src_s.astype(np.int32), "col_type": col_type_s.astype(np.int32),
             "chunks": chunks, "fixups": fixups, "norm": norm,
-            "rows": np.concatenate([pos, zero]).astype(np.int32),
             "rel_idx": np.asarray(r_to_e, dtype=np.int32).reshape(-1),
             "rel_count": rel_count, "rel_chunks": rchunks, "rel_fixups": rfix,
             "rel_start": rel_start.astype(np.int32),
-            "rowptr": rowptr.astype(np.int32), "tiles": tiles,
-            "heavy_chunks": hchunks, "heavy_fixups": hfixups,
-            "item_src": item_src, "item_tl": item_tl, "item_ptr": item_ptr.astype(np.int32),
+            "rowptr": rowptr.astype(np.int32),
         }
-        self.n_pos = int(len(pos))
-        self.n_pos_tiles = int(len(tiles))
-        self.n_heavy = int(len(heavy))
-        self.heavy_slots = hslot
+        self._host.update(fw.host)
+        self.n_pos, self.n_pos_tiles = fw.n_pos, fw.n_pos_tiles
+        self.n_heavy, self.heavy_slots = fw.n_heavy, fw.heavy_slots
         self.n_slots = nslot
         self.rel_slots = rslot
         # relation spans short enough for the GRU kernel's in-kernel mean (csrc/relgru.hip)
@@ -219,6 +197,47 @@ class SnapshotGraph:
         if self.dev is None:
             raise ValueError("SnapshotGraph must be moved to a HIP device (g.to('cuda')) before message passing")
         return self.dev
+
+
+class FusedWork:
+    """Work lists of the fused layer kernel over a set of destination rows (all nodes of
+    a snapshot, or one rank's rows under the owner partition, parallel.py)."""
+
+    def __init__(self, host, n_pos, n_pos_tiles, n_heavy, heavy_slots):
+        self.host, self.n_pos, self.n_pos_tiles = host, n_pos, n_pos_tiles
+        self.n_heavy, self.heavy_slots = n_heavy, heavy_slots
+
+
+def fused_work(nodes, in_deg, rowptr, col_src_s, col_type_s, budget, pack_items, chunk_edges):
+    """rows: the nodes with in-degree > 0 sorted by in-degree (descending, stable), then the
+    rest; tiles packed under `pack_items` inline edges; rows over `budget` pre-aggregated
+    (heavy chunks); per-tile flattened in-edge items (item_src, item_tl = type << 4 |
+    tile-local row, item_ptr)."""
+    nodes = np.asarray(nodes, dtype=np.int64)
+    deg = in_deg[nodes]
+    pos = nodes[deg > 0]
+    pos = pos[np.argsort(-in_deg[pos], kind="stable")]
+    zero = nodes[deg == 0]
+    heavy = pos[in_deg[pos] > budget]
+    inl = np.where(in_deg[pos] > budget, 0, in_deg[pos])
+    tiles = _pack_tiles(inl, pack_items)
+    hchunks, hfixups, hslot = _chunk_spans(rowptr[heavy], in_deg[heavy], heavy, chunk_edges)
+    n_items = int(inl.sum())
+    first = np.cumsum(inl) - inl
+    perm = np.arange(n_items, dtype=np.int64) + np.repeat(rowptr[pos] - first, inl)
+    if len(tiles):
+        local = np.arange(len(pos)) - np.repeat(tiles[:, 0].astype(np.int64), tiles[:, 1].astype(np.int64))
+    else:
+        local = np.zeros(0, np.int64)
+    item_src = col_src_s[perm].astype(np.int32)
+    item_tl = ((col_type_s[perm].astype(np.int64) << 4) | np.repeat(local, inl)).astype(np.int32)
+    item_ptr = np.zeros(len(tiles) + 1, dtype=np.int64)
+    if len(tiles):
+        item_ptr[1:] = np.cumsum(np.add.reduceat(inl, tiles[:, 0]))
+    host = {"rows": np.concatenate([pos, zero]).astype(np.int32), "tiles": tiles, "heavy_chunks": hchunks,
+            "heavy_fixups": hfixups, "item_src": item_src, "item_tl": item_tl,
+            "item_ptr": item_ptr.astype(np.int32)}
+    return FusedWork(host, int(len(pos)), int(len(tiles)), int(len(heavy)), hslot)
 
 
 def tile_budget_for(num_edges, chunk_edges, max_deg=0):

@@ -13,6 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from .parallel import ShardedGraph
 from .tangent import attach, tangent_of
 from .weights import packed
 
@@ -78,16 +79,31 @@ class StepSpec:
 
 
 def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip, drop_mask, c,
-              euclid=False, step=None):
+              euclid=False, step=None, agg=None, out=None):
     """One fused layer launch (regcn_layer_f32): inline gather + GEMMs + epilogue, or with
-    `step` the timestep too.  Returns (h, x_next, r_next) of the layer (or of the step)."""
+    `step` the timestep too.  Returns (h, x_next, r_next) of the layer (or of the step).
+    `g` may be a rank's view of a snapshot (parallel.py): the launch covers its rows only,
+    writing them into full-size outputs (`out`, optional preallocated (h, x, r)).
+    agg (with mode AGG_NONE): the finished aggregation of every in-degree > 0 row."""
+    if isinstance(g, ShardedGraph):  # multi-GPU partition of the snapshot (parallel.py)
+        if agg is not None or out is not None:
+            raise ValueError("agg/out are managed by the sharded layer")
+        return g.run_layer(mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
+                           drop_mask, c, euclid=euclid, step=step)
     wk = g.work()
     V, d = x.shape
+    n_rows = int(wk["rows"].shape[0])
     a = _lib.addr
-    agg = _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c)
-    h = torch.empty_like(x)
-    xn = torch.empty_like(x)
-    rn = torch.empty(V, device=x.device, dtype=torch.float32)
+    if agg is None:
+        agg = _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c)
+    elif mode != _lib.AGG_NONE:
+        raise ValueError("a precomputed aggregation needs mode AGG_NONE")
+    if out is None:
+        h = torch.empty_like(x)
+        xn = torch.empty_like(x)
+        rn = torch.empty(V, device=x.device, dtype=torch.float32)
+    else:
+        h, xn, rn = out
     pk = [packed(w) for w in (w_n, w_loop, w_evolve, w_skip)]
     desc = _lib.LayerDesc()
     desc.agg_mode = mode
@@ -113,7 +129,7 @@ def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_
     desc.b_skip = a(b_skip)
     desc.drop_mask = a(drop_mask)
     desc.rows = a(wk["rows"], torch.int32)
-    desc.n_pos, desc.V, desc.d, desc.euclid = g.n_pos, V, d, int(bool(euclid))
+    desc.n_pos, desc.V, desc.d, desc.euclid = g.n_pos, n_rows, d, int(bool(euclid))
     desc.c = float(c)
     if step is None:
         desc.h_out, desc.x_next, desc.r_next = a(h), a(xn), a(rn)

@@ -284,3 +284,72 @@ def test_roth_query_kernel_matches_torch_sequence(golden, tag):
         s_rel_t = _RelDecoderBase.forward(rdec, emb, r_emb, at)
     assert_close(q, q_t, what="RotH query")
     assert_close(s_rel, s_rel_t, what="RotHRel scores")
+
+
+@pytest.mark.parametrize("kind", ["lorentz", "union", "euclid"])
+@pytest.mark.parametrize("partition,world", [("edge", 2), ("edge", 3), ("owner", 2), ("owner", 3)])
+def test_sharded_layer_ranks_simulated(kind, partition, world):
+    """Both multi-GPU partitions with the ranks run one after another on this device and
+    the collectives done by hand (sum of partials / union of node blocks): equal to the
+    unpartitioned layer (parallel.py)."""
+    import torch.nn.functional as F
+    from oracle import ops as O
+    from regcn_amd import _lib
+    from regcn_amd import graph as G
+    from regcn_amd.hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNLayer, run_layer
+    from regcn_amd.layers import UnionRGCNLayer
+    from regcn_amd.parallel import ShardedGraph
+    from regcn_amd.tangent import tangent_of
+    from regcn_amd.weights import packed
+    V, R, d = 3000, 60, 200
+    g = G.build_sub_graph(V, R, _zipf_snapshot(V, R, 20000, 11), True, DEV)
+    gen = torch.Generator().manual_seed(4)
+    rel = (torch.randn(2 * R, d, generator=gen) * 0.1).to(DEV)
+    torch.manual_seed(1)
+    if kind == "lorentz":
+        lay = LorentzRGCNLayer(d, d, 2 * R, 100, c=C, activation=F.rrelu, self_loop=True).to(DEV).eval()
+        mode, wn, wrel, nb, gamma = _lib.AGG_LORENTZ, None, lay.weight.detach().contiguous(), 100, 0.0
+    elif kind == "union":
+        lay = HyperbolicUnionRGCNLayer(d, d, 2 * R, c=C, activation=F.rrelu, self_loop=True,
+                                       radius_msg_gamma=0.15).to(DEV).eval()
+        mode, wn, wrel, nb, gamma = _lib.AGG_UNION, lay.weight_neighbor, None, 0, 0.15
+    else:
+        lay = UnionRGCNLayer(d, d, 2 * R, -1, activation=F.rrelu, self_loop=True).to(DEV).eval()
+        mode, wn, wrel, nb, gamma = _lib.AGG_EUCLID, lay.weight_neighbor, None, 0, 0.0
+    euclid = kind == "euclid"
+    if euclid:
+        x = (torch.randn(V, d, generator=gen) * 0.1).to(DEV)
+        r = None
+    else:
+        h = O.exp0(torch.randn(V, d, generator=gen) * 0.5, C).to(DEV)
+        x, r = tangent_of(h, C)
+    args = (rel, wrel, nb, gamma, wn, lay.loop_weight, lay.evolve_loop_weight, None, None, None, None, C)
+    with torch.no_grad():
+        ref = run_layer(mode, g, x, r, *args, euclid=euclid)[0]
+        shards = [ShardedGraph(g, partition, rank=k, world=world) for k in range(world)]
+        if partition == "edge":
+            Psum = sum(s.edge_partials(mode, x, r, rel, wrel, nb, gamma, C) for s in shards)
+            agg = shards[0].edge_finish(mode, Psum, x, r, rel, wrel, nb, gamma, C)
+            got = run_layer(_lib.AGG_NONE, g, x, r, *args, euclid=euclid, agg=agg)[0]
+        else:
+            got = torch.full_like(x, float("nan"))
+            xn, rn = torch.empty_like(x), torch.empty(V, device=DEV)
+            for s in shards:
+                run_layer(mode, s.view, x, r, *args, euclid=euclid, out=(got, xn, rn))
+    assert torch.isfinite(got).all()
+    assert_close(got, ref, what="%s %s x%d" % (kind, partition, world))
+
+
+@pytest.mark.parametrize("partition", ["edge", "owner"])
+def test_sharded_graph_model_predict_world1(golden, partition):
+    """HyperbolicRecurrentRGCN.predict over ShardedGraph snapshots (the dispatch the
+    torchrun job uses; world 1 without a process group) matches the golden."""
+    from regcn_amd.parallel import ShardedGraph
+    tag = "lgcn_roth"
+    z = golden("model_%s.npz" % tag)
+    m, glist, (V, R, d, T) = build_hyperbolic_model(z, tag, DEV)
+    sg = [ShardedGraph(g, partition) for g in glist]
+    with torch.no_grad():
+        _, score, score_rel = m.predict(sg, R, None, torch.from_numpy(z["test"]).to(DEV), True)
+    assert_close(score, z["score"], what="entity score")
+    assert_close(score_rel, z["score_rel"], what="relation score")

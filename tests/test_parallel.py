@@ -1,0 +1,128 @@
+"""Multi-GPU partitions (regcn_amd/parallel.py) on CPU: the plans, and the collectives of
+both partitions in a world-size-2 gloo job.  The per-rank compute between
+the collectives is the HIP library (covered on the GPU by test_gpu_parity.py, ranks
+simulated on one device); here a test-local segment sum stands in for it so that the
+partition + all-reduce / all-gather algebra is checked against the unpartitioned sum."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from regcn_amd import graph as G
+from regcn_amd import parallel as P
+
+
+def _snapshot(V=300, R=7, T=2500, seed=0):
+    rng = np.random.default_rng(seed)
+    p = 1.0 / np.arange(1, V + 1) ** 1.2
+    p /= p.sum()
+    tr = np.stack([rng.choice(V, T, p=p), rng.integers(0, R, T), rng.choice(V, T, p=p)], 1)
+    return G.build_sub_graph(V, R, tr, False, 0, chunk_edges=16)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_edge_plan_covers_every_edge_once(world):
+    g = _snapshot()
+    E = g.number_of_edges()
+    rowptr = g._host["rowptr"].astype(np.int64)
+    cov = np.zeros(E, dtype=np.int64)
+    for rank in range(world):
+        pl = P.EdgePlan(g, rank, world)
+        assert pl.e0 <= pl.e1 and pl.e1 - pl.e0 <= E // world + 1  # balanced by edges
+        slots = []
+        for row, b, e, s in pl.chunks:
+            assert rowptr[row] <= b < e <= rowptr[row + 1] and pl.e0 <= b and e <= pl.e1
+            assert e - b <= g.chunk_edges
+            cov[b:e] += 1
+            slots.append(s)
+        assert sorted(slots) == list(range(pl.n_slots))
+        for row, sb, se, _ in pl.fixups:  # each touched row sums exactly its own slots
+            assert set(pl.chunks[(pl.chunks[:, 0] == row), 3]) == set(range(sb, se))
+        fin = pl.finish
+        assert (fin[:, 1] == fin[:, 0]).all() and (fin[:, 2] == fin[:, 0] + 1).all()
+        np.testing.assert_array_equal(np.sort(fin[:, 0]), np.nonzero(g.in_deg_np > 0)[0])
+    assert (cov == 1).all()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_owner_views_partition_the_nodes(world):
+    g = _snapshot()
+    V = g.number_of_nodes()
+    seen = []
+    per, bounds = P.owner_bounds(V, world)
+    for rank in range(world):
+        v = P.OwnerView(g, rank, world)
+        rows = v.fw.host["rows"]
+        assert ((rows >= v.v0) & (rows < v.v1)).all() and v.v1 - v.v0 <= per
+        assert v.n_pos == int((g.in_deg_np[rows] > 0).sum())
+        # the view's items are exactly the in-edges of its inline rows
+        n_inline = int(np.where(g.in_deg_np[rows[:v.n_pos]] > g.budget, 0, g.in_deg_np[rows[:v.n_pos]]).sum())
+        assert v.fw.host["item_ptr"][-1] == n_inline
+        seen += rows.tolist()
+    assert sorted(seen) == list(range(V))
+
+
+def _segment_sum_slice(g, pl, x, rel):
+    """Test-local stand-in for the HIP partial kernels: raw Euclidean partial sums of the
+    plan's edge slice, summed per row (what regcn_partial_sum_f32 leaves in P)."""
+    src = torch.from_numpy(g._host["col_src"].astype(np.int64))
+    typ = torch.from_numpy(g._host["col_type"].astype(np.int64))
+    rowptr = g._host["rowptr"].astype(np.int64)
+    dst = torch.from_numpy(np.repeat(np.arange(len(rowptr) - 1), np.diff(rowptr)))
+    sl = slice(pl.e0, pl.e1)
+    out = torch.zeros(x.shape[0], x.shape[1], dtype=torch.float64)
+    out.index_add_(0, dst[sl], (x[src[sl]] + rel[typ[sl]]).double())
+    return out
+
+
+def _worker(rank, world, port, result_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = _snapshot()
+        V, d = g.number_of_nodes(), 12
+        gen = torch.Generator().manual_seed(5)
+        x = torch.randn(V, d, generator=gen)
+        rel = torch.randn(2 * g.num_rels, d, generator=gen)
+        # edge partition: every rank's partials, all-reduced, equal the full segment sum
+        pl = P.EdgePlan(g, rank, world)
+        part = _segment_sum_slice(g, pl, x, rel)
+        P.allreduce_partials(part)
+        full = _segment_sum_slice(g, P.EdgePlan(g, 0, 1), x, rel)
+        err_edge = float((part - full).abs().max())
+        # owner partition: each rank fills its node block, the all-gather rebuilds all rows
+        per, bounds = P.owner_bounds(V, world)
+        buf = torch.full((per * world, d), float("nan"))
+        ref = torch.arange(V * d, dtype=torch.float32).view(V, d)
+        buf[bounds[rank]:bounds[rank + 1]] = ref[bounds[rank]:bounds[rank + 1]]
+        P.allgather_rows(buf, per)
+        err_owner = float((buf[:V] - ref).abs().max())
+        result_q.put((rank, err_edge, err_owner))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_collectives_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted(q.get() for _ in range(2))
+    for rank, err_edge, err_owner in res:
+        assert err_edge < 1e-9, (rank, err_edge)
+        assert err_owner == 0.0, (rank, err_owner)
