@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work")
+    ap.add_argument("--shard", default="replica", choices=["replica", "edge", "owner"],
+                    help="multi-GPU: independent samples per rank (weak scaling), or every snapshot "
+                         "partitioned across the ranks by edges (all-reduce) / destination owner "
+                         "(all-gather) (strong scaling, SURVEY.md §8(e))")
     return ap.parse_args()
 
 
@@ -63,8 +67,9 @@ def build_model(cfg, d, device, seed):
     return m.to(device).eval()
 
 
-def make_samples(cfg, pool, device, seed):
+def make_samples(cfg, pool, device, seed, shard="replica"):
     from regcn_amd import graph as G
+    from regcn_amd.parallel import ShardedGraph
     from regcn_amd.synthetic import snapshot_series
     V, R, T = cfg["V"], cfg["R"], cfg["T"]
     snaps = snapshot_series(seed, V, R, T + pool, cfg["per_snap"])
@@ -72,6 +77,8 @@ def make_samples(cfg, pool, device, seed):
     for i in range(pool):
         hist = snaps[i:i + T]
         glist = [G.build_sub_graph(V, R, s, True, device) for s in hist]
+        if shard != "replica":
+            glist = [ShardedGraph(g, shard) for g in glist]
         test = torch.from_numpy(snaps[i + T]).to(device)
         out.append((hist, glist, test, snaps[i + T]))
     return out
@@ -145,6 +152,7 @@ def kernel_profile(model, sample, d, device):
     from regcn_amd.tangent import tangent_of
     from regcn_amd.weights import packed
     hist, glist, test, _ = sample
+    glist = [getattr(g, "g", g) for g in glist]  # rank 0 alone: unpartitioned (no collectives)
     g = glist[-1]
     V = g.number_of_nodes()
     E = g.number_of_edges()
@@ -243,7 +251,12 @@ def main():
     cfg = CONFIGS[args.config]
     d = args.d
     model = build_model(cfg, d, device, seed=1234)          # same weights on every rank
-    samples = make_samples(cfg, args.pool, device, seed=100 + 7919 * rank)  # independent data per rank
+    sharded = args.shard != "replica" and world > 1
+    # replicas: independent data per rank; sharded: every rank holds the same snapshots
+    samples = make_samples(cfg, args.pool, device, seed=100 if sharded else 100 + 7919 * rank,
+                           shard=args.shard if sharded else "replica")
+    if sharded:
+        args.no_graph = True  # collectives between the launches: eager
     R = cfg["R"]
 
     def eager(i):
@@ -297,6 +310,8 @@ def main():
         dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed, edges_total = float(tm[0]), float(t[1])
+        if sharded:  # every rank processed the same edges: count them once
+            edges_total = float(edges_local)
     else:
         edges_total = float(edges_local)
     value = edges_total / elapsed / 1e6
@@ -321,12 +336,14 @@ def main():
         ms = elapsed / args.steps * 1e3
         out = {"metric": METRIC, "value": round(value, 3), "unit": "M edges/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "f32",
                "data": "synthetic (%s-shaped snapshots, random-init weights)" % args.config.split("_")[0],
                "config": {"workload": cfg["label"], "V": cfg["V"], "R": cfg["R"], "triples_per_snapshot":
                           cfg["per_snap"], "history_len": cfg["T"], "n_layers": 2, "d": d,
                           "edges_per_step": int(np.mean(epw)), "queries_per_step": 2 * cfg["per_snap"],
-                          "hip_graph": bool(graphs), "parallelism": "replicas x%d" % world},
+                          "hip_graph": bool(graphs),
+                          "parallelism": ("%s-partitioned snapshots x%d" % (args.shard, world)) if sharded
+                          else "replicas x%d" % world},
                "roofline": roof, "kernels": kernels, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if world > 1:
