@@ -1,0 +1,265 @@
+"""`hyperbolic_main.py` command line on the HIP path (mirror of hyperbolic_src/hyperbolic_main.py
+:709-843, evaluation branch :60-161).
+
+    python -m regcn_amd.cli -d ICEWS14s --test --encoder lgcn --decoder roth --gpu 0 \
+        --data-dir ../data --checkpoint ../models/<name>
+
+Every reference flag is accepted with the reference default.  Datasets use the reference's
+on-disk format (`<data-dir>/<dataset>/{train,valid,test}.txt` rows `s\\tr\\to\\tt`,
+`entity2id.txt` / `relation2id.txt` `name\\tid`, opened read-only);
+`-d synthetic:<config>` evaluates a generated snapshot series of a
+`regcn_amd.synthetic.CONFIGS` shape instead.  Checkpoints are read with
+`torch.load(weights_only=True)` (`{'state_dict': ..., 'epoch': ...}` as the reference saves
+them); without one the model keeps its random initialisation.  Training (no `--test`) and
+the out-of-scope features (static graph, EST, fhnn/hgat, Riemannian Adam) raise: the HIP
+path is forward-only in this build.
+"""
+import argparse
+import logging
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+from . import ranking
+from .graph import build_sub_graph
+
+logger = logging.getLogger("regcn_amd.cli")
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="Hyperbolic Temporal RE-GCN (MI355X HIP path)")
+    a = p.add_argument
+    a("--gpu", type=int, default=-1)
+    a("--batch-size", type=int, default=1)
+    a("-d", "--dataset", type=str, required=True)
+    a("--test", action="store_true", default=False)
+    a("--run-analysis", action="store_true", default=False)
+    a("--multi-step", action="store_true", default=False)
+    a("--topk", type=int, default=10)
+    a("--add-static-graph", action="store_true", default=False)
+    a("--relation-evaluation", action="store_true", default=False)
+    a("--curvature", type=float, default=0.01)
+    a("--learn-curvature", action="store_true", default=False)
+    a("--curvature-min", type=float, default=1e-4)
+    a("--curvature-max", type=float, default=1e-1)
+    a("--curvature-warmup-epochs", type=int, default=0)
+    a("--disable-residual", action="store_true", default=False)
+    a("--radius-alpha", type=float, default=0.5)
+    a("--radius-beta", type=float, default=0.5)
+    a("--radius-min", type=float, default=0.5)
+    a("--radius-max", type=float, default=3.0)
+    a("--radius-lambda", type=float, default=0.02)
+    a("--radius-epsilon", type=float, default=0.1)
+    a("--radius-anchor-beta", type=float, default=1.0)
+    a("--radius-msg-gamma", type=float, default=0.15)
+    a("--weight", type=float, default=1)
+    a("--task-weight", type=float, default=0.7)
+    a("--discount", type=float, default=1)
+    a("--angle", type=int, default=10)
+    a("--encoder", type=str, default="hyperbolic_uvrgcn", choices=["hyperbolic_uvrgcn", "fhnn", "lgcn", "hgat"])
+    a("--attn-heads", type=int, default=4)
+    a("--dropout", type=float, default=0.2)
+    a("--skip-connect", action="store_true", default=False)
+    a("--n-hidden", type=int, default=200)
+    a("--opn", type=str, default="sub")
+    a("--n-bases", type=int, default=100)
+    a("--n-layers", type=int, default=2)
+    a("--self-loop", action="store_true", dest="self_loop", default=True)
+    a("--no-self-loop", action="store_false", dest="self_loop")
+    a("--layer-norm", action="store_true", default=False)
+    a("--relation-prediction", action="store_true", default=False)
+    a("--entity-prediction", action="store_true", default=False)
+    a("--n-epochs", type=int, default=500)
+    a("--lr", type=float, default=0.001)
+    a("--grad-norm", type=float, default=1.0)
+    a("--evaluate-every", type=int, default=1)
+    a("--triple-batch-size", type=int, default=64)
+    a("--decoder", type=str, default="hyperbolic_convtranse", choices=["hyperbolic_convtranse", "murp", "roth", "atth"])
+    a("--input-dropout", type=float, default=0.2)
+    a("--hidden-dropout", type=float, default=0.2)
+    a("--feat-dropout", type=float, default=0.2)
+    a("--query-chunk-size", type=int, default=128)
+    a("--candidate-chunk-size", type=int, default=256)
+    a("--hyp-init-scale", type=float, default=1e-3)
+    a("--hyp-score-scale-init", type=float, default=1.0)
+    a("--hyp-score-margin-init", type=float, default=1.0)
+    a("--plus-entity-euclidean-bias", action="store_true", default=False)
+    a("--plus-relation-specific-curvature", action="store_true", default=False)
+    a("--train-history-len", type=int, default=10)
+    a("--test-history-len", type=int, default=20)
+    a("--use-est", action="store_true", default=False)
+    a("--est-history-len", type=int, default=32)
+    a("--est-state-alpha", type=float, default=0.2)
+    a("--est-encoder", type=str, default="gru")
+    a("--use-time-aware-negative", action="store_true", default=False)
+    a("--verbose", action="store_true", default=False)
+    a("--log-file", action="store_true", default=False)
+    a("--log-interval", type=int, default=1)
+    a("--use-riemannian-adam", action="store_true", default=False)
+    # build-only options
+    a("--data-dir", type=str, default="../data", help="dataset root (reference: ../data)")
+    a("--checkpoint", type=str, default=None, help="state checkpoint (torch.save of {'state_dict', 'epoch'})")
+    a("--synthetic-snapshots", type=int, default=12, help="snapshots generated for -d synthetic:<config>")
+    return p
+
+
+def _unsupported(args):
+    bad = [("--add-static-graph", args.add_static_graph), ("--use-est", args.use_est),
+           ("--use-time-aware-negative", args.use_time_aware_negative),
+           ("--use-riemannian-adam", args.use_riemannian_adam),
+           ("--encoder %s" % args.encoder, args.encoder in ("fhnn", "hgat"))]
+    return [name for name, on in bad if on]
+
+
+def load_dataset(args):
+    """(num_nodes, num_rels, train, valid, test) with time in column 3 (reference
+    knowledge_graph.load_from_local / _read_triplets_as_list)."""
+    if args.dataset.startswith("synthetic:"):
+        from .synthetic import CONFIGS, snapshot_series
+        cfg = CONFIGS[args.dataset.split(":", 1)[1]]
+        snaps = snapshot_series(0, cfg["V"], cfg["R"], args.synthetic_snapshots, cfg["per_snap"])
+        rows = [np.concatenate([s, np.full((len(s), 1), t)], 1) for t, s in enumerate(snaps)]
+        n = len(rows)
+        tr, va = int(n * 0.7), int(n * 0.85)
+        cat = lambda rs: np.concatenate(rs) if rs else np.zeros((0, 4), np.int64)  # noqa: E731
+        return cfg["V"], cfg["R"], cat(rows[:tr]), cat(rows[tr:va]), cat(rows[va:])
+    root = os.path.join(args.data_dir, args.dataset)
+
+    def read(name):
+        with open(os.path.join(root, name), "r") as f:  # reference opens 'r+' (fails read-only)
+            return np.array([[int(v) for v in line.strip().split("\t")[:4]] for line in f if line.strip()],
+                            dtype=np.int64).reshape(-1, 4)
+
+    def count(name):
+        with open(os.path.join(root, name), "r") as f:
+            return sum(1 for line in f if line.strip())
+    return count("entity2id.txt"), count("relation2id.txt"), read("train.txt"), read("valid.txt"), read("test.txt")
+
+
+def radius_targets(snapshots, num_nodes, alpha=0.5, beta=0.5, radius_min=0.5, radius_max=3.0):
+    """hyperbolic_main.py:164-185 (_compute_radius_targets)."""
+    neigh = [set() for _ in range(num_nodes)]
+    freq = np.zeros(num_nodes, dtype=np.float64)
+    for snap in snapshots:
+        if len(snap) == 0:
+            continue
+        freq += np.bincount(snap[:, 0], minlength=num_nodes)
+        freq += np.bincount(snap[:, 2], minlength=num_nodes)
+        for s, d in zip(snap[:, 0].tolist(), snap[:, 2].tolist()):
+            neigh[s].add(d)
+            neigh[d].add(s)
+    deg = np.array([len(n) for n in neigh], dtype=np.float64)
+    score = alpha * np.log1p(deg) + beta * np.log1p(freq)
+    if score.max() - score.min() < 1e-9:
+        normed = np.full_like(score, 0.5)
+    else:
+        normed = (score - score.min()) / (score.max() - score.min())
+    return radius_min + (radius_max - radius_min) * normed
+
+
+def build_model(args, num_nodes, num_rels, train_list, device):
+    from .hyperbolic_model import HyperbolicRecurrentRGCN
+    rt = radius_targets(train_list, num_nodes, args.radius_alpha, args.radius_beta, args.radius_min,
+                        args.radius_max)
+    m = HyperbolicRecurrentRGCN(
+        decoder_name=args.decoder, encoder_name=args.encoder, num_ents=num_nodes, num_rels=num_rels,
+        num_static_rels=0, num_words=0, h_dim=args.n_hidden, opn=args.opn, sequence_len=args.train_history_len,
+        num_bases=args.n_bases, num_hidden_layers=args.n_layers, dropout=args.dropout, c=args.curvature,
+        self_loop=args.self_loop, skip_connect=args.skip_connect, layer_norm=args.layer_norm,
+        input_dropout=args.input_dropout, hidden_dropout=args.hidden_dropout, feat_dropout=args.feat_dropout,
+        weight=args.weight, discount=args.discount, angle=args.angle, use_static=False,
+        entity_prediction=args.entity_prediction, relation_prediction=args.relation_prediction,
+        use_cuda=device.type == "cuda", gpu=args.gpu, analysis=args.run_analysis,
+        learn_curvature=args.learn_curvature, use_residual_evolution=not args.disable_residual,
+        radius_target=rt.astype(np.float32), radius_lambda=args.radius_lambda, radius_min=args.radius_min,
+        radius_max=args.radius_max, radius_epsilon=args.radius_epsilon, radius_anchor_beta=args.radius_anchor_beta,
+        curvature_min=args.curvature_min, curvature_max=args.curvature_max, num_heads=args.attn_heads,
+        query_chunk_size=args.query_chunk_size, candidate_chunk_size=args.candidate_chunk_size,
+        hyp_init_scale=args.hyp_init_scale, hyp_score_scale_init=args.hyp_score_scale_init,
+        hyp_score_margin_init=args.hyp_score_margin_init,
+        use_entity_euclidean_bias=args.plus_entity_euclidean_bias,
+        use_relation_specific_curvature=args.plus_relation_specific_curvature,
+        radius_msg_gamma=args.radius_msg_gamma)
+    return m.to(device)
+
+
+def test(model, history_list, test_list, num_rels, num_nodes, device, all_ans_list, all_ans_r_list, args):
+    """hyperbolic_main.py:60-161: roll the history window over the test snapshots, predict,
+    rank (raw + time-filtered; entity and relation), return the four MRRs."""
+    ranks_raw, ranks_filter, ranks_raw_r, ranks_filter_r = [], [], [], []
+    model.eval()
+    input_list = [snap for snap in history_list[-args.test_history_len:]]
+    graphs = {}
+    with torch.no_grad():
+        for time_idx, test_snap in enumerate(test_list):
+            glist = []
+            for s in input_list:  # snapshot graphs cached by identity across the window
+                key = id(s)
+                if key not in graphs:
+                    graphs[key] = (s, build_sub_graph(num_nodes, num_rels, s, True, device))
+                glist.append(graphs[key][1])
+            tt = torch.from_numpy(np.asarray(test_snap, dtype=np.int64)).to(device)
+            test_triples, score, score_r = model.predict(glist, num_rels, None, tt, True)
+            _, _, rr, fr = ranking.get_total_rank(test_triples, score_r, all_ans_r_list[time_idx], 1000, 1)
+            ranks_raw_r.append(rr)
+            ranks_filter_r.append(fr)
+            _, _, re_, fe = ranking.get_total_rank(test_triples, score, all_ans_list[time_idx], 1000, 0)
+            ranks_raw.append(re_)
+            ranks_filter.append(fe)
+            if args.multi_step:
+                pred = (ranking.construct_snap_r(test_triples, num_nodes, num_rels, score_r, args.topk)
+                        if args.relation_evaluation else
+                        ranking.construct_snap(test_triples, num_nodes, num_rels, score, args.topk))
+                if len(pred):
+                    input_list.pop(0)
+                    input_list.append(pred)
+            else:
+                input_list.pop(0)
+                input_list.append(test_snap)
+            live = {id(s) for s in input_list}
+            graphs = {k: v for k, v in graphs.items() if k in live}
+    return (ranking.stat_ranks(ranks_raw, "raw_ent").item(), ranking.stat_ranks(ranks_filter, "filter_ent").item(),
+            ranking.stat_ranks(ranks_raw_r, "raw_rel").item(), ranking.stat_ranks(ranks_filter_r, "filter_rel").item())
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    logging.basicConfig(level=logging.DEBUG if args.verbose else logging.INFO, format="%(message)s")
+    bad = _unsupported(args)
+    if bad:
+        raise SystemExit("not supported in this build (SURVEY.md §2 out of scope): " + ", ".join(bad))
+    if not args.test:
+        raise SystemExit("training is not supported in this build: the HIP path is forward-only "
+                         "(backward kernels are SURVEY.md §8(f) row f1); run with --test")
+    if args.radius_msg_gamma < 0:
+        raise ValueError("--radius-msg-gamma must be non-negative (use 0 to disable the penalty)")
+    if not 0.0 <= args.radius_anchor_beta <= 1.0:
+        raise ValueError("--radius-anchor-beta must be in [0, 1]")
+    if args.gpu < 0 or not torch.cuda.is_available():
+        raise SystemExit("the HIP path needs a GPU (--gpu N); there is no CPU fallback")
+    device = torch.device("cuda", args.gpu)
+    torch.cuda.set_device(device)
+    num_nodes, num_rels, train, valid, test_data = load_dataset(args)
+    train_list = ranking.split_by_time(train)
+    valid_list = ranking.split_by_time(valid)
+    test_list = ranking.split_by_time(test_data)
+    logger.info("Dataset %s: %d entities, %d relations, %d/%d/%d snapshots", args.dataset, num_nodes, num_rels,
+                len(train_list), len(valid_list), len(test_list))
+    all_ans = ranking.load_all_answers_for_time_filter(test_data, num_rels, num_nodes, False)
+    all_ans_r = ranking.load_all_answers_for_time_filter(test_data, num_rels, num_nodes, True)
+    model = build_model(args, num_nodes, num_rels, train_list, device)
+    if args.checkpoint:
+        ck = torch.load(args.checkpoint, map_location=device, weights_only=True)
+        model.load_state_dict(ck["state_dict"] if "state_dict" in ck else ck)
+        logger.info("Load Model: %s. Using best epoch: %s", args.checkpoint, ck.get("epoch", "?"))
+    t0 = time.time()
+    res = test(model, train_list + valid_list, test_list, num_rels, num_nodes, device, all_ans, all_ans_r, args)
+    logger.info("MRR raw %.6f filter %.6f | relation raw %.6f filter %.6f | %.2f s", *res, time.time() - t0)
+    return res
+
+
+if __name__ == "__main__":
+    sys.exit(0 if main() else 1)

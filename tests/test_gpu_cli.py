@@ -1,0 +1,62 @@
+"""The hyperbolic_main.py evaluation path on HIP (regcn_amd.cli) and its MRR against the CPU
+oracle on the same model and snapshots (north star: MRR within +-0.002 of the reference)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def test_cli_eval_mrr_matches_oracle():
+    from oracle import graph as OG
+    from oracle import model as OM
+    from regcn_amd import cli, ranking
+    argv = ["-d", "synthetic:icews14s_lgcn_roth", "--test", "--gpu", "0", "--encoder", "lgcn", "--decoder", "roth",
+            "--n-hidden", "64", "--n-bases", "32", "--synthetic-snapshots", "8", "--test-history-len", "3",
+            "--relation-prediction", "--entity-prediction"]
+    args = cli.build_parser().parse_args(argv)
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    V, R, train, valid, test = cli.load_dataset(args)
+    tl, vl, te = (ranking.split_by_time(x) for x in (train, valid, test))
+    model = cli.build_model(args, V, R, tl, dev)
+    ans = ranking.load_all_answers_for_time_filter(test, R, V, False)
+    ans_r = ranking.load_all_answers_for_time_filter(test, R, V, True)
+    got = cli.test(model, tl + vl, te, R, V, dev, ans, ans_r, args)
+    assert all(0.0 < m <= 1.0 for m in got)
+
+    # the same rolling evaluation on the CPU oracle
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    ocfg = dict(c=args.curvature, n_layers=args.n_layers, n_bases=args.n_bases, radius_min=args.radius_min,
+                radius_max=args.radius_max, radius_epsilon=args.radius_epsilon,
+                radius_anchor_beta=args.radius_anchor_beta, radius_msg_gamma=args.radius_msg_gamma,
+                use_residual_evolution=True, layer_norm=False, encoder="lgcn", decoder="roth")
+    hist = (tl + vl)[-args.test_history_len:]
+    rk = {"re": [], "fe": [], "rr": [], "fr": []}
+    with torch.no_grad():
+        for i, snap in enumerate(te):
+            og = [OG.build_sub_graph(V, R, s) for s in hist]
+            all_tr, score, score_rel, _, _ = OM.hyperbolic_predict(sd, ocfg, og, torch.from_numpy(snap))
+            _, _, a, b = OM.total_rank(all_tr, score, OM.answers_for_filter(snap, R, False))
+            _, _, c, d = OM.total_rank(all_tr, score_rel, OM.answers_for_filter(snap, R, True), True)
+            rk["re"].append(a)
+            rk["fe"].append(b)
+            rk["rr"].append(c)
+            rk["fr"].append(d)
+            hist = hist[1:] + [snap]
+    ref = [float(torch.mean(1.0 / torch.cat(rk[k]).float())) for k in ("re", "fe", "rr", "fr")]
+    np.testing.assert_allclose(got, ref, atol=0.002)
+
+
+def test_cli_rejects_out_of_scope_flags():
+    from regcn_amd import cli
+    with pytest.raises(SystemExit):
+        cli.main(["-d", "synthetic:icews14s_lgcn_roth", "--test", "--gpu", "0", "--use-est"])
+    with pytest.raises(SystemExit):
+        cli.main(["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0"])  # training

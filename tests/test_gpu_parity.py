@@ -353,3 +353,21 @@ def test_sharded_graph_model_predict_world1(golden, partition):
         _, score, score_rel = m.predict(sg, R, None, torch.from_numpy(z["test"]).to(DEV), True)
     assert_close(score, z["score"], what="entity score")
     assert_close(score_rel, z["score_rel"], what="relation score")
+
+
+def test_total_rank_vs_golden(golden):
+    """get_total_rank (raw + time-filtered, entity and relation) against the reference's
+    ranks and MRRs (rgcn/utils.py:136-166) on the golden scores."""
+    from regcn_amd.ranking import get_total_rank, load_all_answers_for_filter
+    z = golden("rank.npz")
+    V, R = (int(v) for v in z["meta"])
+    tr = torch.from_numpy(z["all_triples"]).to(DEV)
+    ans_e = load_all_answers_for_filter(z["snap"], R, False)
+    ans_r = load_all_answers_for_filter(z["snap"], R, True)
+    mf, m, rank, frank = get_total_rank(tr, t(z["score"]), ans_e, 1000)
+    np.testing.assert_array_equal(rank.cpu().numpy(), z["rank"])
+    np.testing.assert_array_equal(frank.cpu().numpy(), z["frank"])
+    mfr, mr, rank_r, frank_r = get_total_rank(tr, t(z["score_rel"]), ans_r, 1000, rel_predict=1)
+    np.testing.assert_array_equal(rank_r.cpu().numpy(), z["rank_r"])
+    np.testing.assert_array_equal(frank_r.cpu().numpy(), z["frank_r"])
+    np.testing.assert_allclose([m, mf, mr, mfr], z["mrr"], rtol=1e-6)

@@ -142,3 +142,15 @@ def test_cpu_graph_has_no_kernel_path():
     g = G.build_sub_graph(10, 3, np.array([[0, 1, 2]]), False, 0)
     with pytest.raises(ValueError):
         g.work()
+
+
+def test_split_by_time_and_filter_answers():
+    """rgcn/utils.py:264-339 host helpers (no GPU)."""
+    from regcn_amd.ranking import load_all_answers_for_filter, split_by_time
+    data = np.array([[0, 1, 2, 5], [3, 1, 4, 5], [0, 2, 4, 7], [1, 0, 2, 9], [2, 0, 1, 9]])
+    snaps = split_by_time(data)
+    assert [s.tolist() for s in snaps] == [[[0, 1, 2], [3, 1, 4]], [[0, 2, 4]], [[1, 0, 2], [2, 0, 1]]]
+    ans = load_all_answers_for_filter(snaps[0], 10)
+    assert ans == {0: {1: {2}}, 2: {11: {0}}, 3: {1: {4}}, 4: {11: {3}}}
+    ans_r = load_all_answers_for_filter(snaps[0], 10, rel_p=True)
+    assert ans_r == {0: {2: {1}}, 2: {0: {11}}, 3: {4: {1}}, 4: {3: {11}}}
