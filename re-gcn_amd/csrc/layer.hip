@@ -1,12 +1,14 @@
 // Fused message-passing layer (+ timestep) kernels.
 //
-// One workgroup = 4 waves = one tile of up to 16 destination rows with all d columns:
-//   1. CSR gather: the tile's in-edges are flattened into one item list and split into 4
-//      contiguous ranges, one per wave; each wave keeps 4 edges in flight and does a
-//      segmented (per-row) reduction into its own LDS partial row, so a tile's hub and its
-//      single-edge rows cost the same wall time.  Partials are combined in wave order
-//      (deterministic, no atomics).  Rows with in-degree > budget were pre-aggregated by
-//      the chunked kernels (aggregate.hip) and are read back instead.
+// One workgroup = NWAVE = 4 waves = one tile of up to 16 destination rows with all d columns:
+//   1. CSR gather: the tile's in-edges are flattened into one item list and split into NWAVE
+//      contiguous ranges, one per wave; each wave keeps 4-8 edges in flight and does a
+//      segmented (per-row) reduction into LDS partial rows, so a tile's hub and its
+//      single-edge rows cost the same wall time.  Items are row-sorted, so wave w touches
+//      a row range starting at or after the last row of wave w - 1: partial slot i + w
+//      (row i, wave w) never collides, and TM + NWAVE - 1 slots hold every partial.  Partials are
+//      combined in wave order (deterministic, no atomics).  Rows with in-degree > budget
+//      were pre-aggregated by the chunked kernels (aggregate.hip) and are read back.
 //   2. Self-loop / neighbour GEMMs on fp32 MFMA (rowtile.h) from LDS tiles.
 //   3. Epilogue in registers: clamp, rrelu, dropout mask, exp0 -> h; then either the next
 //      layer's prologue (x = log0 h, r = |h|) or the whole timestep (time gate GEMM, radius
@@ -24,6 +26,9 @@
 
 namespace regcn {
 
+// partial slots of the gather (TM + NWAVE - 1), reused for the three operand tiles after it
+constexpr int PART_ROWS = (TM + NWAVE - 1) > 3 * TM ? (TM + NWAVE - 1) : 3 * TM;
+
 struct LdsLayout {
   int lda;
   int part, X, red, ints, xsh, total_bytes;  // float offsets; total in bytes
@@ -33,27 +38,25 @@ __host__ __device__ inline LdsLayout lds_layout(int d, bool gen_s) {
   LdsLayout L;
   L.lda = tile_lda(d);
   L.part = 0;
-  L.X = NWAVE * TM * L.lda;
+  L.X = PART_ROWS * L.lda;
   L.red = L.X + TM * L.lda;
   L.ints = L.red + RED_FLOATS;
-  L.xsh = L.ints + 32;  // trow[16], tmask[4] (+pad)
+  L.xsh = L.ints + 32;  // trow[16], tmask[NWAVE] (+pad)
   L.total_bytes = (L.xsh + (gen_s ? NWAVE * MAX_D : 0)) * 4;
   return L;
 }
 
 // ---------------------------------------------------------------------- timestep epilogue
-// ct: current_h rows (Poincare) in fragments; P: clamp(x_prev) tile in LDS.
-//   cur = project(ct); [LN: exp0(normalize(log0(cur)))]; ct = clamp(log0(cur))
-//   tw = sigmoid(P @ W_g + b_g);  h = project(exp0(tw * ct + (1 - tw) * P))
-//   residual: r = beta r_s + (1 - beta)|h| + clamp(log0(h) . w_r + b_r, +-eps_r); else r = r_s
-//   h = apply_radius(h, r); outputs h, x = log0(h), r = max(|h|, eps).
-// n2: |ct row|^2 on entry (known from the producer's row maps); the chain below needs
-// only two cross-wave reductions (the exp0 of the gated mix, the radius-MLP dot).
 __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4], const float* P, int lda,
-                                              const int* trow, int n_valid, const StepArgs& p) {
+                                              const int* trow, int n_valid, const StepArgs& p,
+                                              int64_t* trace = nullptr) {
+  auto stamp = [&](int k) {  // profiling: phase stamps 14, 15 (trace_mark)
+    if (trace && threadIdx.x == 0) trace[blockIdx.x * 16 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
   Frag tw;
   tw.zero();
   mfma_tile(tw, P, lda, p.w_g, p.d);
+  stamp(14);
   project_known(ct, n2, p.k);
   if (p.layer_norm) {
     log0_known(ct, n2, p.k);
@@ -63,10 +66,10 @@ __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4],
   log0_known(ct, n2, p.k);
   Frag pt;
   frag_from_tile(pt, P, lda, p.d);
-  float bg[4];
+  float bg[TPW];
   col_load(bg, p.b_g, p.d);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < TPW; ++j) {
     const f4 c4 = clamp4(ct.t[j], -10.f, 10.f);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -77,42 +80,31 @@ __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4],
   rr.sumsq(ct, n2);
   exp0_known(ct, n2, p.k);
   project_known(ct, n2, p.k);  // hyperbolic_model.py:860
-  float rs[4], newr[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = frag_row(r);
-    rs[r] = p.r_static[trow[i < n_valid ? i : 0]];
-  }
+  stamp(15);
+  // radius: per-row scalars once per lane, for its own row (rowtile.h own_row/spread_rows)
+  const int ri = frag_row(threadIdx.x & 3);
+  const float rs = p.r_static[trow[ri < n_valid ? ri : 0]];
+  const float n2o = own_row(n2);
+  float newr = rs;
   if (p.residual) {
-    float wr[4], dl[4];
+    float wr[TPW], dl[4], lf[4];
     col_load(wr, p.w_r, p.d);
+    spread_rows(log0_factor(n2o, p.k_rad), lf);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float f = log0_factor(n2[r], p.k_rad);
       float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) s += wr[j] * (ct.t[j][r] * f);
+      for (int j = 0; j < TPW; ++j) s += wr[j] * (ct.t[j][r] * lf[r]);
       dl[r] = s;
     }
     rr.allreduce(dl);
-    const float br = *p.b_r;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float delta = fminf(fmaxf(dl[r] + br, -p.eps_r), p.eps_r);
-      const float dyn = fmaxf(sqrtf(n2[r]), REGCN_EPS);
-      newr[r] = (p.beta * rs[r] + (1.f - p.beta) * dyn) + delta;
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) newr[r] = rs[r];
+    const float delta = fminf(fmaxf(own_row(dl) + *p.b_r, -p.eps_r), p.eps_r);
+    const float dyn = fmaxf(sqrtf(n2o), REGCN_EPS);
+    newr = (p.beta * rs + (1.f - p.beta) * dyn) + delta;
   }
-  float f[4];
   const Curv& kr = p.residual ? p.k_rad : p.k;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float n = fmaxf(sqrtf(n2[r]), REGCN_EPS);
-    f[r] = fminf(fmaxf(newr[r], REGCN_EPS), kr.rmax) / n;
-  }
+  float f[4];
+  spread_rows(fminf(fmaxf(newr, REGCN_EPS), kr.rmax) / fmaxf(sqrtf(n2o), REGCN_EPS), f);
   scale_known(ct, n2, f);
   frag_store(ct, p.h_out, trow, n_valid, p.d);
   if (p.r_out) store_radius(n2, p.r_out, trow, n_valid);
@@ -132,7 +124,7 @@ __device__ __forceinline__ void trace_mark(const LayerArgs& p, int k) {
 // the host-built per-tile list (item_src, item_tl = type << 4 | local row), so an edge's
 // row loads depend on one coalesced index load only.  Wave w reduces items [ib, ie), EB
 // edges in flight (all loads unconditional, clamped addresses); each row it touches gets
-// one partial row in part[w][i] (+ the Lorentz time coordinate at column d) and a bit in
+// one partial row in slot i + w (+ the Lorentz time coordinate at column d) and a bit in
 // tmask[w].
 template <int AGG, int S>
 __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int lda, const int* trow, int tile,
@@ -154,7 +146,7 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
   float acc0 = 0.f;
   auto flush = [&]() {
     if (cur >= 0) {
-      float* dst = part + (w * TM + cur) * lda;
+      float* dst = part + (cur + w) * lda;
       if (active) {
         dst[col] = acc.x;
         dst[col + 1] = acc.y;
@@ -272,26 +264,27 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
   if (lane == 0) tmask[w] = (int)mask;
 }
 
-// Combine the wave partials of row i (wave i % 4 does rows i, i+4, ...) and finish it:
+// Combine the wave partials of row i (wave w does rows w, w + NWAVE) and finish it:
 // Lorentz centroid -> log0, or norm-scaled sum; rows over budget read the pre-aggregated
-// row.  The result overwrites part[0][i] (the A operand / agg fragment source).
+// row.  The result overwrites slot i (the A operand / agg fragment source).
 template <int AGG>
 __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int lda, const int* trow, int count,
-                                            const int* tmask) {
+                                            const int* tmask, int rdeg, float rnorm) {
   const int lane = threadIdx.x & 63, w = wave_id();
   const int d = p.d;
   const int col = lane * 4, colc = min(col, d - 4);
   const bool active = col < d;
   const f4 zero = {0.f, 0.f, 0.f, 0.f};
-  // the wave's 4 rows side by side: independent loads and reductions (ILP 4)
-  f4 acc[4], pre[4];
-  float acc0[4];
-  bool heavy[4];
+  // the wave's rows side by side: independent loads and reductions
+  constexpr int RPW = TM / NWAVE;  // rows per wave
+  f4 acc[RPW], pre[RPW];
+  float acc0[RPW];
+  bool heavy[RPW];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < RPW; ++q) {
     const int i = w + NWAVE * q;
     const int row = trow[i < count ? i : 0];
-    heavy[q] = i < count && p.rowptr[row + 1] - p.rowptr[row] > p.budget;
+    heavy[q] = i < count && __builtin_amdgcn_readlane(rdeg, i) > p.budget;
     pre[q] = zero;
     if (heavy[q]) {  // pre-aggregated by the chunked kernels
       const f4 v = *reinterpret_cast<const f4*>(p.agg + (int64_t)row * d + colc);
@@ -301,21 +294,22 @@ __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int
     acc0[q] = 0.f;
 #pragma unroll
     for (int w2 = 0; w2 < NWAVE; ++w2) {
-      const bool on = (tmask[w2] >> i) & 1;  // slot written by wave w2 (else stale LDS)
-      const float* src = part + (w2 * TM + i) * lda;
-      const f4 v = {src[colc], src[colc + 1], src[colc + 2], src[colc + 3]};
-      acc[q] += (on && active) ? v : zero;
-      if (AGG == AGG_LORENTZ) acc0[q] += on ? src[d] : 0.f;
+      if ((tmask[w2] >> i) & 1) {  // slot i + w2 written by wave w2 (wave-uniform branch)
+        const float* src = part + (i + w2) * lda;
+        const f4 v = {src[colc], src[colc + 1], src[colc + 2], src[colc + 3]};
+        acc[q] += active ? v : zero;
+        if (AGG == AGG_LORENTZ) acc0[q] += src[d];
+      }
     }
   }
-  f4 out[4];
+  f4 out[RPW];
   if constexpr (AGG == AGG_LORENTZ) {
-    float ss[4], yy[4];
+    float ss[RPW], yy[RPW];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) ss[q] = row16_sum(dot4(acc[q], acc[q]));
-    f4 y[4];
+    for (int q = 0; q < RPW; ++q) ss[q] = row16_sum(dot4(acc[q], acc[q]));
+    f4 y[RPW];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < RPW; ++q) {
       const float s2 = (rlane(ss[q], 0) + rlane(ss[q], 16)) + (rlane(ss[q], 32) + rlane(ss[q], 48));
       const float ip = -acc0[q] * acc0[q] + s2;
       const float sc = sqrtf(fmaxf(-ip * p.k.c, REGCN_EPS));
@@ -324,19 +318,20 @@ __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int
       yy[q] = row16_sum(dot4(y[q], y[q]));
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < RPW; ++q) {
       const float n2 = (rlane(yy[q], 0) + rlane(yy[q], 16)) + (rlane(yy[q], 32) + rlane(yy[q], 48));
       out[q] = y[q] * log0_factor(n2, p.k);
     }
   } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < RPW; ++q) {
       const int i = w + NWAVE * q;
-      out[q] = acc[q] * p.norm[trow[i < count ? i : 0]];
+      out[q] = acc[q] * rlane(rnorm, i);
     }
   }
+  __syncthreads();  // every partial slot is read before any slot is overwritten
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < RPW; ++q) {
     const int i = w + NWAVE * q;
     f4 a = heavy[q] ? pre[q] : out[q];
     if (i >= count) a = zero;
@@ -388,6 +383,15 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
   if (threadIdx.x < TM) trow[threadIdx.x] = p.rows[start + ((int)threadIdx.x < count ? threadIdx.x : 0)];
   __syncthreads();
   mark(1);
+  // Per-row facts the finish needs (lane i < TM: tile row i), issued now so their latency
+  // hides under the gather rather than stalling the finish.
+  int rdeg = 0;
+  float rnorm = 1.f;
+  if constexpr (AGG != AGG_NONE) {
+    const int lrow = trow[min((int)(threadIdx.x & 63), TM - 1)];
+    rdeg = p.rowptr[lrow + 1] - p.rowptr[lrow];
+    if (AGG != AGG_LORENTZ) rnorm = p.norm[lrow];
+  }
 
   // ---- operands: self-loop rows; pre-aggregated rows (AGG_NONE); gather.  The first
   // GEMM's B ring is issued before the A tiles (it depends on nothing), except on tiles
@@ -407,7 +411,7 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
       tile_gather<AGG, S>(p, part, lda, trow, blockIdx.x, tmask, lds + L.xsh);
       __syncthreads();
       trace_mark(p, 12);
-      tile_finish<AGG>(p, part, lda, trow, count, tmask);
+      tile_finish<AGG>(p, part, lda, trow, count, tmask, rdeg, rnorm);
       trace_mark(p, 13);
     }
     if (STEP) stage_rows<true>(P2, lda, p.step.x_prev, trow, p.d, count);
@@ -425,7 +429,7 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
     else frag_from_tile(v, part, lda, p.d);
     if (!p.euclid) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v.t[j] = clamp4(v.t[j], -10.f, 10.f);
+      for (int j = 0; j < TPW; ++j) v.t[j] = clamp4(v.t[j], -10.f, 10.f);
     }
   }
   if (wsel) {
@@ -439,10 +443,10 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
     mfma_tile(g, P1, lda, p.w_skip, p.d);
     Frag pt;
     frag_from_tile(pt, P1, lda, p.d);
-    float b[4];
+    float b[TPW];
     col_load(b, p.b_skip, p.d);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < TPW; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float gt = sigmoidf(g.t[j][r] + b[j]);
@@ -450,7 +454,7 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
       }
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < TPW; ++j) {
     if (!p.euclid) v.t[j] = clamp4(v.t[j], -10.f, 10.f);
     v.t[j] = leaky4(v.t[j]);
   }
@@ -458,7 +462,7 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
     Frag m;
     frag_load(m, p.drop_mask, trow, count, p.d);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v.t[j] *= m.t[j];
+    for (int j = 0; j < TPW; ++j) v.t[j] *= m.t[j];
   }
   float n2[4];  // |row|^2 of v, carried through the row maps (rowtile.h)
   if (!p.euclid || p.r_next) rr.sumsq(v, n2);
@@ -466,7 +470,7 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
   mark(4);
 
   if constexpr (STEP) {
-    step_epilogue(rr, v, n2, P2, lda, trow, count, p.step);
+    step_epilogue(rr, v, n2, P2, lda, trow, count, p.step, p.trace);
   } else {
     frag_store(v, p.h_out, trow, count, p.d);
     if (p.r_next) store_radius(n2, p.r_next, trow, count);

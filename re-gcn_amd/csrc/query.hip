@@ -14,7 +14,7 @@
 //
 // Each workgroup (4 waves) owns 16 queries and all d columns (rowtile.h): the four small
 // GEMMs (fc1, fc2, rot_proj, trans_proj; nn.Linear weights packed transposed) run on fp32
-// MFMA from LDS tiles, the row maps reduce across the 4 waves through LDS.
+// MFMA from LDS tiles, the row maps reduce across the waves through LDS.
 #include "common.h"
 #include "regcn_internal.h"
 #include "rowtile.h"
@@ -26,10 +26,10 @@ __device__ __forceinline__ void linear(Frag& acc, const float* T, int lda, const
                                        int d_out) {
   acc.zero();
   mfma_tile(acc, T, lda, Wp, d);
-  float bb[4];
+  float bb[TPW];
   col_load(bb, b, d_out);
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < TPW; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc.t[j][r] += bb[j];
 }
@@ -39,7 +39,7 @@ __device__ __forceinline__ void frag_to_tile(const Frag& a, float* T, int lda, i
   for (int r = 0; r < 4; ++r) {
     float* row = T + frag_row(r) * lda;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < TPW; ++j) {
       const int col = frag_col(j);
       if (col < d) row[col] = a.t[j][r];
     }
@@ -53,7 +53,7 @@ template <typename AngleFn>
 __device__ __forceinline__ void givens(Frag& x, int d, AngleFn angle) {
   const bool odd = threadIdx.x & 1;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < TPW; ++j) {
     const int col = frag_col(j);
     const bool ok = col < d;
     const int k2 = min(col, d - 1) >> 1;
@@ -78,7 +78,7 @@ __device__ __forceinline__ void mobius_known(RowRed& rr, Frag& x, const float x2
   for (int r = 0; r < 4; ++r) {
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s += x.t[j][r] * y.t[j][r];
+    for (int j = 0; j < TPW; ++j) s += x.t[j][r] * y.t[j][r];
     xy[r] = s;
   }
   rr.allreduce(xy);
@@ -88,7 +88,7 @@ __device__ __forceinline__ void mobius_known(RowRed& rr, Frag& x, const float x2
     const float B = 1.f - k.c * x2[r];
     const float den = 1.f + 2.f * k.c * xy[r] + k.c * k.c * x2[r] * y2[r] + REGCN_EPS;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) x.t[j][r] = (A * x.t[j][r] + B * y.t[j][r]) / den;
+    for (int j = 0; j < TPW; ++j) x.t[j][r] = (A * x.t[j][r] + B * y.t[j][r]) / den;
     n2[r] = fmaxf(A * A * x2[r] + 2.f * A * B * xy[r] + B * B * y2[r], 0.f) / (den * den);
   }
   project_known(x, n2, k);
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(NTHR) void k_query(QueryArgs p) {
     for (int r = 0; r < 4; ++r) {
       float a = 0.f, b = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < TPW; ++j) {
         a += s.t[j][r] * s.t[j][r];
         b += o.t[j][r] * o.t[j][r];
       }
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(NTHR) void k_query(QueryArgs p) {
     frag_to_tile(ang, T2, lda, d / 2);
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) h1.t[j] = f4{fmaxf(h1.t[j].x, 0.f), fmaxf(h1.t[j].y, 0.f), fmaxf(h1.t[j].z, 0.f),
+  for (int j = 0; j < TPW; ++j) h1.t[j] = f4{fmaxf(h1.t[j].x, 0.f), fmaxf(h1.t[j].y, 0.f), fmaxf(h1.t[j].z, 0.f),
                                            fmaxf(h1.t[j].w, 0.f)};
   __syncthreads();  // every wave is done reading T0
   frag_to_tile(h1, T0, lda, d);
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(NTHR) void k_query(QueryArgs p) {
   Frag s2;
   linear(s2, T0, lda, p.w2, p.b2, d, d);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) s.t[j] += s2.t[j];
+  for (int j = 0; j < TPW; ++j) s.t[j] += s2.t[j];
 
   if (MODE == 0) {
     givens(s, d, [&](int r, int k2) { return T2[frag_row(r) * lda + k2]; });
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(NTHR) void k_query(QueryArgs p) {
     for (int r = 0; r < 4; ++r) {
       float a = 0.f, b = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < TPW; ++j) {
         a += s.t[j][r] * s.t[j][r];
         b += tr.t[j][r] * tr.t[j][r];
       }
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(NTHR) void k_query(QueryArgs p) {
     rr.sumsq(s, n2s);
     exp0_known(s, n2s, p.k);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s.t[j] = -s.t[j];
+    for (int j = 0; j < TPW; ++j) s.t[j] = -s.t[j];
     mobius_known(rr, s, n2s, o, n2o, p.k);
   }
   // store rows b0 .. b0 + nq - 1 (query order, not entity ids)
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(NTHR) void k_query(QueryArgs p) {
     const int i = frag_row(r);
     if (i >= nq) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < TPW; ++j) {
       const int col = frag_col(j);
       if (col < d) p.q_out[(int64_t)(b0 + i) * d + col] = s.t[j][r];
     }

@@ -25,18 +25,21 @@
 
 namespace regcn {
 
-__global__ __launch_bounds__(NTHR) void k_rel_gru(RelGruArgs p) {
+constexpr int GW = 4;  // waves per workgroup (the finish maps C register q to wave q)
+constexpr int GTHR = 64 * GW;
+
+__global__ __launch_bounds__(GTHR) void k_rel_gru(RelGruArgs p) {
   extern __shared__ float lds[];
   const int d = p.d, K = 3 * d, lda = tile_lda(K);
   float* A = lds;                      // TM x lda: [emb_rel | x_mean | h0]
-  f4* red = reinterpret_cast<f4*>(lds + TM * lda);  // [NWAVE][4 acc][64 lanes]
+  f4* red = reinterpret_cast<f4*>(lds + TM * lda);  // [GW][4 acc][64 lanes]
   const int lane = threadIdx.x & 63, w = wave_id();
   const int r0 = blockIdx.x * TM, jt = blockIdx.y;
   const int n_valid = min(TM, p.R2 - r0);
   const int col = lane * 4;
 
   // ---- stage the 16 A rows (wave w: rows w, w + 4, ...)
-  for (int i = w; i < TM; i += NWAVE) {
+  for (int i = w; i < TM; i += GW) {
     const int row = r0 + min(i, n_valid - 1);
     f4 e = load4(p.emb_rel + (int64_t)row * d, col, d);
     f4 h = load4(p.h_prev + (int64_t)row * d, col, d);
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(NTHR) void k_rel_gru(RelGruArgs p) {
   // ---- K split over the waves: steps [0, S_in) read W_ih, [S_in, S_in + S_h) W_hh
   const int S_in = (2 * d) >> 2, S_h = d >> 2, S = S_in + S_h;
   const int NT = (d + 15) >> 4;
-  const int sb = (S * w) / NWAVE, se = (S * (w + 1)) / NWAVE;
+  const int sb = (S * w) / GW, se = (S * (w + 1)) / GW;
   f4 ar = {0.f, 0.f, 0.f, 0.f}, az = ar, ai = ar, ah = ar;
   const float* arow = A + (lane & 15) * lda + (lane >> 4);
   const int gs_in = S_in * NT * 64, gs_h = S_h * NT * 64;  // per-gate stride of the packs
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(NTHR) void k_rel_gru(RelGruArgs p) {
   for (int a = 0; a < 4; ++a) {
     float t = 0.f;
 #pragma unroll
-    for (int w2 = 0; w2 < NWAVE; ++w2) t += red[(w2 * 4 + a) * 64 + lane][q];
+    for (int w2 = 0; w2 < GW; ++w2) t += red[(w2 * 4 + a) * 64 + lane][q];
     v[a] = t;
   }
   const int i = 4 * (lane >> 4) + q;
@@ -188,8 +191,8 @@ int rel_gru(const RelGruArgs& a, hipStream_t st) {
     return set_error(REGCN_EINVAL, "relation GRU needs x_mean or the r_to_e spans");
   if (a.R2 == 0) return 0;
   dim3 grid((unsigned)((a.R2 + TM - 1) / TM), (unsigned)((a.d + 15) / 16));
-  const size_t lds = (size_t)TM * tile_lda(3 * a.d) * 4 + (size_t)NWAVE * 4 * 64 * 16;
-  hipLaunchKernelGGL(k_rel_gru, grid, dim3(NTHR), lds, st, a);
+  const size_t lds = (size_t)TM * tile_lda(3 * a.d) * 4 + (size_t)GW * 4 * 64 * 16;
+  hipLaunchKernelGGL(k_rel_gru, grid, dim3(GTHR), lds, st, a);
   return check_launch("k_rel_gru");
 }
 

@@ -1,42 +1,58 @@
-// Row-tile MFMA building blocks shared by the fused row kernels (rowgemm.hip, layer.hip,
-// relgru.hip, query.hip).
+// Row-tile MFMA building blocks shared by the fused row kernels (layer.hip, query.hip).
 //
-// A workgroup of 4 waves owns a tile of TM = 16 rows and all d <= 256 output columns;
-// wave w owns the four 16-column MFMA tiles [64w, 64w + 64).  An A operand (16 x d) sits
+// A workgroup of NWAVE = 4 waves owns a tile of TM = 16 rows and all d <= 256 output
+// columns; wave w owns TPW = 16 / NWAVE sixteen-column MFMA tiles.  (8 waves x 2 tiles was
+// measured slower: at ~180 VGPRs one 8-wave workgroup fills a CU, so its barriers and
+// serial phases no longer overlap with a second workgroup's.)  An A operand (16 x d) sits
 // in LDS with a row stride `lda` = 2 (mod 32) floats, so the 16 rows x 4 k-offsets one
 // MFMA step reads fall in distinct banks.  B operands are weights prepacked into MFMA
-// fragment order (k_pack_weight, rowgemm.hip):
+// fragment order (k_pack_weight, layer.hip):
 //     Wp[s][jq][lane][e] = W[4s + lane/16][16(4jq + e) + lane%16]
-// so at k-step s wave w reads one coalesced float4 per lane, Wp[s][w][lane].
+// so at k-step s a wave reads one coalesced TPW-float vector per lane.
 //
 // MFMA: v_mfma_f32_16x16x4_f32.  C/D layout: lane l holds rows 4*(l>>4)+r (r = 0..3) and
 // column 16j + (l & 15) of tile j; a row's 16 lanes are one DPP row (row16_sum).
 #pragma once
 #include "common.h"
 
+// Waves per workgroup: 4 by default; a translation unit whose grids are small (query.hip)
+// may define REGCN_ROWTILE_WAVES (8 or 16) before the include for shorter per-wave chains.
+// The helpers live in an inline namespace per wave count, so units built with different
+// counts never share a definition.
+#ifndef REGCN_ROWTILE_WAVES
+#define REGCN_ROWTILE_WAVES 4
+#endif
+#define REGCN_RT_CAT2(a, b) a##b
+#define REGCN_RT_CAT(a, b) REGCN_RT_CAT2(a, b)
+
 namespace regcn {
+inline namespace REGCN_RT_CAT(rowtile_w, REGCN_ROWTILE_WAVES) {
 
 constexpr int MAX_D = 256;
 constexpr int TM = 16;         // rows per workgroup
-constexpr int NWAVE = 4;       // waves per workgroup (= 64-column groups)
+constexpr int NWAVE = REGCN_ROWTILE_WAVES;
+static_assert(NWAVE == 4 || NWAVE == 8 || NWAVE == 16, "row tiles split 16 column tiles over 4, 8 or 16 waves");
+constexpr int TPW = 16 / NWAVE;  // 16-column MFMA tiles per wave
 constexpr int NTHR = 64 * NWAVE;
 constexpr int RING = 8;        // k-steps of B fragments in flight per wave
 constexpr int RED_FLOATS = 4 * NWAVE * TM;  // RowRed scratch (2 buffers x 2 quantities)
+
+typedef float bvec __attribute__((ext_vector_type(TPW)));
 
 // LDS row stride for width d: smallest value >= d + 2 that is 2 (mod 32).
 __host__ __device__ constexpr int tile_lda(int d) { return d + 2 + ((32 - (d + 2) % 32) % 32); }
 
 struct Frag {
-  f4 t[4];
+  f4 t[TPW];
   __device__ __forceinline__ void zero() {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) t[j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TPW; ++j) t[j] = f4{0.f, 0.f, 0.f, 0.f};
   }
 };
 
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 __device__ __forceinline__ int frag_row(int r) { return 4 * ((threadIdx.x & 63) >> 4) + r; }
-__device__ __forceinline__ int frag_col(int jl) { return 64 * wave_id() + 16 * jl + (threadIdx.x & 15); }
+__device__ __forceinline__ int frag_col(int jl) { return 16 * (TPW * wave_id() + jl) + (threadIdx.x & 15); }
 
 // Stage rows A[rows[i]] (i < n_valid; row-major, width d) into the LDS tile T; rows past
 // n_valid are zero.  All loads are issued (clamped addresses) before the LDS stores.
@@ -68,33 +84,38 @@ __device__ __forceinline__ void stage_rows(float* T, int lda, const float* __res
   }
 }
 
-__device__ __forceinline__ void mfma4(Frag& acc, float a, f4 b) {
-  acc.t[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b.x, acc.t[0], 0, 0, 0);
-  acc.t[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b.y, acc.t[1], 0, 0, 0);
-  acc.t[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b.z, acc.t[2], 0, 0, 0);
-  acc.t[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b.w, acc.t[3], 0, 0, 0);
+__device__ __forceinline__ void mfma_tpw(Frag& acc, float a, bvec b) {
+#pragma unroll
+  for (int j = 0; j < TPW; ++j) acc.t[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[j], acc.t[j], 0, 0, 0);
 }
+
+// This wave's B fragments in the packed layout: k-step s lives at bsrc + s * B_STEP.
+__device__ __forceinline__ const bvec* bsrc_of(const float* __restrict__ Wp) {
+  const int tile0 = TPW * wave_id();
+  return reinterpret_cast<const bvec*>(Wp + ((tile0 / 4) * 64 + (threadIdx.x & 63)) * 4 + (tile0 % 4));
+}
+constexpr int B_STEP = 4 * 64 * 4 / TPW;  // bvec elements per k-step of the packed matrix
 
 // The first RING B fragments of a packed weight, loaded ahead of the A tile (they do not
 // depend on it), so the MFMA chain starts without a load latency.
 struct BRing {
-  f4 ring[RING];
+  bvec ring[RING];
   __device__ __forceinline__ void load(const float* __restrict__ Wp, int d) {
-    const f4* bsrc = reinterpret_cast<const f4*>(Wp) + wave_id() * 64 + (threadIdx.x & 63);
+    const bvec* bsrc = bsrc_of(Wp);
     const int S = d >> 2;
 #pragma unroll
-    for (int i = 0; i < RING; ++i) ring[i] = bsrc[(int64_t)min(i, S - 1) * 256];
+    for (int i = 0; i < RING; ++i) ring[i] = bsrc[(int64_t)min(i, S - 1) * B_STEP];
   }
 };
 
 // acc += T[16 x d] @ W (T in LDS, W packed with d_in = d), ring pre-filled by BRing::load.
 __device__ __forceinline__ void mfma_tile_pf(Frag& acc, const float* T, int lda, const float* __restrict__ Wp, int d,
                                              BRing& br) {
-  const int lane = threadIdx.x & 63, w = wave_id();
+  const int lane = threadIdx.x & 63;
   const int S = d >> 2;
-  const f4* bsrc = reinterpret_cast<const f4*>(Wp) + w * 64 + lane;  // + s * 256
+  const bvec* bsrc = bsrc_of(Wp);
   const float* arow = T + (lane & 15) * lda + (lane >> 4);
-  f4* ring = br.ring;
+  bvec* ring = br.ring;
   // A operands ride in their own ring, RING k-steps ahead: an LDS read right before its
   // MFMA would expose the ds_read latency on every step (the sched barriers keep order).
   float aring[RING];
@@ -104,17 +125,17 @@ __device__ __forceinline__ void mfma_tile_pf(Frag& acc, const float* T, int lda,
   for (; s + RING <= S; s += RING) {
 #pragma unroll
     for (int i = 0; i < RING; ++i) {
-      mfma4(acc, aring[i], ring[i]);
+      mfma_tpw(acc, aring[i], ring[i]);
       __builtin_amdgcn_sched_barrier(0);
       const int nx = min(s + i + RING, S - 1);
-      ring[i] = bsrc[(int64_t)nx * 256];  // unconditional: hipcc can count it
+      ring[i] = bsrc[(int64_t)nx * B_STEP];  // unconditional: hipcc can count it
       aring[i] = arow[4 * nx];
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 #pragma unroll
   for (int i = 0; i < RING; ++i)
-    if (s + i < S) mfma4(acc, aring[i], ring[i]);
+    if (s + i < S) mfma_tpw(acc, aring[i], ring[i]);
 }
 
 // acc += T[16 x d] @ W.  No barriers inside.
@@ -124,11 +145,21 @@ __device__ __forceinline__ void mfma_tile(Frag& acc, const float* T, int lda, co
   mfma_tile_pf(acc, T, lda, Wp, d, br);
 }
 
-// Cross-wave row reductions: per-wave partials -> LDS red[buf][wave][row] -> sum.
-// Two buffers alternate so one barrier per reduction suffices.
+// Cross-wave row reductions: per-wave partials -> LDS red[buf][wave][row] -> sum in wave
+// order (deterministic).  Two buffers alternate so one barrier per reduction suffices.
 struct RowRed {
   float* red;  // LDS, RED_FLOATS: 2 buffers x (2 quantities x NWAVE x TM)
   int buf;
+  __device__ __forceinline__ static float sum_waves(const float* b, int i) {  // pairwise tree
+    float v[NWAVE];
+#pragma unroll
+    for (int w = 0; w < NWAVE; ++w) v[w] = b[w * TM + i];
+#pragma unroll
+    for (int h = 1; h < NWAVE; h *= 2)
+#pragma unroll
+      for (int w = 0; w + h < NWAVE; w += 2 * h) v[w] += v[w + h];
+    return v[0];
+  }
   __device__ __forceinline__ void allreduce(float part[4]) {
     const int lane = threadIdx.x & 63, w = wave_id();
     float* b = red + buf * 2 * NWAVE * TM;
@@ -140,10 +171,7 @@ struct RowRed {
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = frag_row(r);
-      part[r] = (b[i] + b[TM + i]) + (b[2 * TM + i] + b[3 * TM + i]);
-    }
+    for (int r = 0; r < 4; ++r) part[r] = sum_waves(b, frag_row(r));
     buf ^= 1;
   }
   // two independent per-row sums in one barrier (uses both halves of the buffer pair)
@@ -166,9 +194,8 @@ struct RowRed {
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = frag_row(r);
-      pa[r] = (ba[i] + ba[TM + i]) + (ba[2 * TM + i] + ba[3 * TM + i]);
-      pb[r] = (bb[i] + bb[TM + i]) + (bb[2 * TM + i] + bb[3 * TM + i]);
+      pa[r] = sum_waves(ba, frag_row(r));
+      pb[r] = sum_waves(bb, frag_row(r));
     }
     buf ^= 1;
   }
@@ -177,7 +204,7 @@ struct RowRed {
     for (int r = 0; r < 4; ++r) {
       float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) s += a.t[j][r] * a.t[j][r];
+      for (int j = 0; j < TPW; ++j) s += a.t[j][r] * a.t[j][r];
       out[r] = s;
     }
     allreduce(out);
@@ -188,7 +215,12 @@ struct RowRed {
 // A row map scales each row by a factor of its norm, so the norm after the map follows
 // analytically (|f x| = f |x|): chains of maps need one cross-wave reduction, not one per
 // map.  n2[r] is |row|^2 of fragment row r, updated in place.
-__device__ __forceinline__ void row_scale(Frag& a, const float f[4]);
+__device__ __forceinline__ void row_scale(Frag& a, const float f[4]) {
+#pragma unroll
+  for (int j = 0; j < TPW; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a.t[j][r] *= f[r];
+}
 
 __device__ __forceinline__ void scale_known(Frag& a, float n2[4], const float f[4]) {
   row_scale(a, f);
@@ -196,73 +228,57 @@ __device__ __forceinline__ void scale_known(Frag& a, float n2[4], const float f[
   for (int r = 0; r < 4; ++r) n2[r] *= f[r] * f[r];
 }
 
+// Per-row scalars are uniform over a row's 16 lanes, and lane l holds rows 4(l>>4) + r,
+// r = 0..3.  Rather than evaluating a factor (sqrt, tanh, atanh, divisions: ~100 VALU
+// instructions) for all four rows in every lane, lane l evaluates it once, for its own row
+// r = l & 3 (own_row), and each lane then takes row r's result from lane r of its DPP row
+// (row_newbcast, one VALU op): a quarter of the transcendental work, bit-identical values.
+__device__ __forceinline__ float own_row(const float v[4]) {
+  // a two-level select tree (a select chain on r == k is turned into a scratch array)
+  const bool b0 = threadIdx.x & 1, b1 = threadIdx.x & 2;
+  const float lo = b0 ? v[1] : v[0], hi = b0 ? v[3] : v[2];
+  return b1 ? hi : lo;
+}
+template <int L>
+__device__ __forceinline__ float row_bcast(float v) {  // lane L of each 16-lane DPP row
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + L, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void spread_rows(float y, float out[4]) {
+  out[0] = row_bcast<0>(y);
+  out[1] = row_bcast<1>(y);
+  out[2] = row_bcast<2>(y);
+  out[3] = row_bcast<3>(y);
+}
+
 __device__ __forceinline__ void project_known(Frag& a, float n2[4], const Curv& k) {
   float f[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) f[r] = project_factor(n2[r], k);
+  spread_rows(project_factor(own_row(n2), k), f);
   scale_known(a, n2, f);
 }
 
 __device__ __forceinline__ void log0_known(Frag& a, float n2[4], const Curv& k) {
   float f[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) f[r] = log0_factor(n2[r], k);
+  spread_rows(log0_factor(own_row(n2), k), f);
   scale_known(a, n2, f);
 }
 
 __device__ __forceinline__ void exp0_known(Frag& a, float n2[4], const Curv& k) {  // exp0 + project
-  float f[4], o[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) f[r] = exp0_factor(n2[r], k, &o[r]);
+  float f[4], o;
+  spread_rows(exp0_factor(own_row(n2), k, &o), f);
   row_scale(a, f);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) n2[r] = o[r];
+  spread_rows(o, n2);
 }
 
 __device__ __forceinline__ void normalize_known(Frag& a, float n2[4]) {  // F.normalize, eps 1e-12
   float f[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) f[r] = 1.0f / fmaxf(sqrtf(n2[r]), 1e-12f);
+  spread_rows(1.0f / fmaxf(sqrtf(own_row(n2)), 1e-12f), f);
   scale_known(a, n2, f);
 }
 
-__device__ __forceinline__ void row_scale(Frag& a, const float f[4]) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) a.t[j][r] *= f[r];
-}
-
-__device__ __forceinline__ void frag_log0(RowRed& rr, Frag& a, const Curv& k) {
-  float n2[4], f[4];
-  rr.sumsq(a, n2);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) f[r] = log0_factor(n2[r], k);
-  row_scale(a, f);
-}
-
 __device__ __forceinline__ void frag_exp0(RowRed& rr, Frag& a, const Curv& k) {
-  float n2[4], f[4];
+  float n2[4];
   rr.sumsq(a, n2);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) f[r] = exp0_factor(n2[r], k);
-  row_scale(a, f);
-}
-
-__device__ __forceinline__ void frag_project(RowRed& rr, Frag& a, const Curv& k) {
-  float n2[4], f[4];
-  rr.sumsq(a, n2);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) f[r] = project_factor(n2[r], k);
-  row_scale(a, f);
-}
-
-__device__ __forceinline__ void frag_normalize(RowRed& rr, Frag& a) {  // F.normalize, eps 1e-12
-  float n2[4], f[4];
-  rr.sumsq(a, n2);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) f[r] = 1.0f / fmaxf(sqrtf(n2[r]), 1e-12f);
-  row_scale(a, f);
+  exp0_known(a, n2, k);
 }
 
 // Fragment of a row-major matrix (width d) for the tile's rows: unconditional loads from
@@ -274,7 +290,7 @@ __device__ __forceinline__ void frag_load(Frag& a, const float* __restrict__ M, 
     const bool ok = i < n_valid;
     const int64_t base = (int64_t)rows[ok ? i : 0] * d;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < TPW; ++j) {
       const int col = frag_col(j);
       const float v = M[base + min(col, d - 1)];
       a.t[j][r] = (ok && col < d) ? v : 0.f;
@@ -283,9 +299,9 @@ __device__ __forceinline__ void frag_load(Frag& a, const float* __restrict__ M, 
 }
 
 // Per-column vector (bias / weight row) in the fragment's column order.
-__device__ __forceinline__ void col_load(float out[4], const float* __restrict__ v, int d) {
+__device__ __forceinline__ void col_load(float out[TPW], const float* __restrict__ v, int d) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < TPW; ++j) {
     const int col = frag_col(j);
     const float x = v[min(col, d - 1)];
     out[j] = col < d ? x : 0.f;
@@ -298,7 +314,7 @@ __device__ __forceinline__ void frag_from_tile(Frag& a, const float* T, int lda,
   for (int r = 0; r < 4; ++r) {
     const float* row = T + frag_row(r) * lda;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < TPW; ++j) {
       const int col = frag_col(j);
       const float v = row[min(col, lda - 1)];
       a.t[j][r] = col < d ? v : 0.f;
@@ -313,7 +329,7 @@ __device__ __forceinline__ void frag_store(const Frag& a, float* __restrict__ M,
     if (i >= n_valid) continue;
     const int64_t base = (int64_t)rows[i] * d;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < TPW; ++j) {
       const int col = frag_col(j);
       if (col < d) M[base + col] = a.t[j][r];
     }
@@ -331,4 +347,5 @@ __device__ __forceinline__ void store_radius(const float n2[4], float* __restric
   }
 }
 
+}  // namespace rowtile_w<N>
 }  // namespace regcn

@@ -54,7 +54,55 @@ def run(V, R, per_snap, d=200, nb=100):
              t_gru * 1e3), flush=True)
 
 
+def trace(V=7128, R=230, per_snap=246, d=200, nb=100):
+    """Per-workgroup phase stamps (s_memrealtime, 10 ns) of the fused Lorentz layer + step
+    kernel (layer.hip trace_mark): where the critical path of a small snapshot goes."""
+    from regcn_amd import hyperbolic_layers as HL
+    snaps = snapshot_series(0, V, R, 1, per_snap)
+    g = G.build_sub_graph(V, R, snaps[0], True, dev)
+    torch.manual_seed(0)
+    h = H.exp_map_zero(torch.randn(V, d, device=dev) * 0.3, C)
+    rel = torch.randn(2 * R, d, device=dev) * 0.1
+    lor = LorentzRGCNLayer(d, d, 2 * R, nb, c=C, activation=F.rrelu, self_loop=True).to(dev).eval()
+    xp = torch.randn(V, d, device=dev) * 0.1
+    step = StepSpec(xp, packed(torch.randn(d, d, device=dev) * 0.05), torch.zeros(d, device=dev),
+                    torch.rand(V, device=dev) + 0.5, torch.randn(d, device=dev) * 0.01, torch.zeros(1, device=dev),
+                    0.1, 1.0, False, True, C)
+    n_wg = g.n_pos_tiles + (V - g.n_pos + 15) // 16
+    for name, kw in (("layer", {}), ("layer+step", {"step": step})):
+        with torch.no_grad():
+            for _ in range(3):
+                lor(g, h, rel, **kw)
+            HL.TRACE = torch.zeros(n_wg * 16, dtype=torch.int64, device=dev)
+            lor(g, h, rel, **kw)
+            torch.cuda.synchronize()
+            t = HL.TRACE.view(n_wg, 16).cpu().double()
+            HL.TRACE = None
+        t0 = t[:, 0].min()
+        us = lambda a, b, sel: ((t[sel, b] - t[sel, a]) / 100.0)  # 100 MHz -> us
+        pos = torch.arange(n_wg) < g.n_pos_tiles
+        print("%s V=%d pos tiles=%d zero tiles=%d total %.1f us (first start -> last end)"
+              % (name, V, int(pos.sum()), int((~pos).sum()), float((t[:, 5].max() - t0) / 100.0)))
+        for label, sel in (("pos", pos), ("zero", ~pos)):
+            if not sel.any():
+                continue
+            start = (t[sel, 0] - t0) / 100.0
+            ph = [("start", start), ("rows", us(0, 1, sel)), ("operands", us(1, 2, sel)), ("gemm", us(2, 3, sel)),
+                  ("act", us(3, 4, sel)), ("epilogue", us(4, 5, sel))]
+            if label == "pos":
+                ph += [("g.idx", us(8, 9, sel)), ("g.loop", us(9, 11, sel)), ("g.sync", us(11, 12, sel)),
+                       ("g.finish", us(12, 13, sel))]
+            if name == "layer+step":
+                ph += [("s.gemm", us(4, 14, sel)), ("s.gate", us(14, 15, sel)), ("s.radius", us(15, 5, sel))]
+            print("  %-4s " % label + " ".join("%s %.2f/%.2f" % (k, float(v.median()), float(v.max())) for k, v in ph))
+        clk = (t[:, 7] - t[:, 6]) / ((t[:, 5] - t[:, 0]).clamp(min=1) / 100.0)
+        print("  shader clock ~%.0f MHz (median over workgroups)" % float(clk.median()))
+
+
 if __name__ == "__main__":
+    if "--trace" in sys.argv:
+        trace()
+        sys.exit(0)
     print("peaks: %.1f TF fp32 MFMA, %.0f GB/s HBM" % (FP32_MFMA_PEAK_TFLOPS, HBM_PEAK_GBS))
     for V, R, ps in [(7128, 230, 246), (23033, 256, 1540), (100000, 256, 250000), (1000000, 256, 2500000)]:
         run(V, R, ps)
