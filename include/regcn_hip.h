@@ -40,6 +40,10 @@ extern "C" {
 
 int regcn_version(void);
 const char* regcn_last_error_string(void);
+/* Profiling hook (not needed in production): while `buf` is non-NULL, the relation GRU,
+ * query and score launches write per-workgroup phase timestamps (s_memrealtime, 100 MHz;
+ * 16 int64 slots per workgroup, indexed by the flattened workgroup id) into it. */
+int regcn_set_trace(int64_t* buf);
 
 /* ---- a3: Poincaré / Lorentz row maps (hyperbolic_src/hyperbolic_ops.py) ------------ */
 /* HyperbolicOps.log_map_zero, hyperbolic_ops.py:97-116 */
@@ -198,8 +202,9 @@ int regcn_layer_f32(const regcn_layer_desc* desc, void* stream);
 
 /* ---- a7: relation evolution (segment mean + GRUCell in one launch) ------------------- */
 /* nn.Linear-layout packing for the relation GRU: W is (n_gates * n_out) x n_in row-major
- * (GRUCell weight_ih: 3d x 2d, weight_hh: 3d x d); packed[g][s][jt][lane] =
- * W[g*n_out + 16 jt + lane%16][4 s + lane/16], zero padded. */
+ * (GRUCell weight_ih: 3d x 2d, weight_hh: 3d x d); packed[g][b][jt][lane][e] =
+ * W[g*n_out + 16 jt + lane%16][16 b + 4 (lane/16) + e], zero padded (16-deep k-blocks:
+ * one float4 per lane, gate and block). */
 size_t regcn_packed_linear_floats(int32_t n_gates, int32_t n_out, int32_t n_in);
 int regcn_pack_linear_f32(const float* w, int32_t n_gates, int32_t n_out, int32_t n_in, float* packed,
                           void* stream);

@@ -7,6 +7,7 @@
 namespace regcn {
 
 static thread_local char g_err[512] = "";
+int64_t* g_trace = nullptr;
 
 int set_error(int code, const char* fmt, ...) {
   va_list ap;
@@ -31,6 +32,10 @@ using namespace regcn;
 extern "C" {
 
 int regcn_version(void) { return REGCN_ABI_VERSION; }
+int regcn_set_trace(int64_t* buf) {
+  g_trace = buf;
+  return 0;
+}
 const char* regcn_last_error_string(void) { return g_err; }
 
 int regcn_log0_f32(const float* x, int64_t rows, int32_t d, float c, float* out, void* s) {

@@ -21,17 +21,21 @@
 
 namespace regcn {
 
-// Linear layer y = x W^T + b with packed W^T: acc from an LDS tile, plus the bias.
-__device__ __forceinline__ void linear(Frag& acc, const float* T, int lda, const float* Wp, const float* b, int d,
-                                       int d_out) {
-  acc.zero();
-  mfma_tile(acc, T, lda, Wp, d);
+__device__ __forceinline__ void add_bias(Frag& acc, const float* b, int d_out) {
   float bb[TPW];
   col_load(bb, b, d_out);
 #pragma unroll
   for (int j = 0; j < TPW; ++j)
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc.t[j][r] += bb[j];
+}
+
+// Linear layer y = x W^T + b with packed W^T: acc from an LDS tile, plus the bias.
+__device__ __forceinline__ void linear(Frag& acc, const float* T, int lda, const float* Wp, const float* b, int d,
+                                       int d_out) {
+  acc.zero();
+  mfma_tile(acc, T, lda, Wp, d);
+  add_bias(acc, b, d_out);
 }
 
 __device__ __forceinline__ void frag_to_tile(const Frag& a, float* T, int lda, int d) {
@@ -61,8 +65,8 @@ __device__ __forceinline__ void givens(Frag& x, int d, AngleFn angle) {
     for (int r = 0; r < 4; ++r) {
       const float v = x.t[j][r];
       const float partner = __shfl_xor(v, 1);
-      const float a = angle(r, k2);
-      const float co = cosf(a), si = sinf(a);
+      float si, co;
+      sincosf(angle(r, k2), &si, &co);  // one shared range reduction
       const float y = odd ? (si * partner + co * v) : (co * v - si * partner);
       x.t[j][r] = ok ? y : 0.f;
     }
@@ -158,12 +162,21 @@ __global__ __launch_bounds__(NTHR) void k_query(QueryArgs p) {
   __syncthreads();
 
   Frag h1, tr;
-  linear(h1, T0, lda, p.w1, p.b1, d, d);
-  if (MODE == 0) {
-    Frag ang;
-    linear(tr, T1, lda, p.wtr, p.btr, d, d);
-    linear(ang, T1, lda, p.wrot, p.brot, d, d / 2);
-    frag_to_tile(ang, T2, lda, d / 2);
+  if (MODE == 0) {  // fc1, trans_proj and rot_proj are independent: one k-loop, 3 x 4 chains
+    Frag acc[3];
+    const float* Ts[3] = {T0, T1, T1};
+    const float* Ws[3] = {p.w1, p.wtr, p.wrot};
+#pragma unroll
+    for (int n = 0; n < 3; ++n) acc[n].zero();
+    mfma_tiles<3, RING>(acc, Ts, Ws, lda, d);
+    h1 = acc[0];
+    tr = acc[1];
+    add_bias(h1, p.b1, d);
+    add_bias(tr, p.btr, d);
+    add_bias(acc[2], p.brot, d / 2);
+    frag_to_tile(acc[2], T2, lda, d / 2);
+  } else {
+    linear(h1, T0, lda, p.w1, p.b1, d, d);
   }
 #pragma unroll
   for (int j = 0; j < TPW; ++j) h1.t[j] = f4{fmaxf(h1.t[j].x, 0.f), fmaxf(h1.t[j].y, 0.f), fmaxf(h1.t[j].z, 0.f),

@@ -9,6 +9,8 @@
 
 namespace regcn {
 
+extern int64_t* g_trace;  // regcn_set_trace (profiling)
+
 int set_error(int code, const char* fmt, ...);
 int check_launch(const char* what);
 
@@ -128,6 +130,7 @@ struct RelGruArgs {
   const float* b_hh;
   int R2, d;
   float* h_out;
+  int64_t* trace;  // profiling stamps (g_trace at launch), or null
 };
 
 // RotH decoder queries (query.hip).  Linear weights are packed transposed (x @ W^T).

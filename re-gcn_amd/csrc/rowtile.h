@@ -145,6 +145,53 @@ __device__ __forceinline__ void mfma_tile(Frag& acc, const float* T, int lda, co
   mfma_tile_pf(acc, T, lda, Wp, d, br);
 }
 
+// N independent GEMMs acc[n] += T[n] @ W[n] (same d) in one k-loop: N x TPW MFMA chains per
+// k-step, so each ring of R B fragments covers N times the latency one GEMM's ring does
+// (the weights of a small grid come from HBM, not a warm L2).
+template <int N, int R>
+__device__ __forceinline__ void mfma_tiles(Frag* acc, const float* const* T, const float* const* W, int lda, int d) {
+  const int lane = threadIdx.x & 63;
+  const int S = d >> 2;
+  const bvec* bsrc[N];
+  const float* arow[N];
+  bvec ring[N][R];
+  float aring[N][R];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    bsrc[n] = bsrc_of(W[n]);
+    arow[n] = T[n] + (lane & 15) * lda + (lane >> 4);
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      ring[n][i] = bsrc[n][(int64_t)min(i, S - 1) * B_STEP];
+      aring[n][i] = arow[n][4 * min(i, S - 1)];
+    }
+  int s = 0;
+  for (; s + R <= S; s += R) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+#pragma unroll
+      for (int n = 0; n < N; ++n) mfma_tpw(acc[n], aring[n][i], ring[n][i]);
+      __builtin_amdgcn_sched_barrier(0);
+      const int nx = min(s + i + R, S - 1);
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        ring[n][i] = bsrc[n][(int64_t)nx * B_STEP];
+        aring[n][i] = arow[n][4 * nx];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+    if (s + i < S) {
+#pragma unroll
+      for (int n = 0; n < N; ++n) mfma_tpw(acc[n], aring[n][i], ring[n][i]);
+    }
+}
+
 // Cross-wave row reductions: per-wave partials -> LDS red[buf][wave][row] -> sum in wave
 // order (deterministic).  Two buffers alternate so one barrier per reduction suffices.
 struct RowRed {

@@ -24,6 +24,7 @@ P = _c_vp
 _SIGS = {
     "regcn_version": [],
     "regcn_last_error_string": [],
+    "regcn_set_trace": [P],
     "regcn_log0_f32": [P, _c_i64, _c_int, _c_f, P, P],
     "regcn_exp0_f32": [P, _c_i64, _c_int, _c_f, P, P],
     "regcn_project_f32": [P, _c_i64, _c_int, _c_f, P, P],

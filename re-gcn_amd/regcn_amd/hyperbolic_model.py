@@ -13,6 +13,7 @@ The initial entity state is one fused row kernel (regcn_init_entities_f32).
 Scope: eval/forward.  Static graph (--add-static-graph), EST components, FHNN/HGAT
 encoders and geoopt manifold parameters are out of scope and raise.
 """
+import contextlib
 import logging
 import math
 
@@ -316,15 +317,34 @@ class HyperbolicRecurrentRGCN(nn.Module):
         """hyperbolic_model.py:892-939."""
         with torch.no_grad():
             c_val = self._c_float()
-            # [o, r, s] (hyperbolic_model.py:917); flip() keeps the index on the device
-            inverse_test_triplets = test_triplets.flip(1)
-            inverse_test_triplets[:, 1] = inverse_test_triplets[:, 1] + num_rels
-            all_triples = torch.cat((test_triplets, inverse_test_triplets))
+            dev = self.dynamic_emb.device
+            # the query triples do not depend on the encoder: on a HIP device they are built on
+            # the side stream while the encoder runs (joined in _decode_both)
+            side = self._side(dev) if dev.type == "cuda" and test_triplets.device == dev else None
+            if side is not None:
+                side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                # [o, r, s] (hyperbolic_model.py:917); flip() keeps the index on the device
+                inverse_test_triplets = test_triplets.flip(1)
+                inverse_test_triplets[:, 1] = inverse_test_triplets[:, 1] + num_rels
+                all_triples = torch.cat((test_triplets, inverse_test_triplets))
+            if side is not None:
+                built = torch.cuda.Event()
+                built.record(side)
             evolve_embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
+            if side is not None:
+                torch.cuda.current_stream(dev).wait_event(built)
+                all_triples.record_stream(torch.cuda.current_stream(dev))
             embedding = self._final_embedding(evolve_embs[-1], c_val)
             at = all_triples.to(embedding.device)
             score, score_rel = self._decode_both(embedding, r_emb, at)
             return all_triples, score, score_rel
+
+    def _side(self, dev):
+        side = getattr(self, "_side_stream", None)
+        if side is None or side.device != dev:
+            side = self._side_stream = torch.cuda.Stream(dev)
+        return side
 
     def _decode_both(self, embedding, r_emb, at):
         """Entity and relation decoders are independent: on a HIP device the relation
@@ -334,9 +354,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
             return (self.decoder_ob.forward(embedding, r_emb, at, mode="test"),
                     self.rdecoder.forward(embedding, r_emb, at, mode="test"))
         main = torch.cuda.current_stream(embedding.device)
-        side = getattr(self, "_side_stream", None)
-        if side is None or side.device != embedding.device:
-            side = self._side_stream = torch.cuda.Stream(embedding.device)
+        side = self._side(embedding.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
             score_rel = self.rdecoder.forward(embedding, r_emb, at, mode="test")

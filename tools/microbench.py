@@ -99,9 +99,39 @@ def trace(V=7128, R=230, per_snap=246, d=200, nb=100):
         print("  shader clock ~%.0f MHz (median over workgroups)" % float(clk.median()))
 
 
+def trace_gru(V=7128, R=230, per_snap=246, d=200):
+    """Phase stamps of the relation GRU kernel (regcn_set_trace): staging (relation means),
+    MFMA k-split, cross-wave reduction, gate epilogue."""
+    from regcn_amd import _lib
+    snaps = snapshot_series(0, V, R, 1, per_snap)
+    g = G.build_sub_graph(V, R, snaps[0], True, dev)
+    torch.manual_seed(0)
+    rel = torch.randn(2 * R, d, device=dev) * 0.1
+    x = torch.randn(V, d, device=dev) * 0.1
+    gru = torch.nn.GRUCell(2 * d, d).to(dev)
+    n_wg = ((2 * R + 15) // 16) * ((d + 15) // 16)
+    with torch.no_grad():
+        for _ in range(3):
+            relation_gru_step(gru, rel, x, g, rel)
+        buf = torch.zeros(n_wg * 16, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        _lib.call("regcn_set_trace", _lib.addr(buf, torch.int64))
+        relation_gru_step(gru, rel, x, g, rel)
+        torch.cuda.synchronize()
+        _lib.call("regcn_set_trace", None)
+    t = buf.view(n_wg, 16).cpu().double()
+    t0 = t[:, 0].min()
+    us = lambda a, b: (t[:, b] - t[:, a]) / 100.0
+    print("rel GRU R2=%d workgroups=%d total %.1f us" % (2 * R, n_wg, float((t[:, 4].max() - t0) / 100.0)))
+    ph = [("start", (t[:, 0] - t0) / 100.0), ("stage", us(0, 1)), ("mfma", us(1, 2)), ("sync", us(2, 3)),
+          ("gates", us(3, 4))]
+    print("  " + " ".join("%s %.2f/%.2f" % (k, float(v.median()), float(v.max())) for k, v in ph))
+
+
 if __name__ == "__main__":
     if "--trace" in sys.argv:
         trace()
+        trace_gru()
         sys.exit(0)
     print("peaks: %.1f TF fp32 MFMA, %.0f GB/s HBM" % (FP32_MFMA_PEAK_TFLOPS, HBM_PEAK_GBS))
     for V, R, ps in [(7128, 230, 246), (23033, 256, 1540), (100000, 256, 250000), (1000000, 256, 2500000)]:
