@@ -50,7 +50,7 @@ struct Frag {
   }
 };
 
-__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }  // scalar
 __device__ __forceinline__ int frag_row(int r) { return 4 * ((threadIdx.x & 63) >> 4) + r; }
 __device__ __forceinline__ int frag_col(int jl) { return 16 * (TPW * wave_id() + jl) + (threadIdx.x & 15); }
 
