@@ -1,0 +1,97 @@
+"""Aggregation at the HBM-roofline stress scale (|V| = 1M,
+|E| = 50M directed edges per snapshot, R = 256, d = 200) on one GPU.
+
+Times, as graph-replayed launches between HIP events (bench.event_time):
+  union aggregation alone   regcn_union_aggregate_f32 over every chunk of the snapshot
+  lorentz aggregation alone regcn_lorentz_aggregate_f32 (2x2 block messages + centroid)
+  fused layers              HyperbolicUnionRGCNLayer / LorentzRGCNLayer forward (gather + GEMMs)
+and reports algorithmic bytes B_agg = E (4d + 12) + V (4d + 12) per aggregation over the time,
+as GB/s and as a fraction of the 8 TB/s HBM peak.
+
+  python tools/aggbench.py [--V 1000000] [--triples 25000000] [--reps 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "re-gcn_amd"))
+sys.path.insert(0, REPO)
+from bench import HBM_PEAK_GBS, event_time  # noqa: E402
+from regcn_amd import _lib  # noqa: E402
+from regcn_amd import graph as G  # noqa: E402
+from regcn_amd.hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNLayer  # noqa: E402
+from regcn_amd.hyperbolic_ops import HyperbolicOps as H  # noqa: E402
+from regcn_amd.synthetic import snapshot_series  # noqa: E402
+
+C = 0.01
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--V", type=int, default=1_000_000)
+    ap.add_argument("--R", type=int, default=256)
+    ap.add_argument("--triples", type=int, default=25_000_000)
+    ap.add_argument("--d", type=int, default=200)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--json", default=None, help="write the results here as well")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    V, R, d = a.V, a.R, a.d
+    t0 = time.time()
+    snap = snapshot_series(0, V, R, 1, a.triples)[0]
+    g = G.build_sub_graph(V, R, snap, True, dev)
+    E = g.number_of_edges()
+    print("graph: V=%d E=%d pos=%d tiles=%d heavy=%d chunks=%d built in %.1f s"
+          % (V, E, g.n_pos, g.n_pos_tiles, g.n_heavy, g.work()["chunks"].shape[0], time.time() - t0), flush=True)
+    torch.manual_seed(0)
+    h = H.apply_radius(H.exp_map_zero(torch.randn(V, d, device=dev), C),
+                       torch.rand(V, 1, device=dev) * 2.5 + 0.5, C)
+    x = H.log_map_zero(h, C).contiguous()
+    r = h.norm(dim=1).clamp_min(1e-6).contiguous()
+    rel = (torch.randn(2 * R, d, device=dev) * 0.1).contiguous()
+    wk = g.work()
+    ch, fx = wk["chunks"], wk["fixups"]
+    stride = d + 4
+    part = torch.empty(max(g.n_slots, 1), stride, device=dev, dtype=torch.float32)
+    out = torch.empty(V, d, device=dev, dtype=torch.float32)
+    f, i = _lib.fptr, _lib.iptr
+    lor = LorentzRGCNLayer(d, d, 2 * R, 100, c=C, activation=F.rrelu, self_loop=True).to(dev).eval()
+    uni = HyperbolicUnionRGCNLayer(d, d, 2 * R, c=C, activation=F.rrelu, self_loop=True,
+                                   radius_msg_gamma=0.15).to(dev).eval()
+    w_rel = lor.weight.detach().contiguous()
+
+    def union_agg():
+        _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(wk["col_src"]), i(wk["col_type"]),
+                  f(wk["norm"]), i(ch), ch.shape[0], i(fx), fx.shape[0], 0.15, d, f(part), stride, f(out),
+                  _lib.stream())
+
+    def lorentz_agg():
+        _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(wk["col_src"]), i(wk["col_type"]),
+                  i(ch), ch.shape[0], i(fx), fx.shape[0], 100, float(C), d, f(part), stride, f(out), _lib.stream())
+
+    st = torch.cuda.Stream(dev)
+    b_agg = E * (4 * d + 12) + V * (4 * d + 12)
+    res = {"V": V, "E": E, "R2": 2 * R, "d": d, "b_agg_bytes": b_agg, "hbm_peak_gbs": HBM_PEAK_GBS}
+    with torch.no_grad():
+        runs = [("union_aggregate", union_agg), ("union_layer", lambda: uni(g, h, rel)),
+                ("lorentz_aggregate", lorentz_agg), ("lorentz_layer", lambda: lor(g, h, rel))]
+        for name, fn in runs:
+            ms = event_time(fn, a.reps, st, replays=3)
+            gbs = b_agg / (ms * 1e-3) / 1e9
+            res[name] = {"ms": round(ms, 4), "edges_per_s_G": round(E / (ms * 1e-3) / 1e9, 3),
+                         "algorithmic_GBps": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+            print("%-18s %8.3f ms  %6.3f G edges/s  %7.1f GB/s  %.1f%% of HBM peak"
+                  % (name, ms, E / (ms * 1e-3) / 1e9, gbs, 100 * gbs / HBM_PEAK_GBS), flush=True)
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump(res, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
