@@ -17,7 +17,9 @@ the path has no exchange step at this size); scaling = weak.
 The timed region replays one captured HIP graph per pool sample (inputs resident in
 HBM).  `roofline` reports the dominant kernel, timed live with HIP events on its own
 stream; `cpu_baseline` times the CPU oracle (oracle/, a restatement of the reference
-op sequence) on the same workload on rank 0.
+op sequence) on the same workload on rank 0.  `aggregation_roofline` (N=1) is the
+north-star HBM check: the d=200 aggregation kernels on a config-5 snapshot
+(|V|=1M, |E|=50M), algorithmic bytes over the HIP-event launch time.
 """
 import argparse
 import json
@@ -47,6 +49,8 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph replay")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work")
+    ap.add_argument("--no-scale", action="store_true",
+                    help="skip the config-5 aggregation roofline (|V|=1M, |E|=50M; ~20 s, N=1 only)")
     ap.add_argument("--shard", default="replica", choices=["replica", "edge", "owner"],
                     help="multi-GPU: independent samples per rank (weak scaling), or every snapshot "
                          "partitioned across the ranks by edges (all-reduce) / destination owner "
@@ -208,6 +212,22 @@ def kernel_profile(model, sample, d, device):
     return res
 
 
+def aggregation_at_scale(device):
+    """North-star roofline check: the d=200 union and Lorentz
+    aggregations over one |V|=1M, |E|=50M synthetic snapshot (Zipf destinations), timed
+    live with HIP events; algorithmic bytes E (4d + 12) + V (4d + 12) per launch."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from aggbench import measure
+    res = measure(dev=device, which=("union_aggregate", "lorentz_aggregate"), log=lambda m: None)
+    out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "config": "synthetic |V|=%d |E|=%d R2=%d d=%d"
+           % (res["V"], res["E"], res["R2"], res["d"]), "bytes_per_launch": res["b_agg_bytes"]}
+    for k in ("union_aggregate", "lorentz_aggregate"):
+        out[k] = {"achieved": res[k]["algorithmic_GBps"], "frac": res[k]["hbm_frac"], "avg_launch_us":
+                  round(res[k]["ms"] * 1e3, 1), "G_edges_per_s": res[k]["edges_per_s_G"]}
+    torch.cuda.empty_cache()
+    return out
+
+
 def cpu_baseline(cfg, d, model, sample, budget):
     """Time the CPU oracle (restatement of the reference op sequence) on one sample."""
     sys.path.insert(0, REPO)
@@ -330,6 +350,9 @@ def main():
         kernels = {k: dict(avg_us=round(v["ms"] * 1e3, 3), per_step=v["per_step"], bound=v["bound"],
                            achieved=round(v["achieved"], 3), unit=v["unit"], frac=round(v["frac"], 4))
                    for k, v in kern.items()}
+        scale = None
+        if not args.no_scale and world == 1:
+            scale = aggregation_at_scale(device)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg, d, model, samples[0], args.cpu_budget)
@@ -344,7 +367,7 @@ def main():
                           "hip_graph": bool(graphs),
                           "parallelism": ("%s-partitioned snapshots x%d" % (args.shard, world)) if sharded
                           else "replicas x%d" % world},
-               "roofline": roof, "kernels": kernels, "cpu_baseline": cpu}
+               "roofline": roof, "kernels": kernels, "aggregation_roofline": scale, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -121,8 +121,8 @@ __global__ __launch_bounds__(256) void k_partial_sum(const float* __restrict__ p
 
 // ------------------------------------------------------------------------------ Lorentz
 // Messages and centroid: gather.h (hyperbolic_layers.py:589-625).
-// S in {1, 2, 4}: blocks held in registers, 4 edges in flight per wave (independent
-// loads and reductions, accumulation in edge order).  S == 0: any s, x row staged in LDS.
+// S in {1, 2, 4}: blocks held in registers, 8 (S = 4: 4) edges in flight per wave
+// (independent loads and reductions, accumulation in edge order).  S == 0: any s, x row staged in LDS.
 template <int S>
 __global__ __launch_bounds__(256) void k_lorentz_sum(
     const float* __restrict__ x, const float* __restrict__ rel, const float* __restrict__ W,
@@ -149,26 +149,40 @@ __global__ __launch_bounds__(256) void k_lorentz_sum(
       }
       int j = 0;
       if constexpr (S > 0) {
-        for (; j + 4 <= n; j += 4) {
-          f4 xs[4], rr[4], m[4];
-          WFrag<S> wf[4];
+        // EB edges per batch, all loads unconditional (clamped columns); the per-edge
+        // scalars of the Lorentz point (exp0 factor, time coordinate, scale) are computed
+        // once per batch with lane u = edge u, not redundantly in all 64 lanes per edge.
+        constexpr int EB = S == 4 ? 4 : 8;
+        const int colc = min(col, d - 4);
+        const f4 zero = {0.f, 0.f, 0.f, 0.f};
+        for (; j + EB <= n; j += EB) {
+          f4 xs[EB], rv[EB];
+          WFrag<S> wf[EB];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < EB; ++u) {
             const int src = rl(my_s, j + u), typ = rl(my_t, j + u);
-            xs[u] = load4(x + (int64_t)src * d, col, d);
-            rr[u] = load4(rel + (int64_t)typ * d, col, d);
-            if (active) wf[u].load(W + (int64_t)typ * wstride, col);
+            xs[u] = *reinterpret_cast<const f4*>(x + (int64_t)src * d + colc);
+            rv[u] = *reinterpret_cast<const f4*>(rel + (int64_t)typ * d + colc);
+            wf[u].load(W + (int64_t)typ * wstride, colc);
           }
-          float n2[4];
+          f4 m[EB];
+          float n2l = 0.f;  // lane u < EB: |m_u|^2
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            m[u] = active ? wf[u].apply(xs[u]) + rr[u] : f4{0.f, 0.f, 0.f, 0.f};
-            n2[u] = row16_sum(dot4(m[u], m[u]));
+          for (int u = 0; u < EB; ++u) {
+            m[u] = active ? wf[u].apply(xs[u]) + rv[u] : zero;
+            const float q = row16_sum(dot4(m[u], m[u]));
+            const float t = (rlane(q, 0) + rlane(q, 16)) + (rlane(q, 32) + rlane(q, 48));
+            n2l = lane == u ? t : n2l;
           }
+          float p2;  // lorentz_accum (gather.h), lane-parallel over the batch
+          const float f = exp0_factor(n2l, k, &p2);
+          const float den = fmaxf(1.f - k.c * p2, REGCN_EPS);
+          const float a0 = (1.f + k.c * p2) / (k.sqrt_c * den);
+          const float sc = 2.f * f / den;
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float t = (rlane(n2[u], 0) + rlane(n2[u], 16)) + (rlane(n2[u], 32) + rlane(n2[u], 48));
-            lorentz_accum(m[u], t, k, acc0, acc);
+          for (int u = 0; u < EB; ++u) {
+            acc0 += rlane(a0, u);
+            acc += m[u] * rlane(sc, u);
           }
         }
       }

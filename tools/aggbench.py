@@ -32,30 +32,24 @@ from regcn_amd.synthetic import snapshot_series  # noqa: E402
 C = 0.01
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--V", type=int, default=1_000_000)
-    ap.add_argument("--R", type=int, default=256)
-    ap.add_argument("--triples", type=int, default=25_000_000)
-    ap.add_argument("--d", type=int, default=200)
-    ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--json", default=None, help="write the results here as well")
-    a = ap.parse_args()
-    dev = torch.device("cuda", 0)
-    V, R, d = a.V, a.R, a.d
+def measure(V=1_000_000, R=256, triples=25_000_000, d=200, reps=3, dev=None,
+            which=("union_aggregate", "union_layer", "lorentz_aggregate", "lorentz_layer"), log=print):
+    """Times the named launches on a synthetic config-5 snapshot; returns the result dict."""
+    dev = dev or torch.device("cuda", 0)
     t0 = time.time()
-    snap = snapshot_series(0, V, R, 1, a.triples)[0]
+    snap = snapshot_series(0, V, R, 1, triples)[0]
     g = G.build_sub_graph(V, R, snap, True, dev)
+    del snap
     E = g.number_of_edges()
-    print("graph: V=%d E=%d pos=%d tiles=%d heavy=%d chunks=%d built in %.1f s"
-          % (V, E, g.n_pos, g.n_pos_tiles, g.n_heavy, g.work()["chunks"].shape[0], time.time() - t0), flush=True)
+    wk = g.work()
+    log("graph: V=%d E=%d pos=%d tiles=%d heavy=%d chunks=%d built in %.1f s"
+        % (V, E, g.n_pos, g.n_pos_tiles, g.n_heavy, wk["chunks"].shape[0], time.time() - t0))
     torch.manual_seed(0)
     h = H.apply_radius(H.exp_map_zero(torch.randn(V, d, device=dev), C),
                        torch.rand(V, 1, device=dev) * 2.5 + 0.5, C)
     x = H.log_map_zero(h, C).contiguous()
     r = h.norm(dim=1).clamp_min(1e-6).contiguous()
     rel = (torch.randn(2 * R, d, device=dev) * 0.1).contiguous()
-    wk = g.work()
     ch, fx = wk["chunks"], wk["fixups"]
     stride = d + 4
     part = torch.empty(max(g.n_slots, 1), stride, device=dev, dtype=torch.float32)
@@ -75,19 +69,32 @@ def main():
         _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(wk["col_src"]), i(wk["col_type"]),
                   i(ch), ch.shape[0], i(fx), fx.shape[0], 100, float(C), d, f(part), stride, f(out), _lib.stream())
 
+    fns = {"union_aggregate": union_agg, "union_layer": lambda: uni(g, h, rel),
+           "lorentz_aggregate": lorentz_agg, "lorentz_layer": lambda: lor(g, h, rel)}
     st = torch.cuda.Stream(dev)
     b_agg = E * (4 * d + 12) + V * (4 * d + 12)
     res = {"V": V, "E": E, "R2": 2 * R, "d": d, "b_agg_bytes": b_agg, "hbm_peak_gbs": HBM_PEAK_GBS}
     with torch.no_grad():
-        runs = [("union_aggregate", union_agg), ("union_layer", lambda: uni(g, h, rel)),
-                ("lorentz_aggregate", lorentz_agg), ("lorentz_layer", lambda: lor(g, h, rel))]
-        for name, fn in runs:
-            ms = event_time(fn, a.reps, st, replays=3)
+        for name in which:
+            ms = event_time(fns[name], reps, st, replays=3)
             gbs = b_agg / (ms * 1e-3) / 1e9
             res[name] = {"ms": round(ms, 4), "edges_per_s_G": round(E / (ms * 1e-3) / 1e9, 3),
                          "algorithmic_GBps": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
-            print("%-18s %8.3f ms  %6.3f G edges/s  %7.1f GB/s  %.1f%% of HBM peak"
-                  % (name, ms, E / (ms * 1e-3) / 1e9, gbs, 100 * gbs / HBM_PEAK_GBS), flush=True)
+            log("%-18s %8.3f ms  %6.3f G edges/s  %7.1f GB/s  %.1f%% of HBM peak"
+                % (name, ms, E / (ms * 1e-3) / 1e9, gbs, 100 * gbs / HBM_PEAK_GBS))
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--V", type=int, default=1_000_000)
+    ap.add_argument("--R", type=int, default=256)
+    ap.add_argument("--triples", type=int, default=25_000_000)
+    ap.add_argument("--d", type=int, default=200)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--json", default=None, help="write the results here as well")
+    a = ap.parse_args()
+    res = measure(a.V, a.R, a.triples, a.d, a.reps, log=lambda m: print(m, flush=True))
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(res, fh, indent=1)
