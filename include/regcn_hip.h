@@ -36,7 +36,10 @@ extern "C" {
 /* Snapshot work lists built by the host (re-gcn_amd/regcn_amd/graph.py):
  * chunks: int32[n_chunks][4] = {row, edge_begin, edge_end, slot}; slot < 0 means
  *         the row is finished by that chunk, slot >= 0 names its partial row.
- * fixups: int32[n_fix][4]    = {row, slot_begin, slot_end, 0}. */
+ * fixups: int32[n_fix][4]    = {row, slot_begin, slot_end, out}: out = 0 finishes `row`
+ *         from the slots' sum; out = k > 0 is a first-level group whose raw sum goes to
+ *         partial slot k - 1 (summed before any out = 0 entry; the host cuts rows with more
+ *         than 64 slots into such groups).  `partial` is written by the groups. */
 
 int regcn_version(void);
 const char* regcn_last_error_string(void);
@@ -112,7 +115,7 @@ int regcn_lorentz_aggregate_f32(const float* x, const float* rel, const float* w
  * coordinate at column d), unfinished, so the cross-rank all-reduce of `out` is a plain
  * sum (SURVEY.md §8(e) partitioning 1).  The all-reduced rows are then finished by the
  * same aggregate call with n_chunks = 0, partial = out and fixups {row, row, row + 1}. */
-int regcn_partial_sum_f32(const float* partial, int32_t partial_stride, const int32_t* fixups, int32_t n_fix,
+int regcn_partial_sum_f32(float* partial, int32_t partial_stride, const int32_t* fixups, int32_t n_fix,
                           int32_t width, float* out, int32_t out_stride, void* stream);
 
 /* ---- a4/a5/a6: layer tail (MFMA GEMMs + fused epilogue) ----------------------------- */

@@ -84,6 +84,59 @@ __global__ __launch_bounds__(256) void k_gather_sum(
   }
 }
 
+// ---------------------------------------------------------------------------- fix-ups
+// A fix-up {row, sbeg, send, out} sums partial slots [sbeg, send) in slot order.  out = 0:
+// the finishing kernels below complete `row` from the sum.  out > 0: a first-level group
+// (graph.py cuts a hub row's slots into groups of <= 64, so no single wave walks thousands
+// of slots): k_fixup_groups writes the raw sum into partial slot out - 1, which the row's
+// own (second-level) fix-up then reads.  The group pass runs first, in its own launch.
+__device__ __forceinline__ f4 slot_sum4(const float* __restrict__ partial, int pstride, int sbeg, int send, int c) {
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  int s = sbeg;
+  for (; s + 4 <= send; s += 4) {  // 4 independent loads in flight, summed in slot order
+    const f4 v0 = *reinterpret_cast<const f4*>(partial + (int64_t)s * pstride + c);
+    const f4 v1 = *reinterpret_cast<const f4*>(partial + (int64_t)(s + 1) * pstride + c);
+    const f4 v2 = *reinterpret_cast<const f4*>(partial + (int64_t)(s + 2) * pstride + c);
+    const f4 v3 = *reinterpret_cast<const f4*>(partial + (int64_t)(s + 3) * pstride + c);
+    acc += v0;
+    acc += v1;
+    acc += v2;
+    acc += v3;
+  }
+  for (; s < send; ++s) acc += *reinterpret_cast<const f4*>(partial + (int64_t)s * pstride + c);
+  return acc;
+}
+
+__device__ __forceinline__ float slot_sum1(const float* __restrict__ partial, int pstride, int sbeg, int send, int c) {
+  float acc = 0.f;
+  for (int s = sbeg; s < send; ++s) acc += partial[(int64_t)s * pstride + c];
+  return acc;
+}
+
+// First-level groups: raw sums of the first `width` columns (d, or d + 1 with the Lorentz
+// time coordinate at column d), float4 up to width & ~3, then scalar.
+__global__ __launch_bounds__(256) void k_fixup_groups(float* __restrict__ partial, int pstride,
+                                                      const Fixup* __restrict__ fx, int n_fix, int width) {
+  const int d = width & ~3;
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n_fix; i += nw) {
+    const Fixup f = fx[i];
+    if (f.pad <= 0) continue;
+    float* dst = partial + (int64_t)(f.pad - 1) * pstride;
+    for (int c = lane * 4; c < d; c += 256) *reinterpret_cast<f4*>(dst + c) = slot_sum4(partial, pstride, f.sbeg, f.send, c);
+    for (int c = d + lane; c < width; c += 64) dst[c] = slot_sum1(partial, pstride, f.sbeg, f.send, c);
+  }
+}
+
+static inline unsigned grid_for(int n_items);
+
+static int launch_groups(float* partial, int pstride, const void* fixups, int n_fix, int width, hipStream_t st) {
+  hipLaunchKernelGGL(k_fixup_groups, dim3(grid_for(n_fix)), dim3(256), 0, st, partial, pstride,
+                     (const Fixup*)fixups, n_fix, width);
+  return check_launch("k_fixup_groups");
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void k_gather_fixup(const float* __restrict__ partial, int pstride,
                                                       const Fixup* __restrict__ fx, int n_fix,
@@ -94,8 +147,8 @@ __global__ __launch_bounds__(256) void k_gather_fixup(const float* __restrict__ 
   const int nw = gridDim.x * (blockDim.x >> 6);
   for (int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n_fix; i += nw) {
     const Fixup f = fx[i];
-    f4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int s = f.sbeg; s < f.send; ++s) acc += load4(partial + (int64_t)s * pstride, col, d);
+    if (f.pad > 0) continue;  // a first-level group (k_fixup_groups)
+    const f4 acc = slot_sum4(partial, pstride, f.sbeg, f.send, min(col, d - 4));
     f4 v = (MODE == AGG_MEAN) ? acc / rowscale[f.row] : acc * rowscale[f.row];
     store4(out + (int64_t)f.row * d, col, d, v);
   }
@@ -111,11 +164,8 @@ __global__ __launch_bounds__(256) void k_partial_sum(const float* __restrict__ p
   const int nw = gridDim.x * (blockDim.x >> 6);
   for (int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n_fix; i += nw) {
     const Fixup f = fx[i];
-    for (int c = lane; c < width; c += 64) {
-      float acc = 0.f;
-      for (int s = f.sbeg; s < f.send; ++s) acc += partial[(int64_t)s * pstride + c];
-      out[(int64_t)f.row * ostride + c] = acc;
-    }
+    if (f.pad > 0) continue;  // a first-level group (k_fixup_groups)
+    for (int c = lane; c < width; c += 64) out[(int64_t)f.row * ostride + c] = slot_sum1(partial, pstride, f.sbeg, f.send, c);
   }
 }
 
@@ -222,13 +272,10 @@ __global__ __launch_bounds__(256) void k_lorentz_fixup(const float* __restrict__
   const int nw = gridDim.x * (blockDim.x >> 6);
   for (int i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n_fix; i += nw) {
     const Fixup f = fx[i];
-    f4 acc = {0.f, 0.f, 0.f, 0.f};
-    float acc0 = 0.f;
-    for (int s = f.sbeg; s < f.send; ++s) {
-      const float* p = partial + (int64_t)s * pstride;
-      acc += load4(p, col, d);
-      acc0 += p[d];
-    }
+    if (f.pad > 0) continue;  // a first-level group (k_fixup_groups)
+    f4 acc = slot_sum4(partial, pstride, f.sbeg, f.send, min(col, d - 4));
+    if (col >= d) acc = f4{0.f, 0.f, 0.f, 0.f};
+    const float acc0 = slot_sum1(partial, pstride, f.sbeg, f.send, d);
     store4(out + (int64_t)f.row * d, col, d, lorentz_finish(acc0, acc, k));
   }
 }
@@ -267,6 +314,8 @@ int gather_sum(int mode, const float* x, const float* radius, const float* rel, 
     if (rc) return rc;
   }
   if (n_fix > 0) {
+    int rc = launch_groups(partial, pstride, fixups, n_fix, d, st);
+    if (rc) return rc;
     dim3 g(grid_for(n_fix)), b(256);
     if (mode == AGG_MEAN)
       hipLaunchKernelGGL(k_gather_fixup<AGG_MEAN>, g, b, 0, st, partial, pstride, fx, n_fix, rowscale, d, out);
@@ -277,11 +326,13 @@ int gather_sum(int mode, const float* x, const float* radius, const float* rel, 
   return 0;
 }
 
-int partial_sum(const float* partial, int pstride, const void* fixups, int n_fix, int width, float* out, int ostride,
+int partial_sum(float* partial, int pstride, const void* fixups, int n_fix, int width, float* out, int ostride,
                 hipStream_t st) {
   if (n_fix == 0) return 0;
   if (!partial || !fixups || !out) return set_error(REGCN_EINVAL, "null pointer");
   if (width <= 0 || width > pstride || width > ostride) return set_error(REGCN_EINVAL, "bad partial-sum width");
+  int rc = launch_groups(partial, pstride, fixups, n_fix, width, st);  // group slots: scratch
+  if (rc) return rc;
   dim3 g(grid_for(n_fix)), b(256);
   hipLaunchKernelGGL(k_partial_sum, g, b, 0, st, partial, pstride, (const Fixup*)fixups, n_fix, width, out, ostride);
   return check_launch("k_partial_sum");
@@ -315,6 +366,8 @@ int lorentz_sum(const float* x, const float* rel, const float* W, const int* col
     if (rc) return rc;
   }
   if (n_fix > 0) {
+    int rc = launch_groups(partial, pstride, fixups, n_fix, d + 1, st);
+    if (rc) return rc;
     dim3 g(grid_for(n_fix)), b(256);
     hipLaunchKernelGGL(k_lorentz_fixup, g, b, 0, st, partial, pstride, (const Fixup*)fixups, n_fix, k, d, out);
     return check_launch("k_lorentz_fixup");

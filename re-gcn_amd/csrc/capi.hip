@@ -105,7 +105,7 @@ int regcn_lorentz_aggregate_f32(const float* x, const float* rel, const float* w
                      partial_stride, out, ST(s));
 }
 
-int regcn_partial_sum_f32(const float* partial, int32_t partial_stride, const int32_t* fixups, int32_t n_fix,
+int regcn_partial_sum_f32(float* partial, int32_t partial_stride, const int32_t* fixups, int32_t n_fix,
                           int32_t width, float* out, int32_t out_stride, void* s) {
   return partial_sum(partial, partial_stride, fixups, n_fix, width, out, out_stride, ST(s));
 }

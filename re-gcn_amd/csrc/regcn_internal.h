@@ -34,7 +34,7 @@ int gather_sum(int mode, const float* x, const float* radius, const float* rel, 
                const int* col_type, const float* rowscale, const void* chunks, int n_chunks,
                const void* fixups, int n_fix, float gamma, int d, float* partial, int pstride, float* out,
                hipStream_t st);
-int partial_sum(const float* partial, int pstride, const void* fixups, int n_fix, int width, float* out, int ostride,
+int partial_sum(float* partial, int pstride, const void* fixups, int n_fix, int width, float* out, int ostride,
                 hipStream_t st);
 int lorentz_sum(const float* x, const float* rel, const float* W, const int* col_src, const int* col_type,
                 const void* chunks, int n_chunks, const void* fixups, int n_fix, int nb, float c, int d,

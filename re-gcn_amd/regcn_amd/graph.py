@@ -58,6 +58,33 @@ def r2e(triplets, num_rels):
     return uniq_r, r_len, np.concatenate(e_idx).tolist()
 
 
+FIX_GROUP = 64  # partial slots one fix-up wave sums; longer rows get a first-level group pass
+
+
+def group_fixups(fixups, nslot, group=FIX_GROUP):
+    """Cut fix-ups over more than `group` slots into first-level groups (csrc/aggregate.hip
+    k_fixup_groups): {0, b, e, k + 1} sums slots [b, e) into new slot k, and the row's own
+    fix-up then sums its groups' slots.  A hub's thousands of chunk partials are thus summed
+    by many waves instead of one wave walking them all.  Returns (fixups, nslot)."""
+    fixups = np.asarray(fixups, dtype=np.int32).reshape(-1, 4)
+    if len(fixups) == 0:
+        return fixups, nslot
+    k = fixups[:, 2].astype(np.int64) - fixups[:, 1]
+    big = k > group
+    if not big.any():
+        return fixups, nslot
+    groups, finals = [], []
+    for row, sb, se, _ in fixups[big].tolist():
+        ng = (se - sb + group - 1) // group
+        for g in range(ng):
+            groups.append((0, sb + g * group, min(sb + (g + 1) * group, se), nslot + g + 1))
+        finals.append((row, nslot, nslot + ng, 0))
+        nslot += ng
+    out = np.concatenate([np.asarray(groups, dtype=np.int32).reshape(-1, 4), fixups[~big],
+                          np.asarray(finals, dtype=np.int32).reshape(-1, 4)])
+    return out, int(nslot)
+
+
 def _chunk_rows(seg_ptr, seg_rows, chunk_edges):
     """Cut segments [seg_ptr[i], seg_ptr[i+1]) of row seg_rows[i] into chunks."""
     lens = np.diff(seg_ptr)
@@ -79,7 +106,8 @@ def _chunk_rows(seg_ptr, seg_rows, chunk_edges):
     ncl = nchunk[nchunk > 1]
     sb = np.cumsum(ncl) - ncl
     fixups = np.stack([long_rows, sb, sb + ncl, np.zeros_like(ncl)], 1).astype(np.int32)
-    return chunks.reshape(-1, 4), fixups.reshape(-1, 4), int(multi.sum())
+    fixups, nslot = group_fixups(fixups, int(multi.sum()))
+    return chunks.reshape(-1, 4), fixups, nslot
 
 
 class _Frame(dict):
@@ -284,8 +312,8 @@ def _chunk_spans(starts, lens, rows, chunk_edges):
             chunks_l.append((r, b + i * chunk_edges, min(b + (i + 1) * chunk_edges, b + n), nslot + i))
         fix_l.append((r, nslot, nslot + k, 0))
         nslot += k
-    return (np.array(chunks_l, dtype=np.int32).reshape(-1, 4), np.array(fix_l, dtype=np.int32).reshape(-1, 4),
-            nslot)
+    fixups, nslot = group_fixups(fix_l, nslot)
+    return np.array(chunks_l, dtype=np.int32).reshape(-1, 4), fixups, nslot
 
 
 def _chunk_rows_spans(start, length, chunk_edges):
@@ -308,7 +336,7 @@ def _chunk_rows_spans(start, length, chunk_edges):
             nslot += k
     del ptr
     chunks = np.array(chunks_l, dtype=np.int32).reshape(-1, 4)
-    fixups = np.array(fix_l, dtype=np.int32).reshape(-1, 4)
+    fixups, nslot = group_fixups(fix_l, nslot)
     return chunks, fixups, nslot
 
 

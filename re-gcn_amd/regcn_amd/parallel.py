@@ -22,7 +22,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .graph import fused_work
+from .graph import fused_work, group_fixups
 
 
 def even_bounds(n, world):
@@ -53,8 +53,7 @@ class EdgePlan:
             fix.append((r, slot, slot + k, 0))
             slot += k
         self.chunks = np.asarray(chunks, dtype=np.int32).reshape(-1, 4)
-        self.fixups = np.asarray(fix, dtype=np.int32).reshape(-1, 4)
-        self.n_slots = slot
+        self.fixups, self.n_slots = group_fixups(fix, slot)
         pos = np.nonzero(np.diff(rowptr) > 0)[0]
         self.finish = np.stack([pos, pos, pos + 1, np.zeros_like(pos)], 1).astype(np.int32).reshape(-1, 4)
         self.V = V

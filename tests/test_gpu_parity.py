@@ -203,10 +203,12 @@ def _zipf_snapshot(V, R, T, seed):
     return np.stack([perm[rng.choice(V, T, p=p)], rng.integers(0, R, T), perm[rng.choice(V, T, p=p)]], 1)
 
 
+@pytest.mark.parametrize("chunk", [None, 2])
 @pytest.mark.parametrize("kind", ["union", "lorentz", "euclid"])
-def test_layers_with_hubs_vs_oracle(kind):
+def test_layers_with_hubs_vs_oracle(kind, chunk):
     """Zipf snapshot with hubs over the tile budget (pre-aggregated + fixups) next to
-    inline-gathered rows, at d = 200 / num_bases = 100 (the bench shape)."""
+    inline-gathered rows, at d = 200 / num_bases = 100 (the bench shape).  chunk = 2 gives
+    the hubs hundreds of partial slots: their fix-ups go through the first-level groups."""
     import torch.nn.functional as F
     from oracle import graph as OG
     from oracle import layers as OL
@@ -216,8 +218,10 @@ def test_layers_with_hubs_vs_oracle(kind):
     from regcn_amd.layers import UnionRGCNLayer
     V, R, T, d = 3000, 60, 20000, 200  # 2R >= num_bases = 100 (else the reference clamps num_bases)
     tr = _zipf_snapshot(V, R, T, 7)
-    g = G.build_sub_graph(V, R, tr, True, DEV)
+    g = G.build_sub_graph(V, R, tr, True, DEV, chunk_edges=chunk)
     assert g.n_heavy > 0 and g.heavy_slots > 0
+    if chunk == 2:
+        assert (g._host["heavy_fixups"][:, 3] > 0).any()
     og = OG.build_sub_graph(V, R, tr)
     gen = torch.Generator().manual_seed(3)
     h = O.exp0(torch.randn(V, d, generator=gen) * 0.5, C)

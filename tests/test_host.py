@@ -76,10 +76,22 @@ def test_work_lists_cover_every_edge_once(chunk):
             assert (b, e) == (ptr[row], ptr[row + 1])
     assert (seen == 1).all()
     slots = sorted(int(s) for s in ch[:, 3] if s >= 0)
-    assert slots == list(range(g.n_slots))
-    for row, sb, se, _ in fx:
-        rc = ch[(ch[:, 0] == row)]
-        assert list(rc[:, 3]) == list(range(sb, se))
+    assert slots == list(range(len(slots)))
+    # fix-ups: first-level groups (out > 0) cover <= 64 consecutive chunk slots each and
+    # write new slots; every row's final fix-up covers its chunk slots, directly or
+    # through its groups, in chunk order
+    group_of = {int(o) - 1: (int(b), int(e)) for _, b, e, o in fx if o > 0}
+    assert all(e - b <= 64 for b, e in group_of.values())
+    assert sorted(group_of) == list(range(len(slots), g.n_slots))
+    finals = [f for f in fx if f[3] == 0]
+    assert len(finals) == len({int(f[0]) for f in finals})
+    for row, sb, se, _ in finals:
+        covered = []
+        for s_ in range(sb, se):
+            b, e = group_of.get(s_, (s_, s_ + 1))
+            covered.extend(range(b, e))
+        assert covered == list(ch[ch[:, 0] == row][:, 3])
+        assert all(e - b <= 64 for b, e in [(sb, se)])
     # CSR columns: stable dst sort of the reference edge order
     order = np.argsort(g.dst_np, kind="stable")
     np.testing.assert_array_equal(h["col_src"], g.src_np[order])

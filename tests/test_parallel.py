@@ -39,9 +39,17 @@ def test_edge_plan_covers_every_edge_once(world):
             assert e - b <= g.chunk_edges
             cov[b:e] += 1
             slots.append(s)
-        assert sorted(slots) == list(range(pl.n_slots))
-        for row, sb, se, _ in pl.fixups:  # each touched row sums exactly its own slots
-            assert set(pl.chunks[(pl.chunks[:, 0] == row), 3]) == set(range(sb, se))
+        assert sorted(slots) == list(range(len(slots)))
+        group_of = {int(o) - 1: (int(b), int(e)) for _, b, e, o in pl.fixups if o > 0}
+        assert sorted(group_of) == list(range(len(slots), pl.n_slots))
+        for row, sb, se, o in pl.fixups:  # each touched row sums exactly its own slots
+            if o > 0:
+                continue
+            covered = set()
+            for s_ in range(sb, se):
+                b, e = group_of.get(s_, (s_, s_ + 1))
+                covered |= set(range(b, e))
+            assert set(pl.chunks[(pl.chunks[:, 0] == row), 3]) == covered
         fin = pl.finish
         assert (fin[:, 1] == fin[:, 0]).all() and (fin[:, 2] == fin[:, 0] + 1).all()
         np.testing.assert_array_equal(np.sort(fin[:, 0]), np.nonzero(g.in_deg_np > 0)[0])
