@@ -113,6 +113,7 @@ struct ScoreArgs {
   float* out;            // [B, N] score (SCORE mode)
   float* part;           // [B, nblk, 2] (CE mode): running max, sum exp
   float* tgt_logit;      // [B] (CE mode)
+  int64_t* trace;        // profiling stamps (g_trace at launch), or null
 };
 
 // Relation GRU of one timestep (relgru.hip).

@@ -28,7 +28,7 @@ template <bool F64>
 struct Chunking {
   static constexpr int NF = 1;
   static constexpr int SKC = 16 * NF;
-  static constexpr int SLD = SKC + 1;
+  static constexpr int SLD = SKC + 2;  // = 2 (mod 32): conflict-free fragment reads
 };
 
 
@@ -92,110 +92,12 @@ struct ScoreT<true> {
 // MODE 0 = write scores, 1 = CE partials.  F64: fp64 MFMA + fp64 epilogue, used for the
 // true-distance mode where the arctanh distance is linear in |num| and the fp32 expansion
 // would lose ~3 digits on near-duplicate pairs (the per-pair fp32 reference does not).
-template <int MODE, bool F64>
-__global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
-  typedef ScoreT<F64> S;
-  typedef typename S::T T;
-  p.scale = p.scale_p ? *p.scale_p : 1.f;
-  if (p.scale_raw && p.scale_p)  // softplus(raw) + 1e-6 (hyperbolic_decoder.py:717; torch threshold 20)
-    p.scale = (p.scale > 20.f ? p.scale : log1pf(expf(p.scale))) + 1e-6f;
-  p.margin = p.margin_p ? *p.margin_p : 0.f;
-  constexpr int NF = Chunking<F64>::NF, SKC = Chunking<F64>::SKC, SLD = Chunking<F64>::SLD;
-  __shared__ T Qs2[2][SQ * SLD];  // double-buffered K chunks
-  __shared__ T Es2[2][SN * SLD];
-  __shared__ T q2s[SQ], e2s[SN];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // consecutive blocks share a query tile (the candidate stream is the large operand)
-  const int nbn = (p.N + SN - 1) / SN;
-  const int bq = blockIdx.x / nbn, bn = blockIdx.x - bq * nbn;
-  const int q0 = bq * SQ, n0 = bn * SN;
-  typename S::V acc[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) acc[j] = typename S::V{0, 0, 0, 0};
-  const int i = tid >> 2, kq = (tid & 3) * 4;
-  T sq_q = 0, sq_e = 0;  // row |.|^2, accumulated by the 4 staging threads of row i
-  // Software pipeline: chunk c + 1 is loaded into registers (unconditional, clamped
-  // addresses) while chunk c is multiplied out of the other LDS buffer.
-  const float* qrow = p.q + (int64_t)min(q0 + i, p.B - 1) * p.d;
-  const float* erow = p.e + (int64_t)min(n0 + i, p.N - 1) * p.d;
-  const bool q_ok = q0 + i < p.B, e_ok = n0 + i < p.N;
-  const f4 z4 = {0.f, 0.f, 0.f, 0.f};
-  auto fetch = [&](int k0, f4* vq, f4* ve) {
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      const int k = k0 + kq + 16 * f;
-      const int c = min(k, p.d - 4);
-      const bool k_ok = k < p.d;
-      const f4 a = *reinterpret_cast<const f4*>(qrow + c);
-      const f4 b = *reinterpret_cast<const f4*>(erow + c);
-      vq[f] = (q_ok && k_ok) ? a : z4;
-      ve[f] = (e_ok && k_ok) ? b : z4;
-    }
-  };
-  f4 vq[NF], ve[NF];
-  fetch(0, vq, ve);
-  int buf = 0;
-  for (int k0 = 0; k0 < p.d; k0 += SKC, buf ^= 1) {
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      T* dq = Qs2[buf] + i * SLD + kq + 16 * f;
-      T* de = Es2[buf] + i * SLD + kq + 16 * f;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const T a = (T)vq[f][u], b = (T)ve[f][u];
-        dq[u] = a;
-        de[u] = b;
-        sq_q += a * a;
-        sq_e += b * b;
-      }
-    }
-    fetch(k0 + SKC, vq, ve);  // unconditional (past the end it reads a clamped chunk it never
-                              // stores): a conditional load would be drained right here
-    __syncthreads();  // chunk k0 staged; the other buffer's readers (chunk k0 - SKC) are done
-    const T* Qs = Qs2[buf];
-    const T* Es = Es2[buf];
-    const int kn = min(SKC, p.d - k0);
-#pragma unroll
-    for (int kk = 0; kk < SKC; kk += 4) {
-      if (kk < kn) {  // wave-uniform: the last chunk stops at d (its tail is zero-staged)
-        const T a = Qs[(16 * wv + (lane & 15)) * SLD + kk + (lane >> 4)];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const T b = Es[(16 * j + (lane & 15)) * SLD + kk + (lane >> 4)];
-          acc[j] = S::mfma(a, b, acc[j]);
-        }
-      }
-    }
-  }
-  sq_q += __shfl_xor(sq_q, 1);
-  sq_q += __shfl_xor(sq_q, 2);
-  sq_e += __shfl_xor(sq_e, 1);
-  sq_e += __shfl_xor(sq_e, 2);
-  if ((tid & 3) == 0) {
-    q2s[i] = sq_q;
-    e2s[i] = sq_e;
-  }
-  __syncthreads();
-  // epilogue: lane holds queries q0 + 16 wv + S::row(lane, r), candidates n0 + 16 j + (lane & 15)
-  T x2[4], cr[4];
-  int qi[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int li = 16 * wv + S::row(lane, r);
-    qi[r] = q0 + li;
-    const bool ok = qi[r] < p.B;
-    x2[r] = q2s[li];
-    cr[r] = (ok && p.c_r) ? (T)p.c_r[qi[r]] : (T)0;
-  }
-  T y2[4], bn_[4];
-  int ni[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    ni[j] = n0 + 16 * j + (lane & 15);
-    const bool ok = ni[j] < p.N;
-    y2[j] = e2s[16 * j + (lane & 15)];
-    bn_[j] = (ok && p.bias) ? (T)p.bias[ni[j]] : (T)0;
-  }
+// Epilogue shared by the score kernels: lane holds queries qi[r] and candidates ni[j];
+// MODE 0 writes the scores, MODE 1 the per-tile (max, sum exp) CE partials + target logit.
+template <int MODE, typename T, typename V>
+__device__ __forceinline__ void score_epilogue(const ScoreArgs& p, const V* acc, const T* x2, const T* y2,
+                                               const T* bn_, const T* cr, const int* qi, const int* ni, int lane,
+                                               int bn) {
   if (MODE == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -233,6 +135,243 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
       }
     }
   }
+}
+
+
+template <int MODE, bool F64>
+__global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
+  typedef ScoreT<F64> S;
+  typedef typename S::T T;
+  p.scale = p.scale_p ? *p.scale_p : 1.f;
+  if (p.scale_raw && p.scale_p)  // softplus(raw) + 1e-6 (hyperbolic_decoder.py:717; torch threshold 20)
+    p.scale = (p.scale > 20.f ? p.scale : log1pf(expf(p.scale))) + 1e-6f;
+  p.margin = p.margin_p ? *p.margin_p : 0.f;
+  constexpr int NF = Chunking<F64>::NF, SKC = Chunking<F64>::SKC, SLD = Chunking<F64>::SLD;
+  __shared__ T Qs2[2][SQ * SLD];  // double-buffered K chunks
+  __shared__ T Es2[2][SN * SLD];
+  __shared__ T q2s[SQ], e2s[SN];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  auto stamp = [&](int k) {  // profiling (regcn_set_trace)
+    if (p.trace && tid == 0) p.trace[(int64_t)blockIdx.x * 16 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  // consecutive blocks share a query tile (the candidate stream is the large operand)
+  const int nbn = (p.N + SN - 1) / SN;
+  const int bq = blockIdx.x / nbn, bn = blockIdx.x - bq * nbn;
+  const int q0 = bq * SQ, n0 = bn * SN;
+  typename S::V acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = typename S::V{0, 0, 0, 0};
+  const int i = tid >> 2, kq = (tid & 3) * 4;
+  T sq_q = 0, sq_e = 0;  // row |.|^2, accumulated by the 4 staging threads of row i
+  // Software pipeline: chunk c + 1 is loaded into registers (unconditional, clamped
+  // addresses) while chunk c is multiplied out of the other LDS buffer.
+  const float* qrow = p.q + (int64_t)min(q0 + i, p.B - 1) * p.d;
+  const float* erow = p.e + (int64_t)min(n0 + i, p.N - 1) * p.d;
+  const bool q_ok = q0 + i < p.B, e_ok = n0 + i < p.N;
+  const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  auto fetch = [&](int k0, f4* vq, f4* ve) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int k = k0 + kq + 16 * f;
+      const int c = min(k, p.d - 4);
+      // raw loads; the mask is applied at staging (a select here would wait for them)
+      vq[f] = *reinterpret_cast<const f4*>(qrow + c);
+      ve[f] = *reinterpret_cast<const f4*>(erow + c);
+    }
+  };
+  // PF chunks of loads in flight (a ring of registers, slot = chunk % PF): one chunk of
+  // MFMA work per wave (16 MFMAs) is far shorter than an L2/MALL round trip.
+  constexpr int PF = 4;
+  f4 vq[PF][NF], ve[PF][NF];
+#pragma unroll
+  for (int c = 0; c < PF; ++c) fetch(c * SKC, vq[c], ve[c]);
+  // the chunk count is padded to a multiple of PF: a padded chunk stages zeros and skips
+  // its MFMAs (kn <= 0), and the loop body has no exit branch, so every wait is counted
+  // (a conditional exit makes hipcc drain vmcnt(0) before each chunk's staging)
+  const int n_pad = ((p.d + SKC - 1) / SKC + PF - 1) / PF * PF;
+  int buf = 0;
+  for (int c0 = 0; c0 < n_pad; c0 += PF) {
+#pragma unroll
+    for (int sl = 0; sl < PF; ++sl) {
+      const int c = c0 + sl;
+      const int k0 = c * SKC;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        T* dq = Qs2[buf] + i * SLD + kq + 16 * f;
+        T* de = Es2[buf] + i * SLD + kq + 16 * f;
+        const bool k_ok = k0 + kq + 16 * f < p.d;
+        const f4 va = (q_ok && k_ok) ? vq[sl][f] : z4, vb = (e_ok && k_ok) ? ve[sl][f] : z4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const T a = (T)va[u], b = (T)vb[u];
+          dq[u] = a;
+          de[u] = b;
+          sq_q += a * a;
+          sq_e += b * b;
+        }
+      }
+      fetch(k0 + PF * SKC, vq[sl], ve[sl]);  // unconditional (past the end: a clamped chunk
+                                             // never stored); a conditional load would drain
+      __syncthreads();  // chunk c staged; the other buffer's readers (chunk c - 1) are done
+      const T* Qs = Qs2[buf];
+      const T* Es = Es2[buf];
+      const int kn = min(SKC, p.d - k0);
+#pragma unroll
+      for (int kk = 0; kk < SKC; kk += 4) {
+        if (kk < kn) {  // wave-uniform: the last chunk stops at d (its tail is zero-staged)
+          const T a = Qs[(16 * wv + (lane & 15)) * SLD + kk + (lane >> 4)];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const T b = Es[(16 * j + (lane & 15)) * SLD + kk + (lane >> 4)];
+            acc[j] = S::mfma(a, b, acc[j]);
+          }
+        }
+      }
+      buf ^= 1;
+    }
+  }
+  stamp(1);
+  sq_q += __shfl_xor(sq_q, 1);
+  sq_q += __shfl_xor(sq_q, 2);
+  sq_e += __shfl_xor(sq_e, 1);
+  sq_e += __shfl_xor(sq_e, 2);
+  if ((tid & 3) == 0) {
+    q2s[i] = sq_q;
+    e2s[i] = sq_e;
+  }
+  __syncthreads();
+  // epilogue: lane holds queries q0 + 16 wv + S::row(lane, r), candidates n0 + 16 j + (lane & 15)
+  T x2[4], cr[4];
+  int qi[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int li = 16 * wv + S::row(lane, r);
+    qi[r] = q0 + li;
+    const bool ok = qi[r] < p.B;
+    x2[r] = q2s[li];
+    cr[r] = (ok && p.c_r) ? (T)p.c_r[qi[r]] : (T)0;
+  }
+  T y2[4], bn_[4];
+  int ni[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ni[j] = n0 + 16 * j + (lane & 15);
+    const bool ok = ni[j] < p.N;
+    y2[j] = e2s[16 * j + (lane & 15)];
+    bn_[j] = (ok && p.bias) ? (T)p.bias[ni[j]] : (T)0;
+  }
+  score_epilogue<MODE, T>(p, acc, x2, y2, bn_, cr, qi, ni, lane, bn);
+  stamp(2);
+}
+
+// fp32 scorer without K-chunk barriers.  A workgroup = 8 waves = 128 queries x 64
+// candidates; wave w owns queries [16w, 16w + 16) and all 64 candidates (4 MFMA tiles).
+// k-block order: MFMA sub-step e of 16-deep block b reads k = 16 b + 4 (lane >> 4) + e, so
+// a lane's operands for a whole block are one contiguous float4: the wave's query rows live
+// in registers for the whole K (one dwordx4 per block, loaded at entry), the candidate tile
+// is staged in LDS once (row stride = 8 mod 16: conflict-free ds_read_b128) behind a single
+// barrier, and the MFMA loop runs with no further synchronisation.  |q|^2 and |e|^2 come
+// from the same operand registers.
+constexpr int SQ2 = 128, SW2 = SQ2 / 16, KB_MAX = 16;  // d <= 256
+
+__host__ __device__ inline int score_lds_stride(int d) { return ((d + 15) & ~15) + 8; }
+
+template <int MODE>
+__global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(4))) void k_score_f32(ScoreArgs p) {
+  extern __shared__ float Es[];  // SN x SE candidate rows, zero past N and d
+  p.scale = p.scale_p ? *p.scale_p : 1.f;
+  if (p.scale_raw && p.scale_p)  // softplus(raw) + 1e-6 (hyperbolic_decoder.py:717; torch threshold 20)
+    p.scale = (p.scale > 20.f ? p.scale : log1pf(expf(p.scale))) + 1e-6f;
+  p.margin = p.margin_p ? *p.margin_p : 0.f;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  auto stamp = [&](int k) {  // profiling (regcn_set_trace)
+    if (p.trace && tid == 0) p.trace[(int64_t)blockIdx.x * 16 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
+  const int nbn = (p.N + SN - 1) / SN;
+  const int bq = blockIdx.x / nbn, bn = blockIdx.x - bq * nbn;
+  const int q0 = bq * SQ2, n0 = bn * SN;
+  const int g4 = 4 * (lane >> 4);
+  const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  // this wave's query rows, all k-blocks (unconditional clamped loads; masked at use)
+  const int qr = q0 + 16 * wv + (lane & 15);
+  const bool q_ok = qr < p.B;
+  const float* qrow = p.q + (int64_t)min(qr, p.B - 1) * d;
+  f4 a[KB_MAX];
+#pragma unroll
+  for (int b = 0; b < KB_MAX; ++b) a[b] = *reinterpret_cast<const f4*>(qrow + min(16 * b + g4, d - 4));
+  // stage the candidate tile in two halves (loads of a half in flight together, then its
+  // LDS writes): half the staging registers, so two workgroups fit a CU
+  {
+    constexpr int IT = (SN * KB_MAX * 4 + 64 * SW2 - 1) / (64 * SW2), HALF = IT / 2;
+    const int per_row = 4 * KB, n_units = SN * per_row;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      f4 v[HALF];
+#pragma unroll
+      for (int it = 0; it < HALF; ++it) {
+        const int u = min(tid + (h * HALF + it) * 64 * SW2, n_units - 1);
+        const int r = u / per_row, k = (u - r * per_row) * 4;
+        v[it] = *reinterpret_cast<const f4*>(p.e + (int64_t)min(n0 + r, p.N - 1) * d + min(k, d - 4));
+      }
+#pragma unroll
+      for (int it = 0; it < HALF; ++it) {
+        const int u = tid + (h * HALF + it) * 64 * SW2;
+        if (u < n_units) {
+          const int r = u / per_row, k = (u - r * per_row) * 4;
+          *reinterpret_cast<f4*>(Es + r * SE + k) = (n0 + r < p.N && k < d) ? v[it] : z4;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  stamp(1);
+  f4 acc[4] = {z4, z4, z4, z4};
+  float xs = 0.f, ys[4] = {0.f, 0.f, 0.f, 0.f};
+  const float* brow = Es + (lane & 15) * SE + g4;
+#pragma unroll
+  for (int b = 0; b < KB_MAX; ++b) {
+    if (b < KB) {  // wave-uniform
+      f4 bv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE + 16 * b);
+      const f4 av = (q_ok && 16 * b + g4 < d) ? a[b] : z4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[j][e], acc[j], 0, 0, 0);
+      xs += dot4(av, av);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ys[j] += dot4(bv[j], bv[j]);
+    }
+  }
+  // |q|^2 of query (lane & 15), |e|^2 of candidate 16 j + (lane & 15): sum the 4 k-quarters
+  xs += __shfl_xor(xs, 16);
+  xs += __shfl_xor(xs, 32);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ys[j] += __shfl_xor(ys[j], 16);
+    ys[j] += __shfl_xor(ys[j], 32);
+  }
+  float x2[4], cr[4] = {0.f, 0.f, 0.f, 0.f}, y2[4], bn_[4];
+  int qi[4], ni[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int li = 4 * (lane >> 4) + r;  // C row of this lane = query 16 wv + li
+    x2[r] = __shfl(xs, li);
+    qi[r] = q0 + 16 * wv + li;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    ni[j] = n0 + 16 * j + (lane & 15);
+    y2[j] = ys[j];
+    bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
+  }
+  score_epilogue<MODE, float>(p, acc, x2, y2, bn_, cr, qi, ni, lane, bn);
+  stamp(2);
 }
 
 // Combine per-tile (max, sumexp) into per-query loss = lse - target logit (one wave per query).
@@ -291,18 +430,25 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   if (a.d <= 0 || (a.d & 3)) return set_error(REGCN_EINVAL, "score needs d %% 4 == 0");
   if (!a.q || !a.e) return set_error(REGCN_EINVAL, "null pointer");
   if (a.B == 0 || a.N == 0) return 0;
+  a.trace = g_trace;
   const int nbq = (a.B + SQ - 1) / SQ, nbn = (a.N + SN - 1) / SN;
   const long blocks = (long)nbq * nbn;
   if (blocks > 0x7fffffffL) return set_error(REGCN_EINVAL, "score grid too large");
   dim3 g((unsigned)blocks), b(256);
+  // fp32 proxy / distance scores (no per-query curvature, d <= 256): the barrier-free kernel
+  const bool fast = !a.use_dist && a.d <= 16 * KB_MAX;
+  const dim3 g2((unsigned)(((long)(a.B + SQ2 - 1) / SQ2) * nbn)), b2(64 * SW2);
+  const size_t lds2 = (size_t)SN * score_lds_stride(a.d) * 4;
   if (mode == 0) {
     if (!a.out) return set_error(REGCN_EINVAL, "null output");
-    if (a.use_dist) hipLaunchKernelGGL((k_score<0, true>), g, b, 0, st, a);
+    if (fast) hipLaunchKernelGGL((k_score_f32<0>), g2, b2, lds2, st, a);
+    else if (a.use_dist) hipLaunchKernelGGL((k_score<0, true>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_score<0, false>), g, b, 0, st, a);
     return check_launch("k_score");
   }
   if (!a.target || !a.part || !a.tgt_logit || !loss) return set_error(REGCN_EINVAL, "CE needs target/workspace/loss");
-  if (a.use_dist) hipLaunchKernelGGL((k_score<1, true>), g, b, 0, st, a);
+  if (fast) hipLaunchKernelGGL((k_score_f32<1>), g2, b2, lds2, st, a);
+  else if (a.use_dist) hipLaunchKernelGGL((k_score<1, true>), g, b, 0, st, a);
   else hipLaunchKernelGGL((k_score<1, false>), g, b, 0, st, a);
   int rc = check_launch("k_score_ce");
   if (rc) return rc;

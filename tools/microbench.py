@@ -128,10 +128,40 @@ def trace_gru(V=7128, R=230, per_snap=246, d=200):
     print("  " + " ".join("%s %.2f/%.2f" % (k, float(v.median()), float(v.max())) for k, v in ph))
 
 
+def trace_score(B=492, N=7128, d=200):
+    """Phase stamps of the all-entity scorer (k_score_f32): operand staging, then the MFMA
+    loop (Q E^T) with the score epilogue."""
+    from regcn_amd import _lib
+    from regcn_amd.hyperbolic_decoder import _chunked_hyperbolic_dist_score as sc
+    torch.manual_seed(0)
+    q = H.exp_map_zero(torch.randn(B, d, device=dev) * 0.3, C)
+    e = H.exp_map_zero(torch.randn(N, d, device=dev) * 0.3, C)
+    bias = torch.randn(N, device=dev) * 0.1
+    n_wg = ((B + 127) // 128) * ((N + 63) // 64)  # k_score_f32: 128 queries x 64 candidates
+    with torch.no_grad():
+        for _ in range(3):
+            sc(q, e, bias, C, 128, 256)
+        buf = torch.zeros(n_wg * 16, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        _lib.call("regcn_set_trace", _lib.addr(buf, torch.int64))
+        sc(q, e, bias, C, 128, 256)
+        torch.cuda.synchronize()
+        _lib.call("regcn_set_trace", None)
+    t = buf.view(n_wg, 16).cpu().double()
+    t0 = t[:, 0].min()
+    us = lambda a, b: (t[:, b] - t[:, a]) / 100.0
+    print("score B=%d N=%d workgroups=%d total %.1f us" % (B, N, n_wg, float((t[:, 2].max() - t0) / 100.0)))
+    start = (t[:, 0] - t0) / 100.0
+    ph = [("start", start), ("stage", us(0, 1)), ("mfma+epilogue", us(1, 2))]
+    print("  " + " ".join("%s %.2f/%.2f" % (k, float(v.median()), float(v.max())) for k, v in ph))
+    print("  start quartiles %s" % [round(float(x), 2) for x in torch.quantile(start, torch.tensor([0.25, 0.5, 0.75, 1.0], dtype=torch.float64))])
+
+
 if __name__ == "__main__":
     if "--trace" in sys.argv:
         trace()
         trace_gru()
+        trace_score()
         sys.exit(0)
     print("peaks: %.1f TF fp32 MFMA, %.0f GB/s HBM" % (FP32_MFMA_PEAK_TFLOPS, HBM_PEAK_GBS))
     for V, R, ps in [(7128, 230, 246), (23033, 256, 1540), (100000, 256, 250000), (1000000, 256, 2500000)]:
