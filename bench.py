@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--pool", type=int, default=4, help="distinct samples cycled through the timed steps")
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph replay")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="steps captured per HIP graph (default: the whole pool, replayed as one launch; "
+                         "1 = one graph per step)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work")
     ap.add_argument("--no-scale", action="store_true",
@@ -287,7 +290,10 @@ def main():
         for w in range(max(args.warmup, 1)):
             eager(w % len(samples))
     torch.cuda.synchronize()
-    graphs = []
+    # HIP graphs: one per step (graph_steps = 1), and one holding the whole pool's steps in
+    # sequence, so consecutive steps do not pay a graph launch each (~20 us on this runtime)
+    graphs, pool_graph = [], None
+    gs = args.graph_steps or len(samples)
     if not args.no_graph:
         cap = torch.cuda.Stream(device)
         with torch.no_grad():
@@ -299,17 +305,32 @@ def main():
                     with torch.cuda.graph(gph, stream=cap):
                         eager(i)
                 graphs.append(gph)
+            if gs > 1 and gs == len(samples):
+                pool_graph = torch.cuda.CUDAGraph()
+                with torch.cuda.stream(cap):
+                    with torch.cuda.graph(pool_graph, stream=cap):
+                        for i in range(len(samples)):
+                            eager(i)
         for gph in graphs:
             gph.replay()
+        if pool_graph is not None:
+            pool_graph.replay()
         torch.cuda.synchronize()
 
-    def step(k):
-        i = k % len(samples)
-        if graphs:
-            graphs[i].replay()
-        else:
-            with torch.no_grad():
-                eager(i)
+    def run_steps(k0, n):
+        """Steps k0 .. k0 + n - 1 (sample k % pool): whole-pool graph launches where aligned."""
+        k = k0
+        while k < k0 + n:
+            if pool_graph is not None and k % len(samples) == 0 and k + len(samples) <= k0 + n:
+                pool_graph.replay()
+                k += len(samples)
+            elif graphs:
+                graphs[k % len(samples)].replay()
+                k += 1
+            else:
+                with torch.no_grad():
+                    eager(k % len(samples))
+                k += 1
 
     epw = [edges_per_step(s[1]) for s in samples]
     if world > 1:
@@ -317,8 +338,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
+    run_steps(0, args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -364,7 +384,7 @@ def main():
                "config": {"workload": cfg["label"], "V": cfg["V"], "R": cfg["R"], "triples_per_snapshot":
                           cfg["per_snap"], "history_len": cfg["T"], "n_layers": 2, "d": d,
                           "edges_per_step": int(np.mean(epw)), "queries_per_step": 2 * cfg["per_snap"],
-                          "hip_graph": bool(graphs),
+                          "hip_graph": bool(graphs), "steps_per_graph_launch": len(samples) if pool_graph else 1,
                           "parallelism": ("%s-partitioned snapshots x%d" % (args.shard, world)) if sharded
                           else "replicas x%d" % world},
                "roofline": roof, "kernels": kernels, "aggregation_roofline": scale, "cpu_baseline": cpu}
