@@ -224,9 +224,17 @@ def aggregation_at_scale(device):
     res = measure(dev=device, which=("union_aggregate", "lorentz_aggregate"), log=lambda m: None)
     out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "config": "synthetic |V|=%d |E|=%d R2=%d d=%d"
            % (res["V"], res["E"], res["R2"], res["d"]), "bytes_per_launch": res["b_agg_bytes"]}
-    for k in ("union_aggregate", "lorentz_aggregate"):
+    try:  # HBM bytes per launch from the committed PMC passes of tools/aggbench.py
+        with open(os.path.join(REPO, "profiles", "pmc_traffic_agg.json")) as fh:
+            pmc = json.load(fh)["kernels"]
+    except (OSError, ValueError, KeyError):
+        pmc = {}
+    for k, kern in (("union_aggregate", "k_gather_sum<0>"), ("lorentz_aggregate", "k_lorentz_sum<2>")):
+        tr = pmc.get(kern, {}).get("hbm_bytes")
         out[k] = {"achieved": res[k]["algorithmic_GBps"], "frac": res[k]["hbm_frac"], "avg_launch_us":
-                  round(res[k]["ms"] * 1e3, 1), "G_edges_per_s": res[k]["edges_per_s_G"]}
+                  round(res[k]["ms"] * 1e3, 1), "G_edges_per_s": res[k]["edges_per_s_G"], "kernel": kern,
+                  "traffic": tr, "traffic_source": "profiles/pmc_traffic_agg.json (rocprofv3 FETCH_SIZE x2 + "
+                  "WRITE_SIZE of tools/aggbench.py)" if tr else None}
     torch.cuda.empty_cache()
     return out
 
