@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 2
+#define REGCN_ABI_VERSION 3
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -270,6 +270,88 @@ int regcn_hyp_ce_f32(const float* q, const float* cand, const float* bias, const
  * true answers (filt_ptr [B+1], filt_idx; NULL filt_ptr skips the filtered rank). */
 int regcn_rank_f32(const float* score, int32_t B, int32_t N, const int32_t* target, const int32_t* filt_ptr,
                    const int32_t* filt_idx, int32_t* rank_raw, int32_t* rank_filt, void* stream);
+
+/* ---- a1 / f3: snapshot construction on the device ------------------------------------
+ * build_sub_graph + r2e (rgcn/utils.py:78-134) and the kernel work lists of
+ * re-gcn_amd/regcn_amd/graph.py, built from the snapshot's triples in HBM.  Every output
+ * is bit-identical to the host build: the destination sort is a stable LSD radix sort (edge
+ * ids keep their order within a destination, as the reference's edge order), r_to_e spans
+ * hold each relation's entities ascending (np.unique), rows are ordered by descending
+ * in-degree (stable), tiles follow the host's greedy packing.
+ *
+ * Two calls on one stream with a host read of `stats` in between (the work-list call needs
+ * the tile budget, which the host derives from the maximum in-degree):
+ *   1. regcn_snapshot_csr_i32   triples -> in_deg, rowptr, col_src/col_type, norm, edge
+ *      type/norm (reference edge order), r2e lists; stats[MAX_DEG, N_POS, INVALID, N_PAIRS,
+ *      REL_MAX].
+ *   2. regcn_snapshot_work_i32  -> rows, tiles + items, heavy / all-row / relation chunk
+ *      and fix-up lists (capacity-sized buffers, counts in stats).
+ * Capacities: regcn_snapshot_capacity(what, ...) elements (int32, x4 for chunk and
+ * fix-up records, x2 for tiles); workspace: regcn_snapshot_workspace_bytes(T, V, R). */
+#define REGCN_SNAP_MAX_DEG 0
+#define REGCN_SNAP_N_POS 1
+#define REGCN_SNAP_INVALID 2    /* triples with an id out of range (the build is then void) */
+#define REGCN_SNAP_N_PAIRS 3    /* sum over relations of |r_to_e[r]| (forward spans) */
+#define REGCN_SNAP_REL_MAX 4    /* longest r_to_e span */
+#define REGCN_SNAP_N_HEAVY 5
+#define REGCN_SNAP_N_TILES 6
+#define REGCN_SNAP_N_ITEMS 7
+#define REGCN_SNAP_WALK_TILES 8 /* tiles placed by the sequential greedy prefix */
+#define REGCN_SNAP_A_STAR 9     /* first row from which 16-row tiles always fit */
+#define REGCN_SNAP_CHUNKS 10    /* all-row chunk list: n_chunks, n_fix, n_slots */
+#define REGCN_SNAP_HEAVY_CHUNKS 13
+#define REGCN_SNAP_REL_CHUNKS 16
+#define REGCN_SNAP_NSTATS 20
+
+#define REGCN_CAP_TILES 0        /* int32[cap][2] */
+#define REGCN_CAP_ITEMS 1
+#define REGCN_CAP_CHUNKS 2       /* int32[cap][4] */
+#define REGCN_CAP_FIXUPS 3
+#define REGCN_CAP_HEAVY_CHUNKS 4
+#define REGCN_CAP_HEAVY_FIXUPS 5
+#define REGCN_CAP_REL_CHUNKS 6
+#define REGCN_CAP_REL_FIXUPS 7
+#define REGCN_CAP_REL_IDX 8
+
+typedef struct regcn_snapshot_desc {
+  const int64_t* triples;  /* T x 3 (s, r, o), device */
+  int64_t T;
+  int32_t V, R;            /* entities, base relations (edge types 0 .. 2R-1) */
+  int32_t budget;          /* graph.py tile_budget_for(); used by call 2 */
+  int32_t pack_items;      /* graph.py pack_items */
+  int32_t chunk_edges;     /* graph.py chunk_size_for() */
+  void* workspace;
+  size_t ws_bytes;
+  int32_t* stats;          /* REGCN_SNAP_NSTATS */
+  /* call 1 outputs */
+  int32_t* in_deg;         /* V */
+  int32_t* rowptr;         /* V + 1 */
+  int32_t* col_src;        /* E = 2T, destination-sorted */
+  int32_t* col_type;       /* E */
+  float* norm;             /* V: 1 / in_deg, 0 -> 1 (utils.py:110-114) */
+  int64_t* edge_type;      /* E, reference edge order: cat(r, r + R) (utils.py:118, :125) */
+  float* edge_norm;        /* E, reference edge order: norm[dst] * norm[src] (utils.py:124) */
+  int32_t* rel_ent_count;  /* R: |r_to_e[r]| */
+  int32_t* rel_idx;        /* REGCN_CAP_REL_IDX: r_to_e flattened in uniq_r order */
+  int32_t* rel_start;      /* 2R */
+  float* rel_count;        /* 2R */
+  /* call 2 outputs */
+  int32_t* rows;           /* V */
+  int32_t* tiles;
+  int32_t* item_ptr;       /* V + 1 */
+  int32_t* item_src;
+  int32_t* item_tl;
+  int32_t* chunks;
+  int32_t* fixups;
+  int32_t* heavy_chunks;
+  int32_t* heavy_fixups;
+  int32_t* rel_chunks;
+  int32_t* rel_fixups;
+} regcn_snapshot_desc;
+size_t regcn_snapshot_workspace_bytes(int64_t T, int32_t V, int32_t R);
+int64_t regcn_snapshot_capacity(int32_t what, int64_t T, int32_t V, int32_t R, int32_t chunk_edges);
+int regcn_snapshot_csr_i32(const regcn_snapshot_desc* desc, void* stream);
+int regcn_snapshot_work_i32(const regcn_snapshot_desc* desc, void* stream);
 
 #ifdef __cplusplus
 }

@@ -339,4 +339,11 @@ int regcn_rank_f32(const float* score_m, int32_t B, int32_t N, const int32_t* ta
   return rank(score_m, B, N, target, filt_ptr, filt_idx, rank_raw, rank_filt, ST(s));
 }
 
+size_t regcn_snapshot_workspace_bytes(int64_t T, int32_t V, int32_t R) { return snapshot_ws_bytes(T, V, R); }
+int64_t regcn_snapshot_capacity(int32_t what, int64_t T, int32_t V, int32_t R, int32_t chunk_edges) {
+  return snapshot_capacity(what, T, V, R, chunk_edges);
+}
+int regcn_snapshot_csr_i32(const regcn_snapshot_desc* desc, void* s) { return snapshot_csr(desc, ST(s)); }
+int regcn_snapshot_work_i32(const regcn_snapshot_desc* desc, void* s) { return snapshot_work(desc, ST(s)); }
+
 }  // extern "C"

@@ -40,6 +40,12 @@ int lorentz_sum(const float* x, const float* rel, const float* W, const int* col
                 const void* chunks, int n_chunks, const void* fixups, int n_fix, int nb, float c, int d,
                 float* partial, int pstride, float* out, hipStream_t st);
 
+// graphbuild.hip
+int snapshot_csr(const regcn_snapshot_desc* d, hipStream_t st);
+int snapshot_work(const regcn_snapshot_desc* d, hipStream_t st);
+size_t snapshot_ws_bytes(int64_t T, int V, int R);
+int64_t snapshot_capacity(int what, int64_t T, int V, int R, int C);
+
 // ---- argument blocks of the fused kernels (layer.hip, score.hip) ----
 struct StepArgs {
   const float* hc;

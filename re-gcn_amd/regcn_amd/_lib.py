@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libregcn_hip.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -56,10 +56,15 @@ _SIGS = {
     "regcn_relation_gru_f32": [P, P, P, P, P, P, P, P, P, P, P, _c_int, _c_int, P, P],
     "regcn_roth_query_f32": [P, P, P, _c_int, _c_int, _c_int, P, P, P, P, P, P, P, P, _c_int, _c_f, P, P],
     "regcn_roth_rel_query_f32": [P, P, _c_int, _c_int, _c_int, P, P, P, P, P, P, _c_int, _c_int, _c_f, P, P, P],
+    "regcn_snapshot_workspace_bytes": [_c_i64, _c_int, _c_int],
+    "regcn_snapshot_capacity": [_c_int, _c_i64, _c_int, _c_int, _c_int],
+    "regcn_snapshot_csr_i32": [P, P],
+    "regcn_snapshot_work_i32": [P, P],
 }
 
 SCORE_DIST, SCORE_RAW_SCALE = 1, 2
 _RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz,
+            "regcn_snapshot_workspace_bytes": _c_sz, "regcn_snapshot_capacity": _c_i64,
             "regcn_packed_weight_floats": _c_sz, "regcn_packed_linear_floats": _c_sz}
 
 _lib = None
@@ -80,6 +85,28 @@ class LayerDesc(ctypes.Structure):
         ("step_layer_norm", _c_int), ("step_residual", _c_int), ("step_c_radius", _c_f), ("step_h_out", P),
         ("step_x_out", P), ("step_r_out", P), ("trace", P),
     ]
+
+
+# regcn_snapshot_desc (include/regcn_hip.h): stats slots and capacity ids
+SNAP = dict(MAX_DEG=0, N_POS=1, INVALID=2, N_PAIRS=3, REL_MAX=4, N_HEAVY=5, N_TILES=6, N_ITEMS=7, WALK_TILES=8,
+            A_STAR=9, CHUNKS=10, HEAVY_CHUNKS=13, REL_CHUNKS=16, NSTATS=20)
+CAP = dict(TILES=0, ITEMS=1, CHUNKS=2, FIXUPS=3, HEAVY_CHUNKS=4, HEAVY_FIXUPS=5, REL_CHUNKS=6, REL_FIXUPS=7,
+           REL_IDX=8)
+
+
+class SnapshotDesc(ctypes.Structure):
+    _fields_ = [
+        ("triples", P), ("T", _c_i64), ("V", _c_int), ("R", _c_int), ("budget", _c_int), ("pack_items", _c_int),
+        ("chunk_edges", _c_int), ("workspace", P), ("ws_bytes", _c_sz), ("stats", P),
+        ("in_deg", P), ("rowptr", P), ("col_src", P), ("col_type", P), ("norm", P), ("edge_type", P),
+        ("edge_norm", P), ("rel_ent_count", P), ("rel_idx", P), ("rel_start", P), ("rel_count", P),
+        ("rows", P), ("tiles", P), ("item_ptr", P), ("item_src", P), ("item_tl", P), ("chunks", P), ("fixups", P),
+        ("heavy_chunks", P), ("heavy_fixups", P), ("rel_chunks", P), ("rel_fixups", P),
+    ]
+
+
+def call_desc(name, desc):
+    check(getattr(lib(), name)(ctypes.byref(desc), stream()), name)
 
 
 class HipLibraryError(RuntimeError):

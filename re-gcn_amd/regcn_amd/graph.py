@@ -19,7 +19,9 @@ object carries the device-side work lists the HIP kernels consume:
   * `rows` int32[V]: rows with in-degree > 0 first, then the rest (`n_pos` of the
     former), so every 64-row tile of the layer GEMM uses one self-loop weight;
   * the same chunking over r_to_e for the relation-context mean.
-Built once per snapshot on the host and cached across epochs.
+Built once per snapshot and cached across epochs: on the device by
+csrc/graphbuild.hip when use_cuda (build_sub_graph_device), else with numpy here; both
+builds produce the same lists bit for bit (tests/test_gpu_graph.py).
 """
 import numpy as np
 import torch
@@ -170,7 +172,7 @@ class SnapshotGraph:
             rchunks, rfix, rslot = _chunk_rows_spans(rel_start, rel_len, self.chunk_edges)
         else:
             rchunks, rfix, rslot = np.zeros((0, 4), np.int32), np.zeros((0, 4), np.int32), 0
-        self._host = {
+        self._host_lists = {
             "col_src": col_src_s.astype(np.int32), "col_type": col_type_s.astype(np.int32),
             "chunks": chunks, "fixups": fixups, "norm": norm,
             "rel_idx": np.asarray(r_to_e, dtype=np.int32).reshape(-1),
@@ -178,7 +180,7 @@ class SnapshotGraph:
             "rel_start": rel_start.astype(np.int32),
             "rowptr": rowptr.astype(np.int32),
         }
-        self._host.update(fw.host)
+        self._host_lists.update(fw.host)
         self.n_pos, self.n_pos_tiles = fw.n_pos, fw.n_pos_tiles
         self.n_heavy, self.heavy_slots = fw.n_heavy, fw.heavy_slots
         self.n_slots = nslot
@@ -212,13 +214,18 @@ class SnapshotGraph:
         device = torch.device(device)
         if device == self.device:
             return self
-        g = object.__new__(SnapshotGraph)
+        g = object.__new__(type(self))
         g.__dict__.update(self.__dict__)
         g.device = device
         g.ndata = _Frame({k: v.to(device) for k, v in self.ndata.items()})
         g.edata = _Frame({k: v.to(device) for k, v in self.edata.items()})
         g.dev = {k: torch.from_numpy(v).to(device) for k, v in self._host.items()} if device.type == "cuda" else None
         return g
+
+    @property
+    def _host(self):
+        """Host copies of the kernel work lists (int32 / fp32 numpy)."""
+        return self._host_lists
 
     def work(self):
         """Device work lists (raises on a CPU graph: the HIP path has no CPU fallback)."""
@@ -340,10 +347,196 @@ def _chunk_rows_spans(start, length, chunk_edges):
     return chunks, fixups, nslot
 
 
+class DeviceSnapshotGraph(SnapshotGraph):
+    """A SnapshotGraph whose CSR, r2e lists and work lists were built by the HIP kernels
+    (csrc/graphbuild.hip) from the triples in HBM.  The device lists are bit-identical to
+    the host build's; the host-side views (edges(), in_degrees(), r_to_e, `_host`) are
+    copied back lazily, only when something asks for them."""
+
+    def _lazy(self, key, fn):
+        v = self.__dict__.get(key)
+        if v is None:
+            v = fn()
+            self.__dict__[key] = v
+        return v
+
+    def _tri(self):
+        return self._lazy("_tri_np", lambda: self._tri_dev.cpu().numpy())
+
+    @property
+    def src_np(self):
+        t = self._tri()
+        return self._lazy("_src", lambda: np.concatenate((t[:, 0], t[:, 2])))
+
+    @property
+    def dst_np(self):
+        t = self._tri()
+        return self._lazy("_dst", lambda: np.concatenate((t[:, 2], t[:, 0])))
+
+    @property
+    def type_np(self):
+        t = self._tri()
+        return self._lazy("_type", lambda: np.concatenate((t[:, 1], t[:, 1] + self.num_rels)))
+
+    @property
+    def in_deg_np(self):
+        return self._lazy("_in_deg", lambda: self.dev_all["in_deg"].cpu().numpy().astype(np.int64))
+
+    @property
+    def r_to_e(self):
+        return self._lazy("_r_to_e", lambda: torch.from_numpy(self.dev_all["rel_idx"].cpu().numpy().astype(np.int64)))
+
+    @property
+    def _host(self):
+        return self._lazy("_host_cache", lambda: {k: v.cpu().numpy() for k, v in self.dev_all.items()
+                                                  if k != "in_deg"})
+
+    def in_degrees(self, v=None):
+        deg = self.dev_all["in_deg"].long()
+        if v is None:
+            return deg
+        idx = torch.as_tensor(list(v) if isinstance(v, range) else v, dtype=torch.long, device=deg.device)
+        return deg[idx]
+
+    def edges(self):
+        return torch.from_numpy(self.src_np), torch.from_numpy(self.dst_np)
+
+    def number_of_edges(self):
+        return 2 * int(self._tri_dev.shape[0])
+
+    def to(self, device):
+        if isinstance(device, int):
+            device = torch.device("cuda", device) if device >= 0 else torch.device("cpu")
+        device = torch.device(device)
+        if device == self.device:
+            return self
+        # another device: rebuild from the host view (rare: the graph is built where it is used)
+        host = SnapshotGraph(self.num_nodes_, self.num_rels, self.src_np, self.dst_np, self.type_np, self.uniq_r,
+                             self.r_len, self.r_to_e.tolist(), chunk_edges=self.chunk_edges, tile_budget=self.budget)
+        return host.to(device)
+
+
+def _ptr(t):
+    import ctypes
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def build_sub_graph_device(num_nodes, num_rels, triples, device, chunk_edges=DEFAULT_CHUNK_EDGES, tile_budget=None):
+    """rgcn/utils.py:100-134 on the device: two library calls
+    (regcn_snapshot_csr_i32, regcn_snapshot_work_i32) with one small host read of the
+    counts between them (the tile budget depends on the maximum in-degree) and one after
+    (list lengths).  Returns a DeviceSnapshotGraph on `device`."""
+    from . import _lib
+    device = torch.device(device)
+    if device.type != "cuda":
+        raise ValueError("the device graph build needs a HIP device (got %s)" % device)
+    V, R = int(num_nodes), int(num_rels)
+    if isinstance(triples, torch.Tensor):
+        tri = triples.to(device=device, dtype=torch.int64).reshape(-1, 3).contiguous()
+        tri_np = None
+    else:
+        tri_np = np.ascontiguousarray(np.asarray(triples, dtype=np.int64).reshape(-1, 3))
+        tri = torch.from_numpy(tri_np).to(device)
+    T = int(tri.shape[0])
+    E = 2 * T
+    ce = int(chunk_edges) if chunk_edges else chunk_size_for(E)
+    lib = _lib.lib()
+    S = _lib.SNAP
+
+    def i32(n):
+        return torch.empty(max(int(n), 1), dtype=torch.int32, device=device)
+
+    def cap(what):
+        c = int(lib.regcn_snapshot_capacity(_lib.CAP[what], T, V, R, ce))
+        if c < 0:
+            raise RuntimeError("regcn_snapshot_capacity(%s) failed" % what)
+        return c
+
+    ws = torch.empty(int(lib.regcn_snapshot_workspace_bytes(T, V, R)), dtype=torch.uint8, device=device)
+    stats = torch.zeros(S["NSTATS"], dtype=torch.int32, device=device)
+    out = {
+        "in_deg": i32(V), "rowptr": i32(V + 1), "col_src": i32(E), "col_type": i32(E),
+        "norm": torch.empty(V, dtype=torch.float32, device=device),
+        "rel_ent_count": i32(R), "rel_idx": i32(cap("REL_IDX")), "rel_start": i32(2 * R),
+        "rel_count": torch.empty(2 * R, dtype=torch.float32, device=device),
+    }
+    etype = torch.empty(max(E, 1), dtype=torch.int64, device=device)
+    enorm = torch.empty(max(E, 1), dtype=torch.float32, device=device)
+    d = _lib.SnapshotDesc()
+    d.triples = _ptr(tri) if T else None
+    d.T, d.V, d.R, d.chunk_edges = T, V, R, ce
+    d.workspace, d.ws_bytes, d.stats = _ptr(ws), ws.numel(), _ptr(stats)
+    for k, v in out.items():
+        setattr(d, k, _ptr(v))
+    d.edge_type, d.edge_norm = _ptr(etype), _ptr(enorm)
+    _lib.call_desc("regcn_snapshot_csr_i32", d)
+    st = stats.cpu().numpy()
+    if st[S["INVALID"]]:
+        raise ValueError("%d triples hold an entity id outside [0, %d) or a relation id outside [0, %d)"
+                         % (int(st[S["INVALID"]]), V, R))
+    budget = int(tile_budget) if tile_budget else tile_budget_for(E, ce, int(st[S["MAX_DEG"]]))
+    pack = min(32, budget) if E <= 65536 else budget
+    work = {
+        "rows": i32(V), "tiles": i32(2 * cap("TILES")), "item_ptr": i32(V + 1), "item_src": i32(cap("ITEMS")),
+        "item_tl": i32(cap("ITEMS")), "chunks": i32(4 * cap("CHUNKS")), "fixups": i32(4 * cap("FIXUPS")),
+        "heavy_chunks": i32(4 * cap("HEAVY_CHUNKS")), "heavy_fixups": i32(4 * cap("HEAVY_FIXUPS")),
+        "rel_chunks": i32(4 * cap("REL_CHUNKS")), "rel_fixups": i32(4 * cap("REL_FIXUPS")),
+    }
+    d.budget, d.pack_items = budget, pack
+    for k, v in work.items():
+        setattr(d, k, _ptr(v))
+    _lib.call_desc("regcn_snapshot_work_i32", d)
+    st = stats.cpu().numpy().astype(np.int64)
+
+    def rec(t, n, w):
+        return t[:n * w].view(n, w)
+
+    n_tiles = int(st[S["N_TILES"]])
+    ch, hc, rc = S["CHUNKS"], S["HEAVY_CHUNKS"], S["REL_CHUNKS"]
+    n_pairs = int(st[S["N_PAIRS"]])
+    dev = {
+        "col_src": out["col_src"][:E], "col_type": out["col_type"][:E],
+        "chunks": rec(work["chunks"], st[ch], 4), "fixups": rec(work["fixups"], st[ch + 1], 4),
+        "norm": out["norm"], "rel_idx": out["rel_idx"][:2 * n_pairs], "rel_count": out["rel_count"],
+        "rel_chunks": rec(work["rel_chunks"], st[rc], 4), "rel_fixups": rec(work["rel_fixups"], st[rc + 1], 4),
+        "rel_start": out["rel_start"], "rowptr": out["rowptr"], "rows": work["rows"][:V],
+        "tiles": rec(work["tiles"], n_tiles, 2), "heavy_chunks": rec(work["heavy_chunks"], st[hc], 4),
+        "heavy_fixups": rec(work["heavy_fixups"], st[hc + 1], 4), "item_src": work["item_src"][:st[S["N_ITEMS"]]],
+        "item_tl": work["item_tl"][:st[S["N_ITEMS"]]], "item_ptr": work["item_ptr"][:n_tiles + 1],
+    }
+    g = object.__new__(DeviceSnapshotGraph)
+    g.num_nodes_, g.num_rels, g.device = V, R, device
+    g._tri_dev = tri
+    if tri_np is not None:
+        g._tri_np = tri_np
+    cnt = out["rel_ent_count"][:R].cpu().numpy().astype(np.int64)
+    present = np.nonzero(cnt)[0]
+    g.uniq_r = np.concatenate((present, present + R))
+    starts = np.cumsum(cnt[present]) - cnt[present]
+    g.r_len = [(int(a), int(a + n)) for a, n in zip(starts, cnt[present])] + \
+              [(int(n_pairs + a), int(n_pairs + a + n)) for a, n in zip(starts, cnt[present])]
+    g.ndata = _Frame(id=torch.arange(V, dtype=torch.long, device=device).view(-1, 1), norm=out["norm"].view(-1, 1))
+    g.edata = _Frame(type=etype[:E], norm=enorm[:E].view(-1, 1))
+    g.chunk_edges, g.budget, g.pack_items = ce, budget, pack
+    g.n_pos, g.n_pos_tiles = int(st[S["N_POS"]]), n_tiles
+    g.n_heavy, g.heavy_slots = int(st[S["N_HEAVY"]]), int(st[hc + 2])
+    g.n_slots, g.rel_slots = int(st[ch + 2]), int(st[rc + 2])
+    g.rel_max_span = int(st[S["REL_MAX"]])
+    g.dev = dev
+    g.dev_all = dict(dev, in_deg=out["in_deg"][:V])
+    return g
+
+
 def build_sub_graph(num_nodes, num_rels, triples, use_cuda=False, gpu=0, chunk_edges=DEFAULT_CHUNK_EDGES,
-                    tile_budget=None):
+                    tile_budget=None, device_build=True):
     """rgcn/utils.py:100-134 (same signature; returns a SnapshotGraph).  chunk_edges /
-    tile_budget override the work-list heuristics (tests use them to force split rows)."""
+    tile_budget override the work-list heuristics (tests use them to force split rows).
+    With use_cuda the snapshot is built on the device (build_sub_graph_device; its lists
+    equal the host build's bit for bit); device_build=False keeps the numpy build."""
+    if use_cuda and device_build:
+        dev = torch.device("cuda", gpu) if isinstance(gpu, int) else torch.device(gpu)
+        return build_sub_graph_device(num_nodes, num_rels, triples, dev, chunk_edges=chunk_edges,
+                                      tile_budget=tile_budget)
     triples = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
     s, r, o = triples[:, 0], triples[:, 1], triples[:, 2]
     src = np.concatenate((s, o))

@@ -17,7 +17,7 @@ LIB = os.path.join(REPO, "re-gcn_amd", "regcn_amd", "libregcn_hip.so")
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*|size_t)\s+(regcn_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*|size_t)\s+(regcn_\w+)\s*\(", txt, re.M)))
 
 
 @pytest.mark.skipif(not os.path.exists(LIB), reason="libregcn_hip.so not built (run __graft_entry__.build())")
