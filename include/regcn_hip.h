@@ -348,10 +348,87 @@ typedef struct regcn_snapshot_desc {
   int32_t* rel_chunks;
   int32_t* rel_fixups;
 } regcn_snapshot_desc;
+/* Transposed edge lists for the backward passes: csr_dst[p] = destination of CSR position p;
+ * positions sorted (stably) by source (sptr [V+1], sp [E]) and by type (tptr [R2+1], tp [E]). */
+typedef struct regcn_transpose_desc {
+  int32_t V, E, R2;
+  const int32_t* rowptr;
+  const int32_t* col_src;
+  const int32_t* col_type;
+  void* workspace;         /* regcn_transpose_workspace_bytes(E, V, R2) */
+  size_t ws_bytes;
+  int32_t* csr_dst;
+  int32_t* sptr;
+  int32_t* sp;
+  int32_t* tptr;
+  int32_t* tp;
+} regcn_transpose_desc;
+size_t regcn_transpose_workspace_bytes(int32_t E, int32_t V, int32_t R2);
+int regcn_snapshot_transpose_i32(const regcn_transpose_desc* desc, void* stream);
 size_t regcn_snapshot_workspace_bytes(int64_t T, int32_t V, int32_t R);
 int64_t regcn_snapshot_capacity(int32_t what, int64_t T, int32_t V, int32_t R, int32_t chunk_edges);
 int regcn_snapshot_csr_i32(const regcn_snapshot_desc* desc, void* stream);
 int regcn_snapshot_work_i32(const regcn_snapshot_desc* desc, void* stream);
+
+/* ---- f1: backward kernels of the training path -----------------------------------------
+ * Gradients as torch autograd computes them through the reference op sequence, clamp
+ * subgradients included (see csrc/backward.hip). */
+#define REGCN_BWD_LOG0 0         /* HyperbolicOps.log_map_zero */
+#define REGCN_BWD_EXP0 1         /* HyperbolicOps.exp_map_zero */
+#define REGCN_BWD_PROJECT 2      /* HyperbolicOps.project_to_ball */
+#define REGCN_BWD_APPLY_RADIUS 3 /* y: radius [rows]; dy: d radius [rows] */
+#define REGCN_BWD_RADIUS 4       /* g: [rows] (get_radius output gradient) */
+#define REGCN_BWD_MOBIUS 5       /* y: second operand; dy: its gradient */
+int regcn_rowmap_bwd_f32(int32_t op, const float* x, const float* y, const float* g, int64_t rows, int32_t d,
+                         float c, float* dx, float* dy, void* stream);
+
+typedef struct regcn_edge_bwd_desc {
+  int32_t V, E, R2, d;
+  const float* x;          /* V x d layer input (tangent) */
+  const float* radius;     /* V (union) */
+  const float* rel;        /* R2 x d */
+  const float* W;          /* R2 x nb*s*s (Lorentz) */
+  const float* norm;       /* V (union) */
+  const int32_t* rowptr;
+  const int32_t* col_src;
+  const int32_t* col_type;
+  const int32_t* csr_dst;  /* regcn_snapshot_transpose_i32 */
+  const int32_t* sptr;
+  const int32_t* sp;
+  const int32_t* tptr;
+  const int32_t* tp;
+  const float* G;          /* V x d: gradient of the aggregation (union) / of the raw sums' space part (Lorentz) */
+  const float* G0;         /* V: gradient of the raw sums' time coordinate (Lorentz) */
+  float* dx;               /* V x d */
+  float* drel;             /* R2 x d */
+  float* dradius;          /* V (union) */
+  float* dW;               /* R2 x nb*s*s (Lorentz) */
+  float* edge_scratch;     /* union: 2E + V floats */
+} regcn_edge_bwd_desc;
+/* HyperbolicUnionRGCNLayer message/sum/apply (hyperbolic_layers.py:222-240, :290) backward:
+ * dx, drel and dradius of agg[v] = norm[v] sum_e w_e (x[src] + rel[type]). */
+int regcn_union_aggregate_bwd_f32(const regcn_edge_bwd_desc* desc, float gamma, void* stream);
+/* LorentzRGCNLayer messages (hyperbolic_layers.py:589-611) summed per destination, before the
+ * centroid: S0[v] = sum_e L0_e, Sv[v] = sum_e L_e[1:] (training forward; the centroid, to_poincare
+ * and log0 run as separate differentiable ops). */
+int regcn_lorentz_sum_raw_f32(const float* x, const float* rel, const float* weight, const int32_t* rowptr,
+                              const int32_t* col_src, const int32_t* col_type, int32_t V, int32_t d, int32_t num_bases,
+                              float c, float* S0, float* Sv, void* stream);
+/* ... and its backward: dx, drel, dW from (G0, G) = gradient of (S0, Sv). */
+int regcn_lorentz_aggregate_bwd_f32(const regcn_edge_bwd_desc* desc, int32_t num_bases, float c, void* stream);
+/* Cross-entropy scorer (regcn_hyp_ce_f32) with the per-query log-sum-exp as an extra output. */
+int regcn_hyp_ce_lse_f32(const float* q, const float* cand, const float* bias, const float* scale,
+                         const float* margin, const int32_t* target, int32_t B, int32_t N, int32_t d, float c,
+                         int32_t flags, void* workspace, float* loss_per_query, float* lse, void* stream);
+/* _chunked_hyperbolic_ce_loss backward (proxy score): with G = gl (softmax - onehot),
+ * coef[b,n] = G dS/d<q_b,e_n>, rsum[b][nblk] (nblk = ceil(N/64)) partial sums over candidates of
+ * G dS/d|q_b|^2, csum[ng][N][3] (ng = 8 ceil(B/128)) partial sums over 16-query groups of
+ * (G dS/d|e_n|^2, G, G (margin - n^2)).  Then dq = coef E + 2 q sum(rsum), de = coef^T Q +
+ * 2 e csum[.,0], dbias = csum[.,1], dscale = sum csum[.,2], dmargin = scale sum csum[.,1]. */
+int regcn_hyp_ce_bwd_f32(const float* q, const float* cand, const float* bias, const float* scale,
+                         const float* margin, const int32_t* target, const float* lse, const float* grad_loss,
+                         int32_t B, int32_t N, int32_t d, float c, int32_t flags, float* coef, float* rsum,
+                         float* csum, void* stream);
 
 #ifdef __cplusplus
 }

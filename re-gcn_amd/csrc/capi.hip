@@ -346,4 +346,49 @@ int64_t regcn_snapshot_capacity(int32_t what, int64_t T, int32_t V, int32_t R, i
 int regcn_snapshot_csr_i32(const regcn_snapshot_desc* desc, void* s) { return snapshot_csr(desc, ST(s)); }
 int regcn_snapshot_work_i32(const regcn_snapshot_desc* desc, void* s) { return snapshot_work(desc, ST(s)); }
 
+int regcn_hyp_ce_lse_f32(const float* q, const float* cand, const float* bias, const float* scale,
+                         const float* margin, const int32_t* target, int32_t B, int32_t N, int32_t d, float c,
+                         int32_t flags, void* workspace, float* loss_per_query, float* lse, void* s) {
+  if (!workspace) return set_error(REGCN_EINVAL, "null workspace");
+  ScoreArgs a = score_args(q, cand, bias, nullptr, scale, margin, B, N, d, c, flags);
+  const size_t nblk = ((size_t)N + 63) / 64;
+  a.target = target;
+  a.part = (float*)workspace;
+  a.tgt_logit = a.part + (size_t)B * nblk * 2;
+  a.lse_out = lse;
+  return score(a, 1, loss_per_query, ST(s));
+}
+int regcn_hyp_ce_bwd_f32(const float* q, const float* cand, const float* bias, const float* scale,
+                         const float* margin, const int32_t* target, const float* lse, const float* grad_loss,
+                         int32_t B, int32_t N, int32_t d, float c, int32_t flags, float* coef, float* rsum,
+                         float* csum, void* s) {
+  ScoreArgs a = score_args(q, cand, bias, nullptr, scale, margin, B, N, d, c, flags);
+  a.target = target;
+  a.lse = lse;
+  a.gl = grad_loss;
+  a.coef = coef;
+  a.rsum = rsum;
+  a.csum = csum;
+  return score_ce_bwd(a, ST(s));
+}
+int regcn_rowmap_bwd_f32(int32_t op, const float* x, const float* y, const float* g, int64_t rows, int32_t d,
+                         float c, float* dx, float* dy, void* s) {
+  return rowmap_bwd(op, x, y, g, rows, d, c, dx, dy, ST(s));
+}
+int regcn_union_aggregate_bwd_f32(const regcn_edge_bwd_desc* desc, float gamma, void* s) {
+  if (!desc) return set_error(REGCN_EINVAL, "null descriptor");
+  return union_bwd(desc, gamma, ST(s));
+}
+int regcn_lorentz_sum_raw_f32(const float* x, const float* rel, const float* weight, const int32_t* rowptr,
+                              const int32_t* col_src, const int32_t* col_type, int32_t V, int32_t d, int32_t num_bases,
+                              float c, float* S0, float* Sv, void* s) {
+  return lorentz_raw(x, rel, weight, rowptr, col_src, col_type, V, d, num_bases, c, S0, Sv, ST(s));
+}
+int regcn_lorentz_aggregate_bwd_f32(const regcn_edge_bwd_desc* desc, int32_t num_bases, float c, void* s) {
+  if (!desc) return set_error(REGCN_EINVAL, "null descriptor");
+  return lorentz_bwd(desc, num_bases, c, ST(s));
+}
+size_t regcn_transpose_workspace_bytes(int32_t E, int32_t V, int32_t R2) { return transpose_ws_bytes(E, V, R2); }
+int regcn_snapshot_transpose_i32(const regcn_transpose_desc* desc, void* s) { return snapshot_transpose(desc, ST(s)); }
+
 }  // extern "C"

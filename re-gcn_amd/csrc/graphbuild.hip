@@ -806,6 +806,62 @@ int snapshot_work(const regcn_snapshot_desc* d, hipStream_t st) {
 
 size_t snapshot_ws_bytes(int64_t T, int V, int R) { return layout(T, V, R).total; }
 
+// ------------------------------------------------------------------- transposed edge lists
+namespace {
+__global__ __launch_bounds__(BT) void k_iota_keys(const int* __restrict__ keys, int n, uint32_t* __restrict__ k,
+                                                  uint32_t* __restrict__ v) {
+  const int i = blockIdx.x * BT + threadIdx.x;
+  if (i < n) {
+    k[i] = (uint32_t)keys[i];
+    v[i] = (uint32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(BT) void k_csr_dst(const int* __restrict__ rowptr, int V, int* __restrict__ csr_dst) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (BT / 64);
+  for (int v = blockIdx.x * (BT / 64) + (threadIdx.x >> 6); v < V; v += nw)
+    for (int p = rowptr[v] + lane; p < rowptr[v + 1]; p += 64) csr_dst[p] = v;
+}
+
+Layout tlayout(int E, int V, int R2) { return layout(((int64_t)E + 1) / 2, V, (R2 + 1) / 2); }
+}  // namespace
+
+size_t transpose_ws_bytes(int E, int V, int R2) { return tlayout(E, V, R2).total; }
+
+int snapshot_transpose(const regcn_transpose_desc* d, hipStream_t st) {
+  if (!d) return set_error(REGCN_EINVAL, "null transpose descriptor");
+  const int V = d->V, E = d->E, R2 = d->R2;
+  if (V <= 0 || E < 0 || R2 <= 0) return set_error(REGCN_EINVAL, "bad transpose sizes");
+  if (!d->rowptr || !d->csr_dst || !d->sptr || !d->tptr || (E > 0 && (!d->col_src || !d->col_type || !d->sp || !d->tp)))
+    return set_error(REGCN_EINVAL, "null pointer");
+  const Layout L = tlayout(E, V, R2);
+  if (!d->workspace || d->ws_bytes < L.total) return set_error(REGCN_EINVAL, "transpose workspace too small");
+  char* ws = (char*)d->workspace;
+  int rc;
+  hipLaunchKernelGGL(k_csr_dst, dim3(std::min<unsigned>(blocks(V, 4), 65536)), dim3(BT), 0, st, d->rowptr, V, d->csr_dst);
+  if ((rc = check_launch("k_csr_dst"))) return rc;
+  const int* keys[2] = {d->col_src, d->col_type};
+  int* ptr[2] = {d->sptr, d->tptr};
+  int* pos[2] = {d->sp, d->tp};
+  const int nkeys[2] = {V, R2};
+  for (int w = 0; w < 2; ++w) {
+    if (E == 0) {
+      hipLaunchKernelGGL(k_zero_ints, dim3(blocks(nkeys[w] + 1)), dim3(BT), 0, st, ptr[w], nkeys[w] + 1);
+      if ((rc = check_launch("k_zero_ints"))) return rc;
+      continue;
+    }
+    hipLaunchKernelGGL(k_iota_keys, dim3(blocks(E)), dim3(BT), 0, st, keys[w], E, (uint32_t*)(ws + L.k0),
+                       (uint32_t*)(ws + L.v0));
+    bool second;
+    if ((rc = radix_sort(ws, L, E, bitlen((uint64_t)nkeys[w] - 1), true, &second, st))) return rc;
+    hipLaunchKernelGGL(k_bounds, dim3(blocks(E)), dim3(BT), 0, st, (const uint32_t*)(ws + (second ? L.k1 : L.k0)), E,
+                       nullptr, 1u, nkeys[w], ptr[w]);
+    if ((rc = d2d(pos[w], ws + (second ? L.v1 : L.v0), (size_t)E * 4, st))) return rc;
+  }
+  return 0;
+}
+
 int64_t snapshot_capacity(int what, int64_t T, int V, int R, int C) {
   const int64_t E = 2 * T, EC = E / std::max(C, 1) + 1, R2 = 2 * (int64_t)R;
   switch (what) {

@@ -40,7 +40,17 @@ int lorentz_sum(const float* x, const float* rel, const float* W, const int* col
                 const void* chunks, int n_chunks, const void* fixups, int n_fix, int nb, float c, int d,
                 float* partial, int pstride, float* out, hipStream_t st);
 
+// backward.hip
+int rowmap_bwd(int op, const float* x, const float* y, const float* g, int64_t rows, int d, float c, float* dx,
+               float* dy, hipStream_t st);
+int union_bwd(const regcn_edge_bwd_desc* a, float gamma, hipStream_t st);
+int lorentz_raw(const float* x, const float* rel, const float* W, const int* rowptr, const int* col_src,
+                const int* col_type, int V, int d, int nb, float c, float* S0, float* Sv, hipStream_t st);
+int lorentz_bwd(const regcn_edge_bwd_desc* a, int nb, float c, hipStream_t st);
+
 // graphbuild.hip
+int snapshot_transpose(const regcn_transpose_desc* d, hipStream_t st);
+size_t transpose_ws_bytes(int E, int V, int R2);
 int snapshot_csr(const regcn_snapshot_desc* d, hipStream_t st);
 int snapshot_work(const regcn_snapshot_desc* d, hipStream_t st);
 size_t snapshot_ws_bytes(int64_t T, int V, int R);
@@ -120,6 +130,13 @@ struct ScoreArgs {
   float* part;           // [B, nblk, 2] (CE mode): running max, sum exp
   float* tgt_logit;      // [B] (CE mode)
   int64_t* trace;        // profiling stamps (g_trace at launch), or null
+  float* lse_out;        // [B] (CE mode, optional): log-sum-exp per query
+  // CE backward (MODE 2): G[b,n] = gl[b] (softmax - onehot), coefficients of dS/d(xy, x2, y2)
+  const float* lse;      // [B]
+  const float* gl;       // [B] upstream gradient of each query's loss
+  float* coef;           // [B, N]: G dS/dxy
+  float* rsum;           // [B, nblk]: per candidate block, sum_n G dS/dx2
+  float* csum;           // [ngroups16, N, 3]: per 16-query group, sum_b (G dS/dy2, G, G (margin - n^2))
 };
 
 // Relation GRU of one timestep (relgru.hip).
@@ -172,6 +189,7 @@ int pack_weight(const float* W, int d_in, int d_out, float* Wp, hipStream_t st);
 int layer(const LayerArgs& a, hipStream_t st);
 int timestep(const StepArgs& a, hipStream_t st);
 int score(ScoreArgs& a, int mode, float* loss, hipStream_t st);
+int score_ce_bwd(ScoreArgs& a, hipStream_t st);
 int rank(const float* S, int B, int N, const int* target, const int* filt_ptr, const int* filt_idx, int* rank_raw,
          int* rank_filt, hipStream_t st);
 

@@ -68,6 +68,28 @@ __device__ __forceinline__ T pair_score(T xy, T x2, T y2, T bias_n, T cr, const 
   return (T)p.scale * ((T)p.margin - dist) + bias_n;
 }
 
+// Gradient of the proxy score S = scale (margin - n^2) w.r.t. (xy, x2, y2): returns n^2,
+// writes dn2/dxy, dn2/dx2, dn2/dy2 (zero where |mobius| is clamped to mx: projected rows
+// pass no radial gradient, as torch's clamp in project_to_ball).
+__device__ __forceinline__ float pair_n2_grad(float xy, float x2, float y2, const ScoreArgs& p, float* gxy,
+                                              float* gx2, float* gy2) {
+  const float c = p.c;
+  const float A = 1.f - 2.f * c * xy + c * y2;
+  const float Bq = 1.f - c * x2;
+  const float num2 = fmaxf(A * A * x2 - 2.f * A * Bq * xy + Bq * Bq * y2, 0.f);
+  const float den = 1.f - 2.f * c * xy + c * c * x2 * y2 + REGCN_EPS;
+  const float nr = sqrtf(num2) / den;
+  if (nr > p.mx) {
+    *gxy = *gx2 = *gy2 = 0.f;
+    return p.mx * p.mx;
+  }
+  const float i2 = 1.f / (den * den), t = 2.f * num2 * i2 / den;
+  *gxy = (-4.f * c * A * x2 + 4.f * c * Bq * xy - 2.f * A * Bq) * i2 + t * (2.f * c);
+  *gx2 = (A * A + 2.f * c * A * xy - 2.f * c * Bq * y2) * i2 - t * (c * c * y2);
+  *gy2 = (2.f * c * A * x2 - 2.f * c * Bq * xy + Bq * Bq) * i2 - t * (c * c * x2);
+  return num2 * i2;
+}
+
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 template <bool F64>
@@ -107,6 +129,44 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& p, const V* acc,
         if (ni[j] < p.N)
           p.out[(int64_t)qi[r] * p.N + ni[j]] = (float)pair_score<T>(acc[j][r], x2[r], y2[j], bn_[j], cr[r], p);
     }
+  } else if (MODE == 2) {  // CE backward coefficients (proxy score, fp32)
+    const int nblk = (p.N + SN - 1) / SN;
+    float cs[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cs[j][0] = cs[j][1] = cs[j][2] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool qok = qi[r] < p.B;
+      const int t = qok ? p.target[qi[r]] : -1;
+      const float lse = qok ? p.lse[qi[r]] : 0.f, gl = qok ? p.gl[qi[r]] : 0.f;
+      float rs = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!qok || ni[j] >= p.N) continue;
+        float gxy, gx2, gy2;
+        const float n2 = pair_n2_grad((float)acc[j][r], (float)x2[r], (float)y2[j], p, &gxy, &gx2, &gy2);
+        const float S = p.scale * (p.margin - n2) + (float)bn_[j];
+        const float G = gl * (expf(S - lse) - (ni[j] == t ? 1.f : 0.f));
+        const float Gs = -p.scale * G;
+        p.coef[(int64_t)qi[r] * p.N + ni[j]] = Gs * gxy;
+        rs += Gs * gx2;
+        cs[j][0] += Gs * gy2;
+        cs[j][1] += G;
+        cs[j][2] += G * (p.margin - n2);
+      }
+      rs = group16_sum(rs);
+      if ((lane & 15) == 0 && qok) p.rsum[(int64_t)qi[r] * nblk + bn] = rs;
+    }
+    const int grp = (qi[0] - 4 * (lane >> 4)) >> 4;  // this wave's 16-query group
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        float v = cs[j][k];
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (lane < 16 && ni[j] < p.N) p.csum[((int64_t)grp * p.N + ni[j]) * 3 + k] = v;
+      }
   } else {
     const int nblk = (p.N + SN - 1) / SN;
 #pragma unroll
@@ -376,7 +436,8 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(4))) v
 
 // Combine per-tile (max, sumexp) into per-query loss = lse - target logit (one wave per query).
 __global__ __launch_bounds__(256) void k_ce_combine(const float* __restrict__ part, const float* __restrict__ tgt,
-                                                    int B, int nblk, float* __restrict__ loss) {
+                                                    int B, int nblk, float* __restrict__ loss,
+                                                    float* __restrict__ lse_out) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
@@ -387,7 +448,11 @@ __global__ __launch_bounds__(256) void k_ce_combine(const float* __restrict__ pa
   float s = 0.f;
   for (int i = lane; i < nblk; i += 64) s += pb[2 * i + 1] * expf(pb[2 * i] - m);
   s = wave_sum(s);
-  if (lane == 0) loss[b] = (m + logf(s)) - tgt[b];
+  if (lane == 0) {
+    const float lse = m + logf(s);
+    loss[b] = lse - tgt[b];
+    if (lse_out) lse_out[b] = lse;
+  }
 }
 
 // Rank of the target under a descending sort, as 1 + #{n : S[b,n] > S[b,t]} (raw)
@@ -452,8 +517,24 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   else hipLaunchKernelGGL((k_score<1, false>), g, b, 0, st, a);
   int rc = check_launch("k_score_ce");
   if (rc) return rc;
-  hipLaunchKernelGGL(k_ce_combine, dim3((a.B + 3) / 4), b, 0, st, a.part, a.tgt_logit, a.B, nbn, loss);
+  hipLaunchKernelGGL(k_ce_combine, dim3((a.B + 3) / 4), b, 0, st, a.part, a.tgt_logit, a.B, nbn, loss, a.lse_out);
   return check_launch("k_ce_combine");
+}
+
+// CE backward coefficients (the B x N GEMM operand and the row / column partial sums; the
+// caller finishes dq = coef E + 2 q rowsum, de = coef^T Q + 2 e colsum on the GEMM library).
+int score_ce_bwd(ScoreArgs& a, hipStream_t st) {
+  if (a.d <= 0 || (a.d & 3) || a.d > 16 * KB_MAX) return set_error(REGCN_ENOTSUP, "CE backward needs d %% 4 == 0, d <= 256");
+  if (a.use_dist) return set_error(REGCN_ENOTSUP, "CE backward of the arctanh-distance score is not built");
+  if (!a.q || !a.e || !a.target || !a.lse || !a.gl || !a.coef || !a.rsum || !a.csum)
+    return set_error(REGCN_EINVAL, "null pointer");
+  if (a.B == 0 || a.N == 0) return 0;
+  a.trace = nullptr;
+  const int nbn = (a.N + SN - 1) / SN;
+  const dim3 g2((unsigned)(((long)(a.B + SQ2 - 1) / SQ2) * nbn)), b2(64 * SW2);
+  const size_t lds2 = (size_t)SN * score_lds_stride(a.d) * 4;
+  hipLaunchKernelGGL((k_score_f32<2>), g2, b2, lds2, st, a);
+  return check_launch("k_score_ce_bwd");
 }
 
 int rank(const float* S, int B, int N, const int* target, const int* filt_ptr, const int* filt_idx, int* rank_raw,

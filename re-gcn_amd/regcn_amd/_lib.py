@@ -60,11 +60,20 @@ _SIGS = {
     "regcn_snapshot_capacity": [_c_int, _c_i64, _c_int, _c_int, _c_int],
     "regcn_snapshot_csr_i32": [P, P],
     "regcn_snapshot_work_i32": [P, P],
+    "regcn_transpose_workspace_bytes": [_c_int, _c_int, _c_int],
+    "regcn_snapshot_transpose_i32": [P, P],
+    "regcn_rowmap_bwd_f32": [_c_int, P, P, P, _c_i64, _c_int, _c_f, P, P, P],
+    "regcn_union_aggregate_bwd_f32": [P, _c_f, P],
+    "regcn_lorentz_sum_raw_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, P, P, P],
+    "regcn_lorentz_aggregate_bwd_f32": [P, _c_int, _c_f, P],
+    "regcn_hyp_ce_lse_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P, P, P],
+    "regcn_hyp_ce_bwd_f32": [P, P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P, P, P],
 }
 
 SCORE_DIST, SCORE_RAW_SCALE = 1, 2
 _RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz,
             "regcn_snapshot_workspace_bytes": _c_sz, "regcn_snapshot_capacity": _c_i64,
+            "regcn_transpose_workspace_bytes": _c_sz,
             "regcn_packed_weight_floats": _c_sz, "regcn_packed_linear_floats": _c_sz}
 
 _lib = None
@@ -103,6 +112,18 @@ class SnapshotDesc(ctypes.Structure):
         ("rows", P), ("tiles", P), ("item_ptr", P), ("item_src", P), ("item_tl", P), ("chunks", P), ("fixups", P),
         ("heavy_chunks", P), ("heavy_fixups", P), ("rel_chunks", P), ("rel_fixups", P),
     ]
+
+
+class TransposeDesc(ctypes.Structure):
+    _fields_ = [("V", _c_int), ("E", _c_int), ("R2", _c_int), ("rowptr", P), ("col_src", P), ("col_type", P),
+                ("workspace", P), ("ws_bytes", _c_sz), ("csr_dst", P), ("sptr", P), ("sp", P), ("tptr", P), ("tp", P)]
+
+
+class EdgeBwdDesc(ctypes.Structure):
+    _fields_ = [("V", _c_int), ("E", _c_int), ("R2", _c_int), ("d", _c_int), ("x", P), ("radius", P), ("rel", P),
+                ("W", P), ("norm", P), ("rowptr", P), ("col_src", P), ("col_type", P), ("csr_dst", P), ("sptr", P),
+                ("sp", P), ("tptr", P), ("tp", P), ("G", P), ("G0", P), ("dx", P), ("drel", P), ("dradius", P),
+                ("dW", P), ("edge_scratch", P)]
 
 
 def call_desc(name, desc):

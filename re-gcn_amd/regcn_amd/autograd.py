@@ -1,0 +1,305 @@
+"""Autograd functions of the training path.
+
+Each function runs its forward AND its backward as hand-written gfx950 kernels
+(csrc/rowwise.hip, aggregate.hip, score.hip forward; csrc/backward.hip, score.hip backward),
+with the gradients torch autograd would compute through the reference's op sequence:
+
+  * row maps of hyperbolic_src/hyperbolic_ops.py (log0, exp0, project, apply_radius,
+    get_radius, mobius_add) -> regcn_rowmap_bwd_f32;
+  * the union layer's message sum (hyperbolic_layers.py:222-240, :290) ->
+    regcn_union_aggregate_bwd_f32 over the snapshot's transposed edge lists;
+  * the Lorentz layer's message sums (hyperbolic_layers.py:589-611) -> regcn_lorentz_sum_raw_f32
+    / regcn_lorentz_aggregate_bwd_f32 (the centroid, to_poincare, log0 follow as row ops);
+  * the all-entity cross entropy (_chunked_hyperbolic_ce_loss, hyperbolic_decoder.py:182-307)
+    -> regcn_hyp_ce_lse_f32 / regcn_hyp_ce_bwd_f32 (+ two library GEMMs for dq, de).
+
+The curvature is a constant here (a learned curvature's gradient is not built).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+EPS = 1e-6
+BWD = dict(log0=0, exp0=1, project=2, apply_radius=3, radius=4, mobius=5)
+FWD = dict(log0="regcn_log0_f32", exp0="regcn_exp0_f32", project="regcn_project_f32")
+
+
+def needs_grad(*ts):
+    return torch.is_grad_enabled() and any(torch.is_tensor(t) and t.requires_grad for t in ts)
+
+
+def _cf(c):
+    if torch.is_tensor(c):
+        if c.requires_grad:
+            raise NotImplementedError("the gradient of a learned curvature is not built (SURVEY.md §8(f) f1)")
+        return float(c.item())
+    return float(c)
+
+
+def _rows(x):
+    return x.reshape(-1, x.shape[-1]).contiguous().float()
+
+
+def _bwd(op, x, y, g, c, dx, dy):
+    f = _lib.fptr
+    _lib.call("regcn_rowmap_bwd_f32", BWD[op], f(x, "x"), f(y), f(g.contiguous(), "grad"), x.shape[0], x.shape[-1],
+              float(c), f(dx), f(dy), _lib.stream())
+
+
+class _Radial(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, op, c):
+        xr = _rows(x)
+        out = torch.empty_like(xr)
+        _lib.call(FWD[op], _lib.fptr(xr, "x"), xr.shape[0], xr.shape[1], float(c), _lib.fptr(out), _lib.stream())
+        ctx.save_for_backward(xr)
+        ctx.op, ctx.c, ctx.shape = op, c, x.shape
+        return out.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        (xr,) = ctx.saved_tensors
+        dx = torch.empty_like(xr)
+        _bwd(ctx.op, xr, None, _rows(g), ctx.c, dx, None)
+        return dx.view(ctx.shape), None, None
+
+
+class _ApplyRadius(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, radius, c):
+        xr = _rows(x)
+        rr = radius.reshape(-1).contiguous().float()
+        out = torch.empty_like(xr)
+        _lib.call("regcn_apply_radius_f32", _lib.fptr(xr, "x"), _lib.fptr(rr, "radius"), xr.shape[0], xr.shape[1],
+                  float(c), _lib.fptr(out), _lib.stream())
+        ctx.save_for_backward(xr, rr)
+        ctx.c, ctx.shape, ctx.rshape = c, x.shape, radius.shape
+        return out.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        xr, rr = ctx.saved_tensors
+        dx = torch.empty_like(xr)
+        dr = torch.empty_like(rr)
+        _bwd("apply_radius", xr, rr, _rows(g), ctx.c, dx, dr)
+        return dx.view(ctx.shape), dr.view(ctx.rshape), None
+
+
+class _Radius(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        xr = _rows(x)
+        out = torch.empty(xr.shape[0], device=x.device, dtype=torch.float32)
+        _lib.call("regcn_radius_f32", _lib.fptr(xr, "x"), xr.shape[0], xr.shape[1], _lib.fptr(out), _lib.stream())
+        ctx.save_for_backward(xr)
+        ctx.shape = x.shape
+        return out.view(x.shape[:-1])
+
+    @staticmethod
+    def backward(ctx, g):
+        (xr,) = ctx.saved_tensors
+        dx = torch.empty_like(xr)
+        _bwd("radius", xr, None, g.reshape(-1).contiguous().float(), 0.01, dx, None)
+        return dx.view(ctx.shape)
+
+
+class _Mobius(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, y, c):
+        xr, yr = _rows(x), _rows(y)
+        out = torch.empty_like(xr)
+        _lib.call("regcn_mobius_add_f32", _lib.fptr(xr, "x"), _lib.fptr(yr, "y"), xr.shape[0], xr.shape[1], float(c),
+                  _lib.fptr(out), _lib.stream())
+        ctx.save_for_backward(xr, yr)
+        ctx.c, ctx.shape = c, x.shape
+        return out.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, g):
+        xr, yr = ctx.saved_tensors
+        dx, dy = torch.empty_like(xr), torch.empty_like(yr)
+        _bwd("mobius", xr, yr, _rows(g), ctx.c, dx, dy)
+        return dx.view(ctx.shape), dy.view(ctx.shape), None
+
+
+def log0(x, c):
+    return _Radial.apply(x, "log0", _cf(c))
+
+
+def exp0(x, c):
+    return _Radial.apply(x, "exp0", _cf(c))
+
+
+def project(x, c):
+    return _Radial.apply(x, "project", _cf(c))
+
+
+def apply_radius(x, radius, c):
+    return _ApplyRadius.apply(x, radius, _cf(c))
+
+
+def get_radius(x):
+    return _Radius.apply(x)
+
+
+def mobius_add(x, y, c):
+    return _Mobius.apply(x, y.expand_as(x), _cf(c))
+
+
+# ------------------------------------------------------------------------ edge aggregation
+def _edge_desc(g, V, d, R2):
+    wk = g.work()
+    tr = g.transposed()
+    a = _lib.EdgeBwdDesc()
+    a.V, a.E, a.R2, a.d = V, int(wk["col_src"].shape[0]), R2, d
+    for k in ("rowptr", "col_src", "col_type"):
+        setattr(a, k, _lib.dptr(wk[k], torch.int32, k))
+    for k in ("csr_dst", "sptr", "sp", "tptr", "tp"):
+        setattr(a, k, _lib.dptr(tr[k], torch.int32, k))
+    return a
+
+
+class _UnionAggregate(torch.autograd.Function):
+    """agg[v] = norm[v] sum_e w_e (x[src] + rel[type]), w_e = exp(-gamma |r_src - r_v|);
+    rows without in-edges are 0 (DGL fn.sum zero fill)."""
+
+    @staticmethod
+    def forward(ctx, x, radius, rel, g, gamma):
+        V, d = x.shape
+        wk = g.work()
+        x, radius, rel = x.contiguous(), radius.contiguous(), rel.contiguous()
+        agg = torch.zeros_like(x)
+        part = torch.empty(max(g.n_slots, 1), d, device=x.device, dtype=torch.float32)
+        f, i = _lib.fptr, _lib.iptr
+        _lib.call("regcn_union_aggregate_f32", f(x, "x"), f(radius, "radius"), f(rel, "rel"), i(wk["col_src"]),
+                  i(wk["col_type"]), f(wk["norm"]), i(wk["chunks"]), wk["chunks"].shape[0], i(wk["fixups"]),
+                  wk["fixups"].shape[0], float(gamma), d, f(part), d, f(agg), _lib.stream())
+        ctx.save_for_backward(x, radius, rel)
+        ctx.g, ctx.gamma = g, float(gamma)
+        return agg
+
+    @staticmethod
+    def backward(ctx, G):
+        x, radius, rel = ctx.saved_tensors
+        V, d = x.shape
+        R2 = rel.shape[0]
+        a = _edge_desc(ctx.g, V, d, R2)
+        E = a.E
+        dx, drel = torch.empty_like(x), torch.empty_like(rel)
+        dr = torch.empty_like(radius)
+        scratch = torch.empty(2 * E + V, device=x.device, dtype=torch.float32)
+        G = G.contiguous()
+        a.x, a.radius, a.rel, a.norm, a.G = (_lib.fptr(t) for t in (x, radius, rel, ctx.g.work()["norm"], G))
+        a.dx, a.drel, a.dradius, a.edge_scratch = (_lib.fptr(t) for t in (dx, drel, dr, scratch))
+        _lib.check(_lib.lib().regcn_union_aggregate_bwd_f32(ctypes.byref(a), ctx.gamma, _lib.stream()),
+                   "regcn_union_aggregate_bwd_f32")
+        return dx, dr, drel, None, None
+
+
+def union_aggregate(x, radius, rel, g, gamma):
+    return _UnionAggregate.apply(x, radius, rel, g, gamma)
+
+
+class _LorentzSum(torch.autograd.Function):
+    """(S0[v], Sv[v]) = sum over v's in-edges of to_lorentz(exp0(blockdiag(W_t) x_src + rel_t))."""
+
+    @staticmethod
+    def forward(ctx, x, rel, W, g, nb, c):
+        V, d = x.shape
+        wk = g.work()
+        x, rel, W = x.contiguous(), rel.contiguous(), W.contiguous()
+        S0 = torch.empty(V, device=x.device, dtype=torch.float32)
+        Sv = torch.empty_like(x)
+        f, i = _lib.fptr, _lib.iptr
+        _lib.call("regcn_lorentz_sum_raw_f32", f(x, "x"), f(rel, "rel"), f(W, "weight"), i(wk["rowptr"]),
+                  i(wk["col_src"]), i(wk["col_type"]), V, d, int(nb), float(c), f(S0), f(Sv), _lib.stream())
+        ctx.save_for_backward(x, rel, W)
+        ctx.g, ctx.nb, ctx.c = g, int(nb), float(c)
+        return S0, Sv
+
+    @staticmethod
+    def backward(ctx, g0, gv):
+        x, rel, W = ctx.saved_tensors
+        V, d = x.shape
+        a = _edge_desc(ctx.g, V, d, rel.shape[0])
+        g0 = torch.zeros(V, device=x.device) if g0 is None else g0.contiguous()
+        gv = torch.zeros_like(x) if gv is None else gv.contiguous()
+        dx, drel, dW = torch.empty_like(x), torch.empty_like(rel), torch.empty_like(W)
+        a.x, a.rel, a.W, a.G, a.G0 = (_lib.fptr(t) for t in (x, rel, W, gv, g0))
+        a.dx, a.drel, a.dW = (_lib.fptr(t) for t in (dx, drel, dW))
+        _lib.check(_lib.lib().regcn_lorentz_aggregate_bwd_f32(ctypes.byref(a), ctx.nb, ctx.c, _lib.stream()),
+                   "regcn_lorentz_aggregate_bwd_f32")
+        return dx, drel, dW, None, None, None
+
+
+def lorentz_sum(x, rel, W, g, nb, c):
+    return _LorentzSum.apply(x, rel, W, g, nb, _cf(c))
+
+
+def lorentz_aggregate(x, rel, W, g, nb, c):
+    """LorentzRGCNLayer reduce + to_poincare + log0 (hyperbolic_layers.py:613-625, :669-670):
+    the uniformly weighted Lorentz centroid is the normalised sum (scale-invariant: the
+    reference's 1/deg weights cancel), rows without in-edges give 0."""
+    cf = _cf(c)
+    S0, Sv = lorentz_sum(x, rel, W, g, nb, cf)
+    ip = -S0 * S0 + (Sv * Sv).sum(-1)
+    sc = torch.sqrt(torch.clamp(-ip * cf, min=EPS))
+    c0 = S0 / sc
+    y = (Sv / sc.unsqueeze(-1)) / torch.clamp(1.0 + c0 * cf ** 0.5, min=EPS).unsqueeze(-1)
+    return log0(y, cf)
+
+
+# ------------------------------------------------------------------------- cross entropy
+class _HypCE(torch.autograd.Function):
+    """Per-query CE loss of the proxy score S = scale (margin - |(-q) (+) e|^2) + bias."""
+
+    @staticmethod
+    def forward(ctx, q, cand, bias, scale, margin, target, c):
+        B, d = q.shape
+        N = cand.shape[0]
+        q, cand = q.contiguous().float(), cand.contiguous().float()
+        b = bias.contiguous().float() if bias is not None else None
+        sc = scale.detach().reshape(1).float().contiguous()
+        mg = margin.detach().reshape(1).float().contiguous()
+        tgt = target.to(device=q.device, dtype=torch.int32).contiguous()
+        ws = torch.empty((_lib.lib().regcn_hyp_ce_workspace_bytes(B, N) + 3) // 4, device=q.device)
+        loss = torch.empty(B, device=q.device, dtype=torch.float32)
+        lse = torch.empty(B, device=q.device, dtype=torch.float32)
+        f = _lib.fptr
+        _lib.call("regcn_hyp_ce_lse_f32", f(q, "query"), f(cand, "candidates"), f(b), f(sc), f(mg),
+                  _lib.iptr(tgt, "target"), B, N, d, float(c), 0, f(ws), f(loss), f(lse), _lib.stream())
+        ctx.save_for_backward(q, cand, b if b is not None else q.new_empty(0), sc, mg, tgt, lse)
+        ctx.has_bias, ctx.c = b is not None, float(c)
+        ctx.scale_shape, ctx.margin_shape = scale.shape, margin.shape
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        q, cand, b, sc, mg, tgt, lse = ctx.saved_tensors
+        B, d = q.shape
+        N = cand.shape[0]
+        nblk, ng = (N + 63) // 64, 8 * ((B + 127) // 128)
+        coef = torch.empty(B, N, device=q.device, dtype=torch.float32)
+        rsum = torch.empty(B, nblk, device=q.device, dtype=torch.float32)
+        csum = torch.zeros(ng, N, 3, device=q.device, dtype=torch.float32)
+        gl = gl.contiguous().float()
+        f = _lib.fptr
+        _lib.call("regcn_hyp_ce_bwd_f32", f(q), f(cand), f(b) if ctx.has_bias else None, f(sc), f(mg),
+                  _lib.iptr(tgt), f(lse), f(gl), B, N, d, ctx.c, 0, f(coef), f(rsum), f(csum), _lib.stream())
+        rs = rsum.sum(1, keepdim=True)
+        cs = csum.sum(0)
+        dq = torch.addmm(2.0 * rs * q, coef, cand)            # coef E + 2 q sum_n G dS/d|q|^2
+        de = torch.addmm(2.0 * cs[:, :1] * cand, coef.t(), q)  # coef^T Q + 2 e sum_b G dS/d|e|^2
+        dbias = cs[:, 1].clone() if ctx.has_bias else None
+        dscale = cs[:, 2].sum().reshape(ctx.scale_shape)
+        dmargin = (sc.reshape(()) * cs[:, 1].sum()).reshape(ctx.margin_shape)
+        return dq, de, dbias, dscale, dmargin, None, None
+
+
+def hyp_ce_loss(q, cand, target, c, bias=None, scale=None, margin=None):
+    """mean over queries of the CE loss (hyperbolic_decoder.py:182-307, proxy score)."""
+    scale = scale if torch.is_tensor(scale) else q.new_tensor(1.0 if scale is None else float(scale))
+    margin = margin if torch.is_tensor(margin) else q.new_tensor(0.0 if margin is None else float(margin))
+    return _HypCE.apply(q, cand, bias, scale, margin, target, _cf(c)).mean()

@@ -227,6 +227,36 @@ class SnapshotGraph:
         """Host copies of the kernel work lists (int32 / fp32 numpy)."""
         return self._host_lists
 
+    def transposed(self):
+        """Edge lists of the backward passes (regcn_snapshot_transpose_i32), built on first use
+        and cached: csr_dst (destination of each CSR position), CSR positions sorted by
+        source (sptr, sp) and by relation type (tptr, tp)."""
+        t = self.__dict__.get("_transposed")
+        if t is not None:
+            return t
+        import ctypes
+        from . import _lib
+        wk = self.work()
+        dev = wk["rowptr"].device
+        V, E, R2 = self.num_nodes_, int(wk["col_src"].shape[0]), 2 * self.num_rels
+        ws = torch.empty(int(_lib.lib().regcn_transpose_workspace_bytes(E, V, R2)), dtype=torch.uint8, device=dev)
+        t = {"csr_dst": torch.empty(max(E, 1), dtype=torch.int32, device=dev),
+             "sptr": torch.empty(V + 1, dtype=torch.int32, device=dev),
+             "sp": torch.empty(max(E, 1), dtype=torch.int32, device=dev),
+             "tptr": torch.empty(R2 + 1, dtype=torch.int32, device=dev),
+             "tp": torch.empty(max(E, 1), dtype=torch.int32, device=dev)}
+        a = _lib.TransposeDesc()
+        a.V, a.E, a.R2 = V, E, R2
+        a.rowptr = ctypes.c_void_p(wk["rowptr"].data_ptr())
+        a.col_src = ctypes.c_void_p(wk["col_src"].data_ptr()) if E else None
+        a.col_type = ctypes.c_void_p(wk["col_type"].data_ptr()) if E else None
+        a.workspace, a.ws_bytes = ctypes.c_void_p(ws.data_ptr()), ws.numel()
+        for k, v in t.items():
+            setattr(a, k, ctypes.c_void_p(v.data_ptr()))
+        _lib.call_desc("regcn_snapshot_transpose_i32", a)
+        self.__dict__["_transposed"] = t
+        return t
+
     def work(self):
         """Device work lists (raises on a CPU graph: the HIP path has no CPU fallback)."""
         if self.dev is None:
