@@ -373,3 +373,25 @@ def answers_for_filter(snap, num_rels, rel_p=False):
             ans.setdefault(o, {}).setdefault(r + num_rels, set()).add(s)
             ans.setdefault(s, {}).setdefault(r, set()).add(o)
     return ans
+
+
+def hyperbolic_get_loss(sd, cfg, glist, triples, radius_target):
+    """HyperbolicRecurrentRGCN.get_loss, hyperbolic_model.py:941-1088 (dropout off, no static
+    graph): entity and relation cross entropy over the triples and their inverses, the
+    radius MSE on the entities in the batch.  Returns (loss_ent, loss_rel, loss_static,
+    loss_radius)."""
+    R = sd["emb_rel"].shape[0] // 2
+    inv = triples[:, [2, 1, 0]].clone()
+    inv[:, 1] += R
+    all_tr = torch.cat([triples, inv])                                     # :982-985
+    embs, h0 = hyperbolic_forward(sd, cfg, glist)
+    emb = embs[-1]
+    c = cfg["c"]
+    if cfg["layer_norm"]:
+        emb = ops.exp0(F.normalize(ops.log0(emb, c)), c)                   # :991-995
+    le = F.cross_entropy(entity_decoder(cfg["decoder"], sd, emb, h0, all_tr, c), all_tr[:, 2].long())
+    lr = F.cross_entropy(relation_decoder(cfg["decoder"], sd, emb, h0, all_tr, c), all_tr[:, 1].long())
+    ids = torch.unique(all_tr[:, [0, 2]].reshape(-1))
+    lrad = cfg.get("radius_lambda", 0.02) * F.mse_loss(static_radius(sd, cfg)[ids],
+                                                       torch.as_tensor(radius_target)[ids].to(emb.dtype))
+    return le, lr, torch.zeros(1, dtype=emb.dtype), lrad

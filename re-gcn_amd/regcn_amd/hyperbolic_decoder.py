@@ -16,6 +16,7 @@ import torch.nn.functional as F
 from torch.nn.parameter import Parameter
 
 from . import _lib
+from . import autograd as _ag
 from .hyperbolic_ops import HyperbolicOps
 from .weights import packed_t
 
@@ -90,6 +91,12 @@ def _chunked_hyperbolic_ce_loss(query, candidates, target, c, c_chunk_size, cand
     B x N logits are never materialised).  query_bias cancels in CE and is ignored (:204-205)."""
     B, d = query.shape
     N = candidates.shape[0]
+    if _ag.needs_grad(query, candidates, candidate_bias, score_scale, score_margin):
+        if use_hyperbolic_distance or query_curvature is not None:
+            raise NotImplementedError("training with the arctanh-distance score (--plus-relation-specific-curvature) "
+                                      "is not built: its backward kernel is missing")
+        return _ag.hyp_ce_loss(query, candidates, target, c, bias=candidate_bias, scale=score_scale,
+                               margin=score_margin)
     q, e, b, cr, sc, mg = _score_operands(query, candidates, candidate_bias, score_scale, score_margin,
                                                     query_curvature if use_hyperbolic_distance else None)
     tgt = target.to(device=q.device, dtype=torch.int32).contiguous()
@@ -101,6 +108,12 @@ def _chunked_hyperbolic_ce_loss(query, candidates, target, c, c_chunk_size, cand
               _lib.iptr(tgt, "target"), B, N, d, _cf(c), int(bool(use_hyperbolic_distance)), f(ws), f(loss),
               _lib.stream())
     return loss.mean()
+
+
+def _grad_path(mod, *ts):
+    """True when autograd must see the decoder (training): the fused eval-only query kernels
+    are skipped for the differentiable op sequence."""
+    return _ag.needs_grad(*ts) or (torch.is_grad_enabled() and any(p.requires_grad for p in mod.parameters()))
 
 
 def givens_rotation(x, angles):
@@ -245,7 +258,8 @@ class HyperbolicRotH(_EntityDecoderBase):
     def _query(self, ent, rel, trip):
         """hyperbolic_decoder.py:1065-1085.  In eval mode (dropout = identity) one HIP launch
         (regcn_roth_query_f32); with active dropout the same op sequence on torch."""
-        if not (self.training and self.dropout.p > 0) and not getattr(self, "_torch_query", False):
+        if not (self.training and self.dropout.p > 0) and not getattr(self, "_torch_query", False) \
+                and not _grad_path(self, ent, rel):
             d = ent.shape[1]
             q = torch.empty(trip.shape[0], d, device=ent.device, dtype=torch.float32)
             f = _lib.fptr
@@ -381,7 +395,7 @@ class HyperbolicRotHRel(_RelDecoderBase):
     def forward(self, entity_embedding, rel_embedding, triplets, mode="train"):
         """Eval mode: queries and the exp0 candidates in one launch (regcn_roth_rel_query_f32),
         then the scorer with softplus(score_scale_raw) applied on the device."""
-        if self.training and self.dropout.p > 0:
+        if (self.training and self.dropout.p > 0) or _grad_path(self, entity_embedding, rel_embedding):
             return super().forward(entity_embedding, rel_embedding, triplets, mode)
         B, d = triplets.shape[0], entity_embedding.shape[1]
         R2 = rel_embedding.shape[0]

@@ -254,16 +254,18 @@ class HyperbolicRecurrentRGCN(nn.Module):
             self._r_static_cache = (key, radius.detach().contiguous())
         return radius
 
-    def _guard_autograd(self):
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError(
-                "the HIP path is forward-only in this build (backward kernels are SURVEY.md §8(f) row f1); "
-                "wrap the call in torch.no_grad()")
+    def _wants_grad(self):
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
     # ---------------------------------------------------------------------------- forward
     def forward(self, g_list, static_graph, use_cuda):
-        """hyperbolic_model.py:722-890."""
-        self._guard_autograd()
+        """hyperbolic_model.py:722-890.  With autograd on (training) the differentiable
+        composition of training.py runs; otherwise the fused inference kernels."""
+        if self._wants_grad():
+            from .training import model_forward
+            out = model_forward(self, g_list)
+            self.h, self.h_0 = out[0][-1], out[2]
+            return out
         c_val = self._c_float()
         dev = self.dynamic_emb.device
         V, d = self.dynamic_emb.shape

@@ -12,6 +12,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from . import autograd as _ag
 
 EPS = 1e-6
 
@@ -45,24 +46,32 @@ class HyperbolicOps:
     def project_to_ball(x, c=0.01, eps=1e-6):
         """hyperbolic_ops.py:55-74."""
         _check_eps(eps)
+        if _ag.needs_grad(x):
+            return _ag.project(x, c)
         return _rowmap("regcn_project_f32", x, c).view(x.shape)
 
     @staticmethod
     def exp_map_zero(v, c=0.01, eps=1e-6):
         """hyperbolic_ops.py:76-95."""
         _check_eps(eps)
+        if _ag.needs_grad(v):
+            return _ag.exp0(v, c)
         return _rowmap("regcn_exp0_f32", v, c).view(v.shape)
 
     @staticmethod
     def log_map_zero(x, c=0.01, eps=1e-6):
         """hyperbolic_ops.py:97-116."""
         _check_eps(eps)
+        if _ag.needs_grad(x):
+            return _ag.log0(x, c)
         return _rowmap("regcn_log0_f32", x, c).view(x.shape)
 
     @staticmethod
     def mobius_add(x, y, c=0.01, eps=1e-6):
         """hyperbolic_ops.py:118-143."""
         _check_eps(eps)
+        if _ag.needs_grad(x, y):
+            return _ag.mobius_add(x, y, c)
         x2, d = _rows(x)
         y2, _ = _rows(y.expand_as(x))
         out = torch.empty_like(x2)
@@ -74,6 +83,8 @@ class HyperbolicOps:
     def get_radius(x, eps=1e-6):
         """hyperbolic_ops.py:193-206."""
         _check_eps(eps)
+        if _ag.needs_grad(x):
+            return _ag.get_radius(x)
         x2, d = _rows(x)
         out = torch.empty(x2.shape[0], device=x.device, dtype=torch.float32)
         _lib.call("regcn_radius_f32", _lib.fptr(x2, "x"), x2.shape[0], d, _lib.fptr(out), _lib.stream())
@@ -85,6 +96,10 @@ class HyperbolicOps:
         if radius is None:
             return x
         _check_eps(eps)
+        if _ag.needs_grad(x, radius):
+            r = radius.reshape(-1)
+            n = x.reshape(-1, x.shape[-1]).shape[0]
+            return _ag.apply_radius(x, r.expand(n) if r.numel() == 1 else r, c)
         x2, d = _rows(x)
         r = radius.reshape(-1).expand(x2.shape[0]).contiguous().float() if radius.numel() in (1, x2.shape[0]) \
             else radius.reshape(-1).contiguous()
@@ -109,6 +124,8 @@ class HyperbolicOps:
     @staticmethod
     def layer_norm_roundtrip(x, c=0.01):
         """exp0(normalize(log0(x))) in one pass (hyperbolic_model.py:832-835, :926-929)."""
+        if _ag.needs_grad(x):
+            return _ag.exp0(torch.nn.functional.normalize(_ag.log0(x, c)), c)
         return _rowmap("regcn_ln_roundtrip_f32", x, c).view(x.shape)
 
     @staticmethod

@@ -1,0 +1,131 @@
+"""Differentiable forward of the recurrent encoder (training path).
+
+The inference forward fuses a whole layer (gather + GEMMs + epilogue [+ timestep]) into one
+launch and keeps no intermediates.  Training needs them, so this path composes the
+autograd functions of autograd.py -- HIP kernels forward and backward for the row maps,
+the union / Lorentz message aggregation and (in the decoders) the all-entity cross
+entropy -- with library GEMMs (rocBLAS via torch.mm) and the elementwise glue (clamp,
+rrelu, sigmoid gates, dropout) as device torch ops.  The op sequence is the reference's:
+
+  HyperbolicUnionRGCNLayer.forward   hyperbolic_layers.py:242-323
+  LorentzRGCNLayer.forward           hyperbolic_layers.py:627-694
+  HyperbolicRecurrentRGCN.forward    hyperbolic_model.py:722-890
+"""
+import torch
+import torch.nn.functional as F
+
+from . import autograd as A
+
+RRELU_SLOPE = (1.0 / 8 + 1.0 / 3) / 2  # F.rrelu(x) with training=False (hyperbolic_model.py:120)
+
+
+def _self_loop(x, g, w_loop, w_evolve):
+    """W_loop for rows with in-edges, W_evolve otherwise (hyperbolic_layers.py:273-280)."""
+    pos = (g.in_degrees() > 0).to(x.device).unsqueeze(-1)
+    return torch.where(pos, torch.mm(x, w_loop), torch.mm(x, w_evolve))
+
+
+def _layer_tail(layer, g, h_new, x, prev_h, c):
+    """clamp -> + loop [-> skip blend] -> clamp -> rrelu -> dropout -> exp0
+    (hyperbolic_layers.py:296-321, :672-694)."""
+    h_new = torch.clamp(h_new, -10.0, 10.0)
+    loop = _self_loop(x, g, layer.loop_weight, layer.evolve_loop_weight) if layer.self_loop else None
+    if layer.skip_connect and prev_h is not None:
+        prev_t = A.log0(prev_h, c)
+        gate = torch.sigmoid(torch.mm(prev_t, layer.skip_weight) + layer.skip_bias)
+        if loop is not None:
+            h_new = h_new + loop
+        h_new = gate * h_new + (1 - gate) * prev_t
+    elif loop is not None:
+        h_new = h_new + loop
+    h_new = torch.clamp(h_new, -10.0, 10.0)
+    h_new = F.leaky_relu(h_new, RRELU_SLOPE)
+    if layer.dropout is not None:
+        h_new = layer.dropout(h_new)
+    return A.exp0(h_new, c)
+
+
+def union_layer(layer, g, h, rel, prev_h=None):
+    """msg = ((x_src + rel) W_n) w_e summed and normalised == (norm sum_e w_e (x_src + rel)) W_n."""
+    c = float(layer.c)
+    x = A.log0(h, c)
+    r = A.get_radius(h)
+    agg = torch.mm(A.union_aggregate(x, r, rel.contiguous(), g, layer.radius_msg_gamma), layer.weight_neighbor)
+    return _layer_tail(layer, g, agg, x, prev_h, c)
+
+
+def lorentz_layer(layer, g, h, rel, prev_h=None):
+    c = float(layer.c)
+    x = A.log0(h, c)
+    d = x.shape[1]
+    rel_d = torch.zeros(layer.num_rels, d, device=x.device) if rel is None else rel[:, :d].contiguous()
+    agg = A.lorentz_aggregate(x, rel_d, layer.weight, g, layer.num_bases, c)
+    return _layer_tail(layer, g, agg, x, prev_h, c)
+
+
+def cell_forward(cell, g, h, rel_embs, lorentz):
+    """HyperbolicRGCNCell (no prev_h, hyperbolic_model.py:142-154) / LorentzRGCNCell
+    (prev_h = the layer input, hyperbolic_layers.py:719-743)."""
+    prev = None
+    for i, layer in enumerate(cell.layers):
+        if lorentz:
+            new = lorentz_layer(layer, g, h, rel_embs[i], prev_h=prev)
+        else:
+            new = union_layer(layer, g, h, rel_embs[i])
+        prev, h = h, new
+    return h
+
+
+def relation_context(x, g, R2):
+    """x_input[r] = mean of the rows of r's r_to_e span, 0 for absent relations
+    (hyperbolic_model.py:802-812).  Spans are laid out in relation-id order."""
+    wk = g.work()
+    idx = wk["rel_idx"]
+    out = torch.zeros(R2, x.shape[1], device=x.device, dtype=x.dtype)
+    if idx.numel() == 0:
+        return out
+    rel_of = g.__dict__.get("_rel_of_item")
+    if rel_of is None:
+        cnt = wk["rel_count"].long()
+        rel_of = torch.repeat_interleave(torch.arange(R2, device=x.device), cnt)
+        g.__dict__["_rel_of_item"] = rel_of
+    out = out.index_add(0, rel_of, x.index_select(0, idx.long()))
+    return out / torch.clamp(wk["rel_count"], min=1.0).unsqueeze(-1)
+
+
+def model_forward(model, g_list):
+    """HyperbolicRecurrentRGCN.forward with autograd (hyperbolic_model.py:722-890)."""
+    c = model._c_float()
+    dev = model.dynamic_emb.device
+    R2 = model.num_rels * 2
+    r_static = model._static_radius(c)
+    dyn = model.dynamic_emb
+    h = A.exp0(F.normalize(dyn) if model.layer_norm else dyn, c)                       # :775-780
+    h = A.apply_radius(h, r_static, c)                                                 # :782
+    trev = model.temporal_radius_evolution
+    lorentz = model.encoder_name == "lgcn"
+    history, h0 = [], None
+    for i, g in enumerate(g_list):
+        g = g.to(dev)
+        x_prev = A.log0(h, c)                                                          # :802
+        x_in = torch.cat([model.emb_rel, relation_context(x_prev, g, R2)], dim=1)
+        h0 = model.relation_gru(x_in, model.emb_rel if i == 0 else h0)                 # :815-823
+        if model.layer_norm:
+            h0 = F.normalize(h0)
+        cur = cell_forward(model.rgcn, g, h, [h0] * len(model.rgcn.layers), lorentz)   # :828
+        cur = A.project(cur, c)                                                        # :829
+        if model.layer_norm:
+            cur = A.exp0(F.normalize(A.log0(cur, c)), c)                              # :832-835
+        ct = torch.clamp(A.log0(cur, c), -10.0, 10.0)                                  # :841-846
+        pt = torch.clamp(x_prev, -10.0, 10.0)
+        tw = torch.sigmoid(torch.mm(pt, model.time_gate_weight) + model.time_gate_bias)
+        h = A.project(A.exp0(tw * ct + (1 - tw) * pt, c), c)                          # :859-860
+        if model.use_residual_evolution:
+            t = A.log0(h, trev.c)                                                      # hyperbolic_ops.py:395-435
+            delta = torch.clamp(trev.radius_mlp(t).squeeze(-1), -trev.epsilon, trev.epsilon)
+            base = trev.anchor_beta * r_static + (1.0 - trev.anchor_beta) * A.get_radius(h)
+            h = A.apply_radius(h, base + delta, trev.c)
+        else:
+            h = A.apply_radius(h, r_static, c)                                         # :869
+        history.append(h)
+    return history, None, h0, [], []

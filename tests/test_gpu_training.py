@@ -1,0 +1,116 @@
+"""Training path on the HIP kernels vs the reference's own loss values and
+parameter gradients of one mini-batch (tests/golden/train_*.npz, made by running the
+reference: tools/goldens/make_golden.py train), plus a few optimizer steps against the oracle.
+
+Tolerance: losses 1e-4 relative; each gradient tensor |delta| <= 2e-3 max|ref| (fp32 backward
+through two recurrent layers x three timesteps, the reference itself fp32)."""
+import numpy as np
+import pytest
+import torch
+
+from regcn_amd import graph as G
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+C = 0.01
+
+CASES = {
+    "uvrgcn_roth": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False),
+    "lgcn_roth": dict(encoder_name="lgcn", decoder_name="roth", layer_norm=False),
+    "lgcn_roth_ln_skip": dict(encoder_name="lgcn", decoder_name="roth", layer_norm=True, skip_connect=True),
+    "uvrgcn_murp_nores": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="murp", layer_norm=False,
+                              use_residual_evolution=False),
+    "uvrgcn_atth_beta": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="atth", layer_norm=True,
+                             radius_anchor_beta=0.5),
+    "uvrgcn_convtranse": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="hyperbolic_convtranse",
+                              layer_norm=True),
+}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def build(z, tag):
+    from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
+    V, R, d, T = (int(v) for v in z["meta"])
+    kw = dict(num_ents=V, num_rels=R, num_static_rels=0, num_words=0, h_dim=d, opn="sub", sequence_len=T,
+              num_bases=d // 2, num_hidden_layers=2, dropout=0.0, c=C, self_loop=True, skip_connect=False,
+              input_dropout=0.0, hidden_dropout=0.0, feat_dropout=0.0, entity_prediction=True,
+              relation_prediction=True, use_cuda=True, gpu=0, radius_target=z["radius_target"],
+              radius_msg_gamma=0.15)
+    kw.update(CASES[tag])
+    m = HyperbolicRecurrentRGCN(**kw)
+    m.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("sd_")}, strict=True)
+    m = m.to(DEV).train()
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.BatchNorm1d):
+            mod.eval()
+    glist = [G.build_sub_graph(V, R, z["snap%d" % t], True, DEV) for t in range(T)]
+    return m, glist
+
+
+@pytest.mark.parametrize("tag", list(CASES))
+def test_training_grads_vs_reference(golden, tag):
+    z = golden("train_%s.npz" % tag)
+    m, glist = build(z, tag)
+    tw = float(z["task_weight"])
+    le, lr, ls, lrad = m.get_loss(glist, torch.from_numpy(z["batch"]).to(DEV), None, True)
+    loss = tw * le + (1 - tw) * lr + ls.sum() + lrad
+    got = np.array([float(x.detach().sum()) for x in (le, lr, lrad, loss)])
+    np.testing.assert_allclose(got, z["losses"][[0, 1, 3, 4]], rtol=1e-4, atol=1e-6)
+    m.zero_grad()
+    loss.backward()
+    params = dict(m.named_parameters())
+    n = 0
+    for k in list(z):
+        if not k.startswith("grad_"):
+            continue
+        g = params[k[5:]].grad
+        assert g is not None, k
+        ref = torch.from_numpy(z[k]).double()
+        scale = max(1e-3, float(ref.abs().max()))
+        err = float((g.detach().double().cpu() - ref).abs().max()) / scale
+        assert err <= 2e-3, "%s: %.3g" % (k, err)
+        n += 1
+    assert n >= 20
+
+
+def test_training_steps_vs_oracle(golden):
+    """Three Adam steps (lr 1e-3, weight decay 1e-5, clip 1.0: hyperbolic_main.py:469, :627-628)
+    on the lgcn+roth case: the HIP model and the oracle (fp64) keep the same loss trajectory."""
+    from oracle import graph as OG
+    from oracle import model as OM
+    z = golden("train_lgcn_roth.npz")
+    m, glist = build(z, "lgcn_roth")
+    V, R, d, T = (int(v) for v in z["meta"])
+    sd = {k[3:]: torch.from_numpy(v).double() if v.dtype == np.float32 else torch.from_numpy(v)
+          for k, v in z.items() if k.startswith("sd_")}
+    names = [k for k, _ in m.named_parameters()]
+    oparams = [sd[k].requires_grad_(True) for k in names]
+    cfg = dict(c=C, n_layers=2, n_bases=d // 2, radius_min=0.5, radius_max=3.0, radius_epsilon=0.1,
+               radius_anchor_beta=1.0, radius_msg_gamma=0.15, use_residual_evolution=True, encoder="lgcn",
+               decoder="roth", layer_norm=False)
+    og = [OG.build_sub_graph(V, R, z["snap%d" % t]) for t in range(T)]
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+    oopt = torch.optim.Adam(oparams, lr=1e-3, weight_decay=1e-5)
+    batch = torch.from_numpy(z["batch"])
+    for step in range(3):
+        opt.zero_grad()
+        le, lr, ls, lrad = m.get_loss(glist, batch.to(DEV), None, True)
+        loss = 0.7 * le + 0.3 * lr + ls.sum() + lrad
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+        opt.step()
+        oopt.zero_grad()
+        ole, olr, ols, olrad = OM.hyperbolic_get_loss(sd, cfg, og, batch, z["radius_target"])
+        oloss = 0.7 * ole + 0.3 * olr + ols.sum() + olrad
+        oloss.backward()
+        torch.nn.utils.clip_grad_norm_(oparams, 1.0)
+        oopt.step()
+        assert abs(float(loss) - float(oloss)) <= 1e-4 * max(1.0, abs(float(oloss))), (step, float(loss), float(oloss))
+    for k, p in zip(names, oparams):
+        got = dict(m.named_parameters())[k].detach().double().cpu()
+        assert float((got - p.detach()).abs().max()) <= 1e-4 * max(1.0, float(p.abs().max())), k

@@ -169,3 +169,52 @@ def test_rank(golden):
     np.testing.assert_array_equal(rank_r.numpy(), z["rank_r"])
     np.testing.assert_array_equal(frank_r.numpy(), z["frank_r"])
     np.testing.assert_allclose([m, mf, mr, mfr], z["mrr"], rtol=1e-6)
+
+
+TRAIN_CASES = {
+    "uvrgcn_roth": dict(encoder="hyperbolic_uvrgcn", decoder="roth", layer_norm=False),
+    "lgcn_roth": dict(encoder="lgcn", decoder="roth", layer_norm=False),
+    "lgcn_roth_ln_skip": dict(encoder="lgcn", decoder="roth", layer_norm=True, skip_connect=True),
+    "uvrgcn_murp_nores": dict(encoder="hyperbolic_uvrgcn", decoder="murp", layer_norm=False,
+                              use_residual_evolution=False),
+    "uvrgcn_atth_beta": dict(encoder="hyperbolic_uvrgcn", decoder="atth", layer_norm=True, radius_anchor_beta=0.5),
+    "uvrgcn_convtranse": dict(encoder="hyperbolic_uvrgcn", decoder="hyperbolic_convtranse", layer_norm=True),
+}
+
+
+def train_cfg(tag, d):
+    cfg = dict(c=C, n_layers=2, n_bases=d // 2, radius_min=0.5, radius_max=3.0, radius_epsilon=0.1,
+               radius_anchor_beta=1.0, radius_msg_gamma=0.15, use_residual_evolution=True)
+    cfg.update(TRAIN_CASES[tag])
+    return cfg
+
+
+@pytest.mark.parametrize("tag", list(TRAIN_CASES))
+def test_oracle_training_grads_vs_reference(golden, tag):
+    """f1 pin: the oracle's get_loss + torch autograd reproduce the reference's loss values and
+    every parameter gradient of one training mini-batch (tools/goldens/make_golden.py train)."""
+    z = golden("train_%s.npz" % tag)
+    V, R, d, T = (int(v) for v in z["meta"])
+    sd = {k[3:]: torch.from_numpy(v).double() if v.dtype == np.float32 else torch.from_numpy(v)
+          for k, v in z.items() if k.startswith("sd_")}
+    for k in sd:
+        if "grad_" + k in z:
+            sd[k].requires_grad_(True)
+    glist = [og.build_sub_graph(V, R, z["snap%d" % t]) for t in range(T)]
+    le, lr, ls, lrad = om.hyperbolic_get_loss(sd, train_cfg(tag, d), glist, torch.from_numpy(z["batch"]),
+                                              z["radius_target"])
+    tw = float(z["task_weight"])
+    loss = tw * le + (1 - tw) * lr + ls.sum() + lrad
+    np.testing.assert_allclose([float(x.detach().sum()) for x in (le, lr, lrad, loss)], z["losses"][[0, 1, 3, 4]],
+                               rtol=1e-5, atol=1e-6)
+    loss.backward()
+    n = 0
+    for k in list(z):
+        if k.startswith("grad_"):
+            g = sd[k[5:]].grad
+            ref = torch.from_numpy(z[k]).double()
+            scale = max(1e-3, float(ref.abs().max()))
+            err = float((g - ref).abs().max()) / scale
+            assert err <= 1e-3, "%s: %.3g" % (k, err)
+            n += 1
+    assert n >= 20
