@@ -10,13 +10,22 @@ on-disk format (`<data-dir>/<dataset>/{train,valid,test}.txt` rows `s\\tr\\to\\t
 `-d synthetic:<config>` evaluates a generated snapshot series of a
 `regcn_amd.synthetic.CONFIGS` shape instead.  Checkpoints are read with
 `torch.load(weights_only=True)` (`{'state_dict': ..., 'epoch': ...}` as the reference saves
-them); without one the model keeps its random initialisation.  Training (no `--test`) and
-the out-of-scope features (static graph, EST, fhnn/hgat, Riemannian Adam) raise: the HIP
-path is forward-only in this build.
+them); without one the model keeps its random initialisation.
+
+Without `--test` the model trains (hyperbolic_main.py:505-705): epochs over the shuffled
+training snapshots, each one's history window as input, its triples in `--triple-batch-size`
+mini-batches whose gradients accumulate, gradient clipping and one Adam step per snapshot,
+validation every `--evaluate-every` epochs saving the best raw MRR to the checkpoint, early
+stop after 20 epochs without improvement, then the test set on the best checkpoint.  The
+forward and backward run on the HIP kernels (training.py / autograd.py); snapshot graphs
+are built once on the device and reused across epochs (the reference rebuilds them per
+sample, :560).  Out-of-scope features (static graph, EST, fhnn/hgat, Riemannian Adam) raise,
+as do the two whose gradients are not built (learned curvature, relation curvature).
 """
 import argparse
 import logging
 import os
+import random
 import sys
 import time
 
@@ -103,6 +112,8 @@ def build_parser():
     a("--data-dir", type=str, default="../data", help="dataset root (reference: ../data)")
     a("--checkpoint", type=str, default=None, help="state checkpoint (torch.save of {'state_dict', 'epoch'})")
     a("--synthetic-snapshots", type=int, default=12, help="snapshots generated for -d synthetic:<config>")
+    a("--seed", type=int, default=None, help="seed python/numpy/torch RNGs (snapshot shuffle, dropout, init)")
+    a("--max-train-snapshots", type=int, default=None, help="train on at most this many snapshots per epoch")
     return p
 
 
@@ -225,15 +236,95 @@ def test(model, history_list, test_list, num_rels, num_nodes, device, all_ans_li
             ranking.stat_ranks(ranks_raw_r, "raw_rel").item(), ranking.stat_ranks(ranks_filter_r, "filter_rel").item())
 
 
+class GraphCache:
+    """Device snapshot graphs keyed by the snapshot array's identity (built once, reused)."""
+
+    def __init__(self, num_nodes, num_rels, device):
+        self.n, self.r, self.dev, self.g = num_nodes, num_rels, device, {}
+
+    def __call__(self, snap):
+        key = id(snap)
+        if key not in self.g:
+            self.g[key] = (snap, build_sub_graph(self.n, self.r, snap, True, self.dev))
+        return self.g[key][1]
+
+
+def train_model(args, model, train_list, valid, num_nodes, num_rels, device, model_state_file):
+    """hyperbolic_main.py:505-640 (`valid`: the validation rows with their time column).
+    Returns {"best_mrr", "best_epoch", "epoch_loss": [mean loss per epoch]}."""
+    optimizer = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=1e-5)   # :469
+    valid_list = ranking.split_by_time(valid)
+    all_ans_v = ranking.load_all_answers_for_time_filter(valid, num_rels, num_nodes, False)
+    all_ans_r_v = ranking.load_all_answers_for_time_filter(valid, num_rels, num_nodes, True)
+    graphs = GraphCache(num_nodes, num_rels, device)
+    best_mrr, best_epoch, patience = 0.0, 0, 20
+    epoch_loss = []
+    t_start = time.time()
+    for epoch in range(args.n_epochs):
+        t0 = time.time()
+        model.train()
+        losses, losses_e, losses_r, losses_rad = [], [], [], []
+        idx = list(range(len(train_list)))
+        random.shuffle(idx)
+        if args.max_train_snapshots:
+            idx = idx[:args.max_train_snapshots]
+        for n in idx:
+            if n == 0:
+                continue
+            inputs = train_list[max(0, n - args.train_history_len):n]
+            glist = [graphs(s) for s in inputs]
+            triples = torch.from_numpy(np.asarray(train_list[n], dtype=np.int64)).to(device)
+            if triples.shape[0] == 0:
+                continue
+            optimizer.zero_grad()
+            se = sr = srad = 0.0
+            nb = 0
+            for b in range(0, triples.shape[0], args.triple_batch_size):
+                le, lr, ls, lrad = model.get_loss(glist, triples[b:b + args.triple_batch_size], None, True,
+                                                  query_time=n)
+                loss = args.task_weight * le + (1 - args.task_weight) * lr + ls.sum() + lrad
+                loss.backward()
+                se += float(le)
+                sr += float(lr)
+                srad += float(lrad)
+                nb += 1
+            losses_e.append(se / nb)
+            losses_r.append(sr / nb)
+            losses_rad.append(srad / nb)
+            losses.append(args.task_weight * losses_e[-1] + (1 - args.task_weight) * losses_r[-1] + losses_rad[-1])
+            torch.nn.utils.clip_grad_norm_(model.parameters(), args.grad_norm)              # :627-628
+            optimizer.step()
+        epoch_loss.append(float(np.mean(losses)) if losses else float("nan"))
+        if epoch % args.log_interval == 0:
+            logger.info("Epoch %04d | Loss: %.4f | E/R/S/Rad: %.4f/%.4f/%.4f/%.4f | Best MRR: %.4f | Time: %.1fs",
+                        epoch, np.mean(losses) if losses else float("nan"), np.mean(losses_e) if losses_e else 0.0,
+                        np.mean(losses_r) if losses_r else 0.0, 0.0, np.mean(losses_rad) if losses_rad else 0.0,
+                        best_mrr, time.time() - t0)
+        if epoch and epoch % args.evaluate_every == 0:                                      # :660-681
+            res = test(model, train_list, valid_list, num_rels, num_nodes, device, all_ans_v, all_ans_r_v, args)
+            logger.info("Validation - MRR: raw=%.4f, filter=%.4f | Rel MRR: raw=%.4f, filter=%.4f", *res)
+            cur = res[2] if args.relation_evaluation else res[0]
+            if cur > best_mrr:
+                best_mrr, best_epoch = cur, epoch
+                os.makedirs(os.path.dirname(os.path.abspath(model_state_file)), exist_ok=True)
+                torch.save({"state_dict": model.state_dict(), "epoch": epoch}, model_state_file)
+                logger.info("New best model saved! MRR: %.4f", best_mrr)
+            elif epoch - best_epoch >= patience:
+                logger.info("Early stopping at epoch %d: no improvement in %d epochs.", epoch, patience)
+                break
+    logger.info("Training completed in %.1f minutes", (time.time() - t_start) / 60)
+    return {"best_mrr": best_mrr, "best_epoch": best_epoch, "epoch_loss": epoch_loss}
+
+
 def main(argv=None):
     args = build_parser().parse_args(argv)
     logging.basicConfig(level=logging.DEBUG if args.verbose else logging.INFO, format="%(message)s")
     bad = _unsupported(args)
     if bad:
         raise SystemExit("not supported in this build (SURVEY.md §2 out of scope): " + ", ".join(bad))
-    if not args.test:
-        raise SystemExit("training is not supported in this build: the HIP path is forward-only "
-                         "(backward kernels are SURVEY.md §8(f) row f1); run with --test")
+    if not args.test and (args.learn_curvature or args.plus_relation_specific_curvature):
+        raise SystemExit("training with --learn-curvature / --plus-relation-specific-curvature is not supported "
+                         "in this build (their gradients are not built)")
     if args.radius_msg_gamma < 0:
         raise ValueError("--radius-msg-gamma must be non-negative (use 0 to disable the penalty)")
     if not 0.0 <= args.radius_anchor_beta <= 1.0:
@@ -242,6 +333,10 @@ def main(argv=None):
         raise SystemExit("the HIP path needs a GPU (--gpu N); there is no CPU fallback")
     device = torch.device("cuda", args.gpu)
     torch.cuda.set_device(device)
+    if args.seed is not None:
+        random.seed(args.seed)
+        np.random.seed(args.seed)
+        torch.manual_seed(args.seed)
     num_nodes, num_rels, train, valid, test_data = load_dataset(args)
     train_list = ranking.split_by_time(train)
     valid_list = ranking.split_by_time(valid)
@@ -251,6 +346,11 @@ def main(argv=None):
     all_ans = ranking.load_all_answers_for_time_filter(test_data, num_rels, num_nodes, False)
     all_ans_r = ranking.load_all_answers_for_time_filter(test_data, num_rels, num_nodes, True)
     model = build_model(args, num_nodes, num_rels, train_list, device)
+    model_state_file = args.checkpoint or os.path.join(
+        "models", "%s-%s-%s.pth" % (args.dataset.replace(":", "_"), args.encoder, args.decoder))
+    if not args.test:
+        train_model(args, model, train_list, valid, num_nodes, num_rels, device, model_state_file)
+        args.checkpoint = model_state_file if os.path.exists(model_state_file) else None
     if args.checkpoint:
         ck = torch.load(args.checkpoint, map_location=device, weights_only=True)
         model.load_state_dict(ck["state_dict"] if "state_dict" in ck else ck)

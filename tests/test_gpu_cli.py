@@ -58,5 +58,36 @@ def test_cli_rejects_out_of_scope_flags():
     from regcn_amd import cli
     with pytest.raises(SystemExit):
         cli.main(["-d", "synthetic:icews14s_lgcn_roth", "--test", "--gpu", "0", "--use-est"])
-    with pytest.raises(SystemExit):
-        cli.main(["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0"])  # training
+    with pytest.raises(SystemExit):  # training needs the gradient of a learned curvature: not built
+        cli.main(["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0", "--learn-curvature"])
+
+
+def test_cli_training_loop(tmp_path):
+    """hyperbolic_main.py training branch on HIP: the loss falls over epochs, validation saves
+    a checkpoint the test phase reloads, and the trained model ranks better than its init."""
+    from regcn_amd import cli, ranking
+    ck = str(tmp_path / "m.pth")
+    common = ["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0", "--encoder", "lgcn", "--decoder", "roth",
+              "--n-hidden", "64", "--n-bases", "32", "--synthetic-snapshots", "10", "--train-history-len", "3",
+              "--test-history-len", "3", "--relation-prediction", "--entity-prediction", "--checkpoint", ck,
+              "--seed", "0", "--lr", "0.01", "--triple-batch-size", "128"]
+    args = cli.build_parser().parse_args(common + ["--n-epochs", "6", "--evaluate-every", "1"])
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    V, R, train, valid, test = cli.load_dataset(args)
+    tl = ranking.split_by_time(train)
+    model = cli.build_model(args, V, R, tl, dev)
+    ans = ranking.load_all_answers_for_time_filter(valid, R, V, False)
+    ans_r = ranking.load_all_answers_for_time_filter(valid, R, V, True)
+    before = cli.test(model, tl, ranking.split_by_time(valid), R, V, dev, ans, ans_r, args)
+    out = cli.train_model(args, model, tl, valid, V, R, dev, ck)
+    losses = out["epoch_loss"]
+    assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
+    assert out["best_mrr"] > before[0], (out["best_mrr"], before)
+    import os
+    assert os.path.exists(ck)
+    sd = torch.load(ck, map_location=dev, weights_only=True)
+    assert sd["epoch"] == out["best_epoch"]
+    # the CLI entry point end to end (train then test on the saved checkpoint)
+    res = cli.main(common + ["--n-epochs", "2"])
+    assert all(0.0 < m <= 1.0 for m in res)
