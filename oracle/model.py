@@ -395,3 +395,18 @@ def hyperbolic_get_loss(sd, cfg, glist, triples, radius_target):
     lrad = cfg.get("radius_lambda", 0.02) * F.mse_loss(static_radius(sd, cfg)[ids],
                                                        torch.as_tensor(radius_target)[ids].to(emb.dtype))
     return le, lr, torch.zeros(1, dtype=emb.dtype), lrad
+
+
+def euclid_get_loss(sd, cfg, glist, triples):
+    """RecurrentRGCN.get_loss, src/rrgcn.py:196-248 (no static graph)."""
+    R = sd["emb_rel"].shape[0] // 2
+    inv = triples[:, [2, 1, 0]].clone()
+    inv[:, 1] += R
+    all_tr = torch.cat([triples, inv])
+    embs, h0 = euclid_forward(sd, cfg, glist)
+    emb = F.normalize(embs[-1]) if cfg["layer_norm"] else embs[-1]
+    le = F.cross_entropy(_conv_decoder(sd, "decoder_ob.", emb, h0, all_tr, None, False, hyperbolic=False),
+                         all_tr[:, 2].long())
+    lr = F.cross_entropy(_conv_decoder(sd, "rdecoder.", emb, h0, all_tr, None, True, hyperbolic=False),
+                         all_tr[:, 1].long())
+    return le, lr, torch.zeros(1, dtype=emb.dtype)

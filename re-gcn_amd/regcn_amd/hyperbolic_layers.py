@@ -6,7 +6,8 @@ signatures follow the reference; forward runs three gfx950 kernels per layer:
   2. CSR gather + segment reduce (csrc/aggregate.hip);
   3. MFMA layer tail: neighbour/self-loop/skip GEMMs + clamp/rrelu/dropout/exp0 and the
      next layer's prologue, fused (csrc/rowgemm.hip).
-Forward only (no autograd); FHNN/HGAT encoders are outside this build's scope.
+With autograd on (training) the model runs training.py instead, the differentiable
+composition of the same layers; FHNN/HGAT encoders are outside this build's scope.
 """
 import torch
 import torch.nn as nn

@@ -3,7 +3,7 @@
 Same class names, method names, argument meaning and defaults as the reference; every
 method runs a hand-written gfx950 kernel (csrc/rowwise.hip) through the C-ABI.  Inputs
 must be fp32 HIP tensors; `c` may be a python float or a 0-dim tensor (read once, as the
-reference's `c.item()` does at hyperbolic_ops.py:72).  No autograd: these are the
+reference's `c.item()` does at hyperbolic_ops.py:72).  With autograd on, the row maps route to autograd.py (HIP backward kernels); these are the
 inference/forward row maps of the hot path.
 """
 import math

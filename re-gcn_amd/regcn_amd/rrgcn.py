@@ -3,7 +3,9 @@
 `RecurrentRGCN.forward(g_list, static_graph, use_cuda)` keeps the reference signature and
 5-tuple return (src/rrgcn.py:142-180).  Message passing and the relation-context mean
 run on HIP; the relation GRU, the time gate and the ConvTransE/R decoders stay on torch
-(host GEMMs).  Forward only.
+(host GEMMs).  With autograd on (training), forward runs
+training.euclid_model_forward (HIP aggregation forward + backward); get_loss mirrors
+src/rrgcn.py:196-248 without the static graph.
 """
 import math
 
@@ -153,7 +155,10 @@ class RecurrentRGCN(nn.Module):
     def forward(self, g_list, static_graph, use_cuda):
         """src/rrgcn.py:142-180."""
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("the HIP path is forward-only in this build; use torch.no_grad()")
+            from .training import euclid_model_forward
+            out = euclid_model_forward(self, g_list)
+            self.h, self.h_0 = out[0][-1], out[2]
+            return out
         dev = self.dynamic_emb.device
         self.h = F.normalize(self.dynamic_emb) if self.layer_norm else self.dynamic_emb[:, :]
         self.h = self.h.contiguous()
@@ -182,3 +187,23 @@ class RecurrentRGCN(nn.Module):
             at = all_triples.to(embedding.device)
             return all_triples, self.decoder_ob.forward(embedding, r_emb, at, mode="test"), \
                 self.rdecoder.forward(embedding, r_emb, at, mode="test")
+
+    def get_loss(self, glist, triples, static_graph, use_cuda):
+        """src/rrgcn.py:196-248 (no static graph): entity / relation cross entropy of the
+        ConvTransE / ConvTransR scores over the triples and their inverses."""
+        dev = self.dynamic_emb.device
+        loss_ent = torch.zeros(1, device=dev)
+        loss_rel = torch.zeros(1, device=dev)
+        loss_static = torch.zeros(1, device=dev)
+        inv = triples[:, [2, 1, 0]].clone()
+        inv[:, 1] = inv[:, 1] + self.num_rels
+        all_triples = torch.cat([triples, inv]).to(dev)
+        evolve_embs, _, r_emb, _, _ = self.forward(glist, static_graph, use_cuda)
+        pre_emb = F.normalize(evolve_embs[-1]) if self.layer_norm else evolve_embs[-1]
+        if self.entity_prediction:
+            scores_ob = self.decoder_ob.forward(pre_emb, r_emb, all_triples).view(-1, self.num_ents)
+            loss_ent = loss_ent + self.loss_e(scores_ob, all_triples[:, 2])
+        if self.relation_prediction:
+            score_rel = self.rdecoder.forward(pre_emb, r_emb, all_triples, mode="train").view(-1, 2 * self.num_rels)
+            loss_rel = loss_rel + self.loss_r(score_rel, all_triples[:, 1])
+        return loss_ent, loss_rel, loss_static

@@ -129,3 +129,39 @@ def model_forward(model, g_list):
             h = A.apply_radius(h, r_static, c)                                         # :869
         history.append(h)
     return history, None, h0, [], []
+
+
+def euclid_layer(layer, g, h, rel):
+    """UnionRGCNLayer.forward, rgcn/layers.py:222-279 (the cell passes prev_h = [], so no skip):
+    norm sum_e (h_src + rel) W_n + loop, rrelu, dropout."""
+    zero_r = torch.zeros(h.shape[0], device=h.device)
+    node = torch.mm(A.union_aggregate(h, zero_r, rel.contiguous(), g, 0.0), layer.weight_neighbor)
+    if layer.self_loop:
+        node = node + _self_loop(h, g, layer.loop_weight, layer.evolve_loop_weight)
+    node = F.leaky_relu(node, RRELU_SLOPE)
+    if layer.dropout is not None:
+        node = layer.dropout(node)
+    return node
+
+
+def euclid_model_forward(model, g_list):
+    """RecurrentRGCN.forward with autograd (src/rrgcn.py:142-180)."""
+    dev = model.dynamic_emb.device
+    R2 = model.num_rels * 2
+    h = F.normalize(model.dynamic_emb) if model.layer_norm else model.dynamic_emb
+    history, h0 = [], None
+    for i, g in enumerate(g_list):
+        g = g.to(dev)
+        x_in = torch.cat([model.emb_rel, relation_context(h, g, R2)], dim=1)
+        h0 = model.relation_cell_1(x_in, model.emb_rel if i == 0 else h0)
+        if model.layer_norm:
+            h0 = F.normalize(h0)
+        cur = h
+        for layer in model.rgcn.layers:
+            cur = euclid_layer(layer, g, cur, h0)
+        if model.layer_norm:
+            cur = F.normalize(cur)
+        tw = torch.sigmoid(torch.mm(h, model.time_gate_weight) + model.time_gate_bias)
+        h = tw * cur + (1 - tw) * h
+        history.append(h)
+    return history, None, h0, [], []

@@ -218,3 +218,30 @@ def test_oracle_training_grads_vs_reference(golden, tag):
             assert err <= 1e-3, "%s: %.3g" % (k, err)
             n += 1
     assert n >= 20
+
+
+@pytest.mark.parametrize("tag", ["noln", "ln"])
+def test_oracle_euclid_training_grads_vs_reference(golden, tag):
+    z = golden("train_rrgcn_%s.npz" % tag)
+    V, R, d, T = (int(v) for v in z["meta"])
+    sd = {k[3:]: torch.from_numpy(v).double() if v.dtype == np.float32 else torch.from_numpy(v)
+          for k, v in z.items() if k.startswith("sd_")}
+    for k in sd:
+        if "grad_" + k in z:
+            sd[k].requires_grad_(True)
+    glist = [og.build_sub_graph(V, R, z["snap%d" % t]) for t in range(T)]
+    le, lr, ls = om.euclid_get_loss(sd, dict(layer_norm=(tag == "ln"), n_layers=2), glist,
+                                    torch.from_numpy(z["batch"]))
+    tw = float(z["task_weight"])
+    loss = tw * le + (1 - tw) * lr + ls.sum()
+    np.testing.assert_allclose([float(x.detach().sum()) for x in (le, lr, loss)], z["losses"][[0, 1, 3]],
+                               rtol=1e-5, atol=1e-6)
+    loss.backward()
+    n = 0
+    for k in list(z):
+        if k.startswith("grad_"):
+            ref = torch.from_numpy(z[k]).double()
+            err = float((sd[k[5:]].grad - ref).abs().max()) / max(1e-3, float(ref.abs().max()))
+            assert err <= 1e-3, "%s: %.3g" % (k, err)
+            n += 1
+    assert n >= 15

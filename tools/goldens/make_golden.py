@@ -377,6 +377,36 @@ def gen_train():
             if p.grad is not None:
                 out["grad_" + k] = p.grad.numpy().copy()
         save("train_%s.npz" % tag, **out)
+    # Euclidean RE-GCN (src/rrgcn.py:196-248, src/main.py's loss).  Its CPU branch adds in place
+    # to a leaf zeros(1, requires_grad=True) and raises; on the GPU branch `.cuda()` returns a
+    # non-leaf copy.  Emulate that branch: use_cuda=True with .cuda() a copy on the CPU.
+    torch.Tensor.cuda = lambda self, *a, **k: self.clone()  # noqa: E731
+    for i, ln in enumerate((False, True)):
+        torch.manual_seed(400 + i)
+        m = RecurrentRGCN("convtranse", "uvrgcn", V, R, 0, 0, d, "sub", T, num_bases=100, num_basis=100,
+                          num_hidden_layers=2, dropout=0.0, self_loop=True, skip_connect=False, layer_norm=ln,
+                          input_dropout=0.0, hidden_dropout=0.0, feat_dropout=0.0, entity_prediction=True,
+                          relation_prediction=True, use_cuda=True, gpu="cpu")
+        sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        m.train()
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.eval()
+        m.zero_grad()
+        le, lr, ls = m.get_loss(glist, batch.clone(), None, True)
+        loss = tw * le + (1 - tw) * lr + ls
+        loss.backward()
+        out = {"meta": np.array([V, R, d, T]), "batch": snaps[T], "task_weight": np.array(tw),
+               "losses": np.array([float(x) for x in (le, lr, ls, loss)])}
+        for t in range(T):
+            out["snap%d" % t] = snaps[t]
+        for k, v in sd.items():
+            out["sd_" + k] = v.numpy().copy()
+        for k, p in m.named_parameters():
+            if p.grad is not None:
+                out["grad_" + k] = p.grad.numpy().copy()
+        save("train_rrgcn_%s.npz" % ("ln" if ln else "noln"), **out)
+    torch.Tensor.cuda = lambda self, *a, **k: self  # noqa: E731
 
 
 def gen_rrgcn():
