@@ -68,28 +68,6 @@ __device__ __forceinline__ T pair_score(T xy, T x2, T y2, T bias_n, T cr, const 
   return (T)p.scale * ((T)p.margin - dist) + bias_n;
 }
 
-// Gradient of the proxy score S = scale (margin - n^2) w.r.t. (xy, x2, y2): returns n^2,
-// writes dn2/dxy, dn2/dx2, dn2/dy2 (zero where |mobius| is clamped to mx: projected rows
-// pass no radial gradient, as torch's clamp in project_to_ball).
-__device__ __forceinline__ float pair_n2_grad(float xy, float x2, float y2, const ScoreArgs& p, float* gxy,
-                                              float* gx2, float* gy2) {
-  const float c = p.c;
-  const float A = 1.f - 2.f * c * xy + c * y2;
-  const float Bq = 1.f - c * x2;
-  const float num2 = fmaxf(A * A * x2 - 2.f * A * Bq * xy + Bq * Bq * y2, 0.f);
-  const float den = 1.f - 2.f * c * xy + c * c * x2 * y2 + REGCN_EPS;
-  const float nr = sqrtf(num2) / den;
-  if (nr > p.mx) {
-    *gxy = *gx2 = *gy2 = 0.f;
-    return p.mx * p.mx;
-  }
-  const float i2 = 1.f / (den * den), t = 2.f * num2 * i2 / den;
-  *gxy = (-4.f * c * A * x2 + 4.f * c * Bq * xy - 2.f * A * Bq) * i2 + t * (2.f * c);
-  *gx2 = (A * A + 2.f * c * A * xy - 2.f * c * Bq * y2) * i2 - t * (c * c * y2);
-  *gy2 = (2.f * c * A * x2 - 2.f * c * Bq * xy + Bq * Bq) * i2 - t * (c * c * x2);
-  return num2 * i2;
-}
-
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 template <bool F64>
@@ -129,44 +107,6 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& p, const V* acc,
         if (ni[j] < p.N)
           p.out[(int64_t)qi[r] * p.N + ni[j]] = (float)pair_score<T>(acc[j][r], x2[r], y2[j], bn_[j], cr[r], p);
     }
-  } else if (MODE == 2) {  // CE backward coefficients (proxy score, fp32)
-    const int nblk = (p.N + SN - 1) / SN;
-    float cs[4][3];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cs[j][0] = cs[j][1] = cs[j][2] = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool qok = qi[r] < p.B;
-      const int t = qok ? p.target[qi[r]] : -1;
-      const float lse = qok ? p.lse[qi[r]] : 0.f, gl = qok ? p.gl[qi[r]] : 0.f;
-      float rs = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (!qok || ni[j] >= p.N) continue;
-        float gxy, gx2, gy2;
-        const float n2 = pair_n2_grad((float)acc[j][r], (float)x2[r], (float)y2[j], p, &gxy, &gx2, &gy2);
-        const float S = p.scale * (p.margin - n2) + (float)bn_[j];
-        const float G = gl * (expf(S - lse) - (ni[j] == t ? 1.f : 0.f));
-        const float Gs = -p.scale * G;
-        p.coef[(int64_t)qi[r] * p.N + ni[j]] = Gs * gxy;
-        rs += Gs * gx2;
-        cs[j][0] += Gs * gy2;
-        cs[j][1] += G;
-        cs[j][2] += G * (p.margin - n2);
-      }
-      rs = group16_sum(rs);
-      if ((lane & 15) == 0 && qok) p.rsum[(int64_t)qi[r] * nblk + bn] = rs;
-    }
-    const int grp = (qi[0] - 4 * (lane >> 4)) >> 4;  // this wave's 16-query group
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        float v = cs[j][k];
-        v += __shfl_xor(v, 16);
-        v += __shfl_xor(v, 32);
-        if (lane < 16 && ni[j] < p.N) p.csum[((int64_t)grp * p.N + ni[j]) * 3 + k] = v;
-      }
   } else {
     const int nblk = (p.N + SN - 1) / SN;
 #pragma unroll
@@ -325,6 +265,151 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
   stamp(2);
 }
 
+// ---- lean fp32 epilogue of the proxy score (k_score_f32; no arctanh distance) -------------
+// S = scale (margin - n^2) + bias with n^2 = min(|num|^2 / den^2, mx^2): no square root, the
+// per-query and per-candidate factors hoisted out of the 16 pairs a lane holds, one v_rcp per
+// pair.  |num|^2 = A (A x2 - 2 Bq xy) + Bq^2 y2 with A = (1 + c y2) - 2c xy, Bq = 1 - c x2;
+// den = (1 + eps + c^2 x2 y2) - 2c xy.
+struct RowK {
+  float x2, m2Bq, Bq2, c2x2;
+};
+struct ColK {
+  float y2, A0, sb;
+};
+
+__device__ __forceinline__ RowK row_k(float x2, const ScoreArgs& p) {
+  const float Bq = 1.f - p.c * x2;
+  return RowK{x2, -2.f * Bq, Bq * Bq, p.c * p.c * x2};
+}
+__device__ __forceinline__ ColK col_k(float y2, float bias, const ScoreArgs& p) {
+  return ColK{y2, 1.f + p.c * y2, p.scale * p.margin + bias};
+}
+
+// n^2 of one pair (clamped to mx^2), and optionally num2 / den for the gradient.
+__device__ __forceinline__ float pair_n2(float xy, const RowK& r, const ColK& q, const ScoreArgs& p, float* num2_o,
+                                         float* rden_o, float* A_o) {
+  const float m2c = -2.f * p.c;
+  const float A = fmaf(m2c, xy, q.A0);
+  const float t = fmaf(A, r.x2, r.m2Bq * xy);
+  const float num2 = fmaxf(fmaf(A, t, r.Bq2 * q.y2), 0.f);
+  const float den = fmaf(m2c, xy, fmaf(r.c2x2, q.y2, 1.f + REGCN_EPS));
+  const float rd = __builtin_amdgcn_rcpf(den);
+  const float n2 = num2 * rd * rd;
+  if (num2_o) {
+    *num2_o = num2;
+    *rden_o = rd;
+    *A_o = A;
+  }
+  return fminf(n2, p.mx * p.mx);
+}
+
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false)));
+  return v;
+}
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+template <int MODE>
+__device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4* acc, const float* x2,
+                                                    const float* y2, const float* bn_, const int* qi, const int* ni,
+                                                    int lane, int bn) {
+  RowK rk[4];
+  ColK ck[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) rk[r] = row_k(x2[r], p);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ck[j] = col_k(y2[j], bn_[j], p);
+  const float mx2 = p.mx * p.mx;
+  if (MODE == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (qi[r] >= p.B) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ni[j] < p.N)
+          p.out[(int64_t)qi[r] * p.N + ni[j]] =
+              fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb);
+    }
+  } else if (MODE == 1) {
+    const int nblk = (p.N + SN - 1) / SN;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float s[4], m = -INFINITY;
+      const int t = qi[r] < p.B ? p.target[qi[r]] : -1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s[j] = ni[j] < p.N ? fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb)
+                           : -INFINITY;
+        m = fmaxf(m, s[j]);
+        if (ni[j] == t) p.tgt_logit[qi[r]] = s[j];
+      }
+      m = row16_max(m);
+      const float ml = m * LOG2E;
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) se += __builtin_amdgcn_exp2f(fmaf(s[j], LOG2E, -ml));  // exp(-inf) = 0
+      se = row16_sum(se);
+      if ((lane & 15) == 0 && qi[r] < p.B) {
+        float* o = p.part + ((int64_t)qi[r] * nblk + bn) * 2;
+        o[0] = m;
+        o[1] = se;
+      }
+    }
+  } else {  // MODE 2: CE backward coefficients
+    const int nblk = (p.N + SN - 1) / SN;
+    const float c = p.c, m2c = -2.f * c;
+    float cs[4][3];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cs[j][0] = cs[j][1] = cs[j][2] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool qok = qi[r] < p.B;
+      const int t = qok ? p.target[qi[r]] : -1;
+      const float lsel = qok ? p.lse[qi[r]] * LOG2E : 0.f, gl = qok ? p.gl[qi[r]] : 0.f;
+      const float X2 = rk[r].x2, Bq = 1.f - c * X2;
+      float rs = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (!qok || ni[j] >= p.N) continue;
+        const float xy = acc[j][r], Y2 = ck[j].y2;
+        float num2, rd, A;
+        const float n2 = pair_n2(xy, rk[r], ck[j], p, &num2, &rd, &A);
+        const float S = fmaf(-p.scale, n2, ck[j].sb);
+        const float G = gl * (__builtin_amdgcn_exp2f(fmaf(S, LOG2E, -lsel)) - (ni[j] == t ? 1.f : 0.f));
+        float gxy = 0.f, gx2 = 0.f, gy2 = 0.f;
+        if (num2 * rd * rd <= mx2) {  // not clamped: dn2/du = dnum2/du / den^2 - 2 num2 dden/du / den^3
+          const float i2 = rd * rd, tt = 2.f * num2 * i2 * rd;
+          gxy = (-4.f * c * A * X2 + 4.f * c * Bq * xy - 2.f * A * Bq) * i2 - tt * m2c;
+          gx2 = (A * A + 2.f * c * A * xy - 2.f * c * Bq * Y2) * i2 - tt * (c * c * Y2);
+          gy2 = (2.f * c * A * X2 - 2.f * c * Bq * xy + Bq * Bq) * i2 - tt * (c * c * X2);
+        }
+        const float Gs = -p.scale * G;
+        p.coef[(int64_t)qi[r] * p.N + ni[j]] = Gs * gxy;
+        rs += Gs * gx2;
+        cs[j][0] += Gs * gy2;
+        cs[j][1] += G;
+        cs[j][2] += G * (p.margin - n2);
+      }
+      rs = group16_sum(rs);
+      if ((lane & 15) == 0 && qok) p.rsum[(int64_t)qi[r] * nblk + bn] = rs;
+    }
+    const int grp = (qi[0] - 4 * (lane >> 4)) >> 4;  // this wave's 16-query group
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        float v = cs[j][k];
+        v += __shfl_xor(v, 16);
+        v += __shfl_xor(v, 32);
+        if (lane < 16 && ni[j] < p.N) p.csum[((int64_t)grp * p.N + ni[j]) * 3 + k] = v;
+      }
+  }
+}
+
 // fp32 scorer without K-chunk barriers.  A workgroup = 8 waves = 128 queries x 64
 // candidates; wave w owns queries [16w, 16w + 16) and all 64 candidates (4 MFMA tiles).
 // k-block order: MFMA sub-step e of 16-deep block b reads k = 16 b + 4 (lane >> 4) + e, so
@@ -336,6 +421,11 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
 constexpr int SQ2 = 128, SW2 = SQ2 / 16, KB_MAX = 16;  // d <= 256
 
 __host__ __device__ inline int score_lds_stride(int d) { return ((d + 15) & ~15) + 8; }
+
+// k_score_f32 grid: 8 XCDs x query tiles x groups of 8 candidate tiles (see the kernel).
+inline unsigned score_f32_grid(int B, int nbn) {
+  return (unsigned)(8L * ((B + SQ2 - 1) / SQ2) * ((nbn + 7) / 8));
+}
 
 template <int MODE>
 __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(4))) void k_score_f32(ScoreArgs p) {
@@ -351,8 +441,13 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(4))) v
   };
   stamp(0);
   const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
-  const int nbn = (p.N + SN - 1) / SN;
-  const int bq = blockIdx.x / nbn, bn = blockIdx.x - bq * nbn;
+  const int nbn = (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
+  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (separate L2s); the nbq
+  // query tiles of one candidate tile run back to back on one XCD, so the tile comes from HBM
+  // once instead of nbq times.  The grid is padded to whole groups of 8 candidate tiles.
+  const int xcd = blockIdx.x & 7, rk = blockIdx.x >> 3;
+  const int bq = rk % nbq, bn = (rk / nbq) * 8 + xcd;
+  if (bn >= nbn) return;  // padding (whole workgroup, before any barrier)
   const int q0 = bq * SQ2, n0 = bn * SN;
   const int g4 = 4 * (lane >> 4);
   const f4 z4 = {0.f, 0.f, 0.f, 0.f};
@@ -364,26 +459,27 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
   for (int b = 0; b < KB_MAX; ++b) a[b] = *reinterpret_cast<const f4*>(qrow + min(16 * b + g4, d - 4));
   // stage the candidate tile in two halves (loads of a half in flight together, then its
-  // LDS writes): half the staging registers, so two workgroups fit a CU
+  // LDS writes): half the staging registers, so two workgroups fit a CU.  Thread tid stages
+  // row tid / 8, float4 units tid % 8 + 8 it (no runtime division in the index math).
   {
-    constexpr int IT = (SN * KB_MAX * 4 + 64 * SW2 - 1) / (64 * SW2), HALF = IT / 2;
-    const int per_row = 4 * KB, n_units = SN * per_row;
+    static_assert(64 * SW2 == 8 * SN, "staging map: 8 threads per candidate row");
+    constexpr int IT = KB_MAX * 4 / 8, HALF = IT / 2;
+    const int r = tid >> 3, sub = tid & 7, per_row = 4 * KB;
+    const bool row_ok = n0 + r < p.N;
+    const float* erow = p.e + (int64_t)min(n0 + r, p.N - 1) * d;
+    float* lrow = Es + r * SE;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       f4 v[HALF];
 #pragma unroll
       for (int it = 0; it < HALF; ++it) {
-        const int u = min(tid + (h * HALF + it) * 64 * SW2, n_units - 1);
-        const int r = u / per_row, k = (u - r * per_row) * 4;
-        v[it] = *reinterpret_cast<const f4*>(p.e + (int64_t)min(n0 + r, p.N - 1) * d + min(k, d - 4));
+        const int k = (sub + 8 * (h * HALF + it)) * 4;
+        v[it] = *reinterpret_cast<const f4*>(erow + min(k, d - 4));
       }
 #pragma unroll
       for (int it = 0; it < HALF; ++it) {
-        const int u = tid + (h * HALF + it) * 64 * SW2;
-        if (u < n_units) {
-          const int r = u / per_row, k = (u - r * per_row) * 4;
-          *reinterpret_cast<f4*>(Es + r * SE + k) = (n0 + r < p.N && k < d) ? v[it] : z4;
-        }
+        const int u = sub + 8 * (h * HALF + it);
+        if (u < per_row) *reinterpret_cast<f4*>(lrow + 4 * u) = (row_ok && 4 * u < d) ? v[it] : z4;
       }
     }
   }
@@ -416,7 +512,7 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(4))) v
     ys[j] += __shfl_xor(ys[j], 16);
     ys[j] += __shfl_xor(ys[j], 32);
   }
-  float x2[4], cr[4] = {0.f, 0.f, 0.f, 0.f}, y2[4], bn_[4];
+  float x2[4], y2[4], bn_[4];
   int qi[4], ni[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -430,7 +526,7 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(4))) v
     y2[j] = ys[j];
     bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
   }
-  score_epilogue<MODE, float>(p, acc, x2, y2, bn_, cr, qi, ni, lane, bn);
+  score_epilogue_fast<MODE>(p, acc, x2, y2, bn_, qi, ni, lane, bn);
   stamp(2);
 }
 
@@ -502,7 +598,7 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   dim3 g((unsigned)blocks), b(256);
   // fp32 proxy / distance scores (no per-query curvature, d <= 256): the barrier-free kernel
   const bool fast = !a.use_dist && a.d <= 16 * KB_MAX;
-  const dim3 g2((unsigned)(((long)(a.B + SQ2 - 1) / SQ2) * nbn)), b2(64 * SW2);
+  const dim3 g2(score_f32_grid(a.B, nbn)), b2(64 * SW2);
   const size_t lds2 = (size_t)SN * score_lds_stride(a.d) * 4;
   if (mode == 0) {
     if (!a.out) return set_error(REGCN_EINVAL, "null output");
@@ -531,7 +627,7 @@ int score_ce_bwd(ScoreArgs& a, hipStream_t st) {
   if (a.B == 0 || a.N == 0) return 0;
   a.trace = nullptr;
   const int nbn = (a.N + SN - 1) / SN;
-  const dim3 g2((unsigned)(((long)(a.B + SQ2 - 1) / SQ2) * nbn)), b2(64 * SW2);
+  const dim3 g2(score_f32_grid(a.B, nbn)), b2(64 * SW2);
   const size_t lds2 = (size_t)SN * score_lds_stride(a.d) * 4;
   hipLaunchKernelGGL((k_score_f32<2>), g2, b2, lds2, st, a);
   return check_launch("k_score_ce_bwd");
