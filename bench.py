@@ -215,6 +215,22 @@ def kernel_profile(model, sample, d, device):
     return res
 
 
+def decoder_at_scale():
+    """Config-5 decoder: all-entity scoring of B = 1024 queries against
+    N = 1M candidates at d = 200, MFMA-bound; flops 2 B N d per launch over the HIP-event
+    launch time against the dense fp32 MFMA peak (tools/scorebench.py)."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    from scorebench import measure
+    r = measure(1024, 1_000_000, 200, reps=3, modes="score,ce", verbose=False)
+    torch.cuda.empty_cache()
+    return {"bound": "mfma", "unit": "TFLOP/s", "peak": FP32_MFMA_PEAK_TFLOPS,
+            "config": "B=1024 queries x N=1000000 candidates, d=200", "flops_per_launch": r["flops_per_launch"],
+            "score": {"achieved": r["score"]["tflops"], "frac": r["score"]["frac"], "avg_launch_us":
+                      round(r["score"]["ms"] * 1e3, 1), "kernel": "k_score_f32<0>"},
+            "cross_entropy": {"achieved": r["ce"]["tflops"], "frac": r["ce"]["frac"], "avg_launch_us":
+                              round(r["ce"]["ms"] * 1e3, 1), "kernel": "k_score_f32<1>"}}
+
+
 def aggregation_at_scale(device):
     """North-star roofline check: the d=200 union and Lorentz
     aggregations over one |V|=1M, |E|=50M synthetic snapshot (Zipf destinations), timed
@@ -378,9 +394,10 @@ def main():
         kernels = {k: dict(avg_us=round(v["ms"] * 1e3, 3), per_step=v["per_step"], bound=v["bound"],
                            achieved=round(v["achieved"], 3), unit=v["unit"], frac=round(v["frac"], 4))
                    for k, v in kern.items()}
-        scale = None
+        scale = dec = None
         if not args.no_scale and world == 1:
             scale = aggregation_at_scale(device)
+            dec = decoder_at_scale()
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(cfg, d, model, samples[0], args.cpu_budget)
@@ -395,7 +412,8 @@ def main():
                           "hip_graph": bool(graphs), "steps_per_graph_launch": len(samples) if pool_graph else 1,
                           "parallelism": ("%s-partitioned snapshots x%d" % (args.shard, world)) if sharded
                           else "replicas x%d" % world},
-               "roofline": roof, "kernels": kernels, "aggregation_roofline": scale, "cpu_baseline": cpu}
+               "roofline": roof, "kernels": kernels, "aggregation_roofline": scale,
+               "decoder_roofline": dec, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -15,6 +15,8 @@
 // candidates as four 16x16 v_mfma_f32_16x16x4_f32 accumulators; K streamed through
 // LDS in 16-deep chunks.  Epilogues: write S (score), or per-tile (max, sum exp)
 // partials + target logit for a fused cross entropy (never materialising B x N).
+#include <algorithm>
+
 #include "common.h"
 #include "regcn_internal.h"
 
@@ -410,26 +412,35 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
   }
 }
 
-// fp32 scorer without K-chunk barriers.  A workgroup = 8 waves = 128 queries x 64
-// candidates; wave w owns queries [16w, 16w + 16) and all 64 candidates (4 MFMA tiles).
-// k-block order: MFMA sub-step e of 16-deep block b reads k = 16 b + 4 (lane >> 4) + e, so
-// a lane's operands for a whole block are one contiguous float4: the wave's query rows live
-// in registers for the whole K (one dwordx4 per block, loaded at entry), the candidate tile
-// is staged in LDS once (row stride = 8 mod 16: conflict-free ds_read_b128) behind a single
-// barrier, and the MFMA loop runs with no further synchronisation.  |q|^2 and |e|^2 come
-// from the same operand registers.
+// fp32 scorer, persistent and double-buffered.  A workgroup = 8 waves = 128 queries; wave w
+// owns queries [16w, 16w + 16), their rows in registers for the whole K.  The workgroup walks
+// a strip of 64-candidate tiles: while tile i is multiplied out of one LDS buffer, tile i + 1
+// is loaded into registers (issued before the MFMA loop, unconditionally) and written to the
+// other buffer after the epilogue, behind the one barrier per tile.  k-block operand order:
+// MFMA sub-step e of 16-deep block b reads k = 16 b + 4 (lane >> 4) + e, so a lane's operands
+// for a block are one float4 (row stride = 8 mod 16: conflict-free ds_read_b128).
+//
+// Work order (XCD-aware): workgroups are dealt round-robin to the 8 XCDs; workgroup w sits on
+// XCD x = w % 8, takes query tile (w / 8) % nbq and stripe k = w / (8 nbq), and walks the
+// candidate tiles x + 8 (k + S i), S = stripes per XCD.  The nbq workgroups of one stripe walk
+// the same tiles in step, so a tile comes from HBM into its XCD's L2 once.
 constexpr int SQ2 = 128, SW2 = SQ2 / 16, KB_MAX = 16;  // d <= 256
 
 __host__ __device__ inline int score_lds_stride(int d) { return ((d + 15) & ~15) + 8; }
 
-// k_score_f32 grid: 8 XCDs x query tiles x groups of 8 candidate tiles (see the kernel).
-inline unsigned score_f32_grid(int B, int nbn) {
-  return (unsigned)(8L * ((B + SQ2 - 1) / SQ2) * ((nbn + 7) / 8));
+// grid = 8 XCDs x query tiles x stripes (about one workgroup per CU when B is small).
+inline int score_f32_stripes(int B, int nbn) {
+  const int nbq = (B + SQ2 - 1) / SQ2;
+  return std::max(1, std::min(32 / nbq, (nbn + 7) / 8));
 }
+inline unsigned score_f32_grid(int B, int nbn) {
+  return (unsigned)(8L * ((B + SQ2 - 1) / SQ2) * score_f32_stripes(B, nbn));
+}
+inline size_t score_f32_lds(int d) { return (size_t)2 * SN * (score_lds_stride(d) + 1) * 4; }
 
 template <int MODE>
-__global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(4))) void k_score_f32(ScoreArgs p) {
-  extern __shared__ float Es[];  // SN x SE candidate rows, zero past N and d
+__global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32(ScoreArgs p) {
+  extern __shared__ float Es[];  // 2 x SN x SE candidate rows, zero past N and d
   p.scale = p.scale_p ? *p.scale_p : 1.f;
   if (p.scale_raw && p.scale_p)  // softplus(raw) + 1e-6 (hyperbolic_decoder.py:717; torch threshold 20)
     p.scale = (p.scale > 20.f ? p.scale : log1pf(expf(p.scale))) + 1e-6f;
@@ -442,13 +453,13 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(4))) v
   stamp(0);
   const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
   const int nbn = (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
-  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (separate L2s); the nbq
-  // query tiles of one candidate tile run back to back on one XCD, so the tile comes from HBM
-  // once instead of nbq times.  The grid is padded to whole groups of 8 candidate tiles.
+  const int S = gridDim.x / (8 * nbq);
   const int xcd = blockIdx.x & 7, rk = blockIdx.x >> 3;
-  const int bq = rk % nbq, bn = (rk / nbq) * 8 + xcd;
-  if (bn >= nbn) return;  // padding (whole workgroup, before any barrier)
-  const int q0 = bq * SQ2, n0 = bn * SN;
+  const int bq = rk % nbq, stripe = rk / nbq;
+  auto tile_of = [&](int i) { return xcd + 8 * (stripe + S * i); };
+  int bn = tile_of(0);
+  if (bn >= nbn) return;  // no work for this stripe (whole workgroup, before any barrier)
+  const int q0 = bq * SQ2;
   const int g4 = 4 * (lane >> 4);
   const f4 z4 = {0.f, 0.f, 0.f, 0.f};
   // this wave's query rows, all k-blocks (unconditional clamped loads; masked at use)
@@ -456,77 +467,101 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(4))) v
   const bool q_ok = qr < p.B;
   const float* qrow = p.q + (int64_t)min(qr, p.B - 1) * d;
   f4 a[KB_MAX];
-#pragma unroll
-  for (int b = 0; b < KB_MAX; ++b) a[b] = *reinterpret_cast<const f4*>(qrow + min(16 * b + g4, d - 4));
-  // stage the candidate tile in two halves (loads of a half in flight together, then its
-  // LDS writes): half the staging registers, so two workgroups fit a CU.  Thread tid stages
-  // row tid / 8, float4 units tid % 8 + 8 it (no runtime division in the index math).
-  {
-    static_assert(64 * SW2 == 8 * SN, "staging map: 8 threads per candidate row");
-    constexpr int IT = KB_MAX * 4 / 8, HALF = IT / 2;
-    const int r = tid >> 3, sub = tid & 7, per_row = 4 * KB;
-    const bool row_ok = n0 + r < p.N;
-    const float* erow = p.e + (int64_t)min(n0 + r, p.N - 1) * d;
-    float* lrow = Es + r * SE;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      f4 v[HALF];
-#pragma unroll
-      for (int it = 0; it < HALF; ++it) {
-        const int k = (sub + 8 * (h * HALF + it)) * 4;
-        v[it] = *reinterpret_cast<const f4*>(erow + min(k, d - 4));
-      }
-#pragma unroll
-      for (int it = 0; it < HALF; ++it) {
-        const int u = sub + 8 * (h * HALF + it);
-        if (u < per_row) *reinterpret_cast<f4*>(lrow + 4 * u) = (row_ok && 4 * u < d) ? v[it] : z4;
-      }
-    }
-  }
-  __syncthreads();
-  stamp(1);
-  f4 acc[4] = {z4, z4, z4, z4};
-  float xs = 0.f, ys[4] = {0.f, 0.f, 0.f, 0.f};
-  const float* brow = Es + (lane & 15) * SE + g4;
+  float xs = 0.f;
 #pragma unroll
   for (int b = 0; b < KB_MAX; ++b) {
-    if (b < KB) {  // wave-uniform
-      f4 bv[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bv[j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE + 16 * b);
-      const f4 av = (q_ok && 16 * b + g4 < d) ? a[b] : z4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[e], bv[j][e], acc[j], 0, 0, 0);
-      xs += dot4(av, av);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ys[j] += dot4(bv[j], bv[j]);
-    }
+    const f4 v = *reinterpret_cast<const f4*>(qrow + min(16 * b + g4, d - 4));
+    a[b] = (q_ok && b < KB && 16 * b + g4 < d) ? v : z4;
+    xs += dot4(a[b], a[b]);
   }
-  // |q|^2 of query (lane & 15), |e|^2 of candidate 16 j + (lane & 15): sum the 4 k-quarters
+  // |q|^2 of query (lane & 15): sum the 4 k-quarters; the C rows of this lane
   xs += __shfl_xor(xs, 16);
   xs += __shfl_xor(xs, 32);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    ys[j] += __shfl_xor(ys[j], 16);
-    ys[j] += __shfl_xor(ys[j], 32);
-  }
-  float x2[4], y2[4], bn_[4];
-  int qi[4], ni[4];
+  float x2[4];
+  int qi[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int li = 4 * (lane >> 4) + r;  // C row of this lane = query 16 wv + li
     x2[r] = __shfl(xs, li);
     qi[r] = q0 + 16 * wv + li;
   }
+  // staging map: thread tid stages candidate row tid / 8, float4 units tid % 8 + 8 it
+  static_assert(64 * SW2 == 8 * SN, "staging map: 8 threads per candidate row");
+  constexpr int IT = KB_MAX * 4 / 8;
+  const int sr = tid >> 3, sub = tid & 7, per_row = 4 * KB;
+  f4 v[IT];
+  auto fetch = [&](int t) {  // unconditional clamped loads (a conditional load drains vmcnt)
+    const float* erow = p.e + (int64_t)min(t * SN + sr, p.N - 1) * d;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    ni[j] = n0 + 16 * j + (lane & 15);
-    y2[j] = ys[j];
-    bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
+    for (int it = 0; it < IT; ++it) v[it] = *reinterpret_cast<const f4*>(erow + min((sub + 8 * it) * 4, d - 4));
+  };
+  // |e|^2 of each staged row, summed over its 8 staging lanes (xor 1, 2, 4), next to the tile
+  float* e2s = Es + 2 * SN * SE;  // [2][SN]
+  auto stash = [&](int buf, int t) {
+    const bool row_ok = t * SN + sr < p.N;
+    float* lrow = Es + buf * SN * SE + sr * SE;
+    float ss = 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int u = sub + 8 * it;
+      const f4 w = (row_ok && 4 * u < d) ? v[it] : z4;
+      ss += dot4(w, w);
+      if (u < per_row) *reinterpret_cast<f4*>(lrow + 4 * u) = w;
+    }
+    ss += __shfl_xor(ss, 1);
+    ss += __shfl_xor(ss, 2);
+    ss += __shfl_xor(ss, 4);
+    if (sub == 0) e2s[buf * SN + sr] = ss;
+  };
+  fetch(bn);
+  stash(0, bn);
+  __syncthreads();
+  stamp(1);
+  int cur = 0;
+  for (int i = 0;; ++i) {
+    const int bn_next = tile_of(i + 1);
+    const bool more = bn_next < nbn;  // workgroup-uniform
+    // next tile's rows in flight under this tile's MFMAs (MODE 2: after its epilogue, whose
+    // live registers would otherwise spill)
+    if (MODE != 2) fetch(min(bn_next, nbn - 1));
+    const int n0 = bn * SN;
+    const float* brow = Es + cur * SN * SE + (lane & 15) * SE + g4;
+    f4 acc[4] = {z4, z4, z4, z4};
+    // B fragments of block b + 1 are read while block b's MFMAs run (register double buffer;
+    // the read past the last block is clamped, never used)
+    f4 bb[2][4];  // ping-pong by block parity (static after unrolling: no copies)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bb[0][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE);
+#pragma unroll
+    for (int b = 0; b < KB_MAX; ++b) {
+      if (b < KB) {  // wave-uniform
+        const int bnx = min(b + 1, KB - 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bb[(b + 1) & 1][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE + 16 * bnx);
+        __builtin_amdgcn_sched_barrier(0);  // keep block b + 1's reads ahead of block b's MFMAs
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[b][e], bb[b & 1][j][e], acc[j], 0, 0, 0);
+      }
+    }
+    float y2[4], bn_[4];
+    int ni[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ni[j] = n0 + 16 * j + (lane & 15);
+      y2[j] = e2s[cur * SN + 16 * j + (lane & 15)];
+      bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
+    }
+    score_epilogue_fast<MODE>(p, acc, x2, y2, bn_, qi, ni, lane, bn);
+    if (!more) break;
+    if (MODE == 2) fetch(bn_next);
+    stash(cur ^ 1, bn_next);  // that buffer's readers passed the last barrier
+    __syncthreads();
+    cur ^= 1;
+    bn = bn_next;
   }
-  score_epilogue_fast<MODE>(p, acc, x2, y2, bn_, qi, ni, lane, bn);
   stamp(2);
 }
 
@@ -599,7 +634,7 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   // fp32 proxy / distance scores (no per-query curvature, d <= 256): the barrier-free kernel
   const bool fast = !a.use_dist && a.d <= 16 * KB_MAX;
   const dim3 g2(score_f32_grid(a.B, nbn)), b2(64 * SW2);
-  const size_t lds2 = (size_t)SN * score_lds_stride(a.d) * 4;
+  const size_t lds2 = score_f32_lds(a.d);
   if (mode == 0) {
     if (!a.out) return set_error(REGCN_EINVAL, "null output");
     if (fast) hipLaunchKernelGGL((k_score_f32<0>), g2, b2, lds2, st, a);
@@ -628,7 +663,7 @@ int score_ce_bwd(ScoreArgs& a, hipStream_t st) {
   a.trace = nullptr;
   const int nbn = (a.N + SN - 1) / SN;
   const dim3 g2(score_f32_grid(a.B, nbn)), b2(64 * SW2);
-  const size_t lds2 = (size_t)SN * score_lds_stride(a.d) * 4;
+  const size_t lds2 = score_f32_lds(a.d);
   hipLaunchKernelGGL((k_score_f32<2>), g2, b2, lds2, st, a);
   return check_launch("k_score_ce_bwd");
 }

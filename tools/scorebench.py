@@ -20,18 +20,11 @@ sys.path.insert(0, os.path.join(REPO, "re-gcn_amd"))
 PEAK = 157.3
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--B", type=int, default=1024)
-    ap.add_argument("--N", type=int, default=1_000_000)
-    ap.add_argument("--d", type=int, default=200)
-    ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--modes", default="score,ce,ce_bwd")
-    a = ap.parse_args()
+def measure(B=1024, N=1_000_000, d=200, reps=5, modes="score,ce,ce_bwd", verbose=True):
+    """HIP-event time per launch of each scorer mode at (B, N, d); returns a dict."""
     from regcn_amd import _lib
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
-    B, N, d = a.B, a.N, a.d
 
     def ball(n):
         x = torch.randn(n, d, device=dev, generator=g)
@@ -45,13 +38,13 @@ def main():
     f = _lib.fptr
     flops = 2.0 * B * N * d
     out = {"B": B, "N": N, "d": d, "flops_per_launch": flops, "peak_tflops": PEAK}
-    S = torch.empty(B, N, device=dev) if "score" in a.modes else None
+    S = torch.empty(B, N, device=dev) if "score" in modes else None
     ws = torch.empty((_lib.lib().regcn_hyp_ce_workspace_bytes(B, N) + 3) // 4, device=dev)
     loss = torch.empty(B, device=dev)
     lse = torch.empty(B, device=dev)
     nblk, ng = (N + 63) // 64, 8 * ((B + 127) // 128)
     coef = rsum = csum = None
-    if "ce_bwd" in a.modes:
+    if "ce_bwd" in modes:
         coef = torch.empty(B, N, device=dev)
         rsum = torch.empty(B, nblk, device=dev)
         csum = torch.zeros(ng, N, 3, device=dev)
@@ -64,24 +57,36 @@ def main():
         "ce_bwd": lambda: _lib.call("regcn_hyp_ce_bwd_f32", f(q), f(e), f(bias), f(scale), f(margin), _lib.iptr(tgt),
                                     f(lse), f(gl), B, N, d, 0.01, 0, f(coef), f(rsum), f(csum), _lib.stream()),
     }
-    if "ce_bwd" in a.modes:
+    if "ce_bwd" in modes:
         runs["ce"]()
-    for mode in a.modes.split(","):
+    for mode in modes.split(","):
         fn = runs[mode]
         fn()
         torch.cuda.synchronize()
         st = torch.cuda.current_stream()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(st)
-        for _ in range(a.reps):
+        for _ in range(reps):
             fn()
         e1.record(st)
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / a.reps
+        ms = e0.elapsed_time(e1) / reps
         tf = flops / (ms * 1e-3) / 1e12
         out[mode] = {"ms": round(ms, 3), "tflops": round(tf, 2), "frac": round(tf / PEAK, 4)}
-        print(json.dumps({mode: out[mode]}), file=sys.stderr, flush=True)
-    print(json.dumps(out), flush=True)
+        if verbose:
+            print(json.dumps({mode: out[mode]}), file=sys.stderr, flush=True)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=1024)
+    ap.add_argument("--N", type=int, default=1_000_000)
+    ap.add_argument("--d", type=int, default=200)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--modes", default="score,ce,ce_bwd")
+    a = ap.parse_args()
+    print(json.dumps(measure(a.B, a.N, a.d, a.reps, a.modes)), flush=True)
 
 
 if __name__ == "__main__":
