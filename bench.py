@@ -201,7 +201,7 @@ def kernel_profile(model, sample, d, device):
         if type(dec).__name__ == "HyperbolicRotH":
             stages.append(("k_query<0>", lambda: dec._query(emb, h0, at), 1, 2.0 * B * 3.5 * d * d,
                            4.0 * B * d * 3))
-        stages.append(("k_score<0, false>", lambda: _chunked_hyperbolic_dist_score(
+        stages.append(("k_score_f32<0>", lambda: _chunked_hyperbolic_dist_score(
             q, emb, dec.entity_bias, dec.c, 128, 256, score_scale=dec.score_scale_raw,
             score_margin=dec.score_margin, _raw_scale=True), 1, 2.0 * B * V * d, 4.0 * (B * d + V * d + B * V)))
         if type(rdec).__name__ == "HyperbolicRotHRel":

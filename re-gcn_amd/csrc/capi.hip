@@ -317,8 +317,7 @@ int regcn_hyp_score_f32(const float* q, const float* cand, const float* bias, co
 }
 
 size_t regcn_hyp_ce_workspace_bytes(int32_t B, int32_t N) {
-  const size_t nblk = ((size_t)N + 63) / 64;
-  return ((size_t)B * nblk * 2 + (size_t)B) * sizeof(float);
+  return ((size_t)B * ce_partial_slots(N) * 2 + (size_t)B) * sizeof(float);
 }
 
 int regcn_hyp_ce_f32(const float* q, const float* cand, const float* bias, const float* c_rel, const float* scale, const float* margin,
@@ -327,7 +326,7 @@ int regcn_hyp_ce_f32(const float* q, const float* cand, const float* bias, const
   if (c_rel && !(use_dist & 1)) return set_error(REGCN_EINVAL, "per-query curvature requires use_dist");
   if (!workspace) return set_error(REGCN_EINVAL, "null workspace");
   ScoreArgs a = score_args(q, cand, bias, c_rel, scale, margin, B, N, d, c, use_dist);
-  const size_t nblk = ((size_t)N + 63) / 64;
+  const size_t nblk = ce_partial_slots(N);
   a.target = target;
   a.part = (float*)workspace;
   a.tgt_logit = a.part + (size_t)B * nblk * 2;
@@ -351,7 +350,7 @@ int regcn_hyp_ce_lse_f32(const float* q, const float* cand, const float* bias, c
                          int32_t flags, void* workspace, float* loss_per_query, float* lse, void* s) {
   if (!workspace) return set_error(REGCN_EINVAL, "null workspace");
   ScoreArgs a = score_args(q, cand, bias, nullptr, scale, margin, B, N, d, c, flags);
-  const size_t nblk = ((size_t)N + 63) / 64;
+  const size_t nblk = ce_partial_slots(N);
   a.target = target;
   a.part = (float*)workspace;
   a.tgt_logit = a.part + (size_t)B * nblk * 2;

@@ -1,5 +1,6 @@
 // Host-side internals shared by the kernel translation units (not part of the C-ABI).
 #pragma once
+#include <algorithm>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -189,6 +190,9 @@ int pack_weight(const float* W, int d_in, int d_out, float* Wp, hipStream_t st);
 int layer(const LayerArgs& a, hipStream_t st);
 int timestep(const StepArgs& a, hipStream_t st);
 int score(ScoreArgs& a, int mode, float* loss, hipStream_t st);
+// CE partial (max, sum exp) slots per query: one per candidate tile (generic kernel) or one per
+// workgroup of the query's tile (persistent fp32 kernel, <= 8 x 32).
+inline size_t ce_partial_slots(int N) { return std::max<size_t>(((size_t)N + 63) / 64, 256); }
 int score_ce_bwd(ScoreArgs& a, hipStream_t st);
 int rank(const float* S, int B, int N, const int* target, const int* filt_ptr, const int* filt_idx, int* rank_raw,
          int* rank_filt, hipStream_t st);

@@ -318,7 +318,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 template <int MODE>
 __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4* acc, const float* x2,
                                                     const float* y2, const float* bn_, const int* qi, const int* ni,
-                                                    int lane, int bn) {
+                                                    int lane, int bn, float* run_m, float* run_se) {
   RowK rk[4];
   ColK ck[4];
 #pragma unroll
@@ -336,30 +336,25 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
           p.out[(int64_t)qi[r] * p.N + ni[j]] =
               fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb);
     }
-  } else if (MODE == 1) {
-    const int nblk = (p.N + SN - 1) / SN;
+  } else if (MODE == 1) {  // this lane's running (max, sum exp) per query row, across tiles
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float s[4], m = -INFINITY;
+      float sv[4], m = -INFINITY;
       const int t = qi[r] < p.B ? p.target[qi[r]] : -1;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        s[j] = ni[j] < p.N ? fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb)
-                           : -INFINITY;
-        m = fmaxf(m, s[j]);
-        if (ni[j] == t) p.tgt_logit[qi[r]] = s[j];
+        sv[j] = ni[j] < p.N ? fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb)
+                            : -INFINITY;
+        m = fmaxf(m, sv[j]);
+        if (ni[j] == t) p.tgt_logit[qi[r]] = sv[j];
       }
-      m = row16_max(m);
-      const float ml = m * LOG2E;
-      float se = 0.f;
+      const float mn = fmaxf(run_m[r], m);
+      const float ml = (mn == -INFINITY ? 0.f : mn) * LOG2E;  // exp2(-inf) = 0 for empty lanes
+      float se = run_se[r] * __builtin_amdgcn_exp2f(fmaf(run_m[r], LOG2E, -ml));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) se += __builtin_amdgcn_exp2f(fmaf(s[j], LOG2E, -ml));  // exp(-inf) = 0
-      se = row16_sum(se);
-      if ((lane & 15) == 0 && qi[r] < p.B) {
-        float* o = p.part + ((int64_t)qi[r] * nblk + bn) * 2;
-        o[0] = m;
-        o[1] = se;
-      }
+      for (int j = 0; j < 4; ++j) se += __builtin_amdgcn_exp2f(fmaf(sv[j], LOG2E, -ml));
+      run_m[r] = mn;
+      run_se[r] = se;
     }
   } else {  // MODE 2: CE backward coefficients
     const int nblk = (p.N + SN - 1) / SN;
@@ -458,9 +453,30 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) v
   const int bq = rk % nbq, stripe = rk / nbq;
   auto tile_of = [&](int i) { return xcd + 8 * (stripe + S * i); };
   int bn = tile_of(0);
-  if (bn >= nbn) return;  // no work for this stripe (whole workgroup, before any barrier)
   const int q0 = bq * SQ2;
   const int g4 = 4 * (lane >> 4);
+  // cross entropy: per-lane running (max, sum exp) over every tile of the strip, reduced over the
+  // 16 lanes of each query row and written once, as partial xcd + 8 stripe of the query
+  float run_m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, run_se[4] = {0.f, 0.f, 0.f, 0.f};
+  auto ce_flush = [&]() {
+    const int np = 8 * S, pidx = xcd + 8 * stripe;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + 16 * wv + 4 * (lane >> 4) + r;
+      const float M = row16_max(run_m[r]);
+      const float Ml = (M == -INFINITY ? 0.f : M) * LOG2E;
+      const float se = row16_sum(run_se[r] * __builtin_amdgcn_exp2f(fmaf(run_m[r], LOG2E, -Ml)));
+      if ((lane & 15) == 0 && q < p.B) {
+        float* o = p.part + ((int64_t)q * np + pidx) * 2;
+        o[0] = M;
+        o[1] = se;
+      }
+    }
+  };
+  if (bn >= nbn) {  // no work for this stripe (whole workgroup, before any barrier)
+    if (MODE == 1) ce_flush();
+    return;
+  }
   const f4 z4 = {0.f, 0.f, 0.f, 0.f};
   // this wave's query rows, all k-blocks (unconditional clamped loads; masked at use)
   const int qr = q0 + 16 * wv + (lane & 15);
@@ -554,7 +570,7 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) v
       y2[j] = e2s[cur * SN + 16 * j + (lane & 15)];
       bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
     }
-    score_epilogue_fast<MODE>(p, acc, x2, y2, bn_, qi, ni, lane, bn);
+    score_epilogue_fast<MODE>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se);
     if (!more) break;
     if (MODE == 2) fetch(bn_next);
     stash(cur ^ 1, bn_next);  // that buffer's readers passed the last barrier
@@ -562,6 +578,7 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) v
     cur ^= 1;
     bn = bn_next;
   }
+  if (MODE == 1) ce_flush();
   stamp(2);
 }
 
@@ -648,7 +665,8 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   else hipLaunchKernelGGL((k_score<1, false>), g, b, 0, st, a);
   int rc = check_launch("k_score_ce");
   if (rc) return rc;
-  hipLaunchKernelGGL(k_ce_combine, dim3((a.B + 3) / 4), b, 0, st, a.part, a.tgt_logit, a.B, nbn, loss, a.lse_out);
+  const int nparts = fast ? 8 * score_f32_stripes(a.B, nbn) : nbn;  // <= ce_partial_slots(N)
+  hipLaunchKernelGGL(k_ce_combine, dim3((a.B + 3) / 4), b, 0, st, a.part, a.tgt_logit, a.B, nparts, loss, a.lse_out);
   return check_launch("k_ce_combine");
 }
 
