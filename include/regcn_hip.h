@@ -270,6 +270,12 @@ int regcn_hyp_ce_f32(const float* q, const float* cand, const float* bias, const
  * true answers (filt_ptr [B+1], filt_idx; NULL filt_ptr skips the filtered rank). */
 int regcn_rank_f32(const float* score, int32_t B, int32_t N, const int32_t* target, const int32_t* filt_ptr,
                    const int32_t* filt_idx, int32_t* rank_raw, int32_t* rank_filt, void* stream);
+/* e: candidate-sharded ranking (SURVEY.md §8(e) decoder).  On a rank's slice of the
+ * candidates: #{n : score[b,n] > threshold[b]} (raw) and the same excluding the slice-local
+ * CSR list of other true answers; summing the counts over the ranks and adding 1 gives
+ * regcn_rank_f32's ranks, threshold = the target's score. */
+int regcn_rank_count_f32(const float* score, int32_t B, int32_t N, const float* threshold, const int32_t* filt_ptr,
+                         const int32_t* filt_idx, int32_t* count_raw, int32_t* count_filt, void* stream);
 
 /* ---- a1 / f3: snapshot construction on the device ------------------------------------
  * build_sub_graph + r2e (rgcn/utils.py:78-134) and the kernel work lists of

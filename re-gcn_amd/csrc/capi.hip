@@ -335,7 +335,12 @@ int regcn_hyp_ce_f32(const float* q, const float* cand, const float* bias, const
 
 int regcn_rank_f32(const float* score_m, int32_t B, int32_t N, const int32_t* target, const int32_t* filt_ptr,
                    const int32_t* filt_idx, int32_t* rank_raw, int32_t* rank_filt, void* s) {
-  return rank(score_m, B, N, target, filt_ptr, filt_idx, rank_raw, rank_filt, ST(s));
+  return rank(score_m, B, N, target, nullptr, filt_ptr, filt_idx, 1, rank_raw, rank_filt, ST(s));
+}
+int regcn_rank_count_f32(const float* score_m, int32_t B, int32_t N, const float* threshold, const int32_t* filt_ptr,
+                         const int32_t* filt_idx, int32_t* count_raw, int32_t* count_filt, void* s) {
+  if (!threshold) return set_error(REGCN_EINVAL, "null threshold");
+  return rank(score_m, B, N, nullptr, threshold, filt_ptr, filt_idx, 0, count_raw, count_filt, ST(s));
 }
 
 size_t regcn_snapshot_workspace_bytes(int64_t T, int32_t V, int32_t R) { return snapshot_ws_bytes(T, V, R); }

@@ -608,13 +608,14 @@ __global__ __launch_bounds__(256) void k_ce_combine(const float* __restrict__ pa
 // filter, rgcn/utils.py:51-75 sets them to -1e7).  filt_ptr/filt_idx: CSR of the
 // entities to exclude per query (target itself excluded by the host).
 __global__ __launch_bounds__(256) void k_rank(const float* __restrict__ S, int B, int N, const int* __restrict__ target,
-                                              const int* __restrict__ filt_ptr, const int* __restrict__ filt_idx,
-                                              int* __restrict__ rank_raw, int* __restrict__ rank_filt) {
+                                              const float* __restrict__ ts_in, const int* __restrict__ filt_ptr,
+                                              const int* __restrict__ filt_idx, int add, int* __restrict__ rank_raw,
+                                              int* __restrict__ rank_filt) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
   const float* row = S + (int64_t)b * N;
-  const float ts = row[target[b]];
+  const float ts = ts_in ? ts_in[b] : row[target[b]];
   int cnt = 0;
   for (int n = lane * 4; n < N; n += 256) {
     if (n + 3 < N && ((reinterpret_cast<uintptr_t>(row + n) & 15) == 0)) {
@@ -634,8 +635,8 @@ __global__ __launch_bounds__(256) void k_rank(const float* __restrict__ S, int B
     f += __shfl_xor(f, o);
   }
   if (lane == 0) {
-    rank_raw[b] = cnt + 1;
-    if (rank_filt) rank_filt[b] = cnt - f + 1;
+    rank_raw[b] = cnt + add;
+    if (rank_filt) rank_filt[b] = cnt - f + add;
   }
 }
 
@@ -686,12 +687,12 @@ int score_ce_bwd(ScoreArgs& a, hipStream_t st) {
   return check_launch("k_score_ce_bwd");
 }
 
-int rank(const float* S, int B, int N, const int* target, const int* filt_ptr, const int* filt_idx, int* rank_raw,
-         int* rank_filt, hipStream_t st) {
-  if (!S || !target || !rank_raw) return set_error(REGCN_EINVAL, "null pointer");
+int rank(const float* S, int B, int N, const int* target, const float* ts, const int* filt_ptr, const int* filt_idx,
+         int add, int* rank_raw, int* rank_filt, hipStream_t st) {
+  if (!S || (!target && !ts) || !rank_raw) return set_error(REGCN_EINVAL, "null pointer");
   if (B == 0) return 0;
-  hipLaunchKernelGGL(k_rank, dim3((B + 3) / 4), dim3(256), 0, st, S, B, N, target, filt_ptr, filt_idx, rank_raw,
-                     rank_filt);
+  hipLaunchKernelGGL(k_rank, dim3((B + 3) / 4), dim3(256), 0, st, S, B, N, target, ts, filt_ptr, filt_idx, add,
+                     rank_raw, rank_filt);
   return check_launch("k_rank");
 }
 

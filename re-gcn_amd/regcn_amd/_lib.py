@@ -49,6 +49,7 @@ _SIGS = {
     "regcn_hyp_ce_workspace_bytes": [_c_int, _c_int],
     "regcn_hyp_ce_f32": [P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P, P],
     "regcn_rank_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
+    "regcn_rank_count_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
     "regcn_layer_f32": [P, P],
     "regcn_partial_sum_f32": [P, _c_int, P, _c_int, _c_int, P, _c_int, P],
     "regcn_packed_linear_floats": [_c_int, _c_int, _c_int],

@@ -212,3 +212,116 @@ class ShardedGraph:
         for t in (h, xn, rn):
             allgather_rows(t, per, self.group)
         return h[:V], xn[:V], rn[:V]
+
+
+# ------------------------------------------------------------------- sharded decoder
+def combine_lse(lse_local, group=None):
+    """log-sum-exp over the ranks' candidate slices of each query's per-slice lse (B floats:
+    one all_gather, SURVEY.md §8(e) decoder)."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return lse_local
+    parts = [torch.empty_like(lse_local) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(parts, lse_local.contiguous(), group=group)
+    return torch.logsumexp(torch.stack(parts), dim=0)
+
+
+def combine_counts(counts, group=None):
+    """Sum of the ranks' count-greater per query (B ints: one all_reduce)."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM, group=group)
+    return counts
+
+
+def shard_filters(filt_ptr, filt_idx, n0, n1):
+    """The slice-local part [n0, n1) of a CSR list of candidate ids (shifted by -n0)."""
+    ptr = np.asarray(filt_ptr, dtype=np.int64)
+    idx = np.asarray(filt_idx, dtype=np.int64)
+    keep = (idx >= n0) & (idx < n1)
+    row = np.repeat(np.arange(len(ptr) - 1), np.diff(ptr))
+    cnt = np.bincount(row[keep], minlength=len(ptr) - 1)
+    new_ptr = np.zeros(len(ptr), dtype=np.int32)
+    np.cumsum(cnt, out=new_ptr[1:])
+    return new_ptr, (idx[keep] - n0).astype(np.int32)
+
+
+class CandidateShard:
+    """Rank `rank`'s contiguous slice [n0, n1) of the N all-entity candidates (SURVEY.md §8(e):
+    the decoder shards its candidates; the cross entropy and the ranks need only B-sized
+    exchanges).  Every rank holds the full candidate rows (the owner partition all-gathers
+    them), scores its slice with the HIP scorer and combines:
+      * cross entropy: per-slice log-sum-exp (regcn_hyp_ce_lse_f32 on the slice) -> combine_lse;
+        the target logit is the pair score of (q_b, e_{t_b}) computed on every rank;
+      * ranks: the target's score as threshold, per-slice count-greater with the slice-local
+        filter list (regcn_rank_count_f32) -> combine_counts, + 1.
+    With group=None the collectives are skipped (a single-process simulation of one rank)."""
+
+    def __init__(self, N, rank, world, group=None):
+        b = even_bounds(N, world)
+        self.N, self.rank, self.world, self.group = N, rank, world, group
+        self.n0, self.n1 = b[rank], b[rank + 1]
+
+    def _slice(self, cand, bias):
+        c = cand[self.n0:self.n1].contiguous()
+        return c, (bias[self.n0:self.n1].contiguous() if bias is not None else None)
+
+    def scores(self, q, cand, bias, c, scale=None, margin=0.0):
+        """Scores of every query against this slice, (B, n1 - n0)."""
+        from .hyperbolic_decoder import _chunked_hyperbolic_dist_score
+        cs, bs = self._slice(cand, bias)
+        return _chunked_hyperbolic_dist_score(q, cs, bs, c, 0, 0, score_scale=scale, score_margin=margin)
+
+    def target_scores(self, q, cand, bias, target, c, scale=None, margin=0.0):
+        """S(q_b, e_{t_b}) for every query (the diagonal of a B x B scoring of the target rows:
+        the same MFMA k-order and norm order as in the full scoring, so the same bits)."""
+        from .hyperbolic_decoder import _chunked_hyperbolic_dist_score
+        t = target.to(cand.device).long()
+        tb = bias[t].contiguous() if bias is not None else None
+        S = _chunked_hyperbolic_dist_score(q, cand[t].contiguous(), tb, c, 0, 0, score_scale=scale,
+                                           score_margin=margin)  # column j carries bias[t_j]
+        return torch.diagonal(S).contiguous()
+
+    def local_lse(self, q, cand, bias, c, scale=None, margin=0.0):
+        from . import _lib
+        from .hyperbolic_decoder import _scalar
+        cs, bs = self._slice(cand, bias)
+        B, d = q.shape
+        n = cs.shape[0]
+        q = q.contiguous().float()
+        tgt = torch.full((B,), -1, device=q.device, dtype=torch.int32)  # no target logit needed here
+        ws = torch.empty((_lib.lib().regcn_hyp_ce_workspace_bytes(B, n) + 3) // 4, device=q.device)
+        loss = torch.empty(B, device=q.device)
+        lse = torch.empty(B, device=q.device)
+        f = _lib.fptr
+        sc = _scalar(scale if scale is not None else 1.0, q)
+        mg = _scalar(margin, q)
+        _lib.call("regcn_hyp_ce_lse_f32", f(q, "query"), f(cs, "candidates"), f(bs), f(sc), f(mg), _lib.iptr(tgt),
+                  B, n, d, float(c), 0, f(ws), f(loss), f(lse), _lib.stream())
+        return lse
+
+    def ce_loss(self, q, cand, target, c, bias=None, scale=None, margin=0.0):
+        """mean_b (lse_b - S(q_b, e_{t_b})) over all N candidates (replicated on every rank)."""
+        lse = combine_lse(self.local_lse(q, cand, bias, c, scale, margin), self.group)
+        return (lse - self.target_scores(q, cand, bias, target, c, scale, margin)).mean()
+
+    def local_counts(self, local_scores, ts, filt_ptr=None, filt_idx=None):
+        from . import _lib
+        B, n = local_scores.shape
+        dev = local_scores.device
+        raw = torch.empty(B, device=dev, dtype=torch.int32)
+        flt = torch.empty(B, device=dev, dtype=torch.int32)
+        fp = fi = None
+        if filt_ptr is not None:
+            p_, i_ = shard_filters(filt_ptr, filt_idx, self.n0, self.n1)
+            fp = torch.from_numpy(p_).to(dev)
+            fi = torch.from_numpy(i_).to(dev) if len(i_) else torch.zeros(1, device=dev, dtype=torch.int32)
+        _lib.call("regcn_rank_count_f32", _lib.fptr(local_scores.contiguous(), "score"), B, n,
+                  _lib.fptr(ts.contiguous().float(), "threshold"), _lib.iptr(fp), _lib.iptr(fi), _lib.iptr(raw),
+                  _lib.iptr(flt) if fp is not None else None, _lib.stream())
+        return raw, (flt if fp is not None else None)
+
+    def ranks(self, local_scores, ts, filt_ptr=None, filt_idx=None):
+        """(rank, filtered rank) over all N candidates, 1-based, replicated."""
+        raw, flt = self.local_counts(local_scores, ts, filt_ptr, filt_idx)
+        both = torch.stack([raw, flt if flt is not None else raw])
+        both = combine_counts(both, self.group)
+        return both[0].long() + 1, both[1].long() + 1

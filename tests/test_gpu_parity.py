@@ -375,3 +375,47 @@ def test_total_rank_vs_golden(golden):
     np.testing.assert_array_equal(rank_r.cpu().numpy(), z["rank_r"])
     np.testing.assert_array_equal(frank_r.cpu().numpy(), z["frank_r"])
     np.testing.assert_allclose([m, mf, mr, mfr], z["mrr"], rtol=1e-6)
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_candidate_sharded_decoder(world):
+    """SURVEY.md §8(e) decoder: each rank scores a slice of the candidates; the ranks (raw and
+    filtered) summed over the slices equal the unsharded ranks exactly, the cross entropy
+    matches the unsharded fused CE.  The ranks are simulated on one GPU (group=None) and
+    combined here with the same reductions the collectives apply."""
+    from regcn_amd import ranking
+    from regcn_amd.hyperbolic_decoder import _chunked_hyperbolic_ce_loss, _chunked_hyperbolic_dist_score
+    from regcn_amd.parallel import CandidateShard
+    g = torch.Generator().manual_seed(world)
+    B, N, d = 300, 5003, 200
+    q = (torch.randn(B, d, generator=g) * 0.3).to(DEV)
+    e = (torch.randn(N, d, generator=g) * 0.3).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    tgt = torch.randint(0, N, (B,), generator=g).to(DEV)
+    scale, margin = torch.tensor(1.3, device=DEV), torch.tensor(0.7, device=DEV)
+    # filter lists: a few random other answers per query
+    rng = np.random.default_rng(world)
+    ptr, idx = [0], []
+    for b in range(B):
+        o = rng.integers(0, N, size=rng.integers(0, 6))
+        idx.extend(sorted(set(o.tolist()) - {int(tgt[b])}))
+        ptr.append(len(idx))
+    fp, fi = np.asarray(ptr, np.int32), np.asarray(idx, np.int32)
+    full = _chunked_hyperbolic_dist_score(q, e, bias, C, 0, 0, score_scale=scale, score_margin=margin)
+    want_raw, want_flt = ranking.ranks(full, tgt, fp, fi)
+    raw = torch.zeros(B, dtype=torch.long, device=DEV)
+    flt = torch.zeros(B, dtype=torch.long, device=DEV)
+    lses = []
+    for rank in range(world):
+        sh = CandidateShard(N, rank, world)
+        ts = sh.target_scores(q, e, bias, tgt, C, scale, margin)
+        assert torch.equal(ts, full[torch.arange(B, device=DEV), tgt])  # the same bits
+        r, f = sh.ranks(sh.scores(q, e, bias, C, scale, margin), ts, fp, fi)
+        raw += r - 1
+        flt += f - 1
+        lses.append(sh.local_lse(q, e, bias, C, scale, margin))
+    assert torch.equal(raw + 1, want_raw) and torch.equal(flt + 1, want_flt)
+    lse = torch.logsumexp(torch.stack(lses), 0)
+    loss = (lse - full[torch.arange(B, device=DEV), tgt]).mean()
+    ref = _chunked_hyperbolic_ce_loss(q, e, tgt, C, 0, candidate_bias=bias, score_scale=scale, score_margin=margin)
+    assert abs(float(loss) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))

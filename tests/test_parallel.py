@@ -134,3 +134,42 @@ def test_collectives_world2_gloo():
     for rank, err_edge, err_owner in res:
         assert err_edge < 1e-9, (rank, err_edge)
         assert err_owner == 0.0, (rank, err_owner)
+
+
+def _lse_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(0)
+        S = torch.randn(5, 20, generator=g, dtype=torch.float64)
+        sl = S[:, rank * 10:(rank + 1) * 10]
+        lse = P.combine_lse(torch.logsumexp(sl, 1))
+        cnt = P.combine_counts((sl > 0.1).sum(1))
+        err = float((lse - torch.logsumexp(S, 1)).abs().max())
+        q.put((rank, err, bool(torch.equal(cnt, (S > 0.1).sum(1)))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_decoder_shard_collectives_gloo():
+    """combine_lse / combine_counts (the B-sized exchanges of the candidate-sharded decoder,
+    SURVEY.md §8(e)) over a world-2 gloo group equal the unsharded log-sum-exp and counts."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lse_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, err, ok in sorted(q.get() for _ in range(2)):
+        assert err < 1e-12 and ok, (rank, err, ok)
+
+
+def test_shard_filters():
+    ptr = np.array([0, 3, 3, 5], np.int32)
+    idx = np.array([1, 7, 12, 0, 9], np.int32)
+    p, i = P.shard_filters(ptr, idx, 5, 10)
+    np.testing.assert_array_equal(p, [0, 1, 1, 2])
+    np.testing.assert_array_equal(i, [2, 4])
