@@ -252,7 +252,14 @@ class GraphCache:
 def train_model(args, model, train_list, valid, num_nodes, num_rels, device, model_state_file):
     """hyperbolic_main.py:505-640 (`valid`: the validation rows with their time column).
     Returns {"best_mrr", "best_epoch", "epoch_loss": [mean loss per epoch]}."""
+    import torch.distributed as dist
+    from .parallel import allreduce_gradients
     optimizer = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=1e-5)   # :469
+    # replicas (SURVEY.md §8(e)): every rank takes its share of the shuffled samples, one gradient
+    # all-reduce per optimizer step; the same seed on every rank keeps the shuffles (and so the
+    # lock-step schedule) identical.  Rank 0 validates and checkpoints.
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
     valid_list = ranking.split_by_time(valid)
     all_ans_v = ranking.load_all_answers_for_time_filter(valid, num_rels, num_nodes, False)
     all_ans_r_v = ranking.load_all_answers_for_time_filter(valid, num_rels, num_nodes, True)
@@ -266,11 +273,12 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
         losses, losses_e, losses_r, losses_rad = [], [], [], []
         idx = list(range(len(train_list)))
         random.shuffle(idx)
+        idx = [n for n in idx if n != 0 and len(train_list[n])]
         if args.max_train_snapshots:
             idx = idx[:args.max_train_snapshots]
+        if world > 1:  # lock-step: every rank one sample per step
+            idx = idx[:len(idx) // world * world][rank::world]
         for n in idx:
-            if n == 0:
-                continue
             inputs = train_list[max(0, n - args.train_history_len):n]
             glist = [graphs(s) for s in inputs]
             triples = torch.from_numpy(np.asarray(train_list[n], dtype=np.int64)).to(device)
@@ -284,14 +292,15 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
                                                   query_time=n)
                 loss = args.task_weight * le + (1 - args.task_weight) * lr + ls.sum() + lrad
                 loss.backward()
-                se += float(le)
-                sr += float(lr)
-                srad += float(lrad)
+                se += float(le.detach())
+                sr += float(lr.detach())
+                srad += float(lrad.detach())
                 nb += 1
             losses_e.append(se / nb)
             losses_r.append(sr / nb)
             losses_rad.append(srad / nb)
             losses.append(args.task_weight * losses_e[-1] + (1 - args.task_weight) * losses_r[-1] + losses_rad[-1])
+            allreduce_gradients(model.parameters())
             torch.nn.utils.clip_grad_norm_(model.parameters(), args.grad_norm)              # :627-628
             optimizer.step()
         epoch_loss.append(float(np.mean(losses)) if losses else float("nan"))
@@ -301,16 +310,22 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
                         np.mean(losses_r) if losses_r else 0.0, 0.0, np.mean(losses_rad) if losses_rad else 0.0,
                         best_mrr, time.time() - t0)
         if epoch and epoch % args.evaluate_every == 0:                                      # :660-681
-            res = test(model, train_list, valid_list, num_rels, num_nodes, device, all_ans_v, all_ans_r_v, args)
-            logger.info("Validation - MRR: raw=%.4f, filter=%.4f | Rel MRR: raw=%.4f, filter=%.4f", *res)
-            cur = res[2] if args.relation_evaluation else res[0]
-            if cur > best_mrr:
-                best_mrr, best_epoch = cur, epoch
-                os.makedirs(os.path.dirname(os.path.abspath(model_state_file)), exist_ok=True)
-                torch.save({"state_dict": model.state_dict(), "epoch": epoch}, model_state_file)
-                logger.info("New best model saved! MRR: %.4f", best_mrr)
-            elif epoch - best_epoch >= patience:
-                logger.info("Early stopping at epoch %d: no improvement in %d epochs.", epoch, patience)
+            stop = torch.zeros(1, device=device)
+            if rank == 0:
+                res = test(model, train_list, valid_list, num_rels, num_nodes, device, all_ans_v, all_ans_r_v, args)
+                logger.info("Validation - MRR: raw=%.4f, filter=%.4f | Rel MRR: raw=%.4f, filter=%.4f", *res)
+                cur = res[2] if args.relation_evaluation else res[0]
+                if cur > best_mrr:
+                    best_mrr, best_epoch = cur, epoch
+                    os.makedirs(os.path.dirname(os.path.abspath(model_state_file)), exist_ok=True)
+                    torch.save({"state_dict": model.state_dict(), "epoch": epoch}, model_state_file)
+                    logger.info("New best model saved! MRR: %.4f", best_mrr)
+                elif epoch - best_epoch >= patience:
+                    logger.info("Early stopping at epoch %d: no improvement in %d epochs.", epoch, patience)
+                    stop.fill_(1.0)
+            if world > 1:
+                dist.broadcast(stop, 0)
+            if float(stop) > 0:
                 break
     logger.info("Training completed in %.1f minutes", (time.time() - t_start) / 60)
     return {"best_mrr": best_mrr, "best_epoch": best_epoch, "epoch_loss": epoch_loss}
@@ -331,6 +346,21 @@ def main(argv=None):
         raise ValueError("--radius-anchor-beta must be in [0, 1]")
     if args.gpu < 0 or not torch.cuda.is_available():
         raise SystemExit("the HIP path needs a GPU (--gpu N); there is no CPU fallback")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        # one process per GPU (torchrun); replicas train on different snapshots and
+        # all-reduce gradients over RCCL
+        import torch.distributed as dist
+        args.gpu = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(args.gpu)
+        if not dist.is_initialized():
+            backend = os.environ.get("REGCN_DIST_BACKEND", "nccl")  # gloo: replicas sharing one GPU in tests
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", args.gpu))
+            else:
+                dist.init_process_group(backend)
+        if args.seed is None:
+            args.seed = 0  # identical shuffles on every rank keep the lock-step schedule
     device = torch.device("cuda", args.gpu)
     torch.cuda.set_device(device)
     if args.seed is not None:
@@ -346,11 +376,21 @@ def main(argv=None):
     all_ans = ranking.load_all_answers_for_time_filter(test_data, num_rels, num_nodes, False)
     all_ans_r = ranking.load_all_answers_for_time_filter(test_data, num_rels, num_nodes, True)
     model = build_model(args, num_nodes, num_rels, train_list, device)
+    if world > 1:
+        from .parallel import broadcast_state
+        broadcast_state(model)
     model_state_file = args.checkpoint or os.path.join(
         "models", "%s-%s-%s.pth" % (args.dataset.replace(":", "_"), args.encoder, args.decoder))
     if not args.test:
         train_model(args, model, train_list, valid, num_nodes, num_rels, device, model_state_file)
         args.checkpoint = model_state_file if os.path.exists(model_state_file) else None
+    if world > 1:  # the test pass runs on rank 0
+        import torch.distributed as dist
+        dist.barrier()
+        rank = dist.get_rank()
+        dist.destroy_process_group()
+        if rank != 0:
+            return True
     if args.checkpoint:
         ck = torch.load(args.checkpoint, map_location=device, weights_only=True)
         model.load_state_dict(ck["state_dict"] if "state_dict" in ck else ck)

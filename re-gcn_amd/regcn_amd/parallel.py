@@ -325,3 +325,39 @@ class CandidateShard:
         both = torch.stack([raw, flt if flt is not None else raw])
         both = combine_counts(both, self.group)
         return both[0].long() + 1, both[1].long() + 1
+
+
+# ------------------------------------------------------------------ training replicas
+def allreduce_gradients(params, group=None):
+    """Data-parallel training (replicas process different (history window,
+    target snapshot) samples): average every parameter gradient over the ranks with ONE
+    all-reduce of the flattened gradients (~2.5-2.8M floats for the reference models: a
+    single bucket, sized for point-to-point xGMI rather than per-tensor calls).  Parameters
+    without a gradient on this rank contribute zeros.  Returns the number of floats reduced."""
+    params = [p for p in params if p.requires_grad]
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1) or not params:
+        return 0
+    world = dist.get_world_size(group)
+    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    flat.div_(world)
+    off = 0
+    for p in params:
+        n = p.numel()
+        g = flat[off:off + n].view_as(p)
+        if p.grad is None:
+            p.grad = g.clone()
+        else:
+            p.grad.copy_(g)
+        off += n
+    return int(flat.numel())
+
+
+def broadcast_state(module, src=0, group=None):
+    """Replicas start from rank `src`'s parameters and buffers (one broadcast per tensor at
+    start-up; the per-step traffic is allreduce_gradients)."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src, group=group)

@@ -91,3 +91,30 @@ def test_cli_training_loop(tmp_path):
     # the CLI entry point end to end (train then test on the saved checkpoint)
     res = cli.main(common + ["--n-epochs", "2"])
     assert all(0.0 < m <= 1.0 for m in res)
+
+
+def test_cli_training_replicas(tmp_path):
+    """Two training replicas launched like the driver launches bench.py (torch.distributed.run,
+    one process per rank): lock-step samples, one gradient all-reduce per step, rank 0
+    validates, checkpoints and runs the test pass.  Both ranks share the box's one GPU, so
+    the group is gloo (REGCN_DIST_BACKEND); on a node each rank owns a GPU and uses RCCL."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ck = str(tmp_path / "m.pth")
+    env = dict(os.environ, PYTHONPATH=os.path.join(repo, "re-gcn_amd"), REGCN_DIST_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "regcn_amd.cli",
+           "-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0", "--encoder", "lgcn", "--decoder", "roth",
+           "--n-hidden", "64", "--n-bases", "32", "--synthetic-snapshots", "10", "--train-history-len", "3",
+           "--test-history-len", "3", "--relation-prediction", "--entity-prediction", "--checkpoint", ck,
+           "--seed", "0", "--lr", "0.01", "--triple-batch-size", "128", "--n-epochs", "2"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert os.path.exists(ck)
+    assert "MRR raw" in r.stdout + r.stderr

@@ -173,3 +173,60 @@ def test_shard_filters():
     p, i = P.shard_filters(ptr, idx, 5, 10)
     np.testing.assert_array_equal(p, [0, 1, 1, 2])
     np.testing.assert_array_equal(i, [2, 4])
+
+
+def _replica_worker(rank, world, port, q):
+    """Two replicas, different samples, one flattened gradient all-reduce per step: the
+    parameters after three Adam steps equal one process stepping on the mean loss."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(1234 + rank)  # different init: broadcast_state must align them
+        m = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Tanh(), torch.nn.Linear(5, 3))
+        m.register_buffer("unused_grad_holder", torch.zeros(1))
+        extra = torch.nn.Parameter(torch.ones(2))  # never used: zero gradient on every rank
+        P.broadcast_state(m)
+        ref = [p.detach().clone() for p in m.parameters()]
+        params = list(m.parameters()) + [extra]
+        opt = torch.optim.Adam(params, lr=1e-2)
+        g = torch.Generator().manual_seed(0)
+        X = torch.randn(3, world, 4, 6, generator=g)
+        for step in range(3):
+            opt.zero_grad()
+            m(X[step, rank]).pow(2).mean().backward()
+            n = P.allreduce_gradients(params)
+            opt.step()
+        q.put((rank, n, [p.detach().numpy().copy() for p in m.parameters()], [r.numpy() for r in ref]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_replica_gradients_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_replica_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted((q.get() for _ in range(2)), key=lambda t: t[0])
+    (_, n0, p0, init), (_, n1, p1, _) = res
+    assert n0 == n1 == 6 * 5 + 5 + 5 * 3 + 3 + 2
+    for a, b in zip(p0, p1):
+        np.testing.assert_array_equal(a, b)
+    # single-process replay: mean of the two replicas' losses
+    m = torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Tanh(), torch.nn.Linear(5, 3))
+    with torch.no_grad():
+        for p, v in zip(m.parameters(), init):
+            p.copy_(torch.from_numpy(v))
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(3, 2, 4, 6, generator=g)
+    for step in range(3):
+        opt.zero_grad()
+        (0.5 * sum(m(X[step, r]).pow(2).mean() for r in range(2))).backward()
+        opt.step()
+    for a, b in zip(m.parameters(), p0):
+        assert float((a.detach() - torch.from_numpy(b)).abs().max()) < 1e-6
