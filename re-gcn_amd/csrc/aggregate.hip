@@ -199,31 +199,33 @@ __global__ __launch_bounds__(256) void k_lorentz_sum(
       }
       int j = 0;
       if constexpr (S > 0) {
-        // EB edges per batch, all loads unconditional (clamped columns); the per-edge
-        // scalars of the Lorentz point (exp0 factor, time coordinate, scale) are computed
-        // once per batch with lane u = edge u, not redundantly in all 64 lanes per edge.
+        // EB edges per batch, all loads unconditional: wave-uniform row base (SGPR pair) +
+        // one per-lane byte offset, so the loads need no per-lane address arithmetic; lanes
+        // past d load the last real columns again and are masked out of |m|^2 (their acc is
+        // zeroed before the finish).  |m_u|^2 of the batch come from one transposing
+        // reduction (batch_sums) and the per-edge scalars of the Lorentz point (exp0 factor,
+        // time coordinate, scale) are computed lane-parallel, edge u in lane batch_lane(u).
         constexpr int EB = S == 4 ? 4 : 8;
-        const int colc = min(col, d - 4);
-        const f4 zero = {0.f, 0.f, 0.f, 0.f};
+        const uint32_t xoff = (uint32_t)min(col, d - 4) * 4u, woff = xoff * S;
+        const float amask = active ? 1.f : 0.f;
         for (; j + EB <= n; j += EB) {
           f4 xs[EB], rv[EB];
           WFrag<S> wf[EB];
 #pragma unroll
           for (int u = 0; u < EB; ++u) {
             const int src = rl(my_s, j + u), typ = rl(my_t, j + u);
-            xs[u] = *reinterpret_cast<const f4*>(x + (int64_t)src * d + colc);
-            rv[u] = *reinterpret_cast<const f4*>(rel + (int64_t)typ * d + colc);
-            wf[u].load(W + (int64_t)typ * wstride, colc);
+            xs[u] = row_load4(x + (int64_t)src * d, xoff);
+            rv[u] = row_load4(rel + (int64_t)typ * d, xoff);
+            wf[u].load_row(W + (int64_t)typ * wstride, woff);
           }
           f4 m[EB];
-          float n2l = 0.f;  // lane u < EB: |m_u|^2
+          float q[EB];
 #pragma unroll
           for (int u = 0; u < EB; ++u) {
-            m[u] = active ? wf[u].apply(xs[u]) + rv[u] : zero;
-            const float q = row16_sum(dot4(m[u], m[u]));
-            const float t = (rlane(q, 0) + rlane(q, 16)) + (rlane(q, 32) + rlane(q, 48));
-            n2l = lane == u ? t : n2l;
+            m[u] = wf[u].apply(xs[u]) + rv[u];
+            q[u] = dot4(m[u], m[u]) * amask;
           }
+          const float n2l = batch_sums<EB>(q, lane);
           float p2;  // lorentz_accum (gather.h), lane-parallel over the batch
           const float f = exp0_factor(n2l, k, &p2);
           const float den = fmaxf(1.f - k.c * p2, REGCN_EPS);
@@ -231,10 +233,11 @@ __global__ __launch_bounds__(256) void k_lorentz_sum(
           const float sc = 2.f * f / den;
 #pragma unroll
           for (int u = 0; u < EB; ++u) {
-            acc0 += rlane(a0, u);
-            acc += m[u] * rlane(sc, u);
+            acc0 += rlane(a0, batch_lane<EB>(u));
+            acc += m[u] * rlane(sc, batch_lane<EB>(u));
           }
         }
+        if (!active) acc = f4{0.f, 0.f, 0.f, 0.f};
       }
       for (; j < n; ++j) {
         const int src = rl(my_s, j), typ = rl(my_t, j);

@@ -12,6 +12,7 @@
 #define WAVE 64
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 namespace regcn {
 

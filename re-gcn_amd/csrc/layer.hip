@@ -165,10 +165,15 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
       acc0 = 0.f;
     }
   };
-  auto row4 = [&](const float* base, int row) {  // unconditional clamped row fragment
-    const f4 v = *reinterpret_cast<const f4*>(base + (int64_t)row * d + colc);
+  const uint32_t xoff = (uint32_t)colc * 4u, woff = xoff * (S > 0 ? S : 1);
+  auto row4 = [&](const float* base, int row) {  // unconditional clamped row fragment, zero past d
+    const f4 v = row_load4(base + (int64_t)row * d, xoff);
     return active ? v : zero;
   };
+  // Batched loads: lanes past d keep their duplicate of the last real columns (a flush stores
+  // active lanes only; the Lorentz |m|^2 masks them), so no per-load select.
+  auto row4u = [&](const float* base, int row) { return row_load4(base + (int64_t)row * d, xoff); };
+  const float amask = active ? 1.f : 0.f;
   trace_mark(p, 8);
   for (int t0 = ib; t0 < ie; t0 += 64) {
     const int n = min(64, ie - t0);
@@ -188,8 +193,8 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
         f4 xs[EB], rv[EB];
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-          xs[u] = row4(p.x, rl(my_s, j + u));
-          rv[u] = row4(p.rel, rl(my_t, j + u));
+          xs[u] = row4u(p.x, rl(my_s, j + u));
+          rv[u] = row4u(p.rel, rl(my_t, j + u));
         }
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
@@ -213,19 +218,18 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
 #pragma unroll
           for (int u = 0; u < EB; ++u) {
             const int src = rl(my_s, j + u), typ = rl(my_t, j + u);
-            xs[u] = row4(p.x, src);
-            rv[u] = row4(p.rel, typ);
-            wf[u].load(p.w_rel + (int64_t)typ * wstride, colc);
+            xs[u] = row4u(p.x, src);
+            rv[u] = row4u(p.rel, typ);
+            wf[u].load_row(p.w_rel + (int64_t)typ * wstride, woff);
           }
           f4 m[EB];
-          float n2l = 0.f;  // lane u < EB holds |m_u|^2
+          float q[EB];
 #pragma unroll
           for (int u = 0; u < EB; ++u) {
-            m[u] = active ? wf[u].apply(xs[u]) + rv[u] : zero;
-            const float q = row16_sum(dot4(m[u], m[u]));
-            const float tt = (rlane(q, 0) + rlane(q, 16)) + (rlane(q, 32) + rlane(q, 48));
-            n2l = lane == u ? tt : n2l;
+            m[u] = wf[u].apply(xs[u]) + rv[u];
+            q[u] = dot4(m[u], m[u]) * amask;
           }
+          const float n2l = batch_sums<EB>(q, lane);  // |m_u|^2 in lane batch_lane(u)
           // the per-edge scalars of the Lorentz point, once per batch with lane = edge
           float p2;
           const float f = exp0_factor(n2l, k, &p2);
@@ -235,8 +239,8 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
 #pragma unroll
           for (int u = 0; u < EB; ++u) {
             take(rl(my_i, j + u));
-            acc0 += rlane(a0, u);
-            acc += m[u] * rlane(sc, u);
+            acc0 += rlane(a0, batch_lane<EB>(u));
+            acc += m[u] * rlane(sc, batch_lane<EB>(u));
           }
           if (j == 0 && t0 == ib) trace_mark(p, 10);
         }

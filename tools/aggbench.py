@@ -69,7 +69,19 @@ def measure(V=1_000_000, R=256, triples=25_000_000, d=200, reps=3, dev=None,
         _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(wk["col_src"]), i(wk["col_type"]),
                   i(ch), ch.shape[0], i(fx), fx.shape[0], 100, float(C), d, f(part), stride, f(out), _lib.stream())
 
-    fns = {"union_aggregate": union_agg, "union_layer": lambda: uni(g, h, rel),
+    rt = {}
+
+    def lorentz_agg_rt():  # the row's edges in type order (regcn_snapshot_row_type_order_i32 layout)
+        if not rt:
+            rp = wk["rowptr"].long()
+            rows = torch.repeat_interleave(torch.arange(V, device=dev), rp[1:] - rp[:-1])
+            order = torch.sort(rows * (2 * R) + wk["col_type"].long(), stable=True).indices
+            rt["s"] = wk["col_src"][order].contiguous()
+            rt["t"] = wk["col_type"][order].contiguous()
+        _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(rt["s"]), i(rt["t"]),
+                  i(ch), ch.shape[0], i(fx), fx.shape[0], 100, float(C), d, f(part), stride, f(out), _lib.stream())
+
+    fns = {"union_aggregate": union_agg, "lorentz_aggregate_rt": lorentz_agg_rt, "union_layer": lambda: uni(g, h, rel),
            "lorentz_aggregate": lorentz_agg, "lorentz_layer": lambda: lor(g, h, rel)}
     st = torch.cuda.Stream(dev)
     b_agg = E * (4 * d + 12) + V * (4 * d + 12)
@@ -93,8 +105,9 @@ def main():
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--json", default=None, help="write the results here as well")
+    ap.add_argument("--which", default="union_aggregate,union_layer,lorentz_aggregate,lorentz_layer")
     a = ap.parse_args()
-    res = measure(a.V, a.R, a.triples, a.d, a.reps, log=lambda m: print(m, flush=True))
+    res = measure(a.V, a.R, a.triples, a.d, a.reps, which=a.which.split(","), log=lambda m: print(m, flush=True))
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(res, fh, indent=1)
