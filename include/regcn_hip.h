@@ -371,6 +371,16 @@ typedef struct regcn_transpose_desc {
 } regcn_transpose_desc;
 size_t regcn_transpose_workspace_bytes(int32_t E, int32_t V, int32_t R2);
 int regcn_snapshot_transpose_i32(const regcn_transpose_desc* desc, void* stream);
+/* The CSR edges with each destination row's edges in relation-type order (stable: ties keep
+ * CSR order): out_src / out_type [E].  Same rows and row pointer as the CSR, so every chunk
+ * list applies unchanged.  Fed to regcn_lorentz_aggregate_f32, a row's run of same-type
+ * edges reuses the type's relation row and W block fragment from L1 (SURVEY.md §8(d)
+ * config 5).  The message pass it serves (hyperbolic_layers.py:589-611) sums a row's
+ * Lorentz points in edge-id order; this order equals it within fp32 rounding. */
+size_t regcn_row_type_order_workspace_bytes(int32_t E, int32_t V, int32_t R2);
+int regcn_snapshot_row_type_order_i32(int32_t V, int32_t E, int32_t R2, const int32_t* rowptr,
+                                      const int32_t* col_src, const int32_t* col_type, int32_t* out_src,
+                                      int32_t* out_type, void* workspace, size_t ws_bytes, void* stream);
 size_t regcn_snapshot_workspace_bytes(int64_t T, int32_t V, int32_t R);
 int64_t regcn_snapshot_capacity(int32_t what, int64_t T, int32_t V, int32_t R, int32_t chunk_edges);
 int regcn_snapshot_csr_i32(const regcn_snapshot_desc* desc, void* stream);

@@ -394,5 +394,11 @@ int regcn_lorentz_aggregate_bwd_f32(const regcn_edge_bwd_desc* desc, int32_t num
 }
 size_t regcn_transpose_workspace_bytes(int32_t E, int32_t V, int32_t R2) { return transpose_ws_bytes(E, V, R2); }
 int regcn_snapshot_transpose_i32(const regcn_transpose_desc* desc, void* s) { return snapshot_transpose(desc, ST(s)); }
+size_t regcn_row_type_order_workspace_bytes(int32_t E, int32_t V, int32_t R2) { return row_type_ws_bytes(E, V, R2); }
+int regcn_snapshot_row_type_order_i32(int32_t V, int32_t E, int32_t R2, const int32_t* rowptr, const int32_t* col_src,
+                                      const int32_t* col_type, int32_t* out_src, int32_t* out_type, void* workspace,
+                                      size_t ws_bytes, void* s) {
+  return row_type_order(V, E, R2, rowptr, col_src, col_type, out_src, out_type, workspace, ws_bytes, ST(s));
+}
 
 }  // extern "C"

@@ -862,6 +862,63 @@ int snapshot_transpose(const regcn_transpose_desc* d, hipStream_t st) {
   return 0;
 }
 
+// ------------------------------------------------------------------- row / type edge order
+namespace {
+// keys of the second (row) pass: the destination of each type-sorted CSR position
+__global__ __launch_bounds__(BT) void k_row_of(const int* __restrict__ csr_dst, const uint32_t* __restrict__ pin,
+                                               int n, uint32_t* __restrict__ k, uint32_t* __restrict__ v) {
+  const int i = blockIdx.x * BT + threadIdx.x;
+  if (i < n) {
+    const uint32_t p = pin[i];
+    k[i] = (uint32_t)csr_dst[p];
+    v[i] = p;
+  }
+}
+
+__global__ __launch_bounds__(BT) void k_permute2(const uint32_t* __restrict__ perm, int n, const int* __restrict__ a,
+                                                 const int* __restrict__ b, int* __restrict__ oa, int* __restrict__ ob) {
+  const int i = blockIdx.x * BT + threadIdx.x;
+  if (i < n) {
+    const uint32_t p = perm[i];
+    oa[i] = a[p];
+    ob[i] = b[p];
+  }
+}
+}  // namespace
+
+size_t row_type_ws_bytes(int E, int V, int R2) {
+  return tlayout(E, V, R2).total + align_up((size_t)std::max(E, 1) * 4);
+}
+
+// Stable LSD radix sort by type, then stably by destination row: CSR positions in (row,
+// type, position) order.
+int row_type_order(int V, int E, int R2, const int* rowptr, const int* col_src, const int* col_type, int* out_src,
+                   int* out_type, void* workspace, size_t ws_bytes, hipStream_t st) {
+  if (V <= 0 || E < 0 || R2 <= 0) return set_error(REGCN_EINVAL, "bad row/type order sizes");
+  if (E == 0) return 0;
+  if (!rowptr || !col_src || !col_type || !out_src || !out_type) return set_error(REGCN_EINVAL, "null pointer");
+  if (!workspace || ws_bytes < row_type_ws_bytes(E, V, R2))
+    return set_error(REGCN_EINVAL, "row/type order workspace too small");
+  const Layout L = tlayout(E, V, R2);
+  char* ws = (char*)workspace;
+  int* csr_dst = (int*)(ws + L.total);
+  int rc;
+  hipLaunchKernelGGL(k_csr_dst, dim3(std::min<unsigned>(blocks(V, 4), 65536)), dim3(BT), 0, st, rowptr, V, csr_dst);
+  if ((rc = check_launch("k_csr_dst"))) return rc;
+  hipLaunchKernelGGL(k_iota_keys, dim3(blocks(E)), dim3(BT), 0, st, col_type, E, (uint32_t*)(ws + L.k0),
+                     (uint32_t*)(ws + L.v0));
+  bool second;
+  if ((rc = radix_sort(ws, L, E, bitlen((uint64_t)R2 - 1), true, &second, st))) return rc;
+  hipLaunchKernelGGL(k_row_of, dim3(blocks(E)), dim3(BT), 0, st, csr_dst,
+                     (const uint32_t*)(ws + (second ? L.v1 : L.v0)), E, (uint32_t*)(ws + L.k0),
+                     (uint32_t*)(ws + L.v0));
+  if ((rc = check_launch("k_row_of"))) return rc;
+  if ((rc = radix_sort(ws, L, E, bitlen((uint64_t)V - 1), true, &second, st))) return rc;
+  hipLaunchKernelGGL(k_permute2, dim3(blocks(E)), dim3(BT), 0, st, (const uint32_t*)(ws + (second ? L.v1 : L.v0)), E,
+                     col_src, col_type, out_src, out_type);
+  return check_launch("k_permute2");
+}
+
 int64_t snapshot_capacity(int what, int64_t T, int V, int R, int C) {
   const int64_t E = 2 * T, EC = E / std::max(C, 1) + 1, R2 = 2 * (int64_t)R;
   switch (what) {

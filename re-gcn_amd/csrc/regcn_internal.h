@@ -52,6 +52,9 @@ int lorentz_bwd(const regcn_edge_bwd_desc* a, int nb, float c, hipStream_t st);
 // graphbuild.hip
 int snapshot_transpose(const regcn_transpose_desc* d, hipStream_t st);
 size_t transpose_ws_bytes(int E, int V, int R2);
+size_t row_type_ws_bytes(int E, int V, int R2);
+int row_type_order(int V, int E, int R2, const int* rowptr, const int* col_src, const int* col_type, int* out_src,
+                   int* out_type, void* ws, size_t ws_bytes, hipStream_t st);
 int snapshot_csr(const regcn_snapshot_desc* d, hipStream_t st);
 int snapshot_work(const regcn_snapshot_desc* d, hipStream_t st);
 size_t snapshot_ws_bytes(int64_t T, int V, int R);

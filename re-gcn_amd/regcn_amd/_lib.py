@@ -63,6 +63,8 @@ _SIGS = {
     "regcn_snapshot_work_i32": [P, P],
     "regcn_transpose_workspace_bytes": [_c_int, _c_int, _c_int],
     "regcn_snapshot_transpose_i32": [P, P],
+    "regcn_row_type_order_workspace_bytes": [_c_int, _c_int, _c_int],
+    "regcn_snapshot_row_type_order_i32": [_c_int, _c_int, _c_int, P, P, P, P, P, P, _c_sz, P],
     "regcn_rowmap_bwd_f32": [_c_int, P, P, P, _c_i64, _c_int, _c_f, P, P, P],
     "regcn_union_aggregate_bwd_f32": [P, _c_f, P],
     "regcn_lorentz_sum_raw_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, P, P, P],
@@ -74,7 +76,7 @@ _SIGS = {
 SCORE_DIST, SCORE_RAW_SCALE = 1, 2
 _RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz,
             "regcn_snapshot_workspace_bytes": _c_sz, "regcn_snapshot_capacity": _c_i64,
-            "regcn_transpose_workspace_bytes": _c_sz,
+            "regcn_transpose_workspace_bytes": _c_sz, "regcn_row_type_order_workspace_bytes": _c_sz,
             "regcn_packed_weight_floats": _c_sz, "regcn_packed_linear_floats": _c_sz}
 
 _lib = None

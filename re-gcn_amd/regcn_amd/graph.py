@@ -257,6 +257,30 @@ class SnapshotGraph:
         self.__dict__["_transposed"] = t
         return t
 
+    def row_type_cols(self):
+        """(col_src, col_type) with each destination row's edges in relation-type order
+        (regcn_snapshot_row_type_order_i32), built on first use and cached: the edge lists
+        the chunked Lorentz aggregation reads (a row's same-type run reuses the type's
+        relation row and W blocks from L1)."""
+        t = self.__dict__.get("_row_type")
+        if t is not None:
+            return t
+        from . import _lib
+        wk = self.work()
+        dev = wk["rowptr"].device
+        V, E, R2 = self.num_nodes_, int(wk["col_src"].shape[0]), 2 * self.num_rels
+        if E == 0:
+            t = (wk["col_src"], wk["col_type"])
+        else:
+            ws = torch.empty(int(_lib.lib().regcn_row_type_order_workspace_bytes(E, V, R2)), dtype=torch.uint8,
+                             device=dev)
+            t = (torch.empty(E, dtype=torch.int32, device=dev), torch.empty(E, dtype=torch.int32, device=dev))
+            _lib.call("regcn_snapshot_row_type_order_i32", V, E, R2, _lib.iptr(wk["rowptr"]), _lib.iptr(wk["col_src"]),
+                      _lib.iptr(wk["col_type"]), _lib.iptr(t[0]), _lib.iptr(t[1]), ws.data_ptr(), ws.numel(),
+                      _lib.stream())
+        self.__dict__["_row_type"] = t
+        return t
+
     def work(self):
         """Device work lists (raises on a CPU graph: the HIP path has no CPU fallback)."""
         if self.dev is None:

@@ -57,8 +57,9 @@ def _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c):
     stride = d + 4
     part = torch.empty(max(g.heavy_slots, 1), stride, device=x.device, dtype=torch.float32)
     f, i = _lib.fptr, _lib.iptr
-    if mode == _lib.AGG_LORENTZ:
-        _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(wk["col_src"]), i(wk["col_type"]), i(hc),
+    if mode == _lib.AGG_LORENTZ:  # hub rows: edges in type order, same-type runs reuse rel/W from L1
+        cs, ct = g.row_type_cols()
+        _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(cs), i(ct), i(hc),
                   hc.shape[0], i(hf), hf.shape[0], nb, float(c), d, f(part), stride, f(agg), _lib.stream())
     elif mode == _lib.AGG_UNION:
         _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(wk["col_src"]), i(wk["col_type"]),

@@ -86,6 +86,9 @@ class OwnerView:
         self.n_heavy, self.heavy_slots = fw.n_heavy, fw.heavy_slots
         self._dev = None
 
+    def row_type_cols(self):
+        return self.g.row_type_cols()
+
     def work(self):
         if self._dev is None:
             wk = dict(self.g.work())
@@ -156,7 +159,8 @@ class ShardedGraph:
         f, i = _lib.fptr, _lib.iptr
         ch = pl["chunks"]
         if mode == _lib.AGG_LORENTZ:
-            _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(wk["col_src"]), i(wk["col_type"]),
+            cs, ct = self.g.row_type_cols()
+            _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(cs), i(ct),
                       i(ch), ch.shape[0], None, 0, nb, float(c), d, f(S), stride, f(P), _lib.stream())
         elif mode == _lib.AGG_UNION:
             _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(wk["col_src"]), i(wk["col_type"]),

@@ -242,5 +242,10 @@ def test_transposed_lists():
     np.testing.assert_array_equal(tr["sptr"].cpu().numpy(), np.concatenate([[0], np.cumsum(np.bincount(cs, minlength=V))]))
     tp = np.argsort(ct, kind="stable")
     np.testing.assert_array_equal(tr["tp"].cpu().numpy(), tp)
+    # row / type order of the Lorentz edge lists: (row, type, CSR position), rows unchanged
+    order = np.lexsort((np.arange(len(ct)), ct, csr_dst))
+    s2, t2 = g.row_type_cols()
+    np.testing.assert_array_equal(s2.cpu().numpy(), cs[order])
+    np.testing.assert_array_equal(t2.cpu().numpy(), ct[order])
     np.testing.assert_array_equal(tr["tptr"].cpu().numpy(),
                                   np.concatenate([[0], np.cumsum(np.bincount(ct, minlength=2 * R))]))

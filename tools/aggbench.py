@@ -65,24 +65,18 @@ def measure(V=1_000_000, R=256, triples=25_000_000, d=200, reps=3, dev=None,
                   f(wk["norm"]), i(ch), ch.shape[0], i(fx), fx.shape[0], 0.15, d, f(part), stride, f(out),
                   _lib.stream())
 
-    def lorentz_agg():
-        _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(wk["col_src"]), i(wk["col_type"]),
+    t0 = time.time()
+    cs, ct = g.row_type_cols()  # the product order of the Lorentz edge lists
+    torch.cuda.synchronize()
+    log("row/type edge order built in %.1f ms" % ((time.time() - t0) * 1e3))
+
+    def lorentz_agg(src=cs, typ=ct):
+        _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(src), i(typ),
                   i(ch), ch.shape[0], i(fx), fx.shape[0], 100, float(C), d, f(part), stride, f(out), _lib.stream())
 
-    rt = {}
-
-    def lorentz_agg_rt():  # the row's edges in type order (regcn_snapshot_row_type_order_i32 layout)
-        if not rt:
-            rp = wk["rowptr"].long()
-            rows = torch.repeat_interleave(torch.arange(V, device=dev), rp[1:] - rp[:-1])
-            order = torch.sort(rows * (2 * R) + wk["col_type"].long(), stable=True).indices
-            rt["s"] = wk["col_src"][order].contiguous()
-            rt["t"] = wk["col_type"][order].contiguous()
-        _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(rt["s"]), i(rt["t"]),
-                  i(ch), ch.shape[0], i(fx), fx.shape[0], 100, float(C), d, f(part), stride, f(out), _lib.stream())
-
-    fns = {"union_aggregate": union_agg, "lorentz_aggregate_rt": lorentz_agg_rt, "union_layer": lambda: uni(g, h, rel),
-           "lorentz_aggregate": lorentz_agg, "lorentz_layer": lambda: lor(g, h, rel)}
+    fns = {"union_aggregate": union_agg, "union_layer": lambda: uni(g, h, rel),
+           "lorentz_aggregate": lorentz_agg, "lorentz_layer": lambda: lor(g, h, rel),
+           "lorentz_aggregate_csr": lambda: lorentz_agg(wk["col_src"], wk["col_type"])}  # edge-id order, for comparison
     st = torch.cuda.Stream(dev)
     b_agg = E * (4 * d + 12) + V * (4 * d + 12)
     res = {"V": V, "E": E, "R2": 2 * R, "d": d, "b_agg_bytes": b_agg, "hbm_peak_gbs": HBM_PEAK_GBS}
