@@ -38,6 +38,10 @@ __device__ __forceinline__ float rlf(float v, int j) {
 // names a lane holding it.
 template <int EB>
 __device__ __forceinline__ int batch_lane(int u) { return EB == 8 ? 16 * (u >> 1) + (u & 1) : 16 * u; }
+// which value's sum lane `lane` holds (valid for lanes 0..63 when EB == 4; EB == 8: the
+// row's value for its lane parity)
+template <int EB>
+__device__ __forceinline__ int batch_row(int lane) { return EB == 8 ? 2 * (lane >> 4) + (lane & 1) : lane >> 4; }
 
 __device__ __forceinline__ float fold_pair32(float a, float b) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);

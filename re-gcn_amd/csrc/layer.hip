@@ -187,9 +187,14 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
       __builtin_amdgcn_s_waitcnt(0);
       trace_mark(p, 9);
     }
+    // Batches of EB edges; the last batch of a window is partial: its missing edges read
+    // lane n-1's (valid) indices, so every load of the batch is in flight at once, and
+    // contribute nothing (wave-uniform guard).  A tile's few edges cost one round trip,
+    // not one per edge.
     int j = 0;
     if constexpr (AGG == AGG_UNION || AGG == AGG_EUCLID) {
-      for (; j + EB <= n; j += EB) {
+      for (; j < n; j += EB) {
+        const int nv = n - j;
         f4 xs[EB], rv[EB];
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
@@ -198,21 +203,17 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
         }
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-          take(rl(my_i, j + u));
-          if (AGG == AGG_EUCLID) acc += xs[u] + rv[u];
-          else acc += rlf(my_w, j + u) * (xs[u] + rv[u]);
+          if (u < nv) {
+            take(rl(my_i, j + u));
+            if (AGG == AGG_EUCLID) acc += xs[u] + rv[u];
+            else acc += rlf(my_w, j + u) * (xs[u] + rv[u]);
+          }
         }
-      }
-      for (; j < n; ++j) {
-        const f4 xs = row4(p.x, rl(my_s, j));
-        const f4 rv = row4(p.rel, rl(my_t, j));
-        take(rl(my_i, j));
-        if (AGG == AGG_EUCLID) acc += xs + rv;
-        else acc += rlf(my_w, j) * (xs + rv);
       }
     } else if constexpr (AGG == AGG_LORENTZ) {
       if constexpr (S > 0) {
-        for (; j + EB <= n; j += EB) {
+        for (; j < n; j += EB) {
+          const int nv = n - j;
           f4 xs[EB], rv[EB];
           WFrag<S> wf[EB];
 #pragma unroll
@@ -238,14 +239,16 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
           const float sc = 2.f * f / den;
 #pragma unroll
           for (int u = 0; u < EB; ++u) {
-            take(rl(my_i, j + u));
-            acc0 += rlane(a0, batch_lane<EB>(u));
-            acc += m[u] * rlane(sc, batch_lane<EB>(u));
+            if (u < nv) {
+              take(rl(my_i, j + u));
+              acc0 += rlane(a0, batch_lane<EB>(u));
+              acc += m[u] * rlane(sc, batch_lane<EB>(u));
+            }
           }
           if (j == 0 && t0 == ib) trace_mark(p, 10);
         }
       }
-      for (; j < n; ++j) {
+      for (; j < n; ++j) {  // general block size s (S == 0)
         const int src = rl(my_s, j), typ = rl(my_t, j);
         const float* Wt = p.w_rel + (int64_t)typ * wstride;
         const f4 xs = row4(p.x, src);
@@ -300,7 +303,7 @@ __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int
     for (int w2 = 0; w2 < NWAVE; ++w2) {
       if ((tmask[w2] >> i) & 1) {  // slot i + w2 written by wave w2 (wave-uniform branch)
         const float* src = part + (i + w2) * lda;
-        const f4 v = {src[colc], src[colc + 1], src[colc + 2], src[colc + 3]};
+        const f4 v = *reinterpret_cast<const f4*>(src + colc);  // rows 128-B aligned (tile_lda)
         acc[q] += active ? v : zero;
         if (AGG == AGG_LORENTZ) acc0[q] += src[d];
       }
@@ -308,24 +311,26 @@ __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int
   }
   f4 out[RPW];
   if constexpr (AGG == AGG_LORENTZ) {
-    float ss[RPW], yy[RPW];
+    // Centroid -> Poincare -> log0 of the wave's RPW rows with the per-row scalar chain run
+    // once, lane-parallel (row q in lane batch_lane<RPW>(q)): |acc_q|^2 from one transposing
+    // reduction, y_q = acc_q / (sc (1 + c0 sqrt_c)) so |y_q|^2 = |acc_q|^2 / (sc den)^2 needs
+    // no second reduction, and out_q = acc_q * (one factor).  gather.h lorentz_finish, batched.
+    static_assert(RPW == 4 || RPW == 8, "batched finish needs 4 or 8 rows per wave");
+    float ss[RPW];
 #pragma unroll
-    for (int q = 0; q < RPW; ++q) ss[q] = row16_sum(dot4(acc[q], acc[q]));
-    f4 y[RPW];
+    for (int q = 0; q < RPW; ++q) ss[q] = dot4(acc[q], acc[q]);
+    const float s2 = batch_sums<RPW>(ss, lane);
+    const int my_q = batch_row<RPW>(lane);
+    float a0 = acc0[0];
 #pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      const float s2 = (rlane(ss[q], 0) + rlane(ss[q], 16)) + (rlane(ss[q], 32) + rlane(ss[q], 48));
-      const float ip = -acc0[q] * acc0[q] + s2;
-      const float sc = sqrtf(fmaxf(-ip * p.k.c, REGCN_EPS));
-      const float c0 = acc0[q] / sc;
-      y[q] = (acc[q] / sc) / fmaxf(1.f + c0 * p.k.sqrt_c, REGCN_EPS);
-      yy[q] = row16_sum(dot4(y[q], y[q]));
-    }
+    for (int q = 1; q < RPW; ++q) a0 = my_q == q ? acc0[q] : a0;
+    const float ip = -a0 * a0 + s2;
+    const float sc = sqrtf(fmaxf(-ip * p.k.c, REGCN_EPS));
+    const float den = fmaxf(1.f + (a0 / sc) * p.k.sqrt_c, REGCN_EPS);
+    const float inv = 1.f / (sc * den);
+    const float fac = inv * log0_factor(s2 * inv * inv, p.k);
 #pragma unroll
-    for (int q = 0; q < RPW; ++q) {
-      const float n2 = (rlane(yy[q], 0) + rlane(yy[q], 16)) + (rlane(yy[q], 32) + rlane(yy[q], 48));
-      out[q] = y[q] * log0_factor(n2, p.k);
-    }
+    for (int q = 0; q < RPW; ++q) out[q] = acc[q] * rlane(fac, batch_lane<RPW>(q));
   } else {
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {

@@ -91,6 +91,35 @@ def measure(V=1_000_000, R=256, triples=25_000_000, d=200, reps=3, dev=None,
     return res
 
 
+def cpu_layers(V=1_000_000, R=256, triples=2_500_000, d=200, log=print):
+    """The CPU baseline of config 5 (full size is infeasible on CPU, so
+    |V| = 1M with |E| = 5M): the oracle's Union and Lorentz layers (oracle/layers.py, test
+    infrastructure) timed on the host cores.  Returns {layer: M edges/s}."""
+    from oracle import graph as og
+    from oracle import layers as ol
+    threads = int(os.environ.get("OMP_NUM_THREADS", "8"))
+    torch.set_num_threads(threads)
+    snap = snapshot_series(0, V, R, 1, triples)[0]
+    g = og.build_sub_graph(V, R, snap)
+    E = 2 * triples
+    gen = torch.Generator().manual_seed(0)
+    h = torch.randn(V, d, generator=gen)
+    h = h / h.norm(dim=1, keepdim=True) * (torch.rand(V, 1, generator=gen) * 2.5 + 0.5) * 0.1
+    rel = torch.randn(2 * R, d, generator=gen) * 0.1
+    w = lambda *s: torch.randn(*s, generator=gen) * 0.05  # noqa: E731
+    out = {"V": V, "E": E, "d": d, "threads": threads}
+    with torch.no_grad():
+        for name, fn in (("union_layer", lambda: ol.union_layer(g, h, rel, w(d, d), w(d, d), w(d, d), C, 0.15)),
+                         ("lorentz_layer", lambda: ol.lorentz_layer(g, h, rel, w(2 * R, 100 * 4), w(d, d), w(d, d),
+                                                                    C, 100))):
+            t0 = time.perf_counter()
+            fn()
+            dt = time.perf_counter() - t0
+            out[name] = {"s": round(dt, 2), "M_edges_per_s": round(E / dt / 1e6, 3)}
+            log("cpu %-14s %7.2f s  %.3f M edges/s (%d threads)" % (name, dt, E / dt / 1e6, threads))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--V", type=int, default=1_000_000)
@@ -100,8 +129,11 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--json", default=None, help="write the results here as well")
     ap.add_argument("--which", default="union_aggregate,union_layer,lorentz_aggregate,lorentz_layer")
+    ap.add_argument("--cpu", action="store_true", help="also time the oracle layers at |V|=1M, |E|=5M on the host")
     a = ap.parse_args()
     res = measure(a.V, a.R, a.triples, a.d, a.reps, which=a.which.split(","), log=lambda m: print(m, flush=True))
+    if a.cpu:
+        res["cpu_oracle_E5M"] = cpu_layers(a.V, a.R, 2_500_000, a.d, log=lambda m: print(m, flush=True))
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(res, fh, indent=1)
