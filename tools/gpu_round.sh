@@ -12,6 +12,7 @@ B="python bench.py --no-cpu-baseline --no-scale"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- $B > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- $B --steps 50 > gpurun_out/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- $B --steps 50 > gpurun_out/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
+timeout -k 10 600 python tools/aggbench.py --cpu --json gpurun_out/aggbench.json > gpurun_out/aggbench.log 2>&1 || { echo "aggbench failed"; exit 1; }
 A="python tools/aggbench.py --reps 2"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/agg_prof -o run -- $A > gpurun_out/agg_prof.log 2>&1 || { echo "agg rocprof failed"; exit 1; }
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/agg_fetch -o run -- $A > gpurun_out/agg_fetch.log 2>&1 || { echo "agg pmc fetch failed"; exit 1; }
