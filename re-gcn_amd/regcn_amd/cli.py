@@ -86,6 +86,9 @@ def build_parser():
     a("--grad-norm", type=float, default=1.0)
     a("--evaluate-every", type=int, default=1)
     a("--triple-batch-size", type=int, default=64)
+    a("--reuse-encoder", action=argparse.BooleanOptionalAction, default=True,
+      help="one encoder forward per training snapshot for all its mini-batches (same gradients; "
+           "--no-reuse-encoder recomputes it per mini-batch as hyperbolic_main.py does)")
     a("--decoder", type=str, default="hyperbolic_convtranse", choices=["hyperbolic_convtranse", "murp", "roth", "atth"])
     a("--input-dropout", type=float, default=0.2)
     a("--hidden-dropout", type=float, default=0.2)
@@ -287,11 +290,21 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
             optimizer.zero_grad()
             se = sr = srad = 0.0
             nb = 0
-            for b in range(0, triples.shape[0], args.triple_batch_size):
-                le, lr, ls, lrad = model.get_loss(glist, triples[b:b + args.triple_batch_size], None, True,
-                                                  query_time=n)
-                loss = args.task_weight * le + (1 - args.task_weight) * lr + ls.sum() + lrad
-                loss.backward()
+            if args.reuse_encoder and hasattr(model, "get_loss_batches"):
+                # one encoder forward/backward per snapshot, the mini-batch losses summed
+                parts = model.get_loss_batches(glist, triples, None, True, args.triple_batch_size, query_time=n)
+                total = sum(args.task_weight * le + (1 - args.task_weight) * lr + ls.sum() + lrad
+                            for le, lr, ls, lrad in parts)
+                total.backward()
+            else:  # hyperbolic_main.py:585-598: the encoder recomputed per mini-batch
+                parts = []
+                for b in range(0, triples.shape[0], args.triple_batch_size):
+                    le, lr, ls, lrad = model.get_loss(glist, triples[b:b + args.triple_batch_size], None, True,
+                                                      query_time=n)
+                    loss = args.task_weight * le + (1 - args.task_weight) * lr + ls.sum() + lrad
+                    loss.backward()
+                    parts.append((le, lr, ls, lrad))
+            for le, lr, ls, lrad in parts:
                 se += float(le.detach())
                 sr += float(lr.detach())
                 srad += float(lrad.detach())

@@ -370,15 +370,34 @@ class HyperbolicRecurrentRGCN(nn.Module):
         c_val = self._c_float()
         self.decoder_ob.c = c_val
         self.rdecoder.c = c_val
-        dev = self.dynamic_emb.device
+        evolve_embs, static_emb, r_emb, _, _ = self.forward(glist, static_graph, use_cuda)
+        pre_emb = self._final_embedding(evolve_embs[-1], c_val)
+        return self._decode_losses(pre_emb, r_emb, triples, c_val)
+
+    def get_loss_batches(self, glist, triples, static_graph, use_cuda, batch_size, query_time=None):
+        """The losses of every `batch_size` mini-batch of one snapshot's triples from ONE
+        encoder forward: hyperbolic_main.py:585-598 recomputes the
+        encoder per mini-batch and accumulates the gradients of the mini-batch losses before
+        one optimizer step, so summing the losses and back-propagating once gives the same
+        gradients (dropout aside: one mask per snapshot instead of one per mini-batch).
+        Returns [(loss_ent, loss_rel, loss_static, loss_radius), ...]."""
+        c_val = self._c_float()
+        self.decoder_ob.c = c_val
+        self.rdecoder.c = c_val
+        evolve_embs, static_emb, r_emb, _, _ = self.forward(glist, static_graph, use_cuda)
+        pre_emb = self._final_embedding(evolve_embs[-1], c_val)
+        return [self._decode_losses(pre_emb, r_emb, triples[b:b + batch_size], c_val)
+                for b in range(0, triples.shape[0], batch_size)]
+
+    def _decode_losses(self, pre_emb, r_emb, triples, c_val):
+        """hyperbolic_model.py:996-1073: decoders on the final embedding + radius loss."""
+        dev = pre_emb.device
         loss_ent = torch.zeros(1, device=dev)
         loss_rel = torch.zeros(1, device=dev)
         loss_static = torch.zeros(1, device=dev)
         inverse_triples = triples.flip(1)
         inverse_triples[:, 1] = inverse_triples[:, 1] + self.num_rels
         all_triples = torch.cat([triples, inverse_triples]).to(dev)
-        evolve_embs, static_emb, r_emb, _, _ = self.forward(glist, static_graph, use_cuda)
-        pre_emb = self._final_embedding(evolve_embs[-1], c_val)
         if self.entity_prediction:
             if hasattr(self.decoder_ob, "loss"):
                 loss_ent = self.decoder_ob.loss(pre_emb, r_emb, all_triples)

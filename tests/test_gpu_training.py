@@ -148,3 +148,26 @@ def test_euclid_training_grads_vs_reference(golden, tag):
             assert err <= 2e-3, "%s: %.3g" % (k, err)
             n += 1
     assert n >= 15
+
+
+@pytest.mark.parametrize("tag", ["lgcn_roth", "uvrgcn_convtranse"])
+def test_encoder_reuse_same_gradients(golden, tag):
+    """get_loss_batches (one encoder forward per snapshot, the CLI default) gives the
+    gradients of hyperbolic_main.py:585-598's per-mini-batch get_loss + backward loop."""
+    z = golden("train_%s.npz" % tag)
+    batch = torch.from_numpy(z["batch"]).to(DEV)
+    bs = max(1, batch.shape[0] // 3)
+    m, glist = build(z, tag)
+    m.zero_grad()
+    for b in range(0, batch.shape[0], bs):
+        le, lr, ls, lrad = m.get_loss(glist, batch[b:b + bs], None, True)
+        (0.7 * le + 0.3 * lr + ls.sum() + lrad).backward()
+    ref = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad()
+    parts = m.get_loss_batches(glist, batch, None, True, bs)
+    assert len(parts) == (batch.shape[0] + bs - 1) // bs
+    sum(0.7 * le + 0.3 * lr + ls.sum() + lrad for le, lr, ls, lrad in parts).backward()
+    for k, p in m.named_parameters():
+        if k in ref:
+            err = float((p.grad - ref[k]).abs().max()) / max(1e-3, float(ref[k].abs().max()))
+            assert err <= 1e-4, (k, err)
