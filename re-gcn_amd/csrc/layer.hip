@@ -49,13 +49,17 @@ __host__ __device__ inline LdsLayout lds_layout(int d, bool gen_s) {
 // ---------------------------------------------------------------------- timestep epilogue
 __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4], const float* P, int lda,
                                               const int* trow, int n_valid, const StepArgs& p,
-                                              int64_t* trace = nullptr) {
+                                              int64_t* trace = nullptr, const Frag* tw_pre = nullptr) {
   auto stamp = [&](int k) {  // profiling: phase stamps 14, 15 (trace_mark)
     if (trace && threadIdx.x == 0) trace[blockIdx.x * 16 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
   };
-  Frag tw;
-  tw.zero();
-  mfma_tile(tw, P, lda, p.w_g, p.d);
+  Frag tw;  // time-gate pre-activation clamp(x_prev) @ W_g, unless the caller ran it already
+  if (tw_pre) {
+    tw = *tw_pre;
+  } else {
+    tw.zero();
+    mfma_tile(tw, P, lda, p.w_g, p.d);
+  }
   stamp(14);
   project_known(ct, n2, p.k);
   if (p.layer_norm) {
@@ -407,8 +411,13 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
   // that gather inline, where it would sit in registers across the gather.
   const float* wsel = pos ? p.w_loop : p.w_evolve;
   const float* wfirst = (pos && p.w_n) ? p.w_n : wsel;
+  // With the timestep fused, the time-gate GEMM (clamp(x_prev) @ W_g) depends only on staged
+  // rows: it runs in the self-loop GEMM's k-loop (two MFMA chains, two B streams in flight)
+  // instead of as a third serial GEMM in the epilogue.
+  const bool gate_with_loop = STEP && wsel != nullptr;
+  const bool prefetch = wfirst && !(gate_with_loop && wfirst == wsel);
   BRing br;
-  if (!inline_gather && wfirst) br.load(wfirst, p.d);
+  if (!inline_gather && prefetch) br.load(wfirst, p.d);
   stage_rows<false>(X, lda, p.x, trow, p.d, count);
   if (pos && AGG == AGG_NONE) stage_rows<false>(part, lda, p.agg, trow, p.d, count);
   if (!inline_gather) {
@@ -425,7 +434,7 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
     }
     if (STEP) stage_rows<true>(P2, lda, p.step.x_prev, trow, p.d, count);
     if (p.prev_t) stage_rows<false>(P1, lda, p.prev_t, trow, p.d, count);
-    if (wfirst) br.load(wfirst, p.d);
+    if (prefetch) br.load(wfirst, p.d);
   }
   __syncthreads();
   mark(2);
@@ -441,7 +450,17 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
       for (int j = 0; j < TPW; ++j) v.t[j] = clamp4(v.t[j], -10.f, 10.f);
     }
   }
-  if (wsel) {
+  Frag tw;
+  if (gate_with_loop) {
+    Frag acc[2];
+    acc[0] = v;
+    acc[1].zero();
+    const float* Ts[2] = {X, P2};
+    const float* Ws[2] = {wsel, p.step.w_g};
+    mfma_tiles<2, RING>(acc, Ts, Ws, lda, p.d);
+    v = acc[0];
+    tw = acc[1];
+  } else if (wsel) {
     if (wfirst == wsel && !(pos && p.w_n)) mfma_tile_pf(v, X, lda, wsel, p.d, br);
     else mfma_tile(v, X, lda, wsel, p.d);
   }
@@ -479,7 +498,7 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
   mark(4);
 
   if constexpr (STEP) {
-    step_epilogue(rr, v, n2, P2, lda, trow, count, p.step, p.trace);
+    step_epilogue(rr, v, n2, P2, lda, trow, count, p.step, p.trace, gate_with_loop ? &tw : nullptr);
   } else {
     frag_store(v, p.h_out, trow, count, p.d);
     if (p.r_next) store_radius(n2, p.r_next, trow, count);
