@@ -408,6 +408,16 @@ def main():
         kernels = {k: dict(avg_us=round(v["ms"] * 1e3, 3), per_step=v["per_step"], bound=v["bound"],
                            achieved=round(v["achieved"], 3), unit=v["unit"], frac=round(v["frac"], 4))
                    for k, v in kern.items()}
+        # SURVEY.md §8(d) asks for edges/s per layer and per encoder forward besides the
+        # end-to-end step: from the live kernel times (sum of per-step kernel time, no gaps)
+        enc_us = sum(v["ms"] * 1e3 * v["per_step"] for k, v in kern.items() if k.startswith(("k_layer", "k_rel_gru")))
+        lay_us = sum(v["ms"] * 1e3 * v["per_step"] for k, v in kern.items() if k.startswith("k_layer"))
+        e_step = float(np.mean(epw))
+        breakdown = {"encoder_kernels_us_per_step": round(enc_us, 2),
+                     "encoder_M_edges_per_s": round(e_step / enc_us, 3) if enc_us else None,
+                     "layers_kernels_us_per_step": round(lay_us, 2),
+                     "layer_M_edges_per_s": round(e_step / lay_us, 3) if lay_us else None,
+                     "note": "kernel time only (sum of the stage launches' HIP-event averages); value is end to end"}
         scale = dec = None
         if not args.no_scale and world == 1:
             scale = aggregation_at_scale(device)
@@ -426,7 +436,7 @@ def main():
                           "hip_graph": bool(graphs), "steps_per_graph_launch": len(samples) if pool_graph else 1,
                           "parallelism": ("%s-partitioned snapshots x%d" % (args.shard, world)) if sharded
                           else "replicas x%d" % world},
-               "roofline": roof, "kernels": kernels, "aggregation_roofline": scale,
+               "roofline": roof, "kernels": kernels, "breakdown": breakdown, "aggregation_roofline": scale,
                "decoder_roofline": dec, "cpu_baseline": cpu, "mrr_parity": mrr}
         print(json.dumps(out), flush=True)
     if world > 1:
