@@ -6,9 +6,11 @@ Times, as graph-replayed launches between HIP events (bench.event_time):
   lorentz aggregation alone regcn_lorentz_aggregate_f32 (2x2 block messages + centroid)
   fused layers              HyperbolicUnionRGCNLayer / LorentzRGCNLayer forward (gather + GEMMs)
 and reports algorithmic bytes B_agg = E (4d + 12) + V (4d + 12) per aggregation over the time,
-as GB/s and as a fraction of the 8 TB/s HBM peak.
+as GB/s and as a fraction of the 8 TB/s HBM peak.  The Lorentz aggregation reads the
+row/type edge order (graph.row_type_cols); `lorentz_aggregate_csr` times the edge-id order.
+--cpu adds the CPU oracle's layers at |V| = 1M, |E| = 5M.
 
-  python tools/aggbench.py [--V 1000000] [--triples 25000000] [--reps 3]
+  python tools/aggbench.py [--V 1000000] [--triples 25000000] [--reps 3] [--cpu] [--which ...]
 """
 import argparse
 import json
