@@ -270,12 +270,24 @@ class HyperbolicRecurrentRGCN(nn.Module):
         dev = self.dynamic_emb.device
         V, d = self.dynamic_emb.shape
         r_static = self._static_radius(c_val).contiguous()
-        dyn = self.dynamic_emb.detach().contiguous()
-        h = torch.empty_like(dyn)
-        x = torch.empty_like(dyn)
-        r = torch.empty(V, device=dev, dtype=torch.float32)
-        _lib.call("regcn_init_entities_f32", _lib.fptr(dyn, "dynamic_emb"), _lib.fptr(r_static), V, d, c_val,
-                  int(bool(self.layer_norm)), _lib.fptr(h), _lib.fptr(x), _lib.fptr(r), _lib.stream())
+        # The initial entity state (hyperbolic_model.py:775-782) is a function of parameters
+        # only: computed once per parameter version and reused by every predict (the kernels
+        # read it, none writes it), so a captured predict graph holds no init launch.
+        pe = self.dynamic_emb
+        key = (pe.data_ptr(), pe._version, self.radius_static.data_ptr(), self.radius_static._version,
+               float(c_val), bool(self.layer_norm))
+        hit = self.__dict__.get("_init_cache")
+        if hit is not None and hit[0] == key:
+            h, x, r = hit[1]
+        else:
+            dyn = pe.detach().contiguous()
+            h = torch.empty_like(dyn)
+            x = torch.empty_like(dyn)
+            r = torch.empty(V, device=dev, dtype=torch.float32)
+            _lib.call("regcn_init_entities_f32", _lib.fptr(dyn, "dynamic_emb"), _lib.fptr(r_static), V, d, c_val,
+                      int(bool(self.layer_norm)), _lib.fptr(h), _lib.fptr(x), _lib.fptr(r), _lib.stream())
+            if not torch.cuda.is_current_stream_capturing():
+                self.__dict__["_init_cache"] = (key, (h, x, r))
         attach(h, x, r, c_val)
         self.h = h
         R2 = self.num_rels * 2
