@@ -292,10 +292,11 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
             nb = 0
             if args.reuse_encoder and hasattr(model, "get_loss_batches"):
                 # one encoder forward/backward per snapshot, the mini-batch losses summed
-                parts = model.get_loss_batches(glist, triples, None, True, args.triple_batch_size, query_time=n)
-                total = sum(args.task_weight * le + (1 - args.task_weight) * lr + ls.sum() + lrad
-                            for le, lr, ls, lrad in parts)
-                total.backward()
+                # (the mini-batch decoder losses are back-propagated one at a time inside)
+                parts = model.get_loss_batches(
+                    glist, triples, None, True, args.triple_batch_size, query_time=n,
+                    combine=lambda le, lr, ls, lrad: args.task_weight * le + (1 - args.task_weight) * lr
+                    + ls.sum() + lrad)
             else:  # hyperbolic_main.py:585-598: the encoder recomputed per mini-batch
                 parts = []
                 for b in range(0, triples.shape[0], args.triple_batch_size):

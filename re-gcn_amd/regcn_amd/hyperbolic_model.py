@@ -27,7 +27,7 @@ from .hyperbolic_decoder import (HyperbolicAttH, HyperbolicAttHRel, HyperbolicCo
 from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell, StepSpec
 from .hyperbolic_ops import HyperbolicOps, TemporalRadiusEvolution
 from .tangent import attach, tangent_of
-from .weights import packed
+from .weights import invalidate, packed
 
 logger = logging.getLogger("hyperbolic_model")
 GEOOPT_AVAILABLE = False
@@ -207,6 +207,9 @@ class HyperbolicRecurrentRGCN(nn.Module):
             torch.as_tensor(radius_target, dtype=torch.float)
         self.register_buffer("radius_target", target)
         self.radius_static = nn.Parameter(self.radius_target.clone())
+        # load_state_dict copies through no-grad in-place writes; drop the parameter-keyed
+        # caches explicitly rather than rely on version counters alone
+        self.register_load_state_dict_post_hook(lambda module, _keys: invalidate(module))
 
     # ---------------------------------------------------------------------------- helpers
     def get_curvature(self):
@@ -275,7 +278,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
         # read it, none writes it), so a captured predict graph holds no init launch.
         pe = self.dynamic_emb
         key = (pe.data_ptr(), pe._version, self.radius_static.data_ptr(), self.radius_static._version,
-               float(c_val), bool(self.layer_norm))
+               float(c_val), bool(self.layer_norm), float(self.radius_min), float(self.radius_max))
         hit = self.__dict__.get("_init_cache")
         if hit is not None and hit[0] == key:
             h, x, r = hit[1]
@@ -386,20 +389,44 @@ class HyperbolicRecurrentRGCN(nn.Module):
         pre_emb = self._final_embedding(evolve_embs[-1], c_val)
         return self._decode_losses(pre_emb, r_emb, triples, c_val)
 
-    def get_loss_batches(self, glist, triples, static_graph, use_cuda, batch_size, query_time=None):
-        """The losses of every `batch_size` mini-batch of one snapshot's triples from ONE
-        encoder forward: hyperbolic_main.py:585-598 recomputes the
-        encoder per mini-batch and accumulates the gradients of the mini-batch losses before
-        one optimizer step, so summing the losses and back-propagating once gives the same
-        gradients (dropout aside: one mask per snapshot instead of one per mini-batch).
-        Returns [(loss_ent, loss_rel, loss_static, loss_radius), ...]."""
+    def get_loss_batches(self, glist, triples, static_graph, use_cuda, batch_size, query_time=None,
+                         combine=None):
+        """One snapshot's training losses and gradients with ONE encoder forward (SURVEY.md
+        §8(f) f1).  hyperbolic_main.py:585-598 recomputes the encoder for every
+        `batch_size` mini-batch, back-propagates each mini-batch loss and steps once per
+        snapshot, so the gradient is the sum over mini-batches.  Here the final entity and
+        relation embeddings are cut from the graph as leaf tensors; each mini-batch's
+        decoder loss is back-propagated as soon as it is formed (the reference's per
+        mini-batch peak memory: one (2*batch_size) x |V| score block alive at a time),
+        accumulating into those leaves and the decoder parameters, and one backward
+        through the encoder follows with the accumulated embedding gradients.  Same
+        gradients as the reference loop; the encoder dropout draws one mask per snapshot
+        instead of one per mini-batch.
+
+        `combine(le, lr, ls, lrad)` -> the scalar each mini-batch back-propagates
+        (default: the plain sum).  Returns the detached [(loss_ent, loss_rel, loss_static,
+        loss_radius), ...]."""
+        if combine is None:
+            combine = lambda le, lr, ls, lrad: le + lr + ls.sum() + lrad  # noqa: E731
         c_val = self._c_float()
         self.decoder_ob.c = c_val
         self.rdecoder.c = c_val
         evolve_embs, static_emb, r_emb, _, _ = self.forward(glist, static_graph, use_cuda)
         pre_emb = self._final_embedding(evolve_embs[-1], c_val)
-        return [self._decode_losses(pre_emb, r_emb, triples[b:b + batch_size], c_val)
-                for b in range(0, triples.shape[0], batch_size)]
+        grad_on = torch.is_grad_enabled()
+        cut = [t.detach().requires_grad_(grad_on and t.requires_grad) for t in (pre_emb, r_emb)]
+        parts = []
+        for b in range(0, triples.shape[0], batch_size):
+            losses = self._decode_losses(cut[0], cut[1], triples[b:b + batch_size], c_val)
+            total = combine(*losses)
+            if grad_on and total.requires_grad:
+                total.backward()
+            parts.append(tuple(t.detach() for t in losses))
+        roots = [(src, leaf.grad) for src, leaf in zip((pre_emb, r_emb), cut)
+                 if src.requires_grad and leaf.grad is not None]
+        if roots:
+            torch.autograd.backward([r[0] for r in roots], [r[1] for r in roots])
+        return parts
 
     def _decode_losses(self, pre_emb, r_emb, triples, c_val):
         """hyperbolic_model.py:996-1073: decoders on the final embedding + radius loss."""

@@ -336,23 +336,35 @@ def allreduce_gradients(params, group=None):
     """Data-parallel training (replicas process different (history window,
     target snapshot) samples): average every parameter gradient over the ranks with ONE
     all-reduce of the flattened gradients (~2.5-2.8M floats for the reference models: a
-    single bucket, sized for point-to-point xGMI rather than per-tensor calls).  Parameters
-    without a gradient on this rank contribute zeros.  Returns the number of floats reduced."""
+    single bucket, sized for point-to-point xGMI rather than per-tensor calls).
+
+    A per-parameter has-gradient flag travels in the same bucket.  A parameter no rank
+    produced a gradient for keeps `grad = None`, exactly as in a single process, so the
+    optimizer skips it (Adam's weight decay would otherwise move it by ~lr per step); one
+    that only some ranks touched gets the mean over all ranks, the others contributing
+    zeros.  Returns the number of floats reduced."""
     params = [p for p in params if p.requires_grad]
     if not (dist.is_initialized() and dist.get_world_size(group) > 1) or not params:
         return 0
     world = dist.get_world_size(group)
-    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
+    dev = params[0].device
+    has = torch.tensor([1.0 if p.grad is not None else 0.0 for p in params], device=dev)
+    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params]
+                     + [has])
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
-    flat.div_(world)
+    flags = flat[-len(params):].tolist()
+    flat = flat[:-len(params)].div_(world)
     off = 0
-    for p in params:
+    for p, f in zip(params, flags):
         n = p.numel()
-        g = flat[off:off + n].view_as(p)
-        if p.grad is None:
-            p.grad = g.clone()
+        if f > 0:
+            g = flat[off:off + n].view_as(p)
+            if p.grad is None:
+                p.grad = g.clone()
+            else:
+                p.grad.copy_(g)
         else:
-            p.grad.copy_(g)
+            p.grad = None
         off += n
     return int(flat.numel())
 
@@ -362,6 +374,10 @@ def broadcast_state(module, src=0, group=None):
     start-up; the per-step traffic is allreduce_gradients)."""
     if not (dist.is_initialized() and dist.get_world_size(group) > 1):
         return
+    # into the tensors themselves (not through `.data`): the in-place write bumps each
+    # tensor's version counter, which the parameter-derived caches are keyed on
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
-            dist.broadcast(t.data, src, group=group)
+            dist.broadcast(t, src, group=group)
+    from .weights import invalidate
+    invalidate(module)

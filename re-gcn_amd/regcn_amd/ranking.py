@@ -9,7 +9,9 @@ and the filtered rank additionally excludes the other true answers of the same s
 (a CSR list built once on the host).  Without score ties against the target this equals
 the reference's sort position + 1; with ties the reference's order is whatever
 `torch.sort` returns (unspecified), the kernel counts the tie as not above (the optimistic
-rank).  Unlike the reference, `score` is not modified in place.
+rank).  As in the reference (filter_score / filter_score_r write into a view of `score`,
+rgcn/utils.py:51-75), `score` leaves get_total_rank with the other true answers set to
+-1e7, so `construct_snap` under --multi-step picks its top-k from the filtered scores.
 """
 import numpy as np
 import torch
@@ -51,6 +53,21 @@ def ranks(score, target, filt_ptr=None, filt_idx=None):
     return raw.long(), flt.long()
 
 
+FILTERED_SCORE = -10000000.0  # rgcn/utils.py:60, :74
+
+
+def apply_filter_(score, filt_ptr, filt_idx):
+    """Write -1e7 into `score[b, filt_idx[filt_ptr[b]:filt_ptr[b+1]]]` in place, as
+    filter_score / filter_score_r do (rgcn/utils.py:51-75): one device index_put."""
+    if filt_idx is None or len(filt_idx) == 0:
+        return score
+    counts = np.diff(filt_ptr).astype(np.int64)
+    rows = torch.from_numpy(np.repeat(np.arange(len(counts), dtype=np.int64), counts)).to(score.device)
+    cols = torch.from_numpy(filt_idx.astype(np.int64)).to(score.device)
+    score[rows, cols] = FILTERED_SCORE
+    return score
+
+
 def sort_and_rank(score, target):
     """rgcn/utils.py:21-25: 0-based position of the target among the candidates."""
     return ranks(score, target)[0] - 1
@@ -62,6 +79,7 @@ def get_total_rank(test_triples, score, all_ans, eval_bz, rel_predict=0):
     target = test_triples[:, col]
     fp, fi = _filter_csr(test_triples, all_ans, bool(rel_predict))
     rank, filter_rank = ranks(score, target, fp, fi)
+    apply_filter_(score, fp, fi)
     mrr = torch.mean(1.0 / rank.float())
     filter_mrr = torch.mean(1.0 / filter_rank.float())
     return filter_mrr.item(), mrr.item(), rank, filter_rank

@@ -151,6 +151,8 @@ class RecurrentRGCN(nn.Module):
             raise NotImplementedError
         self.decoder_ob = ConvTransE(num_ents, h_dim, input_dropout, hidden_dropout, feat_dropout)
         self.rdecoder = ConvTransR(num_rels, h_dim, input_dropout, hidden_dropout, feat_dropout)
+        from .weights import invalidate
+        self.register_load_state_dict_post_hook(lambda module, _keys: invalidate(module))
 
     def forward(self, g_list, static_graph, use_cuda):
         """src/rrgcn.py:142-180."""

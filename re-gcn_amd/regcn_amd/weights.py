@@ -56,3 +56,21 @@ def packed_t(w):
     _lib.call("regcn_pack_weight_f32", _lib.fptr(wt, "weight"), n_in, n_out, _lib.fptr(out), _lib.stream())
     w._regcn_packed_t = (key, out, wt)  # keep wt alive until the packing kernel has run
     return out
+
+
+_CACHE_ATTRS = ("_regcn_packed", "_regcn_packed_lin", "_regcn_packed_t")
+
+
+def invalidate(module):
+    """Drop every parameter-derived cache of `module`: the packed weight copies above and
+    the model's own caches (initial entity state, static radius, curvature).  They are
+    keyed on the tensors' version counters, which writes through `.data` do not bump;
+    load_state_dict and the replica broadcast call this, and so should any other code
+    that edits parameters through `.data`."""
+    for t in list(module.parameters()) + list(module.buffers()):
+        for a in _CACHE_ATTRS:
+            if hasattr(t, a):
+                delattr(t, a)
+    for m in module.modules():
+        for a in ("_init_cache", "_r_static_cache", "_c_cache"):
+            m.__dict__.pop(a, None)

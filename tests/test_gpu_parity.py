@@ -377,6 +377,24 @@ def test_total_rank_vs_golden(golden):
     np.testing.assert_allclose([m, mf, mr, mfr], z["mrr"], rtol=1e-6)
 
 
+def test_multistep_history_from_filtered_scores(golden):
+    """--multi-step (hyperbolic_main.py:135-149): get_total_rank leaves the other true
+    answers at -1e7 in the score (rgcn/utils.py:51-75) and construct_snap(_r) takes the
+    next history snapshot's top-k from those filtered scores; both against the reference."""
+    from regcn_amd.ranking import construct_snap, construct_snap_r, get_total_rank, load_all_answers_for_filter
+    z, zm = golden("rank.npz"), golden("multistep.npz")
+    V, R = (int(v) for v in z["meta"])
+    k = int(zm["topk"][0])
+    tr = torch.from_numpy(z["all_triples"]).to(DEV)
+    score, score_rel = t(z["score"]).clone(), t(z["score_rel"]).clone()
+    get_total_rank(tr, score, load_all_answers_for_filter(z["snap"], R, False), 1000)
+    get_total_rank(tr, score_rel, load_all_answers_for_filter(z["snap"], R, True), 1000, rel_predict=1)
+    np.testing.assert_array_equal(score.cpu().numpy(), zm["filtered_score"])
+    np.testing.assert_array_equal(score_rel.cpu().numpy(), zm["filtered_score_rel"])
+    np.testing.assert_array_equal(construct_snap(tr, V, R, score, k), zm["snap_e"])
+    np.testing.assert_array_equal(construct_snap_r(tr, V, R, score_rel, k), zm["snap_r"])
+
+
 @pytest.mark.parametrize("world", [1, 3, 8])
 def test_candidate_sharded_decoder(world):
     """SURVEY.md §8(e) decoder: each rank scores a slice of the candidates; the ranks (raw and

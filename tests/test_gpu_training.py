@@ -164,9 +164,10 @@ def test_encoder_reuse_same_gradients(golden, tag):
         (0.7 * le + 0.3 * lr + ls.sum() + lrad).backward()
     ref = {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
     m.zero_grad()
-    parts = m.get_loss_batches(glist, batch, None, True, bs)
+    parts = m.get_loss_batches(glist, batch, None, True, bs,
+                               combine=lambda le, lr, ls, lrad: 0.7 * le + 0.3 * lr + ls.sum() + lrad)
     assert len(parts) == (batch.shape[0] + bs - 1) // bs
-    sum(0.7 * le + 0.3 * lr + ls.sum() + lrad for le, lr, ls, lrad in parts).backward()
+    assert all(not t.requires_grad for part in parts for t in part)  # backward already ran per mini-batch
     for k, p in m.named_parameters():
         if k in ref:
             err = float((p.grad - ref[k]).abs().max()) / max(1e-3, float(ref[k].abs().max()))

@@ -166,3 +166,23 @@ def test_split_by_time_and_filter_answers():
     assert ans == {0: {1: {2}}, 2: {11: {0}}, 3: {1: {4}}, 4: {11: {3}}}
     ans_r = load_all_answers_for_filter(snaps[0], 10, rel_p=True)
     assert ans_r == {0: {2: {1}}, 2: {0: {11}}, 3: {4: {1}}, 4: {3: {11}}}
+
+
+def test_multistep_filter_and_snap_vs_reference(golden):
+    """--multi-step host logic (no GPU): the reference's in-place -1e7 filter of the score
+    (rgcn/utils.py:51-75) via the filter CSR, then construct_snap(_r)'s top-k triples
+    (rgcn/utils.py:367-405), against the reference's outputs on the same scores."""
+    import torch
+    from regcn_amd.ranking import _filter_csr, apply_filter_, construct_snap, construct_snap_r, \
+        load_all_answers_for_filter
+    z, zm = golden("rank.npz"), golden("multistep.npz")
+    V, R = (int(v) for v in z["meta"])
+    k = int(zm["topk"][0])
+    tr = torch.from_numpy(z["all_triples"])
+    for rel, key, ref_score, make in ((False, "score", "filtered_score", construct_snap),
+                                      (True, "score_rel", "filtered_score_rel", construct_snap_r)):
+        score = torch.from_numpy(z[key]).clone()
+        fp, fi = _filter_csr(tr, load_all_answers_for_filter(z["snap"], R, rel), rel)
+        apply_filter_(score, fp, fi)
+        np.testing.assert_array_equal(score.numpy(), zm[ref_score])
+        np.testing.assert_array_equal(make(tr, V, R, score, k), zm["snap_r" if rel else "snap_e"])

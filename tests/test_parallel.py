@@ -188,14 +188,18 @@ def _replica_worker(rank, world, port, q):
         P.broadcast_state(m)
         ref = [p.detach().clone() for p in m.parameters()]
         params = list(m.parameters()) + [extra]
-        opt = torch.optim.Adam(params, lr=1e-2)
+        # weight decay on, as the CLI's Adam (hyperbolic_main.py:469): a parameter no rank
+        # produced a gradient for must keep grad=None and so stay untouched
+        opt = torch.optim.Adam(params, lr=1e-2, weight_decay=1e-5)
         g = torch.Generator().manual_seed(0)
         X = torch.randn(3, world, 4, 6, generator=g)
         for step in range(3):
             opt.zero_grad()
             m(X[step, rank]).pow(2).mean().backward()
             n = P.allreduce_gradients(params)
+            assert extra.grad is None
             opt.step()
+        assert torch.equal(extra.detach(), torch.ones(2))
         q.put((rank, n, [p.detach().numpy().copy() for p in m.parameters()], [r.numpy() for r in ref]))
     finally:
         dist.destroy_process_group()
@@ -221,7 +225,7 @@ def test_replica_gradients_gloo():
     with torch.no_grad():
         for p, v in zip(m.parameters(), init):
             p.copy_(torch.from_numpy(v))
-    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2, weight_decay=1e-5)
     g = torch.Generator().manual_seed(0)
     X = torch.randn(3, 2, 4, 6, generator=g)
     for step in range(3):

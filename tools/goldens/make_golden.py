@@ -18,6 +18,9 @@ Each fixture pins one row of SURVEY.md §8(a):
   rrgcn_*.npz          a9  RecurrentRGCN.predict             src/rrgcn.py:142-194
   score.npz            a11/a12 chunked dist score / CE       hyperbolic_decoder.py:89-307
   rank.npz             f2  get_total_rank / filter_score     rgcn/utils.py:21-166
+  multistep.npz        f2  filtered scores left by get_total_rank -> construct_snap(_r)
+                           (the --multi-step history roll)   rgcn/utils.py:51-75, 367-405;
+                                                             hyperbolic_main.py:116-149
   train_*.npz          f1  get_loss + backward: every parameter gradient   hyperbolic_main.py:585-598
 """
 import os
@@ -494,12 +497,36 @@ def gen_rank():
          mrr=np.array([mrr, mrr_f, mrr_r, mrr_fr]), meta=np.array([V, R]))
 
 
+def gen_multistep():
+    """get_total_rank filters `score` in place; --multi-step builds the next history
+    snapshot from those filtered scores (hyperbolic_main.py:116-149)."""
+    z = np.load(os.path.join(OUT, "rank.npz"))
+    V, R = (int(v) for v in z["meta"])
+    snap = z["snap"]
+    all_tr = torch.from_numpy(z["all_triples"])
+    data = np.concatenate([snap, np.zeros((len(snap), 1), np.int64)], 1)
+    ans_e = rutils.load_all_answers_for_time_filter(data, R, V, False)[0]
+    ans_r = rutils.load_all_answers_for_time_filter(data, R, V, True)[0]
+    # ties at the top would leave torch.sort's order unspecified: shift the scores so the
+    # filtered entries (-1e7) are the only ties, far below every top-k
+    score = torch.from_numpy(z["score"]).clone()
+    score_rel = torch.from_numpy(z["score_rel"]).clone()
+    rutils.get_total_rank(all_tr, score, ans_e, 1000, 0)
+    rutils.get_total_rank(all_tr, score_rel, ans_r, 1000, 1)
+    k = 4
+    snap_e = rutils.construct_snap(all_tr, V, R, score, k)
+    snap_r = rutils.construct_snap_r(all_tr, V, R, score_rel, k)
+    save("multistep.npz", filtered_score=score.numpy(), filtered_score_rel=score_rel.numpy(),
+         snap_e=snap_e, snap_r=snap_r, topk=np.array([k]))
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     which = sys.argv[1:] or ["graph", "ops", "union", "euclid", "lorentz", "models", "rrgcn",
                              "score", "rank", "train"]
     table = {"graph": gen_graph_indexing, "ops": gen_ops, "union": gen_layer_union,
              "euclid": gen_layer_euclid, "lorentz": gen_layer_lorentz, "models": gen_models,
-             "rrgcn": gen_rrgcn, "score": gen_score, "rank": gen_rank, "train": gen_train}
+             "rrgcn": gen_rrgcn, "score": gen_score, "rank": gen_rank, "train": gen_train,
+             "multistep": gen_multistep}
     for w in which:
         table[w]()

@@ -65,8 +65,8 @@ def main():
                 (0.7 * le + 0.3 * lr + ls.sum() + lrad).backward()
                 nb += 1
         else:  # the CLI default: one encoder pass per sample, same gradients
-            parts = m.get_loss_batches(glist, tr, None, True, a.batch)
-            sum(0.7 * le + 0.3 * lr + ls.sum() + lrad for le, lr, ls, lrad in parts).backward()
+            m.get_loss_batches(glist, tr, None, True, a.batch,
+                               combine=lambda le, lr, ls, lrad: 0.7 * le + 0.3 * lr + ls.sum() + lrad)
             nb = 1
         torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
         opt.step()
