@@ -50,6 +50,12 @@ def parse():
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="steps captured per HIP graph (default: the whole pool, replayed as one launch; "
                          "1 = one graph per step)")
+    ap.add_argument("--concurrent", type=int, default=1,
+                    help="independent samples in flight together (one stream each inside the pool's HIP "
+                         "graph): predicts of different test snapshots are independent (hyperbolic_main.py "
+                         ":100-149 without --multi-step), so a server may overlap them")
+    ap.add_argument("--per-layer", action="store_true",
+                    help="run the encoder as per-layer launches instead of the timestep phase launches")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work")
     ap.add_argument("--no-scale", action="store_true",
@@ -149,15 +155,13 @@ def _work(flops, nbytes, ms):
 
 
 def kernel_profile(model, sample, d, device):
-    """Live HIP-event timing of each launch of the hot path on the bench workload: every
-    stage of one timestep on the sample's last history snapshot, and the two decoders on
-    its queries.  Each stage is captured `reps` times into a HIP graph on its own stream and
-    replayed between HIP events on that stream.  Returns {kernel: dict(ms, per_step, ...)}."""
+    """Live HIP-event timing of each launch of the hot path on the bench workload: the three
+    timestep phase launches (csrc/timestep.hip) of the sample's last history snapshot, and
+    the two decoders on its queries.  Each stage is captured `reps` times into a HIP graph on
+    its own stream and replayed between HIP events on that stream.  Returns {kernel:
+    dict(ms, per_step, flops, bytes, ...)}."""
+    from regcn_amd import hyperbolic_model as HM
     from regcn_amd.hyperbolic_decoder import _chunked_hyperbolic_dist_score
-    from regcn_amd.hyperbolic_layers import StepSpec
-    from regcn_amd.hyperbolic_model import relation_gru_step
-    from regcn_amd.tangent import tangent_of
-    from regcn_amd.weights import packed
     hist, glist, test, _ = sample
     glist = [getattr(g, "g", g) for g in glist]  # rank 0 alone: unpartitioned (no collectives)
     g = glist[-1]
@@ -165,51 +169,55 @@ def kernel_profile(model, sample, d, device):
     E = g.number_of_edges()
     T = len(glist)
     n_pos = g.n_pos
+    n_zero = V - n_pos
     st = torch.cuda.Stream(device)
     res = {}
     c = model._c_float()
+    R2 = model.emb_rel.shape[0]
+    lorentz = model.encoder_name == "lgcn"
+    lay0 = model.rgcn.layers[0]
+    tag = "3, %d" % (d // lay0.num_bases if d // lay0.num_bases in (1, 2, 4) else 0) if lorentz else "0, 1"
+    gemm = 2.0 * d * d  # flops per row of one d x d product
+    wn = 0 if lorentz else gemm * n_pos  # union: agg @ W_n
+    gather_b = E * (4 * d + 8 + (0 if lorentz else 4)) + V * 4 * 2
+    row_b = 4.0 * d  # bytes of one fp32 row
     with torch.no_grad(), torch.cuda.stream(st):
-        embs, _, h0, _, _ = model.forward(glist, None, True)
-        h = embs[-2] if len(embs) > 1 else embs[-1]
-        x, r = tangent_of(h, c)
-        lay0, lay1 = model.rgcn.layers[0], model.rgcn.layers[-1]
-        trev = model.temporal_radius_evolution
-        step = StepSpec(x, packed(model.time_gate_weight), model.time_gate_bias.detach(),
-                        model._static_radius(c), trev.radius_mlp.weight.detach().reshape(-1).contiguous(),
-                        trev.radius_mlp.bias.detach().reshape(-1).contiguous(), trev.epsilon, trev.anchor_beta,
-                        model.layer_norm, model.use_residual_evolution, trev.c)
-        h1 = lay0(g, h, h0)
-        lorentz = model.encoder_name == "lgcn"
-        tag = "3, %d" % (d // lay0.num_bases if d // lay0.num_bases in (1, 2, 4) else 0) if lorentz else "0, 1"
-        gather_b = E * (4 * d + 8 + (0 if lorentz else 4)) + V * 4 * 2
-        wn_flops = 0 if lorentz else 2.0 * d * d * n_pos
-        R2 = model.emb_rel.shape[0]
-
-        stages = [
-            ("k_rel_gru", lambda: relation_gru_step(model.relation_gru, model.emb_rel, x, g, h0), 1,
-             2.0 * R2 * 9 * d * d, 4.0 * R2 * d * 3 + 4.0 * 9 * d * d + 4.0 * R2 * d),
-            ("k_layer<%s, false>" % tag, lambda: lay0(g, h, h0), 1,
-             2.0 * d * d * V + wn_flops, gather_b + 4.0 * V * d + 4.0 * V * (2 * d + 1)),
-            ("k_layer<%s, true>" % tag, lambda: lay1(g, h1, h0, step=step), 1,
-             4.0 * d * d * V + wn_flops, gather_b + 8.0 * V * d + 4.0 * V * (2 * d + 2)),
-        ]
+        HM.PHASE_CAPTURE = {}
+        try:
+            embs, _, h0, _, _ = model.forward(glist, None, True)
+            cap = HM.PHASE_CAPTURE
+        finally:
+            HM.PHASE_CAPTURE = None
+        stages = []
+        if cap:
+            stages += [
+                ("k_phase_a", cap["A"][0],
+                 2 * gemm * n_pos + 2.0 * R2 * 3 * d * d,
+                 row_b * n_pos * 3 + 4.0 * R2 * d * 6 + 4.0 * 3 * d * d),
+                ("k_phase_b<%s>" % tag, cap["B"][0],
+                 wn + 2 * gemm * n_zero + 2.0 * R2 * 3 * d * 2 * d,
+                 gather_b + row_b * (3 * n_pos + 2 * n_zero) + 4.0 * R2 * d * 6 + 4.0 * 6 * d * d),
+                ("k_phase_c<%s>" % tag, cap["C"][0],
+                 wn + gemm * (n_pos + n_zero),
+                 gather_b + row_b * (4 * n_pos + 4 * n_zero)),
+            ]
         at = torch.cat([test, torch.stack([test[:, 2], test[:, 1] + model.num_rels, test[:, 0]], 1)])
         B = at.shape[0]
         emb = model._final_embedding(embs[-1], c)
         dec, rdec = model.decoder_ob, model.rdecoder
         q = dec._query(emb, h0, at)
         if type(dec).__name__ == "HyperbolicRotH":
-            stages.append(("k_query<0>", lambda: dec._query(emb, h0, at), 1, 2.0 * B * 3.5 * d * d,
+            stages.append(("k_query<0>", lambda: dec._query(emb, h0, at), 2.0 * B * 3.5 * d * d,
                            4.0 * B * d * 3))
         stages.append(("k_score_f32<0>", lambda: _chunked_hyperbolic_dist_score(
             q, emb, dec.entity_bias, dec.c, 128, 256, score_scale=dec.score_scale_raw,
-            score_margin=dec.score_margin, _raw_scale=True), 1, 2.0 * B * V * d, 4.0 * (B * d + V * d + B * V)))
+            score_margin=dec.score_margin, _raw_scale=True), 2.0 * B * V * d, 4.0 * (B * d + V * d + B * V)))
         if type(rdec).__name__ == "HyperbolicRotHRel":
-            stages.append(("k_query<1> + k_score (relations)", lambda: rdec.forward(emb, h0, at), 1,
+            stages.append(("k_query<1> + k_score (relations)", lambda: rdec.forward(emb, h0, at),
                            2.0 * B * 2 * d * d + 2.0 * B * R2 * d, 4.0 * (B * d * 3 + B * R2)))
-        for name, fn, per_layer_step, flops, nbytes in stages:
+        for name, fn, flops, nbytes in stages:
             ms = event_time(fn, 100, st)
-            per_step = T if name.startswith(("k_rel_gru", "k_layer")) else 1
+            per_step = T if name.startswith("k_phase") else 1
             res[name] = dict(ms=ms, per_step=per_step, flops=flops, bytes=nbytes, **_work(flops, nbytes, ms))
     torch.cuda.synchronize()
     return res
@@ -312,6 +320,7 @@ def main():
     cfg = CONFIGS[args.config]
     d = args.d
     model = build_model(cfg, d, device, seed=1234)          # same weights on every rank
+    model.use_phases = not args.per_layer
     sharded = args.shard != "replica" and world > 1
     # replicas: independent data per rank; sharded: every rank holds the same snapshots
     samples = make_samples(cfg, args.pool, device, seed=100 if sharded else 100 + 7919 * rank,
@@ -324,14 +333,36 @@ def main():
         _, glist, test, _ = samples[i]
         return model.predict(glist, R, None, test, True)
 
+    conc = max(1, min(args.concurrent, len(samples)))
+    lanes = [torch.cuda.Stream(device) for _ in range(conc)] if conc > 1 else []
+
+    def pool_pass(origin):
+        """Every pool sample once; with lanes, sample i on lane i % conc, forked from and
+        joined back into `origin` (a fork/join in the captured graph)."""
+        if not lanes:
+            for i in range(len(samples)):
+                eager(i)
+            return
+        for ln in lanes:
+            ln.wait_stream(origin)
+        for i in range(len(samples)):
+            with torch.cuda.stream(lanes[i % conc]):
+                eager(i)
+        for ln in lanes:
+            origin.wait_stream(ln)
+
     with torch.no_grad():
         for w in range(max(args.warmup, 1)):
             eager(w % len(samples))
+        if lanes:
+            pool_pass(torch.cuda.current_stream(device))
     torch.cuda.synchronize()
     # HIP graphs: one per step (graph_steps = 1), and one holding the whole pool's steps in
     # sequence, so consecutive steps do not pay a graph launch each (~20 us on this runtime)
     graphs, pool_graph = [], None
     gs = args.graph_steps or len(samples)
+    if lanes and (args.no_graph or gs != len(samples)):
+        raise SystemExit("--concurrent needs the whole-pool HIP graph (no --no-graph / --graph-steps)")
     if not args.no_graph:
         cap = torch.cuda.Stream(device)
         with torch.no_grad():
@@ -347,8 +378,7 @@ def main():
                 pool_graph = torch.cuda.CUDAGraph()
                 with torch.cuda.stream(cap):
                     with torch.cuda.graph(pool_graph, stream=cap):
-                        for i in range(len(samples)):
-                            eager(i)
+                        pool_pass(cap)
         for gph in graphs:
             gph.replay()
         if pool_graph is not None:
@@ -410,14 +440,12 @@ def main():
                    for k, v in kern.items()}
         # SURVEY.md §8(d) asks for edges/s per layer and per encoder forward besides the
         # end-to-end step: from the live kernel times (sum of per-step kernel time, no gaps)
-        enc_us = sum(v["ms"] * 1e3 * v["per_step"] for k, v in kern.items() if k.startswith(("k_layer", "k_rel_gru")))
-        lay_us = sum(v["ms"] * 1e3 * v["per_step"] for k, v in kern.items() if k.startswith("k_layer"))
+        enc_us = sum(v["ms"] * 1e3 * v["per_step"] for k, v in kern.items() if k.startswith("k_phase"))
         e_step = float(np.mean(epw))
         breakdown = {"encoder_kernels_us_per_step": round(enc_us, 2),
                      "encoder_M_edges_per_s": round(e_step / enc_us, 3) if enc_us else None,
-                     "layers_kernels_us_per_step": round(lay_us, 2),
-                     "layer_M_edges_per_s": round(e_step / lay_us, 3) if lay_us else None,
-                     "note": "kernel time only (sum of the stage launches' HIP-event averages); value is end to end"}
+                     "note": "kernel time only (sum of the stage launches' HIP-event averages, the phase "
+                             "launches of one timestep x history_len); value is end to end"}
         scale = dec = None
         if not args.no_scale and world == 1:
             scale = aggregation_at_scale(device)
@@ -434,6 +462,8 @@ def main():
                           cfg["per_snap"], "history_len": cfg["T"], "n_layers": 2, "d": d,
                           "edges_per_step": int(np.mean(epw)), "queries_per_step": 2 * cfg["per_snap"],
                           "hip_graph": bool(graphs), "steps_per_graph_launch": len(samples) if pool_graph else 1,
+                          "concurrent_samples": conc, "encoder_launches": "per-layer" if args.per_layer
+                          else "timestep phases",
                           "parallelism": ("%s-partitioned snapshots x%d" % (args.shard, world)) if sharded
                           else "replicas x%d" % world},
                "roofline": roof, "kernels": kernels, "breakdown": breakdown, "aggregation_roofline": scale,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 3
+#define REGCN_ABI_VERSION 4
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -203,6 +203,127 @@ typedef struct regcn_layer_desc {
 } regcn_layer_desc;
 int regcn_layer_f32(const regcn_layer_desc* desc, void* stream);
 
+/* ---- a4-a9: history-window schedule ------------------------------------------------- */
+/* A row without in-edges in any snapshot of the window ("cold") evolves through the T
+ * timesteps by row-local maps of parameters only (its cells' message sums are empty), and
+ * no other row reads it before the decoder (every message source has in-edges: edges are
+ * doubled with inverses, rgcn/utils.py:116-118).
+ * regcn_window_plan_i32: from each snapshot's rows[:n_pos] (pos_rows[t], n_pos[t] host
+ *   arrays of T <= REGCN_MAX_WINDOW), in row order: c_rows (V) = cold rows, u_rows (V) = the
+ *   others, z_rows[t] (T x z_stride, z_stride >= min(V, sum n_pos)) = u rows without in-edges
+ *   at t; counts (device int32[2 + T]) = |C|, |U|, |Z_t|.  flags: V ints of scratch.
+ * regcn_cold_chain_f32: the cold rows through T timesteps of a 2-layer cell + timestep in one
+ *   launch (c_rows, device count n_rows; grid_bound >= that count, e.g. V): per timestep
+ *   layer 0 (x @ w_evolve0), layer 1 (x1 @ w_evolve1, skip gate on x when w_skip1), the
+ *   timestep epilogue (step_* as regcn_layer_desc) -> h_out[t], x_out[t], r_out[t] rows.
+ *   Equal bit for bit to the per-layer launches on those rows. */
+#define REGCN_MAX_WINDOW 16
+int regcn_window_plan_i32(int32_t T, const int32_t* const* pos_rows, const int32_t* n_pos, int32_t V, int32_t* flags,
+                          int32_t* c_rows, int32_t* u_rows, int32_t* z_rows, int32_t z_stride, int32_t* counts,
+                          void* stream);
+typedef struct regcn_chain_desc {
+  const int32_t* rows;
+  const int32_t* n_rows;
+  int32_t T, d, grid_bound;
+  float c;
+  const float* x0;
+  const float* w_evolve0;
+  const float* w_evolve1;
+  const float* w_skip1;
+  const float* b_skip1;
+  const float* step_w_g;
+  const float* step_b_g;
+  const float* step_r_static;
+  const float* step_w_r;
+  const float* step_b_r;
+  float step_eps_r, step_beta;
+  int32_t step_layer_norm, step_residual;
+  float step_c_radius;
+  float* h_out[REGCN_MAX_WINDOW];
+  float* x_out[REGCN_MAX_WINDOW];
+  float* r_out[REGCN_MAX_WINDOW];
+} regcn_chain_desc;
+int regcn_cold_chain_f32(const regcn_chain_desc* desc, void* stream);
+
+/* ---- a2-a9: one timestep of a 2-layer cell in three launches on one stream ---------- */
+/* hyperbolic_model.py:797-869 with HyperbolicRGCNCell / LorentzRGCNCell of 2 layers.  The
+ * per-layer launches (regcn_layer_f32) put each tile's whole layer behind its gather; here
+ * work that needs no gather moves to an earlier launch and the rows without in-edges (whose
+ * layers are row-local maps) ride beside the in-edge tiles:
+ *   phase 0 (A): relation GRU x-half -> gru_h_out (needs gru_pre of this timestep);
+ *                in-edge rows: s1 = x0 @ w_loop[0], tw = clamp(x0) @ W_g
+ *   phase 1 (B): in-edge tiles: layer-0 gather with rel = h_0 -> x1, r1;
+ *                other rows: layers 0 and 1 -> h2, n2;  GRU pre-half of the next timestep
+ *                (gru_h_prev = h_0 of this timestep -> gru_pre) unless gru_pre is NULL
+ *   phase 2 (C): in-edge tiles: layer-1 gather (x1, r1) + self loop + skip + timestep
+ *                epilogue; other rows: timestep epilogue on h2 -> step_h/x/r_out.
+ * Field meanings follow regcn_layer_desc (snapshot lists, packed weights, step_*); [0] / [1]
+ * are layer 0 / layer 1.  s1, tw, x1, h2 are V x d and r1, n2 V floats of caller scratch.
+ * Rows with in-degree > budget read agg[l] (chunked pre-aggregation of layer l, run
+ * between the phases).  Each row's values equal regcn_layer_f32 (layer 0) then
+ * regcn_layer_f32 with fuse_step (layer 1) bit for bit. */
+typedef struct regcn_phase_desc {
+  int32_t agg_mode, num_bases;
+  float gamma, c;
+  const int32_t* rowptr;
+  const int32_t* col_src;
+  const int32_t* col_type;
+  const float* norm;
+  int32_t budget;
+  const int32_t* tiles;
+  int32_t n_pos_tiles;
+  const int32_t* item_ptr;
+  const int32_t* item_src;
+  const int32_t* item_tl;
+  const int32_t* rows;
+  int32_t n_pos, V, d;
+  const float* rel;        /* h_0 of this timestep (both layers' messages) */
+  const float* w_rel[2];
+  const float* agg[2];
+  const float* w_n[2];
+  const float* w_loop[2];
+  const float* w_evolve[2];
+  const float* w_skip1;    /* layer-1 skip gate on the cell input (LorentzRGCNCell), or NULL */
+  const float* b_skip1;
+  const float* x0;         /* log0(h_prev) */
+  const float* r0;         /* |h_prev| */
+  float* s1;
+  float* tw;
+  float* x1;
+  float* r1;
+  float* h2;
+  float* n2;
+  const float* step_w_g;
+  const float* step_b_g;
+  const float* step_r_static;
+  const float* step_w_r;
+  const float* step_b_r;
+  float step_eps_r, step_beta;
+  int32_t step_layer_norm, step_residual;
+  float step_c_radius;
+  float* step_h_out;
+  float* step_x_out;
+  float* step_r_out;
+  const int32_t* gru_rel_idx;
+  const int32_t* gru_rel_start;
+  const float* gru_rel_count;
+  const float* gru_x_mean;
+  const float* gru_emb_rel;
+  const float* gru_h_prev;
+  const float* gru_w_ih_e;
+  const float* gru_w_ih_x;
+  const float* gru_w_hh;
+  const float* gru_b_ih;
+  const float* gru_b_hh;
+  int32_t gru_R2;
+  float* gru_pre;
+  float* gru_h_out;
+  const int32_t* zrows;   /* rows without in-edges to run: NULL = rows[n_pos:V]; else a list */
+  const int32_t* zcount;  /*   of *zcount rows (device count, e.g. a window plan's |Z_t|) */
+  int32_t zbound;         /*   bounded by zbound (host) */
+} regcn_phase_desc;
+int regcn_timestep_phase_f32(const regcn_phase_desc* desc, int32_t phase, void* stream);
+
 /* ---- a7: relation evolution (segment mean + GRUCell in one launch) ------------------- */
 /* nn.Linear-layout packing for the relation GRU: W is (n_gates * n_out) x n_in row-major
  * (GRUCell weight_ih: 3d x 2d, weight_hh: 3d x d); packed[g][b][jt][lane][e] =
@@ -219,6 +340,21 @@ int regcn_relation_gru_f32(const float* x, const int32_t* rel_idx, const int32_t
                            const float* x_mean, const float* emb_rel, const float* h_prev, const float* w_ih,
                            const float* w_hh, const float* b_ih, const float* b_hh, int32_t R2, int32_t d,
                            float* h_out, void* stream);
+
+/* The same GRU in two launches, split by what each input depends on.  w_ih_e / w_ih_x are
+ * the emb_rel and x_mean column halves of GRUCell.weight_ih (each 3d x d, packed with
+ * regcn_pack_linear_f32(n_gates = 3, n_out = d, n_in = d)).
+ * regcn_relation_gru_pre_f32: pre[r] = {W_ir^e e + b_ir + W_hr h + b_hr, (z likewise),
+ *   W_in^e e + b_in, W_hn h + b_hn} (R2 x 4 x d) from emb_rel and h_prev only, so it can
+ *   run while the previous timestep's entity rows are still being computed.
+ * regcn_relation_gru_x_f32: x_mean as in regcn_relation_gru_f32, then r = s(pre0 + W_ir^x m),
+ *   z = s(pre1 + W_iz^x m), n = tanh(pre2 + W_in^x m + r pre3), h_out = (1 - z) n + z h_prev. */
+int regcn_relation_gru_pre_f32(const float* emb_rel, const float* h_prev, const float* w_ih_e, const float* w_hh,
+                               const float* b_ih, const float* b_hh, int32_t R2, int32_t d, float* pre,
+                               void* stream);
+int regcn_relation_gru_x_f32(const float* x, const int32_t* rel_idx, const int32_t* rel_start,
+                             const float* rel_count, const float* x_mean, const float* h_prev, const float* w_ih_x,
+                             const float* pre, int32_t R2, int32_t d, float* h_out, void* stream);
 
 /* ---- a8: per-timestep entity evolution (MFMA time gate + fused row epilogue) --------- */
 /* hyperbolic_model.py:829-869 + TemporalRadiusEvolution.forward (hyperbolic_ops.py:395-435):

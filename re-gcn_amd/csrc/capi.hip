@@ -158,6 +158,152 @@ int regcn_layer_tail_f32(const float* agg, const float* w_n, const float* x, con
   return layer(a, ST(s));
 }
 
+int regcn_window_plan_i32(int32_t T, const int32_t* const* pos_rows, const int32_t* n_pos, int32_t V, int32_t* flags,
+                          int32_t* c_rows, int32_t* u_rows, int32_t* z_rows, int32_t z_stride, int32_t* counts,
+                          void* s) {
+  if (T < 1 || T > REGCN_MAX_WINDOW || !pos_rows || !n_pos) return set_error(REGCN_EINVAL, "bad window");
+  PlanArgs a{};
+  a.T = T;
+  a.V = V;
+  for (int t = 0; t < T; ++t) {
+    a.pos_rows[t] = pos_rows[t];
+    a.n_pos[t] = n_pos[t];
+  }
+  a.flags = flags;
+  a.c_rows = c_rows;
+  a.u_rows = u_rows;
+  a.z_rows = z_rows;
+  a.z_stride = z_stride;
+  a.counts = counts;
+  return window_plan(a, ST(s));
+}
+
+int regcn_cold_chain_f32(const regcn_chain_desc* g, void* s) {
+  if (!g) return set_error(REGCN_EINVAL, "null descriptor");
+  ChainArgs a{};
+  a.rows = g->rows;
+  a.n_rows = g->n_rows;
+  a.T = g->T;
+  a.d = g->d;
+  a.x0 = g->x0;
+  a.w_evolve0 = g->w_evolve0;
+  a.w_evolve1 = g->w_evolve1;
+  a.w_skip1 = g->w_skip1;
+  a.b_skip1 = g->b_skip1;
+  a.k = make_curv(g->c);
+  StepArgs& t = a.step;
+  t.x_prev = g->x0;
+  t.w_g = g->step_w_g;
+  t.b_g = g->step_b_g;
+  t.r_static = g->step_r_static;
+  t.w_r = g->step_w_r;
+  t.b_r = g->step_b_r;
+  t.eps_r = g->step_eps_r;
+  t.beta = g->step_beta;
+  t.layer_norm = g->step_layer_norm;
+  t.residual = g->step_residual;
+  t.d = g->d;
+  t.k = a.k;
+  t.k_rad = make_curv(g->step_c_radius);
+  for (int i = 0; i < REGCN_MAX_WINDOW; ++i) {
+    a.h_out[i] = g->h_out[i];
+    a.x_out[i] = g->x_out[i];
+    a.r_out[i] = g->r_out[i];
+  }
+  return cold_chain(a, g->grid_bound, ST(s));
+}
+
+int regcn_timestep_phase_f32(const regcn_phase_desc* g, int32_t phase, void* s) {
+  if (!g) return set_error(REGCN_EINVAL, "null descriptor");
+  PhaseArgs a{};
+  const Curv k = make_curv(g->c);
+  for (int i = 0; i < 2; ++i) {
+    LayerArgs& l = a.L[i];
+    l.agg_mode = g->agg_mode;
+    l.nb = g->num_bases;
+    l.gamma = g->gamma;
+    l.rowptr = g->rowptr;
+    l.col_src = g->col_src;
+    l.col_type = g->col_type;
+    l.norm = g->norm;
+    l.budget = g->budget;
+    l.tiles = g->tiles;
+    l.n_pos_tiles = g->n_pos_tiles;
+    l.item_ptr = g->item_ptr;
+    l.item_src = g->item_src;
+    l.item_tl = g->item_tl;
+    l.rows = g->rows;
+    l.n_pos = g->n_pos;
+    l.V = g->V;
+    l.d = g->d;
+    l.k = k;
+    l.rel = g->rel;
+    l.w_rel = g->w_rel[i];
+    l.agg = g->agg[i];
+    l.w_n = g->w_n[i];
+    l.w_loop = g->w_loop[i];
+    l.w_evolve = g->w_evolve[i];
+  }
+  a.L[0].x = g->x0;
+  a.L[0].radius = g->r0;
+  a.L[1].x = g->x1;
+  a.L[1].radius = g->r1;
+  if (g->w_skip1) {
+    a.L[1].prev_t = g->x0;
+    a.L[1].w_skip = g->w_skip1;
+    a.L[1].b_skip = g->b_skip1;
+  }
+  StepArgs& t = a.step;
+  t.x_prev = g->x0;
+  t.w_g = g->step_w_g;
+  t.b_g = g->step_b_g;
+  t.r_static = g->step_r_static;
+  t.w_r = g->step_w_r;
+  t.b_r = g->step_b_r;
+  t.eps_r = g->step_eps_r;
+  t.beta = g->step_beta;
+  t.layer_norm = g->step_layer_norm;
+  t.residual = g->step_residual;
+  t.V = g->V;
+  t.d = g->d;
+  t.k = k;
+  t.k_rad = make_curv(g->step_c_radius);
+  t.h_out = g->step_h_out;
+  t.x_out = g->step_x_out;
+  t.r_out = g->step_r_out;
+  if (t.residual && (!t.w_r || !t.b_r)) return set_error(REGCN_EINVAL, "residual radius needs w_r and b_r");
+  if (!t.r_static || !t.b_g) return set_error(REGCN_EINVAL, "null timestep pointer");
+  RelGru2Args& r = a.gru;
+  r.x = g->x0;
+  r.rel_idx = g->gru_rel_idx;
+  r.rel_start = g->gru_rel_start;
+  r.rel_count = g->gru_rel_count;
+  r.x_mean = g->gru_x_mean;
+  r.emb_rel = g->gru_emb_rel;
+  r.h_prev = g->gru_h_prev;
+  r.w_ih_e = g->gru_w_ih_e;
+  r.w_ih_x = g->gru_w_ih_x;
+  r.w_hh = g->gru_w_hh;
+  r.b_ih = g->gru_b_ih;
+  r.b_hh = g->gru_b_hh;
+  r.R2 = g->gru_R2;
+  r.d = g->d;
+  r.pre = g->gru_pre;
+  r.h_out = g->gru_h_out;
+  a.zrows = g->zrows;
+  a.zcount = g->zcount;
+  a.zbound = g->zbound;
+  if (a.zrows && (!a.zcount || a.zbound < 0)) return set_error(REGCN_EINVAL, "a zero-row list needs its count and bound");
+  a.d = g->d;
+  a.s1 = g->s1;
+  a.tw = g->tw;
+  a.x1 = g->x1;
+  a.r1 = g->r1;
+  a.h2 = g->h2;
+  a.n2 = g->n2;
+  return timestep_phase(a, phase, ST(s));
+}
+
 int regcn_layer_f32(const regcn_layer_desc* g, void* s) {
   if (!g) return set_error(REGCN_EINVAL, "null descriptor");
   LayerArgs a{};
@@ -245,6 +391,39 @@ int regcn_relation_gru_f32(const float* x, const int32_t* rel_idx, const int32_t
                            float* h_out, void* s) {
   RelGruArgs a{x, rel_idx, rel_start, rel_count, x_mean, emb_rel, h_prev, w_ih, w_hh, b_ih, b_hh, R2, d, h_out};
   return rel_gru(a, ST(s));
+}
+
+int regcn_relation_gru_pre_f32(const float* emb_rel, const float* h_prev, const float* w_ih_e, const float* w_hh,
+                               const float* b_ih, const float* b_hh, int32_t R2, int32_t d, float* pre, void* s) {
+  RelGru2Args a{};
+  a.emb_rel = emb_rel;
+  a.h_prev = h_prev;
+  a.w_ih_e = w_ih_e;
+  a.w_hh = w_hh;
+  a.b_ih = b_ih;
+  a.b_hh = b_hh;
+  a.R2 = R2;
+  a.d = d;
+  a.pre = pre;
+  return rel_gru_pre(a, ST(s));
+}
+
+int regcn_relation_gru_x_f32(const float* x, const int32_t* rel_idx, const int32_t* rel_start,
+                             const float* rel_count, const float* x_mean, const float* h_prev, const float* w_ih_x,
+                             const float* pre, int32_t R2, int32_t d, float* h_out, void* s) {
+  RelGru2Args a{};
+  a.x = x;
+  a.rel_idx = rel_idx;
+  a.rel_start = rel_start;
+  a.rel_count = rel_count;
+  a.x_mean = x_mean;
+  a.h_prev = h_prev;
+  a.w_ih_x = w_ih_x;
+  a.pre = const_cast<float*>(pre);
+  a.R2 = R2;
+  a.d = d;
+  a.h_out = h_out;
+  return rel_gru_x(a, ST(s));
 }
 
 int regcn_roth_query_f32(const float* ent, const float* rel, const int64_t* trip, int32_t n_test, int32_t B,

@@ -161,6 +161,78 @@ struct RelGruArgs {
   int64_t* trace;  // profiling stamps (g_trace at launch), or null
 };
 
+// Two-phase relation GRU (relgru.hip k_gru_pre / k_gru_x).
+struct RelGru2Args {
+  const float* x;          // V x d entity tangent rows (x_mean source)
+  const int* rel_idx;
+  const int* rel_start;
+  const float* rel_count;
+  const float* x_mean;     // R2 x d precomputed means, or null (gathered in-kernel)
+  const float* emb_rel;    // R2 x d
+  const float* h_prev;     // R2 x d GRU state
+  const float* w_ih_e;     // packed (3 gates, d x d): W_ih[:, :d]
+  const float* w_ih_x;     // packed (3 gates, d x d): W_ih[:, d:]
+  const float* w_hh;       // packed (3 gates, d x d)
+  const float* b_ih;
+  const float* b_hh;
+  int R2, d;
+  float* pre;              // R2 x 4 x d gate partials (k_gru_pre out, k_gru_x in)
+  float* h_out;
+};
+int rel_gru_pre(const RelGru2Args& a, hipStream_t st);
+int rel_gru_x(const RelGru2Args& a, hipStream_t st);
+
+// History-window plan and the cold-row chain (window.hip).
+struct PlanArgs {
+  int T, V;
+  const int* pos_rows[REGCN_MAX_WINDOW];  // rows[:n_pos] of each snapshot
+  int n_pos[REGCN_MAX_WINDOW];
+  int* flags;    // V scratch
+  int* c_rows;   // V: rows without in-edges in every snapshot
+  int* u_rows;   // V: the others
+  int* z_rows;   // T x z_stride: U rows without in-edges at t
+  int z_stride;
+  int* counts;   // 2 + T: |C|, |U|, |Z_t|
+};
+int window_plan(const PlanArgs& a, hipStream_t st);
+
+struct ChainArgs {
+  const int* rows;     // C rows
+  const int* n_rows;   // device count
+  int T, d;
+  const float* x0;     // log0(h_init) rows
+  const float* w_evolve0;
+  const float* w_evolve1;
+  const float* w_skip1;
+  const float* b_skip1;
+  Curv k;
+  StepArgs step;       // per-timestep outputs below
+  float* h_out[REGCN_MAX_WINDOW];
+  float* x_out[REGCN_MAX_WINDOW];
+  float* r_out[REGCN_MAX_WINDOW];
+};
+int cold_chain(const ChainArgs& a, int grid_bound, hipStream_t st);
+
+// One timestep of a 2-layer cell in three phase launches (timestep.hip).
+struct PhaseArgs {
+  LayerArgs L[2];     // layer 0 / 1: snapshot lists, inputs (x, radius, rel, prev_t), weights
+  StepArgs step;      // x_prev = x0 (the timestep input), outputs h/x/r
+  RelGru2Args gru;    // phase A: x-half of this timestep's GRU; phase B: pre-half of the next
+  int d;
+  float* s1;          // V x d: x0 @ W_loop[0] (in-edge rows)
+  float* tw;          // V x d: clamp(x0) @ W_g (in-edge rows)
+  float* x1;          // V x d: layer-0 output tangent rows
+  float* r1;          // V: |layer-0 output|
+  float* h2;          // V x d: layer-1 output of rows without in-edges (Poincare)
+  float* n2;          // V: its |.|^2 as the epilogue carries it
+  const int* zrows;   // rows without in-edges to run (NULL: rows[n_pos:V]); with a device count:
+  const int* zcount;  //   *zcount rows, at most zbound
+  int zbound;
+  int n_pos_rt, n_zero_rt, n_gru, gru_rt;  // block counts (set by the launcher)
+  int64_t* trace;     // profiling (regcn_set_trace): {start, end} s_memrealtime per workgroup
+};
+int timestep_phase(PhaseArgs a, int phase, hipStream_t st);
+
 // RotH decoder queries (query.hip).  Linear weights are packed transposed (x @ W^T).
 struct QueryArgs {
   const float* ent;         // V x d final entity embedding

@@ -24,6 +24,7 @@
 #include "gather.h"
 #include "regcn_internal.h"
 #include "rowtile.h"
+#include "gru_parts.h"
 
 namespace regcn {
 
@@ -32,7 +33,6 @@ namespace regcn {
 constexpr int IH_WAVES = 4, HH_WAVES = 2;
 constexpr int GW = IH_WAVES + HH_WAVES;  // waves per workgroup (waves 0-3 finish C registers 0-3)
 constexpr int GTHR = 64 * GW;
-constexpr int GR4 = 4;  // k-blocks (16 k-steps each) of operands in flight per wave
 
 // A tile row stride: >= 3d + 16 (a zero tail for the last k-block of W_hh) and = 8 (mod 16),
 // which makes the ds_read_b128 fragment reads below bank-conflict free.
@@ -186,6 +186,40 @@ __global__ __launch_bounds__(GTHR) void k_rel_gru(RelGruArgs p) {
     p.h_out[(int64_t)(r0 + i) * d + n] = (1.f - z) * nn + z * h;
   }
   stamp(4);
+}
+
+// ============================================================ two-phase relation GRU (gru_parts.h)
+__global__ __launch_bounds__(64 * PRE_WAVES) void k_gru_pre(RelGru2Args p) {
+  extern __shared__ float lds[];
+  gru_pre_block(p, blockIdx.x, blockIdx.y, lds);
+}
+
+__global__ __launch_bounds__(64 * X_WAVES) void k_gru_x(RelGru2Args p) {
+  extern __shared__ float lds[];
+  gru_x_block(p, blockIdx.x, blockIdx.y, lds);
+}
+
+int rel_gru_pre(const RelGru2Args& a, hipStream_t st) {
+  if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "relation GRU needs d %% 4 == 0, d <= 256");
+  if (!a.emb_rel || !a.h_prev || !a.w_ih_e || !a.w_hh || !a.b_ih || !a.b_hh || !a.pre)
+    return set_error(REGCN_EINVAL, "null pointer");
+  if (a.R2 == 0) return 0;
+  dim3 grid((unsigned)((a.R2 + TM - 1) / TM), (unsigned)(gru_dpad(a.d) / 16));
+  const size_t lds = gru_pre_lds_bytes(a.d);
+  hipLaunchKernelGGL(k_gru_pre, grid, dim3(64 * PRE_WAVES), lds, st, a);
+  return check_launch("k_gru_pre");
+}
+
+int rel_gru_x(const RelGru2Args& a, hipStream_t st) {
+  if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "relation GRU needs d %% 4 == 0, d <= 256");
+  if (!a.h_prev || !a.w_ih_x || !a.pre || !a.h_out) return set_error(REGCN_EINVAL, "null pointer");
+  if (!a.x_mean && (!a.x || !a.rel_start || !a.rel_count))
+    return set_error(REGCN_EINVAL, "relation GRU needs x_mean or the r_to_e spans");
+  if (a.R2 == 0) return 0;
+  dim3 grid((unsigned)((a.R2 + TM - 1) / TM), (unsigned)(gru_dpad(a.d) / 16));
+  const size_t lds = gru_x_lds_bytes(a.d);
+  hipLaunchKernelGGL(k_gru_x, grid, dim3(64 * X_WAVES), lds, st, a);
+  return check_launch("k_gru_x");
 }
 
 // Wp[g][b][jt][lane][e] = W[g*n_out + 16 jt + lane%16][16 b + 4 (lane/16) + e]  (zero padded)

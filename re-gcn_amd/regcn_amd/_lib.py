@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libregcn_hip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -51,10 +51,15 @@ _SIGS = {
     "regcn_rank_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
     "regcn_rank_count_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
     "regcn_layer_f32": [P, P],
+    "regcn_timestep_phase_f32": [P, _c_int, P],
+    "regcn_window_plan_i32": [_c_int, P, P, _c_int, P, P, P, P, _c_int, P, P],
+    "regcn_cold_chain_f32": [P, P],
     "regcn_partial_sum_f32": [P, _c_int, P, _c_int, _c_int, P, _c_int, P],
     "regcn_packed_linear_floats": [_c_int, _c_int, _c_int],
     "regcn_pack_linear_f32": [P, _c_int, _c_int, _c_int, P, P],
     "regcn_relation_gru_f32": [P, P, P, P, P, P, P, P, P, P, P, _c_int, _c_int, P, P],
+    "regcn_relation_gru_pre_f32": [P, P, P, P, P, P, _c_int, _c_int, P, P],
+    "regcn_relation_gru_x_f32": [P, P, P, P, P, P, P, P, _c_int, _c_int, P, P],
     "regcn_roth_query_f32": [P, P, P, _c_int, _c_int, _c_int, P, P, P, P, P, P, P, P, _c_int, _c_f, P, P],
     "regcn_roth_rel_query_f32": [P, P, _c_int, _c_int, _c_int, P, P, P, P, P, P, _c_int, _c_int, _c_f, P, P, P],
     "regcn_snapshot_workspace_bytes": [_c_i64, _c_int, _c_int],
@@ -96,6 +101,37 @@ class LayerDesc(ctypes.Structure):
         ("step_r_static", P), ("step_w_r", P), ("step_b_r", P), ("step_eps_r", _c_f), ("step_beta", _c_f),
         ("step_layer_norm", _c_int), ("step_residual", _c_int), ("step_c_radius", _c_f), ("step_h_out", P),
         ("step_x_out", P), ("step_r_out", P), ("trace", P),
+    ]
+
+
+class PhaseDesc(ctypes.Structure):
+    """regcn_phase_desc (include/regcn_hip.h)."""
+    _fields_ = [
+        ("agg_mode", _c_int), ("num_bases", _c_int), ("gamma", _c_f), ("c", _c_f), ("rowptr", P), ("col_src", P),
+        ("col_type", P), ("norm", P), ("budget", _c_int), ("tiles", P), ("n_pos_tiles", _c_int), ("item_ptr", P),
+        ("item_src", P), ("item_tl", P), ("rows", P), ("n_pos", _c_int), ("V", _c_int), ("d", _c_int), ("rel", P),
+        ("w_rel", P * 2), ("agg", P * 2), ("w_n", P * 2), ("w_loop", P * 2), ("w_evolve", P * 2), ("w_skip1", P),
+        ("b_skip1", P), ("x0", P), ("r0", P), ("s1", P), ("tw", P), ("x1", P), ("r1", P), ("h2", P), ("n2", P),
+        ("step_w_g", P), ("step_b_g", P), ("step_r_static", P), ("step_w_r", P), ("step_b_r", P),
+        ("step_eps_r", _c_f), ("step_beta", _c_f), ("step_layer_norm", _c_int), ("step_residual", _c_int),
+        ("step_c_radius", _c_f), ("step_h_out", P), ("step_x_out", P), ("step_r_out", P),
+        ("gru_rel_idx", P), ("gru_rel_start", P), ("gru_rel_count", P), ("gru_x_mean", P), ("gru_emb_rel", P),
+        ("gru_h_prev", P), ("gru_w_ih_e", P), ("gru_w_ih_x", P), ("gru_w_hh", P), ("gru_b_ih", P), ("gru_b_hh", P),
+        ("gru_R2", _c_int), ("gru_pre", P), ("gru_h_out", P), ("zrows", P), ("zcount", P), ("zbound", _c_int),
+    ]
+
+
+MAX_WINDOW = 16  # REGCN_MAX_WINDOW
+
+
+class ChainDesc(ctypes.Structure):
+    """regcn_chain_desc (include/regcn_hip.h)."""
+    _fields_ = [
+        ("rows", P), ("n_rows", P), ("T", _c_int), ("d", _c_int), ("grid_bound", _c_int), ("c", _c_f), ("x0", P),
+        ("w_evolve0", P), ("w_evolve1", P), ("w_skip1", P), ("b_skip1", P), ("step_w_g", P), ("step_b_g", P),
+        ("step_r_static", P), ("step_w_r", P), ("step_b_r", P), ("step_eps_r", _c_f), ("step_beta", _c_f),
+        ("step_layer_norm", _c_int), ("step_residual", _c_int), ("step_c_radius", _c_f),
+        ("h_out", P * MAX_WINDOW), ("x_out", P * MAX_WINDOW), ("r_out", P * MAX_WINDOW),
     ]
 
 

@@ -81,14 +81,15 @@ class StepSpec:
 
 
 def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip, drop_mask, c,
-              euclid=False, step=None, agg=None, out=None):
+              euclid=False, step=None, agg=None, out=None, pos_only=False):
     """One fused layer launch (regcn_layer_f32): inline gather + GEMMs + epilogue, or with
     `step` the timestep too.  Returns (h, x_next, r_next) of the layer (or of the step).
     `g` may be a rank's view of a snapshot (parallel.py): the launch covers its rows only,
     writing them into full-size outputs (`out`, optional preallocated (h, x, r)).
-    agg (with mode AGG_NONE): the finished aggregation of every in-degree > 0 row."""
+    agg (with mode AGG_NONE): the finished aggregation of every in-degree > 0 row.
+    pos_only: the launch covers the rows with in-edges only (rows[:n_pos])."""
     if isinstance(g, ShardedGraph):  # multi-GPU partition of the snapshot (parallel.py)
-        if agg is not None or out is not None:
+        if agg is not None or out is not None or pos_only:
             raise ValueError("agg/out are managed by the sharded layer")
         return g.run_layer(mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
                            drop_mask, c, euclid=euclid, step=step)
@@ -100,6 +101,8 @@ def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_
         agg = _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c)
     elif mode != _lib.AGG_NONE:
         raise ValueError("a precomputed aggregation needs mode AGG_NONE")
+    if g.n_pos == 0:  # an edgeless snapshot: nothing to gather, every row takes the evolve loop
+        mode = _lib.AGG_NONE
     if out is None:
         h = torch.empty_like(x)
         xn = torch.empty_like(x)
@@ -131,7 +134,7 @@ def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_
     desc.b_skip = a(b_skip)
     desc.drop_mask = a(drop_mask)
     desc.rows = a(wk["rows"], torch.int32)
-    desc.n_pos, desc.V, desc.d, desc.euclid = g.n_pos, n_rows, d, int(bool(euclid))
+    desc.n_pos, desc.V, desc.d, desc.euclid = g.n_pos, g.n_pos if pos_only else n_rows, d, int(bool(euclid))
     desc.c = float(c)
     if step is None:
         desc.h_out, desc.x_next, desc.r_next = a(h), a(xn), a(rn)
@@ -184,8 +187,9 @@ class HyperbolicUnionRGCNLayer(nn.Module):
             self.skip_bias = nn.Parameter(torch.zeros(out_feat))
         self.dropout = nn.Dropout(dropout) if dropout > 0 else None
 
-    def forward(self, g, h_hyper, rel_emb, prev_h=None, step=None):
-        """hyperbolic_layers.py:242-323 (one fused launch; `step` fuses the timestep)."""
+    def forward(self, g, h_hyper, rel_emb, prev_h=None, step=None, pos_only=False, out=None):
+        """hyperbolic_layers.py:242-323 (one fused launch; `step` fuses the timestep;
+        pos_only/out: see run_layer)."""
         if self.activation is None:
             raise NotImplementedError("the fused tail applies rrelu; activation=None is not supported")
         self.rel_emb = rel_emb
@@ -200,7 +204,7 @@ class HyperbolicUnionRGCNLayer(nn.Module):
                               self.weight_neighbor, wl, we, prev_t,
                               self.skip_weight if prev_t is not None else None,
                               self.skip_bias.detach() if prev_t is not None else None,
-                              _drop_mask(self, x), c, step=step)
+                              _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only)
         return attach(h, xn, rn, c)
 
 
@@ -235,8 +239,9 @@ class LorentzRGCNLayer(nn.Module):
         self.dropout = nn.Dropout(dropout) if dropout > 0 else None
         self.rel_emb = None
 
-    def forward(self, g, h_hyper, rel_emb=None, prev_h=None, step=None):
-        """hyperbolic_layers.py:627-694 (one fused launch; `step` fuses the timestep)."""
+    def forward(self, g, h_hyper, rel_emb=None, prev_h=None, step=None, pos_only=False, out=None):
+        """hyperbolic_layers.py:627-694 (one fused launch; `step` fuses the timestep;
+        pos_only/out: see run_layer)."""
         if self.activation is None:
             raise NotImplementedError("the fused tail applies rrelu; activation=None is not supported")
         if self.submat_in * self.num_bases != self.in_feat:
@@ -260,7 +265,7 @@ class LorentzRGCNLayer(nn.Module):
                               None, wl, we, prev_t,
                               self.skip_weight if prev_t is not None else None,
                               self.skip_bias.detach() if prev_t is not None else None,
-                              _drop_mask(self, x), c, step=step)
+                              _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only)
         return attach(h, xn, rn, c)
 
 
@@ -278,15 +283,18 @@ class LorentzRGCNCell(nn.Module):
             self.layers.append(LorentzRGCNLayer(h_dim, h_dim, num_rels, num_bases, c=c, activation=F.rrelu,
                                                 self_loop=self_loop, dropout=dropout, skip_connect=sc))
 
-    def forward(self, g, init_ent_emb, init_rel_emb, step=None):
+    def forward(self, g, init_ent_emb, init_rel_emb, step=None, pos_only=False, out=None):
         """`step` (StepSpec): run the timestep fused into the last layer's launch and
-        return its output instead of the cell output."""
+        return its output instead of the cell output.  pos_only/out (with step): the
+        launches cover the rows with in-edges only, the last one writing into `out`."""
         h = init_ent_emb  # node ids are arange(V) (rgcn/utils.py:122): the gather is the identity
         rel_embs = init_rel_emb if isinstance(init_rel_emb, list) else [init_rel_emb] * len(self.layers)
         prev_h = None
         n = len(self.layers)
         for i, layer in enumerate(self.layers):
-            h_new = layer(g, h, rel_embs[i], prev_h=prev_h, step=step if i == n - 1 else None)
+            last = i == n - 1
+            h_new = layer(g, h, rel_embs[i], prev_h=prev_h, step=step if last else None, pos_only=pos_only,
+                          out=out if last else None)
             prev_h = h
             h = h_new
         return h

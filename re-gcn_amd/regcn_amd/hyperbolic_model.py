@@ -14,6 +14,7 @@ Scope: eval/forward.  Static graph (--add-static-graph), EST components, FHNN/HG
 encoders and geoopt manifold parameters are out of scope and raise.
 """
 import contextlib
+import ctypes
 import logging
 import math
 
@@ -24,12 +25,16 @@ import torch.nn.functional as F
 from . import _lib
 from .hyperbolic_decoder import (HyperbolicAttH, HyperbolicAttHRel, HyperbolicConvTransE, HyperbolicConvTransR,
                                  HyperbolicMuRP, HyperbolicMuRPRel, HyperbolicRotH, HyperbolicRotHRel)
-from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell, StepSpec
+from .graph import SnapshotGraph
+from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell, LorentzRGCNLayer, StepSpec, \
+    _heavy_aggregate
 from .hyperbolic_ops import HyperbolicOps, TemporalRadiusEvolution
 from .tangent import attach, tangent_of
 from .weights import invalidate, packed
 
 logger = logging.getLogger("hyperbolic_model")
+PHASE_TRACE = None  # profiling: a list to collect per-workgroup stamps of the phase launches
+PHASE_CAPTURE = None  # profiling: a dict to receive replayable launches of the last timestep's phases
 GEOOPT_AVAILABLE = False
 
 
@@ -60,14 +65,16 @@ class HyperbolicRGCNCell(HyperbolicBaseRGCN):
                                         activation=F.rrelu, self_loop=self.self_loop, dropout=self.dropout,
                                         skip_connect=sc, radius_msg_gamma=self.radius_msg_gamma)
 
-    def forward(self, g, init_ent_emb, init_rel_emb, step=None):
-        """`step` (StepSpec): the timestep runs fused into the last layer's launch."""
+    def forward(self, g, init_ent_emb, init_rel_emb, step=None, pos_only=False, out=None):
+        """`step` (StepSpec): the timestep runs fused into the last layer's launch;
+        pos_only/out: the launches cover the rows with in-edges only (run_layer)."""
         h = init_ent_emb  # node ids are arange(V): the reference gather is the identity
         rel_embs = init_rel_emb if isinstance(init_rel_emb, list) else [init_rel_emb] * len(self.layers)
         n = len(self.layers)
         for i, layer in enumerate(self.layers):
             # prev_h is never passed (hyperbolic_model.py:152)
-            h = layer(g, h, rel_embs[i], step=step if i == n - 1 else None)
+            last = i == n - 1
+            h = layer(g, h, rel_embs[i], step=step if last else None, pos_only=pos_only, out=out if last else None)
         return h
 
 
@@ -108,8 +115,75 @@ def relation_gru_step(gru, emb_rel, x, g, h_prev):
     return out
 
 
+PLAN_MAX_V = 1 << 18  # the plan's list compaction runs in one workgroup
+
+
+def window_plan(g_list, V):
+    """regcn_window_plan_i32 over the window's snapshots (device lists, device counts):
+    c_rows = rows with no in-edge in any snapshot, z_rows[t] = the other rows without
+    in-edges at t; counts = (|C|, |U|, |Z_0|, ...)."""
+    dev = g_list[0].work()["rows"].device
+    T = len(g_list)
+    zs = max(1, min(V, sum(g.n_pos for g in g_list)))
+    i32 = torch.int32
+    plan = {"flags": torch.empty(V, device=dev, dtype=i32), "c_rows": torch.empty(V, device=dev, dtype=i32),
+            "u_rows": torch.empty(V, device=dev, dtype=i32), "z_rows": torch.empty(T * zs, device=dev, dtype=i32),
+            "counts": torch.empty(2 + T, device=dev, dtype=i32), "z_stride": zs}
+    rows = (ctypes.c_void_p * T)(*[g.work()["rows"].data_ptr() for g in g_list])
+    n_pos = (ctypes.c_int32 * T)(*[g.n_pos for g in g_list])
+    a = _lib.addr
+    _lib.call("regcn_window_plan_i32", T, rows, n_pos, V, a(plan["flags"], i32), a(plan["c_rows"], i32),
+              a(plan["u_rows"], i32), a(plan["z_rows"], i32), zs, a(plan["counts"], i32), _lib.stream())
+    return plan
+
+
+def _gru_biases(gru, d, device):
+    zeros = None
+    if gru.bias_ih is None or gru.bias_hh is None:
+        zeros = torch.zeros(3 * d, device=device, dtype=torch.float32)
+    b_ih = gru.bias_ih.detach() if gru.bias_ih is not None else zeros
+    b_hh = gru.bias_hh.detach() if gru.bias_hh is not None else zeros
+    return b_ih, b_hh
+
+
+def relation_gru_pre(gru, emb_rel, h_prev):
+    """The gate pre-activations of GRUCell([emb_rel | x_mean], h_prev) that do not depend on
+    x_mean (regcn_relation_gru_pre_f32): R2 x 4 x d."""
+    from .weights import packed_linear, packed_linear_cols
+    R2, d = emb_rel.shape
+    b_ih, b_hh = _gru_biases(gru, d, emb_rel.device)
+    pre = torch.empty(R2, 4, d, device=emb_rel.device, dtype=torch.float32)
+    f = _lib.fptr
+    _lib.call("regcn_relation_gru_pre_f32", f(emb_rel.detach(), "emb_rel"), f(h_prev.detach().contiguous(), "h_0"),
+              f(packed_linear_cols(gru.weight_ih, 3, 0, d)), f(packed_linear(gru.weight_hh, 3)), f(b_ih), f(b_hh),
+              R2, d, f(pre), _lib.stream())
+    return pre
+
+
+def relation_gru_x(gru, x, g, h_prev, pre):
+    """h_0' from the relation means of x over the snapshot's r_to_e spans and `pre`
+    (regcn_relation_gru_x_f32; hyperbolic_model.py:797-818)."""
+    from .weights import packed_linear_cols
+    wk = g.work()
+    R2, d = h_prev.shape
+    x_mean = relation_context(x, g, R2) if g.rel_max_span > REL_INLINE_MAX_SPAN else None
+    out = torch.empty(R2, d, device=h_prev.device, dtype=torch.float32)
+    f = _lib.fptr
+    _lib.call("regcn_relation_gru_x_f32", f(x, "x"), _lib.iptr(wk["rel_idx"]) if wk["rel_idx"].numel() else None,
+              _lib.iptr(wk["rel_start"]), f(wk["rel_count"]), f(x_mean), f(h_prev.detach().contiguous(), "h_0"),
+              f(packed_linear_cols(gru.weight_ih, 3, d, 2 * d)), f(pre), R2, d, f(out), _lib.stream())
+    return out
+
+
 class HyperbolicRecurrentRGCN(nn.Module):
     """hyperbolic_model.py:157-1128."""
+
+    # inference of a 2-layer cell: each timestep in three phase launches (_forward_phases,
+    # csrc/timestep.hip); False keeps the per-layer launches (same values bit for bit)
+    use_phases = True
+    # with the phases: rows without in-edges in every snapshot of the window evolve in one
+    # launch on a side stream (regcn_cold_chain_f32; window_plan); same values bit for bit
+    window_plan = False
 
     def __init__(self, decoder_name, encoder_name, num_ents, num_rels, num_static_rels, num_words, h_dim, opn,
                  sequence_len, num_bases=-1, num_hidden_layers=1, dropout=0, c=0.01, self_loop=False,
@@ -300,11 +374,14 @@ class HyperbolicRecurrentRGCN(nn.Module):
         b_r = trev.radius_mlp.bias.detach().reshape(-1).contiguous()
         wg = packed(self.time_gate_weight)
         bg = self.time_gate_bias.detach().contiguous()
+        if self._phases_ok(g_list):
+            return self._forward_phases(g_list, c_val, r_static, wg, bg, w_r, b_r)
         for i, g in enumerate(g_list):
             g = g.to(dev)
             x_prev, _ = tangent_of(self.h, c_val)
-            self.h_0 = relation_gru_step(self.relation_gru, self.emb_rel, x_prev, g,
-                                         self.emb_rel if i == 0 else self.h_0)
+            h_prev = self.emb_rel if i == 0 else self.h_0  # the two-phase GRU, as _forward_phases runs it
+            self.h_0 = relation_gru_x(self.relation_gru, x_prev, g, h_prev,
+                                      relation_gru_pre(self.relation_gru, self.emb_rel, h_prev))
             self.h_0 = F.normalize(self.h_0) if self.layer_norm else self.h_0
             if len(self.rgcn.layers) and not self.run_analysis:
                 # cell + timestep: the last layer's launch runs the timestep on its output
@@ -323,6 +400,191 @@ class HyperbolicRecurrentRGCN(nn.Module):
                           _lib.fptr(x_new), _lib.fptr(r_new), _lib.stream())
                 self.h = attach(h_new, x_new, r_new, c_val)
             history_embs.append(self.h)
+        return history_embs, None, self.h_0, [], []
+
+    def _phases_ok(self, g_list):
+        """The phase pipeline serves eval forwards of a 2-layer cell over plain snapshots
+        (no dropout masks, no analysis hooks, no multi-GPU partition)."""
+        layers = list(self.rgcn.layers)
+        return (self.use_phases and self.dynamic_emb.device.type == "cuda" and len(layers) == 2
+                and not self.run_analysis and not any(l.training for l in layers)
+                and all(isinstance(g, SnapshotGraph) for g in g_list))
+
+    def _gru_pre_initial(self):
+        """Timestep 0's GRU pre-half: a function of parameters only (h_prev = emb_rel),
+        computed once per parameter version."""
+        gru, emb = self.relation_gru, self.emb_rel
+        key = tuple((t.data_ptr(), t._version) for t in (emb, gru.weight_ih, gru.weight_hh, gru.bias_ih, gru.bias_hh)
+                    if t is not None)
+        hit = self.__dict__.get("_gru_pre0")
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        pre = relation_gru_pre(gru, emb, emb)
+        if not torch.cuda.is_current_stream_capturing():
+            self.__dict__["_gru_pre0"] = (key, pre)
+        return pre
+
+    def _forward_phases(self, g_list, c_val, r_static, wg, bg, w_r, b_r):
+        """The timestep loop with a 2-layer cell as three launches per snapshot on one
+        stream (regcn_timestep_phase_f32, csrc/timestep.hip):
+          A  relation GRU x-half; in-edge rows' self-loop and time-gate GEMMs (need only the
+             timestep input); rows without in-edges: layer 0;
+          B  in-edge tiles: layer-0 gather -> finish -> epilogue; other rows: layer 1;
+             relation GRU pre-half of the next timestep;
+          C  in-edge tiles: layer-1 gather -> self loop -> timestep; other rows: timestep.
+        Same values as the per-layer launches bit for bit (tests/test_gpu_parity.py)."""
+        from .weights import packed_linear, packed_linear_cols
+        dev = self.dynamic_emb.device
+        V, d = self.dynamic_emb.shape
+        R2 = self.emb_rel.shape[0]
+        layers = list(self.rgcn.layers)
+        lorentz = isinstance(layers[0], LorentzRGCNLayer)
+        trev = self.temporal_radius_evolution
+        gru, emb = self.relation_gru, self.emb_rel.detach()
+        b_ih, b_hh = _gru_biases(gru, d, dev)
+        a = _lib.addr
+        f32 = torch.float32
+        s1, tw, x1, h2 = (torch.empty(V, d, device=dev, dtype=f32) for _ in range(4))
+        r1, n2 = torch.empty(V, device=dev, dtype=f32), torch.empty(V, device=dev, dtype=f32)
+        pre = self._gru_pre_initial()
+        keep = [s1, tw, x1, h2, r1, n2, b_ih, b_hh]  # tensors the launches read (profiling replays them)
+        desc = _lib.PhaseDesc()
+        desc.agg_mode = _lib.AGG_LORENTZ if lorentz else _lib.AGG_UNION
+        desc.c, desc.d = float(layers[0].c), d  # the layers' own curvature, as their launches use
+        for i, l in enumerate(layers):
+            if lorentz:
+                desc.w_rel[i] = a(l.weight.detach().contiguous())
+                desc.num_bases = int(l.num_bases)
+            else:
+                desc.w_n[i] = a(packed(l.weight_neighbor))
+                desc.gamma = float(l.radius_msg_gamma)
+            if l.self_loop:
+                desc.w_loop[i] = a(packed(l.loop_weight))
+                desc.w_evolve[i] = a(packed(l.evolve_loop_weight))
+        if lorentz and layers[1].skip_connect:
+            desc.w_skip1 = a(packed(layers[1].skip_weight))
+            desc.b_skip1 = a(layers[1].skip_bias.detach())
+        desc.s1, desc.tw, desc.x1, desc.r1, desc.h2, desc.n2 = a(s1), a(tw), a(x1), a(r1), a(h2), a(n2)
+        desc.step_w_g, desc.step_b_g, desc.step_r_static = a(wg), a(bg), a(r_static)
+        desc.step_w_r, desc.step_b_r = a(w_r), a(b_r)
+        desc.step_eps_r, desc.step_beta = float(trev.epsilon), float(trev.anchor_beta)
+        desc.step_layer_norm, desc.step_residual = int(bool(self.layer_norm)), int(bool(self.use_residual_evolution))
+        desc.step_c_radius = float(trev.c)
+        desc.gru_emb_rel, desc.gru_R2 = a(emb), R2
+        desc.gru_w_ih_e = a(packed_linear_cols(gru.weight_ih, 3, 0, d))
+        desc.gru_w_ih_x = a(packed_linear_cols(gru.weight_ih, 3, d, 2 * d))
+        desc.gru_w_hh = a(packed_linear(gru.weight_hh, 3))
+        desc.gru_b_ih, desc.gru_b_hh = a(b_ih), a(b_hh)
+        lib_call = _lib.lib().regcn_timestep_phase_f32
+
+        def call(dp, phase, stream):
+            if PHASE_CAPTURE is not None:  # profiling: a replayable launch of this phase (bench.py)
+                snap = type(desc).from_buffer_copy(desc)
+                PHASE_CAPTURE["ABC"[phase]] = (lambda: _lib.check(lib_call(ctypes.byref(snap), phase, _lib.stream()),
+                                                                  "regcn_timestep_phase_f32"), keep + [snap])
+            if PHASE_TRACE is None:
+                return lib_call(dp, phase, stream)
+            # profiling: per-workgroup {start, end} stamps of this launch (tools/phasetrace.py)
+            n_gru = ((R2 + 15) // 16) * ((d + 15) // 16)
+            n_zero = ((desc.zbound if desc.zrows else V - desc.n_pos) + 15) // 16
+            kinds = ([("pos_rows", (desc.n_pos + 15) // 16), ("gru_x", n_gru)] if phase == 0 else
+                     [("pos_tiles", desc.n_pos_tiles), ("zero", n_zero)]
+                     + ([("gru_pre", n_gru)] if phase == 1 and desc.gru_pre else []))
+            buf = torch.zeros(4 * max(1, sum(n for _, n in kinds)), dtype=torch.int64, device=dev)
+            _lib.call("regcn_set_trace", _lib.addr(buf, torch.int64))
+            rc = lib_call(dp, phase, stream)
+            _lib.call("regcn_set_trace", None)
+            PHASE_TRACE.append(("ABC"[phase], kinds, buf))
+            return rc
+
+        h_prev = emb
+        history_embs = []
+        g_list = [g.to(dev) for g in g_list]
+        T = len(g_list)
+        outs = [(torch.empty(V, d, device=dev, dtype=f32), torch.empty(V, d, device=dev, dtype=f32),
+                 torch.empty(V, device=dev, dtype=f32)) for _ in g_list]
+        ev_cold = None
+        if self.window_plan and T <= _lib.MAX_WINDOW and V <= PLAN_MAX_V:
+            # rows without in-edges anywhere in the window: their whole evolution in one launch
+            # on a side stream (fork here, join at the end); the phases run the other rows
+            plan = window_plan(g_list, V)
+            main = torch.cuda.current_stream(dev)
+            side = self._side(dev)
+            side.wait_stream(main)
+            x_init, _ = tangent_of(self.h, c_val)
+            ch = _lib.ChainDesc()
+            ch.rows, ch.n_rows = a(plan["c_rows"], torch.int32), a(plan["counts"], torch.int32)
+            ch.T, ch.d, ch.grid_bound, ch.c, ch.x0 = T, d, V, desc.c, a(x_init)
+            ch.w_evolve0, ch.w_evolve1 = desc.w_evolve[0], desc.w_evolve[1]
+            ch.w_skip1, ch.b_skip1 = desc.w_skip1, desc.b_skip1
+            for f in ("w_g", "b_g", "r_static", "w_r", "b_r", "eps_r", "beta", "layer_norm", "residual",
+                      "c_radius"):
+                setattr(ch, "step_" + f, getattr(desc, "step_" + f))
+            for t, (ho, xo, ro) in enumerate(outs):
+                ch.h_out[t], ch.x_out[t], ch.r_out[t] = a(ho), a(xo), a(ro)
+            with torch.cuda.stream(side):
+                _lib.call_desc("regcn_cold_chain_f32", ch)
+            ev_cold = torch.cuda.Event()
+            ev_cold.record(side)
+            desc.zbound = plan["z_stride"]
+            desc.zcount = None
+            keep.append(plan)
+        else:
+            plan = None
+        for t, g in enumerate(g_list):
+            wk = g.work()
+            x0, r0 = tangent_of(self.h, c_val)
+            h0 = torch.empty(R2, d, device=dev, dtype=f32)
+            out = outs[t]
+            if plan is not None:  # this timestep's rows without in-edges, among the window's touched rows
+                desc.zrows = a(plan["z_rows"], torch.int32) + 4 * t * plan["z_stride"]
+                desc.zcount = a(plan["counts"], torch.int32) + 4 * (2 + t)
+            desc.rowptr, desc.col_src, desc.col_type = (a(wk[k], torch.int32) for k in ("rowptr", "col_src", "col_type"))
+            desc.norm, desc.budget = a(wk["norm"]), g.budget
+            desc.tiles, desc.n_pos_tiles = a(wk["tiles"], torch.int32), g.n_pos_tiles
+            desc.item_ptr = a(wk["item_ptr"], torch.int32)
+            desc.item_src = a(wk["item_src"], torch.int32) if wk["item_src"].numel() else None
+            desc.item_tl = a(wk["item_tl"], torch.int32) if wk["item_tl"].numel() else None
+            desc.rows, desc.n_pos, desc.V = a(wk["rows"], torch.int32), g.n_pos, V
+            desc.x0, desc.r0 = a(x0), a(r0)
+            keep.extend([x0, r0, h0, out])
+            desc.step_h_out, desc.step_x_out, desc.step_r_out = a(out[0]), a(out[1]), a(out[2])
+            # A: GRU x-half (relation means of x0 over this snapshot's r_to_e spans)
+            x_mean = relation_context(x0, g, R2) if g.rel_max_span > REL_INLINE_MAX_SPAN else None
+            desc.gru_rel_idx = a(wk["rel_idx"], torch.int32) if wk["rel_idx"].numel() else None
+            desc.gru_rel_start, desc.gru_rel_count = a(wk["rel_start"], torch.int32), a(wk["rel_count"])
+            desc.gru_x_mean = a(x_mean)
+            keep.extend([x_mean, pre, h_prev])
+            desc.gru_h_prev, desc.gru_pre, desc.gru_h_out = a(h_prev.detach().contiguous()), a(pre), a(h0)
+            desc.rel = None
+            _lib.check(call(ctypes.byref(desc), 0, _lib.stream()), "regcn_timestep_phase_f32(A)")
+            if self.layer_norm:
+                h0 = F.normalize(h0)
+            # B: layer 0 of the in-edge rows (messages use h_0), layer 1 of the others, and the
+            # next timestep's GRU pre-half (h_prev = h_0)
+            desc.rel = a(h0)
+            if g.n_heavy:
+                agg0 = _heavy_aggregate(desc.agg_mode, g, x0, r0, h0, layers[0].weight.detach().contiguous()
+                                        if lorentz else None, desc.num_bases, desc.gamma, c_val)
+                desc.agg[0] = a(agg0)
+                keep.append(agg0)
+            pre_next = torch.empty(R2, 4, d, device=dev, dtype=f32) if t + 1 < len(g_list) else None
+            keep.append(pre_next)
+            desc.gru_h_prev, desc.gru_pre, desc.gru_h_out = a(h0), a(pre_next), None
+            _lib.check(call(ctypes.byref(desc), 1, _lib.stream()), "regcn_timestep_phase_f32(B)")
+            if g.n_heavy:
+                agg1 = _heavy_aggregate(desc.agg_mode, g, x1, r1, h0, layers[1].weight.detach().contiguous()
+                                        if lorentz else None, desc.num_bases, desc.gamma, c_val)
+                desc.agg[1] = a(agg1)
+                keep.append(agg1)
+            _lib.check(call(ctypes.byref(desc), 2, _lib.stream()), "regcn_timestep_phase_f32(C)")
+            desc.agg[0] = desc.agg[1] = None
+            pre, h_prev = pre_next, h0
+            self.h_0 = h0
+            self.h = attach(out[0], out[1], out[2], c_val)
+            history_embs.append(self.h)
+        if ev_cold is not None:
+            torch.cuda.current_stream(dev).wait_event(ev_cold)
         return history_embs, None, self.h_0, [], []
 
     def _final_embedding(self, emb, c_val):
@@ -357,10 +619,15 @@ class HyperbolicRecurrentRGCN(nn.Module):
             score, score_rel = self._decode_both(embedding, r_emb, at)
             return all_triples, score, score_rel
 
-    def _side(self, dev):
-        side = getattr(self, "_side_stream", None)
+    def _side(self, dev, k=1):
+        """Side stream k of the calling stream (1: relation decoder / query triples / cold
+        rows): keyed by the current stream, so predicts issued on different streams (e.g.
+        independent samples in flight together) never share a side stream."""
+        streams = self.__dict__.setdefault("_side_streams", {})
+        key = (torch.cuda.current_stream(dev).cuda_stream, k)
+        side = streams.get(key)
         if side is None or side.device != dev:
-            side = self._side_stream = torch.cuda.Stream(dev)
+            side = streams[key] = torch.cuda.Stream(dev)
         return side
 
     def _decode_both(self, embedding, r_emb, at):

@@ -43,6 +43,24 @@ def packed_linear(w, n_gates=1):
     return out
 
 
+def packed_linear_cols(w, n_gates, c0, c1):
+    """`packed_linear` of the column slice w[:, c0:c1] (e.g. the emb_rel / x_mean halves of
+    a GRUCell weight_ih), cached on the weight per slice."""
+    key = (w.data_ptr(), w._version, tuple(w.shape), n_gates, c0, c1)
+    cache = w.__dict__.setdefault("_regcn_packed_cols", {})
+    hit = cache.get((n_gates, c0, c1))
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    rows = w.shape[0]
+    n_out, n_in = rows // n_gates, c1 - c0
+    wc = w.detach()[:, c0:c1].contiguous()
+    out = torch.empty(_lib.lib().regcn_packed_linear_floats(n_gates, n_out, n_in), device=w.device,
+                      dtype=torch.float32)
+    _lib.call("regcn_pack_linear_f32", _lib.fptr(wc, "weight"), n_gates, n_out, n_in, _lib.fptr(out), _lib.stream())
+    cache[(n_gates, c0, c1)] = (key, out, wc)  # keep wc alive until the packing kernel has run
+    return out
+
+
 def packed_t(w):
     """`packed` of the transpose of an nn.Linear weight (out x in): the B operand of
     x @ W^T, cached on the weight itself."""
@@ -58,7 +76,7 @@ def packed_t(w):
     return out
 
 
-_CACHE_ATTRS = ("_regcn_packed", "_regcn_packed_lin", "_regcn_packed_t")
+_CACHE_ATTRS = ("_regcn_packed", "_regcn_packed_lin", "_regcn_packed_t", "_regcn_packed_cols")
 
 
 def invalidate(module):
@@ -72,5 +90,5 @@ def invalidate(module):
             if hasattr(t, a):
                 delattr(t, a)
     for m in module.modules():
-        for a in ("_init_cache", "_r_static_cache", "_c_cache"):
+        for a in ("_init_cache", "_r_static_cache", "_c_cache", "_gru_pre0"):
             m.__dict__.pop(a, None)

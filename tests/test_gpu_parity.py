@@ -133,6 +133,72 @@ def test_hyperbolic_model_predict_vs_golden(golden, tag):
     assert_close(score_rel, z["score_rel"], what="relation score")
 
 
+@pytest.mark.parametrize("V,R,T,hub", [(500, 10, 300, False), (4000, 40, 2000, True), (300, 60, 5, False)])
+def test_relation_gru_two_phase(V, R, T, hub):
+    """regcn_relation_gru_pre_f32 + regcn_relation_gru_x_f32 against torch.nn.GRUCell on
+    [emb_rel | mean over the r_to_e span of x] (hyperbolic_model.py:797-818), fp32,
+    tolerance 1e-4 * max(1, |ref|); absent relations (mean 0), spans over the in-kernel
+    limit (precomputed means) and a single-triple relation covered; also the one-launch
+    kernel (regcn_relation_gru_f32) on the same inputs."""
+    from regcn_amd import graph as G
+    from regcn_amd.hyperbolic_model import relation_gru_pre, relation_gru_step, relation_gru_x
+    rng = np.random.default_rng(V)
+    tri = np.stack([rng.integers(0, V, T), rng.integers(0, R // 2, T), rng.integers(0, V, T)], 1)
+    if hub:
+        tri[:300, 1] = 3  # a relation whose span is longer than the in-kernel limit
+    g = G.build_sub_graph(V, R, tri, True, DEV)
+    d = 200
+    torch.manual_seed(V)
+    gru = torch.nn.GRUCell(2 * d, d).to(DEV)
+    x = torch.randn(V, d, device=DEV)
+    emb = torch.randn(2 * R, d, device=DEV)
+    h_prev = torch.randn(2 * R, d, device=DEV)
+    with torch.no_grad():
+        got = relation_gru_x(gru, x, g, h_prev, relation_gru_pre(gru, emb, h_prev))
+        one = relation_gru_step(gru, emb, x, g, h_prev)
+        means = torch.zeros(2 * R, d, device=DEV)
+        r2e = g.r_to_e.to(DEV) if torch.is_tensor(g.r_to_e) else torch.tensor(g.r_to_e, device=DEV)
+        for (a, b), r in zip(g.r_len, g.uniq_r):
+            means[int(r)] = x[r2e[a:b]].mean(0)
+        ref = gru(torch.cat([emb, means], 1), h_prev)
+    assert_close(got, ref.cpu().numpy(), what="two-phase GRU")
+    assert_close(one, ref.cpu().numpy(), what="one-launch GRU")
+
+
+@pytest.mark.parametrize("encoder,layers,skip,self_loop,ln", [
+    ("lgcn", 2, False, True, False), ("hyperbolic_uvrgcn", 2, False, True, True),
+    ("lgcn", 2, True, True, False), ("lgcn", 2, True, False, True), ("hyperbolic_uvrgcn", 1, False, True, False),
+])
+def test_phase_pipeline_bitwise(encoder, layers, skip, self_loop, ln):
+    """_forward_phases (three phase launches per timestep, csrc/timestep.hip) equals the
+    per-layer launches bit for bit, history embeddings, tangent caches and h_0 included; the
+    window holds an empty snapshot (no in-edge rows) and a one-triple one."""
+    from regcn_amd import graph as G
+    from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
+    from regcn_amd.synthetic import snapshot_series
+    from regcn_amd.tangent import tangent_of
+    V, R, d = 3000, 50, 200  # R2 = 100 = num_bases: d / num_bases = 2 (lgcn blocks)
+    snaps = snapshot_series(3, V, R, 4, 300)
+    snaps[1] = np.zeros((0, 3), np.int64)
+    snaps[2] = snaps[2][:1]
+    torch.manual_seed(0)
+    m = HyperbolicRecurrentRGCN("roth", encoder, V, R, 0, 0, d, "sub", 4, num_bases=100, num_hidden_layers=layers,
+                                dropout=0.2, c=C, self_loop=self_loop, skip_connect=skip, layer_norm=ln,
+                                entity_prediction=True, relation_prediction=True, use_cuda=True,
+                                radius_target=np.random.default_rng(0).uniform(0.5, 3, V).astype(np.float32),
+                                radius_msg_gamma=0.15).to(DEV).eval()
+    glist = [G.build_sub_graph(V, R, s, True, DEV) for s in snaps]
+    res = {}
+    for split in (True, False):
+        m.use_phases = split
+        with torch.no_grad():
+            embs, _, h0, _, _ = m.forward(glist, None, True)
+        torch.cuda.synchronize()
+        res[split] = [e.clone() for e in embs] + [tangent_of(e, C)[k].clone() for e in embs for k in (0, 1)] + [h0]
+    for a, b in zip(res[True], res[False]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("tag", ["uvrgcn_roth", "lgcn_roth", "uvrgcn_murp_nores", "uvrgcn_atth_beta",
                                  "lgcn_roth_bias_crel"])
 def test_get_loss_vs_golden(golden, tag):

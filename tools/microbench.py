@@ -99,6 +99,45 @@ def trace(V=7128, R=230, per_snap=246, d=200, nb=100):
         print("  shader clock ~%.0f MHz (median over workgroups)" % float(clk.median()))
 
 
+def trace_pos(V=7128, R=230, per_snap=246, d=200, nb=100):
+    """The in-edge tiles alone (run_layer pos_only): per-phase stamps and launch times of the
+    layer and layer+step kernels over rows[:n_pos], and of the in-degree-0 chain kernel."""
+    from regcn_amd import hyperbolic_layers as HL
+    snaps = snapshot_series(0, V, R, 1, per_snap)
+    g = G.build_sub_graph(V, R, snaps[0], True, dev)
+    torch.manual_seed(0)
+    h = H.exp_map_zero(torch.randn(V, d, device=dev) * 0.3, C)
+    rel = torch.randn(2 * R, d, device=dev) * 0.1
+    lor = LorentzRGCNLayer(d, d, 2 * R, nb, c=C, activation=F.rrelu, self_loop=True).to(dev).eval()
+    lor2 = LorentzRGCNLayer(d, d, 2 * R, nb, c=C, activation=F.rrelu, self_loop=True).to(dev).eval()
+    xp = torch.randn(V, d, device=dev) * 0.1
+    step = StepSpec(xp, packed(torch.randn(d, d, device=dev) * 0.05), torch.zeros(d, device=dev),
+                    torch.rand(V, device=dev) + 0.5, torch.randn(d, device=dev) * 0.01, torch.zeros(1, device=dev),
+                    0.1, 1.0, False, True, C)
+    out = (torch.empty(V, d, device=dev), torch.empty(V, d, device=dev), torch.empty(V, device=dev))
+    st = torch.cuda.Stream(dev)
+    n_wg = g.n_pos_tiles
+    with torch.no_grad():
+        for name, fn in (("pos layer", lambda: lor(g, h, rel, pos_only=True)),
+                         ("pos layer+step", lambda: lor(g, h, rel, step=step, pos_only=True, out=out))):
+            ms = event_time(fn, 20, st)
+            for _ in range(2):
+                fn()
+            HL.TRACE = torch.zeros(max(n_wg, 1) * 16, dtype=torch.int64, device=dev)
+            fn()
+            torch.cuda.synchronize()
+            t = HL.TRACE.view(-1, 16).cpu().double()
+            HL.TRACE = None
+            t0 = t[:, 0].min()
+            us = lambda a, b: ((t[:, b] - t[:, a]) / 100.0)  # noqa: E731
+            ph = [("start", (t[:, 0] - t0) / 100.0), ("rows", us(0, 1)), ("operands", us(1, 2)), ("gemm", us(2, 3)),
+                  ("act", us(3, 4)), ("epilogue", us(4, 5)), ("g.idx", us(8, 9)), ("g.loop", us(9, 11)),
+                  ("g.sync", us(11, 12)), ("g.finish", us(12, 13))]
+            print("%s: %d tiles, launch %.1f us, span %.1f us | " % (name, n_wg, ms * 1e3,
+                                                                    float((t[:, 5].max() - t0) / 100.0))
+                  + " ".join("%s %.2f/%.2f" % (k, float(v.median()), float(v.max())) for k, v in ph), flush=True)
+
+
 def trace_gru(V=7128, R=230, per_snap=246, d=200):
     """Phase stamps of the relation GRU kernel (regcn_set_trace): staging (relation means),
     MFMA k-split, cross-wave reduction, gate epilogue."""
@@ -158,6 +197,9 @@ def trace_score(B=492, N=7128, d=200):
 
 
 if __name__ == "__main__":
+    if "--pos" in sys.argv:
+        trace_pos()
+        sys.exit(0)
     if "--trace" in sys.argv:
         trace()
         trace_gru()

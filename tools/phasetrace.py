@@ -1,0 +1,64 @@
+"""Per-workgroup timing of the timestep phase launches (csrc/timestep.hip) on the bench
+workload: each workgroup stamps its start and end (s_memrealtime, 100 MHz); per launch and
+block kind (in-edge tiles, rows without in-edges, relation GRU blocks) the start offsets,
+durations and the last end are printed.  Profiling only (regcn_set_trace)."""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "re-gcn_amd"))
+sys.path.insert(0, REPO)
+import bench  # noqa: E402
+from regcn_amd import hyperbolic_model as HM  # noqa: E402
+from regcn_amd.synthetic import CONFIGS  # noqa: E402
+
+
+def main(config="icews14s_lgcn_roth", empty=""):
+    dev = torch.device("cuda", 0)
+    cfg = CONFIGS[config]
+    model = bench.build_model(cfg, 200, dev, seed=1234)
+    sample = bench.make_samples(cfg, 1, dev, seed=100)[0]
+    _, glist, _, _ = sample
+    if empty:  # edgeless snapshots: every row on the in-degree-0 path (throughput of that path alone)
+        import numpy as np
+        from regcn_amd import graph as G
+        glist = [G.build_sub_graph(cfg["V"], cfg["R"], np.zeros((0, 3), np.int64), True, dev) for _ in glist]
+    with torch.no_grad():
+        for _ in range(3):
+            model.forward(glist, None, True)
+        torch.cuda.synchronize()
+        HM.PHASE_TRACE = []
+        model.forward(glist, None, True)
+        torch.cuda.synchronize()
+        rec, HM.PHASE_TRACE = HM.PHASE_TRACE, None
+    for t, (phase, kinds, buf) in enumerate(rec):
+        st = buf.view(-1, 4).cpu().double()
+        t0 = st[st[:, 0] > 0, 0].min()
+        line = "%s%d span %6.2f us |" % (phase, t // 3, float((st[:, 3].max() - t0) / 100.0))
+        off = 0
+        for name, n in kinds:
+            if n == 0:
+                continue
+            s = st[off:off + n]
+            off += n
+            s = s[s[:, 3] > 0]  # workgroups past a device-counted list exit unstamped
+            if len(s) == 0:
+                continue
+            n = len(s)
+            start = (s[:, 0] - t0) / 100.0
+            dur = (s[:, 3] - s[:, 0]) / 100.0
+            end = (s[:, 3] - t0) / 100.0
+            line += " %s x%d start %.2f/%.2f dur %.2f/%.2f end %.2f" % (
+                name, n, float(start.median()), float(start.max()), float(dur.median()), float(dur.max()),
+                float(end.max()))
+            if bool((s[:, 1] > 0).all()) and bool((s[:, 2] > 0).all()):
+                seg = [(s[:, 1] - s[:, 0]) / 100.0, (s[:, 2] - s[:, 1]) / 100.0, (s[:, 3] - s[:, 2]) / 100.0]
+                line += " [%s]" % " ".join("%.2f" % float(x.median()) for x in seg)
+            line += " |"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
