@@ -56,6 +56,9 @@ def parse():
                          ":100-149 without --multi-step), so a server may overlap them")
     ap.add_argument("--per-layer", action="store_true",
                     help="run the encoder as per-layer launches instead of the timestep phase launches")
+    ap.add_argument("--window-plan", action="store_true",
+                    help="with the phase launches: rows without in-edges in the whole window evolve in one "
+                         "side-stream launch (csrc/window.hip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work")
     ap.add_argument("--no-scale", action="store_true",
@@ -321,6 +324,7 @@ def main():
     d = args.d
     model = build_model(cfg, d, device, seed=1234)          # same weights on every rank
     model.use_phases = not args.per_layer
+    model.window_plan = args.window_plan and not args.per_layer
     sharded = args.shard != "replica" and world > 1
     # replicas: independent data per rank; sharded: every rank holds the same snapshots
     samples = make_samples(cfg, args.pool, device, seed=100 if sharded else 100 + 7919 * rank,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 4
+#define REGCN_ABI_VERSION 5
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -384,6 +384,37 @@ int regcn_roth_rel_query_f32(const float* ent, const int64_t* trip, int32_t n_te
                              const float* global_rot, const float* rel, int32_t n_cand, int32_t d, float c,
                              float* q_out, float* cand_out, void* stream);
 
+/* The decoder front of a RotH predict in ONE launch (replaces the two calls above and the
+ * inverse-triple torch.cat of HyperbolicRecurrentRGCN.predict, hyperbolic_model.py:915-919):
+ * RotH entity queries -> q_ent, RotHRel relation queries -> q_rel, exp0(rel) rows -> cand,
+ * and all_triples = [trip; (o, r + num_rels, s)] (B x 3 int64).  4-query tiles on the
+ * 4x4x1 fp32 MFMA.  Weights: nn.Linear (out x in) packed by regcn_pack_k4_f32.  A NULL
+ * q_ent / q_rel / cand (n_cand = 0) / all_triples skips that part (all_triples needs q_ent). */
+typedef struct regcn_roth_queries_desc {
+  const float* ent;        /* V x d final entity embedding */
+  const float* rel;        /* R2 x d relation embedding */
+  const int64_t* trip;     /* n_test x 3 test triples (s, r, o) */
+  int32_t n_test, B, num_rels, d;
+  float c;
+  /* HyperbolicRotH (hyperbolic_decoder.py:1065-1085) */
+  const float *w1, *b1, *w2, *b2;           /* reshape_fc1 / reshape_fc2 */
+  const float *w_rot, *b_rot;               /* rot_proj (d -> d/2) */
+  const float *w_trans, *b_trans;           /* trans_proj */
+  float* q_ent;                             /* B x d */
+  /* HyperbolicRotHRel (hyperbolic_decoder.py:1223-1243) */
+  const float *rw1, *rb1, *rw2, *rb2;       /* its reshape_fc1 / reshape_fc2 */
+  const float* global_rot;                  /* d/2 */
+  float* q_rel;                             /* B x d */
+  int32_t n_cand;                           /* relation rows of exp0(rel) */
+  float* cand;                              /* n_cand x d */
+  int64_t* all_triples;                     /* B x 3, or NULL */
+} regcn_roth_queries_desc;
+/* k4 packing of an nn.Linear weight W (n_out x n_in, n_out <= 256, n_in % 4 == 0):
+ * out[g][c][e] = W[c][4g + e], zero for n_out <= c < 256. */
+size_t regcn_packed_k4_floats(int32_t n_out, int32_t n_in);
+int regcn_pack_k4_f32(const float* W, int32_t n_out, int32_t n_in, float* out, void* stream);
+int regcn_roth_queries_f32(const regcn_roth_queries_desc* desc, void* stream);
+
 /* ---- a11/a12/f2: all-entity hyperbolic scoring ------------------------------------- */
 #define REGCN_SCORE_DIST 1       /* flags: true hyperbolic distance (fp64 MFMA) */
 #define REGCN_SCORE_RAW_SCALE 2  /* flags: `scale` is score_scale_raw; softplus(raw) + 1e-6 in-kernel */
@@ -395,6 +426,21 @@ int regcn_roth_rel_query_f32(const float* ent, const int64_t* trip, int32_t n_te
  * (or NULL) the per-query curvature of --plus-relation-specific-curvature.  out: [B][N]. */
 int regcn_hyp_score_f32(const float* q, const float* cand, const float* bias, const float* c_rel, const float* scale, const float* margin, int32_t B,
                         int32_t N, int32_t d, float c, int32_t flags, float* out, void* stream);
+/* Up to two independent regcn_hyp_score_f32 jobs (no REGCN_SCORE_DIST, no c_rel, one d) in
+ * ONE launch: a predict's entity scores and relation scores.  Job 1's workgroups follow job
+ * 0's and take the CUs job 0's shorter candidate strips free. */
+typedef struct regcn_score_job {
+  const float* q;
+  const float* cand;
+  const float* bias;     /* [N] or NULL */
+  const float* scale;    /* device scalar or NULL */
+  const float* margin;   /* device scalar or NULL */
+  int32_t B, N, d;
+  float c;
+  int32_t flags;         /* REGCN_SCORE_RAW_SCALE only */
+  float* out;            /* B x N */
+} regcn_score_job;
+int regcn_hyp_score_jobs_f32(const regcn_score_job* jobs, int32_t n_jobs, void* stream);
 /* _chunked_hyperbolic_ce_loss, hyperbolic_decoder.py:182-307: per-query lse - target logit
  * (the caller takes the mean).  workspace: regcn_hyp_ce_workspace_bytes(B, N) bytes. */
 size_t regcn_hyp_ce_workspace_bytes(int32_t B, int32_t N);

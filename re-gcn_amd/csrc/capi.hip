@@ -495,6 +495,27 @@ int regcn_hyp_score_f32(const float* q, const float* cand, const float* bias, co
   return score(a, 0, nullptr, ST(s));
 }
 
+size_t regcn_packed_k4_floats(int32_t n_out, int32_t n_in) { return packed_k4_floats(n_out, n_in); }
+int regcn_pack_k4_f32(const float* W, int32_t n_out, int32_t n_in, float* out, void* s) {
+  return pack_k4(W, n_out, n_in, out, ST(s));
+}
+int regcn_roth_queries_f32(const regcn_roth_queries_desc* desc, void* s) {
+  if (!desc) return set_error(REGCN_EINVAL, "null desc");
+  return roth_queries(*desc, ST(s));
+}
+
+int regcn_hyp_score_jobs_f32(const regcn_score_job* jobs, int32_t n_jobs, void* s) {
+  if (!jobs || n_jobs < 1 || n_jobs > 2) return set_error(REGCN_EINVAL, "1 or 2 score jobs");
+  ScoreArgs a[2];
+  for (int i = 0; i < 2; ++i) {
+    const regcn_score_job& j = jobs[i < n_jobs ? i : 0];
+    if (j.flags & REGCN_SCORE_DIST) return set_error(REGCN_ENOTSUP, "score jobs compute the proxy score only");
+    a[i] = score_args(j.q, j.cand, j.bias, nullptr, j.scale, j.margin, j.B, i < n_jobs ? j.N : 0, j.d, j.c, j.flags);
+    a[i].out = j.out;
+  }
+  return score_jobs(a[0], a[1], ST(s));
+}
+
 size_t regcn_hyp_ce_workspace_bytes(int32_t B, int32_t N) {
   return ((size_t)B * ce_partial_slots(N) * 2 + (size_t)B) * sizeof(float);
 }

@@ -255,6 +255,10 @@ struct QueryArgs {
   float* cand_out;
 };
 int query(const QueryArgs& a, int mode, hipStream_t st);
+// queries.hip: a predict's RotH + RotHRel queries, candidates and all_triples in one launch
+size_t packed_k4_floats(int n_out, int n_in);
+int pack_k4(const float* W, int n_out, int n_in, float* out, hipStream_t st);
+int roth_queries(const regcn_roth_queries_desc& a, hipStream_t st);
 
 size_t packed_linear_floats(int n_gates, int n_out, int n_in);
 int pack_linear(const float* W, int n_gates, int n_out, int n_in, float* Wp, hipStream_t st);
@@ -265,6 +269,7 @@ int pack_weight(const float* W, int d_in, int d_out, float* Wp, hipStream_t st);
 int layer(const LayerArgs& a, hipStream_t st);
 int timestep(const StepArgs& a, hipStream_t st);
 int score(ScoreArgs& a, int mode, float* loss, hipStream_t st);
+int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st);
 // CE partial (max, sum exp) slots per query: one per candidate tile (generic kernel) or one per
 // workgroup of the query's tile (persistent fp32 kernel, <= 8 x 32).
 inline size_t ce_partial_slots(int N) { return std::max<size_t>(((size_t)N + 63) / 64, 256); }

@@ -433,8 +433,10 @@ inline unsigned score_f32_grid(int B, int nbn) {
 }
 inline size_t score_f32_lds(int d) { return (size_t)2 * SN * (score_lds_stride(d) + 1) * 4; }
 
+// One workgroup's work: `blk` of `nblk` workgroups of this job (the XCD of blk is blk % 8:
+// a job's first workgroup must sit at a multiple of 8 in the launch).
 template <int MODE>
-__global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32(ScoreArgs p) {
+__device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const int nblk) {
   extern __shared__ float Es[];  // 2 x SN x SE candidate rows, zero past N and d
   p.scale = p.scale_p ? *p.scale_p : 1.f;
   if (p.scale_raw && p.scale_p)  // softplus(raw) + 1e-6 (hyperbolic_decoder.py:717; torch threshold 20)
@@ -443,13 +445,13 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) v
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto stamp = [&](int k) {  // profiling (regcn_set_trace)
-    if (p.trace && tid == 0) p.trace[(int64_t)blockIdx.x * 16 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (p.trace && tid == 0) p.trace[(int64_t)blk * 16 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
   const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
   const int nbn = (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
-  const int S = gridDim.x / (8 * nbq);
-  const int xcd = blockIdx.x & 7, rk = blockIdx.x >> 3;
+  const int S = nblk / (8 * nbq);
+  const int xcd = blk & 7, rk = blk >> 3;
   const int bq = rk % nbq, stripe = rk / nbq;
   auto tile_of = [&](int i) { return xcd + 8 * (stripe + S * i); };
   int bn = tile_of(0);
@@ -582,6 +584,21 @@ __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) v
   stamp(2);
 }
 
+template <int MODE>
+__global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32(ScoreArgs p) {
+  score_f32_body<MODE>(p, blockIdx.x, gridDim.x);
+}
+
+// Two independent score jobs in one launch (a predict's entity and relation scores): job 1's
+// workgroups follow job 0's in dispatch order, so they take the CUs that job 0's shorter
+// strips free instead of running as a second serial launch.
+__global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32_jobs(ScoreArgs p0,
+                                                                                                      ScoreArgs p1,
+                                                                                                      int g0) {
+  if ((int)blockIdx.x < g0) score_f32_body<0>(p0, blockIdx.x, g0);
+  else score_f32_body<0>(p1, blockIdx.x - g0, gridDim.x - g0);
+}
+
 // Combine per-tile (max, sumexp) into per-query loss = lse - target logit (one wave per query).
 __global__ __launch_bounds__(256) void k_ce_combine(const float* __restrict__ part, const float* __restrict__ tgt,
                                                     int B, int nblk, float* __restrict__ loss,
@@ -669,6 +686,25 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   const int nparts = fast ? 8 * score_f32_stripes(a.B, nbn) : nbn;  // <= ce_partial_slots(N)
   hipLaunchKernelGGL(k_ce_combine, dim3((a.B + 3) / 4), b, 0, st, a.part, a.tgt_logit, a.B, nparts, loss, a.lse_out);
   return check_launch("k_ce_combine");
+}
+
+int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st) {
+  for (ScoreArgs* a : {&a0, &a1}) {
+    if (a->d <= 0 || (a->d & 3) || a->d > 16 * KB_MAX) return set_error(REGCN_EINVAL, "score jobs need d %% 4 == 0, d <= 256");
+    if (a->use_dist || a->c_r) return set_error(REGCN_ENOTSUP, "score jobs compute the proxy score only");
+    if (a->B > 0 && a->N > 0 && (!a->q || !a->e || !a->out)) return set_error(REGCN_EINVAL, "null pointer");
+    a->trace = g_trace;
+  }
+  if (a0.d != a1.d) return set_error(REGCN_EINVAL, "score jobs need one d");
+  const bool e0 = a0.B > 0 && a0.N > 0, e1 = a1.B > 0 && a1.N > 0;
+  if (!e0 || !e1) {
+    if (e0) return score(a0, 0, nullptr, st);
+    if (e1) return score(a1, 0, nullptr, st);
+    return 0;
+  }
+  const unsigned g0 = score_f32_grid(a0.B, (a0.N + SN - 1) / SN), g1 = score_f32_grid(a1.B, (a1.N + SN - 1) / SN);
+  hipLaunchKernelGGL(k_score_f32_jobs, dim3(g0 + g1), dim3(64 * SW2), score_f32_lds(a0.d), st, a0, a1, (int)g0);
+  return check_launch("k_score_f32_jobs");
 }
 
 // CE backward coefficients (the B x N GEMM operand and the row / column partial sums; the

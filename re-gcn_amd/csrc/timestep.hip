@@ -382,6 +382,8 @@ __global__ __launch_bounds__(NTHR) void k_phase_a(PhaseArgs p) {
   extern __shared__ float lds[];
   PhaseStamp stamp(p);
   int b = blockIdx.x;
+  // every block of A is on the timestep's critical path
+  __builtin_amdgcn_s_setprio(2);
   if (b < p.n_pos_rt) return a_pos_rows(p, b, lds);
   b -= p.n_pos_rt;
   gru_x_block(p.gru, b % p.gru_rt, b / p.gru_rt, lds);
@@ -392,7 +394,12 @@ __global__ __launch_bounds__(NTHR) void k_phase_b(PhaseArgs p) {
   extern __shared__ float lds[];
   PhaseStamp stamp(p);
   int b = blockIdx.x;
-  if (b < p.L[0].n_pos_tiles) return b_pos_tile<AGG, S>(p, b, lds);
+  // in-edge tiles carry the critical path; rows without in-edges and the next GRU pre-half
+  // fill the SIMDs' idle issue slots at the default priority
+  if (b < p.L[0].n_pos_tiles) {
+    __builtin_amdgcn_s_setprio(2);
+    return b_pos_tile<AGG, S>(p, b, lds);
+  }
   b -= p.L[0].n_pos_tiles;
   if (b < p.n_zero_rt) return b_zero_rows(p, b, lds);
   b -= p.n_zero_rt;
@@ -404,7 +411,10 @@ __global__ __launch_bounds__(NTHR) void k_phase_c(PhaseArgs p) {
   extern __shared__ float lds[];
   PhaseStamp stamp(p);
   int b = blockIdx.x;
-  if (b < p.L[1].n_pos_tiles) return c_pos_tile<AGG, S>(p, b, lds);
+  if (b < p.L[1].n_pos_tiles) {
+    __builtin_amdgcn_s_setprio(2);
+    return c_pos_tile<AGG, S>(p, b, lds);
+  }
   b -= p.L[1].n_pos_tiles;
   c_zero_rows(p, b, lds);
 }

@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libregcn_hip.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -62,6 +62,10 @@ _SIGS = {
     "regcn_relation_gru_x_f32": [P, P, P, P, P, P, P, P, _c_int, _c_int, P, P],
     "regcn_roth_query_f32": [P, P, P, _c_int, _c_int, _c_int, P, P, P, P, P, P, P, P, _c_int, _c_f, P, P],
     "regcn_roth_rel_query_f32": [P, P, _c_int, _c_int, _c_int, P, P, P, P, P, P, _c_int, _c_int, _c_f, P, P, P],
+    "regcn_packed_k4_floats": [_c_int, _c_int],
+    "regcn_pack_k4_f32": [P, _c_int, _c_int, P, P],
+    "regcn_roth_queries_f32": [P, P],
+    "regcn_hyp_score_jobs_f32": [P, _c_int, P],
     "regcn_snapshot_workspace_bytes": [_c_i64, _c_int, _c_int],
     "regcn_snapshot_capacity": [_c_int, _c_i64, _c_int, _c_int, _c_int],
     "regcn_snapshot_csr_i32": [P, P],
@@ -82,7 +86,8 @@ SCORE_DIST, SCORE_RAW_SCALE = 1, 2
 _RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz,
             "regcn_snapshot_workspace_bytes": _c_sz, "regcn_snapshot_capacity": _c_i64,
             "regcn_transpose_workspace_bytes": _c_sz, "regcn_row_type_order_workspace_bytes": _c_sz,
-            "regcn_packed_weight_floats": _c_sz, "regcn_packed_linear_floats": _c_sz}
+            "regcn_packed_weight_floats": _c_sz, "regcn_packed_linear_floats": _c_sz,
+            "regcn_packed_k4_floats": _c_sz}
 
 _lib = None
 
@@ -140,6 +145,20 @@ SNAP = dict(MAX_DEG=0, N_POS=1, INVALID=2, N_PAIRS=3, REL_MAX=4, N_HEAVY=5, N_TI
             A_STAR=9, CHUNKS=10, HEAVY_CHUNKS=13, REL_CHUNKS=16, NSTATS=20)
 CAP = dict(TILES=0, ITEMS=1, CHUNKS=2, FIXUPS=3, HEAVY_CHUNKS=4, HEAVY_FIXUPS=5, REL_CHUNKS=6, REL_FIXUPS=7,
            REL_IDX=8)
+
+
+class RothQueriesDesc(ctypes.Structure):
+    """regcn_roth_queries_desc (include/regcn_hip.h)."""
+    _fields_ = [("ent", P), ("rel", P), ("trip", P), ("n_test", _c_int), ("B", _c_int), ("num_rels", _c_int),
+                ("d", _c_int), ("c", _c_f), ("w1", P), ("b1", P), ("w2", P), ("b2", P), ("w_rot", P), ("b_rot", P),
+                ("w_trans", P), ("b_trans", P), ("q_ent", P), ("rw1", P), ("rb1", P), ("rw2", P), ("rb2", P),
+                ("global_rot", P), ("q_rel", P), ("n_cand", _c_int), ("cand", P), ("all_triples", P)]
+
+
+class ScoreJob(ctypes.Structure):
+    """regcn_score_job (include/regcn_hip.h)."""
+    _fields_ = [("q", P), ("cand", P), ("bias", P), ("scale", P), ("margin", P), ("B", _c_int), ("N", _c_int),
+                ("d", _c_int), ("c", _c_f), ("flags", _c_int), ("out", P)]
 
 
 class SnapshotDesc(ctypes.Structure):

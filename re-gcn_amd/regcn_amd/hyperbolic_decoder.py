@@ -8,6 +8,7 @@ math (hyperbolic_decoder.py:104-106).  Query prologues (MuRP / RotH / AttH and t
 relation variants) keep the reference's parameters and state_dict keys; their row maps
 run on the HIP row kernels, their small projections on torch.  Forward only.
 """
+import ctypes
 import math
 
 import torch
@@ -18,7 +19,7 @@ from torch.nn.parameter import Parameter
 from . import _lib
 from . import autograd as _ag
 from .hyperbolic_ops import HyperbolicOps
-from .weights import packed_t
+from .weights import packed_k4, packed_t
 
 SCORE_SCALE_EPSILON = 1e-6
 REL_CURVATURE_EPSILON = 1e-5
@@ -320,6 +321,65 @@ class HyperbolicAttH(_EntityDecoderBase):
         t_r = HyperbolicOps.exp_map_zero(self.trans_proj(rr).contiguous(), c)
         return HyperbolicOps.mobius_add(HyperbolicOps.project_to_ball(mixed, c),
                                         HyperbolicOps.project_to_ball(t_r, c), c)
+
+
+def roth_pair_fusable(dec, rdec, ent):
+    """The RotH entity decoder and the RotHRel relation decoder of an eval predict can run as
+    the two-launch front (roth_pair_predict): eval-mode dropout, proxy score (no relation
+    curvature), no per-query entity bias, one curvature, d <= 256 on a HIP device."""
+    return (isinstance(dec, HyperbolicRotH) and isinstance(rdec, HyperbolicRotHRel) and ent.is_cuda
+            and not (dec.training and dec.dropout.p > 0) and not (rdec.training and rdec.dropout.p > 0)
+            and not _grad_path(dec, ent) and not _grad_path(rdec, ent)
+            and dec.entity_bias is None and not dec.use_relation_specific_curvature
+            and _cf(dec.c) == _cf(rdec.c) and ent.shape[1] <= 256 and ent.shape[1] % 4 == 0)
+
+
+def roth_pair_predict(dec, rdec, ent, rel, test_triplets, num_rels, parts=None):
+    """The decoders of HyperbolicRecurrentRGCN.predict (hyperbolic_model.py:915-939) for RotH +
+    RotHRel in two launches on the calling stream: regcn_roth_queries_f32 (entity and
+    relation queries, relation candidates exp0(R), all_triples) and regcn_hyp_score_jobs_f32
+    (entity and relation scores).  Returns (all_triples, score, score_rel), the values of
+    torch.cat + decoder_ob.forward + rdecoder.forward.  `parts` (a dict) receives the queries
+    and the relation candidates."""
+    n, d = test_triplets.shape[0], ent.shape[1]
+    B, R2 = 2 * n, rel.shape[0]
+    dev = ent.device
+    ent = ent.contiguous()
+    rel = rel.detach().contiguous()
+    trip = test_triplets.contiguous()
+    f32 = torch.float32
+    q_ent = torch.empty(B, d, device=dev, dtype=f32)
+    q_rel = torch.empty(B, d, device=dev, dtype=f32)
+    cand = torch.empty(R2, d, device=dev, dtype=f32)
+    all_triples = torch.empty(B, 3, device=dev, dtype=torch.int64)
+    a = _lib.addr
+    qd = _lib.RothQueriesDesc()
+    qd.ent, qd.rel, qd.trip = a(ent), a(rel), a(trip, torch.int64)
+    qd.n_test, qd.B, qd.num_rels, qd.d, qd.c = n, B, int(num_rels), d, _cf(dec.c)
+    qd.w1, qd.b1 = a(packed_k4(dec.reshape_fc1.weight)), a(dec.reshape_fc1.bias.detach())
+    qd.w2, qd.b2 = a(packed_k4(dec.reshape_fc2.weight)), a(dec.reshape_fc2.bias.detach())
+    qd.w_rot, qd.b_rot = a(packed_k4(dec.rot_proj.weight)), a(dec.rot_proj.bias.detach())
+    qd.w_trans, qd.b_trans = a(packed_k4(dec.trans_proj.weight)), a(dec.trans_proj.bias.detach())
+    qd.rw1, qd.rb1 = a(packed_k4(rdec.reshape_fc1.weight)), a(rdec.reshape_fc1.bias.detach())
+    qd.rw2, qd.rb2 = a(packed_k4(rdec.reshape_fc2.weight)), a(rdec.reshape_fc2.bias.detach())
+    qd.global_rot = a(rdec.global_rot.detach())
+    qd.q_ent, qd.q_rel, qd.n_cand, qd.cand = a(q_ent), a(q_rel), R2, a(cand)
+    qd.all_triples = a(all_triples, torch.int64)
+    _lib.check(_lib.lib().regcn_roth_queries_f32(ctypes.byref(qd), _lib.stream()), "regcn_roth_queries_f32")
+    score = torch.empty(B, ent.shape[0], device=dev, dtype=f32)
+    score_rel = torch.empty(B, R2, device=dev, dtype=f32)
+    jobs = (_lib.ScoreJob * 2)()
+    for j, (q, cd, bias, m, out) in enumerate(((q_ent, ent, None, dec, score),
+                                               (q_rel, cand, rdec.rel_bias, rdec, score_rel))):
+        jobs[j].q, jobs[j].cand, jobs[j].bias = a(q), a(cd), a(bias.detach() if bias is not None else None)
+        jobs[j].scale = a(_scalar(m.score_scale_raw, q))
+        jobs[j].margin = a(_scalar(m.score_margin, q))
+        jobs[j].B, jobs[j].N, jobs[j].d, jobs[j].c = B, cd.shape[0], d, _cf(dec.c)
+        jobs[j].flags, jobs[j].out = _lib.SCORE_RAW_SCALE, a(out)
+    _lib.check(_lib.lib().regcn_hyp_score_jobs_f32(jobs, 2, _lib.stream()), "regcn_hyp_score_jobs_f32")
+    if parts is not None:
+        parts.update(q_ent=q_ent, q_rel=q_rel, cand=cand)
+    return all_triples, score, score_rel
 
 
 class _RelDecoderBase(nn.Module):

@@ -24,7 +24,8 @@ import torch.nn.functional as F
 
 from . import _lib
 from .hyperbolic_decoder import (HyperbolicAttH, HyperbolicAttHRel, HyperbolicConvTransE, HyperbolicConvTransR,
-                                 HyperbolicMuRP, HyperbolicMuRPRel, HyperbolicRotH, HyperbolicRotHRel)
+                                 HyperbolicMuRP, HyperbolicMuRPRel, HyperbolicRotH, HyperbolicRotHRel,
+                                 roth_pair_fusable, roth_pair_predict)
 from .graph import SnapshotGraph
 from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell, LorentzRGCNLayer, StepSpec, \
     _heavy_aggregate
@@ -184,6 +185,9 @@ class HyperbolicRecurrentRGCN(nn.Module):
     # with the phases: rows without in-edges in every snapshot of the window evolve in one
     # launch on a side stream (regcn_cold_chain_f32; window_plan); same values bit for bit
     window_plan = False
+    # eval predict with RotH + RotHRel: the decoders as two launches on the calling stream
+    # (hyperbolic_decoder.roth_pair_predict); False keeps the per-decoder path on two streams
+    fused_decoders = True
 
     def __init__(self, decoder_name, encoder_name, num_ents, num_rels, num_static_rels, num_words, h_dim, opn,
                  sequence_len, num_bases=-1, num_hidden_layers=1, dropout=0, c=0.01, self_loop=False,
@@ -597,6 +601,13 @@ class HyperbolicRecurrentRGCN(nn.Module):
         with torch.no_grad():
             c_val = self._c_float()
             dev = self.dynamic_emb.device
+            if self.fused_decoders and test_triplets.device == dev and \
+                    roth_pair_fusable(self.decoder_ob, self.rdecoder, self.dynamic_emb):
+                # one stream end to end: encoder, then the two-launch RotH/RotHRel front
+                # (queries + candidates + all_triples, then both scores in one launch)
+                evolve_embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
+                embedding = self._final_embedding(evolve_embs[-1], c_val)
+                return roth_pair_predict(self.decoder_ob, self.rdecoder, embedding, r_emb, test_triplets, num_rels)
             # the query triples do not depend on the encoder: on a HIP device they are built on
             # the side stream while the encoder runs (joined in _decode_both)
             side = self._side(dev) if dev.type == "cuda" and test_triplets.device == dev else None

@@ -76,7 +76,22 @@ def packed_t(w):
     return out
 
 
-_CACHE_ATTRS = ("_regcn_packed", "_regcn_packed_lin", "_regcn_packed_t", "_regcn_packed_cols")
+def packed_k4(w):
+    """k4 packing of an nn.Linear weight (out x in, regcn_pack_k4_f32) for the 4-row query
+    kernel (csrc/queries.hip), cached on the weight like `packed`."""
+    key = (w.data_ptr(), w._version, tuple(w.shape))
+    hit = getattr(w, "_regcn_packed_k4", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    n_out, n_in = w.shape
+    wc = w.detach().contiguous()
+    out = torch.empty(_lib.lib().regcn_packed_k4_floats(n_out, n_in), device=w.device, dtype=torch.float32)
+    _lib.call("regcn_pack_k4_f32", _lib.fptr(wc, "weight"), n_out, n_in, _lib.fptr(out), _lib.stream())
+    w._regcn_packed_k4 = (key, out, wc)  # keep wc alive until the packing kernel has run
+    return out
+
+
+_CACHE_ATTRS = ("_regcn_packed", "_regcn_packed_lin", "_regcn_packed_t", "_regcn_packed_cols", "_regcn_packed_k4")
 
 
 def invalidate(module):

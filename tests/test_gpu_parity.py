@@ -170,9 +170,10 @@ def test_relation_gru_two_phase(V, R, T, hub):
     ("lgcn", 2, True, True, False), ("lgcn", 2, True, False, True), ("hyperbolic_uvrgcn", 1, False, True, False),
 ])
 def test_phase_pipeline_bitwise(encoder, layers, skip, self_loop, ln):
-    """_forward_phases (three phase launches per timestep, csrc/timestep.hip) equals the
-    per-layer launches bit for bit, history embeddings, tangent caches and h_0 included; the
-    window holds an empty snapshot (no in-edge rows) and a one-triple one."""
+    """_forward_phases (three phase launches per timestep, csrc/timestep.hip), with and
+    without the window plan (cold rows in one side-stream launch, csrc/window.hip), equals
+    the per-layer launches bit for bit, history embeddings, tangent caches and h_0 included;
+    the window holds an empty snapshot (no in-edge rows) and a one-triple one."""
     from regcn_amd import graph as G
     from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
     from regcn_amd.synthetic import snapshot_series
@@ -189,14 +190,62 @@ def test_phase_pipeline_bitwise(encoder, layers, skip, self_loop, ln):
                                 radius_msg_gamma=0.15).to(DEV).eval()
     glist = [G.build_sub_graph(V, R, s, True, DEV) for s in snaps]
     res = {}
-    for split in (True, False):
-        m.use_phases = split
+    for mode in ("phases", "window", "layers"):
+        m.use_phases = mode != "layers"
+        m.window_plan = mode == "window"
         with torch.no_grad():
             embs, _, h0, _, _ = m.forward(glist, None, True)
         torch.cuda.synchronize()
-        res[split] = [e.clone() for e in embs] + [tangent_of(e, C)[k].clone() for e in embs for k in (0, 1)] + [h0]
-    for a, b in zip(res[True], res[False]):
-        assert torch.equal(a, b)
+        res[mode] = [e.clone() for e in embs] + [tangent_of(e, C)[k].clone() for e in embs for k in (0, 1)] + [h0]
+    m.window_plan = HyperbolicRecurrentRGCN.window_plan
+    for mode in ("phases", "window"):
+        for a, b in zip(res[mode], res["layers"]):
+            assert torch.equal(a, b), mode
+
+
+@pytest.mark.parametrize("n_test,d", [(37, 200), (1, 200), (64, 256), (5, 12)])
+def test_fused_roth_decoders(n_test, d):
+    """HyperbolicRecurrentRGCN.predict with the two-launch RotH/RotHRel front
+    (regcn_roth_queries_f32 on 4-query tiles + regcn_hyp_score_jobs_f32) against the
+    per-decoder path (16-row query kernels on two streams + torch.cat): all_triples exact,
+    scores within 1e-4 * max(1, |ref|) (the MFMA shapes differ, so do the summation orders),
+    ranks of the targets equal; decoder weights drawn well away from their 1e-3 init so the
+    reshape MLP and the projections matter.  B = 2 n_test is not a multiple of 4 in two cases."""
+    from regcn_amd import graph as G
+    from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
+    from regcn_amd.synthetic import snapshot_series
+    V, R = 2000, 30
+    snaps = snapshot_series(4, V, R, 7, 400)
+    torch.manual_seed(n_test)
+    m = HyperbolicRecurrentRGCN("roth", "hyperbolic_uvrgcn", V, R, 0, 0, d, "sub", 3, num_bases=10, num_hidden_layers=2,
+                                dropout=0.2, c=C, self_loop=True, entity_prediction=True, relation_prediction=True,
+                                use_cuda=True, radius_target=np.random.default_rng(0).uniform(0.5, 3, V).astype(np.float32),
+                                radius_msg_gamma=0.15).to(DEV).eval()
+    with torch.no_grad():
+        for dec in (m.decoder_ob, m.rdecoder):
+            for name, p in dec.named_parameters():
+                if name.endswith("weight") or name.endswith("bias"):
+                    p.normal_(0.0, 0.08)
+        m.rdecoder.score_margin.fill_(0.7)
+    glist = [G.build_sub_graph(V, R, s, True, DEV) for s in snaps[:3]]
+    test = torch.from_numpy(snaps[3][:n_test]).to(DEV)
+    res = {}
+    for fused in (True, False):
+        m.fused_decoders = fused
+        with torch.no_grad():
+            res[fused] = [x.clone() for x in m.predict(glist, R, None, test, True)]
+        torch.cuda.synchronize()
+    m.fused_decoders = HyperbolicRecurrentRGCN.fused_decoders
+    assert torch.equal(res[True][0], res[False][0])
+    assert_close(res[True][1], res[False][1].cpu().numpy(), what="entity score")
+    assert_close(res[True][2], res[False][2].cpu().numpy(), what="relation score")
+    at = res[False][0]
+    for k, col in ((1, 2), (2, 1)):
+        a, b = res[True][k], res[False][k]
+        ra = (a > a.gather(1, at[:, col:col + 1])).sum(1)
+        rb = (b > b.gather(1, at[:, col:col + 1])).sum(1)
+        diff = (ra - rb).abs()
+        assert int(diff.max()) <= 1 and int((diff > 0).sum()) <= 2  # near-ties may flip
 
 
 @pytest.mark.parametrize("tag", ["uvrgcn_roth", "lgcn_roth", "uvrgcn_murp_nores", "uvrgcn_atth_beta",
