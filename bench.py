@@ -56,9 +56,9 @@ def parse():
                          ":100-149 without --multi-step), so a server may overlap them")
     ap.add_argument("--per-layer", action="store_true",
                     help="run the encoder as per-layer launches instead of the timestep phase launches")
-    ap.add_argument("--window-plan", action="store_true",
-                    help="with the phase launches: rows without in-edges in the whole window evolve in one "
-                         "side-stream launch (csrc/window.hip)")
+    ap.add_argument("--no-memo", action="store_true",
+                    help="with the phase launches: run every row without in-edges at every timestep instead of "
+                         "copying the memoised parameter-only state of rows that had no in-edge yet")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work")
     ap.add_argument("--no-scale", action="store_true",
@@ -164,7 +164,8 @@ def kernel_profile(model, sample, d, device):
     its own stream and replayed between HIP events on that stream.  Returns {kernel:
     dict(ms, per_step, flops, bytes, ...)}."""
     from regcn_amd import hyperbolic_model as HM
-    from regcn_amd.hyperbolic_decoder import _chunked_hyperbolic_dist_score
+    from regcn_amd.hyperbolic_decoder import (_chunked_hyperbolic_dist_score, roth_pair_fusable, roth_pair_queries,
+                                              roth_pair_scores)
     hist, glist, test, _ = sample
     glist = [getattr(g, "g", g) for g in glist]  # rank 0 alone: unpartitioned (no collectives)
     g = glist[-1]
@@ -206,16 +207,27 @@ def kernel_profile(model, sample, d, device):
             ]
         at = torch.cat([test, torch.stack([test[:, 2], test[:, 1] + model.num_rels, test[:, 0]], 1)])
         B = at.shape[0]
-        emb = model._final_embedding(embs[-1], c)
+        emb = model._final_embedding(embs[-1], c).contiguous()
         dec, rdec = model.decoder_ob, model.rdecoder
-        q = dec._query(emb, h0, at)
-        if type(dec).__name__ == "HyperbolicRotH":
+        fdec = dec
+        if model.fused_decoders and roth_pair_fusable(dec, rdec, emb):
+            # the predict's two decoder launches (csrc/queries.hip, score.hip jobs)
+            rel = h0.detach().contiguous()
+            _, qe, qr, cand = roth_pair_queries(fdec, rdec, emb, rel, test, model.num_rels)
+            stages.append(("k_queries4", lambda: roth_pair_queries(fdec, rdec, emb, rel, test, model.num_rels),
+                           2.0 * B * 5.5 * d * d, 4.0 * (B * d * 5 + R2 * d * 2)))
+            stages.append(("k_score_f32_jobs", lambda: roth_pair_scores(fdec, rdec, emb, qe, qr, cand),
+                           2.0 * B * (V + R2) * d, 4.0 * (B * d * 2 + (V + R2) * d + B * (V + R2))))
+            dec = None
+        q = dec._query(emb, h0, at) if dec is not None else None
+        if dec is not None and type(dec).__name__ == "HyperbolicRotH":
             stages.append(("k_query<0>", lambda: dec._query(emb, h0, at), 2.0 * B * 3.5 * d * d,
                            4.0 * B * d * 3))
-        stages.append(("k_score_f32<0>", lambda: _chunked_hyperbolic_dist_score(
-            q, emb, dec.entity_bias, dec.c, 128, 256, score_scale=dec.score_scale_raw,
-            score_margin=dec.score_margin, _raw_scale=True), 2.0 * B * V * d, 4.0 * (B * d + V * d + B * V)))
-        if type(rdec).__name__ == "HyperbolicRotHRel":
+        if dec is not None:
+            stages.append(("k_score_f32<0>", lambda: _chunked_hyperbolic_dist_score(
+                q, emb, dec.entity_bias, dec.c, 128, 256, score_scale=dec.score_scale_raw,
+                score_margin=dec.score_margin, _raw_scale=True), 2.0 * B * V * d, 4.0 * (B * d + V * d + B * V)))
+        if dec is not None and type(rdec).__name__ == "HyperbolicRotHRel":
             stages.append(("k_query<1> + k_score (relations)", lambda: rdec.forward(emb, h0, at),
                            2.0 * B * 2 * d * d + 2.0 * B * R2 * d, 4.0 * (B * d * 3 + B * R2)))
         for name, fn, flops, nbytes in stages:
@@ -324,7 +336,7 @@ def main():
     d = args.d
     model = build_model(cfg, d, device, seed=1234)          # same weights on every rank
     model.use_phases = not args.per_layer
-    model.window_plan = args.window_plan and not args.per_layer
+    model.memo_pristine = not args.no_memo
     sharded = args.shard != "replica" and world > 1
     # replicas: independent data per rank; sharded: every rank holds the same snapshots
     samples = make_samples(cfg, args.pool, device, seed=100 if sharded else 100 + 7919 * rank,

@@ -318,9 +318,20 @@ typedef struct regcn_phase_desc {
   int32_t gru_R2;
   float* gru_pre;
   float* gru_h_out;
-  const int32_t* zrows;   /* rows without in-edges to run: NULL = rows[n_pos:V]; else a list */
-  const int32_t* zcount;  /*   of *zcount rows (device count, e.g. a window plan's |Z_t|) */
-  int32_t zbound;         /*   bounded by zbound (host) */
+  /* Memo mode (memo_h != NULL).  A row without an in-edge at any timestep so far evolves by
+   * an input-independent map of the parameters (W_evolve, skip gate, time gate, static
+   * radius): its state after this timestep is memo_* (F^{t+1} of the initial state, computed
+   * once per parameter version by regcn_cold_chain_f32 over all rows), which phase A copies
+   * to step_*_out.  The rows without in-edges that run are those with an in-edge at an earlier
+   * timestep and none since, taken from the earlier snapshots' rows[:n_pos] lists.  NULL:
+   * every row without in-edges (rows[n_pos:V]) runs. */
+  const float* memo_h;
+  const float* memo_x;
+  const float* memo_r;
+  int32_t n_prev;                                /* earlier snapshots of the window (t) */
+  const int32_t* prev_rows[REGCN_MAX_WINDOW];    /* their rows (in-edge rows first) */
+  const int32_t* prev_rowptr[REGCN_MAX_WINDOW];  /* their rowptr */
+  int32_t prev_n_pos[REGCN_MAX_WINDOW];
 } regcn_phase_desc;
 int regcn_timestep_phase_f32(const regcn_phase_desc* desc, int32_t phase, void* stream);
 

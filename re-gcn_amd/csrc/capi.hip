@@ -290,10 +290,21 @@ int regcn_timestep_phase_f32(const regcn_phase_desc* g, int32_t phase, void* s) 
   r.d = g->d;
   r.pre = g->gru_pre;
   r.h_out = g->gru_h_out;
-  a.zrows = g->zrows;
-  a.zcount = g->zcount;
-  a.zbound = g->zbound;
-  if (a.zrows && (!a.zcount || a.zbound < 0)) return set_error(REGCN_EINVAL, "a zero-row list needs its count and bound");
+  a.memo_h = g->memo_h;
+  a.memo_x = g->memo_x;
+  a.memo_r = g->memo_r;
+  a.n_prev = a.memo_h ? g->n_prev : 0;
+  if (a.memo_h) {
+    if (!a.memo_x || !a.memo_r) return set_error(REGCN_EINVAL, "memo mode needs memo_h, memo_x, memo_r");
+    if (a.n_prev < 0 || a.n_prev > REGCN_MAX_WINDOW) return set_error(REGCN_EINVAL, "n_prev out of range");
+    for (int i = 0; i < a.n_prev; ++i) {
+      a.prev_rows[i] = g->prev_rows[i];
+      a.prev_rowptr[i] = g->prev_rowptr[i];
+      a.prev_n_pos[i] = g->prev_n_pos[i];
+      if (a.prev_n_pos[i] < 0 || (a.prev_n_pos[i] && (!a.prev_rows[i] || !a.prev_rowptr[i])))
+        return set_error(REGCN_EINVAL, "earlier snapshot %d: null rows / rowptr", i);
+    }
+  }
   a.d = g->d;
   a.s1 = g->s1;
   a.tw = g->tw;

@@ -82,12 +82,35 @@ __device__ __forceinline__ void gru_pre_block(const RelGru2Args& p, int bx, int 
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r0 = bx * TM, jt = by;
   const int n_valid = min(TM, p.R2 - r0);
-  for (int t = threadIdx.x; t < TM * lda; t += 64 * PRE_WAVES) {
-    const int i = t / lda, c = t - i * lda;
-    const int part = c / dp, k = c - part * dp;
-    float v = 0.f;
-    if (i < n_valid && part < 2 && k < d) v = (part ? p.h_prev : p.emb_rel)[(int64_t)(r0 + i) * d + k];
-    A[t] = v;
+  {  // [emb_rel | h_prev] rows as float4s, every load issued before the first LDS store
+    constexpr int IT = TM * 2 * (MAX_D / 4) / (64 * PRE_WAVES);
+    const int q4 = d >> 2, n = TM * 2 * q4;
+    f4 v[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = min((int)threadIdx.x + it * 64 * PRE_WAVES, n - 1);
+      const int i = idx / (2 * q4), rem = idx - i * 2 * q4, part = rem / q4, c = (rem - part * q4) * 4;
+      v[it] = *reinterpret_cast<const f4*>((part ? p.h_prev : p.emb_rel) + (int64_t)(r0 + min(i, n_valid - 1)) * d + c);
+    }
+    // zero padding: columns [d, dp) of each part and [2 dp, lda)
+    const int npad = 2 * (dp - d) + (lda - 2 * dp);
+    for (int t = threadIdx.x; t < TM * npad; t += 64 * PRE_WAVES) {
+      const int i = t / npad, j = t - i * npad;
+      const int c = j < dp - d ? d + j : j < 2 * (dp - d) ? dp + d + (j - (dp - d)) : 2 * dp + (j - 2 * (dp - d));
+      A[i * lda + c] = 0.f;
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = threadIdx.x + it * 64 * PRE_WAVES;
+      if (idx >= n) break;
+      const int i = idx / (2 * q4), rem = idx - i * 2 * q4, part = rem / q4, c = (rem - part * q4) * 4;
+      const f4 x = i < n_valid ? v[it] : f4{0.f, 0.f, 0.f, 0.f};
+      float* dst = A + i * lda + part * dp + c;
+      dst[0] = x.x;
+      dst[1] = x.y;
+      dst[2] = x.z;
+      dst[3] = x.w;
+    }
   }
   __syncthreads();
   const bool hh = w >= PRE_WAVES / 2;

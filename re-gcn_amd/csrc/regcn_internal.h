@@ -225,10 +225,16 @@ struct PhaseArgs {
   float* r1;          // V: |layer-0 output|
   float* h2;          // V x d: layer-1 output of rows without in-edges (Poincare)
   float* n2;          // V: its |.|^2 as the epilogue carries it
-  const int* zrows;   // rows without in-edges to run (NULL: rows[n_pos:V]); with a device count:
-  const int* zcount;  //   *zcount rows, at most zbound
-  int zbound;
-  int n_pos_rt, n_zero_rt, n_gru, gru_rt;  // block counts (set by the launcher)
+  // memo mode (memo_h != NULL, regcn_phase_desc): pristine rows copy memo_* in phase A; the
+  // rows without in-edges that run come from the earlier snapshots' in-edge rows
+  const float* memo_h;
+  const float* memo_x;
+  const float* memo_r;
+  int n_prev;
+  const int* prev_rows[REGCN_MAX_WINDOW];
+  const int* prev_rowptr[REGCN_MAX_WINDOW];
+  int prev_n_pos[REGCN_MAX_WINDOW];
+  int n_pos_rt, n_zero_rt, n_gru, gru_rt, n_copy;  // block counts (set by the launcher)
   int64_t* trace;     // profiling (regcn_set_trace): {start, end} s_memrealtime per workgroup
 };
 int timestep_phase(PhaseArgs a, int phase, hipStream_t st);

@@ -41,15 +41,59 @@ __device__ __forceinline__ int load_trow(int* trow, const int* rows, int start, 
   return count;
 }
 
-// Tile b of the rows without in-edges: rows[n_pos:V], or the explicit list zrows[0:*zcount].
-// Returns the tile's row count (0: past the list; the grid is sized by a host bound).
+__device__ __forceinline__ bool row_hot(const int* rowptr, int v) { return rowptr[v + 1] > rowptr[v]; }
+
+// Tile b of the rows without in-edges that run at this timestep.  Plain mode: rows[n_pos:V].
+// Memo mode: entries [16 b, 16 b + 16) of the earlier snapshots' in-edge rows, concatenated;
+// entry v of snapshot t' runs iff v has no in-edge now nor at any snapshot after t' (so a
+// row runs once, for its last earlier snapshot), compacted by a ballot in every wave.
+// Returns the tile's row count (0: nothing to run; uniform over the workgroup).
 __device__ __forceinline__ int zero_tile_rows(const PhaseArgs& p, int b, int* trow) {
   const LayerArgs& l = p.L[0];
-  const int* zr = p.zrows ? p.zrows : l.rows + l.n_pos;
-  const int zn = p.zrows ? *p.zcount : l.V - l.n_pos;
-  const int start = b * TM;
-  if (start >= zn) return 0;
-  return load_trow(trow, zr, start, min(TM, zn - start));
+  if (!p.memo_h) {
+    const int start = b * TM, zn = l.V - l.n_pos;
+    if (start >= zn) return 0;
+    return load_trow(trow, l.rows + l.n_pos, start, min(TM, zn - start));
+  }
+  const int lane = threadIdx.x & 63;
+  int v = 0;
+  bool ok = false;
+  if (lane < TM) {
+    int e = b * TM + lane, tp = -1;
+    for (int i = 0; i < p.n_prev; ++i) {
+      if (e < p.prev_n_pos[i]) {
+        tp = i;
+        break;
+      }
+      e -= p.prev_n_pos[i];
+    }
+    if (tp >= 0) {
+      v = p.prev_rows[tp][e];
+      ok = !row_hot(l.rowptr, v);
+      for (int i = tp + 1; i < p.n_prev && ok; ++i) ok = !row_hot(p.prev_rowptr[i], v);
+    }
+  }
+  const uint64_t m = __ballot(ok);
+  if (ok && wave_id() == 0) trow[__popcll(m & ((1ull << lane) - 1ull))] = v;
+  __syncthreads();
+  return __popcll(m);
+}
+
+// Phase A, memo mode: this timestep's output rows start as the memoised pristine state
+// (the running rows overwrite theirs in phase C).  Bandwidth work at the lowest priority.
+__device__ __forceinline__ void copy_block(const PhaseArgs& p, int b) {
+  __builtin_amdgcn_s_setprio(0);
+  const int64_t n4 = (int64_t)p.L[0].V * p.d / 4, stride = (int64_t)p.n_copy * NTHR;
+  const f4* hs = reinterpret_cast<const f4*>(p.memo_h);
+  const f4* xs = reinterpret_cast<const f4*>(p.memo_x);
+  f4* hd = reinterpret_cast<f4*>(p.step.h_out);
+  f4* xd = reinterpret_cast<f4*>(p.step.x_out);
+  for (int64_t i = (int64_t)b * NTHR + threadIdx.x; i < n4; i += stride) {
+    const f4 h = hs[i], x = xs[i];
+    hd[i] = h;
+    xd[i] = x;
+  }
+  for (int64_t i = (int64_t)b * NTHR + threadIdx.x; i < p.L[0].V; i += stride) p.step.r_out[i] = p.memo_r[i];
 }
 
 __device__ __forceinline__ void store_rows_scalar(const float n2[4], float* __restrict__ out, const int* rows,
@@ -386,7 +430,8 @@ __global__ __launch_bounds__(NTHR) void k_phase_a(PhaseArgs p) {
   __builtin_amdgcn_s_setprio(2);
   if (b < p.n_pos_rt) return a_pos_rows(p, b, lds);
   b -= p.n_pos_rt;
-  gru_x_block(p.gru, b % p.gru_rt, b / p.gru_rt, lds);
+  if (b < p.n_gru) return gru_x_block(p.gru, b % p.gru_rt, b / p.gru_rt, lds);
+  copy_block(p, b - p.n_gru);
 }
 
 template <int AGG, int S>
@@ -447,7 +492,13 @@ int timestep_phase(PhaseArgs a, int phase, hipStream_t st) {
         return set_error(REGCN_EINVAL, "lorentz gather needs weights and d %% num_bases == 0");
     }
   }
-  const int n_zero_rt = ((a.zrows ? a.zbound : l0.V - l0.n_pos) + TM - 1) / TM;
+  int n_zero = l0.V - l0.n_pos;
+  if (a.memo_h) {
+    n_zero = 0;
+    for (int i = 0; i < a.n_prev; ++i) n_zero += a.prev_n_pos[i];
+  }
+  const int n_zero_rt = (n_zero + TM - 1) / TM;
+  a.n_copy = a.memo_h ? std::min(128, (int)(((int64_t)l0.V * d / 4 + NTHR * 8 - 1) / (NTHR * 8))) : 0;
   a.n_zero_rt = n_zero_rt;
   a.trace = g_trace;
   a.n_pos_rt = (l0.n_pos + TM - 1) / TM;
@@ -463,7 +514,7 @@ int timestep_phase(PhaseArgs a, int phase, hipStream_t st) {
     a.n_gru = a.gru.h_out ? gru_blocks : 0;
     if (a.n_gru && (!a.gru.h_prev || !a.gru.w_ih_x || !a.gru.pre || (!a.gru.x_mean && !a.gru.rel_start)))
       return set_error(REGCN_EINVAL, "GRU x-phase operands missing");
-    grid = (unsigned)(a.n_pos_rt + a.n_gru);
+    grid = (unsigned)(a.n_pos_rt + a.n_gru + a.n_copy);
     lds = std::max(2 * tile + TM * 4, a.n_gru ? gru_x_lds_bytes(d) : 0);
     if (grid) hipLaunchKernelGGL(k_phase_a, dim3(grid), dim3(NTHR), lds, st, a);
     return grid ? check_launch("k_phase_a") : 0;

@@ -22,50 +22,56 @@
 namespace regcn {
 
 // ---------------------------------------------------------------------------------- plan
-__global__ void k_plan_flags(PlanArgs p) {
-  const int t = blockIdx.y;
-  const int n = p.n_pos[t];
-  const int* rows = p.pos_rows[t];
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    atomicOr(p.flags + rows[i], 1 << t);
-}
-
-// One workgroup: each thread takes a contiguous run of rows, counts its C / U / Z_t rows,
-// a block-wide exclusive scan places the runs, then each thread writes its rows in order.
-constexpr int PLAN_THREADS = 1024;
-__global__ __launch_bounds__(PLAN_THREADS) void k_plan_lists(PlanArgs p) {
-  __shared__ int scan[PLAN_THREADS];
-  __shared__ int tot;
-  const int tid = threadIdx.x;
-  const int per = (p.V + PLAN_THREADS - 1) / PLAN_THREADS;
-  const int beg = min(p.V, tid * per), end = min(p.V, beg + per);
-  // lists: 0 = C, 1 = U, 2 + t = Z_t
-  for (int list = 0; list < 2 + p.T; ++list) {
-    int cnt = 0;
-    for (int v = beg; v < end; ++v) {
-      const unsigned f = (unsigned)p.flags[v];
-      cnt += list == 0 ? f == 0 : list == 1 ? f != 0 : (f != 0 && !((f >> (list - 2)) & 1u));
-    }
-    scan[tid] = cnt;
-    __syncthreads();
-    for (int off = 1; off < PLAN_THREADS; off <<= 1) {  // inclusive Hillis-Steele scan
-      const int add = tid >= off ? scan[tid - off] : 0;
-      __syncthreads();
-      scan[tid] += add;
-      __syncthreads();
-    }
-    int pos = scan[tid] - cnt;
-    if (tid == PLAN_THREADS - 1) tot = scan[tid];
-    int* out = list == 0 ? p.c_rows : list == 1 ? p.u_rows : p.z_rows + (int64_t)(list - 2) * p.z_stride;
-    for (int v = beg; v < end; ++v) {
-      const unsigned f = (unsigned)p.flags[v];
-      const bool in = list == 0 ? f == 0 : list == 1 ? f != 0 : (f != 0 && !((f >> (list - 2)) & 1u));
-      if (in) out[pos++] = v;
+// One workgroup: zero the flags, OR in bit t for each snapshot's in-edge rows, then compact
+// C / U / Z_t in row order, 1024 rows per pass: per list a wave ballot gives each row its
+// rank in the wave, per-wave counts in LDS give the wave offsets (a 16-entry scan per list).
+constexpr int PLAN_THREADS = 1024, PLAN_WAVES = PLAN_THREADS / 64, PLAN_LISTS = 2 + REGCN_MAX_WINDOW;
+__global__ __launch_bounds__(PLAN_THREADS) void k_plan(PlanArgs p) {
+  __shared__ int wofs[PLAN_LISTS][PLAN_WAVES];
+  __shared__ int base[PLAN_LISTS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nl = 2 + p.T;
+  for (int v = tid; v < p.V; v += PLAN_THREADS) p.flags[v] = 0;
+  if (tid < PLAN_LISTS) base[tid] = 0;
+  __threadfence();
+  __syncthreads();
+  for (int t = 0; t < p.T; ++t)
+    for (int i = tid; i < p.n_pos[t]; i += PLAN_THREADS) atomicOr(p.flags + p.pos_rows[t][i], 1 << t);
+  __threadfence();
+  __syncthreads();
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int v0 = 0; v0 < p.V; v0 += PLAN_THREADS) {
+    const int v = v0 + tid;
+    const unsigned f = v < p.V ? (unsigned)__hip_atomic_load(p.flags + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    bool in[PLAN_LISTS];
+    int pos[PLAN_LISTS];
+#pragma unroll
+    for (int L = 0; L < PLAN_LISTS; ++L) {
+      in[L] = v < p.V && L < nl && (L == 0 ? f == 0u : L == 1 ? f != 0u : (f != 0u && !((f >> (L - 2)) & 1u)));
+      const uint64_t m = __ballot(in[L]);
+      pos[L] = __popcll(m & lt);
+      if (lane == 0) wofs[L][w] = __popcll(m);
     }
     __syncthreads();
-    if (tid == 0) p.counts[list] = tot;
+    if (tid < nl) {  // exclusive scan of the per-wave counts, after the running base
+      int s = base[tid];
+      for (int ww = 0; ww < PLAN_WAVES; ++ww) {
+        const int c = wofs[tid][ww];
+        wofs[tid][ww] = s;
+        s += c;
+      }
+      base[tid] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int L = 0; L < PLAN_LISTS; ++L) {
+      if (!in[L]) continue;
+      int* out = L == 0 ? p.c_rows : L == 1 ? p.u_rows : p.z_rows + (int64_t)(L - 2) * p.z_stride;
+      out[wofs[L][w] + pos[L]] = v;
+    }
     __syncthreads();
   }
+  if (tid < nl) p.counts[tid] = base[tid];
 }
 
 int window_plan(const PlanArgs& a, hipStream_t st) {
@@ -78,10 +84,9 @@ int window_plan(const PlanArgs& a, hipStream_t st) {
   }
   if (a.z_stride < std::min(a.V, [&] { int s = 0; for (int t = 0; t < a.T; ++t) s += a.n_pos[t]; return s; }()))
     return set_error(REGCN_EINVAL, "z_stride below the U bound");
-  hipMemsetAsync(a.flags, 0, (size_t)a.V * sizeof(int), st);
-  if (max_pos) hipLaunchKernelGGL(k_plan_flags, dim3((max_pos + 255) / 256, a.T), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(k_plan_lists, dim3(1), dim3(PLAN_THREADS), 0, st, a);
-  return check_launch("k_plan_lists");
+  (void)max_pos;
+  hipLaunchKernelGGL(k_plan, dim3(1), dim3(PLAN_THREADS), 0, st, a);
+  return check_launch("k_plan");
 }
 
 // ----------------------------------------------------------------------------- cold chain
@@ -89,8 +94,7 @@ int window_plan(const PlanArgs& a, hipStream_t st) {
 // X1 = layer-0 output, P2 = clamp(x) (time-gate operand).  Per timestep exactly the
 // per-layer zero-tile path: layer 0 (k_layer<., ., false> zero tile), layer 1 with the
 // timestep (k_layer<., ., true> zero tile: loop and gate GEMMs in one k-loop).
-__global__ __launch_bounds__(NTHR) void k_cold_chain(ChainArgs p) {
-  extern __shared__ float lds[];
+__device__ __forceinline__ void cold_tile(const ChainArgs& p, int tile, float* lds) {
   const int lda = tile_lda(p.d);
   float* XI = lds;
   float* X1 = lds + TM * lda;
@@ -98,8 +102,7 @@ __global__ __launch_bounds__(NTHR) void k_cold_chain(ChainArgs p) {
   RowRed rr{lds + 3 * TM * lda, 0};
   int* trow = reinterpret_cast<int*>(lds + 3 * TM * lda + RED_FLOATS);
   const int n_rows = *p.n_rows;
-  const int start = blockIdx.x * TM;
-  if (start >= n_rows) return;  // grid sized by the host's bound; the plan's count is on the device
+  const int start = tile * TM;
   const int count = min(TM, n_rows - start);
   if (threadIdx.x < TM) trow[threadIdx.x] = p.rows[start + ((int)threadIdx.x < count ? threadIdx.x : 0)];
   __syncthreads();
@@ -182,6 +185,19 @@ __global__ __launch_bounds__(NTHR) void k_cold_chain(ChainArgs p) {
   }
 }
 
+// Persistent: one workgroup per CU walks the tiles (the plan's count is on the device), at
+// the lowest wave priority, so the timestep phases' waves (raised priority) win the SIMDs'
+// issue slots and this chain fills what they leave idle.
+__global__ __launch_bounds__(NTHR) void k_cold_chain(ChainArgs p) {
+  extern __shared__ float lds[];
+  __builtin_amdgcn_s_setprio(0);
+  const int n_tiles = (*p.n_rows + TM - 1) / TM;
+  for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    cold_tile(p, tile, lds);
+    __syncthreads();  // the LDS tiles are reused by the next tile
+  }
+}
+
 int cold_chain(const ChainArgs& a, int grid_bound, hipStream_t st) {
   if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "chain needs d %% 4 == 0, d <= 256 (d=%d)", a.d);
   if (a.T < 1 || a.T > REGCN_MAX_WINDOW) return set_error(REGCN_EINVAL, "chain needs 1..%d timesteps", REGCN_MAX_WINDOW);
@@ -193,7 +209,14 @@ int cold_chain(const ChainArgs& a, int grid_bound, hipStream_t st) {
     if (!a.h_out[t] || !a.x_out[t] || !a.r_out[t]) return set_error(REGCN_EINVAL, "null output of timestep %d", t);
   if (grid_bound <= 0) return 0;
   const size_t lds = (size_t)(3 * TM * tile_lda(a.d) + RED_FLOATS + TM) * 4;
-  hipLaunchKernelGGL(k_cold_chain, dim3((unsigned)((grid_bound + TM - 1) / TM)), dim3(NTHR), lds, st, a);
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n_cu = 256;
+  }
+  const int grid = std::min((grid_bound + TM - 1) / TM, n_cu);
+  hipLaunchKernelGGL(k_cold_chain, dim3((unsigned)grid), dim3(NTHR), lds, st, a);
   return check_launch("k_cold_chain");
 }
 

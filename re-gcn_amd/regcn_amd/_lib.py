@@ -122,7 +122,8 @@ class PhaseDesc(ctypes.Structure):
         ("step_c_radius", _c_f), ("step_h_out", P), ("step_x_out", P), ("step_r_out", P),
         ("gru_rel_idx", P), ("gru_rel_start", P), ("gru_rel_count", P), ("gru_x_mean", P), ("gru_emb_rel", P),
         ("gru_h_prev", P), ("gru_w_ih_e", P), ("gru_w_ih_x", P), ("gru_w_hh", P), ("gru_b_ih", P), ("gru_b_hh", P),
-        ("gru_R2", _c_int), ("gru_pre", P), ("gru_h_out", P), ("zrows", P), ("zcount", P), ("zbound", _c_int),
+        ("gru_R2", _c_int), ("gru_pre", P), ("gru_h_out", P), ("memo_h", P), ("memo_x", P), ("memo_r", P),
+        ("n_prev", _c_int), ("prev_rows", P * 16), ("prev_rowptr", P * 16), ("prev_n_pos", _c_int * 16),
     ]
 
 

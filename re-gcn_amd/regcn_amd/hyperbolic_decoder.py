@@ -334,19 +334,13 @@ def roth_pair_fusable(dec, rdec, ent):
             and _cf(dec.c) == _cf(rdec.c) and ent.shape[1] <= 256 and ent.shape[1] % 4 == 0)
 
 
-def roth_pair_predict(dec, rdec, ent, rel, test_triplets, num_rels, parts=None):
-    """The decoders of HyperbolicRecurrentRGCN.predict (hyperbolic_model.py:915-939) for RotH +
-    RotHRel in two launches on the calling stream: regcn_roth_queries_f32 (entity and
-    relation queries, relation candidates exp0(R), all_triples) and regcn_hyp_score_jobs_f32
-    (entity and relation scores).  Returns (all_triples, score, score_rel), the values of
-    torch.cat + decoder_ob.forward + rdecoder.forward.  `parts` (a dict) receives the queries
-    and the relation candidates."""
+def roth_pair_queries(dec, rdec, ent, rel, test_triplets, num_rels):
+    """regcn_roth_queries_f32: the entity (RotH) and relation (RotHRel) queries of a predict,
+    the relation candidates exp0(R) and all_triples, in one launch.  Returns
+    (all_triples, q_ent, q_rel, cand)."""
     n, d = test_triplets.shape[0], ent.shape[1]
     B, R2 = 2 * n, rel.shape[0]
     dev = ent.device
-    ent = ent.contiguous()
-    rel = rel.detach().contiguous()
-    trip = test_triplets.contiguous()
     f32 = torch.float32
     q_ent = torch.empty(B, d, device=dev, dtype=f32)
     q_rel = torch.empty(B, d, device=dev, dtype=f32)
@@ -354,7 +348,7 @@ def roth_pair_predict(dec, rdec, ent, rel, test_triplets, num_rels, parts=None):
     all_triples = torch.empty(B, 3, device=dev, dtype=torch.int64)
     a = _lib.addr
     qd = _lib.RothQueriesDesc()
-    qd.ent, qd.rel, qd.trip = a(ent), a(rel), a(trip, torch.int64)
+    qd.ent, qd.rel, qd.trip = a(ent), a(rel), a(test_triplets, torch.int64)
     qd.n_test, qd.B, qd.num_rels, qd.d, qd.c = n, B, int(num_rels), d, _cf(dec.c)
     qd.w1, qd.b1 = a(packed_k4(dec.reshape_fc1.weight)), a(dec.reshape_fc1.bias.detach())
     qd.w2, qd.b2 = a(packed_k4(dec.reshape_fc2.weight)), a(dec.reshape_fc2.bias.detach())
@@ -366,8 +360,17 @@ def roth_pair_predict(dec, rdec, ent, rel, test_triplets, num_rels, parts=None):
     qd.q_ent, qd.q_rel, qd.n_cand, qd.cand = a(q_ent), a(q_rel), R2, a(cand)
     qd.all_triples = a(all_triples, torch.int64)
     _lib.check(_lib.lib().regcn_roth_queries_f32(ctypes.byref(qd), _lib.stream()), "regcn_roth_queries_f32")
-    score = torch.empty(B, ent.shape[0], device=dev, dtype=f32)
-    score_rel = torch.empty(B, R2, device=dev, dtype=f32)
+    return all_triples, q_ent, q_rel, cand
+
+
+def roth_pair_scores(dec, rdec, ent, q_ent, q_rel, cand):
+    """regcn_hyp_score_jobs_f32: the entity scores (q_ent against every entity) and the
+    relation scores (q_rel against the candidates, + rel_bias) in one launch."""
+    B, d = q_ent.shape
+    dev = ent.device
+    score = torch.empty(B, ent.shape[0], device=dev, dtype=torch.float32)
+    score_rel = torch.empty(B, cand.shape[0], device=dev, dtype=torch.float32)
+    a = _lib.addr
     jobs = (_lib.ScoreJob * 2)()
     for j, (q, cd, bias, m, out) in enumerate(((q_ent, ent, None, dec, score),
                                                (q_rel, cand, rdec.rel_bias, rdec, score_rel))):
@@ -377,6 +380,18 @@ def roth_pair_predict(dec, rdec, ent, rel, test_triplets, num_rels, parts=None):
         jobs[j].B, jobs[j].N, jobs[j].d, jobs[j].c = B, cd.shape[0], d, _cf(dec.c)
         jobs[j].flags, jobs[j].out = _lib.SCORE_RAW_SCALE, a(out)
     _lib.check(_lib.lib().regcn_hyp_score_jobs_f32(jobs, 2, _lib.stream()), "regcn_hyp_score_jobs_f32")
+    return score, score_rel
+
+
+def roth_pair_predict(dec, rdec, ent, rel, test_triplets, num_rels, parts=None):
+    """The decoders of HyperbolicRecurrentRGCN.predict (hyperbolic_model.py:915-939) for RotH +
+    RotHRel in two launches on the calling stream (roth_pair_queries, roth_pair_scores).
+    Returns (all_triples, score, score_rel), the values of torch.cat + decoder_ob.forward +
+    rdecoder.forward.  `parts` (a dict) receives the queries and the relation candidates."""
+    ent = ent.contiguous()
+    all_triples, q_ent, q_rel, cand = roth_pair_queries(dec, rdec, ent, rel.detach().contiguous(),
+                                                        test_triplets.contiguous(), num_rels)
+    score, score_rel = roth_pair_scores(dec, rdec, ent, q_ent, q_rel, cand)
     if parts is not None:
         parts.update(q_ent=q_ent, q_rel=q_rel, cand=cand)
     return all_triples, score, score_rel

@@ -116,28 +116,6 @@ def relation_gru_step(gru, emb_rel, x, g, h_prev):
     return out
 
 
-PLAN_MAX_V = 1 << 18  # the plan's list compaction runs in one workgroup
-
-
-def window_plan(g_list, V):
-    """regcn_window_plan_i32 over the window's snapshots (device lists, device counts):
-    c_rows = rows with no in-edge in any snapshot, z_rows[t] = the other rows without
-    in-edges at t; counts = (|C|, |U|, |Z_0|, ...)."""
-    dev = g_list[0].work()["rows"].device
-    T = len(g_list)
-    zs = max(1, min(V, sum(g.n_pos for g in g_list)))
-    i32 = torch.int32
-    plan = {"flags": torch.empty(V, device=dev, dtype=i32), "c_rows": torch.empty(V, device=dev, dtype=i32),
-            "u_rows": torch.empty(V, device=dev, dtype=i32), "z_rows": torch.empty(T * zs, device=dev, dtype=i32),
-            "counts": torch.empty(2 + T, device=dev, dtype=i32), "z_stride": zs}
-    rows = (ctypes.c_void_p * T)(*[g.work()["rows"].data_ptr() for g in g_list])
-    n_pos = (ctypes.c_int32 * T)(*[g.n_pos for g in g_list])
-    a = _lib.addr
-    _lib.call("regcn_window_plan_i32", T, rows, n_pos, V, a(plan["flags"], i32), a(plan["c_rows"], i32),
-              a(plan["u_rows"], i32), a(plan["z_rows"], i32), zs, a(plan["counts"], i32), _lib.stream())
-    return plan
-
-
 def _gru_biases(gru, d, device):
     zeros = None
     if gru.bias_ih is None or gru.bias_hh is None:
@@ -182,9 +160,12 @@ class HyperbolicRecurrentRGCN(nn.Module):
     # inference of a 2-layer cell: each timestep in three phase launches (_forward_phases,
     # csrc/timestep.hip); False keeps the per-layer launches (same values bit for bit)
     use_phases = True
-    # with the phases: rows without in-edges in every snapshot of the window evolve in one
-    # launch on a side stream (regcn_cold_chain_f32; window_plan); same values bit for bit
-    window_plan = False
+    # with the phases: a row without an in-edge so far in the window holds a state that is a
+    # function of the parameters only (F^t of the initial state, F = the cell and timestep of
+    # a row without messages); those states are memoised per parameter version
+    # (regcn_cold_chain_f32 over all rows, _pristine_states) and copied, so a timestep runs
+    # only its in-edge rows and the rows that had in-edges earlier.  Same values bit for bit.
+    memo_pristine = True
     # eval predict with RotH + RotHRel: the decoders as two launches on the calling stream
     # (hyperbolic_decoder.roth_pair_predict); False keeps the per-decoder path on two streams
     fused_decoders = True
@@ -490,8 +471,10 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 return lib_call(dp, phase, stream)
             # profiling: per-workgroup {start, end} stamps of this launch (tools/phasetrace.py)
             n_gru = ((R2 + 15) // 16) * ((d + 15) // 16)
-            n_zero = ((desc.zbound if desc.zrows else V - desc.n_pos) + 15) // 16
-            kinds = ([("pos_rows", (desc.n_pos + 15) // 16), ("gru_x", n_gru)] if phase == 0 else
+            n_zero = ((sum(desc.prev_n_pos[i] for i in range(desc.n_prev)) if desc.memo_h else V - desc.n_pos)
+                      + 15) // 16
+            n_copy = min(128, (V * d // 4 + 2047) // 2048) if desc.memo_h else 0  # timestep.hip launcher
+            kinds = ([("pos_rows", (desc.n_pos + 15) // 16), ("gru_x", n_gru), ("copy", n_copy)] if phase == 0 else
                      [("pos_tiles", desc.n_pos_tiles), ("zero", n_zero)]
                      + ([("gru_pre", n_gru)] if phase == 1 and desc.gru_pre else []))
             buf = torch.zeros(4 * max(1, sum(n for _, n in kinds)), dtype=torch.int64, device=dev)
@@ -507,42 +490,21 @@ class HyperbolicRecurrentRGCN(nn.Module):
         T = len(g_list)
         outs = [(torch.empty(V, d, device=dev, dtype=f32), torch.empty(V, d, device=dev, dtype=f32),
                  torch.empty(V, device=dev, dtype=f32)) for _ in g_list]
-        ev_cold = None
-        if self.window_plan and T <= _lib.MAX_WINDOW and V <= PLAN_MAX_V:
-            # rows without in-edges anywhere in the window: their whole evolution in one launch
-            # on a side stream (fork here, join at the end); the phases run the other rows
-            plan = window_plan(g_list, V)
-            main = torch.cuda.current_stream(dev)
-            side = self._side(dev)
-            side.wait_stream(main)
-            x_init, _ = tangent_of(self.h, c_val)
-            ch = _lib.ChainDesc()
-            ch.rows, ch.n_rows = a(plan["c_rows"], torch.int32), a(plan["counts"], torch.int32)
-            ch.T, ch.d, ch.grid_bound, ch.c, ch.x0 = T, d, V, desc.c, a(x_init)
-            ch.w_evolve0, ch.w_evolve1 = desc.w_evolve[0], desc.w_evolve[1]
-            ch.w_skip1, ch.b_skip1 = desc.w_skip1, desc.b_skip1
-            for f in ("w_g", "b_g", "r_static", "w_r", "b_r", "eps_r", "beta", "layer_norm", "residual",
-                      "c_radius"):
-                setattr(ch, "step_" + f, getattr(desc, "step_" + f))
-            for t, (ho, xo, ro) in enumerate(outs):
-                ch.h_out[t], ch.x_out[t], ch.r_out[t] = a(ho), a(xo), a(ro)
-            with torch.cuda.stream(side):
-                _lib.call_desc("regcn_cold_chain_f32", ch)
-            ev_cold = torch.cuda.Event()
-            ev_cold.record(side)
-            desc.zbound = plan["z_stride"]
-            desc.zcount = None
-            keep.append(plan)
-        else:
-            plan = None
+        memo = self._pristine_states(T, c_val, desc) if self.memo_pristine and T <= _lib.MAX_WINDOW else None
+        if memo is not None:
+            keep.append(memo)
         for t, g in enumerate(g_list):
             wk = g.work()
             x0, r0 = tangent_of(self.h, c_val)
             h0 = torch.empty(R2, d, device=dev, dtype=f32)
             out = outs[t]
-            if plan is not None:  # this timestep's rows without in-edges, among the window's touched rows
-                desc.zrows = a(plan["z_rows"], torch.int32) + 4 * t * plan["z_stride"]
-                desc.zcount = a(plan["counts"], torch.int32) + 4 * (2 + t)
+            if memo is not None:  # pristine rows: memoised; rows without in-edges: the earlier in-edge rows
+                desc.memo_h, desc.memo_x, desc.memo_r = (a(m) for m in memo[t])
+                desc.n_prev = t
+                for i, gp in enumerate(g_list[:t]):
+                    wp = gp.work()
+                    desc.prev_rows[i], desc.prev_rowptr[i] = a(wp["rows"], torch.int32), a(wp["rowptr"], torch.int32)
+                    desc.prev_n_pos[i] = gp.n_pos
             desc.rowptr, desc.col_src, desc.col_type = (a(wk[k], torch.int32) for k in ("rowptr", "col_src", "col_type"))
             desc.norm, desc.budget = a(wk["norm"]), g.budget
             desc.tiles, desc.n_pos_tiles = a(wk["tiles"], torch.int32), g.n_pos_tiles
@@ -587,9 +549,45 @@ class HyperbolicRecurrentRGCN(nn.Module):
             self.h_0 = h0
             self.h = attach(out[0], out[1], out[2], c_val)
             history_embs.append(self.h)
-        if ev_cold is not None:
-            torch.cuda.current_stream(dev).wait_event(ev_cold)
         return history_embs, None, self.h_0, [], []
+
+    def _pristine_states(self, T, c_val, desc):
+        """[(h, x, r) after timestep k for k < T] of a row that receives no message in
+        timesteps 0..k: F^(k+1)(initial state) with F = layer 0 and layer 1 without messages
+        (W_evolve, the skip gate) and the timestep (time gate, radius evolution), all rows in
+        one regcn_cold_chain_f32 launch (the zero-tile op sequence: same bits).  A function of
+        the parameters only: computed once per parameter version and per T."""
+        pe = self.dynamic_emb
+        key = (T, float(c_val), bool(self.layer_norm), bool(self.use_residual_evolution), float(self.radius_min),
+               float(self.radius_max)) + tuple((p.data_ptr(), p._version) for p in self.parameters()) \
+            + tuple((b.data_ptr(), b._version) for b in self.buffers())
+        hit = self.__dict__.get("_pristine_cache")
+        if hit is not None and hit[0] == key:
+            return hit[1]
+        V, d = pe.shape
+        dev = pe.device
+        f32 = torch.float32
+        states = [(torch.empty(V, d, device=dev, dtype=f32), torch.empty(V, d, device=dev, dtype=f32),
+                   torch.empty(V, device=dev, dtype=f32)) for _ in range(T)]
+        rows = torch.arange(V, device=dev, dtype=torch.int32)
+        n_rows = torch.full((1,), V, device=dev, dtype=torch.int32)
+        x_init, _ = tangent_of(self.h, c_val)
+        a = _lib.addr
+        ch = _lib.ChainDesc()
+        ch.rows, ch.n_rows = a(rows, torch.int32), a(n_rows, torch.int32)
+        ch.T, ch.d, ch.grid_bound, ch.c, ch.x0 = T, d, V, desc.c, a(x_init)
+        ch.w_evolve0, ch.w_evolve1 = desc.w_evolve[0], desc.w_evolve[1]
+        ch.w_skip1, ch.b_skip1 = desc.w_skip1, desc.b_skip1
+        for f in ("w_g", "b_g", "r_static", "w_r", "b_r", "eps_r", "beta", "layer_norm", "residual", "c_radius"):
+            setattr(ch, "step_" + f, getattr(desc, "step_" + f))
+        for t, (ho, xo, ro) in enumerate(states):
+            ch.h_out[t], ch.x_out[t], ch.r_out[t] = a(ho), a(xo), a(ro)
+        _lib.call_desc("regcn_cold_chain_f32", ch)
+        if not torch.cuda.is_current_stream_capturing():
+            self.__dict__["_pristine_cache"] = (key, states)
+        else:
+            self.__dict__.setdefault("_capture_keep", []).append((rows, n_rows, states))
+        return states
 
     def _final_embedding(self, emb, c_val):
         if self.layer_norm:

@@ -171,9 +171,10 @@ def test_relation_gru_two_phase(V, R, T, hub):
 ])
 def test_phase_pipeline_bitwise(encoder, layers, skip, self_loop, ln):
     """_forward_phases (three phase launches per timestep, csrc/timestep.hip), with and
-    without the window plan (cold rows in one side-stream launch, csrc/window.hip), equals
-    the per-layer launches bit for bit, history embeddings, tangent caches and h_0 included;
-    the window holds an empty snapshot (no in-edge rows) and a one-triple one."""
+    without the memoised pristine states (rows without an in-edge so far: copied from
+    F^t(initial state), csrc/window.hip over all rows), equals the per-layer launches bit for
+    bit, history embeddings, tangent caches and h_0 included; the window holds an empty
+    snapshot (no in-edge rows) and a one-triple one."""
     from regcn_amd import graph as G
     from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
     from regcn_amd.synthetic import snapshot_series
@@ -190,15 +191,15 @@ def test_phase_pipeline_bitwise(encoder, layers, skip, self_loop, ln):
                                 radius_msg_gamma=0.15).to(DEV).eval()
     glist = [G.build_sub_graph(V, R, s, True, DEV) for s in snaps]
     res = {}
-    for mode in ("phases", "window", "layers"):
+    for mode in ("memo", "phases", "layers"):
         m.use_phases = mode != "layers"
-        m.window_plan = mode == "window"
+        m.memo_pristine = mode == "memo"
         with torch.no_grad():
             embs, _, h0, _, _ = m.forward(glist, None, True)
         torch.cuda.synchronize()
         res[mode] = [e.clone() for e in embs] + [tangent_of(e, C)[k].clone() for e in embs for k in (0, 1)] + [h0]
-    m.window_plan = HyperbolicRecurrentRGCN.window_plan
-    for mode in ("phases", "window"):
+    m.memo_pristine = HyperbolicRecurrentRGCN.memo_pristine
+    for mode in ("memo", "phases"):
         for a, b in zip(res[mode], res["layers"]):
             assert torch.equal(a, b), mode
 
