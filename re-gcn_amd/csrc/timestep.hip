@@ -9,13 +9,14 @@
 //
 //   A  relation GRU, x-half (k_gru_x blocks: relation means over r_to_e + W_ih^x)
 //      in-edge rows:  s1 = x0 @ W_loop[0],  tw = clamp(x0) @ W_g      (two MFMA chains)
+//      other rows:    layer 0: x1 = log0(exp0(rrelu(clamp(x0 @ W_evolve[0]))))
 //   B  in-edge tiles: layer-0 gather (messages need h_0 from A) -> finish ->
-//                     v = clamp(agg [@ W_n[0]]) + s1 -> x1, r1
-//      other rows:    layers 0 and 1 (x1 in LDS between them):
-//                     h2 = exp0(rrelu(clamp(x1 @ W_evolve[1] [skip on x0]))), |h2|^2
+//                     v = clamp(agg [@ W_n[0]]) + s1 -> x1, r1;  then s1 = x1 @ W_loop[1]
+//                     (layer 1's self-loop message, off phase C's critical path)
+//      other rows:    layer 1: h2 = exp0(rrelu(clamp(x1 @ W_evolve[1] [skip on x0]))), |h2|^2
 //      relation GRU pre-half of the NEXT timestep (k_gru_pre blocks: needs h_0 from A)
 //   C  in-edge tiles: layer-1 gather (x1, r1 from B) -> finish ->
-//                     v = clamp(agg [@ W_n[1]]) + x1 @ W_loop[1] [skip] -> timestep epilogue
+//                     v = clamp(agg [@ W_n[1]]) + s1 [skip] -> timestep epilogue
 //                     with the gate pre-activation tw from A
 //      other rows:    timestep epilogue on h2 with tw = clamp(x0) @ W_g
 //
@@ -29,9 +30,11 @@
 
 namespace regcn {
 
-// intermediate stamps 1, 2 of a workgroup (wave 0)
+// profiling (regcn_set_trace): TRACE_SLOTS stamps per workgroup, 0 = start, TRACE_SLOTS - 1 =
+// end, intermediate stamps 1 .. TRACE_SLOTS - 2 (wave 0)
+constexpr int TRACE_SLOTS = 8;
 __device__ __forceinline__ void mid_stamp(const PhaseArgs& p, int k) {
-  if (p.trace && threadIdx.x == 0) p.trace[4 * blockIdx.x + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  if (p.trace && threadIdx.x == 0) p.trace[TRACE_SLOTS * blockIdx.x + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
 }
 
 // Rows [start, start + count) of the snapshot's row list into trow; returns count.
@@ -221,25 +224,43 @@ struct RowRegs {
   }
 };
 
+// The rows of destination tile `tile` into trow, plus each lane's row degree / norm for the
+// finish; returns the row count.
+struct TileRows {
+  int count, rdeg;
+  float rnorm;
+};
+template <int AGG>
+__device__ __forceinline__ TileRows tile_rows(const LayerArgs& l, int tile, int* trow) {
+  TileRows t;
+  const int start = l.tiles[2 * tile];
+  t.count = load_trow(trow, l.rows, start, l.tiles[2 * tile + 1]);
+  const int lrow = trow[min((int)(threadIdx.x & 63), TM - 1)];
+  t.rdeg = l.rowptr[lrow + 1] - l.rowptr[lrow];
+  t.rnorm = AGG != AGG_LORENTZ ? l.norm[lrow] : 1.f;
+  return t;
+}
+
 // Gather + finish of destination tile `tile` for layer l (layer.hip k_layer's pos path).
 template <int AGG, int S>
-__device__ __forceinline__ int gather_tile(const LayerArgs& l, int tile, float* lds, const GLds& L, int* trow) {
-  const int lda = L.lda;
+__device__ __forceinline__ void gather_finish(const PhaseArgs& p, const LayerArgs& l, int tile, float* lds,
+                                              const GLds& L, int* trow, const TileRows& t) {
   float* part = lds + L.part;
   int* tmask = trow + TM;
-  const int start = l.tiles[2 * tile];
-  const int count = load_trow(trow, l.rows, start, l.tiles[2 * tile + 1]);
-  int rdeg = 0;
-  float rnorm = 1.f;
-  {
-    const int lrow = trow[min((int)(threadIdx.x & 63), TM - 1)];
-    rdeg = l.rowptr[lrow + 1] - l.rowptr[lrow];
-    if (AGG != AGG_LORENTZ) rnorm = l.norm[lrow];
-  }
-  tile_gather<AGG, S>(l, part, lda, trow, tile, tmask, lds + L.xsh);
+  mid_stamp(p, 1);
+  tile_gather<AGG, S>(l, part, L.lda, trow, tile, tmask, lds + L.xsh);
+  mid_stamp(p, 2);
   __syncthreads();
-  tile_finish<AGG>(l, part, lda, trow, count, tmask, rdeg, rnorm);
-  return count;
+  tile_finish<AGG>(l, part, L.lda, trow, t.count, tmask, t.rdeg, t.rnorm);
+  mid_stamp(p, 3);
+}
+
+template <int AGG, int S>
+__device__ __forceinline__ int gather_tile(const PhaseArgs& p, const LayerArgs& l, int tile, float* lds, const GLds& L,
+                                           int* trow) {
+  const TileRows t = tile_rows<AGG>(l, tile, trow);
+  gather_finish<AGG, S>(p, l, tile, lds, L, trow, t);
+  return t.count;
 }
 
 // v = clamp(agg [@ W_n]) from the finished tile in `part`; the B ring of W_n (if any) is
@@ -258,11 +279,13 @@ __device__ __forceinline__ void b_pos_tile(const PhaseArgs& p, int tile, float* 
   const GLds L = glds(p.d, AGG == AGG_LORENTZ && S == 0, GATHER_ROWS);
   int* trow = reinterpret_cast<int*>(lds + L.ints);
   RowRed rr{lds + L.red, 0};
-  const int count = gather_tile<AGG, S>(l, tile, lds, L, trow);
+  const TileRows tr = tile_rows<AGG>(l, tile, trow);
+  const int count = tr.count;
+  Frag lp;  // the self-loop message from phase A, in flight under the gather
+  if (l.w_loop) frag_load(lp, p.s1, trow, count, p.d);
+  gather_finish<AGG, S>(p, l, tile, lds, L, trow, tr);
   BRing br;
   if (l.w_n) br.load(l.w_n, p.d);
-  Frag lp;  // the self-loop message from phase A
-  if (l.w_loop) frag_load(lp, p.s1, trow, count, p.d);
   __syncthreads();
   Frag v;
   agg_term(v, l, lds + L.part, L.lda, br);
@@ -273,10 +296,27 @@ __device__ __forceinline__ void b_pos_tile(const PhaseArgs& p, int tile, float* 
   rrelu_clamp(v);
   float n2[4];
   rr.sumsq(v, n2);
+  mid_stamp(p, 4);
   exp0_known(v, n2, l.k);
   store_radius(n2, p.r1, trow, count);
   log0_known(v, n2, l.k);
   frag_store(v, p.x1, trow, count, p.d);
+  mid_stamp(p, 5);
+  // layer 1's self-loop message x1 @ W_loop[1] of these rows: it needs no gather, so it
+  // leaves phase C's critical path for this one (into s1: this tile read its s1 rows above)
+  const LayerArgs& l1 = p.L[1];
+  if (l1.w_loop) {
+    BRing br1;
+    br1.load(l1.w_loop, p.d);
+    float* X = lds + L.part;  // the finished tile is consumed
+    frag_to_tile(v, X, L.lda, count, p.d);
+    __syncthreads();
+    Frag lp;
+    lp.zero();
+    mfma_tile_pf(lp, X, L.lda, l1.w_loop, p.d, br1);
+    mid_stamp(p, 6);
+    frag_store(lp, p.s1, trow, count, p.d);
+  }
 }
 
 template <int AGG, int S>
@@ -286,41 +326,37 @@ __device__ __forceinline__ void c_pos_tile(const PhaseArgs& p, int tile, float* 
   const GLds L = glds(p.d, AGG == AGG_LORENTZ && S == 0, c_part_rows(skip));
   const int lda = L.lda;
   float* part = lds + L.part;
-  float* X = part;                  // after the finish: the layer input rows x1
   float* P2 = part + TM * lda;      // clamp(x0): the timestep gate operand
   float* P1 = part + 2 * TM * lda;  // skip operand: the cell input x0
   int* trow = reinterpret_cast<int*>(lds + L.ints);
   RowRed rr{lds + L.red, 0};
-  const int count = gather_tile<AGG, S>(l, tile, lds, L, trow);
-  mid_stamp(p, 1);
-  // operand rows in flight while the aggregation term is formed from the finished tile
-  RowRegs rx, r2, r1;
-  rx.load(l.x, trow, p.d, count);
+  const TileRows tr = tile_rows<AGG>(l, tile, trow);
+  const int count = tr.count;
+  // operand rows in flight under the gather: x_prev (gate blend), tw (gate pre-activation,
+  // phase A), s1 = x1 @ W_loop[1] (phase B), the skip operand
+  RowRegs r2, r1;
   r2.load(p.step.x_prev, trow, p.d, count);
   if (skip) r1.load(l.prev_t, trow, p.d, count);
-  Frag tw;
+  Frag tw, lp;
   frag_load(tw, p.tw, trow, count, p.d);
+  if (l.w_loop) frag_load(lp, p.s1, trow, count, p.d);
+  gather_finish<AGG, S>(p, l, tile, lds, L, trow, tr);
   BRing br;
-  const float* wfirst = l.w_n ? l.w_n : l.w_loop;
-  if (wfirst) br.load(wfirst, p.d);
+  if (l.w_n) br.load(l.w_n, p.d);
   __syncthreads();
   Frag v;
   agg_term(v, l, part, lda, br);
   __syncthreads();  // the finished tile is consumed: its rows take the operands
-  rx.store<false>(X, lda, p.d, count);
+  mid_stamp(p, 4);
   r2.store<true>(P2, lda, p.d, count);
   if (skip) r1.store<false>(P1, lda, p.d, count);
-  if (l.w_n && l.w_loop) br.load(l.w_loop, p.d);
   __syncthreads();
   if (l.w_loop) {
-    Frag lp;
-    lp.zero();
-    mfma_tile_pf(lp, X, lda, l.w_loop, p.d, br);
 #pragma unroll
     for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
   }
   if (skip) skip_gate(v, P1, lda, l.w_skip, l.b_skip, p.d);
-  mid_stamp(p, 2);
+  mid_stamp(p, 5);
   rrelu_clamp(v);
   float n2[4];
   rr.sumsq(v, n2);
@@ -331,11 +367,41 @@ __device__ __forceinline__ void c_pos_tile(const PhaseArgs& p, int tile, float* 
 // ------------------------------------------------------------ rows without in-edges, B, C
 // Layers 0 and 1 of a tile of rows without in-edges (k_layer's zero-tile paths), the
 // layer-0 output kept in LDS -> h2 (Poincare rows) and |h2|^2 as the epilogue carries it.
-__device__ __forceinline__ void b_zero_rows(const PhaseArgs& p, int b, float* lds) {
+__device__ __forceinline__ void a_zero_rows(const PhaseArgs& p, int b, float* lds) {
   const LayerArgs& l0 = p.L[0];
+  const int lda = tile_lda(p.d);
+  float* X = lds;  // x0
+  RowRed rr{lds + TM * lda, 0};
+  int* trow = reinterpret_cast<int*>(lds + TM * lda + RED_FLOATS);
+  const int count = zero_tile_rows(p, b, trow);
+  if (!count) return;
+  BRing br;
+  if (l0.w_evolve) br.load(l0.w_evolve, p.d);
+  stage_rows<false>(X, lda, l0.x, trow, p.d, count);
+  __syncthreads();
+  Frag v;
+  v.zero();
+  if (l0.w_evolve) {
+    Frag lp;
+    lp.zero();
+    mfma_tile_pf(lp, X, lda, l0.w_evolve, p.d, br);
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
+  }
+  rrelu_clamp(v);
+  float n2[4];
+  rr.sumsq(v, n2);
+  exp0_known(v, n2, l0.k);
+  log0_known(v, n2, l0.k);
+  frag_store(v, p.x1, trow, count, p.d);
+}
+
+// Layer 1 of a tile of rows without in-edges (their layer 0 ran in phase A: x1 in HBM)
+// -> h2 (Poincare rows) and |h2|^2 as the epilogue carries it.
+__device__ __forceinline__ void b_zero_rows(const PhaseArgs& p, int b, float* lds) {
   const LayerArgs& l = p.L[1];
   const int lda = tile_lda(p.d);
-  float* X = lds;                // x0, then the skip operand
+  float* X = lds;                // the skip operand: the cell input x0
   float* X1 = lds + TM * lda;    // layer-0 output x1
   RowRed rr{lds + 2 * TM * lda, 0};
   int* trow = reinterpret_cast<int*>(lds + 2 * TM * lda + RED_FLOATS);
@@ -343,34 +409,17 @@ __device__ __forceinline__ void b_zero_rows(const PhaseArgs& p, int b, float* ld
   if (!count) return;
   mid_stamp(p, 1);
   BRing br;
-  if (l0.w_evolve) br.load(l0.w_evolve, p.d);
-  stage_rows<false>(X, lda, l0.x, trow, p.d, count);
+  if (l.w_evolve) br.load(l.w_evolve, p.d);
+  stage_rows<false>(X1, lda, p.x1, trow, p.d, count);
+  if (l.prev_t) stage_rows<false>(X, lda, p.L[0].x, trow, p.d, count);
   __syncthreads();
-  {  // layer 0
-    Frag v;
-    v.zero();
-    if (l0.w_evolve) {
-      Frag lp;
-      lp.zero();
-      mfma_tile_pf(lp, X, lda, l0.w_evolve, p.d, br);
-#pragma unroll
-      for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
-    }
-    rrelu_clamp(v);
-    float n2[4];
-    rr.sumsq(v, n2);
-    exp0_known(v, n2, l0.k);
-    log0_known(v, n2, l0.k);
-    frag_to_tile(v, X1, lda, count, p.d);
-    __syncthreads();
-  }
   mid_stamp(p, 2);
-  Frag v;  // layer 1 (skip operand: the cell input x0, still in X)
+  Frag v;
   v.zero();
   if (l.w_evolve) {
     Frag lp;
     lp.zero();
-    mfma_tile(lp, X1, lda, l.w_evolve, p.d);
+    mfma_tile_pf(lp, X1, lda, l.w_evolve, p.d, br);
 #pragma unroll
     for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
   }
@@ -384,7 +433,6 @@ __device__ __forceinline__ void b_zero_rows(const PhaseArgs& p, int b, float* ld
 }
 
 __device__ __forceinline__ void c_zero_rows(const PhaseArgs& p, int b, float* lds) {
-  const LayerArgs& l = p.L[1];
   const int lda = tile_lda(p.d);
   float* P2 = lds;
   RowRed rr{lds + TM * lda, 0};
@@ -412,12 +460,12 @@ __device__ __forceinline__ void c_zero_rows(const PhaseArgs& p, int b, float* ld
 struct PhaseStamp {  // profiling: a workgroup's start / end (100 MHz) when p.trace is set
   const PhaseArgs& p;
   __device__ __forceinline__ explicit PhaseStamp(const PhaseArgs& a) : p(a) {
-    if (p.trace && threadIdx.x == 0) p.trace[4 * blockIdx.x] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (p.trace && threadIdx.x == 0) p.trace[TRACE_SLOTS * blockIdx.x] = (int64_t)__builtin_amdgcn_s_memrealtime();
   }
   __device__ __forceinline__ ~PhaseStamp() {
     if (p.trace) {
       __syncthreads();
-      if (threadIdx.x == 0) p.trace[4 * blockIdx.x + 3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      if (threadIdx.x == 0) p.trace[TRACE_SLOTS * blockIdx.x + TRACE_SLOTS - 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
     }
   }
 };
@@ -431,7 +479,9 @@ __global__ __launch_bounds__(NTHR) void k_phase_a(PhaseArgs p) {
   if (b < p.n_pos_rt) return a_pos_rows(p, b, lds);
   b -= p.n_pos_rt;
   if (b < p.n_gru) return gru_x_block(p.gru, b % p.gru_rt, b / p.gru_rt, lds);
-  copy_block(p, b - p.n_gru);
+  b -= p.n_gru;
+  if (b < p.n_zero_rt) return a_zero_rows(p, b, lds);
+  copy_block(p, b - p.n_zero_rt);
 }
 
 template <int AGG, int S>
@@ -514,8 +564,8 @@ int timestep_phase(PhaseArgs a, int phase, hipStream_t st) {
     a.n_gru = a.gru.h_out ? gru_blocks : 0;
     if (a.n_gru && (!a.gru.h_prev || !a.gru.w_ih_x || !a.gru.pre || (!a.gru.x_mean && !a.gru.rel_start)))
       return set_error(REGCN_EINVAL, "GRU x-phase operands missing");
-    grid = (unsigned)(a.n_pos_rt + a.n_gru + a.n_copy);
-    lds = std::max(2 * tile + TM * 4, a.n_gru ? gru_x_lds_bytes(d) : 0);
+    grid = (unsigned)(a.n_pos_rt + a.n_gru + n_zero_rt + a.n_copy);
+    lds = std::max({2 * tile + TM * 4, tile + small, a.n_gru ? gru_x_lds_bytes(d) : 0});
     if (grid) hipLaunchKernelGGL(k_phase_a, dim3(grid), dim3(NTHR), lds, st, a);
     return grid ? check_launch("k_phase_a") : 0;
   }

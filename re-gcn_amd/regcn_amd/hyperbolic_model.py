@@ -34,6 +34,7 @@ from .tangent import attach, tangent_of
 from .weights import invalidate, packed
 
 logger = logging.getLogger("hyperbolic_model")
+TRACE_SLOTS = 8  # timestep.hip: stamps per workgroup
 PHASE_TRACE = None  # profiling: a list to collect per-workgroup stamps of the phase launches
 PHASE_CAPTURE = None  # profiling: a dict to receive replayable launches of the last timestep's phases
 GEOOPT_AVAILABLE = False
@@ -414,9 +415,9 @@ class HyperbolicRecurrentRGCN(nn.Module):
         stream (regcn_timestep_phase_f32, csrc/timestep.hip):
           A  relation GRU x-half; in-edge rows' self-loop and time-gate GEMMs (need only the
              timestep input); rows without in-edges: layer 0;
-          B  in-edge tiles: layer-0 gather -> finish -> epilogue; other rows: layer 1;
-             relation GRU pre-half of the next timestep;
-          C  in-edge tiles: layer-1 gather -> self loop -> timestep; other rows: timestep.
+          B  in-edge tiles: layer-0 gather -> finish -> epilogue -> layer 1's self-loop
+             GEMM; other rows: layer 1; relation GRU pre-half of the next timestep;
+          C  in-edge tiles: layer-1 gather -> timestep; other rows: timestep.
         Same values as the per-layer launches bit for bit (tests/test_gpu_parity.py)."""
         from .weights import packed_linear, packed_linear_cols
         dev = self.dynamic_emb.device
@@ -474,10 +475,11 @@ class HyperbolicRecurrentRGCN(nn.Module):
             n_zero = ((sum(desc.prev_n_pos[i] for i in range(desc.n_prev)) if desc.memo_h else V - desc.n_pos)
                       + 15) // 16
             n_copy = min(128, (V * d // 4 + 2047) // 2048) if desc.memo_h else 0  # timestep.hip launcher
-            kinds = ([("pos_rows", (desc.n_pos + 15) // 16), ("gru_x", n_gru), ("copy", n_copy)] if phase == 0 else
+            kinds = ([("pos_rows", (desc.n_pos + 15) // 16), ("gru_x", n_gru), ("zero", n_zero), ("copy", n_copy)]
+                     if phase == 0 else
                      [("pos_tiles", desc.n_pos_tiles), ("zero", n_zero)]
                      + ([("gru_pre", n_gru)] if phase == 1 and desc.gru_pre else []))
-            buf = torch.zeros(4 * max(1, sum(n for _, n in kinds)), dtype=torch.int64, device=dev)
+            buf = torch.zeros(TRACE_SLOTS * max(1, sum(n for _, n in kinds)), dtype=torch.int64, device=dev)
             _lib.call("regcn_set_trace", _lib.addr(buf, torch.int64))
             rc = lib_call(dp, phase, stream)
             _lib.call("regcn_set_trace", None)

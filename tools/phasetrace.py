@@ -33,29 +33,32 @@ def main(config="icews14s_lgcn_roth", empty=""):
         model.forward(glist, None, True)
         torch.cuda.synchronize()
         rec, HM.PHASE_TRACE = HM.PHASE_TRACE, None
+    K = HM.TRACE_SLOTS
     for t, (phase, kinds, buf) in enumerate(rec):
-        st = buf.view(-1, 4).cpu().double()
+        st = buf.view(-1, K).cpu().double()
         t0 = st[st[:, 0] > 0, 0].min()
-        line = "%s%d span %6.2f us |" % (phase, t // 3, float((st[:, 3].max() - t0) / 100.0))
+        line = "%s%d span %6.2f us |" % (phase, t // 3, float((st[:, K - 1].max() - t0) / 100.0))
         off = 0
         for name, n in kinds:
             if n == 0:
                 continue
             s = st[off:off + n]
             off += n
-            s = s[s[:, 3] > 0]  # workgroups past a device-counted list exit unstamped
+            s = s[s[:, K - 1] > 0]  # workgroups past a device-counted list exit unstamped
             if len(s) == 0:
                 continue
             n = len(s)
             start = (s[:, 0] - t0) / 100.0
-            dur = (s[:, 3] - s[:, 0]) / 100.0
-            end = (s[:, 3] - t0) / 100.0
+            dur = (s[:, K - 1] - s[:, 0]) / 100.0
+            end = (s[:, K - 1] - t0) / 100.0
             line += " %s x%d start %.2f/%.2f dur %.2f/%.2f end %.2f" % (
                 name, n, float(start.median()), float(start.max()), float(dur.median()), float(dur.max()),
                 float(end.max()))
-            if bool((s[:, 1] > 0).all()) and bool((s[:, 2] > 0).all()):
-                seg = [(s[:, 1] - s[:, 0]) / 100.0, (s[:, 2] - s[:, 1]) / 100.0, (s[:, 3] - s[:, 2]) / 100.0]
-                line += " [%s]" % " ".join("%.2f" % float(x.median()) for x in seg)
+            # segments between consecutive stamps present in every workgroup of the kind
+            cols = [0] + [k for k in range(1, K - 1) if bool((s[:, k] > 0).all())] + [K - 1]
+            if len(cols) > 2:
+                seg = [(s[:, b] - s[:, a]) / 100.0 for a, b in zip(cols[:-1], cols[1:])]
+                line += " [%s]" % " ".join("%d:%.2f" % (b, float(x.median())) for b, x in zip(cols[1:], seg))
             line += " |"
         print(line, flush=True)
 
