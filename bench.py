@@ -14,8 +14,14 @@ doubling x GCN layers x history snapshots), whole job.
 Multi-GPU: one process per GPU, each rank runs its own independent samples (replicas:
 the path has no exchange step at this size); scaling = weak.
 
-The timed region replays one captured HIP graph per pool sample (inputs resident in
-HBM).  `roofline` reports the dominant kernel, timed live with HIP events on its own
+Every step computes everything from the parameters and its snapshots: no state is kept
+across steps except the weights' MFMA fragment packing (a layout of each weight, redone
+when the weight changes).  `--serving-cache` keeps the parameter-only states (initial
+entity state, the pristine-row memo) across steps instead; it is reported separately.
+Predicts of different test snapshots are independent (hyperbolic_main.py:100-149 without
+--multi-step), so `--concurrent` (default 4) of the pool's samples run together, one
+stream each, inside one captured HIP graph of the whole pool (inputs resident in HBM);
+`latency_ms_per_predict` is one sample's predict alone.  `roofline` reports the dominant kernel, timed live with HIP events on its own
 stream; `cpu_baseline` times the CPU oracle (oracle/, a restatement of the reference
 op sequence) on the same workload on rank 0.  `aggregation_roofline` (N=1) is the
 north-star HBM check: the d=200 aggregation kernels on a config-5 snapshot
@@ -44,21 +50,24 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="icews14s_lgcn_roth")
-    ap.add_argument("--pool", type=int, default=4, help="distinct samples cycled through the timed steps")
+    ap.add_argument("--pool", type=int, default=8, help="distinct samples cycled through the timed steps")
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph replay")
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="steps captured per HIP graph (default: the whole pool, replayed as one launch; "
                          "1 = one graph per step)")
-    ap.add_argument("--concurrent", type=int, default=1,
+    ap.add_argument("--concurrent", type=int, default=4,
                     help="independent samples in flight together (one stream each inside the pool's HIP "
                          "graph): predicts of different test snapshots are independent (hyperbolic_main.py "
                          ":100-149 without --multi-step), so a server may overlap them")
     ap.add_argument("--per-layer", action="store_true",
                     help="run the encoder as per-layer launches instead of the timestep phase launches")
-    ap.add_argument("--no-memo", action="store_true",
-                    help="with the phase launches: run every row without in-edges at every timestep instead of "
-                         "copying the memoised parameter-only state of rows that had no in-edge yet")
+    ap.add_argument("--serving-cache", action="store_true",
+                    help="keep parameter-only states across steps (initial entity state, timestep 0's GRU "
+                         "pre-half, and the memoised state of rows without an in-edge so far in the window, "
+                         "copied instead of recomputed); default: every step computes everything from the "
+                         "parameters and its snapshots")
+    ap.add_argument("--no-memo", action="store_true", help=argparse.SUPPRESS)  # the default now
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work")
     ap.add_argument("--no-scale", action="store_true",
@@ -173,18 +182,24 @@ def kernel_profile(model, sample, d, device):
     E = g.number_of_edges()
     T = len(glist)
     n_pos = g.n_pos
-    n_zero = V - n_pos
+    # rows without in-edges that the captured launches (the window's last timestep) run: all
+    # of them, or with the pristine memo only the earlier snapshots' in-edge rows (the
+    # kernel's grid bound; an upper bound of the rows it runs)
+    memo = model.memo_pristine and model.param_caches
+    n_zero = sum(x.n_pos for x in glist[:-1]) if memo else V - n_pos
     st = torch.cuda.Stream(device)
     res = {}
     c = model._c_float()
     R2 = model.emb_rel.shape[0]
     lorentz = model.encoder_name == "lgcn"
-    lay0 = model.rgcn.layers[0]
+    lay0, lay1 = model.rgcn.layers[0], model.rgcn.layers[1]
     tag = "3, %d" % (d // lay0.num_bases if d // lay0.num_bases in (1, 2, 4) else 0) if lorentz else "0, 1"
     gemm = 2.0 * d * d  # flops per row of one d x d product
     wn = 0 if lorentz else gemm * n_pos  # union: agg @ W_n
+    skip = 2 if getattr(lay1, "skip_connect", False) else 1
     gather_b = E * (4 * d + 8 + (0 if lorentz else 4)) + V * 4 * 2
     row_b = 4.0 * d  # bytes of one fp32 row
+    gru_w = 4.0 * 3 * d * d  # one 3d x d GRU weight half
     with torch.no_grad(), torch.cuda.stream(st):
         HM.PHASE_CAPTURE = {}
         try:
@@ -194,16 +209,21 @@ def kernel_profile(model, sample, d, device):
             HM.PHASE_CAPTURE = None
         stages = []
         if cap:
+            # per launch: A = in-edge rows' self-loop + time-gate GEMMs, layer 0 of the other
+            # rows, the GRU x-half (R2 x 3d x d); B = layer-0 gathers (+ W_n), layer 1's
+            # self-loop GEMM of the in-edge rows, layer 1 of the other rows (the last
+            # timestep's B has no next GRU pre-half); C = layer-1 gathers (+ W_n), the time
+            # gate of the other rows (the in-edge rows' ran in A)
             stages += [
                 ("k_phase_a", cap["A"][0],
-                 2 * gemm * n_pos + 2.0 * R2 * 3 * d * d,
-                 row_b * n_pos * 3 + 4.0 * R2 * d * 6 + 4.0 * 3 * d * d),
+                 2 * gemm * n_pos + gemm * n_zero + 2.0 * R2 * 3 * d * d,
+                 row_b * (4 * n_pos + 2 * n_zero) + 4.0 * R2 * d * 3 + gru_w),
                 ("k_phase_b<%s>" % tag, cap["B"][0],
-                 wn + 2 * gemm * n_zero + 2.0 * R2 * 3 * d * 2 * d,
-                 gather_b + row_b * (3 * n_pos + 2 * n_zero) + 4.0 * R2 * d * 6 + 4.0 * 6 * d * d),
+                 wn + gemm * n_pos + skip * gemm * n_zero,
+                 gather_b + row_b * (3 * n_pos + (1 + skip) * n_zero)),
                 ("k_phase_c<%s>" % tag, cap["C"][0],
-                 wn + gemm * (n_pos + n_zero),
-                 gather_b + row_b * (4 * n_pos + 4 * n_zero)),
+                 wn + gemm * n_zero,
+                 gather_b + row_b * ((4 + skip) * n_pos + 4 * n_zero)),
             ]
         at = torch.cat([test, torch.stack([test[:, 2], test[:, 1] + model.num_rels, test[:, 0]], 1)])
         B = at.shape[0]
@@ -336,7 +356,7 @@ def main():
     d = args.d
     model = build_model(cfg, d, device, seed=1234)          # same weights on every rank
     model.use_phases = not args.per_layer
-    model.memo_pristine = not args.no_memo
+    model.memo_pristine = model.param_caches = args.serving_cache
     sharded = args.shard != "replica" and world > 1
     # replicas: independent data per rank; sharded: every rank holds the same snapshots
     samples = make_samples(cfg, args.pool, device, seed=100 if sharded else 100 + 7919 * rank,
@@ -440,6 +460,17 @@ def main():
         edges_total = float(edges_local)
     value = edges_total / elapsed / 1e6
 
+    # latency of one predict alone (concurrency 1): its HIP graph replayed and waited for
+    lat_ms = None
+    if graphs and rank == 0:
+        lat = []
+        for k in range(40):
+            t1 = time.perf_counter()
+            graphs[k % len(graphs)].replay()
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t1)
+        lat_ms = float(np.median(lat)) * 1e3
+
     kern = kernel_profile(model, samples[0], d, device) if rank == 0 else {}
     out = None
     if rank == 0:
@@ -479,9 +510,10 @@ def main():
                           "edges_per_step": int(np.mean(epw)), "queries_per_step": 2 * cfg["per_snap"],
                           "hip_graph": bool(graphs), "steps_per_graph_launch": len(samples) if pool_graph else 1,
                           "concurrent_samples": conc, "encoder_launches": "per-layer" if args.per_layer
-                          else "timestep phases",
+                          else "timestep phases", "serving_cache": bool(args.serving_cache),
                           "parallelism": ("%s-partitioned snapshots x%d" % (args.shard, world)) if sharded
                           else "replicas x%d" % world},
+               "latency_ms_per_predict": round(lat_ms, 4) if lat_ms else None,
                "roofline": roof, "kernels": kernels, "breakdown": breakdown, "aggregation_roofline": scale,
                "decoder_roofline": dec, "cpu_baseline": cpu, "mrr_parity": mrr}
         print(json.dumps(out), flush=True)

@@ -15,10 +15,11 @@ from regcn_amd import hyperbolic_model as HM  # noqa: E402
 from regcn_amd.synthetic import CONFIGS  # noqa: E402
 
 
-def main(config="icews14s_lgcn_roth", empty=""):
+def main(config="icews14s_lgcn_roth", empty="", memo="1"):
     dev = torch.device("cuda", 0)
     cfg = CONFIGS[config]
     model = bench.build_model(cfg, 200, dev, seed=1234)
+    model.memo_pristine = memo != "0"  # "0": every row runs at every timestep
     sample = bench.make_samples(cfg, 1, dev, seed=100)[0]
     _, glist, _, _ = sample
     if empty:  # edgeless snapshots: every row on the in-degree-0 path (throughput of that path alone)
