@@ -186,7 +186,9 @@ def kernel_profile(model, sample, d, device):
     # of them, or with the pristine memo only the earlier snapshots' in-edge rows (the
     # kernel's grid bound; an upper bound of the rows it runs)
     memo = model.memo_pristine and model.param_caches
-    n_zero = sum(x.n_pos for x in glist[:-1]) if memo else V - n_pos
+    split = not memo and model.split_zero_rows  # the rows without in-edges in k_zero_step
+    n_zero = sum(x.n_pos for x in glist[:-1]) if memo else 0 if split else V - n_pos
+    n_zs = V - n_pos if split else 0
     st = torch.cuda.Stream(device)
     res = {}
     c = model._c_float()
@@ -225,6 +227,8 @@ def kernel_profile(model, sample, d, device):
                  wn + gemm * n_zero,
                  gather_b + row_b * ((4 + skip) * n_pos + 4 * n_zero)),
             ]
+            if "Z" in cap:  # rows without in-edges: W_evolve[0], W_evolve[1] (+ skip), W_g; x0 in, h, x out
+                stages.append(("k_zero_step", cap["Z"][0], (2 + skip) * gemm * n_zs, row_b * 3 * n_zs))
         at = torch.cat([test, torch.stack([test[:, 2], test[:, 1] + model.num_rels, test[:, 0]], 1)])
         B = at.shape[0]
         emb = model._final_embedding(embs[-1], c).contiguous()
@@ -252,7 +256,7 @@ def kernel_profile(model, sample, d, device):
                            2.0 * B * 2 * d * d + 2.0 * B * R2 * d, 4.0 * (B * d * 3 + B * R2)))
         for name, fn, flops, nbytes in stages:
             ms = event_time(fn, 100, st)
-            per_step = T if name.startswith("k_phase") else 1
+            per_step = T if name.startswith(("k_phase", "k_zero")) else 1
             res[name] = dict(ms=ms, per_step=per_step, flops=flops, bytes=nbytes, **_work(flops, nbytes, ms))
     torch.cuda.synchronize()
     return res
@@ -487,7 +491,7 @@ def main():
                    for k, v in kern.items()}
         # SURVEY.md §8(d) asks for edges/s per layer and per encoder forward besides the
         # end-to-end step: from the live kernel times (sum of per-step kernel time, no gaps)
-        enc_us = sum(v["ms"] * 1e3 * v["per_step"] for k, v in kern.items() if k.startswith("k_phase"))
+        enc_us = sum(v["ms"] * 1e3 * v["per_step"] for k, v in kern.items() if k.startswith(("k_phase", "k_zero")))
         e_step = float(np.mean(epw))
         breakdown = {"encoder_kernels_us_per_step": round(enc_us, 2),
                      "encoder_M_edges_per_s": round(e_step / enc_us, 3) if enc_us else None,

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 5
+#define REGCN_ABI_VERSION 6
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -244,6 +244,13 @@ typedef struct regcn_chain_desc {
   float* r_out[REGCN_MAX_WINDOW];
 } regcn_chain_desc;
 int regcn_cold_chain_f32(const regcn_chain_desc* desc, void* stream);
+/* regcn_zero_step_f32: the rows of ONE snapshot without in-edges (e.g. rows + n_pos of its
+ *   row list) through one timestep (T == 1): layer 0, layer 1, the timestep epilogue with
+ *   x0 as the timestep input, one workgroup per 16 rows; rows[0 .. grid_bound) (host count;
+ *   n_rows unused).  The phase launches of that timestep then set skip_zero_rows; it runs on
+ *   any stream ordered after the previous timestep and before the next one's phase A.
+ *   Equal bit for bit to the phases' rows-without-in-edges paths. */
+int regcn_zero_step_f32(const regcn_chain_desc* desc, void* stream);
 
 /* ---- a2-a9: one timestep of a 2-layer cell in three launches on one stream ---------- */
 /* hyperbolic_model.py:797-869 with HyperbolicRGCNCell / LorentzRGCNCell of 2 layers.  The
@@ -332,6 +339,9 @@ typedef struct regcn_phase_desc {
   const int32_t* prev_rows[REGCN_MAX_WINDOW];    /* their rows (in-edge rows first) */
   const int32_t* prev_rowptr[REGCN_MAX_WINDOW];  /* their rowptr */
   int32_t prev_n_pos[REGCN_MAX_WINDOW];
+  /* Plain mode only: 1 = the launches skip the rows without in-edges (the caller runs them
+   * through regcn_zero_step_f32 beside the phases); 0 = the phases run them. */
+  int32_t skip_zero_rows;
 } regcn_phase_desc;
 int regcn_timestep_phase_f32(const regcn_phase_desc* desc, int32_t phase, void* stream);
 

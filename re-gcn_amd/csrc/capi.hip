@@ -178,9 +178,9 @@ int regcn_window_plan_i32(int32_t T, const int32_t* const* pos_rows, const int32
   return window_plan(a, ST(s));
 }
 
-int regcn_cold_chain_f32(const regcn_chain_desc* g, void* s) {
+// regcn_cold_chain_f32 / regcn_zero_step_f32 share the descriptor
+static int chain_args(const regcn_chain_desc* g, ChainArgs& a) {
   if (!g) return set_error(REGCN_EINVAL, "null descriptor");
-  ChainArgs a{};
   a.rows = g->rows;
   a.n_rows = g->n_rows;
   a.T = g->T;
@@ -210,7 +210,19 @@ int regcn_cold_chain_f32(const regcn_chain_desc* g, void* s) {
     a.x_out[i] = g->x_out[i];
     a.r_out[i] = g->r_out[i];
   }
+  return 0;
+}
+
+int regcn_cold_chain_f32(const regcn_chain_desc* g, void* s) {
+  ChainArgs a{};
+  if (int rc = chain_args(g, a)) return rc;
   return cold_chain(a, g->grid_bound, ST(s));
+}
+
+int regcn_zero_step_f32(const regcn_chain_desc* g, void* s) {
+  ChainArgs a{};
+  if (int rc = chain_args(g, a)) return rc;
+  return zero_step(a, g->grid_bound, ST(s));
 }
 
 int regcn_timestep_phase_f32(const regcn_phase_desc* g, int32_t phase, void* s) {
@@ -305,6 +317,7 @@ int regcn_timestep_phase_f32(const regcn_phase_desc* g, int32_t phase, void* s) 
         return set_error(REGCN_EINVAL, "earlier snapshot %d: null rows / rowptr", i);
     }
   }
+  a.skip_zero_rows = a.memo_h ? 0 : g->skip_zero_rows;
   a.d = g->d;
   a.s1 = g->s1;
   a.tw = g->tw;

@@ -171,7 +171,8 @@ __global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
   mark(4);
 
   if constexpr (STEP) {
-    step_epilogue(rr, v, n2, P2, lda, trow, count, p.step, p.trace, gate_with_loop ? &tw : nullptr);
+    if (gate_with_loop) step_epilogue_tw(rr, v, n2, P2, lda, trow, count, p.step, tw, p.trace);
+    else step_epilogue(rr, v, n2, P2, lda, trow, count, p.step, p.trace);
   } else {
     frag_store(v, p.h_out, trow, count, p.d);
     if (p.r_next) store_radius(n2, p.r_next, trow, count);

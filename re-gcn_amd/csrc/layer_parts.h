@@ -46,20 +46,17 @@ __device__ __forceinline__ void frag_to_tile(const Frag& a, float* T, int lda, i
 // x_lds / p2_lds (optional): the output tangent rows and their +-10 clamp also into LDS tiles
 // (the next timestep's operands when a kernel runs several timesteps; they may alias P: P's
 // last read precedes the radius reduction's barrier).
-__device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4], const float* P, int lda,
-                                              const int* trow, int n_valid, const StepArgs& p,
-                                              int64_t* trace = nullptr, const Frag* tw_pre = nullptr,
-                                              float* x_lds = nullptr, float* p2_lds = nullptr) {
+// tw: the time-gate pre-activation clamp(x_prev) @ W_g (taken by reference: a pointer to a
+// local Frag compared against null pins it in scratch memory, private null being nonzero).
+// h_out / x_out / r_out: the output rows (p's own, or per-timestep ones of a chain: passed
+// apart, since a local copy of StepArgs would live in scratch).
+__device__ __forceinline__ void step_epilogue_out(RowRed& rr, Frag& ct, float n2[4], const float* P, int lda,
+                                                  const int* trow, int n_valid, const StepArgs& p, const Frag& tw,
+                                                  float* h_out, float* x_out, float* r_out, int64_t* trace = nullptr,
+                                                  float* x_lds = nullptr, float* p2_lds = nullptr) {
   auto stamp = [&](int k) {  // profiling: phase stamps 14, 15 (trace_mark)
     if (trace && threadIdx.x == 0) trace[blockIdx.x * 16 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
   };
-  Frag tw;  // time-gate pre-activation clamp(x_prev) @ W_g, unless the caller ran it already
-  if (tw_pre) {
-    tw = *tw_pre;
-  } else {
-    tw.zero();
-    mfma_tile(tw, P, lda, p.w_g, p.d);
-  }
   stamp(14);
   project_known(ct, n2, p.k);
   if (p.layer_norm) {
@@ -106,15 +103,15 @@ __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4],
     const float dyn = fmaxf(sqrtf(n2o), REGCN_EPS);
     newr = (p.beta * rs + (1.f - p.beta) * dyn) + delta;
   }
-  const Curv& kr = p.residual ? p.k_rad : p.k;
+  const Curv kr = p.residual ? p.k_rad : p.k;  // by value: a pointer select would pin a local StepArgs in scratch
   float f[4];
   spread_rows(fminf(fmaxf(newr, REGCN_EPS), kr.rmax) / fmaxf(sqrtf(n2o), REGCN_EPS), f);
   scale_known(ct, n2, f);
-  frag_store(ct, p.h_out, trow, n_valid, p.d);
-  if (p.r_out) store_radius(n2, p.r_out, trow, n_valid);
-  if (p.x_out || x_lds) {
+  frag_store(ct, h_out, trow, n_valid, p.d);
+  if (r_out) store_radius(n2, r_out, trow, n_valid);
+  if (x_out || x_lds) {
     log0_known(ct, n2, p.k);
-    if (p.x_out) frag_store(ct, p.x_out, trow, n_valid, p.d);
+    if (x_out) frag_store(ct, x_out, trow, n_valid, p.d);
     if (x_lds) {
       frag_to_tile(ct, x_lds, lda, n_valid, p.d);
 #pragma unroll
@@ -122,6 +119,24 @@ __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4],
       frag_to_tile(ct, p2_lds, lda, n_valid, p.d);
     }
   }
+}
+
+__device__ __forceinline__ void step_epilogue_tw(RowRed& rr, Frag& ct, float n2[4], const float* P, int lda,
+                                                 const int* trow, int n_valid, const StepArgs& p, const Frag& tw,
+                                                 int64_t* trace = nullptr) {
+  step_epilogue_out(rr, ct, n2, P, lda, trow, n_valid, p, tw, p.h_out, p.x_out, p.r_out, trace);
+}
+
+// The timestep epilogue computing the time-gate GEMM itself (tw_pre == nullptr) or taking the
+// caller's.
+__device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4], const float* P, int lda,
+                                              const int* trow, int n_valid, const StepArgs& p,
+                                              int64_t* trace = nullptr, const Frag* tw_pre = nullptr) {
+  if (tw_pre) return step_epilogue_tw(rr, ct, n2, P, lda, trow, n_valid, p, *tw_pre, trace);
+  Frag tw;
+  tw.zero();
+  mfma_tile(tw, P, lda, p.w_g, p.d);
+  step_epilogue_tw(rr, ct, n2, P, lda, trow, n_valid, p, tw, trace);
 }
 
 // Profiling hook: wall-clock phase stamps (100 MHz) of wave 0, 16 slots per workgroup.
@@ -313,7 +328,7 @@ __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int
     for (int w2 = 0; w2 < NWAVE; ++w2) {
       if ((tmask[w2] >> i) & 1) {  // slot i + w2 written by wave w2 (wave-uniform branch)
         const float* src = part + (i + w2) * lda;
-        const f4 v = *reinterpret_cast<const f4*>(src + colc);  // rows 128-B aligned (tile_lda)
+        const f4 v = *reinterpret_cast<const f4*>(src + colc);  // rows 16-B aligned (tile_lda)
         acc[q] += active ? v : zero;
         if (AGG == AGG_LORENTZ) acc0[q] += src[d];
       }

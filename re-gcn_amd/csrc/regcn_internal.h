@@ -212,6 +212,7 @@ struct ChainArgs {
   float* r_out[REGCN_MAX_WINDOW];
 };
 int cold_chain(const ChainArgs& a, int grid_bound, hipStream_t st);
+int zero_step(const ChainArgs& a, int n_rows, hipStream_t st);
 
 // One timestep of a 2-layer cell in three phase launches (timestep.hip).
 struct PhaseArgs {
@@ -234,6 +235,7 @@ struct PhaseArgs {
   const int* prev_rows[REGCN_MAX_WINDOW];
   const int* prev_rowptr[REGCN_MAX_WINDOW];
   int prev_n_pos[REGCN_MAX_WINDOW];
+  int skip_zero_rows;  // plain mode: the rows without in-edges run in k_zero_step instead
   int n_pos_rt, n_zero_rt, n_gru, gru_rt, n_copy;  // block counts (set by the launcher)
   int64_t* trace;     // profiling (regcn_set_trace): {start, end} s_memrealtime per workgroup
 };

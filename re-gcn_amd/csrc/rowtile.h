@@ -5,7 +5,7 @@
 // measured slower: at ~180 VGPRs one 8-wave workgroup fills a CU, so its barriers and
 // serial phases no longer overlap with a second workgroup's.)  An A operand (16 x d) sits
 // in LDS with a row stride `lda` = 2 (mod 32) floats, so the 16 rows x 4 k-offsets one
-// MFMA step reads fall in distinct banks.  B operands are weights prepacked into MFMA
+// MFMA step reads fall in distinct banks (tile_lda).  B operands are weights prepacked into MFMA
 // fragment order (k_pack_weight, layer.hip):
 //     Wp[s][jq][lane][e] = W[4s + lane/16][16(4jq + e) + lane%16]
 // so at k-step s a wave reads one coalesced TPW-float vector per lane.
@@ -39,8 +39,14 @@ constexpr int RED_FLOATS = 4 * NWAVE * TM;  // RowRed scratch (2 buffers x 2 qua
 
 typedef float bvec __attribute__((ext_vector_type(TPW)));
 
-// LDS row stride for width d: smallest value >= d + 2 that is 2 (mod 32).
-__host__ __device__ constexpr int tile_lda(int d) { return d + 2 + ((32 - (d + 2) % 32) % 32); }
+// LDS row stride for width d: the smallest multiple of 4 that is >= d + 1 (a Lorentz gather
+// partial keeps its time coordinate in column d) with lda / 4 odd.  Rows stay 16-B aligned
+// (ds_read/write_b128), and the 64 banks see no conflict in the MFMA A reads (16 rows x 4
+// k-offsets: rows at i * lda mod 64 = 4 (i * lda/4 mod 16), distinct for lda/4 odd) nor in
+// the C-layout tile reads/writes (4 rows x 16 columns: rows 4 * lda apart = 16 banks).
+__host__ __device__ constexpr int tile_lda(int d) {
+  return ((d + 4) & ~3) + ((((d + 4) >> 2) & 1) ? 0 : 4);
+}
 
 struct Frag {
   f4 t[TPW];
@@ -76,11 +82,7 @@ __device__ __forceinline__ void stage_rows(float* T, int lda, const float* __res
     f4 x = v[it];
     if (CLAMP10) x = clamp4(x, -10.f, 10.f);
     if (i >= n_valid) x = f4{0.f, 0.f, 0.f, 0.f};
-    float* dst = T + i * lda + c;
-    dst[0] = x.x;
-    dst[1] = x.y;
-    dst[2] = x.z;
-    dst[3] = x.w;
+    *reinterpret_cast<f4*>(T + i * lda + c) = x;  // 16-B aligned rows (tile_lda)
   }
 }
 

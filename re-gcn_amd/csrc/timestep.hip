@@ -215,11 +215,7 @@ struct RowRegs {
       f4 x = v[it];
       if (CLAMP10) x = clamp4(x, -10.f, 10.f);
       if (i >= n_valid) x = f4{0.f, 0.f, 0.f, 0.f};
-      float* dst = T + i * lda + c;
-      dst[0] = x.x;
-      dst[1] = x.y;
-      dst[2] = x.z;
-      dst[3] = x.w;
+      *reinterpret_cast<f4*>(T + i * lda + c) = x;
     }
   }
 };
@@ -361,7 +357,7 @@ __device__ __forceinline__ void c_pos_tile(const PhaseArgs& p, int tile, float* 
   float n2[4];
   rr.sumsq(v, n2);
   exp0_known(v, n2, l.k);
-  step_epilogue(rr, v, n2, P2, lda, trow, count, p.step, nullptr, &tw);
+  step_epilogue_tw(rr, v, n2, P2, lda, trow, count, p.step, tw);
 }
 
 // ------------------------------------------------------------ rows without in-edges, B, C
@@ -452,7 +448,7 @@ __device__ __forceinline__ void c_zero_rows(const PhaseArgs& p, int b, float* ld
   tw.zero();
   mfma_tile_pf(tw, P2, lda, p.step.w_g, p.d, br);
   mid_stamp(p, 2);
-  step_epilogue(rr, v, n2, P2, lda, trow, count, p.step, nullptr, &tw);
+  step_epilogue_tw(rr, v, n2, P2, lda, trow, count, p.step, tw);
 }
 
 // ---------------------------------------------------------------------------- the kernels
@@ -542,7 +538,7 @@ int timestep_phase(PhaseArgs a, int phase, hipStream_t st) {
         return set_error(REGCN_EINVAL, "lorentz gather needs weights and d %% num_bases == 0");
     }
   }
-  int n_zero = l0.V - l0.n_pos;
+  int n_zero = a.skip_zero_rows ? 0 : l0.V - l0.n_pos;
   if (a.memo_h) {
     n_zero = 0;
     for (int i = 0; i < a.n_prev; ++i) n_zero += a.prev_n_pos[i];

@@ -94,14 +94,16 @@ int window_plan(const PlanArgs& a, hipStream_t st) {
 // X1 = layer-0 output, P2 = clamp(x) (time-gate operand).  Per timestep exactly the
 // per-layer zero-tile path: layer 0 (k_layer<., ., false> zero tile), layer 1 with the
 // timestep (k_layer<., ., true> zero tile: loop and gate GEMMs in one k-loop).
-__device__ __forceinline__ void cold_tile(const ChainArgs& p, int tile, float* lds) {
+// SEQ: layer 1's two GEMMs one after the other (one B ring: fewer registers, more resident
+// workgroups for the throughput-bound per-timestep launch); same k-order, same bits.
+template <bool SEQ>
+__device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_rows, float* lds) {
   const int lda = tile_lda(p.d);
   float* XI = lds;
   float* X1 = lds + TM * lda;
   float* P2 = lds + 2 * TM * lda;
   RowRed rr{lds + 3 * TM * lda, 0};
   int* trow = reinterpret_cast<int*>(lds + 3 * TM * lda + RED_FLOATS);
-  const int n_rows = *p.n_rows;
   const int start = tile * TM;
   const int count = min(TM, n_rows - start);
   if (threadIdx.x < TM) trow[threadIdx.x] = p.rows[start + ((int)threadIdx.x < count ? threadIdx.x : 0)];
@@ -111,7 +113,8 @@ __device__ __forceinline__ void cold_tile(const ChainArgs& p, int tile, float* l
   stage_rows<false>(XI, lda, p.x0, trow, p.d, count);
   stage_rows<true>(P2, lda, p.x0, trow, p.d, count);
   __syncthreads();
-  for (int t = 0; t < p.T; ++t) {
+  const int T = SEQ ? 1 : p.T;  // the per-timestep launch: one timestep, a static index
+  for (int t = 0; t < T; ++t) {
     // ---- layer 0: v = x @ W_evolve[0]; rrelu(clamp); exp0; x1 = log0
     {
       Frag v;
@@ -139,7 +142,17 @@ __device__ __forceinline__ void cold_tile(const ChainArgs& p, int tile, float* l
     {
       Frag v, tw;
       v.zero();
-      if (p.w_evolve1) {
+      if (SEQ) {
+        if (p.w_evolve1) {
+          Frag lp;
+          lp.zero();
+          mfma_tile(lp, X1, lda, p.w_evolve1, p.d);
+#pragma unroll
+          for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
+        }
+        tw.zero();
+        mfma_tile(tw, P2, lda, p.step.w_g, p.d);
+      } else if (p.w_evolve1) {
         Frag acc[2];
         acc[0].zero();
         acc[1].zero();
@@ -174,12 +187,9 @@ __device__ __forceinline__ void cold_tile(const ChainArgs& p, int tile, float* l
       float n2[4];
       rr.sumsq(v, n2);
       exp0_known(v, n2, p.k);
-      StepArgs st = p.step;
-      st.h_out = p.h_out[t];
-      st.x_out = p.x_out[t];
-      st.r_out = p.r_out[t];
-      const bool more = t + 1 < p.T;
-      step_epilogue(rr, v, n2, P2, lda, trow, count, st, nullptr, &tw, more ? XI : nullptr, more ? P2 : nullptr);
+      const bool more = t + 1 < T;
+      step_epilogue_out(rr, v, n2, P2, lda, trow, count, p.step, tw, p.h_out[t], p.x_out[t], p.r_out[t], nullptr,
+                        more ? XI : nullptr, more ? P2 : nullptr);
       __syncthreads();
     }
   }
@@ -191,11 +201,23 @@ __device__ __forceinline__ void cold_tile(const ChainArgs& p, int tile, float* l
 __global__ __launch_bounds__(NTHR) void k_cold_chain(ChainArgs p) {
   extern __shared__ float lds[];
   __builtin_amdgcn_s_setprio(0);
-  const int n_tiles = (*p.n_rows + TM - 1) / TM;
+  const int n_rows = *p.n_rows;
+  const int n_tiles = (n_rows + TM - 1) / TM;
   for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    cold_tile(p, tile, lds);
+    chain_tile<false>(p, tile, n_rows, lds);
     __syncthreads();  // the LDS tiles are reused by the next tile
   }
+}
+
+// ------------------------------------------------------------- one timestep, no in-edges
+// The rows of one snapshot that receive no message (rows[n_pos:V]) through this timestep:
+// layer 0, layer 1, the timestep epilogue in one tile pass (rows held in LDS between them),
+// one workgroup per 16-row tile.  Launched on a side stream beside the phase launches, which
+// then carry only the in-edge tiles and the relation GRU (regcn_phase_desc.skip_zero_rows):
+// the phases keep their registers for the gather paths and these tiles keep theirs.
+__global__ __launch_bounds__(NTHR) void k_zero_step(ChainArgs p, int n_rows) {
+  extern __shared__ float lds[];
+  chain_tile<true>(p, blockIdx.x, n_rows, lds);
 }
 
 int cold_chain(const ChainArgs& a, int grid_bound, hipStream_t st) {
@@ -218,6 +240,21 @@ int cold_chain(const ChainArgs& a, int grid_bound, hipStream_t st) {
   const int grid = std::min((grid_bound + TM - 1) / TM, n_cu);
   hipLaunchKernelGGL(k_cold_chain, dim3((unsigned)grid), dim3(NTHR), lds, st, a);
   return check_launch("k_cold_chain");
+}
+
+int zero_step(const ChainArgs& a, int n_rows, hipStream_t st) {
+  if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "zero step needs d %% 4 == 0, d <= 256 (d=%d)", a.d);
+  if (a.T != 1) return set_error(REGCN_EINVAL, "zero step runs one timestep (T=%d)", a.T);
+  const StepArgs& s = a.step;
+  if (n_rows < 0) return set_error(REGCN_EINVAL, "negative row count");
+  if (n_rows && (!a.rows || !a.x0 || !s.w_g || !s.b_g || !s.r_static)) return set_error(REGCN_EINVAL, "null pointer");
+  if (s.residual && (!s.w_r || !s.b_r)) return set_error(REGCN_EINVAL, "residual radius needs w_r and b_r");
+  if (a.w_skip1 && !a.b_skip1) return set_error(REGCN_EINVAL, "skip needs a bias");
+  if (!a.h_out[0] || !a.x_out[0] || !a.r_out[0]) return set_error(REGCN_EINVAL, "null output");
+  if (!n_rows) return 0;
+  const size_t lds = (size_t)(3 * TM * tile_lda(a.d) + RED_FLOATS + TM) * 4;
+  hipLaunchKernelGGL(k_zero_step, dim3((unsigned)((n_rows + TM - 1) / TM)), dim3(NTHR), lds, st, a, n_rows);
+  return check_launch("k_zero_step");
 }
 
 }  // namespace regcn

@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libregcn_hip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -54,6 +54,7 @@ _SIGS = {
     "regcn_timestep_phase_f32": [P, _c_int, P],
     "regcn_window_plan_i32": [_c_int, P, P, _c_int, P, P, P, P, _c_int, P, P],
     "regcn_cold_chain_f32": [P, P],
+    "regcn_zero_step_f32": [P, P],
     "regcn_partial_sum_f32": [P, _c_int, P, _c_int, _c_int, P, _c_int, P],
     "regcn_packed_linear_floats": [_c_int, _c_int, _c_int],
     "regcn_pack_linear_f32": [P, _c_int, _c_int, _c_int, P, P],
@@ -124,6 +125,7 @@ class PhaseDesc(ctypes.Structure):
         ("gru_h_prev", P), ("gru_w_ih_e", P), ("gru_w_ih_x", P), ("gru_w_hh", P), ("gru_b_ih", P), ("gru_b_hh", P),
         ("gru_R2", _c_int), ("gru_pre", P), ("gru_h_out", P), ("memo_h", P), ("memo_x", P), ("memo_r", P),
         ("n_prev", _c_int), ("prev_rows", P * 16), ("prev_rowptr", P * 16), ("prev_n_pos", _c_int * 16),
+        ("skip_zero_rows", _c_int),
     ]
 
 

@@ -171,6 +171,11 @@ class HyperbolicRecurrentRGCN(nn.Module):
     # the pristine-row memo) kept across calls per parameter version; False recomputes them in
     # every forward (bench.py's headline: a step computes everything from the parameters)
     param_caches = True
+    # with the phases and no memo: a snapshot's rows without in-edges run their whole
+    # timestep in one launch (regcn_zero_step_f32) on a side stream beside the phase launches,
+    # which then carry only the in-edge tiles and the relation GRU.  Same values bit for bit.
+    split_zero_rows = True
+    zero_rows_side_stream = False  # True: the zero-row launch forks to a side stream
     # eval predict with RotH + RotHRel: the decoders as two launches on the calling stream
     # (hyperbolic_decoder.roth_pair_predict); False keeps the per-decoder path on two streams
     fused_decoders = True
@@ -422,6 +427,9 @@ class HyperbolicRecurrentRGCN(nn.Module):
           B  in-edge tiles: layer-0 gather -> finish -> epilogue -> layer 1's self-loop
              GEMM; other rows: layer 1; relation GRU pre-half of the next timestep;
           C  in-edge tiles: layer-1 gather -> timestep; other rows: timestep.
+        Without the memo (split_zero_rows) the rows without in-edges leave A/B/C: one
+        regcn_zero_step_f32 launch on a side stream runs their layer 0, layer 1 and timestep,
+        forked after timestep t - 1 and joined after C.
         Same values as the per-layer launches bit for bit (tests/test_gpu_parity.py)."""
         from .weights import packed_linear, packed_linear_cols
         dev = self.dynamic_emb.device
@@ -476,8 +484,8 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 return lib_call(dp, phase, stream)
             # profiling: per-workgroup {start, end} stamps of this launch (tools/phasetrace.py)
             n_gru = ((R2 + 15) // 16) * ((d + 15) // 16)
-            n_zero = ((sum(desc.prev_n_pos[i] for i in range(desc.n_prev)) if desc.memo_h else V - desc.n_pos)
-                      + 15) // 16
+            n_zero = ((sum(desc.prev_n_pos[i] for i in range(desc.n_prev)) if desc.memo_h else
+                       0 if desc.skip_zero_rows else V - desc.n_pos) + 15) // 16
             n_copy = min(128, (V * d // 4 + 2047) // 2048) if desc.memo_h else 0  # timestep.hip launcher
             kinds = ([("pos_rows", (desc.n_pos + 15) // 16), ("gru_x", n_gru), ("zero", n_zero), ("copy", n_copy)]
                      if phase == 0 else
@@ -499,6 +507,18 @@ class HyperbolicRecurrentRGCN(nn.Module):
         memo = self._pristine_states(T, c_val, desc) if self.memo_pristine and T <= _lib.MAX_WINDOW else None
         if memo is not None:
             keep.append(memo)
+        split = memo is None and self.split_zero_rows
+        desc.skip_zero_rows = int(split)
+        cur = torch.cuda.current_stream(dev)
+        side = self._side(dev, 2) if split and self.zero_rows_side_stream else cur
+        if split:
+            zd = _lib.ChainDesc()
+            zd.T, zd.d, zd.c = 1, d, desc.c
+            zd.w_evolve0, zd.w_evolve1 = desc.w_evolve[0], desc.w_evolve[1]
+            zd.w_skip1, zd.b_skip1 = desc.w_skip1, desc.b_skip1
+            for f in ("w_g", "b_g", "r_static", "w_r", "b_r", "eps_r", "beta", "layer_norm", "residual", "c_radius"):
+                setattr(zd, "step_" + f, getattr(desc, "step_" + f))
+            zero_call = _lib.lib().regcn_zero_step_f32
         for t, g in enumerate(g_list):
             wk = g.work()
             x0, r0 = tangent_of(self.h, c_val)
@@ -521,6 +541,20 @@ class HyperbolicRecurrentRGCN(nn.Module):
             desc.x0, desc.r0 = a(x0), a(r0)
             keep.extend([x0, r0, h0, out])
             desc.step_h_out, desc.step_x_out, desc.step_r_out = a(out[0]), a(out[1]), a(out[2])
+            if split and V > g.n_pos:
+                # Z: this snapshot's rows without in-edges through the timestep, on the side
+                # stream: after timestep t - 1 (its input x0), joined before timestep t + 1
+                zd.rows, zd.grid_bound = a(wk["rows"], torch.int32) + 4 * g.n_pos, V - g.n_pos
+                zd.x0 = a(x0)
+                zd.h_out[0], zd.x_out[0], zd.r_out[0] = a(out[0]), a(out[1]), a(out[2])
+                if PHASE_CAPTURE is not None:  # profiling: a replayable launch (bench.py)
+                    zsnap = type(zd).from_buffer_copy(zd)
+                    PHASE_CAPTURE["Z"] = (lambda: _lib.check(zero_call(ctypes.byref(zsnap), _lib.stream()),
+                                                             "regcn_zero_step_f32"), keep + [zsnap])
+                if side is not cur:
+                    side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    _lib.check(zero_call(ctypes.byref(zd), _lib.stream()), "regcn_zero_step_f32")
             # A: GRU x-half (relation means of x0 over this snapshot's r_to_e spans)
             x_mean = relation_context(x0, g, R2) if g.rel_max_span > REL_INLINE_MAX_SPAN else None
             desc.gru_rel_idx = a(wk["rel_idx"], torch.int32) if wk["rel_idx"].numel() else None
@@ -550,6 +584,8 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 desc.agg[1] = a(agg1)
                 keep.append(agg1)
             _lib.check(call(ctypes.byref(desc), 2, _lib.stream()), "regcn_timestep_phase_f32(C)")
+            if split and side is not cur:
+                cur.wait_stream(side)  # the timestep's rows are complete
             desc.agg[0] = desc.agg[1] = None
             pre, h_prev = pre_next, h0
             self.h_0 = h0

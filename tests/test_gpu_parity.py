@@ -170,7 +170,8 @@ def test_relation_gru_two_phase(V, R, T, hub):
     ("lgcn", 2, True, True, False), ("lgcn", 2, True, False, True), ("hyperbolic_uvrgcn", 1, False, True, False),
 ])
 def test_phase_pipeline_bitwise(encoder, layers, skip, self_loop, ln):
-    """_forward_phases (three phase launches per timestep, csrc/timestep.hip), with and
+    """_forward_phases (three phase launches per timestep, csrc/timestep.hip; without the memo
+    also with the rows without in-edges in their own side-stream launch, csrc/window.hip), with and
     without the memoised pristine states (rows without an in-edge so far: copied from
     F^t(initial state), csrc/window.hip over all rows), equals the per-layer launches bit for
     bit, history embeddings, tangent caches and h_0 included; the window holds an empty
@@ -191,15 +192,17 @@ def test_phase_pipeline_bitwise(encoder, layers, skip, self_loop, ln):
                                 radius_msg_gamma=0.15).to(DEV).eval()
     glist = [G.build_sub_graph(V, R, s, True, DEV) for s in snaps]
     res = {}
-    for mode in ("memo", "phases", "layers"):
+    for mode in ("memo", "split", "phases", "layers"):
         m.use_phases = mode != "layers"
         m.memo_pristine = mode == "memo"
+        m.split_zero_rows = mode == "split"  # rows without in-edges in regcn_zero_step_f32
         with torch.no_grad():
             embs, _, h0, _, _ = m.forward(glist, None, True)
         torch.cuda.synchronize()
         res[mode] = [e.clone() for e in embs] + [tangent_of(e, C)[k].clone() for e in embs for k in (0, 1)] + [h0]
     m.memo_pristine = HyperbolicRecurrentRGCN.memo_pristine
-    for mode in ("memo", "phases"):
+    m.split_zero_rows = HyperbolicRecurrentRGCN.split_zero_rows
+    for mode in ("memo", "split", "phases"):
         for a, b in zip(res[mode], res["layers"]):
             assert torch.equal(a, b), mode
 
