@@ -13,7 +13,9 @@ timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1 || { echo "bench f
 timeout -k 10 200 python bench.py --serving-cache --no-scale --no-cpu-baseline > gpurun_out/bench_serving.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench_serving.log; exit 1; }
 timeout -k 10 200 python bench.py --concurrent 1 --no-scale --no-cpu-baseline > gpurun_out/bench_c1.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench_c1.log; exit 1; }
 timeout -k 10 120 python tools/phasetrace.py icews14s_lgcn_roth "" 0 > gpurun_out/trace.log 2>&1 || { echo "trace failed"; tail -20 gpurun_out/trace.log; exit 1; }
-B="python bench.py --no-cpu-baseline --no-scale"
+# the profiled command runs one predict at a time, so the per-kernel durations match the
+# live (isolated) HIP-event averages of the bench line
+B="python bench.py --no-cpu-baseline --no-scale --concurrent 1"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- $B > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- $B --steps 48 > gpurun_out/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- $B --steps 48 > gpurun_out/pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
