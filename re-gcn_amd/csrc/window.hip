@@ -96,8 +96,15 @@ int window_plan(const PlanArgs& a, hipStream_t st) {
 // timestep (k_layer<., ., true> zero tile: loop and gate GEMMs in one k-loop).
 // SEQ: layer 1's two GEMMs one after the other (one B ring: fewer registers, more resident
 // workgroups for the throughput-bound per-timestep launch); same k-order, same bits.
+// trace (profiling, regcn_set_trace): 8 stamps per workgroup, 0 = start, 7 = end, 1-6 after
+// staging / layer-0 GEMM / layer-0 epilogue / layer-1 GEMMs / skip + activation / timestep.
 template <bool SEQ>
-__device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_rows, float* lds) {
+__device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_rows, float* lds,
+                                           int64_t* trace = nullptr) {
+  auto stamp = [&](int k) {
+    if (trace && threadIdx.x == 0) trace[8 * blockIdx.x + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   const int lda = tile_lda(p.d);
   float* XI = lds;
   float* X1 = lds + TM * lda;
@@ -113,6 +120,8 @@ __device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_r
   stage_rows<false>(XI, lda, p.x0, trow, p.d, count);
   stage_rows<true>(P2, lda, p.x0, trow, p.d, count);
   __syncthreads();
+  stamp(1);
+  Frag tw;
   const int T = SEQ ? 1 : p.T;  // the per-timestep launch: one timestep, a static index
   for (int t = 0; t < T; ++t) {
     // ---- layer 0: v = x @ W_evolve[0]; rrelu(clamp); exp0; x1 = log0
@@ -127,6 +136,7 @@ __device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_r
 #pragma unroll
         for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
       }
+      stamp(2);
 #pragma unroll
       for (int j = 0; j < TPW; ++j) v.t[j] = leaky4(clamp4(v.t[j], -10.f, 10.f));
       float n2[4];
@@ -135,12 +145,13 @@ __device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_r
       log0_known(v, n2, p.k);
       frag_to_tile(v, X1, lda, count, p.d);
       __syncthreads();
+      stamp(3);
     }
     // ---- layer 1 + timestep: v = x1 @ W_evolve[1] beside tw = clamp(x) @ W_g; skip gate on
     // the cell input; rrelu(clamp); exp0; the timestep epilogue (outputs of timestep t, and
     // the next timestep's operands into XI / P2)
     {
-      Frag v, tw;
+      Frag v;
       v.zero();
       if (SEQ) {
         if (p.w_evolve1) {
@@ -166,6 +177,7 @@ __device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_r
         tw.zero();
         mfma_tile(tw, P2, lda, p.step.w_g, p.d);
       }
+      stamp(4);
       if (p.w_skip1) {  // v = g v + (1 - g) x, g = sigmoid(x @ W_skip + b)
         Frag g;
         g.zero();
@@ -187,10 +199,12 @@ __device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_r
       float n2[4];
       rr.sumsq(v, n2);
       exp0_known(v, n2, p.k);
+      stamp(5);
       const bool more = t + 1 < T;
       step_epilogue_out(rr, v, n2, P2, lda, trow, count, p.step, tw, p.h_out[t], p.x_out[t], p.r_out[t], nullptr,
                         more ? XI : nullptr, more ? P2 : nullptr);
       __syncthreads();
+      stamp(7);
     }
   }
 }
@@ -215,9 +229,9 @@ __global__ __launch_bounds__(NTHR) void k_cold_chain(ChainArgs p) {
 // one workgroup per 16-row tile.  Launched on a side stream beside the phase launches, which
 // then carry only the in-edge tiles and the relation GRU (regcn_phase_desc.skip_zero_rows):
 // the phases keep their registers for the gather paths and these tiles keep theirs.
-__global__ __launch_bounds__(NTHR) void k_zero_step(ChainArgs p, int n_rows) {
+__global__ __launch_bounds__(NTHR) void k_zero_step(ChainArgs p, int n_rows, int64_t* trace) {
   extern __shared__ float lds[];
-  chain_tile<true>(p, blockIdx.x, n_rows, lds);
+  chain_tile<true>(p, blockIdx.x, n_rows, lds, trace);
 }
 
 int cold_chain(const ChainArgs& a, int grid_bound, hipStream_t st) {
@@ -253,7 +267,7 @@ int zero_step(const ChainArgs& a, int n_rows, hipStream_t st) {
   if (!a.h_out[0] || !a.x_out[0] || !a.r_out[0]) return set_error(REGCN_EINVAL, "null output");
   if (!n_rows) return 0;
   const size_t lds = (size_t)(3 * TM * tile_lda(a.d) + RED_FLOATS + TM) * 4;
-  hipLaunchKernelGGL(k_zero_step, dim3((unsigned)((n_rows + TM - 1) / TM)), dim3(NTHR), lds, st, a, n_rows);
+  hipLaunchKernelGGL(k_zero_step, dim3((unsigned)((n_rows + TM - 1) / TM)), dim3(NTHR), lds, st, a, n_rows, g_trace);
   return check_launch("k_zero_step");
 }
 

@@ -554,7 +554,14 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 if side is not cur:
                     side.wait_stream(cur)
                 with torch.cuda.stream(side):
+                    if PHASE_TRACE is not None:  # profiling: per-workgroup stamps (tools/phasetrace.py)
+                        n_zt = (V - g.n_pos + 15) // 16
+                        zbuf = torch.zeros(TRACE_SLOTS * n_zt, dtype=torch.int64, device=dev)
+                        _lib.call("regcn_set_trace", _lib.addr(zbuf, torch.int64))
                     _lib.check(zero_call(ctypes.byref(zd), _lib.stream()), "regcn_zero_step_f32")
+                    if PHASE_TRACE is not None:
+                        _lib.call("regcn_set_trace", None)
+                        PHASE_TRACE.append(("Z", [("zero_step", n_zt)], zbuf))
             # A: GRU x-half (relation means of x0 over this snapshot's r_to_e spans)
             x_mean = relation_context(x0, g, R2) if g.rel_max_span > REL_INLINE_MAX_SPAN else None
             desc.gru_rel_idx = a(wk["rel_idx"], torch.int32) if wk["rel_idx"].numel() else None

@@ -35,10 +35,12 @@ def main(config="icews14s_lgcn_roth", empty="", memo="1"):
         torch.cuda.synchronize()
         rec, HM.PHASE_TRACE = HM.PHASE_TRACE, None
     K = HM.TRACE_SLOTS
-    for t, (phase, kinds, buf) in enumerate(rec):
+    seen = {}
+    for phase, kinds, buf in rec:
+        t = seen[phase] = seen.get(phase, -1) + 1  # timestep of this launch
         st = buf.view(-1, K).cpu().double()
         t0 = st[st[:, 0] > 0, 0].min()
-        line = "%s%d span %6.2f us |" % (phase, t // 3, float((st[:, K - 1].max() - t0) / 100.0))
+        line = "%s%d span %6.2f us |" % (phase, t, float((st[:, K - 1].max() - t0) / 100.0))
         off = 0
         for name, n in kinds:
             if n == 0:
