@@ -405,6 +405,13 @@ def main():
         raise SystemExit("--concurrent needs the whole-pool HIP graph (no --no-graph / --graph-steps)")
     if not args.no_graph:
         cap = torch.cuda.Stream(device)
+        # one predict alone (the per-sample graphs: latency, --graph-steps 1) keeps its rows
+        # without in-edges inside the phase launches, beside the in-edge tiles' latency
+        # chains; with several predicts in flight they run as their own launch
+        # (regcn_zero_step_f32), whose workgroups the other predicts' chains overlap.  Both
+        # are bit for bit the same values (tests/test_gpu_parity.py).
+        split_many = model.split_zero_rows
+        model.split_zero_rows = False
         with torch.no_grad():
             for i in range(len(samples)):
                 gph = torch.cuda.CUDAGraph()
@@ -414,6 +421,7 @@ def main():
                     with torch.cuda.graph(gph, stream=cap):
                         eager(i)
                 graphs.append(gph)
+            model.split_zero_rows = split_many and bool(lanes)
             if gs > 1 and gs == len(samples):
                 pool_graph = torch.cuda.CUDAGraph()
                 with torch.cuda.stream(cap):
