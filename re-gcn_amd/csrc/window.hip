@@ -209,9 +209,9 @@ __device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_r
   }
 }
 
-// Persistent: one workgroup per CU walks the tiles (the plan's count is on the device), at
-// the lowest wave priority, so the timestep phases' waves (raised priority) win the SIMDs'
-// issue slots and this chain fills what they leave idle.
+// One workgroup per tile (the tile count is on the device: a grid over the host's bound,
+// the loop covers a bound beyond 64 workgroups per CU), at the lowest wave priority, so
+// concurrent timestep phases' waves (raised priority) win the SIMDs' issue slots.
 __global__ __launch_bounds__(NTHR) void k_cold_chain(ChainArgs p) {
   extern __shared__ float lds[];
   __builtin_amdgcn_s_setprio(0);
@@ -251,7 +251,8 @@ int cold_chain(const ChainArgs& a, int grid_bound, hipStream_t st) {
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       n_cu = 256;
   }
-  const int grid = std::min((grid_bound + TM - 1) / TM, n_cu);
+  // one workgroup per tile up to the bound (the device count may be smaller: the rest exit)
+  const int grid = std::max(1, std::min((grid_bound + TM - 1) / TM, 64 * n_cu));
   hipLaunchKernelGGL(k_cold_chain, dim3((unsigned)grid), dim3(NTHR), lds, st, a);
   return check_launch("k_cold_chain");
 }

@@ -341,34 +341,19 @@ class HyperbolicRecurrentRGCN(nn.Module):
         c_val = self._c_float()
         dev = self.dynamic_emb.device
         V, d = self.dynamic_emb.shape
-        r_static = self._static_radius(c_val).contiguous()
-        # The initial entity state (hyperbolic_model.py:775-782) is a function of parameters
-        # only: computed once per parameter version and reused by every predict (the kernels
-        # read it, none writes it), so a captured predict graph holds no init launch.
-        pe = self.dynamic_emb
-        key = (pe.data_ptr(), pe._version, self.radius_static.data_ptr(), self.radius_static._version,
-               float(c_val), bool(self.layer_norm), float(self.radius_min), float(self.radius_max))
-        hit = self.__dict__.get("_init_cache")
-        if hit is not None and hit[0] == key and self.param_caches:
-            h, x, r = hit[1]
+        scope = self.__dict__.get("_scope")
+        if scope is not None and scope["c"] == c_val:  # a batch's shared parameter-only states
+            r_static = scope["r_static"]
+            h, x, r = scope["init"]
         else:
-            dyn = pe.detach().contiguous()
-            h = torch.empty_like(dyn)
-            x = torch.empty_like(dyn)
-            r = torch.empty(V, device=dev, dtype=torch.float32)
-            _lib.call("regcn_init_entities_f32", _lib.fptr(dyn, "dynamic_emb"), _lib.fptr(r_static), V, d, c_val,
-                      int(bool(self.layer_norm)), _lib.fptr(h), _lib.fptr(x), _lib.fptr(r), _lib.stream())
-            if not torch.cuda.is_current_stream_capturing():
-                self.__dict__["_init_cache"] = (key, (h, x, r))
+            r_static = self._static_radius(c_val).contiguous()
+            h, x, r = self._initial_state(c_val, r_static)
         attach(h, x, r, c_val)
         self.h = h
         R2 = self.num_rels * 2
         history_embs = []
         trev = self.temporal_radius_evolution
-        w_r = trev.radius_mlp.weight.detach().reshape(-1).contiguous()
-        b_r = trev.radius_mlp.bias.detach().reshape(-1).contiguous()
-        wg = packed(self.time_gate_weight)
-        bg = self.time_gate_bias.detach().contiguous()
+        wg, bg, w_r, b_r = self._step_tensors()
         if self._phases_ok(g_list):
             return self._forward_phases(g_list, c_val, r_static, wg, bg, w_r, b_r)
         for i, g in enumerate(g_list):
@@ -397,6 +382,67 @@ class HyperbolicRecurrentRGCN(nn.Module):
             history_embs.append(self.h)
         return history_embs, None, self.h_0, [], []
 
+    def _initial_state(self, c_val, r_static):
+        """(h, x, r) of the initial entity state (hyperbolic_model.py:775-782): a function of
+        parameters only, computed once per parameter version (param_caches) and reused by every
+        predict (the kernels read it, none writes it), so a captured predict graph holds no init
+        launch."""
+        pe = self.dynamic_emb
+        V, d = pe.shape
+        key = (pe.data_ptr(), pe._version, self.radius_static.data_ptr(), self.radius_static._version,
+               float(c_val), bool(self.layer_norm), float(self.radius_min), float(self.radius_max))
+        hit = self.__dict__.get("_init_cache")
+        if hit is not None and hit[0] == key and self.param_caches:
+            return hit[1]
+        dyn = pe.detach().contiguous()
+        h = torch.empty_like(dyn)
+        x = torch.empty_like(dyn)
+        r = torch.empty(V, device=pe.device, dtype=torch.float32)
+        _lib.call("regcn_init_entities_f32", _lib.fptr(dyn, "dynamic_emb"), _lib.fptr(r_static), V, d, c_val,
+                  int(bool(self.layer_norm)), _lib.fptr(h), _lib.fptr(x), _lib.fptr(r), _lib.stream())
+        if not torch.cuda.is_current_stream_capturing():
+            self.__dict__["_init_cache"] = (key, (h, x, r))
+        return h, x, r
+
+    def _step_tensors(self):
+        """Timestep operands: packed time-gate weight, its bias, the radius MLP row and bias."""
+        trev = self.temporal_radius_evolution
+        w_r = trev.radius_mlp.weight.detach().reshape(-1).contiguous()
+        b_r = trev.radius_mlp.bias.detach().reshape(-1).contiguous()
+        return packed(self.time_gate_weight), self.time_gate_bias.detach().contiguous(), w_r, b_r
+
+    @contextlib.contextmanager
+    def shared_parameter_states(self, T):
+        """A batch of independent predicts (e.g. the test snapshots of one evaluation pass
+        without --multi-step, hyperbolic_main.py:100-149) over windows of T snapshots shares its
+        parameter-only states: the static radius, the initial entity state, timestep 0's GRU
+        pre-half and, with the phase launches, the states F^t(initial state) of rows without an
+        in-edge so far in the window (regcn_cold_chain_f32 over all rows: every predict inside
+        copies them instead of running those rows).  Computed once on entry, on the current
+        stream, and dropped on exit: nothing outlives the batch.  Same values bit for bit."""
+        with torch.no_grad():
+            c_val = self._c_float()
+            saved = self.__dict__.get("_scope")
+            self.__dict__["_scope"] = None
+            r_static = self._static_radius(c_val).contiguous()
+            init = self._initial_state(c_val, r_static)
+            pre0 = relation_gru_pre(self.relation_gru, self.emb_rel, self.emb_rel)
+            memo, keep = None, []
+            layers = list(self.rgcn.layers)
+            if (self.use_phases and self.dynamic_emb.device.type == "cuda" and len(layers) == 2
+                    and not self.run_analysis and not any(l.training for l in layers) and T <= _lib.MAX_WINDOW):
+                desc, keep = self._phase_desc(r_static, *self._step_tensors())
+                memo = self._pristine_states(T, c_val, desc, cache=False, x_init=init[1])
+                keep = keep + [self.__dict__.pop("_chain_operands")]
+            scope = dict(T=T, c=c_val, r_static=r_static, init=init, pre0=pre0, memo=memo, keep=keep)
+            self.__dict__["_scope"] = scope
+        try:
+            yield
+        finally:
+            self.__dict__["_scope"] = saved
+            if torch.cuda.is_current_stream_capturing():  # a captured graph reads them at replay
+                self.__dict__.setdefault("_capture_keep", []).append(scope)
+
     def _phases_ok(self, g_list):
         """The phase pipeline serves eval forwards of a 2-layer cell over plain snapshots
         (no dropout masks, no analysis hooks, no multi-GPU partition)."""
@@ -408,6 +454,9 @@ class HyperbolicRecurrentRGCN(nn.Module):
     def _gru_pre_initial(self):
         """Timestep 0's GRU pre-half: a function of parameters only (h_prev = emb_rel),
         computed once per parameter version."""
+        scope = self.__dict__.get("_scope")
+        if scope is not None:
+            return scope["pre0"]
         gru, emb = self.relation_gru, self.emb_rel
         key = tuple((t.data_ptr(), t._version) for t in (emb, gru.weight_ih, gru.weight_hh, gru.bias_ih, gru.bias_hh)
                     if t is not None)
@@ -419,21 +468,12 @@ class HyperbolicRecurrentRGCN(nn.Module):
             self.__dict__["_gru_pre0"] = (key, pre)
         return pre
 
-    def _forward_phases(self, g_list, c_val, r_static, wg, bg, w_r, b_r):
-        """The timestep loop with a 2-layer cell as three launches per snapshot on one
-        stream (regcn_timestep_phase_f32, csrc/timestep.hip):
-          A  relation GRU x-half; in-edge rows' self-loop and time-gate GEMMs (need only the
-             timestep input); rows without in-edges: layer 0;
-          B  in-edge tiles: layer-0 gather -> finish -> epilogue -> layer 1's self-loop
-             GEMM; other rows: layer 1; relation GRU pre-half of the next timestep;
-          C  in-edge tiles: layer-1 gather -> timestep; other rows: timestep.
-        Without the memo (split_zero_rows) the rows without in-edges leave A/B/C: one
-        regcn_zero_step_f32 launch on a side stream runs their layer 0, layer 1 and timestep,
-        forked after timestep t - 1 and joined after C.
-        Same values as the per-layer launches bit for bit (tests/test_gpu_parity.py)."""
+    def _phase_desc(self, r_static, wg, bg, w_r, b_r):
+        """regcn_phase_desc fields that depend on the parameters only (packed weights, the
+        timestep and relation-GRU operands); returns (desc, tensors it points into)."""
         from .weights import packed_linear, packed_linear_cols
         dev = self.dynamic_emb.device
-        V, d = self.dynamic_emb.shape
+        d = self.dynamic_emb.shape[1]
         R2 = self.emb_rel.shape[0]
         layers = list(self.rgcn.layers)
         lorentz = isinstance(layers[0], LorentzRGCNLayer)
@@ -441,11 +481,6 @@ class HyperbolicRecurrentRGCN(nn.Module):
         gru, emb = self.relation_gru, self.emb_rel.detach()
         b_ih, b_hh = _gru_biases(gru, d, dev)
         a = _lib.addr
-        f32 = torch.float32
-        s1, tw, x1, h2 = (torch.empty(V, d, device=dev, dtype=f32) for _ in range(4))
-        r1, n2 = torch.empty(V, device=dev, dtype=f32), torch.empty(V, device=dev, dtype=f32)
-        pre = self._gru_pre_initial()
-        keep = [s1, tw, x1, h2, r1, n2, b_ih, b_hh]  # tensors the launches read (profiling replays them)
         desc = _lib.PhaseDesc()
         desc.agg_mode = _lib.AGG_LORENTZ if lorentz else _lib.AGG_UNION
         desc.c, desc.d = float(layers[0].c), d  # the layers' own curvature, as their launches use
@@ -462,7 +497,6 @@ class HyperbolicRecurrentRGCN(nn.Module):
         if lorentz and layers[1].skip_connect:
             desc.w_skip1 = a(packed(layers[1].skip_weight))
             desc.b_skip1 = a(layers[1].skip_bias.detach())
-        desc.s1, desc.tw, desc.x1, desc.r1, desc.h2, desc.n2 = a(s1), a(tw), a(x1), a(r1), a(h2), a(n2)
         desc.step_w_g, desc.step_b_g, desc.step_r_static = a(wg), a(bg), a(r_static)
         desc.step_w_r, desc.step_b_r = a(w_r), a(b_r)
         desc.step_eps_r, desc.step_beta = float(trev.epsilon), float(trev.anchor_beta)
@@ -473,6 +507,34 @@ class HyperbolicRecurrentRGCN(nn.Module):
         desc.gru_w_ih_x = a(packed_linear_cols(gru.weight_ih, 3, d, 2 * d))
         desc.gru_w_hh = a(packed_linear(gru.weight_hh, 3))
         desc.gru_b_ih, desc.gru_b_hh = a(b_ih), a(b_hh)
+        return desc, [b_ih, b_hh]
+
+    def _forward_phases(self, g_list, c_val, r_static, wg, bg, w_r, b_r):
+        """The timestep loop with a 2-layer cell as three launches per snapshot on one
+        stream (regcn_timestep_phase_f32, csrc/timestep.hip):
+          A  relation GRU x-half; in-edge rows' self-loop and time-gate GEMMs (need only the
+             timestep input); rows without in-edges: layer 0;
+          B  in-edge tiles: layer-0 gather -> finish -> epilogue -> layer 1's self-loop
+             GEMM; other rows: layer 1; relation GRU pre-half of the next timestep;
+          C  in-edge tiles: layer-1 gather -> timestep; other rows: timestep.
+        Without the memo (split_zero_rows) the rows without in-edges leave A/B/C: one
+        regcn_zero_step_f32 launch on a side stream runs their layer 0, layer 1 and timestep,
+        forked after timestep t - 1 and joined after C.
+        Same values as the per-layer launches bit for bit (tests/test_gpu_parity.py)."""
+        dev = self.dynamic_emb.device
+        V, d = self.dynamic_emb.shape
+        R2 = self.emb_rel.shape[0]
+        a = _lib.addr
+        f32 = torch.float32
+        layers = list(self.rgcn.layers)
+        lorentz = isinstance(layers[0], LorentzRGCNLayer)
+        emb = self.emb_rel.detach()
+        s1, tw, x1, h2 = (torch.empty(V, d, device=dev, dtype=f32) for _ in range(4))
+        r1, n2 = torch.empty(V, device=dev, dtype=f32), torch.empty(V, device=dev, dtype=f32)
+        pre = self._gru_pre_initial()
+        desc, keep = self._phase_desc(r_static, wg, bg, w_r, b_r)
+        keep += [s1, tw, x1, h2, r1, n2]  # tensors the launches read (profiling replays them)
+        desc.s1, desc.tw, desc.x1, desc.r1, desc.h2, desc.n2 = a(s1), a(tw), a(x1), a(r1), a(h2), a(n2)
         lib_call = _lib.lib().regcn_timestep_phase_f32
 
         def call(dp, phase, stream):
@@ -504,7 +566,11 @@ class HyperbolicRecurrentRGCN(nn.Module):
         T = len(g_list)
         outs = [(torch.empty(V, d, device=dev, dtype=f32), torch.empty(V, d, device=dev, dtype=f32),
                  torch.empty(V, device=dev, dtype=f32)) for _ in g_list]
-        memo = self._pristine_states(T, c_val, desc) if self.memo_pristine and T <= _lib.MAX_WINDOW else None
+        scope = self.__dict__.get("_scope")
+        if scope is not None and scope["memo"] is not None and scope["T"] == T:
+            memo = scope["memo"]  # computed once for the batch (shared_parameter_states)
+        else:
+            memo = self._pristine_states(T, c_val, desc) if self.memo_pristine and T <= _lib.MAX_WINDOW else None
         if memo is not None:
             keep.append(memo)
         split = memo is None and self.split_zero_rows
@@ -600,7 +666,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
             history_embs.append(self.h)
         return history_embs, None, self.h_0, [], []
 
-    def _pristine_states(self, T, c_val, desc):
+    def _pristine_states(self, T, c_val, desc, cache=True, x_init=None):
         """[(h, x, r) after timestep k for k < T] of a row that receives no message in
         timesteps 0..k: F^(k+1)(initial state) with F = layer 0 and layer 1 without messages
         (W_evolve, the skip gate) and the timestep (time gate, radius evolution), all rows in
@@ -611,7 +677,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
                float(self.radius_max)) + tuple((p.data_ptr(), p._version) for p in self.parameters()) \
             + tuple((b.data_ptr(), b._version) for b in self.buffers())
         hit = self.__dict__.get("_pristine_cache")
-        if hit is not None and hit[0] == key and self.param_caches:
+        if cache and hit is not None and hit[0] == key and self.param_caches:
             return hit[1]
         V, d = pe.shape
         dev = pe.device
@@ -620,7 +686,8 @@ class HyperbolicRecurrentRGCN(nn.Module):
                    torch.empty(V, device=dev, dtype=f32)) for _ in range(T)]
         rows = torch.arange(V, device=dev, dtype=torch.int32)
         n_rows = torch.full((1,), V, device=dev, dtype=torch.int32)
-        x_init, _ = tangent_of(self.h, c_val)
+        if x_init is None:  # the initial state forward() just attached
+            x_init, _ = tangent_of(self.h, c_val)
         a = _lib.addr
         ch = _lib.ChainDesc()
         ch.rows, ch.n_rows = a(rows, torch.int32), a(n_rows, torch.int32)
@@ -631,7 +698,13 @@ class HyperbolicRecurrentRGCN(nn.Module):
             setattr(ch, "step_" + f, getattr(desc, "step_" + f))
         for t, (ho, xo, ro) in enumerate(states):
             ch.h_out[t], ch.x_out[t], ch.r_out[t] = a(ho), a(xo), a(ro)
+        if PHASE_CAPTURE is not None:  # profiling: a replayable launch (bench.py)
+            chs = type(ch).from_buffer_copy(ch)
+            PHASE_CAPTURE["chain"] = (lambda: _lib.call_desc("regcn_cold_chain_f32", chs), [chs, rows, n_rows, states])
         _lib.call_desc("regcn_cold_chain_f32", ch)
+        if not cache:  # the caller keeps the launch's operands alive (shared_parameter_states)
+            self.__dict__["_chain_operands"] = (rows, n_rows)
+            return states
         if not torch.cuda.is_current_stream_capturing():
             self.__dict__["_pristine_cache"] = (key, states)
         else:

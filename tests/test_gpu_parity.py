@@ -207,6 +207,41 @@ def test_phase_pipeline_bitwise(encoder, layers, skip, self_loop, ln):
             assert torch.equal(a, b), mode
 
 
+@pytest.mark.parametrize("encoder,ln", [("lgcn", False), ("hyperbolic_uvrgcn", True)])
+def test_shared_parameter_states_bitwise(encoder, ln):
+    """A batch of independent predicts inside HyperbolicRecurrentRGCN.shared_parameter_states
+    (parameter-only states computed once: initial state, GRU pre-half, pristine rows copied
+    from the batch's cold chain) returns exactly what each predict computes alone, every
+    parameter cache off; two batches in a row (nothing carried over), windows sharing
+    snapshots, an empty snapshot among them."""
+    from regcn_amd import graph as G
+    from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
+    from regcn_amd.synthetic import snapshot_series
+    V, R, d, T = 2500, 50, 200, 3
+    snaps = snapshot_series(5, V, R, 7, 250)
+    snaps[3] = np.zeros((0, 3), np.int64)
+    torch.manual_seed(1)
+    m = HyperbolicRecurrentRGCN("roth", encoder, V, R, 0, 0, d, "sub", T, num_bases=100, num_hidden_layers=2,
+                                dropout=0.2, c=C, self_loop=True, layer_norm=ln, entity_prediction=True,
+                                relation_prediction=True, use_cuda=True,
+                                radius_target=np.random.default_rng(1).uniform(0.5, 3, V).astype(np.float32),
+                                radius_msg_gamma=0.15).to(DEV).eval()
+    m.param_caches = m.memo_pristine = False
+    glists = [[G.build_sub_graph(V, R, s, True, DEV) for s in snaps[i:i + T]] for i in range(4)]
+    tests = [torch.from_numpy(snaps[i + T]).to(DEV) for i in range(4)]
+    with torch.no_grad():
+        alone = [[x.clone() for x in m.predict(gl, R, None, te, True)] for gl, te in zip(glists, tests)]
+        for _ in range(2):
+            with m.shared_parameter_states(T):
+                batch = [[x.clone() for x in m.predict(gl, R, None, te, True)] for gl, te in zip(glists, tests)]
+            torch.cuda.synchronize()
+            for a, b in zip(alone, batch):
+                for x, y in zip(a, b):
+                    assert torch.equal(x, y)
+    m.param_caches = HyperbolicRecurrentRGCN.param_caches
+    m.memo_pristine = HyperbolicRecurrentRGCN.memo_pristine
+
+
 @pytest.mark.parametrize("n_test,d", [(37, 200), (1, 200), (64, 256), (5, 12)])
 def test_fused_roth_decoders(n_test, d):
     """HyperbolicRecurrentRGCN.predict with the two-launch RotH/RotHRel front
