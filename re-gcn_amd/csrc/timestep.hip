@@ -145,29 +145,25 @@ __device__ __forceinline__ void skip_gate(Frag& v, const float* P, int lda, cons
 }
 
 // ------------------------------------------------------------------------------- phase A
-// In-edge rows (plain 16-row tiles over rows[:n_pos]): the two GEMMs that need only x0.
+// In-edge rows (plain 16-row tiles over rows[:n_pos]): the two GEMMs that need only x0, one
+// per workgroup (block 2 t: s1 = x0 @ W_loop[0]; block 2 t + 1: tw = clamp(x_prev) @ W_g), so
+// the phase's critical path is one GEMM deep.
 __device__ __forceinline__ void a_pos_rows(const PhaseArgs& p, int b, float* lds) {
   const int lda = tile_lda(p.d);
   float* X = lds;
-  float* P2 = lds + TM * lda;
-  int* trow = reinterpret_cast<int*>(lds + 2 * TM * lda);
-  const int start = b * TM;
+  int* trow = reinterpret_cast<int*>(lds + TM * lda);
+  const bool gate = (b & 1) || !p.L[0].w_loop;
+  const int start = (b >> 1) * TM;
   const int count = load_trow(trow, p.L[0].rows, start, min(TM, p.L[0].n_pos - start));
-  stage_rows<false>(X, lda, p.L[0].x, trow, p.d, count);
-  stage_rows<true>(P2, lda, p.step.x_prev, trow, p.d, count);
+  BRing br;
+  br.load(gate ? p.step.w_g : p.L[0].w_loop, p.d);
+  if (gate) stage_rows<true>(X, lda, p.step.x_prev, trow, p.d, count);
+  else stage_rows<false>(X, lda, p.L[0].x, trow, p.d, count);
   __syncthreads();
-  Frag acc[2];
-  acc[0].zero();
-  acc[1].zero();
-  if (p.L[0].w_loop) {
-    const float* Ts[2] = {X, P2};
-    const float* Ws[2] = {p.L[0].w_loop, p.step.w_g};
-    mfma_tiles<2, RING>(acc, Ts, Ws, lda, p.d);
-    frag_store(acc[0], p.s1, trow, count, p.d);
-  } else {
-    mfma_tile(acc[1], P2, lda, p.step.w_g, p.d);
-  }
-  frag_store(acc[1], p.tw, trow, count, p.d);
+  Frag acc;
+  acc.zero();
+  mfma_tile_pf(acc, X, lda, gate ? p.step.w_g : p.L[0].w_loop, p.d, br);
+  frag_store(acc, gate ? p.tw : p.s1, trow, count, p.d);
 }
 
 // ------------------------------------------------------------------ in-edge tiles, B and C
@@ -472,8 +468,11 @@ __global__ __launch_bounds__(NTHR) void k_phase_a(PhaseArgs p) {
   int b = blockIdx.x;
   // every block of A is on the timestep's critical path
   __builtin_amdgcn_s_setprio(2);
-  if (b < p.n_pos_rt) return a_pos_rows(p, b, lds);
-  b -= p.n_pos_rt;
+  if (b < 2 * p.n_pos_rt) {
+    if ((b & 1) == 0 && !p.L[0].w_loop) return;  // no self loop: the gate GEMM only
+    return a_pos_rows(p, b, lds);
+  }
+  b -= 2 * p.n_pos_rt;
   if (b < p.n_gru) return gru_x_block(p.gru, b % p.gru_rt, b / p.gru_rt, lds);
   b -= p.n_gru;
   if (b < p.n_zero_rt) return a_zero_rows(p, b, lds);
@@ -560,7 +559,7 @@ int timestep_phase(PhaseArgs a, int phase, hipStream_t st) {
     a.n_gru = a.gru.h_out ? gru_blocks : 0;
     if (a.n_gru && (!a.gru.h_prev || !a.gru.w_ih_x || !a.gru.pre || (!a.gru.x_mean && !a.gru.rel_start)))
       return set_error(REGCN_EINVAL, "GRU x-phase operands missing");
-    grid = (unsigned)(a.n_pos_rt + a.n_gru + n_zero_rt + a.n_copy);
+    grid = (unsigned)(2 * a.n_pos_rt + a.n_gru + n_zero_rt + a.n_copy);
     lds = std::max({2 * tile + TM * 4, tile + small, a.n_gru ? gru_x_lds_bytes(d) : 0});
     if (grid) hipLaunchKernelGGL(k_phase_a, dim3(grid), dim3(NTHR), lds, st, a);
     return grid ? check_launch("k_phase_a") : 0;
