@@ -23,6 +23,7 @@ sample, :560).  Out-of-scope features (static graph, EST, fhnn/hgat, Riemannian 
 as do the two whose gradients are not built (learned curvature, relation curvature).
 """
 import argparse
+import contextlib
 import logging
 import os
 import random
@@ -207,7 +208,9 @@ def test(model, history_list, test_list, num_rels, num_nodes, device, all_ans_li
     model.eval()
     input_list = [snap for snap in history_list[-args.test_history_len:]]
     graphs = {}
-    with torch.no_grad():
+    # the pass is one batch of predicts: parameter-only states once (bit-identical results)
+    share = getattr(model, "shared_parameter_states", None)
+    with torch.no_grad(), share(args.test_history_len) if share else contextlib.nullcontext():
         for time_idx, test_snap in enumerate(test_list):
             glist = []
             for s in input_list:  # snapshot graphs cached by identity across the window
