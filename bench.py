@@ -359,11 +359,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; BENCH_DIST_BACKEND=gloo rehearses several ranks on one card
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     from regcn_amd.synthetic import CONFIGS
     cfg = CONFIGS[args.config]
     d = args.d
@@ -474,7 +481,8 @@ def main():
     elapsed = time.perf_counter() - t0
     edges_local = sum(epw[k % len(samples)] for k in range(args.steps))
     if world > 1:
-        t = torch.tensor([elapsed, float(edges_local)], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed, float(edges_local)], dtype=torch.float64,
+                         device=device if backend == "nccl" else "cpu")
         tm = t.clone()
         dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)

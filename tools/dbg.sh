@@ -1,11 +1,5 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -q -x --timeout 120 --timeout-method thread -k "shared or phase or layers" > gpurun_out/pt.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pt.log; exit 1; }
-tail -1 gpurun_out/pt.log
-for v in "" "--concurrent 1"; do
-timeout -k 10 200 python bench.py $v --no-scale --no-cpu-baseline > gpurun_out/dbg.log 2>&1 || { echo "$v failed"; tail -20 gpurun_out/dbg.log; exit 1; }
-grep '^{' gpurun_out/dbg.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("'"$v"'", d["value"], d["ms_per_step"], d["latency_ms_per_predict"], d["roofline"]["kernel"], d["roofline"]["frac"], " ".join("%s=%.2f" % (k, v["avg_us"]) for k, v in d["kernels"].items()))'
-done
-timeout -k 10 120 python tools/phasetrace.py icews14s_lgcn_roth "" 1 > gpurun_out/trace.log 2>&1 || { echo "trace failed"; tail -20 gpurun_out/trace.log; exit 1; }
-grep -v amdgpu gpurun_out/trace.log | head -3
+BENCH_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 48 --warmup 4 > gpurun_out/b2.log 2>&1 || { echo "2-rank failed"; tail -30 gpurun_out/b2.log; exit 1; }
+grep '^{' gpurun_out/b2.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["n_gpus"], d["ms_per_step"], d["config"]["parallelism"])'
