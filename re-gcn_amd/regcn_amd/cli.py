@@ -35,6 +35,7 @@ import torch
 
 from . import ranking
 from .graph import build_sub_graph
+from .training import GraphedSteps
 
 logger = logging.getLogger("regcn_amd.cli")
 
@@ -90,6 +91,10 @@ def build_parser():
     a("--reuse-encoder", action=argparse.BooleanOptionalAction, default=True,
       help="one encoder forward per training snapshot for all its mini-batches (same gradients; "
            "--no-reuse-encoder recomputes it per mini-batch as hyperbolic_main.py does)")
+    a("--hip-graph", action="store_true",
+      help="replay each training sample's whole step (forward, backward, clip, Adam) from a HIP graph "
+           "captured after its first step (single process; same math, dropout masks from the graph-safe "
+           "generator)")
     a("--decoder", type=str, default="hyperbolic_convtranse", choices=["hyperbolic_convtranse", "murp", "roth", "atth"])
     a("--input-dropout", type=float, default=0.2)
     a("--hidden-dropout", type=float, default=0.2)
@@ -260,7 +265,10 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
     Returns {"best_mrr", "best_epoch", "epoch_loss": [mean loss per epoch]}."""
     import torch.distributed as dist
     from .parallel import allreduce_gradients
-    optimizer = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=1e-5)   # :469
+    world0 = dist.get_world_size() if dist.is_initialized() else 1
+    graphed = GraphedSteps(device) if args.hip_graph and world0 == 1 else None
+    optimizer = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=1e-5,   # :469
+                                 capturable=graphed is not None)
     # replicas (SURVEY.md §8(e)): every rank takes its share of the shuffled samples, one gradient
     # all-reduce per optimizer step; the same seed on every rank keeps the shuffles (and so the
     # lock-step schedule) identical.  Rank 0 validates and checkpoints.
@@ -270,13 +278,22 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
     all_ans_v = ranking.load_all_answers_for_time_filter(valid, num_rels, num_nodes, False)
     all_ans_r_v = ranking.load_all_answers_for_time_filter(valid, num_rels, num_nodes, True)
     graphs = GraphCache(num_nodes, num_rels, device)
+    tcache = {}
+
+    def triple_cache(n):  # device triples per training snapshot, kept (a captured step reads them)
+        if n not in tcache:
+            tcache[n] = torch.from_numpy(np.asarray(train_list[n], dtype=np.int64)).to(device)
+        return tcache[n]
+
     best_mrr, best_epoch, patience = 0.0, 0, 20
     epoch_loss = []
     t_start = time.time()
     for epoch in range(args.n_epochs):
         t0 = time.time()
         model.train()
-        losses, losses_e, losses_r, losses_rad = [], [], [], []
+        # per-sample losses accumulated on the device (the reference's four .item() per
+        # mini-batch, :600-603, would synchronise every step): one read per epoch
+        acc = torch.zeros(4, device=device, dtype=torch.float64)  # sum of e, r, rad; samples
         idx = list(range(len(train_list)))
         random.shuffle(idx)
         idx = [n for n in idx if n != 0 and len(train_list[n])]
@@ -287,45 +304,46 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
         for n in idx:
             inputs = train_list[max(0, n - args.train_history_len):n]
             glist = [graphs(s) for s in inputs]
-            triples = torch.from_numpy(np.asarray(train_list[n], dtype=np.int64)).to(device)
-            if triples.shape[0] == 0:
+            if not len(train_list[n]):
                 continue
-            optimizer.zero_grad()
-            se = sr = srad = 0.0
-            nb = 0
-            if args.reuse_encoder and hasattr(model, "get_loss_batches"):
-                # one encoder forward/backward per snapshot, the mini-batch losses summed
-                # (the mini-batch decoder losses are back-propagated one at a time inside)
-                parts = model.get_loss_batches(
-                    glist, triples, None, True, args.triple_batch_size, query_time=n,
-                    combine=lambda le, lr, ls, lrad: args.task_weight * le + (1 - args.task_weight) * lr
-                    + ls.sum() + lrad)
-            else:  # hyperbolic_main.py:585-598: the encoder recomputed per mini-batch
-                parts = []
-                for b in range(0, triples.shape[0], args.triple_batch_size):
-                    le, lr, ls, lrad = model.get_loss(glist, triples[b:b + args.triple_batch_size], None, True,
-                                                      query_time=n)
-                    loss = args.task_weight * le + (1 - args.task_weight) * lr + ls.sum() + lrad
-                    loss.backward()
-                    parts.append((le, lr, ls, lrad))
-            for le, lr, ls, lrad in parts:
-                se += float(le.detach())
-                sr += float(lr.detach())
-                srad += float(lrad.detach())
-                nb += 1
-            losses_e.append(se / nb)
-            losses_r.append(sr / nb)
-            losses_rad.append(srad / nb)
-            losses.append(args.task_weight * losses_e[-1] + (1 - args.task_weight) * losses_r[-1] + losses_rad[-1])
-            allreduce_gradients(model.parameters())
-            torch.nn.utils.clip_grad_norm_(model.parameters(), args.grad_norm)              # :627-628
-            optimizer.step()
-        epoch_loss.append(float(np.mean(losses)) if losses else float("nan"))
+            triples = triple_cache(n)
+
+            def step():
+                optimizer.zero_grad()
+                if args.reuse_encoder and hasattr(model, "get_loss_batches"):
+                    # one encoder forward/backward per snapshot, the mini-batch losses summed
+                    # (the mini-batch decoder losses are back-propagated one at a time inside)
+                    parts = model.get_loss_batches(
+                        glist, triples, None, True, args.triple_batch_size, query_time=n,
+                        combine=lambda le, lr, ls, lrad: args.task_weight * le + (1 - args.task_weight) * lr
+                        + ls.sum() + lrad)
+                else:  # hyperbolic_main.py:585-598: the encoder recomputed per mini-batch
+                    parts = []
+                    for b in range(0, triples.shape[0], args.triple_batch_size):
+                        le, lr, ls, lrad = model.get_loss(glist, triples[b:b + args.triple_batch_size], None, True,
+                                                          query_time=n)
+                        loss = args.task_weight * le + (1 - args.task_weight) * lr + ls.sum() + lrad
+                        loss.backward()
+                        parts.append((le, lr, ls, lrad))
+                allreduce_gradients(model.parameters())
+                torch.nn.utils.clip_grad_norm_(model.parameters(), args.grad_norm)          # :627-628
+                optimizer.step()
+                # the sample's mean mini-batch losses (entity, relation, radius)
+                return torch.stack([torch.stack([p[k].detach().double() for p in parts]).mean() for k in (0, 1, 3)])
+
+            means = graphed.run(n, step) if graphed is not None else step()
+            acc[:3] += means
+            acc[3] += 1
+        tot = acc.cpu().numpy()
+        if tot[3] > 0:
+            me, mr, mrad = tot[:3] / tot[3]
+            epoch_loss.append(float(args.task_weight * me + (1 - args.task_weight) * mr + mrad))
+        else:
+            me = mr = mrad = float("nan")
+            epoch_loss.append(float("nan"))
         if epoch % args.log_interval == 0:
             logger.info("Epoch %04d | Loss: %.4f | E/R/S/Rad: %.4f/%.4f/%.4f/%.4f | Best MRR: %.4f | Time: %.1fs",
-                        epoch, np.mean(losses) if losses else float("nan"), np.mean(losses_e) if losses_e else 0.0,
-                        np.mean(losses_r) if losses_r else 0.0, 0.0, np.mean(losses_rad) if losses_rad else 0.0,
-                        best_mrr, time.time() - t0)
+                        epoch, epoch_loss[-1], me, mr, 0.0, mrad, best_mrr, time.time() - t0)
         if epoch and epoch % args.evaluate_every == 0:                                      # :660-681
             stop = torch.zeros(1, device=device)
             if rank == 0:

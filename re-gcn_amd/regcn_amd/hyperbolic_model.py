@@ -847,10 +847,13 @@ class HyperbolicRecurrentRGCN(nn.Module):
             else:
                 score_rel = self.rdecoder.forward(pre_emb, r_emb, all_triples, mode="train").view(-1, 2 * self.num_rels)
                 loss_rel = self.loss_r(score_rel, all_triples[:, 1])
-        entity_ids = torch.unique(all_triples[:, [0, 2]].reshape(-1))
-        radius_static = self._static_radius(float(c_val)).index_select(0, entity_ids)
-        radius_target = self.radius_target.to(dev).index_select(0, entity_ids)
-        loss_radius = self.radius_lambda * F.mse_loss(radius_static, radius_target)
+        # MSE over the batch's distinct entities (hyperbolic_model.py:1067-1073 takes
+        # torch.unique of them): a membership mask over all entities instead, so the loss has
+        # a static shape and no host synchronisation (unique's output size is data-dependent)
+        seen = torch.zeros(self.num_ents, device=dev, dtype=torch.float32)
+        seen.index_fill_(0, all_triples[:, 0::2].reshape(-1), 1.0)  # s and o (a view)
+        diff = self._static_radius(float(c_val)) - self.radius_target.to(dev)
+        loss_radius = self.radius_lambda * (seen * diff * diff).sum() / seen.sum()
         return loss_ent, loss_rel, loss_static, loss_radius
 
     def get_training_summary(self):

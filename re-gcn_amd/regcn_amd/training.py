@@ -165,3 +165,44 @@ def euclid_model_forward(model, g_list):
         h = tw * cur + (1 - tw) * h
         history.append(h)
     return history, None, h0, [], []
+
+
+class GraphedSteps:
+    """Whole training steps replayed from HIP graphs: one graph per key
+    (a training sample: its snapshot shapes fix every launch), captured right after the
+    key's first step, which runs eagerly.  The step is launch-bound at ICEWS size (~1,000
+    launches of 2-30 us), so a replay removes the host's launch cost; it needs a step free of
+    host synchronisation (the radius loss's distinct-entity mask, curvature floats cached per
+    version) and an optimizer whose step counter lives on the device (Adam capturable=True).
+
+    All graphs share one memory pool: each is self-contained (it reads the parameters, the
+    sample's snapshot graphs and triples, which the caller keeps alive for the key, and
+    writes parameters, optimizer state and its returned tensor), so replays may come in any
+    order; the returned tensor is valid until the next `run`.  Dropout draws from the
+    graph-safe generator (a different mask per replay, as in eager steps)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.stream = torch.cuda.Stream(device)
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs = {}
+
+    def run(self, key, step):
+        """`step()` -> device tensor: one full step (zero_grad, forward, backward, clip,
+        optimizer step).  Runs it eagerly the first time `key` is seen and captures it for the
+        later calls, which replay.  Ordered after the calling stream's prior work."""
+        cur = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            g = self.graphs.get(key)
+            if g is not None:
+                g[0].replay()
+                out = g[1]
+            else:
+                out = step()  # eager: lazily built caches (transposed edge lists, ...) exist after it
+                gph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gph, pool=self.pool, stream=self.stream):
+                    static = step()
+                self.graphs[key] = (gph, static)
+        cur.wait_stream(self.stream)
+        return out

@@ -118,3 +118,50 @@ def test_cli_training_replicas(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     assert os.path.exists(ck)
     assert "MRR raw" in r.stdout + r.stderr
+
+
+def test_cli_training_hip_graph_matches_eager(tmp_path):
+    """--hip-graph (each sample's whole step captured after its first run and replayed:
+    training.GraphedSteps) trains the same model as the eager loop: dropout off, the same
+    seeds and sample order; epoch losses agree to 1e-4 and every parameter tensor to 2e-3 in
+    relative norm (epochs 1-2 are replays)."""
+    import random
+    from regcn_amd import cli, ranking
+    common = ["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0", "--encoder", "lgcn", "--decoder", "roth",
+              "--n-hidden", "64", "--n-bases", "32", "--synthetic-snapshots", "10", "--train-history-len", "3",
+              "--test-history-len", "3", "--relation-prediction", "--entity-prediction",
+              "--checkpoint", str(tmp_path / "m.pth"), "--seed", "0", "--lr", "0.01", "--triple-batch-size", "64",
+              "--dropout", "0", "--input-dropout", "0", "--hidden-dropout", "0", "--feat-dropout", "0",
+              "--n-epochs", "3", "--evaluate-every", "100"]
+    dev = torch.device("cuda", 0)
+    runs = []
+    adam = torch.optim.Adam
+
+    class CapturableAdam(adam):  # both runs step the same optimizer code (device step counter)
+        def __init__(self, *a, **k):
+            k["capturable"] = True
+            super().__init__(*a, **k)
+
+    torch.optim.Adam = CapturableAdam
+    try:
+        for extra in ([], ["--hip-graph"]):
+            args = cli.build_parser().parse_args(common + extra)
+            V, R, train, valid, test = cli.load_dataset(args)
+            tl = ranking.split_by_time(train)
+            torch.manual_seed(0)
+            model = cli.build_model(args, V, R, tl, dev)
+            random.seed(0)
+            out = cli.train_model(args, model, tl, valid, V, R, dev, str(tmp_path / "m.pth"))
+            torch.cuda.synchronize()
+            runs.append((out["epoch_loss"], {k: v.detach().clone() for k, v in model.state_dict().items()}))
+    finally:
+        torch.optim.Adam = adam
+    (l0, s0), (l1, s1) = runs
+    np.testing.assert_allclose(l1, l0, rtol=1e-4)
+    # the parameters in norm: the embedding gradients accumulate with atomics (index_add), so
+    # two eager runs differ in the last bits too, and Adam's first steps (update ~ lr * sign g)
+    # turn last-bit differences of near-zero gradients into +-lr on those few elements
+    for k in s0:
+        a, b = s0[k].float(), s1[k].float()
+        rel = float((a - b).norm() / a.norm().clamp_min(1e-6))
+        assert rel < 2e-3, (k, rel)

@@ -1,5 +1,9 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-BENCH_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 48 --warmup 4 > gpurun_out/b2.log 2>&1 || { echo "2-rank failed"; tail -30 gpurun_out/b2.log; exit 1; }
-grep '^{' gpurun_out/b2.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["n_gpus"], d["ms_per_step"], d["config"]["parallelism"])'
+timeout -k 10 400 python -u -m pytest tests/test_gpu_cli.py -q -x -k hip_graph --timeout 200 --timeout-method thread > gpurun_out/pt.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pt.log; exit 1; }
+tail -1 gpurun_out/pt.log
+for v in "" "--graph"; do
+timeout -k 10 300 python tools/trainbench.py --no-cpu $v > gpurun_out/tb.log 2>&1 || { echo "failed $v"; tail -30 gpurun_out/tb.log; exit 1; }
+grep '^{' gpurun_out/tb.log
+done

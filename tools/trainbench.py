@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture each sample's whole step (forward, backward, clip, Adam) in a HIP graph once "
+                         "and replay it (Adam capturable; the step has no host synchronisation)")
     ap.add_argument("--per-batch-encoder", action="store_true",
                     help="recompute the encoder per mini-batch (the reference loop) instead of once per sample")
     a = ap.parse_args()
@@ -49,7 +52,7 @@ def main():
                                 dropout=0.2, c=0.01, self_loop=True, layer_norm=False, input_dropout=0.2,
                                 hidden_dropout=0.2, feat_dropout=0.2, entity_prediction=True, relation_prediction=True,
                                 use_cuda=True, gpu=0, radius_target=rt, radius_msg_gamma=0.15).to(dev).train()
-    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5, capturable=a.graph)
     snaps = snapshot_series(1, V, R, T + 8, per)
     graphs = [G.build_sub_graph(V, R, s, True, dev) for s in snaps]
     samples = [(graphs[i:i + T], torch.from_numpy(snaps[i + T]).to(dev)) for i in range(8)]
@@ -72,19 +75,40 @@ def main():
         opt.step()
         return nb
 
-    for k in range(a.warmup):
-        step(k)
+    cap = torch.cuda.Stream(dev) if a.graph else torch.cuda.current_stream(dev)
+    cap.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(cap):  # with --graph every step runs on the capture stream
+        for k in range(max(a.warmup, len(samples) if a.graph else 0)):
+            step(k)
     torch.cuda.synchronize()
+    graphs = []
+    if a.graph:  # one graph per sample (its snapshot shapes), captured after an eager warmup
+        with torch.cuda.stream(cap):
+            for k in range(len(samples)):
+                opt.zero_grad(set_to_none=True)
+                gph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gph, stream=cap):
+                    step(k)
+                graphs.append(gph)
+        torch.cuda.synchronize()
+        for gph in graphs:
+            gph.replay()
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     edges = 0
     for k in range(a.steps):
-        nb = step(k)
+        if graphs:
+            graphs[k % len(samples)].replay()
+            nb = 1 if not a.per_batch_encoder else (samples[k % len(samples)][1].shape[0] + a.batch - 1) // a.batch
+        else:
+            nb = step(k)
         edges += edges_fwd[k % len(samples)] * nb
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     out = {"workload": "ICEWS14s-shaped training sample, encoder=%s, decoder=roth, d=%d, history 3, "
-                       "mini-batch %d (reference defaults, dropout 0.2), encoder %s" % (
-                           a.encoder, a.d, a.batch, "per mini-batch" if a.per_batch_encoder else "once per sample"),
+                       "mini-batch %d (reference defaults, dropout 0.2), encoder %s%s" % (
+                           a.encoder, a.d, a.batch, "per mini-batch" if a.per_batch_encoder else "once per sample",
+                           ", HIP graph per sample" if a.graph else ""),
            "ms_per_sample": round(dt / a.steps * 1e3, 3), "samples_per_s": round(a.steps / dt, 2),
            "fwd_M_edges_per_s": round(edges / dt / 1e6, 3), "triples_per_sample": per}
     if not a.no_cpu:
