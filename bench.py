@@ -140,6 +140,36 @@ def event_time(fn, reps, stream, replays=5):
     return s.elapsed_time(e) / (reps * replays)
 
 
+def sequence_times(fns, reps, stream, replays=3):
+    """Average device time of each launch in ms when the launches run in their pipeline order
+    (each one after its real predecessor, so caches hold what the pipeline leaves them): the
+    prefix fns[0..i] captured `reps` times into a HIP graph on `stream`, replayed between HIP
+    events on that stream, and launch i timed as the prefix-to-prefix difference.  (Events
+    recorded inside a captured graph cannot be timed on this runtime.)"""
+    totals = [0.0]
+    with torch.cuda.stream(stream):
+        for fn in fns:
+            fn()
+        torch.cuda.synchronize()
+        for i in range(1, len(fns) + 1):
+            gph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gph, stream=stream):
+                for _ in range(reps):
+                    for fn in fns[:i]:
+                        fn()
+            gph.replay()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            for _ in range(replays):
+                gph.replay()
+            e.record(stream)
+            e.synchronize()
+            totals.append(s.elapsed_time(e) / (reps * replays))
+            del gph
+    torch.cuda.synchronize()
+    return [max(totals[i + 1] - totals[i], 1e-6) for i in range(len(fns))]
+
+
 def pmc_traffic(kernel, config, d):
     """HBM bytes per launch of `kernel` from the committed PMC summary of this same bench
     command (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate
@@ -172,11 +202,11 @@ def _work(flops, nbytes, ms):
 
 
 def kernel_profile(model, sample, d, device, share=False, pool=1):
-    """Live HIP-event timing of each launch of the hot path on the bench workload: the three
-    timestep phase launches (csrc/timestep.hip) of the sample's last history snapshot, and
-    the two decoders on its queries.  Each stage is captured `reps` times into a HIP graph on
-    its own stream and replayed between HIP events on that stream.  Returns {kernel:
-    dict(ms, per_step, flops, bytes, ...)}."""
+    """Live HIP-event timing of each launch of the hot path on the bench workload: the batch's
+    cold chain, the timestep phase launches (csrc/timestep.hip) of the sample's last history
+    snapshot and the two decoders on its queries, in pipeline order (sequence_times: one
+    HIP graph on a stream of its own, a HIP event between consecutive launches).  Returns
+    {kernel: dict(ms, per_step, flops, bytes, ...)}."""
     from regcn_amd import hyperbolic_model as HM
     from regcn_amd.hyperbolic_decoder import (_chunked_hyperbolic_dist_score, roth_pair_fusable, roth_pair_queries,
                                               roth_pair_scores)
@@ -234,8 +264,8 @@ def kernel_profile(model, sample, d, device, share=False, pool=1):
                  gather_b + row_b * ((4 + skip) * n_pos + 4 * n_zero)),
             ]
             if "chain" in cap:  # the batch's pristine states: all rows x T timesteps, once per pool pass
-                stages.append(("k_cold_chain", cap["chain"][0], (2 + skip) * gemm * V * T,
-                               row_b * V * (1 + 2 * T)))
+                stages.insert(0, ("k_cold_chain", cap["chain"][0], (2 + skip) * gemm * V * T,
+                                  row_b * V * (1 + 2 * T)))
             if "Z" in cap:  # rows without in-edges: W_evolve[0], W_evolve[1] (+ skip), W_g; x0 in, h, x out
                 stages.append(("k_zero_step", cap["Z"][0], (2 + skip) * gemm * n_zs, row_b * 3 * n_zs))
         at = torch.cat([test, torch.stack([test[:, 2], test[:, 1] + model.num_rels, test[:, 0]], 1)])
@@ -263,8 +293,8 @@ def kernel_profile(model, sample, d, device, share=False, pool=1):
         if dec is not None and type(rdec).__name__ == "HyperbolicRotHRel":
             stages.append(("k_query<1> + k_score (relations)", lambda: rdec.forward(emb, h0, at),
                            2.0 * B * 2 * d * d + 2.0 * B * R2 * d, 4.0 * (B * d * 3 + B * R2)))
-        for name, fn, flops, nbytes in stages:
-            ms = event_time(fn, 100, st)
+        seq = sequence_times([fn for _, fn, _, _ in stages], 30, st)
+        for (name, fn, flops, nbytes), ms in zip(stages, seq):
             per_step = T if name.startswith(("k_phase", "k_zero")) else 1.0 / pool if name == "k_cold_chain" else 1
             res[name] = dict(ms=ms, per_step=per_step, flops=flops, bytes=nbytes, **_work(flops, nbytes, ms))
     torch.cuda.synchronize()

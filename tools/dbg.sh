@@ -1,5 +1,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tprof -o run -- python tools/trainbench.py --no-cpu --graph --steps 40 > gpurun_out/tprof.log 2>&1 || { echo "failed"; tail -20 gpurun_out/tprof.log; exit 1; }
-grep '^{' gpurun_out/tprof.log
+for v in "" "--concurrent 1" "--no-batch-share"; do
+timeout -k 10 200 python bench.py $v --no-scale --no-cpu-baseline > gpurun_out/dbg.log 2>&1 || { echo "$v failed"; tail -20 gpurun_out/dbg.log; exit 1; }
+grep '^{' gpurun_out/dbg.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("'"$v"'", d["value"], d["ms_per_step"], d["latency_ms_per_predict"], d["roofline"]["kernel"], d["roofline"]["frac"], " ".join("%s=%.2f" % (k, v["avg_us"]) for k, v in d["kernels"].items()))'
+done
