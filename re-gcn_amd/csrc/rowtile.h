@@ -342,7 +342,7 @@ __device__ __forceinline__ void frag_load(Frag& a, const float* __restrict__ M, 
     for (int j = 0; j < TPW; ++j) {
       const int col = frag_col(j);
       const float v = M[base + min(col, d - 1)];
-      a.t[j][r] = (ok && col < d) ? v : 0.f;
+      a.t[j][r] = (ok & (col < d)) ? v : 0.f;  // no short circuit: it would branch around the load (vmcnt(0) each)
     }
   }
 }

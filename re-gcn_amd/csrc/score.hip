@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
         T* dq = Qs2[buf] + i * SLD + kq + 16 * f;
         T* de = Es2[buf] + i * SLD + kq + 16 * f;
         const bool k_ok = k0 + kq + 16 * f < p.d;
-        const f4 va = (q_ok && k_ok) ? vq[sl][f] : z4, vb = (e_ok && k_ok) ? ve[sl][f] : z4;
+        const f4 va = (q_ok & k_ok) ? vq[sl][f] : z4, vb = (e_ok & k_ok) ? ve[sl][f] : z4;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const T a = (T)va[u], b = (T)vb[u];
@@ -489,7 +489,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
 #pragma unroll
   for (int b = 0; b < KB_MAX; ++b) {
     const f4 v = *reinterpret_cast<const f4*>(qrow + min(16 * b + g4, d - 4));
-    a[b] = (q_ok && b < KB && 16 * b + g4 < d) ? v : z4;
+    a[b] = (q_ok & (b < KB) & (16 * b + g4 < d)) ? v : z4;
     xs += dot4(a[b], a[b]);
   }
   // |q|^2 of query (lane & 15): sum the 4 k-quarters; the C rows of this lane
@@ -522,7 +522,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int u = sub + 8 * it;
-      const f4 w = (row_ok && 4 * u < d) ? v[it] : z4;
+      const f4 w = (row_ok & (4 * u < d)) ? v[it] : z4;
       ss += dot4(w, w);
       if (u < per_row) *reinterpret_cast<f4*>(lrow + 4 * u) = w;
     }
