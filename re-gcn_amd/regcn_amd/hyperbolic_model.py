@@ -420,10 +420,25 @@ class HyperbolicRecurrentRGCN(nn.Module):
         in-edge so far in the window (regcn_cold_chain_f32 over all rows: every predict inside
         copies them instead of running those rows).  Computed once on entry, on the current
         stream, and dropped on exit: nothing outlives the batch.  Same values bit for bit."""
+        saved = self.__dict__.get("_scope")
+        try:
+            scope = self._shared_states(T)
+        except BaseException:
+            self.__dict__["_scope"] = saved
+            raise
+        self.__dict__["_scope"] = scope
+        try:
+            yield
+        finally:
+            self.__dict__["_scope"] = saved
+            if torch.cuda.is_current_stream_capturing():  # a captured graph reads them at replay
+                self.__dict__.setdefault("_capture_keep", []).append(scope)
+
+    def _shared_states(self, T):
+        """The dict shared_parameter_states installs (computed with no scope active)."""
+        self.__dict__["_scope"] = None
         with torch.no_grad():
             c_val = self._c_float()
-            saved = self.__dict__.get("_scope")
-            self.__dict__["_scope"] = None
             r_static = self._static_radius(c_val).contiguous()
             init = self._initial_state(c_val, r_static)
             pre0 = relation_gru_pre(self.relation_gru, self.emb_rel, self.emb_rel)
@@ -434,14 +449,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 desc, keep = self._phase_desc(r_static, *self._step_tensors())
                 memo = self._pristine_states(T, c_val, desc, cache=False, x_init=init[1])
                 keep = keep + [self.__dict__.pop("_chain_operands")]
-            scope = dict(T=T, c=c_val, r_static=r_static, init=init, pre0=pre0, memo=memo, keep=keep)
-            self.__dict__["_scope"] = scope
-        try:
-            yield
-        finally:
-            self.__dict__["_scope"] = saved
-            if torch.cuda.is_current_stream_capturing():  # a captured graph reads them at replay
-                self.__dict__.setdefault("_capture_keep", []).append(scope)
+            return dict(T=T, c=c_val, r_static=r_static, init=init, pre0=pre0, memo=memo, keep=keep)
 
     def _phases_ok(self, g_list):
         """The phase pipeline serves eval forwards of a 2-layer cell over plain snapshots

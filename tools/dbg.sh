@@ -1,7 +1,9 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-for v in "--pool 16" "" "--pool 16" ""; do
-timeout -k 10 200 python bench.py $v --no-scale --no-cpu-baseline > gpurun_out/dbg.log 2>&1 || { echo "$v failed"; tail -20 gpurun_out/dbg.log; exit 1; }
-grep '^{' gpurun_out/dbg.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print("'"$v"'", d["value"], d["ms_per_step"], d["latency_ms_per_predict"])'
+timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py tests/test_gpu_autograd.py tests/test_gpu_cli.py tests/test_gpu_parity.py -q -x --timeout 200 --timeout-method thread > gpurun_out/pt.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pt.log; exit 1; }
+tail -1 gpurun_out/pt.log
+for v in "--graph" ""; do
+timeout -k 10 300 python tools/trainbench.py --no-cpu $v > gpurun_out/tb.log 2>&1 || { echo "failed $v"; tail -30 gpurun_out/tb.log; exit 1; }
+grep '^{' gpurun_out/tb.log
 done
