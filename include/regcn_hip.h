@@ -126,6 +126,21 @@ int regcn_partial_sum_f32(float* partial, int32_t partial_stride, const int32_t*
  * regcn_layer_tail_f32 and regcn_timestep_f32 is such a packed matrix. */
 size_t regcn_packed_weight_floats(int32_t d_in);
 int regcn_pack_weight_f32(const float* w, int32_t d_in, int32_t d_out, float* packed, void* stream);
+/* Small-output products of the training path: out (M x N, row-major) = sum_k A(k, m) B(k, n)
+ * (+ c0[m * c0_ld + n]; c0 nullable, c0_ld = 0 broadcasts a bias row), fp32 on MFMA, K split
+ * over workgroups and the partials summed in a fixed order (deterministic).
+ * a_kmajor = 1: A is K x M row-major (x of the weight gradient x^T dy); 0: A is M x K
+ * row-major (coef of the CE backward's dq = coef E).  b_kmajor = 1: B is K x N row-major;
+ * 0: N x K (an nn.Linear weight in x W^T).  Replaces the
+ * library GEMMs torch autograd runs for the weight gradients of torch.mm(x, W)
+ * (hyperbolic_layers.py:273-280 self/evolve loop, :290 neighbour weight, :315-318 skip gate;
+ * hyperbolic_model.py:852-858 time gate), the decoders' nn.Linear products on a mini-batch of
+ * queries (forward and both gradients; hyperbolic_decoder.py RotH/RefH/AttH projections) and
+ * the dq/de GEMMs of the CE backward.
+ * workspace: regcn_kreduce_workspace_floats(K, M, N) floats (0: none needed). */
+size_t regcn_kreduce_workspace_floats(int64_t K, int32_t M, int32_t N);
+int regcn_kreduce_gemm_f32(const float* a, int32_t a_kmajor, const float* b, int32_t b_kmajor, int64_t K, int32_t M,
+                           int32_t N, const float* c0, int64_t c0_ld, float* out, float* workspace, void* stream);
 /* rows: permutation of 0..V-1 with the n_pos in-degree>0 rows first.
  * hyperbolic (euclid=0): v = clamp(agg @ w_n | agg, +-10) + x @ (w_loop | w_evolve)
  *   [skip: g = sigmoid(prev_t @ w_skip + b_skip); v = g v + (1-g) prev_t]

@@ -116,6 +116,13 @@ int regcn_pack_weight_f32(const float* w, int32_t d_in, int32_t d_out, float* pa
   return pack_weight(w, d_in, d_out, packed, ST(s));
 }
 
+size_t regcn_kreduce_workspace_floats(int64_t K, int32_t M, int32_t N) { return kreduce_workspace_floats(K, M, N); }
+
+int regcn_kreduce_gemm_f32(const float* a, int32_t a_kmajor, const float* b, int32_t b_kmajor, int64_t K, int32_t M,
+                           int32_t N, const float* c0, int64_t c0_ld, float* out, float* workspace, void* s) {
+  return kreduce_gemm(a, a_kmajor, b, b_kmajor, K, M, N, c0, c0_ld, out, workspace, ST(s));
+}
+
 int regcn_layer_tail_f32(const float* agg, const float* w_n, const float* x, const float* w_loop,
                          const float* w_evolve, const float* prev_t, const float* w_skip, const float* b_skip,
                          const float* drop_mask, const int32_t* rows, int32_t n_pos, int32_t V, int32_t d,

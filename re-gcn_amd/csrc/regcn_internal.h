@@ -274,6 +274,9 @@ int rel_gru(const RelGruArgs& a, hipStream_t st);
 
 size_t packed_weight_floats(int d_in);
 int pack_weight(const float* W, int d_in, int d_out, float* Wp, hipStream_t st);
+size_t kreduce_workspace_floats(int64_t K, int M, int N);
+int kreduce_gemm(const float* A, int a_kmajor, const float* B, int b_kmajor, int64_t K, int M, int N, const float* C0,
+                 int64_t c0_ld, float* out, float* ws, hipStream_t st);
 int layer(const LayerArgs& a, hipStream_t st);
 int timestep(const StepArgs& a, hipStream_t st);
 int score(ScoreArgs& a, int mode, float* loss, hipStream_t st);

@@ -43,6 +43,8 @@ _SIGS = {
     "regcn_lorentz_aggregate_f32": [P, P, P, P, P, P, _c_int, P, _c_int, _c_int, _c_f, _c_int, P, _c_int, P, P],
     "regcn_packed_weight_floats": [_c_int],
     "regcn_pack_weight_f32": [P, _c_int, _c_int, P, P],
+    "regcn_kreduce_workspace_floats": [_c_i64, _c_int, _c_int],
+    "regcn_kreduce_gemm_f32": [P, _c_int, P, _c_int, _c_i64, _c_int, _c_int, P, _c_i64, P, P, P],
     "regcn_layer_tail_f32": [P, P, P, P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_int, _c_f, P, P, P, P],
     "regcn_timestep_f32": [P, P, P, P, P, P, P, _c_f, _c_f, _c_int, _c_int, _c_int, _c_int, _c_f, _c_f, P, P, P, P],
     "regcn_hyp_score_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P],
@@ -85,7 +87,7 @@ _SIGS = {
 
 SCORE_DIST, SCORE_RAW_SCALE = 1, 2
 _RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz,
-            "regcn_snapshot_workspace_bytes": _c_sz, "regcn_snapshot_capacity": _c_i64,
+            "regcn_snapshot_workspace_bytes": _c_sz, "regcn_kreduce_workspace_floats": _c_sz, "regcn_snapshot_capacity": _c_i64,
             "regcn_transpose_workspace_bytes": _c_sz, "regcn_row_type_order_workspace_bytes": _c_sz,
             "regcn_packed_weight_floats": _c_sz, "regcn_packed_linear_floats": _c_sz,
             "regcn_packed_k4_floats": _c_sz}

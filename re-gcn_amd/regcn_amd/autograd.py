@@ -11,7 +11,8 @@ with the gradients torch autograd would compute through the reference's op seque
   * the Lorentz layer's message sums (hyperbolic_layers.py:589-611) -> regcn_lorentz_sum_raw_f32
     / regcn_lorentz_aggregate_bwd_f32 (the centroid, to_poincare, log0 follow as row ops);
   * the all-entity cross entropy (_chunked_hyperbolic_ce_loss, hyperbolic_decoder.py:182-307)
-    -> regcn_hyp_ce_lse_f32 / regcn_hyp_ce_bwd_f32 (+ two library GEMMs for dq, de).
+    -> regcn_hyp_ce_lse_f32 / regcn_hyp_ce_bwd_f32 (+ dq, de on regcn_kreduce_gemm_f32);
+  * the weight gradients of the (V x d) @ (d x d) products -> regcn_kreduce_gemm_f32.
 
 The curvature is a constant here (a learned curvature's gradient is not built).
 """
@@ -290,8 +291,8 @@ class _HypCE(torch.autograd.Function):
                   _lib.iptr(tgt), f(lse), f(gl), B, N, d, ctx.c, 0, f(coef), f(rsum), f(csum), _lib.stream())
         rs = rsum.sum(1, keepdim=True)
         cs = csum.sum(0)
-        dq = torch.addmm(2.0 * rs * q, coef, cand)            # coef E + 2 q sum_n G dS/d|q|^2
-        de = torch.addmm(2.0 * cs[:, :1] * cand, coef.t(), q)  # coef^T Q + 2 e sum_b G dS/d|e|^2
+        dq = kreduce_mm(coef, cand, False, 2.0 * rs * q)            # coef E + 2 q sum_n G dS/d|q|^2
+        de = kreduce_mm(coef, q, True, 2.0 * cs[:, :1] * cand)      # coef^T Q + 2 e sum_b G dS/d|e|^2
         dbias = cs[:, 1].clone() if ctx.has_bias else None
         dscale = cs[:, 2].sum().reshape(ctx.scale_shape)
         dmargin = (sc.reshape(()) * cs[:, 1].sum()).reshape(ctx.margin_shape)
@@ -303,3 +304,88 @@ def hyp_ce_loss(q, cand, target, c, bias=None, scale=None, margin=None):
     scale = scale if torch.is_tensor(scale) else q.new_tensor(1.0 if scale is None else float(scale))
     margin = margin if torch.is_tensor(margin) else q.new_tensor(0.0 if margin is None else float(margin))
     return _HypCE.apply(q, cand, bias, scale, margin, target, _cf(c)).mean()
+
+
+# ------------------------------------------------------------------ long-K products
+def kreduce_mm(a, b, a_kmajor, c0=None, b_kmajor=True):
+    """(a^T if a_kmajor else a) @ (b if b_kmajor else b^T) (+ c0: M x N, or a length-N bias
+    row) on regcn_kreduce_gemm_f32: K split over workgroups, partials summed in a fixed order.
+    a: K x M (a_kmajor) or M x K; b: K x N (b_kmajor) or N x K; fp32."""
+    a, b = a.contiguous().float(), b.contiguous().float()
+    K = a.shape[0] if a_kmajor else a.shape[1]
+    M = a.shape[1] if a_kmajor else a.shape[0]
+    N = b.shape[1] if b_kmajor else b.shape[0]
+    if (b.shape[0] if b_kmajor else b.shape[1]) != K:
+        raise ValueError(f"kreduce_mm: a {tuple(a.shape)} does not match b {tuple(b.shape)}")
+    out = torch.empty(M, N, device=b.device, dtype=torch.float32)
+    c0_ld = 0
+    if c0 is not None:
+        c0 = c0.contiguous().float()
+        if c0.dim() == 1 and c0.shape[0] == N:
+            c0_ld = 0
+        elif tuple(c0.shape) == (M, N):
+            c0_ld = N
+        else:
+            c0, c0_ld = c0.expand(M, N).contiguous(), N
+    ws = torch.empty(max(1, _lib.lib().regcn_kreduce_workspace_floats(K, M, N)), device=b.device, dtype=torch.float32)
+    f = _lib.fptr
+    _lib.call("regcn_kreduce_gemm_f32", f(a, "a"), 1 if a_kmajor else 0, f(b, "b"), 1 if b_kmajor else 0, K, M, N,
+              f(c0), c0_ld, f(out), f(ws), _lib.stream())
+    return out
+
+
+class _Linear(torch.autograd.Function):
+    """F.linear(x, W, bias) for a mini-batch of query rows: y = x W^T + bias, dx = dy W,
+    dW = dy^T x, dbias = sum dy, all three products on regcn_kreduce_gemm_f32."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias):
+        x = x.contiguous()
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = bias is not None
+        return kreduce_mm(x, w, False, bias, b_kmajor=False)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = kreduce_mm(gy, w, False) if ctx.needs_input_grad[0] else None
+        gw = kreduce_mm(gy, x, True) if ctx.needs_input_grad[1] else None
+        gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+def linear(layer, x):
+    """layer(x) for an nn.Linear on 2-D fp32 CUDA rows (the decoders' projections,
+    hyperbolic_decoder.py:212-321), on the split-K kernel; anything else goes to the layer."""
+    if (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and layer.weight.dtype == torch.float32
+            and torch.is_grad_enabled()):
+        return _Linear.apply(x, layer.weight, layer.bias)
+    return layer(x)
+
+
+class _RowsByWeight(torch.autograd.Function):
+    """x (V x d_in) @ W (d_in x d_out): forward and the input gradient dy W^T are library GEMMs
+    (large M, short K); the weight gradient x^T dy (K = V) runs on regcn_kreduce_gemm_f32."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        x = x.contiguous()
+        ctx.save_for_backward(x, w)
+        return torch.mm(x, w)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        gx = torch.mm(gy, w.t()) if ctx.needs_input_grad[0] else None
+        gw = kreduce_mm(x, gy, True) if ctx.needs_input_grad[1] else None
+        return gx, gw
+
+
+def mm_weight(x, w):
+    """torch.mm(x, w) for the training path's (V x d) @ (d x d) products (hyperbolic_layers.py
+    self/evolve loop :273-280, neighbour weight :290, skip gate :315-318; hyperbolic_model.py
+    time gate :852-858), with the weight gradient on the split-K kernel."""
+    if x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 2 and w.dim() == 2:
+        return _RowsByWeight.apply(x, w)
+    return torch.mm(x, w)

@@ -223,8 +223,8 @@ class HyperbolicMuRP(_EntityDecoderBase):
         r_idx = trip[:, 1]
         s_emb = HyperbolicOps.project_to_ball(ent[trip[:, 0]], c)
         s_tan = self.dropout(HyperbolicOps.log_map_zero(s_emb, c))
-        rot_s = HyperbolicOps.exp_map_zero((self.rot_proj(rel[r_idx]) * s_tan).contiguous(), c)
-        t_r = HyperbolicOps.exp_map_zero(self.trans_proj(rel[r_idx]).contiguous(), c)
+        rot_s = HyperbolicOps.exp_map_zero((_ag.linear(self.rot_proj, rel[r_idx]) * s_tan).contiguous(), c)
+        t_r = HyperbolicOps.exp_map_zero(_ag.linear(self.trans_proj, rel[r_idx]).contiguous(), c)
         return HyperbolicOps.mobius_add(HyperbolicOps.project_to_ball(rot_s, c),
                                         HyperbolicOps.project_to_ball(t_r, c), c)
 
@@ -254,7 +254,7 @@ class HyperbolicRotH(_EntityDecoderBase):
     givens_rotation = staticmethod(givens_rotation)
 
     def _reshape_tangent(self, x):
-        return x + self.reshape_fc2(F.relu(self.reshape_fc1(x)))
+        return x + _ag.linear(self.reshape_fc2, F.relu(_ag.linear(self.reshape_fc1, x)))
 
     def _query(self, ent, rel, trip):
         """hyperbolic_decoder.py:1065-1085.  In eval mode (dropout = identity) one HIP launch
@@ -276,8 +276,8 @@ class HyperbolicRotH(_EntityDecoderBase):
         r_idx = trip[:, 1]
         s_emb = HyperbolicOps.project_to_ball(ent[trip[:, 0]], c)
         s_tan = self._reshape_tangent(self.dropout(HyperbolicOps.log_map_zero(s_emb, c)))
-        rot_s = HyperbolicOps.exp_map_zero(givens_rotation(s_tan, self.rot_proj(rel[r_idx])).contiguous(), c)
-        t_r = HyperbolicOps.exp_map_zero(self.trans_proj(rel[r_idx]).contiguous(), c)
+        rot_s = HyperbolicOps.exp_map_zero(givens_rotation(s_tan, _ag.linear(self.rot_proj, rel[r_idx])).contiguous(), c)
+        t_r = HyperbolicOps.exp_map_zero(_ag.linear(self.trans_proj, rel[r_idx]).contiguous(), c)
         return HyperbolicOps.mobius_add(HyperbolicOps.project_to_ball(rot_s, c),
                                         HyperbolicOps.project_to_ball(t_r, c), c)
 
@@ -314,11 +314,11 @@ class HyperbolicAttH(_EntityDecoderBase):
         s_emb = HyperbolicOps.project_to_ball(ent[trip[:, 0]], c)
         s_tan = self.dropout(HyperbolicOps.log_map_zero(s_emb, c))
         rr = rel[r_idx]
-        rot_s = givens_rotation(s_tan, self.rot_proj(rr))
-        ref_s = givens_reflection(s_tan, self.ref_proj(rr))
-        a_r = torch.sigmoid(torch.sum(self.attn_proj(rr) * torch.cat([s_tan, rr], dim=-1), dim=-1, keepdim=True))
+        rot_s = givens_rotation(s_tan, _ag.linear(self.rot_proj, rr))
+        ref_s = givens_reflection(s_tan, _ag.linear(self.ref_proj, rr))
+        a_r = torch.sigmoid(torch.sum(_ag.linear(self.attn_proj, rr) * torch.cat([s_tan, rr], dim=-1), dim=-1, keepdim=True))
         mixed = HyperbolicOps.exp_map_zero((a_r * rot_s + (1.0 - a_r) * ref_s).contiguous(), c)
-        t_r = HyperbolicOps.exp_map_zero(self.trans_proj(rr).contiguous(), c)
+        t_r = HyperbolicOps.exp_map_zero(_ag.linear(self.trans_proj, rr).contiguous(), c)
         return HyperbolicOps.mobius_add(HyperbolicOps.project_to_ball(mixed, c),
                                         HyperbolicOps.project_to_ball(t_r, c), c)
 
@@ -492,7 +492,7 @@ class HyperbolicRotHRel(_RelDecoderBase):
         c = self.c
         o_emb = ent[trip[:, 2]].contiguous()
         s_tan = self.dropout(HyperbolicOps.log_map_zero(ent[trip[:, 0]], c))
-        s_tan = s_tan + self.reshape_fc2(F.relu(self.reshape_fc1(s_tan)))
+        s_tan = s_tan + _ag.linear(self.reshape_fc2, F.relu(_ag.linear(self.reshape_fc1, s_tan)))
         rot_s = HyperbolicOps.exp_map_zero(givens_rotation(s_tan, self.global_rot).contiguous(), c)
         return HyperbolicOps.mobius_add(-rot_s, o_emb, c)
 
@@ -557,7 +557,7 @@ class HyperbolicConvTransE(nn.Module):
         B = len(triplets)
         x = torch.cat([et[triplets[:, 0]].unsqueeze(1), rel_embedding[triplets[:, 1]].unsqueeze(1)], 1)
         x = self.feature_map_drop(F.relu(self.bn1(self.conv1(self.inp_drop(self.bn0(x))))))
-        x = self.hidden_drop(self.fc(x.view(B, -1)))
+        x = self.hidden_drop(_ag.linear(self.fc, x.view(B, -1)))
         if B > 1:
             x = self.bn2(x)
         return torch.mm(F.relu(x), et.transpose(1, 0)) + self.b
@@ -586,5 +586,5 @@ class HyperbolicConvTransR(nn.Module):
         B = len(triplets)
         x = torch.cat([et[triplets[:, 0]].unsqueeze(1), et[triplets[:, 2]].unsqueeze(1)], 1)
         x = self.feature_map_drop(F.relu(self.bn1(self.conv1(self.inp_drop(self.bn0(x))))))
-        x = self.bn2(self.hidden_drop(self.fc(x.view(B, -1))))
+        x = self.bn2(self.hidden_drop(_ag.linear(self.fc, x.view(B, -1))))
         return torch.mm(F.relu(x), rel_embedding.transpose(1, 0)) + self.b

@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch.nn.parameter import Parameter
 
+from . import autograd as _ag
 from .hyperbolic_model import relation_gru_step
 from .layers import UnionRGCNLayer
 
@@ -76,7 +77,7 @@ class ConvTransE(nn.Module):
         B = len(triplets)
         x = torch.cat([e_all[triplets[:, 0]].unsqueeze(1), emb_rel[triplets[:, 1]].unsqueeze(1)], 1)
         x = self.feature_map_drop(F.relu(self.bn1(self.conv1(self.inp_drop(self.bn0(x))))))
-        x = self.hidden_drop(self.fc(x.view(B, -1)))
+        x = self.hidden_drop(_ag.linear(self.fc, x.view(B, -1)))
         if B > 1:
             x = self.bn2(x)
         x = F.relu(x)
@@ -107,7 +108,7 @@ class ConvTransR(nn.Module):
         B = len(triplets)
         x = torch.cat([e_all[triplets[:, 0]].unsqueeze(1), e_all[triplets[:, 2]].unsqueeze(1)], 1)
         x = self.feature_map_drop(F.relu(self.bn1(self.conv1(self.inp_drop(self.bn0(x))))))
-        x = self.bn2(self.hidden_drop(self.fc(x.view(B, -1))))
+        x = self.bn2(self.hidden_drop(_ag.linear(self.fc, x.view(B, -1))))
         return torch.mm(F.relu(x), emb_rel.transpose(1, 0))
 
 

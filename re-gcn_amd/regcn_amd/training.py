@@ -22,7 +22,7 @@ RRELU_SLOPE = (1.0 / 8 + 1.0 / 3) / 2  # F.rrelu(x) with training=False (hyperbo
 def _self_loop(x, g, w_loop, w_evolve):
     """W_loop for rows with in-edges, W_evolve otherwise (hyperbolic_layers.py:273-280)."""
     pos = (g.in_degrees() > 0).to(x.device).unsqueeze(-1)
-    return torch.where(pos, torch.mm(x, w_loop), torch.mm(x, w_evolve))
+    return torch.where(pos, A.mm_weight(x, w_loop), A.mm_weight(x, w_evolve))
 
 
 def _layer_tail(layer, g, h_new, x, prev_h, c):
@@ -32,7 +32,7 @@ def _layer_tail(layer, g, h_new, x, prev_h, c):
     loop = _self_loop(x, g, layer.loop_weight, layer.evolve_loop_weight) if layer.self_loop else None
     if layer.skip_connect and prev_h is not None:
         prev_t = A.log0(prev_h, c)
-        gate = torch.sigmoid(torch.mm(prev_t, layer.skip_weight) + layer.skip_bias)
+        gate = torch.sigmoid(A.mm_weight(prev_t, layer.skip_weight) + layer.skip_bias)
         if loop is not None:
             h_new = h_new + loop
         h_new = gate * h_new + (1 - gate) * prev_t
@@ -50,7 +50,7 @@ def union_layer(layer, g, h, rel, prev_h=None):
     c = float(layer.c)
     x = A.log0(h, c)
     r = A.get_radius(h)
-    agg = torch.mm(A.union_aggregate(x, r, rel.contiguous(), g, layer.radius_msg_gamma), layer.weight_neighbor)
+    agg = A.mm_weight(A.union_aggregate(x, r, rel.contiguous(), g, layer.radius_msg_gamma), layer.weight_neighbor)
     return _layer_tail(layer, g, agg, x, prev_h, c)
 
 
@@ -118,11 +118,11 @@ def model_forward(model, g_list):
             cur = A.exp0(F.normalize(A.log0(cur, c)), c)                              # :832-835
         ct = torch.clamp(A.log0(cur, c), -10.0, 10.0)                                  # :841-846
         pt = torch.clamp(x_prev, -10.0, 10.0)
-        tw = torch.sigmoid(torch.mm(pt, model.time_gate_weight) + model.time_gate_bias)
+        tw = torch.sigmoid(A.mm_weight(pt, model.time_gate_weight) + model.time_gate_bias)
         h = A.project(A.exp0(tw * ct + (1 - tw) * pt, c), c)                          # :859-860
         if model.use_residual_evolution:
             t = A.log0(h, trev.c)                                                      # hyperbolic_ops.py:395-435
-            delta = torch.clamp(trev.radius_mlp(t).squeeze(-1), -trev.epsilon, trev.epsilon)
+            delta = torch.clamp(A.linear(trev.radius_mlp, t).squeeze(-1), -trev.epsilon, trev.epsilon)
             base = trev.anchor_beta * r_static + (1.0 - trev.anchor_beta) * A.get_radius(h)
             h = A.apply_radius(h, base + delta, trev.c)
         else:
@@ -135,7 +135,7 @@ def euclid_layer(layer, g, h, rel):
     """UnionRGCNLayer.forward, rgcn/layers.py:222-279 (the cell passes prev_h = [], so no skip):
     norm sum_e (h_src + rel) W_n + loop, rrelu, dropout."""
     zero_r = torch.zeros(h.shape[0], device=h.device)
-    node = torch.mm(A.union_aggregate(h, zero_r, rel.contiguous(), g, 0.0), layer.weight_neighbor)
+    node = A.mm_weight(A.union_aggregate(h, zero_r, rel.contiguous(), g, 0.0), layer.weight_neighbor)
     if layer.self_loop:
         node = node + _self_loop(h, g, layer.loop_weight, layer.evolve_loop_weight)
     node = F.leaky_relu(node, RRELU_SLOPE)
@@ -161,7 +161,7 @@ def euclid_model_forward(model, g_list):
             cur = euclid_layer(layer, g, cur, h0)
         if model.layer_norm:
             cur = F.normalize(cur)
-        tw = torch.sigmoid(torch.mm(h, model.time_gate_weight) + model.time_gate_bias)
+        tw = torch.sigmoid(A.mm_weight(h, model.time_gate_weight) + model.time_gate_bias)
         h = tw * cur + (1 - tw) * h
         history.append(h)
     return history, None, h0, [], []

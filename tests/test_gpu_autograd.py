@@ -249,3 +249,54 @@ def test_transposed_lists():
     np.testing.assert_array_equal(t2.cpu().numpy(), ct[order])
     np.testing.assert_array_equal(tr["tptr"].cpu().numpy(),
                                   np.concatenate([[0], np.cumsum(np.bincount(ct, minlength=2 * R))]))
+
+
+@pytest.mark.parametrize("K,M,N,ak,bk", [(7128, 200, 200, True, True), (7128, 64, 200, False, True),
+                                          (7127, 64, 200, False, True), (64, 7128, 200, True, True),
+                                          (200, 128, 200, False, False), (201, 108, 100, False, False),
+                                          (10000, 128, 200, False, False), (7128, 1, 200, True, True),
+                                          (1, 3, 5, True, True), (37, 65, 129, False, True), (0, 16, 16, True, True),
+                                          (100000, 16, 48, True, False)])
+def test_kreduce_mm(K, M, N, ak, bk):
+    """regcn_kreduce_gemm_f32 (split-K MFMA, deterministic partial sum) against fp64 torch:
+    every A/B layout, the float4 R-major reads (K % 4 == 0) and their scalar fallback (K odd),
+    ragged M/N, K = 0, a K long enough for many splits; no c0, a full c0, a bias row."""
+    g = torch.Generator(device="cpu").manual_seed(K * 7 + M + N)
+    a = torch.randn((K, M) if ak else (M, K), generator=g)
+    b = torch.randn((K, N) if bk else (N, K), generator=g)
+    ref = (a.double().t() if ak else a.double()) @ (b.double() if bk else b.double().t())
+    tol = 1e-5 * max(1.0, float(ref.abs().max())) * max(1.0, K ** 0.5 / 30)
+    for cc in (None, torch.randn(M, N, generator=g), torch.randn(N, generator=g)):
+        got = A.kreduce_mm(a.to(DEV), b.to(DEV), ak, None if cc is None else cc.to(DEV), b_kmajor=bk)
+        want = ref if cc is None else ref + cc.double()
+        assert float((got.double().cpu() - want).abs().max()) <= tol
+    again = A.kreduce_mm(a.to(DEV), b.to(DEV), ak, b_kmajor=bk)
+    torch.testing.assert_close(again, A.kreduce_mm(a.to(DEV), b.to(DEV), ak, b_kmajor=bk), rtol=0, atol=0)
+
+
+def test_linear_grads():
+    """A.linear (nn.Linear forward, dx, dW, dbias on the split-K kernel) against fp64 torch."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    lin = torch.nn.Linear(200, 100).to(DEV)
+    x = torch.randn(128, 200, generator=g).to(DEV).requires_grad_(True)
+    gy = torch.randn(128, 100, generator=g).to(DEV)
+    A.linear(lin, x).backward(gy)
+    x64 = x.detach().double().requires_grad_(True)
+    w64 = lin.weight.detach().double().requires_grad_(True)
+    b64 = lin.bias.detach().double().requires_grad_(True)
+    torch.nn.functional.linear(x64, w64, b64).backward(gy.double())
+    for got, ref in ((x.grad, x64.grad), (lin.weight.grad, w64.grad), (lin.bias.grad, b64.grad)):
+        assert float((got.double() - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
+
+
+def test_mm_weight_grads():
+    """A.mm_weight: x @ W with the weight gradient x^T dy on the split-K kernel."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(7128, 200, generator=g).to(DEV).requires_grad_(True)
+    w = (torch.randn(200, 200, generator=g) / 200 ** 0.5).to(DEV).requires_grad_(True)
+    gy = torch.randn(7128, 200, generator=g).to(DEV)
+    A.mm_weight(x, w).backward(gy)
+    x64, w64 = x.detach().double().requires_grad_(True), w.detach().double().requires_grad_(True)
+    (x64 @ w64).backward(gy.double())
+    for got, ref in ((x.grad, x64.grad), (w.grad, w64.grad)):
+        assert float((got.double() - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
