@@ -141,6 +141,23 @@ int regcn_pack_weight_f32(const float* w, int32_t d_in, int32_t d_out, float* pa
 size_t regcn_kreduce_workspace_floats(int64_t K, int32_t M, int32_t N);
 int regcn_kreduce_gemm_f32(const float* a, int32_t a_kmajor, const float* b, int32_t b_kmajor, int64_t K, int32_t M,
                            int32_t N, const float* c0, int64_t c0_ld, float* out, float* workspace, void* stream);
+/* Fused elementwise layer tail / time gate of the training path, forward and backward (V x d,
+ * d % 4 == 0, contiguous, 16-B aligned):
+ *   a = clamp(agg, +-10) [CLAMP_IN]; a += pos[v] ? lx : ex [lx != NULL];
+ *   g = sigmoid(z + bias[col]), a = g a + (1 - g) p [z != NULL; bias nullable];
+ *   a = clamp(a, +-10) [CLAMP_OUT]; a = a > 0 ? a : slope a [LEAKY].
+ * grad_out == NULL: forward into out.  Otherwise backward: d_agg, d_lx / d_ex (the gradient
+ * routed by pos), d_z (pre-sigmoid; the bias gradient is its column sum), d_p; each output
+ * nullable.  Replaces the torch op chains of hyperbolic_layers.py:296-321 / :672-694 (clamp,
+ * self loop where, skip gate, clamp, rrelu) and hyperbolic_model.py:841-860 (time gate). */
+#define REGCN_TAIL_CLAMP_IN 1
+#define REGCN_TAIL_CLAMP_OUT 2
+#define REGCN_TAIL_LEAKY 4
+int regcn_tail_f32(const float* agg, const float* lx, const float* ex, const uint8_t* pos, const float* z,
+                   const float* bias, const float* p, int64_t V, int32_t d, int32_t flags, float slope,
+                   const float* grad_out, float* out, float* d_agg, float* d_lx, float* d_ex, float* d_z, float* d_p,
+                   void* stream);
+
 /* rows: permutation of 0..V-1 with the n_pos in-degree>0 rows first.
  * hyperbolic (euclid=0): v = clamp(agg @ w_n | agg, +-10) + x @ (w_loop | w_evolve)
  *   [skip: g = sigmoid(prev_t @ w_skip + b_skip); v = g v + (1-g) prev_t]

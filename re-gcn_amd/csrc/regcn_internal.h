@@ -275,6 +275,15 @@ int rel_gru(const RelGruArgs& a, hipStream_t st);
 size_t packed_weight_floats(int d_in);
 int pack_weight(const float* W, int d_in, int d_out, float* Wp, hipStream_t st);
 size_t kreduce_workspace_floats(int64_t K, int M, int N);
+struct TailArgs {
+  const float *agg, *lx, *ex, *z, *bias, *p, *gy;
+  const uint8_t* pos;
+  float *out, *dagg, *dlx, *dex, *dz, *dp;
+  int64_t V;
+  int d, flags;
+  float slope;
+};
+int tail(const TailArgs& t, int backward, hipStream_t st);
 int kreduce_gemm(const float* A, int a_kmajor, const float* B, int b_kmajor, int64_t K, int M, int N, const float* C0,
                  int64_t c0_ld, float* out, float* ws, hipStream_t st);
 int layer(const LayerArgs& a, hipStream_t st);

@@ -1,0 +1,116 @@
+// Fused elementwise tail of a training-path layer and of the time gate,
+// forward and backward, replacing ~10 forward and ~15 backward torch elementwise launches
+// on V x d tensors per use (the replayed training step is bound by such launches):
+//
+//   a = clamp(agg, -10, 10)                     [CLAMP_IN]   hyperbolic_layers.py:296 / :672
+//   a = a + (pos[v] ? lx : ex)                  [lx != 0]    self / evolve loop :273-280
+//   g = sigmoid(z + bias); a = g a + (1 - g) p  [z != 0]     skip gate :315-318, time gate
+//                                                            hyperbolic_model.py:852-860
+//   a = clamp(a, -10, 10)                       [CLAMP_OUT]  :319
+//   a = a > 0 ? a : slope a                     [LEAKY]      rrelu in eval form :320
+//
+// The forward keeps torch's fp32 op order with no contraction (__fmul_rn / __fadd_rn), so
+// it equals the op-by-op composition bit for bit (sigmoid aside: 1 / (1 + expf(-x)) as
+// torch's kernel, ocml expf).  The backward recomputes the forward from its inputs and
+// applies torch's derivative conventions (clamp passes the gradient on the closed interval,
+// leaky_relu uses x > 0, sigmoid' = (1 - y) y); the bias gradient (a column sum of dz) is
+// left to the caller.  Memory-bound: float4 per lane, one pass.
+#include "regcn_internal.h"
+#include "common.h"
+
+namespace regcn {
+namespace {
+
+constexpr int TAIL_THR = 256;
+
+__device__ __forceinline__ float clamp10(float x) { return fminf(fmaxf(x, -10.f), 10.f); }
+__device__ __forceinline__ bool in10(float x) { return x >= -10.f && x <= 10.f; }
+
+template <bool BWD>
+__global__ __launch_bounds__(TAIL_THR) void k_tail(TailArgs t) {
+  const int64_t n4 = t.V * t.d / 4;
+  for (int64_t i4 = (int64_t)blockIdx.x * TAIL_THR + threadIdx.x; i4 < n4; i4 += (int64_t)gridDim.x * TAIL_THR) {
+    const int64_t e0 = i4 * 4;
+    const int64_t v = e0 / t.d;
+    const int j0 = (int)(e0 - v * t.d);
+    const f4 agg = *reinterpret_cast<const f4*>(t.agg + e0);
+    f4 lx = {0.f, 0.f, 0.f, 0.f}, z = lx, p = lx, b = lx, gy = lx;
+    bool pos = false;
+    if (t.lx) {
+      pos = t.pos[v] != 0;
+      lx = *reinterpret_cast<const f4*>((pos ? t.lx : t.ex) + e0);
+    }
+    if (t.z) {
+      z = *reinterpret_cast<const f4*>(t.z + e0);
+      p = *reinterpret_cast<const f4*>(t.p + e0);
+      if (t.bias) b = *reinterpret_cast<const f4*>(t.bias + j0);
+    }
+    if (BWD) gy = *reinterpret_cast<const f4*>(t.gy + e0);
+    f4 out, dagg, dl, dz, dp;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float a = (t.flags & REGCN_TAIL_CLAMP_IN) ? clamp10(agg[e]) : agg[e];
+      if (t.lx) a = __fadd_rn(a, lx[e]);
+      const float s1 = a;  // gate input
+      float gt = 0.f, om = 0.f;
+      if (t.z) {
+        gt = 1.f / (1.f + expf(-__fadd_rn(z[e], b[e])));
+        om = __fsub_rn(1.f, gt);
+        a = __fadd_rn(__fmul_rn(gt, a), __fmul_rn(om, p[e]));
+      }
+      const float s2 = a;  // clamp_out input
+      if (t.flags & REGCN_TAIL_CLAMP_OUT) a = clamp10(a);
+      const float s3 = a;  // leaky input
+      if (t.flags & REGCN_TAIL_LEAKY) a = a > 0.f ? a : __fmul_rn(a, t.slope);
+      out[e] = a;
+      if (BWD) {
+        float g = gy[e];
+        if (t.flags & REGCN_TAIL_LEAKY) g = s3 > 0.f ? g : __fmul_rn(g, t.slope);
+        if ((t.flags & REGCN_TAIL_CLAMP_OUT) && !in10(s2)) g = 0.f;
+        if (t.z) {
+          const float dgt = __fadd_rn(__fmul_rn(g, s1), -__fmul_rn(g, p[e]));
+          dz[e] = __fmul_rn(__fmul_rn(dgt, om), gt);
+          dp[e] = __fmul_rn(g, om);
+          g = __fmul_rn(g, gt);
+        }
+        dl[e] = g;
+        dagg[e] = ((t.flags & REGCN_TAIL_CLAMP_IN) && !in10(agg[e])) ? 0.f : g;
+      }
+    }
+    if (!BWD) {
+      *reinterpret_cast<f4*>(t.out + e0) = out;
+    } else {
+      if (t.dagg) *reinterpret_cast<f4*>(t.dagg + e0) = dagg;
+      if (t.lx) {
+        const f4 zero = {0.f, 0.f, 0.f, 0.f};
+        if (t.dlx) *reinterpret_cast<f4*>(t.dlx + e0) = pos ? dl : zero;
+        if (t.dex) *reinterpret_cast<f4*>(t.dex + e0) = pos ? zero : dl;
+      }
+      if (t.z) {
+        if (t.dz) *reinterpret_cast<f4*>(t.dz + e0) = dz;
+        if (t.dp) *reinterpret_cast<f4*>(t.dp + e0) = dp;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+int tail(const TailArgs& t, int backward, hipStream_t st) {
+  if (t.V < 0 || t.d <= 0 || (t.d & 3)) return set_error(REGCN_EINVAL, "tail needs d %% 4 == 0 (d=%d)", t.d);
+  if (!t.agg || (!backward && !t.out) || (backward && !t.gy)) return set_error(REGCN_EINVAL, "null pointer");
+  if (t.lx && (!t.ex || !t.pos)) return set_error(REGCN_EINVAL, "tail: the self loop needs lx, ex and pos");
+  if (t.z && !t.p) return set_error(REGCN_EINVAL, "tail: the gate needs z and p");
+  const uintptr_t al = (uintptr_t)t.agg | (uintptr_t)t.lx | (uintptr_t)t.ex | (uintptr_t)t.z | (uintptr_t)t.p |
+                       (uintptr_t)t.bias | (uintptr_t)t.gy | (uintptr_t)t.out | (uintptr_t)t.dagg | (uintptr_t)t.dlx |
+                       (uintptr_t)t.dex | (uintptr_t)t.dz | (uintptr_t)t.dp;
+  if (al & 15) return set_error(REGCN_EINVAL, "tail needs 16-byte aligned rows");
+  const int64_t n4 = t.V * t.d / 4;
+  if (n4 == 0) return 0;
+  const unsigned grid = (unsigned)std::min<int64_t>((n4 + TAIL_THR - 1) / TAIL_THR, 8192);
+  if (backward) hipLaunchKernelGGL(k_tail<true>, dim3(grid), dim3(TAIL_THR), 0, st, t);
+  else hipLaunchKernelGGL(k_tail<false>, dim3(grid), dim3(TAIL_THR), 0, st, t);
+  return check_launch("k_tail");
+}
+
+}  // namespace regcn

@@ -4,8 +4,9 @@ The inference forward fuses a whole layer (gather + GEMMs + epilogue [+ timestep
 launch and keeps no intermediates.  Training needs them, so this path composes the
 autograd functions of autograd.py -- HIP kernels forward and backward for the row maps,
 the union / Lorentz message aggregation and (in the decoders) the all-entity cross
-entropy -- with library GEMMs (rocBLAS via torch.mm) and the elementwise glue (clamp,
-rrelu, sigmoid gates, dropout) as device torch ops.  The op sequence is the reference's:
+entropy -- with the split-K products (autograd.mm_weight / linear), the fused layer tail
+(autograd.tail: clamp, self loop, skip / time gates, rrelu) and the remaining glue (dropout,
+normalize, GRUCell) as device torch ops.  The op sequence is the reference's:
 
   HyperbolicUnionRGCNLayer.forward   hyperbolic_layers.py:242-323
   LorentzRGCNLayer.forward           hyperbolic_layers.py:627-694
@@ -19,27 +20,28 @@ from . import autograd as A
 RRELU_SLOPE = (1.0 / 8 + 1.0 / 3) / 2  # F.rrelu(x) with training=False (hyperbolic_model.py:120)
 
 
-def _self_loop(x, g, w_loop, w_evolve):
-    """W_loop for rows with in-edges, W_evolve otherwise (hyperbolic_layers.py:273-280)."""
-    pos = (g.in_degrees() > 0).to(x.device).unsqueeze(-1)
-    return torch.where(pos, A.mm_weight(x, w_loop), A.mm_weight(x, w_evolve))
+def _pos_rows(g, device):
+    """uint8 per row: 1 where the row has in-edges (hyperbolic_layers.py:273-280), cached."""
+    pos = g.__dict__.get("_pos_u8")
+    if pos is None or pos.device != device:
+        pos = (g.in_degrees() > 0).to(device=device, dtype=torch.uint8).contiguous()
+        g.__dict__["_pos_u8"] = pos
+    return pos
 
 
 def _layer_tail(layer, g, h_new, x, prev_h, c):
     """clamp -> + loop [-> skip blend] -> clamp -> rrelu -> dropout -> exp0
-    (hyperbolic_layers.py:296-321, :672-694)."""
-    h_new = torch.clamp(h_new, -10.0, 10.0)
-    loop = _self_loop(x, g, layer.loop_weight, layer.evolve_loop_weight) if layer.self_loop else None
+    (hyperbolic_layers.py:296-321, :672-694); everything up to rrelu is one fused launch
+    (A.tail), the loop's W_loop / W_evolve products (rows with / without in-edges) feed it."""
+    lx = ex = pos = z = bias = prev_t = None
+    if layer.self_loop:
+        lx, ex = A.mm_weight(x, layer.loop_weight), A.mm_weight(x, layer.evolve_loop_weight)
+        pos = _pos_rows(g, x.device)
     if layer.skip_connect and prev_h is not None:
         prev_t = A.log0(prev_h, c)
-        gate = torch.sigmoid(A.mm_weight(prev_t, layer.skip_weight) + layer.skip_bias)
-        if loop is not None:
-            h_new = h_new + loop
-        h_new = gate * h_new + (1 - gate) * prev_t
-    elif loop is not None:
-        h_new = h_new + loop
-    h_new = torch.clamp(h_new, -10.0, 10.0)
-    h_new = F.leaky_relu(h_new, RRELU_SLOPE)
+        z, bias = A.mm_weight(prev_t, layer.skip_weight), layer.skip_bias
+    h_new = A.tail(h_new, lx, ex, pos, z, bias, prev_t,
+                   A.TAIL_CLAMP_IN | A.TAIL_CLAMP_OUT | A.TAIL_LEAKY, RRELU_SLOPE)
     if layer.dropout is not None:
         h_new = layer.dropout(h_new)
     return A.exp0(h_new, c)
@@ -116,10 +118,10 @@ def model_forward(model, g_list):
         cur = A.project(cur, c)                                                        # :829
         if model.layer_norm:
             cur = A.exp0(F.normalize(A.log0(cur, c)), c)                              # :832-835
-        ct = torch.clamp(A.log0(cur, c), -10.0, 10.0)                                  # :841-846
-        pt = torch.clamp(x_prev, -10.0, 10.0)
-        tw = torch.sigmoid(A.mm_weight(pt, model.time_gate_weight) + model.time_gate_bias)
-        h = A.project(A.exp0(tw * ct + (1 - tw) * pt, c), c)                          # :859-860
+        pt = torch.clamp(x_prev, -10.0, 10.0)                                          # :841-846
+        z = A.mm_weight(pt, model.time_gate_weight)                                    # tw = sigmoid(z + b)
+        mix = A.tail(A.log0(cur, c), z=z, bias=model.time_gate_bias, p=pt, flags=A.TAIL_CLAMP_IN)
+        h = A.project(A.exp0(mix, c), c)                                               # :859-860
         if model.use_residual_evolution:
             t = A.log0(h, trev.c)                                                      # hyperbolic_ops.py:395-435
             delta = torch.clamp(A.linear(trev.radius_mlp, t).squeeze(-1), -trev.epsilon, trev.epsilon)
@@ -136,9 +138,11 @@ def euclid_layer(layer, g, h, rel):
     norm sum_e (h_src + rel) W_n + loop, rrelu, dropout."""
     zero_r = torch.zeros(h.shape[0], device=h.device)
     node = A.mm_weight(A.union_aggregate(h, zero_r, rel.contiguous(), g, 0.0), layer.weight_neighbor)
+    lx = ex = pos = None
     if layer.self_loop:
-        node = node + _self_loop(h, g, layer.loop_weight, layer.evolve_loop_weight)
-    node = F.leaky_relu(node, RRELU_SLOPE)
+        lx, ex = A.mm_weight(h, layer.loop_weight), A.mm_weight(h, layer.evolve_loop_weight)
+        pos = _pos_rows(g, h.device)
+    node = A.tail(node, lx, ex, pos, flags=A.TAIL_LEAKY, slope=RRELU_SLOPE)
     if layer.dropout is not None:
         node = layer.dropout(node)
     return node
@@ -161,8 +165,7 @@ def euclid_model_forward(model, g_list):
             cur = euclid_layer(layer, g, cur, h0)
         if model.layer_norm:
             cur = F.normalize(cur)
-        tw = torch.sigmoid(A.mm_weight(h, model.time_gate_weight) + model.time_gate_bias)
-        h = tw * cur + (1 - tw) * h
+        h = A.tail(cur, z=A.mm_weight(h, model.time_gate_weight), bias=model.time_gate_bias, p=h)  # tw cur + (1 - tw) h
         history.append(h)
     return history, None, h0, [], []
 

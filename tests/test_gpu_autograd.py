@@ -300,3 +300,29 @@ def test_mm_weight_grads():
     (x64 @ w64).backward(gy.double())
     for got, ref in ((x.grad, x64.grad), (w.grad, w64.grad)):
         assert float((got.double() - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("case", ["layer_skip", "layer", "time_gate", "euclid"])
+def test_fused_tail(case):
+    """A.tail (regcn_tail_f32) against the op-by-op torch composition it replaces: forward to
+    2e-5 absolute (same fp32 op order without contraction; only sigmoid's expf may differ in
+    the last ulp), gradients of every input to 1e-5 of their max; values straddle the +-10
+    clamps and 0."""
+    V, d = 1037, 200
+    g = torch.Generator(device="cpu").manual_seed(11)
+    mk = lambda s=1.0: (s * torch.randn(V, d, generator=g)).to(DEV).requires_grad_(True)
+    agg, lx, ex, z, p = mk(8.0), mk(4.0), mk(4.0), mk(2.0), mk(6.0)
+    bias = (0.3 * torch.randn(d, generator=g)).to(DEV).requires_grad_(True)
+    pos = (torch.rand(V, generator=g) > 0.4).to(torch.uint8).to(DEV)
+    slope = (1.0 / 8 + 1.0 / 3) / 2
+    args = {"layer_skip": (agg, lx, ex, pos, z, bias, p, 7, slope), "layer": (agg, lx, ex, pos, None, None, None, 7, slope),
+            "time_gate": (agg, None, None, None, z, bias, p, 1, 0.0), "euclid": (agg, lx, ex, pos, None, None, None, 4, slope)}[case]
+    gy = torch.randn(V, d, generator=g).to(DEV)
+    ins = [t for t in args[:7] if t is not None and t.dtype == torch.float32]
+    out = A.tail(*args)
+    got = torch.autograd.grad(out, ins, gy)
+    ref_out = A._tail_torch(*args)
+    ref = torch.autograd.grad(ref_out, ins, gy)
+    assert float((out - ref_out).abs().max()) <= 2e-6 * 10
+    for a, b in zip(got, ref):
+        assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
