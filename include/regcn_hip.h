@@ -158,6 +158,13 @@ int regcn_tail_f32(const float* agg, const float* lx, const float* ex, const uin
                    const float* grad_out, float* out, float* d_agg, float* d_lx, float* d_ex, float* d_z, float* d_p,
                    void* stream);
 
+/* Lorentz centroid -> Poincare ball of a Lorentz layer's raw message sums (regcn_lorentz_sum_raw_f32)
+ * for the training path: y = (Sv / sc) / max(1 + sqrt_c S0 / sc, eps), sc = sqrt(max(c (S0^2 -
+ * |Sv|^2), eps)) (hyperbolic_layers.py:613-625, :669).  grad_y == NULL: forward into y; else
+ * backward into d_S0 (V) and d_Sv (V x d).  d % 4 == 0, d <= 256. */
+int regcn_lorentz_centroid_f32(const float* S0, const float* Sv, int64_t V, int32_t d, float c, float sqrt_c,
+                               const float* grad_y, float* y, float* d_S0, float* d_Sv, void* stream);
+
 /* rows: permutation of 0..V-1 with the n_pos in-degree>0 rows first.
  * hyperbolic (euclid=0): v = clamp(agg @ w_n | agg, +-10) + x @ (w_loop | w_evolve)
  *   [skip: g = sigmoid(prev_t @ w_skip + b_skip); v = g v + (1-g) prev_t]

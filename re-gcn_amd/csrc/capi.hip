@@ -131,6 +131,11 @@ int regcn_tail_f32(const float* agg, const float* lx, const float* ex, const uin
   return tail(t, grad_out != nullptr, ST(s));
 }
 
+int regcn_lorentz_centroid_f32(const float* S0, const float* Sv, int64_t V, int32_t d, float c, float sqrt_c,
+                               const float* grad_y, float* y, float* d_S0, float* d_Sv, void* s) {
+  return centroid(S0, Sv, V, d, c, sqrt_c, grad_y, y, d_S0, d_Sv, ST(s));
+}
+
 int regcn_layer_tail_f32(const float* agg, const float* w_n, const float* x, const float* w_loop,
                          const float* w_evolve, const float* prev_t, const float* w_skip, const float* b_skip,
                          const float* drop_mask, const int32_t* rows, int32_t n_pos, int32_t V, int32_t d,

@@ -9,9 +9,9 @@
 //   a = clamp(a, -10, 10)                       [CLAMP_OUT]  :319
 //   a = a > 0 ? a : slope a                     [LEAKY]      rrelu in eval form :320
 //
-// The forward keeps torch's fp32 op order with no contraction (__fmul_rn / __fadd_rn), so
-// it equals the op-by-op composition bit for bit (sigmoid aside: 1 / (1 + expf(-x)) as
-// torch's kernel, ocml expf).  The backward recomputes the forward from its inputs and
+// The forward keeps torch's fp32 op order with no contraction (__fmul_rn / __fadd_rn); it
+// differs from the op-by-op composition only through sigmoid's expf (1 / (1 + expf(-x)) as
+// torch's kernel, ocml expf: last-ulp differences).  The backward recomputes the forward from its inputs and
 // applies torch's derivative conventions (clamp passes the gradient on the closed interval,
 // leaky_relu uses x > 0, sigmoid' = (1 - y) y); the bias gradient (a column sum of dz) is
 // left to the caller.  Memory-bound: float4 per lane, one pass.
@@ -94,6 +94,44 @@ __global__ __launch_bounds__(TAIL_THR) void k_tail(TailArgs t) {
   }
 }
 
+// Lorentz centroid -> Poincare ball of a Lorentz layer's message sums (S0, Sv), one wave
+// per row (lane l: columns 4l..4l+3, d <= 256), forward and backward:
+//   ip = -S0^2 + |Sv|^2, sc = sqrt(max(-c ip, eps)), c0 = S0 / sc,
+//   y = (Sv / sc) / max(1 + sqrt(c) c0, eps)          (hyperbolic_layers.py:613-625, :669)
+// The backward follows torch's conventions for the clamps (gradient on x >= eps).
+template <bool BWD>
+__global__ __launch_bounds__(256) void k_centroid(const float* __restrict__ S0, const float* __restrict__ Sv,
+                                                  int64_t V, int d, float c, float sqc,
+                                                  const float* __restrict__ gy, float* __restrict__ y,
+                                                  float* __restrict__ dS0, float* __restrict__ dSv) {
+  const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (v >= V) return;
+  const int col = 4 * (threadIdx.x & 63);
+  const float s0 = S0[v];
+  const f4 sv = load4(Sv + v * d, col, d);
+  const float ip = -s0 * s0 + wave_sum(dot4(sv, sv));
+  const float inner = -ip * c;
+  const float sc = sqrtf(fmaxf(inner, REGCN_EPS));
+  const float c0 = s0 / sc;
+  const float dn = 1.f + c0 * sqc;
+  const float den = fmaxf(dn, REGCN_EPS);
+  const f4 u = sv / sc;
+  const f4 yy = u / den;
+  if (!BWD) {
+    store4(y + v * d, col, d, yy);
+    return;
+  }
+  const f4 g = load4(gy + v * d, col, d);
+  const float dden = -wave_sum(dot4(g, yy)) / den;
+  const float dc0 = dn >= REGCN_EPS ? dden * sqc : 0.f;
+  const f4 du = g / den;
+  const float dsc = -dc0 * s0 / (sc * sc) - wave_sum(dot4(du, sv)) / (sc * sc);
+  const float dinner = inner >= REGCN_EPS ? dsc * 0.5f / sc : 0.f;
+  const float dip = -c * dinner;
+  if ((threadIdx.x & 63) == 0) dS0[v] = dc0 / sc + dip * (-2.f * s0);
+  store4(dSv + v * d, col, d, du / sc + (2.f * dip) * sv);
+}
+
 }  // namespace
 
 int tail(const TailArgs& t, int backward, hipStream_t st) {
@@ -111,6 +149,17 @@ int tail(const TailArgs& t, int backward, hipStream_t st) {
   if (backward) hipLaunchKernelGGL(k_tail<true>, dim3(grid), dim3(TAIL_THR), 0, st, t);
   else hipLaunchKernelGGL(k_tail<false>, dim3(grid), dim3(TAIL_THR), 0, st, t);
   return check_launch("k_tail");
+}
+
+int centroid(const float* S0, const float* Sv, int64_t V, int d, float c, float sqc, const float* gy, float* y,
+             float* dS0, float* dSv, hipStream_t st) {
+  if (V < 0 || d <= 0 || d > 256 || (d & 3)) return set_error(REGCN_EINVAL, "centroid needs d %% 4 == 0, d <= 256");
+  if (!S0 || !Sv || (gy ? (!dS0 || !dSv) : !y)) return set_error(REGCN_EINVAL, "null pointer");
+  if (V == 0) return 0;
+  const dim3 grid((unsigned)((V + 3) / 4));
+  if (gy) hipLaunchKernelGGL(k_centroid<true>, grid, dim3(256), 0, st, S0, Sv, V, d, c, sqc, gy, y, dS0, dSv);
+  else hipLaunchKernelGGL(k_centroid<false>, grid, dim3(256), 0, st, S0, Sv, V, d, c, sqc, gy, y, dS0, dSv);
+  return check_launch("k_centroid");
 }
 
 }  // namespace regcn

@@ -245,11 +245,42 @@ def lorentz_aggregate(x, rel, W, g, nb, c):
     reference's 1/deg weights cancel), rows without in-edges give 0."""
     cf = _cf(c)
     S0, Sv = lorentz_sum(x, rel, W, g, nb, cf)
+    if Sv.shape[1] % 4 == 0 and Sv.shape[1] <= 256:
+        y = _Centroid.apply(S0, Sv, cf)
+    else:
+        y = _centroid_torch(S0, Sv, cf)
+    return log0(y, cf)
+
+
+def _centroid_torch(S0, Sv, cf):
     ip = -S0 * S0 + (Sv * Sv).sum(-1)
     sc = torch.sqrt(torch.clamp(-ip * cf, min=EPS))
     c0 = S0 / sc
-    y = (Sv / sc.unsqueeze(-1)) / torch.clamp(1.0 + c0 * cf ** 0.5, min=EPS).unsqueeze(-1)
-    return log0(y, cf)
+    return (Sv / sc.unsqueeze(-1)) / torch.clamp(1.0 + c0 * cf ** 0.5, min=EPS).unsqueeze(-1)
+
+
+class _Centroid(torch.autograd.Function):
+    """_centroid_torch in one row kernel forward and one backward (regcn_lorentz_centroid_f32)."""
+
+    @staticmethod
+    def forward(ctx, S0, Sv, cf):
+        S0, Sv = S0.contiguous(), Sv.contiguous()
+        y = torch.empty_like(Sv)
+        f = _lib.fptr
+        _lib.call("regcn_lorentz_centroid_f32", f(S0, "S0"), f(Sv, "Sv"), Sv.shape[0], Sv.shape[1], float(cf),
+                  float(cf ** 0.5), None, f(y), None, None, _lib.stream())
+        ctx.save_for_backward(S0, Sv)
+        ctx.cf = cf
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        S0, Sv = ctx.saved_tensors
+        dS0, dSv = torch.empty_like(S0), torch.empty_like(Sv)
+        f = _lib.fptr
+        _lib.call("regcn_lorentz_centroid_f32", f(S0), f(Sv), Sv.shape[0], Sv.shape[1], float(ctx.cf),
+                  float(ctx.cf ** 0.5), f(gy.contiguous()), None, f(dS0), f(dSv), _lib.stream())
+        return dS0, dSv, None
 
 
 # ------------------------------------------------------------------------- cross entropy

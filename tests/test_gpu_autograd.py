@@ -326,3 +326,23 @@ def test_fused_tail(case):
     assert float((out - ref_out).abs().max()) <= 2e-6 * 10
     for a, b in zip(got, ref):
         assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
+
+
+def test_lorentz_centroid():
+    """regcn_lorentz_centroid_f32 (A._Centroid) against the torch composition it replaces,
+    forward and both gradients; raw sums shaped like a Lorentz layer's (S0 > |Sv|), plus rows
+    hitting the eps clamps (S0 = |Sv| = 0)."""
+    V, d, c = 513, 200, 0.01
+    g = torch.Generator(device="cpu").manual_seed(13)
+    Sv = torch.randn(V, d, generator=g)
+    S0 = (Sv.norm(dim=1) ** 2 + 1.0 / c).sqrt() * (1 + torch.rand(V, generator=g))
+    S0[:7], Sv[:7] = 0.0, 0.0
+    S0, Sv = S0.to(DEV).requires_grad_(True), Sv.to(DEV).requires_grad_(True)
+    gy = torch.randn(V, d, generator=g).to(DEV)
+    y = A._Centroid.apply(S0, Sv, c)
+    got = torch.autograd.grad(y, (S0, Sv), gy)
+    yr = A._centroid_torch(S0, Sv, c)
+    ref = torch.autograd.grad(yr, (S0, Sv), gy)
+    assert float((y - yr).abs().max()) <= 1e-5 * max(1.0, float(yr.abs().max()))
+    for a, b in zip(got, ref):
+        assert float((a - b).abs().max()) <= 1e-4 * max(1.0, float(b.abs().max()))
