@@ -165,6 +165,15 @@ int regcn_tail_f32(const float* agg, const float* lx, const float* ex, const uin
 int regcn_lorentz_centroid_f32(const float* S0, const float* Sv, int64_t V, int32_t d, float c, float sqrt_c,
                                const float* grad_y, float* y, float* d_S0, float* d_Sv, void* stream);
 
+/* Givens rotation of interleaved pairs for the training path's RotH/RefH/AttH queries
+ * (hyperbolic_decoder.py:1032-1051 givens_rotation; reflect = 1: :1392-1401 givens_reflection):
+ * pair i = (x[2i], x[2i+1]) with t = angles[i] (angles row-major B x d/2 over x B x d, so
+ * pairs and angles share one index) -> (cos x1 - sin x2, sin x1 + cos x2), reflected
+ * (cos x1 + sin x2, sin x1 - cos x2).  grad_out == NULL: forward into out; else backward
+ * into d_x and d_angles. */
+int regcn_givens_rotation_f32(const float* x, const float* angles, int64_t n_pairs, int32_t reflect,
+                              const float* grad_out, float* out, float* d_x, float* d_angles, void* stream);
+
 /* rows: permutation of 0..V-1 with the n_pos in-degree>0 rows first.
  * hyperbolic (euclid=0): v = clamp(agg @ w_n | agg, +-10) + x @ (w_loop | w_evolve)
  *   [skip: g = sigmoid(prev_t @ w_skip + b_skip); v = g v + (1-g) prev_t]

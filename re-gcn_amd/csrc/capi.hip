@@ -136,6 +136,11 @@ int regcn_lorentz_centroid_f32(const float* S0, const float* Sv, int64_t V, int3
   return centroid(S0, Sv, V, d, c, sqrt_c, grad_y, y, d_S0, d_Sv, ST(s));
 }
 
+int regcn_givens_rotation_f32(const float* x, const float* angles, int64_t n_pairs, int32_t reflect,
+                              const float* grad_out, float* out, float* d_x, float* d_angles, void* s) {
+  return givens(x, angles, n_pairs, reflect, grad_out, out, d_x, d_angles, ST(s));
+}
+
 int regcn_layer_tail_f32(const float* agg, const float* w_n, const float* x, const float* w_loop,
                          const float* w_evolve, const float* prev_t, const float* w_skip, const float* b_skip,
                          const float* drop_mask, const int32_t* rows, int32_t n_pos, int32_t V, int32_t d,

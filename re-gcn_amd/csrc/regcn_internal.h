@@ -284,6 +284,8 @@ struct TailArgs {
   float slope;
 };
 int tail(const TailArgs& t, int backward, hipStream_t st);
+int givens(const float* x, const float* ang, int64_t n_pairs, int reflect, const float* gy, float* out, float* dx, float* dang,
+           hipStream_t st);
 int centroid(const float* S0, const float* Sv, int64_t V, int d, float c, float sqc, const float* gy, float* y,
              float* dS0, float* dSv, hipStream_t st);
 int kreduce_gemm(const float* A, int a_kmajor, const float* B, int b_kmajor, int64_t K, int M, int N, const float* C0,

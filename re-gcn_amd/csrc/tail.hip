@@ -132,6 +132,49 @@ __global__ __launch_bounds__(256) void k_centroid(const float* __restrict__ S0, 
   store4(dSv + v * d, col, d, du / sc + (2.f * dip) * sv);
 }
 
+// Givens rotation (REF: reflection) of interleaved pairs (hyperbolic_decoder.py:1032-1051,
+// :1392-1401): for pair i, (x1, x2) = (x[2i], x[2i+1]), t = ang[i]:
+//   rotation   out = (cos x1 - sin x2, sin x1 + cos x2)
+//   reflection out = (cos x1 + sin x2, sin x1 - cos x2)      (torch's op order, no contraction)
+// backward: rotation   dx = (cos g1 + sin g2, cos g2 - sin g1),
+//                      dt = g2 (cos x1 - sin x2) - g1 (sin x1 + cos x2);
+//           reflection dx = (cos g1 + sin g2, sin g1 - cos g2),
+//                      dt = g1 (cos x2 - sin x1) + g2 (cos x1 + sin x2).
+template <bool BWD, bool REF>
+__global__ __launch_bounds__(256) void k_givens(const float* __restrict__ x, const float* __restrict__ ang,
+                                                int64_t n_pairs, const float* __restrict__ gy,
+                                                float* __restrict__ out, float* __restrict__ dx,
+                                                float* __restrict__ dang) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pairs; i += (int64_t)gridDim.x * 256) {
+    const f2 xv = *reinterpret_cast<const f2*>(x + 2 * i);
+    const float t = ang[i];
+    const float co = cosf(t), si = sinf(t);
+    if (!BWD) {
+      f2 o;
+      if (REF) {
+        o.x = __fadd_rn(__fmul_rn(co, xv.x), __fmul_rn(si, xv.y));
+        o.y = __fsub_rn(__fmul_rn(si, xv.x), __fmul_rn(co, xv.y));
+      } else {
+        o.x = __fsub_rn(__fmul_rn(co, xv.x), __fmul_rn(si, xv.y));
+        o.y = __fadd_rn(__fmul_rn(si, xv.x), __fmul_rn(co, xv.y));
+      }
+      *reinterpret_cast<f2*>(out + 2 * i) = o;
+    } else {
+      const f2 g = *reinterpret_cast<const f2*>(gy + 2 * i);
+      f2 d;
+      d.x = co * g.x + si * g.y;
+      if (REF) {
+        d.y = si * g.x - co * g.y;
+        dang[i] = g.x * (co * xv.y - si * xv.x) + g.y * (co * xv.x + si * xv.y);
+      } else {
+        d.y = co * g.y - si * g.x;
+        dang[i] = g.y * (co * xv.x - si * xv.y) - g.x * (si * xv.x + co * xv.y);
+      }
+      *reinterpret_cast<f2*>(dx + 2 * i) = d;
+    }
+  }
+}
+
 }  // namespace
 
 int tail(const TailArgs& t, int backward, hipStream_t st) {
@@ -160,6 +203,20 @@ int centroid(const float* S0, const float* Sv, int64_t V, int d, float c, float 
   if (gy) hipLaunchKernelGGL(k_centroid<true>, grid, dim3(256), 0, st, S0, Sv, V, d, c, sqc, gy, y, dS0, dSv);
   else hipLaunchKernelGGL(k_centroid<false>, grid, dim3(256), 0, st, S0, Sv, V, d, c, sqc, gy, y, dS0, dSv);
   return check_launch("k_centroid");
+}
+
+int givens(const float* x, const float* ang, int64_t n_pairs, int reflect, const float* gy, float* out, float* dx, float* dang,
+           hipStream_t st) {
+  if (n_pairs < 0 || !x || !ang || (gy ? (!dx || !dang) : !out)) return set_error(REGCN_EINVAL, "null pointer");
+  if (((uintptr_t)x | (uintptr_t)gy | (uintptr_t)out | (uintptr_t)dx) & 7)
+    return set_error(REGCN_EINVAL, "givens needs 8-byte aligned pairs");
+  if (n_pairs == 0) return 0;
+  const unsigned grid = (unsigned)std::min<int64_t>((n_pairs + 255) / 256, 8192);
+  if (gy && reflect) hipLaunchKernelGGL((k_givens<true, true>), dim3(grid), dim3(256), 0, st, x, ang, n_pairs, gy, out, dx, dang);
+  else if (gy) hipLaunchKernelGGL((k_givens<true, false>), dim3(grid), dim3(256), 0, st, x, ang, n_pairs, gy, out, dx, dang);
+  else if (reflect) hipLaunchKernelGGL((k_givens<false, true>), dim3(grid), dim3(256), 0, st, x, ang, n_pairs, gy, out, dx, dang);
+  else hipLaunchKernelGGL((k_givens<false, false>), dim3(grid), dim3(256), 0, st, x, ang, n_pairs, gy, out, dx, dang);
+  return check_launch("k_givens");
 }
 
 }  // namespace regcn

@@ -480,3 +480,37 @@ def tail(agg, lx=None, ex=None, pos=None, z=None, bias=None, p=None, flags=0, sl
             and all(t.dtype == torch.float32 for t in ts)):
         return _Tail.apply(agg, lx, ex, z, bias, p, pos, flags, slope)
     return _tail_torch(agg, lx, ex, pos, z, bias, p, flags, slope)
+
+
+# ------------------------------------------------------------------ Givens rotation
+class _Givens(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, angles, reflect):
+        x, angles = x.contiguous(), angles.contiguous()
+        out = torch.empty_like(x)
+        f = _lib.fptr
+        _lib.call("regcn_givens_rotation_f32", f(x, "x"), f(angles, "angles"), angles.numel(), int(reflect), None,
+                  f(out), None, None, _lib.stream())
+        ctx.save_for_backward(x, angles)
+        ctx.reflect = int(reflect)
+        return out
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, angles = ctx.saved_tensors
+        dx, da = torch.empty_like(x), torch.empty_like(angles)
+        f = _lib.fptr
+        _lib.call("regcn_givens_rotation_f32", f(x), f(angles), angles.numel(), ctx.reflect, f(gy.contiguous()), None,
+                  f(dx), f(da), _lib.stream())
+        return dx, da, None
+
+
+def givens_rotation(x, angles, reflect=False):
+    """hyperbolic_decoder.py:1032-1051 (rotation) / :1392-1401 (reflection, reflect=True) of
+    interleaved pairs as one launch each way (regcn_givens_rotation_f32) for B x d rows with
+    B x d/2 angles; None otherwise."""
+    if (x.is_cuda and x.dim() == 2 and angles.dim() == 2 and x.dtype == torch.float32
+            and angles.dtype == torch.float32 and tuple(angles.shape) == (x.shape[0], x.shape[1] // 2)
+            and x.shape[1] % 2 == 0):
+        return _Givens.apply(x, angles, reflect)
+    return None

@@ -119,6 +119,10 @@ def _grad_path(mod, *ts):
 
 def givens_rotation(x, angles):
     """hyperbolic_decoder.py:1032-1051 (interleaved pairs)."""
+    if torch.is_grad_enabled():
+        fused = _ag.givens_rotation(x, angles)
+        if fused is not None:
+            return fused
     if angles.dim() == 1:
         angles = angles.unsqueeze(0).expand(x.shape[0], -1)
     x1, x2 = x[:, 0::2], x[:, 1::2]
@@ -128,6 +132,10 @@ def givens_rotation(x, angles):
 
 def givens_reflection(x, angles):
     """hyperbolic_decoder.py:1392-1401."""
+    if torch.is_grad_enabled():
+        fused = _ag.givens_rotation(x, angles, reflect=True)
+        if fused is not None:
+            return fused
     if angles.dim() == 1:
         angles = angles.unsqueeze(0).expand(x.shape[0], -1)
     x1, x2 = x[:, 0::2], x[:, 1::2]

@@ -346,3 +346,24 @@ def test_lorentz_centroid():
     assert float((y - yr).abs().max()) <= 1e-5 * max(1.0, float(yr.abs().max()))
     for a, b in zip(got, ref):
         assert float((a - b).abs().max()) <= 1e-4 * max(1.0, float(b.abs().max()))
+
+
+@pytest.mark.parametrize("reflect", [False, True])
+def test_givens_rotation(reflect):
+    """regcn_givens_rotation_f32 (A.givens_rotation) against the torch compositions of
+    hyperbolic_decoder.givens_rotation / givens_reflection: forward to 1e-6, both gradients
+    to 1e-5."""
+    g = torch.Generator(device="cpu").manual_seed(17)
+    x = torch.randn(128, 200, generator=g).to(DEV).requires_grad_(True)
+    a = (3 * torch.randn(128, 100, generator=g)).to(DEV).requires_grad_(True)
+    gy = torch.randn(128, 200, generator=g).to(DEV)
+    out = A.givens_rotation(x, a, reflect=reflect)
+    got = torch.autograd.grad(out, (x, a), gy)
+    x1, x2 = x[:, 0::2], x[:, 1::2]
+    co, si = torch.cos(a), torch.sin(a)
+    pair = [co * x1 + si * x2, si * x1 - co * x2] if reflect else [co * x1 - si * x2, si * x1 + co * x2]
+    ref_t = torch.stack(pair, dim=2).reshape(128, 200)
+    ref = torch.autograd.grad(ref_t, (x, a), gy)
+    assert float((out - ref_t).abs().max()) <= 1e-6 * max(1.0, float(ref_t.abs().max()))
+    for u, v in zip(got, ref):
+        assert float((u - v).abs().max()) <= 1e-5 * max(1.0, float(v.abs().max()))
