@@ -8,12 +8,13 @@
 // a library GEMM runs these on ONE 256 x 224 macro tile, 33-46 us each).
 // A library GEMM tiles the small output into a few dozen macro tiles and walks the whole K
 // in each (measured 54 us for 7128 x 200 x 200 on 49 workgroups); here K is split over
-// workgroups so a launch fills the 256 CUs, and a second pass sums the split partials in a
-// fixed order (deterministic; no atomics).
+// workgroups (and over the waves of a workgroup) so a launch fills the 256 CUs; a long K's
+// split partials are summed by a second pass in a fixed order (deterministic; no atomics).
 //
-// A workgroup (4 waves) owns a 64 x 64 output tile and one K chunk; wave w a 32 x 32
-// quarter as 2 x 2 v_mfma_f32_16x16x4_f32 tiles.  Operands are read straight from global
-// memory (each element is used by two waves of the workgroup; L1/L2 absorb the reuse): in a
+// A workgroup (4 waves) owns a 32 x 32 output tile (2 x 2 v_mfma_f32_16x16x4_f32 tiles) and
+// one K chunk, whose 32-k groups its waves take round-robin; the four partial tiles are
+// summed through LDS in wave order, so a short K (the K = d products) needs no second
+// launch.  Operands are read straight from global memory (L1/L2 absorb the reuse): in a
 // group of 32 k, lane (lo = l & 15, q = l >> 4) supplies at MFMA step e (0..7) the A value
 // A(32u + 8q + e, m0 + lo) and the B value B(32u + 8q + e, n0 + lo); any permutation of k is
 // a valid order for a sum as long as A and B agree, and this one lets an M-major A (an
@@ -30,6 +31,8 @@ namespace {
 
 constexpr int KR_THR = 256;
 constexpr int KR_TARGET_WG = 512;  // ~2 workgroups per CU
+constexpr int KR_WAVES = 4;
+constexpr int KR_TILE = 32;        // output tile per workgroup
 
 constexpr int KG = 8;  // k per lane per group: a group covers 4 * KG = 32 k
 
@@ -78,12 +81,13 @@ template <bool AK, bool AV, bool BK, bool BV>
 __global__ __launch_bounds__(KR_THR) void k_kreduce(const float* __restrict__ a, const float* __restrict__ b,
                                                     int64_t K, int M, int N, int64_t chunk,
                                                     const float* __restrict__ c0, int64_t c0_ld, float* __restrict__ out) {
+  __shared__ float red[KR_WAVES - 1][16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int tiles_n = (N + 63) >> 6;
+  const int tiles_n = (N + KR_TILE - 1) / KR_TILE;
   const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
   const int64_t kbeg = (int64_t)blockIdx.y * chunk;
   const int64_t kend = min(K, kbeg + chunk);
-  const int mb = tm * 64 + (w >> 1) * 32, nb = tn * 64 + (w & 1) * 32;
+  const int mb = tm * KR_TILE, nb = tn * KR_TILE;
   const int lo = lane & 15, q = lane >> 4;
   int mrow[2], ncol[2];
 #pragma unroll
@@ -97,12 +101,14 @@ __global__ __launch_bounds__(KR_THR) void k_kreduce(const float* __restrict__ a,
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
+  // wave w takes the chunk's groups w, w + 4, ... (32 k each)
+  constexpr int GK = 4 * KG, STRIDE = KR_WAVES * GK;
   KrOps cur, nxt;
-  kr_operand<AK, AV>(cur.a, a, kbeg + KG * q, kend, mrow, M, K);
-  kr_operand<BK, BV>(cur.b, b, kbeg + KG * q, kend, ncol, N, K);
-  for (int64_t k0 = kbeg; k0 < kend; k0 += 4 * KG) {
-    kr_operand<AK, AV>(nxt.a, a, k0 + 4 * KG + KG * q, kend, mrow, M, K);
-    kr_operand<BK, BV>(nxt.b, b, k0 + 4 * KG + KG * q, kend, ncol, N, K);
+  kr_operand<AK, AV>(cur.a, a, kbeg + w * GK + KG * q, kend, mrow, M, K);
+  kr_operand<BK, BV>(cur.b, b, kbeg + w * GK + KG * q, kend, ncol, N, K);
+  for (int64_t k0 = kbeg + w * GK; k0 < kend; k0 += STRIDE) {
+    kr_operand<AK, AV>(nxt.a, a, k0 + STRIDE + KG * q, kend, mrow, M, K);
+    kr_operand<BK, BV>(nxt.b, b, k0 + STRIDE + KG * q, kend, ncol, N, K);
 #pragma unroll
     for (int e = 0; e < KG; ++e)
 #pragma unroll
@@ -112,6 +118,26 @@ __global__ __launch_bounds__(KR_THR) void k_kreduce(const float* __restrict__ a,
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.a[i][e], cur.b[j][e], acc[i][j], 0, 0, 0);
     cur = nxt;
   }
+
+  // the four waves' partial tiles summed in wave order (deterministic) through LDS
+  if (w > 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[w - 1][(2 * i + j) * 4 + r][lane] = acc[i][j][r];
+  }
+  __syncthreads();
+  if (w > 0) return;
+#pragma unroll
+  for (int u = 0; u < KR_WAVES - 1; ++u)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += red[u][(2 * i + j) * 4 + r][lane];
 
   // C/D layout: lane l holds rows 4 (l >> 4) + r, column l & 15 of each 16 x 16 tile.
   float* dst = gridDim.y > 1 ? out + (int64_t)blockIdx.y * M * N : out;
@@ -153,10 +179,12 @@ __global__ __launch_bounds__(256) void k_kreduce_sum(const float* __restrict__ p
 }
 
 void kr_plan(int64_t K, int M, int N, int64_t* nsplit, int64_t* chunk) {
-  const int64_t tiles = (int64_t)((M + 63) / 64) * ((N + 63) / 64);
+  const int64_t tiles = (int64_t)((M + KR_TILE - 1) / KR_TILE) * ((N + KR_TILE - 1) / KR_TILE);
   const int64_t groups = (K + 4 * KG - 1) / (4 * KG);
   int64_t ns = (KR_TARGET_WG + tiles - 1) / tiles;
-  ns = std::min(ns, std::max<int64_t>(1, groups / 2));  // at least 2 groups (64 k) per split
+  // at least 2 groups per wave (8 per workgroup) in a split: shorter K runs unsplit, its
+  // four waves' partials reduced in LDS, with no second launch
+  ns = std::min(ns, std::max<int64_t>(1, groups / (2 * KR_WAVES)));
   ns = std::max<int64_t>(1, ns);
   const int64_t gpc = std::max<int64_t>(1, (groups + ns - 1) / ns);
   *chunk = gpc * 4 * KG;
@@ -205,7 +233,7 @@ int kreduce_gemm(const float* A, int a_kmajor, const float* B, int b_kmajor, int
   if (ns > 1 && !ws) return set_error(REGCN_EINVAL, "kreduce_gemm needs a workspace of %zu floats",
                                       kreduce_workspace_floats(K, M, N));
   if (ns > 65535) return set_error(REGCN_EINVAL, "kreduce_gemm: too many K splits");
-  const dim3 grid((unsigned)(((M + 63) / 64) * ((N + 63) / 64)), (unsigned)ns);
+  const dim3 grid((unsigned)(((M + KR_TILE - 1) / KR_TILE) * ((N + KR_TILE - 1) / KR_TILE)), (unsigned)ns);
   float* dst = ns > 1 ? ws : out;
   const int am = kr_mode(a_kmajor, A, K), bm = kr_mode(b_kmajor, B, K);
   if (am == 0) kr_launch_b<true, false>(bm, grid, st, A, B, K, M, N, chunk, C0, c0_ld, dst);
