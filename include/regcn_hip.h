@@ -142,7 +142,8 @@ size_t regcn_kreduce_workspace_floats(int64_t K, int32_t M, int32_t N);
 int regcn_kreduce_gemm_f32(const float* a, int32_t a_kmajor, const float* b, int32_t b_kmajor, int64_t K, int32_t M,
                            int32_t N, const float* c0, int64_t c0_ld, float* out, float* workspace, void* stream);
 /* Fused elementwise layer tail / time gate of the training path, forward and backward (V x d,
- * d % 4 == 0, contiguous, 16-B aligned):
+ * d % 4 == 0, contiguous, 16-B aligned; lx / ex / d_lx / d_ex rows loop_ld floats apart,
+ * e.g. the two halves of one V x 2d product x [W_loop | W_evolve] with loop_ld = 2d):
  *   a = clamp(agg, +-10) [CLAMP_IN]; a += pos[v] ? lx : ex [lx != NULL];
  *   g = sigmoid(z + bias[col]), a = g a + (1 - g) p [z != NULL; bias nullable];
  *   a = clamp(a, +-10) [CLAMP_OUT]; a = a > 0 ? a : slope a [LEAKY].
@@ -153,8 +154,8 @@ int regcn_kreduce_gemm_f32(const float* a, int32_t a_kmajor, const float* b, int
 #define REGCN_TAIL_CLAMP_IN 1
 #define REGCN_TAIL_CLAMP_OUT 2
 #define REGCN_TAIL_LEAKY 4
-int regcn_tail_f32(const float* agg, const float* lx, const float* ex, const uint8_t* pos, const float* z,
-                   const float* bias, const float* p, int64_t V, int32_t d, int32_t flags, float slope,
+int regcn_tail_f32(const float* agg, const float* lx, const float* ex, int64_t loop_ld, const uint8_t* pos,
+                   const float* z, const float* bias, const float* p, int64_t V, int32_t d, int32_t flags, float slope,
                    const float* grad_out, float* out, float* d_agg, float* d_lx, float* d_ex, float* d_z, float* d_p,
                    void* stream);
 

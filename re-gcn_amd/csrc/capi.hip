@@ -123,11 +123,11 @@ int regcn_kreduce_gemm_f32(const float* a, int32_t a_kmajor, const float* b, int
   return kreduce_gemm(a, a_kmajor, b, b_kmajor, K, M, N, c0, c0_ld, out, workspace, ST(s));
 }
 
-int regcn_tail_f32(const float* agg, const float* lx, const float* ex, const uint8_t* pos, const float* z,
-                   const float* bias, const float* p, int64_t V, int32_t d, int32_t flags, float slope,
+int regcn_tail_f32(const float* agg, const float* lx, const float* ex, int64_t loop_ld, const uint8_t* pos,
+                   const float* z, const float* bias, const float* p, int64_t V, int32_t d, int32_t flags, float slope,
                    const float* grad_out, float* out, float* d_agg, float* d_lx, float* d_ex, float* d_z, float* d_p,
                    void* s) {
-  TailArgs t{agg, lx, ex, z, bias, p, grad_out, pos, out, d_agg, d_lx, d_ex, d_z, d_p, V, d, flags, slope};
+  TailArgs t{agg, lx, ex, z, bias, p, grad_out, pos, out, d_agg, d_lx, d_ex, d_z, d_p, V, loop_ld, d, flags, slope};
   return tail(t, grad_out != nullptr, ST(s));
 }
 

@@ -279,7 +279,7 @@ struct TailArgs {
   const float *agg, *lx, *ex, *z, *bias, *p, *gy;
   const uint8_t* pos;
   float *out, *dagg, *dlx, *dex, *dz, *dp;
-  int64_t V;
+  int64_t V, loop_ld;
   int d, flags;
   float slope;
 };

@@ -4,6 +4,8 @@
 //
 //   a = clamp(agg, -10, 10)                     [CLAMP_IN]   hyperbolic_layers.py:296 / :672
 //   a = a + (pos[v] ? lx : ex)                  [lx != 0]    self / evolve loop :273-280
+//                                               (lx, ex rows loop_ld apart: the two halves
+//                                                of one x [W_loop | W_evolve] product)
 //   g = sigmoid(z + bias); a = g a + (1 - g) p  [z != 0]     skip gate :315-318, time gate
 //                                                            hyperbolic_model.py:852-860
 //   a = clamp(a, -10, 10)                       [CLAMP_OUT]  :319
@@ -38,7 +40,7 @@ __global__ __launch_bounds__(TAIL_THR) void k_tail(TailArgs t) {
     bool pos = false;
     if (t.lx) {
       pos = t.pos[v] != 0;
-      lx = *reinterpret_cast<const f4*>((pos ? t.lx : t.ex) + e0);
+      lx = *reinterpret_cast<const f4*>((pos ? t.lx : t.ex) + v * t.loop_ld + j0);
     }
     if (t.z) {
       z = *reinterpret_cast<const f4*>(t.z + e0);
@@ -83,8 +85,8 @@ __global__ __launch_bounds__(TAIL_THR) void k_tail(TailArgs t) {
       if (t.dagg) *reinterpret_cast<f4*>(t.dagg + e0) = dagg;
       if (t.lx) {
         const f4 zero = {0.f, 0.f, 0.f, 0.f};
-        if (t.dlx) *reinterpret_cast<f4*>(t.dlx + e0) = pos ? dl : zero;
-        if (t.dex) *reinterpret_cast<f4*>(t.dex + e0) = pos ? zero : dl;
+        if (t.dlx) *reinterpret_cast<f4*>(t.dlx + v * t.loop_ld + j0) = pos ? dl : zero;
+        if (t.dex) *reinterpret_cast<f4*>(t.dex + v * t.loop_ld + j0) = pos ? zero : dl;
       }
       if (t.z) {
         if (t.dz) *reinterpret_cast<f4*>(t.dz + e0) = dz;
@@ -181,6 +183,7 @@ int tail(const TailArgs& t, int backward, hipStream_t st) {
   if (t.V < 0 || t.d <= 0 || (t.d & 3)) return set_error(REGCN_EINVAL, "tail needs d %% 4 == 0 (d=%d)", t.d);
   if (!t.agg || (!backward && !t.out) || (backward && !t.gy)) return set_error(REGCN_EINVAL, "null pointer");
   if (t.lx && (!t.ex || !t.pos)) return set_error(REGCN_EINVAL, "tail: the self loop needs lx, ex and pos");
+  if (t.lx && (t.loop_ld < t.d || (t.loop_ld & 3))) return set_error(REGCN_EINVAL, "tail needs loop_ld >= d, loop_ld %% 4 == 0");
   if (t.z && !t.p) return set_error(REGCN_EINVAL, "tail: the gate needs z and p");
   const uintptr_t al = (uintptr_t)t.agg | (uintptr_t)t.lx | (uintptr_t)t.ex | (uintptr_t)t.z | (uintptr_t)t.p |
                        (uintptr_t)t.bias | (uintptr_t)t.gy | (uintptr_t)t.out | (uintptr_t)t.dagg | (uintptr_t)t.dlx |

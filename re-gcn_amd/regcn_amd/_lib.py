@@ -46,7 +46,7 @@ _SIGS = {
     "regcn_kreduce_workspace_floats": [_c_i64, _c_int, _c_int],
     "regcn_lorentz_centroid_f32": [P, P, _c_i64, _c_int, _c_f, _c_f, P, P, P, P, P],
     "regcn_givens_rotation_f32": [P, P, _c_i64, _c_int, P, P, P, P, P],
-    "regcn_tail_f32": [P, P, P, P, P, P, P, _c_i64, _c_int, _c_int, _c_f, P, P, P, P, P, P, P, P],
+    "regcn_tail_f32": [P, P, P, _c_i64, P, P, P, P, _c_i64, _c_int, _c_int, _c_f, P, P, P, P, P, P, P, P],
     "regcn_kreduce_gemm_f32": [P, _c_int, P, _c_int, _c_i64, _c_int, _c_int, P, _c_i64, P, P, P],
     "regcn_layer_tail_f32": [P, P, P, P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_int, _c_f, P, P, P, P],
     "regcn_timestep_f32": [P, P, P, P, P, P, P, _c_f, _c_f, _c_int, _c_int, _c_int, _c_int, _c_f, _c_f, P, P, P, P],

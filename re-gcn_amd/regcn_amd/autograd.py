@@ -426,11 +426,12 @@ def mm_weight(x, w):
 TAIL_CLAMP_IN, TAIL_CLAMP_OUT, TAIL_LEAKY = 1, 2, 4
 
 
-def _tail_torch(agg, lx, ex, pos, z, bias, p, flags, slope):
+def _tail_torch(agg, loop, pos, z, bias, p, flags, slope):
     """The op-by-op composition regcn_tail_f32 fuses (used where the kernel does not apply)."""
     a = torch.clamp(agg, -10.0, 10.0) if flags & TAIL_CLAMP_IN else agg
-    if lx is not None:
-        a = a + torch.where(pos.bool().unsqueeze(-1), lx, ex)
+    if loop is not None:
+        d = agg.shape[1]
+        a = a + torch.where(pos.bool().unsqueeze(-1), loop[:, :d], loop[:, d:])
     if z is not None:
         g = torch.sigmoid(z + bias if bias is not None else z)
         a = g * a + (1 - g) * p
@@ -441,45 +442,60 @@ def _tail_torch(agg, lx, ex, pos, z, bias, p, flags, slope):
     return a
 
 
+def _halves(t, d):
+    """(first, second) half-row pointers of a V x 2d tensor (None -> None, None)."""
+    if t is None:
+        return None, None
+    base = _lib.addr(t)
+    return ctypes.c_void_p(base), ctypes.c_void_p(base + 4 * d)
+
+
 class _Tail(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, agg, lx, ex, z, bias, p, pos, flags, slope):
+    def forward(ctx, agg, loop, z, bias, p, pos, flags, slope):
         agg = agg.contiguous()
-        lx, ex = (lx.contiguous(), ex.contiguous()) if lx is not None else (None, None)
+        d = agg.shape[1]
+        loop = loop.contiguous() if loop is not None else None
         z, p = (z.contiguous(), p.contiguous()) if z is not None else (None, None)
         bias = bias.contiguous() if bias is not None else None
         out = torch.empty_like(agg)
         f = _lib.fptr
-        _lib.call("regcn_tail_f32", f(agg, "agg"), f(lx), f(ex), _lib.dptr(pos, torch.uint8, "pos"), f(z), f(bias), f(p),
-                  agg.shape[0], agg.shape[1], flags, float(slope), None, f(out), None, None, None, None, None,
-                  _lib.stream())
-        ctx.save_for_backward(agg, lx, ex, z, bias, p, pos)
+        lx, ex = _halves(loop, d)
+        _lib.call("regcn_tail_f32", f(agg, "agg"), lx, ex, 2 * d, _lib.dptr(pos, torch.uint8, "pos"), f(z), f(bias),
+                  f(p), agg.shape[0], d, flags, float(slope), None, f(out), None, None, None, None, None, _lib.stream())
+        ctx.save_for_backward(agg, loop, z, bias, p, pos)
         ctx.flags, ctx.slope = flags, slope
         return out
 
     @staticmethod
     def backward(ctx, gy):
-        agg, lx, ex, z, bias, p, pos = ctx.saved_tensors
+        agg, loop, z, bias, p, pos = ctx.saved_tensors
+        d = agg.shape[1]
         gy = gy.contiguous()
         need = ctx.needs_input_grad
-        e = lambda t, i: torch.empty_like(t) if t is not None and (need[i] or (i == 3 and need[4])) else None
-        dagg, dlx, dex, dz, dp = e(agg, 0), e(lx, 1), e(ex, 2), e(z, 3), e(p, 5)
+        dagg = torch.empty_like(agg) if need[0] else None
+        dloop = torch.empty_like(loop) if loop is not None and need[1] else None
+        dz = torch.empty_like(z) if z is not None and (need[2] or need[3]) else None
+        dp = torch.empty_like(p) if p is not None and need[4] else None
         f = _lib.fptr
-        _lib.call("regcn_tail_f32", f(agg), f(lx), f(ex), _lib.dptr(pos, torch.uint8), f(z), f(bias), f(p),
-                  agg.shape[0], agg.shape[1], ctx.flags, float(ctx.slope), f(gy), None, f(dagg), f(dlx), f(dex),
-                  f(dz), f(dp), _lib.stream())
-        dbias = dz.sum(0) if bias is not None and need[4] else None
-        return dagg, dlx, dex, dz if need[3] else None, dbias, dp, None, None, None
+        lx, ex = _halves(loop, d)
+        dlx, dex = _halves(dloop, d)
+        _lib.call("regcn_tail_f32", f(agg), lx, ex, 2 * d, _lib.dptr(pos, torch.uint8), f(z), f(bias), f(p),
+                  agg.shape[0], d, ctx.flags, float(ctx.slope), f(gy), None, f(dagg), dlx, dex, f(dz), f(dp),
+                  _lib.stream())
+        dbias = dz.sum(0) if bias is not None and need[3] else None
+        return dagg, dloop, dz if need[2] else None, dbias, dp, None, None, None
 
 
-def tail(agg, lx=None, ex=None, pos=None, z=None, bias=None, p=None, flags=0, slope=0.0):
-    """clamp_in -> + (pos ? lx : ex) -> sigmoid(z + bias) gate with p -> clamp_out -> leaky,
-    one HIP launch forward and one backward (regcn_tail_f32).  pos: uint8 per row."""
-    ts = [t for t in (agg, lx, ex, z, bias, p) if t is not None]
+def tail(agg, loop=None, pos=None, z=None, bias=None, p=None, flags=0, slope=0.0):
+    """clamp_in -> + (pos ? loop[:, :d] : loop[:, d:]) -> sigmoid(z + bias) gate with p ->
+    clamp_out -> leaky, one HIP launch forward and one backward (regcn_tail_f32).
+    loop: V x 2d, the product x [W_loop | W_evolve]; pos: uint8 per row."""
+    ts = [t for t in (agg, loop, z, bias, p) if t is not None]
     if (agg.is_cuda and agg.dim() == 2 and agg.shape[1] % 4 == 0
             and all(t.dtype == torch.float32 for t in ts)):
-        return _Tail.apply(agg, lx, ex, z, bias, p, pos, flags, slope)
-    return _tail_torch(agg, lx, ex, pos, z, bias, p, flags, slope)
+        return _Tail.apply(agg, loop, z, bias, p, pos, flags, slope)
+    return _tail_torch(agg, loop, pos, z, bias, p, flags, slope)
 
 
 # ------------------------------------------------------------------ Givens rotation

@@ -29,18 +29,24 @@ def _pos_rows(g, device):
     return pos
 
 
+def _loop_product(x, layer):
+    """x [W_loop | W_evolve] (V x 2d): one GEMM forward, one for dx, one split-K for dW."""
+    return A.mm_weight(x, torch.cat([layer.loop_weight, layer.evolve_loop_weight], dim=1))
+
+
 def _layer_tail(layer, g, h_new, x, prev_h, c):
     """clamp -> + loop [-> skip blend] -> clamp -> rrelu -> dropout -> exp0
     (hyperbolic_layers.py:296-321, :672-694); everything up to rrelu is one fused launch
-    (A.tail), the loop's W_loop / W_evolve products (rows with / without in-edges) feed it."""
-    lx = ex = pos = z = bias = prev_t = None
+    (A.tail), fed by ONE product x [W_loop | W_evolve] (rows with / without in-edges pick a
+    half) instead of two."""
+    loop = pos = z = bias = prev_t = None
     if layer.self_loop:
-        lx, ex = A.mm_weight(x, layer.loop_weight), A.mm_weight(x, layer.evolve_loop_weight)
+        loop = _loop_product(x, layer)
         pos = _pos_rows(g, x.device)
     if layer.skip_connect and prev_h is not None:
         prev_t = A.log0(prev_h, c)
         z, bias = A.mm_weight(prev_t, layer.skip_weight), layer.skip_bias
-    h_new = A.tail(h_new, lx, ex, pos, z, bias, prev_t,
+    h_new = A.tail(h_new, loop, pos, z, bias, prev_t,
                    A.TAIL_CLAMP_IN | A.TAIL_CLAMP_OUT | A.TAIL_LEAKY, RRELU_SLOPE)
     if layer.dropout is not None:
         h_new = layer.dropout(h_new)
@@ -138,11 +144,10 @@ def euclid_layer(layer, g, h, rel):
     norm sum_e (h_src + rel) W_n + loop, rrelu, dropout."""
     zero_r = torch.zeros(h.shape[0], device=h.device)
     node = A.mm_weight(A.union_aggregate(h, zero_r, rel.contiguous(), g, 0.0), layer.weight_neighbor)
-    lx = ex = pos = None
+    loop = pos = None
     if layer.self_loop:
-        lx, ex = A.mm_weight(h, layer.loop_weight), A.mm_weight(h, layer.evolve_loop_weight)
-        pos = _pos_rows(g, h.device)
-    node = A.tail(node, lx, ex, pos, flags=A.TAIL_LEAKY, slope=RRELU_SLOPE)
+        loop, pos = _loop_product(h, layer), _pos_rows(g, h.device)
+    node = A.tail(node, loop, pos, flags=A.TAIL_LEAKY, slope=RRELU_SLOPE)
     if layer.dropout is not None:
         node = layer.dropout(node)
     return node

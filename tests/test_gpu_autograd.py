@@ -311,14 +311,15 @@ def test_fused_tail(case):
     V, d = 1037, 200
     g = torch.Generator(device="cpu").manual_seed(11)
     mk = lambda s=1.0: (s * torch.randn(V, d, generator=g)).to(DEV).requires_grad_(True)
-    agg, lx, ex, z, p = mk(8.0), mk(4.0), mk(4.0), mk(2.0), mk(6.0)
+    agg, z, p = mk(8.0), mk(2.0), mk(6.0)
+    loop = (4.0 * torch.randn(V, 2 * d, generator=g)).to(DEV).requires_grad_(True)
     bias = (0.3 * torch.randn(d, generator=g)).to(DEV).requires_grad_(True)
     pos = (torch.rand(V, generator=g) > 0.4).to(torch.uint8).to(DEV)
     slope = (1.0 / 8 + 1.0 / 3) / 2
-    args = {"layer_skip": (agg, lx, ex, pos, z, bias, p, 7, slope), "layer": (agg, lx, ex, pos, None, None, None, 7, slope),
-            "time_gate": (agg, None, None, None, z, bias, p, 1, 0.0), "euclid": (agg, lx, ex, pos, None, None, None, 4, slope)}[case]
+    args = {"layer_skip": (agg, loop, pos, z, bias, p, 7, slope), "layer": (agg, loop, pos, None, None, None, 7, slope),
+            "time_gate": (agg, None, None, z, bias, p, 1, 0.0), "euclid": (agg, loop, pos, None, None, None, 4, slope)}[case]
     gy = torch.randn(V, d, generator=g).to(DEV)
-    ins = [t for t in args[:7] if t is not None and t.dtype == torch.float32]
+    ins = [t for t in args[:6] if t is not None and t.dtype == torch.float32]
     out = A.tail(*args)
     got = torch.autograd.grad(out, ins, gy)
     ref_out = A._tail_torch(*args)
