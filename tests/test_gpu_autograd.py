@@ -256,10 +256,12 @@ def test_transposed_lists():
                                           (200, 128, 200, False, False), (201, 108, 100, False, False),
                                           (10000, 128, 200, False, False), (7128, 1, 200, True, True),
                                           (1, 3, 5, True, True), (37, 65, 129, False, True), (0, 16, 16, True, True),
-                                          (100000, 16, 48, True, False)])
+                                          (100000, 16, 48, True, False), (3001, 204, 100, True, True),
+                                          (7128, 200, 400, True, True), (100, 36, 52, True, True)])
 def test_kreduce_mm(K, M, N, ak, bk):
     """regcn_kreduce_gemm_f32 (split-K MFMA, deterministic partial sum) against fp64 torch:
     every A/B layout, the float4 R-major reads (K % 4 == 0) and their scalar fallback (K odd),
+    both-K-major products with odd K and partial tiles,
     ragged M/N, K = 0, a K long enough for many splits; no c0, a full c0, a bias row."""
     g = torch.Generator(device="cpu").manual_seed(K * 7 + M + N)
     a = torch.randn((K, M) if ak else (M, K), generator=g)
