@@ -1,9 +1,9 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_training.py tests/test_gpu_autograd.py tests/test_gpu_cli.py tests/test_gpu_parity.py -q -x --timeout 200 --timeout-method thread > gpurun_out/pt.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pt.log; exit 1; }
-tail -1 gpurun_out/pt.log
-for v in "--graph" ""; do
-timeout -k 10 300 python tools/trainbench.py --no-cpu $v > gpurun_out/tb.log 2>&1 || { echo "failed $v"; tail -30 gpurun_out/tb.log; exit 1; }
-grep '^{' gpurun_out/tb.log
-done
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pt_all.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/pt_all.log; exit 1; }
+tail -1 gpurun_out/pt_all.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
+echo smoke ok
+timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench.log; exit 1; }
+grep '^{' gpurun_out/bench.log | cut -c1-200
