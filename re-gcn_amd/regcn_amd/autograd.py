@@ -17,6 +17,7 @@ with the gradients torch autograd would compute through the reference's op seque
 The curvature is a constant here (a learned curvature's gradient is not built).
 """
 import ctypes
+import functools
 
 import torch
 
@@ -338,6 +339,11 @@ def hyp_ce_loss(q, cand, target, c, bias=None, scale=None, margin=None):
 
 
 # ------------------------------------------------------------------ long-K products
+@functools.lru_cache(maxsize=4096)
+def _kreduce_ws(K, M, N):
+    return max(1, _lib.lib().regcn_kreduce_workspace_floats(K, M, N))
+
+
 def kreduce_mm(a, b, a_kmajor, c0=None, b_kmajor=True):
     """(a^T if a_kmajor else a) @ (b if b_kmajor else b^T) (+ c0: M x N, or a length-N bias
     row) on regcn_kreduce_gemm_f32: K split over workgroups, partials summed in a fixed order.
@@ -358,7 +364,7 @@ def kreduce_mm(a, b, a_kmajor, c0=None, b_kmajor=True):
             c0_ld = N
         else:
             c0, c0_ld = c0.expand(M, N).contiguous(), N
-    ws = torch.empty(max(1, _lib.lib().regcn_kreduce_workspace_floats(K, M, N)), device=b.device, dtype=torch.float32)
+    ws = torch.empty(_kreduce_ws(K, M, N), device=b.device, dtype=torch.float32)
     f = _lib.fptr
     _lib.call("regcn_kreduce_gemm_f32", f(a, "a"), 1 if a_kmajor else 0, f(b, "b"), 1 if b_kmajor else 0, K, M, N,
               f(c0), c0_ld, f(out), f(ws), _lib.stream())
