@@ -266,21 +266,27 @@ __device__ __forceinline__ void wfrag_outer_acc(WFrag<S>& acc, f4 xs, f4 dm) {  
   }
 }
 
-// Raw Lorentz sums (training forward): S0[v] = sum_e L0_e, Sv[v] = sum_e Li_e, edge order.
+// Raw Lorentz sums (training forward): S0[v] = sum_e L0_e, Sv[v] = sum_e Li_e.  One
+// workgroup per destination row, its 4 waves on contiguous quarters of the row's edges,
+// combined in wave order: a hub row's serial chain (one wave reduction per edge) is a
+// quarter as long as with one wave per row.
 template <int S>
 __global__ __launch_bounds__(256) void k_lorentz_raw(const float* __restrict__ x, const float* __restrict__ rel,
                                                      const float* __restrict__ W, const int* __restrict__ rowptr,
                                                      const int* __restrict__ col_src, const int* __restrict__ col_type,
                                                      int V, int d, int wstride, Curv k, float* __restrict__ S0,
                                                      float* __restrict__ Sv) {
-  const int lane = threadIdx.x & 63, col = lane * 4;
+  __shared__ f4 part[4][64];
+  __shared__ float part0[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, col = lane * 4;
   const bool active = col < d;
   const int colc = min(col, d - 4);
-  const int nw = gridDim.x * (blockDim.x >> 6);
-  for (int v = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); v < V; v += nw) {
+  for (int v = blockIdx.x; v < V; v += gridDim.x) {
+    const int b = rowptr[v], e = rowptr[v + 1];
+    const int q = (e - b + 3) / 4;
     f4 acc = {0.f, 0.f, 0.f, 0.f};
     float acc0 = 0.f;
-    for (int p = rowptr[v]; p < rowptr[v + 1]; ++p) {
+    for (int p = b + wv * q; p < min(e, b + (wv + 1) * q); ++p) {
       const int u = col_src[p], t = col_type[p];
       WFrag<S> wf;
       wf.load(W + (int64_t)t * wstride, colc);
@@ -291,8 +297,14 @@ __global__ __launch_bounds__(256) void k_lorentz_raw(const float* __restrict__ x
       acc0 += L.L0;
       acc += m * L.beta_phi;
     }
-    store4(Sv + (int64_t)v * d, col, d, acc);
-    if (lane == 0) S0[v] = acc0;
+    part[wv][lane] = acc;
+    if (lane == 0) part0[wv] = acc0;
+    __syncthreads();
+    if (wv == 0) {
+      store4(Sv + (int64_t)v * d, col, d, ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
+      if (lane == 0) S0[v] = ((part0[0] + part0[1]) + part0[2]) + part0[3];
+    }
+    __syncthreads();
   }
 }
 
@@ -312,7 +324,8 @@ __device__ __forceinline__ f4 lorentz_edge_dm(const float* __restrict__ x, const
   return active ? gv * bp + m * coef : f4{0.f, 0.f, 0.f, 0.f};
 }
 
-// Source pass: dx[u] = sum over u's out-edges of blockdiag(W_t)^T dm_e.
+// Source pass: dx[u] = sum over u's out-edges of blockdiag(W_t)^T dm_e; one workgroup per
+// source row, 4 waves on contiguous quarters of its out-edges, combined in wave order.
 template <int S>
 __global__ __launch_bounds__(256) void k_lorentz_bwd_src(const float* __restrict__ x, const float* __restrict__ rel,
                                                          const float* __restrict__ W, const int* __restrict__ sptr,
@@ -320,21 +333,26 @@ __global__ __launch_bounds__(256) void k_lorentz_bwd_src(const float* __restrict
                                                          const int* __restrict__ col_type, const float* __restrict__ g0,
                                                          const float* __restrict__ gS, int V, int d, int wstride,
                                                          Curv k, float* __restrict__ dx) {
-  const int lane = threadIdx.x & 63, col = lane * 4;
+  __shared__ f4 part[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, col = lane * 4;
   const bool active = col < d;
   const int colc = min(col, d - 4);
-  const int nw = gridDim.x * (blockDim.x >> 6);
-  for (int u = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < V; u += nw) {
+  for (int u = blockIdx.x; u < V; u += gridDim.x) {
     const f4 xs = *reinterpret_cast<const f4*>(x + (int64_t)u * d + colc);
+    const int b = sptr[u], e = sptr[u + 1];
+    const int q = (e - b + 3) / 4;
     f4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int i = sptr[u]; i < sptr[u + 1]; ++i) {
+    for (int i = b + wv * q; i < min(e, b + (wv + 1) * q); ++i) {
       const int p = sp[i], v = csr_dst[p], t = col_type[p];
       WFrag<S> wf;
       wf.load(W + (int64_t)t * wstride, colc);
       const f4 dm = lorentz_edge_dm<S>(x, rel, wf, xs, t, v, g0, gS, d, col, colc, active, k);
       acc += wfrag_apply_t<S>(wf, dm);
     }
-    store4(dx + (int64_t)u * d, col, d, acc);
+    part[wv][lane] = acc;
+    __syncthreads();
+    if (wv == 0) store4(dx + (int64_t)u * d, col, d, ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
+    __syncthreads();
   }
 }
 
@@ -446,7 +464,7 @@ int lorentz_raw(const float* x, const float* rel, const float* W, const int* row
   const int s = d / nb, ws = nb * s * s;
   if (!x || !rel || !W || !rowptr || !S0 || !Sv) return set_error(REGCN_EINVAL, "null pointer");
   const Curv k = make_curv(c);
-  const dim3 g(waves_grid(V)), b(256);
+  const dim3 g((unsigned)std::max(1, std::min(V, 65535))), b(256);  // one workgroup per row
   if (s == 1) hipLaunchKernelGGL(k_lorentz_raw<1>, g, b, 0, st, x, rel, W, rowptr, col_src, col_type, V, d, ws, k, S0, Sv);
   else if (s == 2) hipLaunchKernelGGL(k_lorentz_raw<2>, g, b, 0, st, x, rel, W, rowptr, col_src, col_type, V, d, ws, k, S0, Sv);
   else if (s == 4) hipLaunchKernelGGL(k_lorentz_raw<4>, g, b, 0, st, x, rel, W, rowptr, col_src, col_type, V, d, ws, k, S0, Sv);
@@ -463,7 +481,7 @@ int lorentz_bwd(const regcn_edge_bwd_desc* a, int nb, float c, hipStream_t st) {
   if (!a->x || !a->rel || !a->W || !a->G || !a->G0 || !a->dx || !a->drel || !a->dW)
     return set_error(REGCN_EINVAL, "null pointer");
   const Curv k = make_curv(c);
-  const dim3 g(waves_grid(V)), gt(std::max(1, std::min(R2, 65535))), b(256);
+  const dim3 g((unsigned)std::max(1, std::min(V, 65535))), gt(std::max(1, std::min(R2, 65535))), b(256);
 #define LB(SS)                                                                                                   \
   {                                                                                                              \
   hipLaunchKernelGGL(k_lorentz_bwd_src<SS>, g, b, 0, st, a->x, a->rel, a->W, a->sptr, a->sp, a->csr_dst,       \
