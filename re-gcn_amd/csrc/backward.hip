@@ -267,23 +267,24 @@ __device__ __forceinline__ void wfrag_outer_acc(WFrag<S>& acc, f4 xs, f4 dm) {  
 }
 
 // Raw Lorentz sums (training forward): S0[v] = sum_e L0_e, Sv[v] = sum_e Li_e.  One
-// workgroup per destination row, its 4 waves on contiguous quarters of the row's edges,
-// combined in wave order: a hub row's serial chain (one wave reduction per edge) is a
-// quarter as long as with one wave per row.
+// workgroup per destination row, its LW waves on contiguous slices of the row's edges,
+// combined in wave order: a hub row's serial chain (one wave reduction per edge) is 1/LW as
+// long as with one wave per row.
+constexpr int LW = 8;
 template <int S>
-__global__ __launch_bounds__(256) void k_lorentz_raw(const float* __restrict__ x, const float* __restrict__ rel,
+__global__ __launch_bounds__(64 * LW) void k_lorentz_raw(const float* __restrict__ x, const float* __restrict__ rel,
                                                      const float* __restrict__ W, const int* __restrict__ rowptr,
                                                      const int* __restrict__ col_src, const int* __restrict__ col_type,
                                                      int V, int d, int wstride, Curv k, float* __restrict__ S0,
                                                      float* __restrict__ Sv) {
-  __shared__ f4 part[4][64];
-  __shared__ float part0[4];
+  __shared__ f4 part[LW][64];
+  __shared__ float part0[LW];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, col = lane * 4;
   const bool active = col < d;
   const int colc = min(col, d - 4);
   for (int v = blockIdx.x; v < V; v += gridDim.x) {
     const int b = rowptr[v], e = rowptr[v + 1];
-    const int q = (e - b + 3) / 4;
+    const int q = (e - b + LW - 1) / LW;
     f4 acc = {0.f, 0.f, 0.f, 0.f};
     float acc0 = 0.f;
     for (int p = b + wv * q; p < min(e, b + (wv + 1) * q); ++p) {
@@ -301,8 +302,15 @@ __global__ __launch_bounds__(256) void k_lorentz_raw(const float* __restrict__ x
     if (lane == 0) part0[wv] = acc0;
     __syncthreads();
     if (wv == 0) {
-      store4(Sv + (int64_t)v * d, col, d, ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
-      if (lane == 0) S0[v] = ((part0[0] + part0[1]) + part0[2]) + part0[3];
+      f4 sv = part[0][lane];
+      float s0 = part0[0];
+#pragma unroll
+      for (int w = 1; w < LW; ++w) {
+        sv += part[w][lane];
+        s0 += part0[w];
+      }
+      store4(Sv + (int64_t)v * d, col, d, sv);
+      if (lane == 0) S0[v] = s0;
     }
     __syncthreads();
   }
@@ -325,22 +333,22 @@ __device__ __forceinline__ f4 lorentz_edge_dm(const float* __restrict__ x, const
 }
 
 // Source pass: dx[u] = sum over u's out-edges of blockdiag(W_t)^T dm_e; one workgroup per
-// source row, 4 waves on contiguous quarters of its out-edges, combined in wave order.
+// source row, LW waves on contiguous slices of its out-edges, combined in wave order.
 template <int S>
-__global__ __launch_bounds__(256) void k_lorentz_bwd_src(const float* __restrict__ x, const float* __restrict__ rel,
+__global__ __launch_bounds__(64 * LW) void k_lorentz_bwd_src(const float* __restrict__ x, const float* __restrict__ rel,
                                                          const float* __restrict__ W, const int* __restrict__ sptr,
                                                          const int* __restrict__ sp, const int* __restrict__ csr_dst,
                                                          const int* __restrict__ col_type, const float* __restrict__ g0,
                                                          const float* __restrict__ gS, int V, int d, int wstride,
                                                          Curv k, float* __restrict__ dx) {
-  __shared__ f4 part[4][64];
+  __shared__ f4 part[LW][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, col = lane * 4;
   const bool active = col < d;
   const int colc = min(col, d - 4);
   for (int u = blockIdx.x; u < V; u += gridDim.x) {
     const f4 xs = *reinterpret_cast<const f4*>(x + (int64_t)u * d + colc);
     const int b = sptr[u], e = sptr[u + 1];
-    const int q = (e - b + 3) / 4;
+    const int q = (e - b + LW - 1) / LW;
     f4 acc = {0.f, 0.f, 0.f, 0.f};
     for (int i = b + wv * q; i < min(e, b + (wv + 1) * q); ++i) {
       const int p = sp[i], v = csr_dst[p], t = col_type[p];
@@ -351,7 +359,12 @@ __global__ __launch_bounds__(256) void k_lorentz_bwd_src(const float* __restrict
     }
     part[wv][lane] = acc;
     __syncthreads();
-    if (wv == 0) store4(dx + (int64_t)u * d, col, d, ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
+    if (wv == 0) {
+      f4 sx = part[0][lane];
+#pragma unroll
+      for (int w = 1; w < LW; ++w) sx += part[w][lane];
+      store4(dx + (int64_t)u * d, col, d, sx);
+    }
     __syncthreads();
   }
 }
@@ -464,7 +477,7 @@ int lorentz_raw(const float* x, const float* rel, const float* W, const int* row
   const int s = d / nb, ws = nb * s * s;
   if (!x || !rel || !W || !rowptr || !S0 || !Sv) return set_error(REGCN_EINVAL, "null pointer");
   const Curv k = make_curv(c);
-  const dim3 g((unsigned)std::max(1, std::min(V, 65535))), b(256);  // one workgroup per row
+  const dim3 g((unsigned)std::max(1, std::min(V, 65535))), b(64 * LW);  // one workgroup per row
   if (s == 1) hipLaunchKernelGGL(k_lorentz_raw<1>, g, b, 0, st, x, rel, W, rowptr, col_src, col_type, V, d, ws, k, S0, Sv);
   else if (s == 2) hipLaunchKernelGGL(k_lorentz_raw<2>, g, b, 0, st, x, rel, W, rowptr, col_src, col_type, V, d, ws, k, S0, Sv);
   else if (s == 4) hipLaunchKernelGGL(k_lorentz_raw<4>, g, b, 0, st, x, rel, W, rowptr, col_src, col_type, V, d, ws, k, S0, Sv);
@@ -484,7 +497,7 @@ int lorentz_bwd(const regcn_edge_bwd_desc* a, int nb, float c, hipStream_t st) {
   const dim3 g((unsigned)std::max(1, std::min(V, 65535))), gt(std::max(1, std::min(R2, 65535))), b(256);
 #define LB(SS)                                                                                                   \
   {                                                                                                              \
-  hipLaunchKernelGGL(k_lorentz_bwd_src<SS>, g, b, 0, st, a->x, a->rel, a->W, a->sptr, a->sp, a->csr_dst,       \
+  hipLaunchKernelGGL(k_lorentz_bwd_src<SS>, g, dim3(64 * LW), 0, st, a->x, a->rel, a->W, a->sptr, a->sp, a->csr_dst,       \
                      a->col_type, a->G0, a->G, V, d, ws, k, a->dx);                                              \
   hipLaunchKernelGGL(k_lorentz_bwd_type<SS>, gt, b, 0, st, a->x, a->rel, a->W, a->tptr, a->tp, a->csr_dst,     \
                      a->col_src, a->G0, a->G, R2, d, ws, k, a->drel, a->dW);                               \
