@@ -7,3 +7,5 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 echo smoke ok
 timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench.log; exit 1; }
 grep '^{' gpurun_out/bench.log | cut -c1-200
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/tprof -o run -- python tools/trainbench.py --no-cpu --graph --steps 40 > gpurun_out/tprof.log 2>&1 || { echo "failed"; tail -20 gpurun_out/tprof.log; exit 1; }
+grep '^{' gpurun_out/tprof.log | cut -c 190-
