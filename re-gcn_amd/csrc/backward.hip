@@ -129,62 +129,91 @@ __global__ __launch_bounds__(256) void k_rowmap_bwd(const float* __restrict__ x,
 }
 
 // ------------------------------------------------------------------------- union backward
+// Rows whose edges are walked serially (a Zipf hub has hundreds) run one workgroup per row,
+// its LW waves on contiguous slices of the edges, partials combined in wave order.
+constexpr int LW = 8;
+
 // Pass 1, destination rows: per in-edge (CSR position p) the weight w_p and
 // q_p = (G[v] norm[v] . (x[u] + rel[t])) dw_p/dr_u; the destination's radius gradient
 // -sum q_p goes to drd[v].
-__global__ __launch_bounds__(256) void k_union_bwd_dst(const float* __restrict__ x, const float* __restrict__ radius,
-                                                       const float* __restrict__ rel, const float* __restrict__ norm,
-                                                       const int* __restrict__ rowptr, const int* __restrict__ col_src,
-                                                       const int* __restrict__ col_type, const float* __restrict__ G,
-                                                       int V, int d, float gamma, float* __restrict__ we,
-                                                       float* __restrict__ qe, float* __restrict__ drd) {
-  const int lane = threadIdx.x & 63, col = lane * 4;
-  const int nw = gridDim.x * (blockDim.x >> 6);
-  for (int v = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); v < V; v += nw) {
+__global__ __launch_bounds__(64 * LW) void k_union_bwd_dst(const float* __restrict__ x, const float* __restrict__ radius,
+                                                           const float* __restrict__ rel, const float* __restrict__ norm,
+                                                           const int* __restrict__ rowptr, const int* __restrict__ col_src,
+                                                           const int* __restrict__ col_type, const float* __restrict__ G,
+                                                           int V, int d, float gamma, float* __restrict__ we,
+                                                           float* __restrict__ qe, float* __restrict__ drd) {
+  __shared__ float part[LW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, col = lane * 4;
+  for (int v = blockIdx.x; v < V; v += gridDim.x) {
     const int b = rowptr[v], e = rowptr[v + 1];
+    const int q = (e - b + LW - 1) / LW;
     float acc = 0.f;
     if (e > b) {
       const f4 gv = load4(G + (int64_t)v * d, col, d) * norm[v];
       const float rv = radius[v];
-      for (int p = b; p < e; ++p) {
+      for (int p = b + wv * q; p < min(e, b + (wv + 1) * q); ++p) {
         const int u = col_src[p], t = col_type[p];
         const f4 m = load4(x + (int64_t)u * d, col, d) + load4(rel + (int64_t)t * d, col, d);
         const float s = wave_sum(dot4(gv, m));
         const float diff = radius[u] - rv;
         const float w = expf(-gamma * fabsf(diff));
         const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-        const float q = s * (-gamma * w * sg);
+        const float qq = s * (-gamma * w * sg);
         if (lane == 0) {
           we[p] = w;
-          qe[p] = q;
+          qe[p] = qq;
         }
-        acc -= q;
+        acc -= qq;
       }
     }
-    if (lane == 0) drd[v] = acc;
+    if (lane == 0) part[wv] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = part[0];
+#pragma unroll
+      for (int w = 1; w < LW; ++w) t += part[w];
+      drd[v] = t;
+    }
+    __syncthreads();
   }
 }
 
 // Pass 2, source rows (src-sorted positions sp[sptr[u] .. sptr[u+1])):
 // dx[u] = sum_p w_p norm[dst] G[dst];  dradius[u] = drd[u] + sum_p q_p.
-__global__ __launch_bounds__(256) void k_union_bwd_src(const float* __restrict__ norm, const int* __restrict__ sptr,
-                                                       const int* __restrict__ sp, const int* __restrict__ csr_dst,
-                                                       const float* __restrict__ G, const float* __restrict__ we,
-                                                       const float* __restrict__ qe, const float* __restrict__ drd,
-                                                       int V, int d, float* __restrict__ dx,
-                                                       float* __restrict__ dradius) {
-  const int lane = threadIdx.x & 63, col = lane * 4;
-  const int nw = gridDim.x * (blockDim.x >> 6);
-  for (int u = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < V; u += nw) {
+__global__ __launch_bounds__(64 * LW) void k_union_bwd_src(const float* __restrict__ norm, const int* __restrict__ sptr,
+                                                           const int* __restrict__ sp, const int* __restrict__ csr_dst,
+                                                           const float* __restrict__ G, const float* __restrict__ we,
+                                                           const float* __restrict__ qe, const float* __restrict__ drd,
+                                                           int V, int d, float* __restrict__ dx,
+                                                           float* __restrict__ dradius) {
+  __shared__ f4 part[LW][64];
+  __shared__ float partq[LW];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, col = lane * 4;
+  for (int u = blockIdx.x; u < V; u += gridDim.x) {
+    const int b = sptr[u], e = sptr[u + 1];
+    const int q = (e - b + LW - 1) / LW;
     f4 acc = {0.f, 0.f, 0.f, 0.f};
     float qs = 0.f;
-    for (int i = sptr[u]; i < sptr[u + 1]; ++i) {
+    for (int i = b + wv * q; i < min(e, b + (wv + 1) * q); ++i) {
       const int p = sp[i], v = csr_dst[p];
       acc += load4(G + (int64_t)v * d, col, d) * (we[p] * norm[v]);
       qs += qe[p];
     }
-    store4(dx + (int64_t)u * d, col, d, acc);
-    if (lane == 0) dradius[u] = drd[u] + qs;
+    part[wv][lane] = acc;
+    if (lane == 0) partq[wv] = qs;
+    __syncthreads();
+    if (wv == 0) {
+      f4 sx = part[0][lane];
+      float sq = partq[0];
+#pragma unroll
+      for (int w = 1; w < LW; ++w) {
+        sx += part[w][lane];
+        sq += partq[w];
+      }
+      store4(dx + (int64_t)u * d, col, d, sx);
+      if (lane == 0) dradius[u] = drd[u] + sq;
+    }
+    __syncthreads();
   }
 }
 
@@ -270,7 +299,6 @@ __device__ __forceinline__ void wfrag_outer_acc(WFrag<S>& acc, f4 xs, f4 dm) {  
 // workgroup per destination row, its LW waves on contiguous slices of the row's edges,
 // combined in wave order: a hub row's serial chain (one wave reduction per edge) is 1/LW as
 // long as with one wave per row.
-constexpr int LW = 8;
 template <int S>
 __global__ __launch_bounds__(64 * LW) void k_lorentz_raw(const float* __restrict__ x, const float* __restrict__ rel,
                                                      const float* __restrict__ W, const int* __restrict__ rowptr,
@@ -460,9 +488,10 @@ int union_bwd(const regcn_edge_bwd_desc* a, float gamma, hipStream_t st) {
   float* qe = we + a->E;
   float* drd = qe + a->E;
   const dim3 b(256);
-  hipLaunchKernelGGL(k_union_bwd_dst, dim3(waves_grid(V)), b, 0, st, a->x, a->radius, a->rel, a->norm, a->rowptr,
+  const dim3 gr((unsigned)std::max(1, std::min(V, 65535))), bl(64 * LW);  // one workgroup per row
+  hipLaunchKernelGGL(k_union_bwd_dst, gr, bl, 0, st, a->x, a->radius, a->rel, a->norm, a->rowptr,
                      a->col_src, a->col_type, a->G, V, d, gamma, we, qe, drd);
-  hipLaunchKernelGGL(k_union_bwd_src, dim3(waves_grid(V)), b, 0, st, a->norm, a->sptr, a->sp, a->csr_dst, a->G, we, qe,
+  hipLaunchKernelGGL(k_union_bwd_src, gr, bl, 0, st, a->norm, a->sptr, a->sp, a->csr_dst, a->G, we, qe,
                      drd, V, d, a->dx, a->dradius);
   hipLaunchKernelGGL(k_union_bwd_type, dim3(std::max(1, std::min(R2, 65535))), b, 0, st, a->norm, a->tptr, a->tp,
                      a->csr_dst, a->G, we, R2, d, a->drel);
