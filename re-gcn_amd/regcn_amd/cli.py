@@ -375,6 +375,9 @@ def main(argv=None):
     if not args.test and (args.learn_curvature or args.plus_relation_specific_curvature):
         raise SystemExit("training with --learn-curvature / --plus-relation-specific-curvature is not supported "
                          "in this build (their gradients are not built)")
+    if not args.test and args.hip_graph and args.decoder == "murp":
+        raise SystemExit("--hip-graph: the MuRP decoder's training step is not capturable yet "
+                         "(a host-synchronising op inside the step); train it without --hip-graph")
     if args.radius_msg_gamma < 0:
         raise ValueError("--radius-msg-gamma must be non-negative (use 0 to disable the penalty)")
     if not 0.0 <= args.radius_anchor_beta <= 1.0:

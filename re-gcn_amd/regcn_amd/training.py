@@ -97,7 +97,9 @@ def relation_context(x, g, R2):
         cnt = wk["rel_count"].long()
         rel_of = torch.repeat_interleave(torch.arange(R2, device=x.device), cnt)
         g.__dict__["_rel_of_item"] = rel_of
-    out = out.index_add(0, rel_of, x.index_select(0, idx.long()))
+    # advanced indexing + index_put(accumulate): sort-based, so forward and backward are
+    # deterministic (index_select / index_add accumulate with atomics)
+    out = out.index_put((rel_of,), x[idx.long()], accumulate=True)
     return out / torch.clamp(wk["rel_count"], min=1.0).unsqueeze(-1)
 
 

@@ -120,14 +120,17 @@ def test_cli_training_replicas(tmp_path):
     assert "MRR raw" in r.stdout + r.stderr
 
 
-def test_cli_training_hip_graph_matches_eager(tmp_path):
+@pytest.mark.parametrize("encoder,decoder", [("lgcn", "roth"), ("hyperbolic_uvrgcn", "atth")])
+def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder):
     """--hip-graph (each sample's whole step captured after its first run and replayed:
     training.GraphedSteps) trains the same model as the eager loop: dropout off, the same
-    seeds and sample order; epoch losses agree to 5e-4 and every parameter tensor to 2e-3 in
-    relative norm (epochs 2-3 are replays)."""
+    seeds and sample order; epoch losses bit for bit and every parameter tensor to 1e-6 in
+    relative norm (epochs 2-3 are replays; measured: bitwise equal).  Not covered: ConvTransE
+    (its eager runs differ in the 6th digit: MIOpen convolution), MuRP (not capturable; the
+    CLI refuses --hip-graph with it)."""
     import random
     from regcn_amd import cli, ranking
-    common = ["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0", "--encoder", "lgcn", "--decoder", "roth",
+    common = ["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0", "--encoder", encoder, "--decoder", decoder,
               "--n-hidden", "64", "--n-bases", "32", "--synthetic-snapshots", "10", "--train-history-len", "3",
               "--test-history-len", "3", "--relation-prediction", "--entity-prediction",
               "--checkpoint", str(tmp_path / "m.pth"), "--seed", "0", "--lr", "0.01", "--triple-batch-size", "64",
@@ -157,14 +160,14 @@ def test_cli_training_hip_graph_matches_eager(tmp_path):
     finally:
         torch.optim.Adam = adam
     (l0, s0), (l1, s1) = runs
-    # epoch 1 runs eagerly in both (a sample's first step precedes its capture) and already
-    # differs in the 6th digit: index_add's atomics (relation_context, embedding gradients)
-    # reorder sums run to run, and Adam's first steps amplify that drift over epochs 2-3
-    np.testing.assert_allclose(l1, l0, rtol=5e-4)
-    # the parameters in norm: the embedding gradients accumulate with atomics (index_add), so
-    # two eager runs differ in the last bits too, and Adam's first steps (update ~ lr * sign g)
-    # turn last-bit differences of near-zero gradients into +-lr on those few elements
+    # the step is deterministic (no atomics: relation_context and the embedding gathers
+    # accumulate through sort-based index_put, the HIP kernels sum in fixed orders), so the
+    # replays reproduce the eager run's losses bit for bit
+    np.testing.assert_array_equal(l1, l0)
+    worst = 0.0
     for k in s0:
         a, b = s0[k].float(), s1[k].float()
         rel = float((a - b).norm() / a.norm().clamp_min(1e-6))
-        assert rel < 2e-3, (k, rel)
+        worst = max(worst, rel)
+        assert rel < 1e-6, (k, rel)
+    print("graph-vs-eager worst parameter relative difference", worst)
