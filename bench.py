@@ -1,31 +1,33 @@
 #!/usr/bin/env python
 """Benchmark of the RE-GCN hot path on MI355X (contract: one JSON line on rank 0).
 
-A step is one pass of the hot path over one batch of synthetic input: the
-`HyperbolicRecurrentRGCN.predict` of one sample = the recurrent encoder over a
-history_len=3 window of snapshots (relation context, relation GRU, 2 message-passing
-layers, time gate + radius evolution per snapshot) followed by all-entity RotH scoring
-of the target snapshot's queries (entity and relation decoders).  The default workload
-is BASELINE.json configs[1] (ICEWS14s-shaped, encoder=lgcn, decoder=roth, c=0.01,
-d=200) on synthetic snapshots (the datasets are absent).
+Headline workload (default `--config synthetic_1m`): BASELINE.json configs[4], the
+north-star stress snapshot shape on ONE GPU -- |V| = 1M entities, |E| = 50M directed
+message edges per snapshot (25M triples + inverses), |R| = 256 (R2 = 512), d = 200,
+history_len = 3, encoder hyperbolic_uvrgcn (2 layers), decoder RotH.  A step is one
+`HyperbolicRecurrentRGCN.predict` (hyperbolic_model.py:892-939): the full recurrent
+forward over a 3-snapshot window (hyperbolic_model.py:797-884: relation context, relation
+GRU, 2 message-passing layers, time gate + radius evolution per snapshot) followed by the
+entity (RotH) and relation (RotHRel) decoders on a 1,024-query chunk (512 test triples
+and their inverses) scored against all 1M entities.  Every step computes everything from
+the parameters and its snapshots (no state kept across steps except the weights' MFMA
+fragment packing); the snapshot graphs are built once, in HBM, before the timed region.
 
 metric = million directed message edges aggregated per second (edges after inverse
-doubling x GCN layers x history snapshots), whole job.
-Multi-GPU: one process per GPU, each rank runs its own independent samples (replicas:
-the path has no exchange step at this size); scaling = weak.
+doubling x GCN layers x history snapshots = 300M per step), whole job:
+K steps timed exactly, between barriers + device synchronisation, max over ranks.
+Multi-GPU: one process per GPU; each rank runs its own windows (replicas, weak scaling).
 
-Every step computes everything from the parameters and its snapshots: no state is kept
-across steps except the weights' MFMA fragment packing (a layout of each weight, redone
-when the weight changes).  `--serving-cache` keeps the parameter-only states (initial
-entity state, the pristine-row memo) across steps instead; it is reported separately.
-Predicts of different test snapshots are independent (hyperbolic_main.py:100-149 without
---multi-step), so `--concurrent` (default 4) of the pool's samples run together, one
-stream each, inside one captured HIP graph of the whole pool (inputs resident in HBM);
-`latency_ms_per_predict` is one sample's predict alone.  `roofline` reports the dominant kernel, timed live with HIP events on its own
-stream; `cpu_baseline` times the CPU oracle (oracle/, a restatement of the reference
-op sequence) on the same workload on rank 0.  `aggregation_roofline` (N=1) is the
-north-star HBM check: the d=200 aggregation kernels on a config-5 snapshot
-(|V|=1M, |E|=50M), algorithmic bytes over the HIP-event launch time.
+Per-call device times come from HIP events recorded on the launching stream after every
+library call during the timed steps (`_lib.EVENT_TRACE`); `roofline` reports the call
+with the largest time per step against its algorithmic bytes (or flops), with the HBM
+traffic of its kernel from the committed rocprofv3 PMC passes (profiles/).
+`cpu_baseline` times the CPU oracle's encoder forward on a bounded sample on rank 0.
+
+The dataset-sized configs (ICEWS14s lgcn+roth, ICEWS18 roth, GDELT) run with `--config`
+(latency-bound, pools of independent predicts in one HIP graph, whole pool passes timed);
+the headline line carries ICEWS14s and ICEWS18 results (and the MRR parity of the HIP
+predict against the oracle) as extra keys.
 """
 import argparse
 import contextlib
@@ -45,15 +47,22 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix peak (MI355X_MICROARCH.md)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="icews14s_lgcn_roth")
-    ap.add_argument("--pool", type=int, default=16,
-                    help="distinct samples cycled through the timed steps; one pool pass is one batch of "
-                         "independent predicts (ICEWS14s has 31 test snapshots)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="synthetic_1m")
+    ap.add_argument("--pool", type=int, default=0,
+                    help="distinct samples cycled through the timed steps (default: 2 windows at config 5; 16 "
+                         "for the dataset configs, where one pool pass is one batch of independent predicts)")
+    ap.add_argument("--queries", type=int, default=1024,
+                    help="config 5: queries per step (half test triples, half their inverses)")
+    ap.add_argument("--encoder-launches", default="auto", choices=["auto", "phases", "layers"],
+                    help="timestep phase launches or per-layer launches (auto: layers at config 5, phases "
+                         "for the dataset configs); both give the same values bit for bit")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="config 5: skip the ICEWS14s / ICEWS18 sub-benchmarks and the MRR parity leg")
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP graph replay")
     ap.add_argument("--graph-steps", type=int, default=0,
@@ -63,8 +72,7 @@ def parse():
                     help="independent samples in flight together (one stream each inside the pool's HIP "
                          "graph): predicts of different test snapshots are independent (hyperbolic_main.py "
                          ":100-149 without --multi-step), so a server may overlap them")
-    ap.add_argument("--per-layer", action="store_true",
-                    help="run the encoder as per-layer launches instead of the timestep phase launches")
+    ap.add_argument("--per-layer", action="store_true", help=argparse.SUPPRESS)  # = --encoder-launches layers
     ap.add_argument("--serving-cache", action="store_true",
                     help="keep parameter-only states across steps (initial entity state, timestep 0's GRU "
                          "pre-half, and the memoised state of rows without an in-edge so far in the window, "
@@ -78,12 +86,15 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work")
     ap.add_argument("--no-scale", action="store_true",
-                    help="skip the config-5 aggregation roofline (|V|=1M, |E|=50M; ~20 s, N=1 only)")
+                    help="skip the config-5 aggregation and decoder rooflines (N=1 only)")
     ap.add_argument("--shard", default="replica", choices=["replica", "edge", "owner"],
                     help="multi-GPU: independent samples per rank (weak scaling), or every snapshot "
                          "partitioned across the ranks by edges (all-reduce) / destination owner "
                          "(all-gather) (strong scaling, SURVEY.md §8(e))")
-    return ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.per_layer:
+        a.encoder_launches = "layers"
+    return a
 
 
 def build_model(cfg, d, device, seed):
@@ -381,17 +392,17 @@ def cpu_baseline(cfg, d, model, sample, budget):
         mrr["note"] = "random-init weights on synthetic snapshots: absolute MRR is near chance; the delta is the check"
     per = float(np.mean(times))
     return dict(value=edges_per_step(glist) / per / 1e6, unit="M edges/s", cores=torch.get_num_threads(),
-                kind="port",
+                kind="port", **cpu_info(),
                 sample="%d x oracle predict (%s, history %d, %d queries) on host CPU; %.2f s each"
                        % (len(times), cfg["label"], cfg["T"], 2 * len(test_np), per)), mrr
 
 
-def main():
-    args = parse()
+def _ctx():
+    """(world, rank, device, backend): one process per GPU; BENCH_DIST_BACKEND=gloo rehearses
+    several ranks on one card."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; BENCH_DIST_BACKEND=gloo rehearses several ranks on one card
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
     if backend != "nccl":
         local %= torch.cuda.device_count()
@@ -399,22 +410,67 @@ def main():
     device = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(backend)
-    from regcn_amd.synthetic import CONFIGS
-    cfg = CONFIGS[args.config]
+        if not dist.is_initialized():
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=device)
+            else:
+                dist.init_process_group(backend)
+    return world, rank, device, backend
+
+
+def _timed(world, device, backend, run, edges_local):
+    """Barrier + synchronise, run(), synchronise + barrier; returns (elapsed max over ranks,
+    edges summed over ranks)."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed, float(edges_local)], dtype=torch.float64,
+                         device=device if backend == "nccl" else "cpu")
+        tm = t.clone()
+        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        return float(tm[0]), float(t[1])
+    return elapsed, float(edges_local)
+
+
+def cpu_info():
+    """Host CPU model and the threads the CPU baseline used (lscpu model
+    and core count)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "host_logical_cpus": os.cpu_count()}
+
+
+# ------------------------------------------------------------------------- dataset configs
+def run_small(args, cfg, world, rank, device, backend, extras=True):
+    """The dataset-sized configs: pools of independent predicts (see the module docstring).
+    Whole pool passes are timed (steps rounded up to a multiple of the pool when the pool
+    runs as one HIP graph), so the value does not depend on the step count."""
     d = args.d
+    pool_n = args.pool or 16
     model = build_model(cfg, d, device, seed=1234)          # same weights on every rank
-    model.use_phases = not args.per_layer
+    model.use_phases = args.encoder_launches != "layers"
     model.memo_pristine = model.param_caches = args.serving_cache
     sharded = args.shard != "replica" and world > 1
     # replicas: independent data per rank; sharded: every rank holds the same snapshots
-    samples = make_samples(cfg, args.pool, device, seed=100 if sharded else 100 + 7919 * rank,
+    samples = make_samples(cfg, pool_n, device, seed=100 if sharded else 100 + 7919 * rank,
                            shard=args.shard if sharded else "replica")
-    if sharded:
-        args.no_graph = True  # collectives between the launches: eager
+    no_graph = args.no_graph or sharded  # sharded: collectives between the launches, eager
     R = cfg["R"]
 
     def eager(i):
@@ -422,8 +478,7 @@ def main():
         return model.predict(glist, R, None, test, True)
 
     conc = max(1, min(args.concurrent, len(samples)))
-    lanes = [torch.cuda.Stream(device) for _ in range(conc)] if conc > 1 else []
-
+    lanes = [torch.cuda.Stream(device) for _ in range(conc)] if conc > 1 and not no_graph else []
     share = not args.no_batch_share and not args.serving_cache
 
     def pool_pass(origin):
@@ -453,9 +508,9 @@ def main():
     # sequence, so consecutive steps do not pay a graph launch each (~20 us on this runtime)
     graphs, pool_graph = [], None
     gs = args.graph_steps or len(samples)
-    if lanes and (args.no_graph or gs != len(samples)):
-        raise SystemExit("--concurrent needs the whole-pool HIP graph (no --no-graph / --graph-steps)")
-    if not args.no_graph:
+    if lanes and gs != len(samples):
+        raise SystemExit("--concurrent needs the whole-pool HIP graph (no --graph-steps)")
+    if not no_graph:
         cap = torch.cuda.Stream(device)
         # one predict alone (the per-sample graphs: latency, --graph-steps 1) keeps its rows
         # without in-edges inside the phase launches, beside the in-edge tiles' latency
@@ -485,11 +540,16 @@ def main():
             pool_graph.replay()
         torch.cuda.synchronize()
 
-    def run_steps(k0, n):
-        """Steps k0 .. k0 + n - 1 (sample k % pool): whole-pool graph launches where aligned."""
-        k = k0
-        while k < k0 + n:
-            if pool_graph is not None and k % len(samples) == 0 and k + len(samples) <= k0 + n:
+    # whole pool passes only when the pool is one graph launch (the value would otherwise
+    # depend on steps mod pool: the remainder would replay single-predict latency graphs)
+    steps = args.steps
+    if pool_graph is not None:
+        steps = -(-steps // len(samples)) * len(samples)
+
+    def run_steps():
+        k = 0
+        while k < steps:
+            if pool_graph is not None:
                 pool_graph.replay()
                 k += len(samples)
             elif graphs:
@@ -501,27 +561,9 @@ def main():
                 k += 1
 
     epw = [edges_per_step(s[1]) for s in samples]
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run_steps(0, args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    edges_local = sum(epw[k % len(samples)] for k in range(args.steps))
-    if world > 1:
-        t = torch.tensor([elapsed, float(edges_local)], dtype=torch.float64,
-                         device=device if backend == "nccl" else "cpu")
-        tm = t.clone()
-        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed, edges_total = float(tm[0]), float(t[1])
-        if sharded:  # every rank processed the same edges: count them once
-            edges_total = float(edges_local)
-    else:
+    edges_local = sum(epw[k % len(samples)] for k in range(steps))
+    elapsed, edges_total = _timed(world, device, backend, run_steps, edges_local)
+    if sharded:  # every rank processed the same edges: count them once
         edges_total = float(edges_local)
     value = edges_total / elapsed / 1e6
 
@@ -550,44 +592,300 @@ def main():
         if kd["frac"] < 0.1:  # the ICEWS-size launches move <= a few MB each
             roof["note"] = ("latency-bound at this size (a few MB and ~20 in-edge tiles per launch, one "
                             "gather -> GEMM -> epilogue chain per tile); the HBM and MFMA rooflines of the "
-                            "same kernels are aggregation_roofline (config 5) and decoder_roofline")
+                            "same kernels are the config-5 headline's")
         kernels = {k: dict(avg_us=round(v["ms"] * 1e3, 3), per_step=v["per_step"], bound=v["bound"],
                            achieved=round(v["achieved"], 3), unit=v["unit"], frac=round(v["frac"], 4))
                    for k, v in kern.items()}
-        # SURVEY.md §8(d) asks for edges/s per layer and per encoder forward besides the
-        # end-to-end step: from the live kernel times (sum of per-step kernel time, no gaps)
         enc_us = sum(v["ms"] * 1e3 * v["per_step"] for k, v in kern.items() if k.startswith(("k_phase", "k_zero", "k_cold")))
         e_step = float(np.mean(epw))
         breakdown = {"encoder_kernels_us_per_step": round(enc_us, 2),
                      "encoder_M_edges_per_s": round(e_step / enc_us, 3) if enc_us else None,
                      "note": "kernel time only (sum of the stage launches' HIP-event averages, the phase "
                              "launches of one timestep x history_len); value is end to end"}
-        scale = dec = None
-        if not args.no_scale and world == 1:
-            scale = aggregation_at_scale(device)
-            dec = decoder_at_scale()
         cpu = mrr = None
-        if not args.no_cpu_baseline and world == 1:
+        if extras and not args.no_cpu_baseline and world == 1:
             cpu, mrr = cpu_baseline(cfg, d, model, samples[0], args.cpu_budget)
-        ms = elapsed / args.steps * 1e3
+        ms = elapsed / steps * 1e3
         out = {"metric": METRIC, "value": round(value, 3), "unit": "M edges/s", "n_gpus": world,
-               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+               "steps": steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
                "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "f32",
                "data": "synthetic (%s-shaped snapshots, random-init weights)" % args.config.split("_")[0],
                "config": {"workload": cfg["label"], "V": cfg["V"], "R": cfg["R"], "triples_per_snapshot":
                           cfg["per_snap"], "history_len": cfg["T"], "n_layers": 2, "d": d,
                           "edges_per_step": int(np.mean(epw)), "queries_per_step": 2 * cfg["per_snap"],
                           "hip_graph": bool(graphs), "steps_per_graph_launch": len(samples) if pool_graph else 1,
-                          "concurrent_samples": conc, "encoder_launches": "per-layer" if args.per_layer
-                          else "timestep phases", "serving_cache": bool(args.serving_cache),
-                          "batch_shared_states": share,
+                          "concurrent_samples": conc if lanes else 1,
+                          "encoder_launches": "per-layer" if not model.use_phases else "timestep phases",
+                          "serving_cache": bool(args.serving_cache), "batch_shared_states": share,
                           "parallelism": ("%s-partitioned snapshots x%d" % (args.shard, world)) if sharded
                           else "replicas x%d" % world},
                "latency_ms_per_predict": round(lat_ms, 4) if lat_ms else None,
-               "roofline": roof, "kernels": kernels, "breakdown": breakdown, "aggregation_roofline": scale,
-               "decoder_roofline": dec, "cpu_baseline": cpu, "mrr_parity": mrr}
+               "roofline": roof, "kernels": kernels, "breakdown": breakdown,
+               "cpu_baseline": cpu, "mrr_parity": mrr}
+    del graphs, pool_graph, samples, model
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+# --------------------------------------------------------------------------- config 5
+SCALE_KERNEL = {  # library call -> its main kernel (rocprof / PMC name)
+    "regcn_union_aggregate_f32": "k_gather_sum<0>",
+    "regcn_segment_mean_f32": "k_gather_sum<1>",
+    "regcn_layer_f32": "k_layer<0, 1, false>",
+    "regcn_layer_f32(step)": "k_layer<0, 1, true>",
+    "regcn_timestep_phase_f32(A)": "k_phase_a",
+    "regcn_timestep_phase_f32(B)": "k_phase_b<0, 1>",
+    "regcn_timestep_phase_f32(C)": "k_phase_c<0, 1>",
+    "regcn_zero_step_f32": "k_zero_step",
+    "regcn_hyp_score_jobs_f32": "k_score_f32_jobs",
+    "regcn_roth_queries_f32": "k_queries4",
+    "regcn_relation_gru_x_f32": "k_rel_gru_x",
+    "regcn_relation_gru_pre_f32": "k_rel_gru_pre",
+    "regcn_init_entities_f32": "k_init_entities",
+}
+
+
+def scale_work(model, glist, B):
+    """Algorithmic (flops, bytes) per launch of each library call of one config-5 predict,
+    averaged over the window's snapshots (gathered source row + indices +
+    radius per edge; row reads/writes per node; d x d products 2 d^2 flops per row)."""
+    d = model.dynamic_emb.shape[1]
+    V = model.num_ents
+    R2 = 2 * model.num_rels
+    gemm = 2.0 * d * d
+    row = 4.0 * d
+    st = []
+    for g in glist:
+        wk = g.work()
+        hc = wk["heavy_chunks"]
+        e_heavy = int((hc[:, 2] - hc[:, 1]).sum()) if hc.numel() else 0
+        st.append(dict(n_pos=g.n_pos, items=int(wk["item_src"].numel()), e_heavy=e_heavy, n_heavy=g.n_heavy,
+                       pairs=int(wk["rel_idx"].numel()) // 2))
+    m = {k: float(np.mean([x[k] for x in st])) for k in st[0]}
+    per_edge = row + 12.0  # source row + col_src + col_type + radius[src]
+    io_layer = V * (row + 4) + V * (2 * row + 4) + V * 4.0  # x, r in; h, x', r' out; norm
+    w = {
+        "regcn_union_aggregate_f32": (0.0, m["e_heavy"] * per_edge + m["n_heavy"] * (row + 12)),
+        "regcn_segment_mean_f32": (0.0, m["pairs"] * (row + 4) + R2 * row),
+        "regcn_layer_f32": (gemm * (m["n_pos"] + V), m["items"] * per_edge + m["n_heavy"] * row + io_layer),
+        "regcn_layer_f32(step)": (gemm * (m["n_pos"] + 2 * V),
+                                  m["items"] * per_edge + m["n_heavy"] * row + io_layer + V * (2 * row + 4)),
+        "regcn_timestep_phase_f32(A)": (2 * gemm * m["n_pos"] + 2.0 * R2 * 3 * d * d,
+                                        V * row + 2 * m["n_pos"] * row + 4.0 * R2 * d * 3 + 4.0 * 3 * d * d),
+        "regcn_timestep_phase_f32(B)": (2 * gemm * m["n_pos"], m["items"] * per_edge + m["n_heavy"] * row
+                                        + m["n_pos"] * 3 * row),
+        "regcn_timestep_phase_f32(C)": (gemm * m["n_pos"], m["items"] * per_edge + m["n_heavy"] * row
+                                        + m["n_pos"] * 5 * row),
+        "regcn_zero_step_f32": (3 * gemm * (V - m["n_pos"]), (V - m["n_pos"]) * 3 * row),
+        "regcn_hyp_score_jobs_f32": (2.0 * B * (V + R2) * d, 4.0 * (B * (V + R2) + (V + R2) * d)),
+        "regcn_roth_queries_f32": (2.0 * B * 5.5 * d * d, 4.0 * (B * d * 5 + R2 * d * 2)),
+        "regcn_init_entities_f32": (0.0, V * (3 * row + 8)),
+    }
+    return w, m
+
+
+def summarize_trace(trace, steps):
+    """Per library call: launches per step and mean device ms per launch, from the events
+    recorded after each call (the interval since the previous event on the same stream)."""
+    per = {}
+    prev = None
+    for name, ev in trace:
+        if prev is not None and name != "__step__":
+            per.setdefault(name, []).append(prev.elapsed_time(ev))
+        prev = ev
+    return {k: dict(ms=float(np.mean(v)), per_step=len(v) / steps) for k, v in per.items()}
+
+
+def pmc_for(kernel, config, d):
+    path = os.path.join(REPO, "profiles", "pmc_traffic_%s.json" % config)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        pm = json.load(f)
+    if pm.get("config") != config or int(pm.get("d", -1)) != d:
+        return None, None
+    k = pm["kernels"].get(kernel)
+    if k is None:
+        return None, None
+    return k["hbm_bytes"], "profiles/pmc_traffic_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, %d launches)" % (
+        config, k["launches"])
+
+
+def cpu_baseline_scale(cfg, d, budget):
+    """The CPU oracle's encoder forward (oracle/model.py hyperbolic_forward, the reference op
+    sequence with per-edge message materialisation) over ONE snapshot at |V| = 1M with a
+    bounded edge count (full |E| = 50M is infeasible on the host)."""
+    sys.path.insert(0, REPO)
+    from oracle import graph as OG
+    from oracle import model as OM
+    from regcn_amd.synthetic import snapshot_series
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    V, R = cfg["V"], cfg["R"]
+    triples = 2_500_000
+    snap = snapshot_series(7, V, R, 1, triples)[0]
+    g = OG.build_sub_graph(V, R, snap)
+    del snap
+    m = build_model(dict(cfg, V=V), d, torch.device("cpu"), seed=1234)
+    sd = {k: v.detach() for k, v in m.state_dict().items()}
+    del m
+    ocfg = dict(c=0.01, n_layers=2, n_bases=cfg["n_bases"], radius_min=0.5, radius_max=3.0, radius_epsilon=0.1,
+                radius_anchor_beta=1.0, radius_msg_gamma=0.15, use_residual_evolution=True, layer_norm=False,
+                encoder=cfg["encoder"], decoder=cfg["decoder"])
+    times = []
+    t_end = time.time() + budget
+    with torch.no_grad():
+        while True:
+            t0 = time.time()
+            OM.hyperbolic_forward(sd, ocfg, [g])
+            times.append(time.time() - t0)
+            if time.time() > t_end or len(times) >= 3:
+                break
+    per = float(np.mean(times))
+    edges = 2 * 2 * triples  # directed edges x 2 layers
+    return dict(value=round(edges / per / 1e6, 4), unit="M edges/s", cores=torch.get_num_threads(), kind="port",
+                sample="%d x oracle encoder forward (1 snapshot, |V|=%d, |E|=%d directed, R2=%d, d=%d, 2 layers: "
+                       "%d message edges; the full |E|=50M window is infeasible on the host), %.2f s each"
+                       % (len(times), V, 2 * triples, 2 * R, d, edges, per), **cpu_info())
+
+
+def run_scale(args, cfg, world, rank, device, backend):
+    """Config 5 headline (see the module docstring)."""
+    from regcn_amd import _lib
+    from regcn_amd import graph as G
+    from regcn_amd.synthetic import snapshot_series
+    d, T, V, R = args.d, cfg["T"], cfg["V"], cfg["R"]
+    n_win = args.pool or 2
+    t_setup = time.time()
+    snaps = snapshot_series(100 + 7919 * rank, V, R, T + n_win, cfg["per_snap"])  # replicas: own data per rank
+    graphs = [G.build_sub_graph(V, R, s, True, device) for s in snaps[:T + n_win - 1]]
+    tests = [torch.from_numpy(np.ascontiguousarray(snaps[T + i][:args.queries // 2])).to(device)
+             for i in range(n_win)]
+    del snaps
+    windows = [graphs[i:i + T] for i in range(n_win)]
+    model = build_model(cfg, d, device, seed=1234)
+    model.use_phases = args.encoder_launches == "phases"
+    model.memo_pristine = model.param_caches = False  # every step computes everything
+    B = 2 * tests[0].shape[0]
+
+    def step(k):
+        i = k % n_win
+        _lib.trace_mark("__step__")
+        return model.predict(windows[i], R, None, tests[i], True)
+
+    with torch.no_grad():
+        for k in range(max(args.warmup, 1)):
+            step(k)
+    torch.cuda.synchronize()
+    setup_s = time.time() - t_setup
+    epw = [edges_per_step(w) for w in windows]
+    edges_local = sum(epw[k % n_win] for k in range(args.steps))
+    trace = []
+
+    def run():
+        _lib.EVENT_TRACE = trace
+        try:
+            with torch.no_grad():
+                for k in range(args.steps):
+                    step(k)
+        finally:
+            _lib.EVENT_TRACE = None
+
+    elapsed, edges_total = _timed(world, device, backend, run, edges_local)
+    value = edges_total / elapsed / 1e6
+    out = None
+    if rank == 0:
+        calls = summarize_trace(trace, args.steps)
+        work, stats = scale_work(model, windows[0], B)
+        kernels = {}
+        for name, v in calls.items():
+            flops, nbytes = work.get(name, (0.0, 0.0))
+            e = dict(avg_us=round(v["ms"] * 1e3, 1), per_step=round(v["per_step"], 3),
+                     kernel=SCALE_KERNEL.get(name, name))
+            if flops or nbytes:
+                wv = _work(flops, nbytes, v["ms"])
+                e.update(bound=wv["bound"], achieved=round(wv["achieved"], 1), unit=wv["unit"],
+                         frac=round(wv["frac"], 4))
+            kernels[name] = e
+        dom = max(calls, key=lambda k: calls[k]["ms"] * calls[k]["per_step"])
+        flops, nbytes = work[dom]
+        wv = _work(flops, nbytes, calls[dom]["ms"])
+        kname = SCALE_KERNEL.get(dom, dom)
+        traffic, tsrc = pmc_for(kname, args.config, d)
+        roof = dict(bound=wv["bound"], kernel=kname, call=dom, achieved=round(wv["achieved"], 1),
+                    peak=wv["peak"], unit=wv["unit"], frac=round(wv["frac"], 4), traffic=traffic,
+                    traffic_source=tsrc, flops_per_launch=flops, algorithmic_bytes_per_launch=nbytes,
+                    avg_launch_us=round(calls[dom]["ms"] * 1e3, 1), launches_per_step=calls[dom]["per_step"])
+        if traffic:
+            roof["traffic_GBps"] = round(traffic / (calls[dom]["ms"] * 1e-3) / 1e9, 1)
+            roof["traffic_frac"] = round(roof["traffic_GBps"] / HBM_PEAK_GBS, 4)
+        ms = elapsed / args.steps * 1e3
+        enc_ms = sum(v["ms"] * v["per_step"] for k, v in calls.items()
+                     if k not in ("regcn_hyp_score_jobs_f32", "regcn_roth_queries_f32"))
+        out = {"metric": METRIC, "value": round(value, 3), "unit": "M edges/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic (config-5 snapshots: Zipf(1.1) subjects/objects, uniform relations, 60% "
+                       "recurring triples; random-init weights)",
+               "config": {"workload": cfg["label"] + " (BASELINE.json configs[4]) on 1 GPU per rank: "
+                          "HyperbolicRecurrentRGCN.predict, encoder hyperbolic_uvrgcn x2 layers, RotH + RotHRel "
+                          "decoders on a %d-query chunk" % B,
+                          "V": V, "R": R, "R2": 2 * R, "triples_per_snapshot": cfg["per_snap"],
+                          "edges_per_snapshot": 2 * cfg["per_snap"], "history_len": T, "n_layers": 2, "d": d,
+                          "edges_per_step": int(np.mean(epw)), "queries_per_step": B, "windows": n_win,
+                          "encoder_launches": "timestep phases" if model.use_phases else "per-layer",
+                          "hip_graph": False, "parallelism": "replicas x%d" % world,
+                          "snapshot_stats": {k: round(v) for k, v in stats.items()}},
+               "roofline": roof, "kernels": kernels,
+               "breakdown": {"encoder_ms_per_step": round(enc_ms, 3),
+                             "encoder_M_edges_per_s": round(np.mean(epw) / enc_ms / 1e3, 1),
+                             "decoder_ms_per_step": round(sum(calls[k]["ms"] * calls[k]["per_step"] for k in calls
+                                                              if k in ("regcn_hyp_score_jobs_f32",
+                                                                       "regcn_roth_queries_f32")), 3),
+                             "setup_s": round(setup_s, 1),
+                             "note": "per-call device time from HIP events recorded after each library call on "
+                                     "the launching stream during the timed steps"}}
+    del windows, graphs, tests, model, trace
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    args = parse()
+    world, rank, device, backend = _ctx()
+    from regcn_amd.synthetic import CONFIGS
+    cfg = CONFIGS[args.config]
+    if args.encoder_launches == "auto":
+        args.encoder_launches = "layers" if cfg.get("scale") else "phases"
+    if cfg.get("scale"):
+        out = run_scale(args, cfg, world, rank, device, backend)
+        if rank == 0 and world == 1:
+            if not args.no_cpu_baseline:
+                out["cpu_baseline"] = cpu_baseline_scale(cfg, args.d, args.cpu_budget)
+            if not args.no_scale:
+                out["aggregation_roofline"] = aggregation_at_scale(device)
+                out["decoder_roofline"] = decoder_at_scale()
+        if world == 1 and not args.no_extras:
+            for key, name in (("icews14s", "icews14s_lgcn_roth"), ("icews18", "icews18_roth")):
+                sub = parse(["--config", name, "--steps", "64", "--warmup", "4", "--cpu-budget", "10"]
+                            + (["--no-cpu-baseline"] if name != "icews14s_lgcn_roth" else []))
+                r = run_small(sub, CONFIGS[name], world, rank, device, backend)
+                if rank == 0:
+                    out[key] = {k: r[k] for k in ("value", "unit", "ms_per_step", "latency_ms_per_predict",
+                                                  "steps", "config", "roofline", "kernels")}
+                    if r.get("mrr_parity"):
+                        out["mrr_parity"] = dict(r["mrr_parity"], workload=CONFIGS[name]["label"])
+                        out[key]["cpu_baseline"] = r["cpu_baseline"]
+    else:
+        out = run_small(args, cfg, world, rank, device, backend)
+        if rank == 0 and world == 1 and not args.no_scale:
+            out["aggregation_roofline"] = aggregation_at_scale(device)
+            out["decoder_roofline"] = decoder_at_scale()
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()
 

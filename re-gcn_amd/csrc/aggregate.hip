@@ -23,64 +23,146 @@
 
 namespace regcn {
 
-// ------------------------------------------------------------------------ Union / mean
-// UNION : acc = sum_e w_e (x[src_e] + rel[type_e]),  w_e = exp(-gamma |r_src - r_dst|)
-//         out = norm[row] * acc          (hyperbolic_layers.py:222-240, linearity of W_n)
-// EUCLID: same with w_e = 1              (rgcn/layers.py:257-279)
-// MEAN  : acc = sum_e x[idx_e];  out = acc / count  (hyperbolic_model.py:802-812)
+// ------------------------------------------------------------------------------ mean
+// MEAN: acc = sum_e x[idx_e];  out = acc / count  (hyperbolic_model.py:802-812), one wave
+// per chunk, 8 gathered rows in flight, unconditional loads (clamped column).
 template <int MODE>
 __global__ __launch_bounds__(256) void k_gather_sum(
     const float* __restrict__ x, const float* __restrict__ radius, const float* __restrict__ rel,
     const int* __restrict__ col_src, const int* __restrict__ col_type, const float* __restrict__ rowscale,
     const Chunk* __restrict__ chunks, int n_chunks, float gamma, int d, float* __restrict__ partial,
     int pstride, float* __restrict__ out) {
+  static_assert(MODE == AGG_MEAN, "union / euclid: k_union_runs");
   const int lane = threadIdx.x & 63;
   const int col = lane * 4;
+  const uint32_t off = (uint32_t)min(col, d - 4) * 4u;
   const int nw = gridDim.x * (blockDim.x >> 6);
   for (int ci = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ci < n_chunks; ci += nw) {
     const Chunk ch = chunks[ci];
     f4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float r_dst = (MODE == AGG_UNION) ? radius[ch.row] : 0.f;
     for (int e0 = ch.beg; e0 < ch.end; e0 += 64) {
       const int n = min(64, ch.end - e0);
-      int my_s = 0, my_t = 0;
-      float my_w = 1.f;
-      if (lane < n) {
-        my_s = col_src[e0 + lane];
-        if (MODE != AGG_MEAN) my_t = col_type[e0 + lane];
-        if (MODE == AGG_UNION) my_w = expf(-gamma * fabsf(radius[my_s] - r_dst));
-      }
+      const int my_s = col_src[e0 + min(lane, n - 1)];
       int j = 0;
-      for (; j + 4 <= n; j += 4) {
-        f4 xs[4], rr[4];
+      for (; j + 8 <= n; j += 8) {
+        f4 xs[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          xs[u] = load4(x + (int64_t)rl(my_s, j + u) * d, col, d);
-          if (MODE != AGG_MEAN) rr[u] = load4(rel + (int64_t)rl(my_t, j + u) * d, col, d);
-        }
+        for (int u = 0; u < 8; ++u) xs[u] = row_load4(x + (int64_t)rl(my_s, j + u) * d, off);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (MODE == AGG_MEAN) acc += xs[u];
-          else if (MODE == AGG_EUCLID) acc += xs[u] + rr[u];
-          else acc += rlf(my_w, j + u) * (xs[u] + rr[u]);
+        for (int u = 0; u < 8; ++u) acc += xs[u];
+      }
+      for (; j < n; ++j) acc += row_load4(x + (int64_t)rl(my_s, j) * d, off);
+    }
+    if (ch.slot < 0) store4(out + (int64_t)ch.row * d, col, d, acc / rowscale[ch.row]);
+    else store4(partial + (int64_t)ch.slot * pstride, col, d, acc);
+  }
+}
+
+// UNION / EUCLID with relation-type runs.  By linearity
+//   sum_e w_e (x[src_e] + rel[t_e]) = sum_e w_e x[src_e] + sum_runs (sum_{e in run} w_e) rel[t_run]
+// over the maximal runs of equal type in the chunk's edge order.  A hub row's edges in
+// row/type order (graph.row_type_cols: the fused layers' heavy rows) are a few long runs,
+// so the relation rows are read once per run instead of once per edge: the per-edge load
+// stream is the gathered source row alone (8 rows in flight per wave).  Any edge order is
+// valid (CSR order: runs of about one edge, relation rows loaded 4 at a time).
+// Per 64-edge batch, lane = edge: run heads by ballot, a segmented lane scan of the
+// weights, then each closed run's relation row once; the batch's last run stays open
+// into the next batch.  Deterministic (fixed lane and run order, no atomics).
+template <bool EUCLID>
+__global__ __launch_bounds__(256) void k_union_runs(
+    const float* __restrict__ x, const float* __restrict__ radius, const float* __restrict__ rel,
+    const int* __restrict__ col_src, const int* __restrict__ col_type, const float* __restrict__ rowscale,
+    const Chunk* __restrict__ chunks, int n_chunks, float gamma, int d, float* __restrict__ partial,
+    int pstride, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int col = lane * 4;
+  // clamped column: lanes past d re-read the row's last quad (same cache lines, never
+  // stored), so every row load is unconditional
+  const uint32_t off = (uint32_t)min(col, d - 4) * 4u;
+  const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);  // lanes 0..lane
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int ci = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); ci < n_chunks; ci += nw) {
+    const Chunk ch = chunks[ci];
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float r_dst = EUCLID ? 0.f : radius[ch.row];
+    int run_t = -1;     // the open run (wave-uniform)
+    float run_w = 0.f;
+    for (int e0 = ch.beg; e0 < ch.end; e0 += 64) {
+      const int n = min(64, ch.end - e0);
+      const int ei = e0 + min(lane, n - 1);
+      const int my_s = col_src[ei];
+      const int my_t = col_type[ei];
+      const float my_w = EUCLID ? 1.f : expf(-gamma * fabsf(radius[my_s] - r_dst));
+      // gathered source rows
+      int j = 0;
+      for (; j + 8 <= n; j += 8) {
+        f4 xs[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) xs[u] = row_load4(x + (int64_t)rl(my_s, j + u) * d, off);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (EUCLID) acc += xs[u];
+          else acc += rlf(my_w, j + u) * xs[u];
         }
       }
       for (; j < n; ++j) {
-        f4 xs = load4(x + (int64_t)rl(my_s, j) * d, col, d);
-        if (MODE == AGG_MEAN) acc += xs;
-        else {
-          f4 rr = load4(rel + (int64_t)rl(my_t, j) * d, col, d);
-          if (MODE == AGG_EUCLID) acc += xs + rr;
-          else acc += rlf(my_w, j) * (xs + rr);
-        }
+        const f4 xs = row_load4(x + (int64_t)rl(my_s, j) * d, off);
+        if (EUCLID) acc += xs;
+        else acc += rlf(my_w, j) * xs;
+      }
+      // runs: a head starts a run (lane 0 compares with the open run's type)
+      int prev_t = __shfl_up(my_t, 1);
+      if (lane == 0) prev_t = run_t;
+      const uint64_t hm = __ballot(lane < n && my_t != prev_t);
+      const uint64_t below = hm & upto;
+      const int start = below ? 63 - __builtin_clzll(below) : 0;
+      float v = lane < n ? my_w : 0.f;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float u = __shfl_up(v, o);
+        if (lane - o >= start) v += u;
+      }
+      // lane 0 starts a new run: the open run ended with the previous batch
+      if ((hm & 1ull) && run_t >= 0) acc += run_w * row_load4(rel + (int64_t)run_t * d, off);
+      float cw = (hm & 1ull) ? 0.f : run_w;  // otherwise the first closed run continues it
+      uint64_t m = hm & ~1ull;                // each head > 0 closes the run ending just before it
+      while (m) {
+        const int h0 = __builtin_ctzll(m);
+        m &= m - 1;
+        const bool ok1 = m != 0;
+        const int h1 = ok1 ? __builtin_ctzll(m) : h0;
+        if (ok1) m &= m - 1;
+        const bool ok2 = m != 0;
+        const int h2 = ok2 ? __builtin_ctzll(m) : h0;
+        if (ok2) m &= m - 1;
+        const bool ok3 = m != 0;
+        const int h3 = ok3 ? __builtin_ctzll(m) : h0;
+        if (ok3) m &= m - 1;
+        const float w0 = rlf(v, h0 - 1) + cw;
+        cw = 0.f;
+        const float w1 = ok1 ? rlf(v, h1 - 1) : 0.f;
+        const float w2 = ok2 ? rlf(v, h2 - 1) : 0.f;
+        const float w3 = ok3 ? rlf(v, h3 - 1) : 0.f;
+        const f4 a0 = row_load4(rel + (int64_t)rl(my_t, h0 - 1) * d, off);
+        const f4 a1 = row_load4(rel + (int64_t)rl(my_t, h1 - 1) * d, off);
+        const f4 a2 = row_load4(rel + (int64_t)rl(my_t, h2 - 1) * d, off);
+        const f4 a3 = row_load4(rel + (int64_t)rl(my_t, h3 - 1) * d, off);
+        acc += w0 * a0;
+        acc += w1 * a1;
+        acc += w2 * a2;
+        acc += w3 * a3;
+      }
+      const float wl = rlf(v, n - 1);
+      if (hm == 0ull) {
+        run_w += wl;  // the whole batch continues the open run
+      } else {
+        run_t = rl(my_t, n - 1);
+        run_w = wl;
       }
     }
-    if (ch.slot < 0) {
-      f4 v = (MODE == AGG_MEAN) ? acc / rowscale[ch.row] : acc * rowscale[ch.row];
-      store4(out + (int64_t)ch.row * d, col, d, v);
-    } else {
-      store4(partial + (int64_t)ch.slot * pstride, col, d, acc);
-    }
+    if (run_t >= 0) acc += run_w * row_load4(rel + (int64_t)run_t * d, off);
+    if (ch.slot < 0) store4(out + (int64_t)ch.row * d, col, d, acc * rowscale[ch.row]);
+    else store4(partial + (int64_t)ch.slot * pstride, col, d, acc);
   }
 }
 
@@ -303,10 +385,10 @@ int gather_sum(int mode, const float* x, const float* radius, const float* rel, 
   if (n_chunks > 0) {
     dim3 g(grid_for(n_chunks)), b(256);
     if (mode == AGG_UNION)
-      hipLaunchKernelGGL(k_gather_sum<AGG_UNION>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,
+      hipLaunchKernelGGL(k_union_runs<false>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,
                          n_chunks, gamma, d, partial, pstride, out);
     else if (mode == AGG_EUCLID)
-      hipLaunchKernelGGL(k_gather_sum<AGG_EUCLID>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,
+      hipLaunchKernelGGL(k_union_runs<true>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,
                          n_chunks, gamma, d, partial, pstride, out);
     else if (mode == AGG_MEAN)
       hipLaunchKernelGGL(k_gather_sum<AGG_MEAN>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,

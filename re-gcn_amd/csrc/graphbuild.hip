@@ -800,7 +800,9 @@ int snapshot_work(const regcn_snapshot_desc* d, hipStream_t st) {
     return rc;
   Spans all{0, V, R, d->rowptr, d->in_deg, nullptr, nullptr};
   if ((rc = chunker(all, C, ws, L, (int4*)d->chunks, (int4*)d->fixups, stats + REGCN_SNAP_CHUNKS, st))) return rc;
-  Spans rel{2, 2 * R, R, d->rel_start, d->rel_ent_count, nullptr, nullptr};
+  // forward relations only: an inverse id's span holds the same entities in the same order
+  // (rgcn/utils.py:88-89), so its mean is a copy of the forward one (regcn_segment_mean_f32 callers)
+  Spans rel{2, R, R, d->rel_start, d->rel_ent_count, nullptr, nullptr};
   return chunker(rel, C, ws, L, (int4*)d->rel_chunks, (int4*)d->rel_fixups, stats + REGCN_SNAP_REL_CHUNKS, st);
 }
 

@@ -224,10 +224,26 @@ def exported_symbols():
     return list(_SIGS)
 
 
+# measurement (bench.py): when a list, every library call appends (name, HIP event recorded
+# on the current stream right after the call's launches); consecutive events bracket the
+# device time of each call on an in-order stream
+EVENT_TRACE = None
+
+
+def trace_mark(name):
+    """Record a named HIP event on the current stream into EVENT_TRACE (if tracing)."""
+    if EVENT_TRACE is not None:
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        EVENT_TRACE.append((name, ev))
+
+
 def check(rc, name):
     if rc != 0:
         msg = lib().regcn_last_error_string().decode(errors="replace")
         raise RuntimeError("%s failed (rc=%d): %s" % (name, rc, msg))
+    if EVENT_TRACE is not None:
+        trace_mark(name)
 
 
 def call(name, *args):
@@ -235,7 +251,8 @@ def call(name, *args):
 
 
 def call_layer(desc):
-    check(lib().regcn_layer_f32(ctypes.byref(desc), stream()), "regcn_layer_f32")
+    check(lib().regcn_layer_f32(ctypes.byref(desc), stream()),
+          "regcn_layer_f32(step)" if desc.fuse_step else "regcn_layer_f32")
 
 
 def stream():

@@ -36,6 +36,7 @@ import torch
 from . import ranking
 from .graph import build_sub_graph
 from .training import GraphedSteps
+from .weights import invalidate
 
 logger = logging.getLogger("regcn_amd.cli")
 
@@ -266,6 +267,9 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
     import torch.distributed as dist
     from .parallel import allreduce_gradients
     world0 = dist.get_world_size() if dist.is_initialized() else 1
+    if args.hip_graph and world0 > 1:
+        logger.warning("--hip-graph is ignored with %d ranks: the replica step holds a gradient all-reduce "
+                       "between its launches, so it runs eagerly", world0)
     graphed = GraphedSteps(device) if args.hip_graph and world0 == 1 else None
     optimizer = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=1e-5,   # :469
                                  capturable=graphed is not None)
@@ -347,6 +351,11 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
         if epoch and epoch % args.evaluate_every == 0:                                      # :660-681
             stop = torch.zeros(1, device=device)
             if rank == 0:
+                if graphed is not None:
+                    # a replay updates the parameters on the device without bumping their
+                    # version counters: drop every parameter-keyed cache (packed weights,
+                    # initial state, memo) so validation scores the current weights
+                    invalidate(model)
                 res = test(model, train_list, valid_list, num_rels, num_nodes, device, all_ans_v, all_ans_r_v, args)
                 logger.info("Validation - MRR: raw=%.4f, filter=%.4f | Rel MRR: raw=%.4f, filter=%.4f", *res)
                 cur = res[2] if args.relation_evaluation else res[0]

@@ -18,7 +18,8 @@ object carries the device-side work lists the HIP kernels consume:
     slot_end, 0} for rows split over several chunks (see csrc/aggregate.hip);
   * `rows` int32[V]: rows with in-degree > 0 first, then the rest (`n_pos` of the
     former), so every 64-row tile of the layer GEMM uses one self-loop weight;
-  * the same chunking over r_to_e for the relation-context mean.
+  * the same chunking over the forward relations' r_to_e spans for the relation-context
+    mean (an inverse relation's span repeats its forward relation's entities).
 Built once per snapshot and cached across epochs: on the device by
 csrc/graphbuild.hip when use_cuda (build_sub_graph_device), else with numpy here; both
 builds produce the same lists bit for bit (tests/test_gpu_graph.py).
@@ -169,7 +170,10 @@ class SnapshotGraph:
             rel_start[ur] = starts
             rel_len = np.zeros(R2, dtype=np.int64)
             rel_len[ur] = lens
-            rchunks, rfix, rslot = _chunk_rows_spans(rel_start, rel_len, self.chunk_edges)
+            # forward relations only: the inverse id r + R has the same span contents (r2e), so
+            # its mean is a copy of r's (hyperbolic_model.relation_context)
+            rchunks, rfix, rslot = _chunk_rows_spans(rel_start[:self.num_rels], rel_len[:self.num_rels],
+                                                     self.chunk_edges)
         else:
             rchunks, rfix, rslot = np.zeros((0, 4), np.int32), np.zeros((0, 4), np.int32), 0
         self._host_lists = {

@@ -61,12 +61,14 @@ def _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c):
         cs, ct = g.row_type_cols()
         _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(cs), i(ct), i(hc),
                   hc.shape[0], i(hf), hf.shape[0], nb, float(c), d, f(part), stride, f(agg), _lib.stream())
-    elif mode == _lib.AGG_UNION:
-        _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(wk["col_src"]), i(wk["col_type"]),
+    elif mode == _lib.AGG_UNION:  # type order too: one relation-row read per same-type run
+        cs, ct = g.row_type_cols()
+        _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(cs), i(ct),
                   f(wk["norm"]), i(hc), hc.shape[0], i(hf), hf.shape[0], float(gamma), d, f(part), stride, f(agg),
                   _lib.stream())
     else:
-        _lib.call("regcn_euclid_aggregate_f32", f(x), f(rel), i(wk["col_src"]), i(wk["col_type"]), f(wk["norm"]),
+        cs, ct = g.row_type_cols()
+        _lib.call("regcn_euclid_aggregate_f32", f(x), f(rel), i(cs), i(ct), f(wk["norm"]),
                   i(hc), hc.shape[0], i(hf), hf.shape[0], d, f(part), stride, f(agg), _lib.stream())
     return agg
 

@@ -81,15 +81,20 @@ class HyperbolicRGCNCell(HyperbolicBaseRGCN):
 
 
 def relation_context(x, g, num_rels2):
-    """x_input[r] = mean_{e in r_to_e span} x[e] (hyperbolic_model.py:802-812), HIP."""
+    """x_input[r] = mean_{e in r_to_e span} x[e] (hyperbolic_model.py:802-812), HIP.  The
+    work lists chunk the forward relations' spans only: r2e gives an inverse id r + R the
+    same entity list as r, in the same order (rgcn/utils.py:88-89), so its mean is the
+    same sum of the same rows, copied instead of recomputed (half the row gathers)."""
     wk = g.work()
     V, d = x.shape
+    R = num_rels2 // 2
     out = torch.zeros(num_rels2, d, device=x.device, dtype=torch.float32)
     ch, fx = wk["rel_chunks"], wk["rel_fixups"]
     part = torch.empty(g.rel_slots, d, device=x.device, dtype=torch.float32) if g.rel_slots else None
     _lib.call("regcn_segment_mean_f32", _lib.fptr(x, "x"), _lib.iptr(wk["rel_idx"]), _lib.fptr(wk["rel_count"]),
               _lib.iptr(ch), ch.shape[0], _lib.iptr(fx), fx.shape[0], d, _lib.fptr(part), d, _lib.fptr(out),
               _lib.stream())
+    out[R:].copy_(out[:R])
     return out
 
 

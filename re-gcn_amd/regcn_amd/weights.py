@@ -105,5 +105,5 @@ def invalidate(module):
             if hasattr(t, a):
                 delattr(t, a)
     for m in module.modules():
-        for a in ("_init_cache", "_r_static_cache", "_c_cache", "_gru_pre0"):
+        for a in ("_init_cache", "_r_static_cache", "_c_cache", "_gru_pre0", "_pristine_cache"):
             m.__dict__.pop(a, None)

@@ -100,12 +100,16 @@ def test_work_lists_cover_every_edge_once(chunk):
     assert (deg[h["rows"][:g.n_pos]] > 0).all() and (deg[h["rows"][g.n_pos:]] == 0).all()
     assert sorted(h["rows"].tolist()) == list(range(V))
     # relation spans
+    # relation spans: the forward relations' spans are chunked exactly once; the inverse
+    # spans (second half of rel_idx) repeat them and are not chunked
     rc = h["rel_chunks"]
     cov = np.zeros(len(h["rel_idx"]), dtype=np.int64)
     for r, b, e, s in rc:
         cov[b:e] += 1
-        assert h["rel_count"][r] > 0
-    assert (cov == 1).all()
+        assert h["rel_count"][r] > 0 and r < g.num_rels
+    half = len(h["rel_idx"]) // 2
+    assert (cov[:half] == 1).all() and (cov[half:] == 0).all()
+    np.testing.assert_array_equal(h["rel_idx"][:half], h["rel_idx"][half:])
 
 
 @pytest.mark.parametrize("V,T", [(200, 1500), (50, 40), (3000, 70000)])

@@ -35,11 +35,14 @@ C = 0.01
 
 
 def measure(V=1_000_000, R=256, triples=25_000_000, d=200, reps=3, dev=None,
-            which=("union_aggregate", "union_layer", "lorentz_aggregate", "lorentz_layer"), log=print):
-    """Times the named launches on a synthetic config-5 snapshot; returns the result dict."""
+            which=("union_aggregate", "union_layer", "lorentz_aggregate", "lorentz_layer"), log=print,
+            uniform_s=False):
+    """Times the named launches on a synthetic config-5 snapshot; returns the result dict.
+    uniform_s: subjects uniform (objects Zipf), so the hub rows' gathered sources are spread
+    over the whole table and really come from HBM."""
     dev = dev or torch.device("cuda", 0)
     t0 = time.time()
-    snap = snapshot_series(0, V, R, 1, triples)[0]
+    snap = snapshot_series(0, V, R, 1, triples, uniform_s=uniform_s)[0]
     g = G.build_sub_graph(V, R, snap, True, dev)
     del snap
     E = g.number_of_edges()
@@ -62,15 +65,15 @@ def measure(V=1_000_000, R=256, triples=25_000_000, d=200, reps=3, dev=None,
                                    radius_msg_gamma=0.15).to(dev).eval()
     w_rel = lor.weight.detach().contiguous()
 
-    def union_agg():
-        _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(wk["col_src"]), i(wk["col_type"]),
-                  f(wk["norm"]), i(ch), ch.shape[0], i(fx), fx.shape[0], 0.15, d, f(part), stride, f(out),
-                  _lib.stream())
-
     t0 = time.time()
-    cs, ct = g.row_type_cols()  # the product order of the Lorentz edge lists
+    cs, ct = g.row_type_cols()  # the product order of the chunked edge lists (same-type runs)
     torch.cuda.synchronize()
     log("row/type edge order built in %.1f ms" % ((time.time() - t0) * 1e3))
+
+    def union_agg(src=cs, typ=ct):
+        _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(src), i(typ),
+                  f(wk["norm"]), i(ch), ch.shape[0], i(fx), fx.shape[0], 0.15, d, f(part), stride, f(out),
+                  _lib.stream())
 
     def lorentz_agg(src=cs, typ=ct):
         _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(src), i(typ),
@@ -78,10 +81,12 @@ def measure(V=1_000_000, R=256, triples=25_000_000, d=200, reps=3, dev=None,
 
     fns = {"union_aggregate": union_agg, "union_layer": lambda: uni(g, h, rel),
            "lorentz_aggregate": lorentz_agg, "lorentz_layer": lambda: lor(g, h, rel),
-           "lorentz_aggregate_csr": lambda: lorentz_agg(wk["col_src"], wk["col_type"])}  # edge-id order, for comparison
+           "lorentz_aggregate_csr": lambda: lorentz_agg(wk["col_src"], wk["col_type"]),  # edge-id order, for comparison
+           "union_aggregate_csr": lambda: union_agg(wk["col_src"], wk["col_type"])}
     st = torch.cuda.Stream(dev)
     b_agg = E * (4 * d + 12) + V * (4 * d + 12)
-    res = {"V": V, "E": E, "R2": 2 * R, "d": d, "b_agg_bytes": b_agg, "hbm_peak_gbs": HBM_PEAK_GBS}
+    res = {"V": V, "E": E, "R2": 2 * R, "d": d, "b_agg_bytes": b_agg, "hbm_peak_gbs": HBM_PEAK_GBS,
+           "sources": "uniform subjects, Zipf objects" if uniform_s else "Zipf subjects and objects"}
     with torch.no_grad():
         for name in which:
             ms = event_time(fns[name], reps, st, replays=3)
@@ -132,8 +137,10 @@ def main():
     ap.add_argument("--json", default=None, help="write the results here as well")
     ap.add_argument("--which", default="union_aggregate,union_layer,lorentz_aggregate,lorentz_layer")
     ap.add_argument("--cpu", action="store_true", help="also time the oracle layers at |V|=1M, |E|=5M on the host")
+    ap.add_argument("--uniform-src", action="store_true", help="uniform subjects (objects stay Zipf)")
     a = ap.parse_args()
-    res = measure(a.V, a.R, a.triples, a.d, a.reps, which=a.which.split(","), log=lambda m: print(m, flush=True))
+    res = measure(a.V, a.R, a.triples, a.d, a.reps, which=a.which.split(","), log=lambda m: print(m, flush=True),
+                  uniform_s=a.uniform_src)
     if a.cpu:
         res["cpu_oracle_E5M"] = cpu_layers(a.V, a.R, 2_500_000, a.d, log=lambda m: print(m, flush=True))
     if a.json:

@@ -1,0 +1,75 @@
+"""Config-5 probe (|V| = 1M, |E| = 50M per snapshot, R = 256, d = 200,
+history 3): one HyperbolicRecurrentRGCN.predict on 512 test triples (1,024 queries), phase
+launches vs per-layer launches, wall time per predict and peak memory.
+
+  python tools/c5probe.py [--V 1000000] [--triples 25000000] [--reps 5] [--modes phases,layers]
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "re-gcn_amd"))
+sys.path.insert(0, REPO)
+from bench import build_model  # noqa: E402
+from regcn_amd import graph as G  # noqa: E402
+from regcn_amd.synthetic import CONFIGS, snapshot_series  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--V", type=int, default=1_000_000)
+    ap.add_argument("--triples", type=int, default=25_000_000)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--modes", default="phases,layers")
+    ap.add_argument("--encoder", default="hyperbolic_uvrgcn")
+    a = ap.parse_args()
+    cfg = dict(CONFIGS["synthetic_1m"], V=a.V, per_snap=a.triples, encoder=a.encoder)
+    dev = torch.device("cuda", 0)
+    t0 = time.time()
+    snaps = snapshot_series(100, cfg["V"], cfg["R"], cfg["T"] + 1, cfg["per_snap"])
+    print("generated %d snapshots in %.1f s" % (len(snaps), time.time() - t0), flush=True)
+    t0 = time.time()
+    glist = [G.build_sub_graph(cfg["V"], cfg["R"], s, True, dev) for s in snaps[:cfg["T"]]]
+    torch.cuda.synchronize()
+    print("built in %.2f s" % (time.time() - t0), flush=True)
+    for g in glist:
+        print("  E=%d n_pos=%d tiles=%d heavy=%d budget=%d chunk=%d rel_max_span=%d items=%d heavy_chunks=%d"
+              % (g.number_of_edges(), g.n_pos, g.n_pos_tiles, g.n_heavy, g.budget, g.chunk_edges,
+                 g.rel_max_span, g.work()["item_src"].numel(), g.work()["heavy_chunks"].shape[0]), flush=True)
+    model = build_model(cfg, 200, dev, seed=1234)
+    model.param_caches = False
+    model.memo_pristine = False
+    test = torch.from_numpy(snaps[cfg["T"]][:512]).to(dev)
+    edges = 2 * sum(g.number_of_edges() for g in glist)
+    outs = {}
+    for mode in a.modes.split(","):
+        model.use_phases = mode == "phases"
+        with torch.no_grad():
+            for _ in range(2):
+                r = model.predict(glist, cfg["R"], None, test, True)
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.time()
+            s.record()
+            for _ in range(a.reps):
+                r = model.predict(glist, cfg["R"], None, test, True)
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / a.reps
+        outs[mode] = [t.clone() for t in r]
+        print("%-7s %9.3f ms per predict (wall %.3f)  %.1f M edges/s   peak mem %.1f GB"
+              % (mode, ms, (time.time() - t0) / a.reps * 1e3, edges / ms / 1e3,
+                 torch.cuda.max_memory_allocated() / 1e9), flush=True)
+    if len(outs) == 2:
+        p, l = outs["phases"], outs["layers"]
+        for name, x, y in (("score", p[1], l[1]), ("score_rel", p[2], l[2])):
+            print("%s equal=%s max|d|=%.3g finite=%s" % (name, bool(torch.equal(x, y)), float((x - y).abs().max()),
+                                                        bool(torch.isfinite(x).all())), flush=True)
+
+
+if __name__ == "__main__":
+    main()
