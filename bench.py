@@ -250,6 +250,10 @@ def kernel_profile(model, sample, d, device, share=False, pool=1):
     gather_b = E * (4 * d + 8 + (0 if lorentz else 4)) + V * 4 * 2
     row_b = 4.0 * d  # bytes of one fp32 row
     gru_w = 4.0 * 3 * d * d  # one 3d x d GRU weight half
+    w_dd = 4.0 * d * d  # one d x d weight
+    # per-launch tables every in-edge tile reads: the relation rows (h_0) and the Lorentz block
+    # table (R2 x num_bases s^2) or the union W_n
+    tables = 4.0 * R2 * d + (4.0 * lay0.weight.numel() if lorentz else w_dd)
     with torch.no_grad(), torch.cuda.stream(st):
         HM.PHASE_CAPTURE = {}
         try:
@@ -265,16 +269,19 @@ def kernel_profile(model, sample, d, device, share=False, pool=1):
             # self-loop GEMM of the in-edge rows, layer 1 of the other rows (the last
             # timestep's B has no next GRU pre-half); C = layer-1 gathers (+ W_n), the time
             # gate of the other rows (the in-edge rows' ran in A)
+            # bytes: the rows each launch moves plus every weight / table it reads once (the
+            # GRU halves, W_loop / W_evolve / W_g, the relation and Lorentz block tables)
             stages += [
                 ("k_phase_a", cap["A"][0],
                  2 * gemm * n_pos + gemm * n_zero + 2.0 * R2 * 3 * d * d,
-                 row_b * (4 * n_pos + 2 * n_zero) + 4.0 * R2 * d * 3 + gru_w),
+                 row_b * (4 * n_pos + 2 * n_zero) + 4.0 * R2 * d * 3 + gru_w + 3 * w_dd),
                 ("k_phase_b<%s>" % tag, cap["B"][0],
                  wn + gemm * n_pos + skip * gemm * n_zero,
-                 gather_b + row_b * (3 * n_pos + (1 + skip) * n_zero)),
+                 gather_b + row_b * (3 * n_pos + (1 + skip) * n_zero) + tables + 2 * w_dd
+                 + 2 * gru_w + 4.0 * 2 * R2 * d),
                 ("k_phase_c<%s>" % tag, cap["C"][0],
                  wn + gemm * n_zero,
-                 gather_b + row_b * ((4 + skip) * n_pos + 4 * n_zero)),
+                 gather_b + row_b * ((4 + skip) * n_pos + 4 * n_zero) + tables + w_dd),
             ]
             if "chain" in cap:  # the batch's pristine states: all rows x T timesteps, once per pool pass
                 stages.insert(0, ("k_cold_chain", cap["chain"][0], (2 + skip) * gemm * V * T,
@@ -332,25 +339,42 @@ def decoder_at_scale():
 
 def aggregation_at_scale(device):
     """North-star roofline check: the d=200 union and Lorentz
-    aggregations over one |V|=1M, |E|=50M synthetic snapshot (Zipf destinations), timed
-    live with HIP events; algorithmic bytes E (4d + 12) + V (4d + 12) per launch."""
+    aggregations over one |V|=1M, |E|=50M synthetic snapshot, timed live with HIP events;
+    algorithmic bytes E (4d + 12) + V (4d + 12) per launch.  Two source distributions:
+    Zipf(1.1) subjects and objects (the headline's snapshots: the hub rows' sources are hot
+    rows that L2 / the Infinity Cache serve, so the algorithmic rate can pass the HBM peak),
+    and uniform subjects with Zipf objects (the hub rows' sources spread over the whole
+    800 MB table: the gathers really stream from HBM).  `traffic` is the rocprofv3
+    FETCH_SIZE x2 + WRITE_SIZE bytes per launch of the same command (profiles/), and
+    `traffic_frac` those bytes over the launch time against the 8 TB/s peak."""
     sys.path.insert(0, os.path.join(REPO, "tools"))
     from aggbench import measure
-    res = measure(dev=device, which=("union_aggregate", "lorentz_aggregate"), log=lambda m: None)
-    out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS, "config": "synthetic |V|=%d |E|=%d R2=%d d=%d"
-           % (res["V"], res["E"], res["R2"], res["d"]), "bytes_per_launch": res["b_agg_bytes"]}
-    try:  # HBM bytes per launch from the committed PMC passes of tools/aggbench.py
-        with open(os.path.join(REPO, "profiles", "pmc_traffic_agg.json")) as fh:
-            pmc = json.load(fh)["kernels"]
-    except (OSError, ValueError, KeyError):
-        pmc = {}
-    for k, kern in (("union_aggregate", "k_gather_sum<0>"), ("lorentz_aggregate", "k_lorentz_sum<2>")):
-        tr = pmc.get(kern, {}).get("hbm_bytes")
-        out[k] = {"achieved": res[k]["algorithmic_GBps"], "frac": res[k]["hbm_frac"], "avg_launch_us":
-                  round(res[k]["ms"] * 1e3, 1), "G_edges_per_s": res[k]["edges_per_s_G"], "kernel": kern,
-                  "traffic": tr, "traffic_source": "profiles/pmc_traffic_agg.json (rocprofv3 FETCH_SIZE x2 + "
-                  "WRITE_SIZE of tools/aggbench.py)" if tr else None}
-    torch.cuda.empty_cache()
+    out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS}
+    for tag, uniform, pmc_file in (("zipf_src", False, "pmc_traffic_agg.json"),
+                                   ("uniform_src", True, "pmc_traffic_agg_uniform.json")):
+        res = measure(dev=device, which=("union_aggregate", "lorentz_aggregate"), log=lambda m: None,
+                      uniform_s=uniform)
+        try:  # HBM bytes per launch from the committed PMC passes of tools/aggbench.py
+            with open(os.path.join(REPO, "profiles", pmc_file)) as fh:
+                pmc = json.load(fh)["kernels"]
+        except (OSError, ValueError, KeyError):
+            pmc = {}
+        sub = {"config": "synthetic |V|=%d |E|=%d R2=%d d=%d, %s" % (res["V"], res["E"], res["R2"], res["d"],
+                                                                   res["sources"]),
+               "bytes_per_launch": res["b_agg_bytes"]}
+        for k, kern in (("union_aggregate", "k_union_runs<false>"), ("lorentz_aggregate", "k_lorentz_sum<2>")):
+            tr = pmc.get(kern, {}).get("hbm_bytes")
+            e = {"achieved": res[k]["algorithmic_GBps"], "frac": res[k]["hbm_frac"],
+                 "avg_launch_us": round(res[k]["ms"] * 1e3, 1), "G_edges_per_s": res[k]["edges_per_s_G"],
+                 "kernel": kern, "traffic": tr}
+            if tr:
+                e["traffic_GBps"] = round(tr / (res[k]["ms"] * 1e-3) / 1e9, 1)
+                e["traffic_frac"] = round(e["traffic_GBps"] / HBM_PEAK_GBS, 4)
+                e["traffic_source"] = "profiles/%s (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of tools/aggbench.py%s)" % (
+                    pmc_file, " --uniform-src" if uniform else "")
+            sub[k] = e
+        out[tag] = sub
+        torch.cuda.empty_cache()
     return out
 
 
@@ -630,7 +654,7 @@ def run_small(args, cfg, world, rank, device, backend, extras=True):
 
 # --------------------------------------------------------------------------- config 5
 SCALE_KERNEL = {  # library call -> its main kernel (rocprof / PMC name)
-    "regcn_union_aggregate_f32": "k_gather_sum<0>",
+    "regcn_union_aggregate_f32": "k_union_runs<false>",
     "regcn_segment_mean_f32": "k_gather_sum<1>",
     "regcn_layer_f32": "k_layer<0, 1, false>",
     "regcn_layer_f32(step)": "k_layer<0, 1, true>",

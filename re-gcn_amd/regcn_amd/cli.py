@@ -155,8 +155,10 @@ def load_dataset(args):
                             dtype=np.int64).reshape(-1, 4)
 
     def count(name):
+        """len of the {id: name} dict of knowledge_graph._read_dictionary (:526-532): ids
+        repeated under several names count once."""
         with open(os.path.join(root, name), "r") as f:
-            return sum(1 for line in f if line.strip())
+            return len({int(line.strip().split("\t")[1]) for line in f if line.strip()})
     return count("entity2id.txt"), count("relation2id.txt"), read("train.txt"), read("valid.txt"), read("test.txt")
 
 

@@ -33,6 +33,14 @@ MODEL_CASES = {
                                 use_entity_euclidean_bias=True, use_relation_specific_curvature=True),
     "uvrgcn_convtranse": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="hyperbolic_convtranse",
                               layer_norm=True),
+    # d = 200 at the dataset shapes (tools/goldens/make_golden.py LARGE_CASES): ICEWS18's
+    # R2 = 512 with hub rows over the inline budget, |E| = 80k snapshots (large-graph work
+    # lists), GDELT's history length 7 for both encoders; their goldens hold the last
+    # history embedding only ("embs_last")
+    "uvrgcn_roth_r512_d200": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False),
+    "uvrgcn_roth_e80k_d200": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False),
+    "uvrgcn_roth_h7_d200": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False),
+    "lgcn_roth_h7_d200": dict(encoder_name="lgcn", decoder_name="roth", layer_norm=True),
 }
 
 

@@ -127,10 +127,15 @@ def test_hyperbolic_model_predict_vs_golden(golden, tag):
         embs, _, h0, _, _ = m.forward(glist, None, True)
         all_tr, score, score_rel = m.predict(glist, R, None, torch.from_numpy(z["test"]).to(DEV), True)
     np.testing.assert_array_equal(all_tr.cpu().numpy(), z["all_triples"])
-    assert_close(torch.stack(embs), z["embs"], what="history_embs")
+    if "embs" in z:
+        assert_close(torch.stack(embs), z["embs"], what="history_embs")
+    else:  # the dataset-shaped goldens keep the last history embedding
+        assert_close(embs[-1], z["embs_last"], what="last history embedding")
     assert_close(h0, z["h0"], what="h_0")
     assert_close(score, z["score"], what="entity score")
     assert_close(score_rel, z["score_rel"], what="relation score")
+    if "r512" in tag or "e80k" in tag:
+        assert any(g.n_heavy > 0 for g in glist), "the golden must reach the pre-aggregated hub rows"
 
 
 @pytest.mark.parametrize("V,R,T,hub", [(500, 10, 300, False), (4000, 40, 2000, True), (300, 60, 5, False)])

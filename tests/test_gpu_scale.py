@@ -1,0 +1,105 @@
+"""Config-5 scale parity (-m gpu): BASELINE.json configs[4] snapshot shape, |V| = 1M,
+|E| = 50M directed edges, R2 = 512, d = 200 (Zipf(1.1) subjects and objects).
+
+At this size the oracle's per-edge message tensor alone is 40 GB, so the check is a
+size-independent property of the layer (linearity of W_n): the fused layer
+launch (inline gathers of the in-budget rows in per-tile item order + the hub rows'
+pre-aggregation in row/type order + MFMA tail) equals the chunked aggregation of every row
+in CSR edge order (regcn_union_aggregate_f32 / regcn_lorentz_aggregate_f32) followed by the
+reference tail in plain torch fp32 on the device (hyperbolic_layers.py:242-323, :627-694,
+the oracle's op sequence): |delta| <= 1e-4 * max(1, |ref|) over all 1M rows."""
+import numpy as np
+import pytest
+import torch
+
+from gpu_helpers import assert_close
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+C = 0.01
+
+
+@pytest.fixture(scope="module")
+def snapshot():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from regcn_amd import graph as G
+    from regcn_amd.synthetic import snapshot_series
+    V, R, d = 1_000_000, 256, 200
+    snap = snapshot_series(3, V, R, 1, 25_000_000)[0]
+    g = G.build_sub_graph(V, R, snap, True, DEV)
+    del snap
+    assert g.n_heavy > 0 and g.number_of_edges() == 50_000_000
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    from oracle import ops
+    v = torch.randn(V, d, device=DEV, generator=gen)
+    h = ops.apply_radius(ops.exp0(v, C), torch.rand(V, device=DEV, generator=gen) * 2.5 + 0.5, C).contiguous()
+    rel = (torch.randn(2 * R, d, device=DEV, generator=gen) * 0.3).contiguous()
+    yield g, h, rel
+    torch.cuda.empty_cache()
+
+
+def _tail(agg, x, g, w_loop, w_evolve):
+    """clamp(agg) + self loop (W_loop rows with in-edges, W_evolve the others) -> clamp ->
+    rrelu(11/48) -> exp0 (hyperbolic_layers.py:273-321)."""
+    from oracle import ops
+    deg = g.in_degrees()
+    loop = torch.where((deg > 0).unsqueeze(1), x @ w_loop, x @ w_evolve)
+    hn = torch.clamp(torch.clamp(agg, -10.0, 10.0) + loop, -10.0, 10.0)
+    return ops.exp0(ops.leaky(hn), C)
+
+
+def test_union_layer_config5(snapshot):
+    import torch.nn.functional as F
+    from oracle import ops
+    from regcn_amd import _lib
+    from regcn_amd.hyperbolic_layers import HyperbolicUnionRGCNLayer
+    g, h, rel = snapshot
+    V, d = h.shape
+    torch.manual_seed(0)
+    lay = HyperbolicUnionRGCNLayer(d, d, rel.shape[0], c=C, activation=F.rrelu, self_loop=True,
+                                   radius_msg_gamma=0.15).to(DEV).eval()
+    with torch.no_grad():
+        got = lay(g, h, rel)
+        x = ops.log0(h, C).contiguous()
+        r = h.norm(dim=1).contiguous()
+        wk = g.work()
+        ch, fx = wk["chunks"], wk["fixups"]
+        part = torch.empty(max(g.n_slots, 1), d, device=DEV)
+        s = torch.zeros(V, d, device=DEV)  # norm * sum_e w_e (x_src + rel_type), CSR edge order; 0 without in-edges
+        f, i = _lib.fptr, _lib.iptr
+        _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(wk["col_src"]), i(wk["col_type"]),
+                  f(wk["norm"]), i(ch), ch.shape[0], i(fx), fx.shape[0], 0.15, d, f(part), d, f(s), _lib.stream())
+        ref = _tail(s @ lay.weight_neighbor, x, g, lay.loop_weight, lay.evolve_loop_weight)
+    assert torch.isfinite(got).all()
+    assert_close(got, ref, what="config-5 union layer")
+
+
+def test_lorentz_layer_config5(snapshot):
+    import torch.nn.functional as F
+    from oracle import ops
+    from regcn_amd import _lib
+    from regcn_amd.hyperbolic_layers import LorentzRGCNLayer
+    g, h, rel = snapshot
+    V, d = h.shape
+    torch.manual_seed(1)
+    lay = LorentzRGCNLayer(d, d, rel.shape[0], 100, c=C, activation=F.rrelu, self_loop=True).to(DEV).eval()
+    with torch.no_grad():
+        got = lay(g, h, rel)
+        x = ops.log0(h, C).contiguous()
+        wk = g.work()
+        ch, fx = wk["chunks"], wk["fixups"]
+        part = torch.empty(max(g.n_slots, 1), d + 4, device=DEV)
+        s = torch.zeros(V, d, device=DEV)  # log0(to_poincare(centroid)), CSR edge order; 0 without in-edges
+        f, i = _lib.fptr, _lib.iptr
+        _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(lay.weight.detach().contiguous()),
+                  i(wk["col_src"]), i(wk["col_type"]), i(ch), ch.shape[0], i(fx), fx.shape[0], 100, C, d, f(part),
+                  d + 4, f(s), _lib.stream())
+        ref = _tail(s, x, g, lay.loop_weight, lay.evolve_loop_weight)
+    assert torch.isfinite(got).all()
+    assert_close(got, ref, what="config-5 lorentz layer")
+    # rows without in-edges: zero aggregate, W_evolve loop only
+    zero = (g.in_degrees() == 0)
+    if bool(zero.any()):
+        assert_close(got[zero], ref[zero], what="rows without in-edges")
+    np.testing.assert_array_equal(int(zero.sum()), V - g.n_pos)

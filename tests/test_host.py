@@ -190,3 +190,22 @@ def test_multistep_filter_and_snap_vs_reference(golden):
         apply_filter_(score, fp, fi)
         np.testing.assert_array_equal(score.numpy(), zm[ref_score])
         np.testing.assert_array_equal(make(tr, V, R, score, k), zm["snap_r" if rel else "snap_e"])
+
+
+def test_dataset_directory_vs_reference(golden):
+    """The reference's on-disk format read by the CLI loader (knowledge_graph.py:189-206,
+    :526-555: num_nodes = len of the id-keyed dict, rows s r o t) and split into snapshots
+    (rgcn/utils.py:306-339) as the reference's own load_from_local + split_by_time did on the
+    same directory (tests/golden/tkg_tiny, tools/goldens/make_golden.py gen_dataset)."""
+    import os
+    from regcn_amd import cli, ranking
+    z = golden("dataset_tiny.npz")
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    args = cli.build_parser().parse_args(["-d", "tkg_tiny", "--data-dir", root, "--test"])
+    V, R, train, valid, test = cli.load_dataset(args)
+    assert (V, R) == (int(z["num_nodes"]), int(z["num_rels"]))
+    for name, arr in (("train", train), ("valid", valid), ("test", test)):
+        np.testing.assert_array_equal(arr, z[name])
+        snaps = ranking.split_by_time(arr)
+        np.testing.assert_array_equal([len(s) for s in snaps], z[name + "_snap_len"])
+        np.testing.assert_array_equal(np.concatenate(snaps), z[name + "_snaps"])

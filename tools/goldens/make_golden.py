@@ -15,6 +15,7 @@ Each fixture pins one row of SURVEY.md §8(a):
   layer_euclid.npz     a5  UnionRGCNLayer                    rgcn/layers.py:182-279
   layer_lorentz.npz    a6  LorentzRGCNLayer                  hyperbolic_layers.py:524-694
   model_*.npz          a9  HyperbolicRecurrentRGCN.predict / get_loss   hyperbolic_model.py:722-1088
+                           (models_large: d = 200 at the ICEWS18 / GDELT shapes, predict only)
   rrgcn_*.npz          a9  RecurrentRGCN.predict             src/rrgcn.py:142-194
   score.npz            a11/a12 chunked dist score / CE       hyperbolic_decoder.py:89-307
   rank.npz             f2  get_total_rank / filter_score     rgcn/utils.py:21-166
@@ -22,6 +23,9 @@ Each fixture pins one row of SURVEY.md §8(a):
                            (the --multi-step history roll)   rgcn/utils.py:51-75, 367-405;
                                                              hyperbolic_main.py:116-149
   train_*.npz          f1  get_loss + backward: every parameter gradient   hyperbolic_main.py:585-598
+  tkg_tiny/ + dataset_tiny.npz  f4  load_from_local + split_by_time on a dataset directory
+                                                             knowledge_graph.py:189-206, 526-555;
+                                                             rgcn/utils.py:306-339
 """
 import os
 import sys
@@ -318,6 +322,62 @@ def gen_models():
         save("model_%s.npz" % tag, **out)
 
 
+# Dataset-shaped model goldens at d = 200: the ICEWS18 relation
+# count (R2 = 512) with hub rows over the fused kernel's inline budget, the same at |E| = 80k
+# (the large-snapshot work lists: short chunks, small budget, many pre-aggregated rows), and
+# the GDELT history length 7 for both encoders.  Only the last history embedding is stored.
+LARGE_CASES = [
+    ("uvrgcn_roth_r512_d200", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False),
+     dict(V=1536, R=256, T=3, per_snap=2500, n_test=64, seed=50)),
+    ("uvrgcn_roth_e80k_d200", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False),
+     dict(V=2048, R=256, T=3, per_snap=40000, n_test=64, seed=51)),
+    ("uvrgcn_roth_h7_d200", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False),
+     dict(V=1024, R=240, T=7, per_snap=770, n_test=128, seed=52)),
+    ("lgcn_roth_h7_d200", dict(encoder_name="lgcn", decoder_name="roth", layer_norm=True),
+     dict(V=1024, R=240, T=7, per_snap=770, n_test=128, seed=53)),
+]
+
+
+def gen_models_large():
+    d = 200
+    for i, (tag, kw, sz) in enumerate(LARGE_CASES):
+        V, R, T = sz["V"], sz["R"], sz["T"]
+        snaps = snapshot_series(sz["seed"], V, R, T + 1, sz["per_snap"])
+        rng = np.random.default_rng(sz["seed"] + 100)
+        radius_target = rng.uniform(0.5, 3.0, size=V).astype(np.float32)
+        glist = [rutils.build_sub_graph(V, R, s, False, "cpu") for s in snaps[:T]]
+        test_np = snaps[T][:sz["n_test"]]
+        test = torch.from_numpy(test_np)
+        torch.manual_seed(500 + i)
+        base = dict(num_ents=V, num_rels=R, num_static_rels=0, num_words=0, h_dim=d, opn="sub",
+                    sequence_len=T, num_bases=d // 2, num_hidden_layers=2, dropout=0.2, c=C,
+                    self_loop=True, skip_connect=False, input_dropout=0.2, hidden_dropout=0.2,
+                    feat_dropout=0.2, entity_prediction=True, relation_prediction=True,
+                    use_cuda=False, gpu="cpu", radius_target=radius_target, radius_msg_gamma=0.15)
+        base.update(kw)
+        m = HyperbolicRecurrentRGCN(**base)
+        with torch.no_grad():
+            for mod in (m.decoder_ob, m.rdecoder):
+                if hasattr(mod, "score_margin"):
+                    mod.score_margin.fill_(0.7)
+                    mod.score_scale_raw.fill_(0.4)
+                if getattr(mod, "rel_bias", None) is not None:
+                    mod.rel_bias.normal_(0, 0.1)
+            m.radius_static.add_(torch.randn(V) * 0.2)
+        m.eval()
+        with torch.no_grad():
+            embs, _, h0, _, _ = m.forward(glist, None, False)
+            all_tr, score, score_rel = m.predict(glist, R, None, test.clone(), False)
+        out = {"meta": np.array([V, R, d, T]), "test": test_np, "all_triples": all_tr.numpy(),
+               "score": score.numpy(), "score_rel": score_rel.numpy(), "h0": h0.numpy(),
+               "embs_last": embs[-1].numpy(), "radius_target": radius_target}
+        for t in range(T):
+            out["snap%d" % t] = snaps[t].astype(np.int32)  # ids < 2^31: half the fixture
+        for k, v in m.state_dict().items():
+            out["sd_" + k] = v.numpy().copy()
+        save("model_%s.npz" % tag, **out)
+
+
 TRAIN_CASES = [
     ("uvrgcn_roth", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False)),
     ("lgcn_roth", dict(encoder_name="lgcn", decoder_name="roth", layer_norm=False)),
@@ -497,6 +557,44 @@ def gen_rank():
          mrr=np.array([mrr, mrr_f, mrr_r, mrr_fr]), meta=np.array([V, R]))
 
 
+def gen_dataset():
+    """A tiny dataset directory in the reference's on-disk format (knowledge_graph.py:189-206,
+    :526-555) and what the reference's load_from_local + split_by_time (rgcn/utils.py:306-339)
+    make of it.  entity2id.txt repeats one id under two names (num_nodes = len of the dict
+    keyed by id, not the line count); the time column starts at a nonzero t and holds a
+    one-triple snapshot."""
+    from rgcn import knowledge_graph as kg
+    root = os.path.join(OUT, "tkg_tiny")
+    os.makedirs(root, exist_ok=True)
+    rng = np.random.default_rng(7)
+    V, R = 40, 6
+    names = ["ent_%d" % i for i in range(V)] + ["ent_alias_7"]
+    ids = list(range(V)) + [7]
+    with open(os.path.join(root, "entity2id.txt"), "w") as f:
+        f.writelines("%s\t%d\n" % (n, i) for n, i in zip(names, ids))
+    with open(os.path.join(root, "relation2id.txt"), "w") as f:
+        f.writelines("rel_%d\t%d\n" % (i, i) for i in range(R))
+    t0 = 3
+    splits = {"train": (0, 6), "valid": (6, 8), "test": (8, 10)}
+    for name, (a, b) in splits.items():
+        rows = []
+        for t in range(a, b):
+            n = 1 if t == 4 else int(rng.integers(5, 15))
+            tr = np.stack([rng.integers(0, V, n), rng.integers(0, R, n), rng.integers(0, V, n)], 1)
+            rows += [(int(x[0]), int(x[1]), int(x[2]), t0 + 24 * t) for x in tr]
+        with open(os.path.join(root, name + ".txt"), "w") as f:
+            f.writelines("%d\t%d\t%d\t%d\t0\n" % r for r in rows)
+    data = kg.load_from_local(OUT, "tkg_tiny")
+    out = {"num_nodes": np.array(data.num_nodes), "num_rels": np.array(data.num_rels)}
+    for name in splits:
+        arr = getattr(data, name)
+        snaps = rutils.split_by_time(arr)
+        out[name] = arr
+        out[name + "_snap_len"] = np.array([len(x) for x in snaps])
+        out[name + "_snaps"] = np.concatenate(snaps)
+    save("dataset_tiny.npz", **out)
+
+
 def gen_multistep():
     """get_total_rank filters `score` in place; --multi-step builds the next history
     snapshot from those filtered scores (hyperbolic_main.py:116-149)."""
@@ -527,6 +625,7 @@ if __name__ == "__main__":
     table = {"graph": gen_graph_indexing, "ops": gen_ops, "union": gen_layer_union,
              "euclid": gen_layer_euclid, "lorentz": gen_layer_lorentz, "models": gen_models,
              "rrgcn": gen_rrgcn, "score": gen_score, "rank": gen_rank, "train": gen_train,
+             "models_large": gen_models_large, "dataset": gen_dataset,
              "multistep": gen_multistep}
     for w in which:
         table[w]()
