@@ -124,6 +124,10 @@ def build_parser():
     a("--synthetic-snapshots", type=int, default=12, help="snapshots generated for -d synthetic:<config>")
     a("--seed", type=int, default=None, help="seed python/numpy/torch RNGs (snapshot shuffle, dropout, init)")
     a("--max-train-snapshots", type=int, default=None, help="train on at most this many snapshots per epoch")
+    a("--shard", type=str, default="none", choices=["none", "owner", "edge"],
+      help="--test with several ranks (torchrun): partition every snapshot over the ranks (destination "
+           "owners + all-gather, or edge slices + all-reduce) and the entity candidates of the decoder "
+           "(SURVEY.md §8(e)); default: rank 0 evaluates alone")
     return p
 
 
@@ -213,6 +217,8 @@ def test(model, history_list, test_list, num_rels, num_nodes, device, all_ans_li
     """hyperbolic_main.py:60-161: roll the history window over the test snapshots, predict,
     rank (raw + time-filtered; entity and relation), return the four MRRs."""
     ranks_raw, ranks_filter, ranks_raw_r, ranks_filter_r = [], [], [], []
+    import torch.distributed as dist
+    shard = getattr(args, "shard", "none") if dist.is_initialized() and dist.get_world_size() > 1 else "none"
     model.eval()
     input_list = [snap for snap in history_list[-args.test_history_len:]]
     graphs = {}
@@ -224,16 +230,27 @@ def test(model, history_list, test_list, num_rels, num_nodes, device, all_ans_li
             for s in input_list:  # snapshot graphs cached by identity across the window
                 key = id(s)
                 if key not in graphs:
-                    graphs[key] = (s, build_sub_graph(num_nodes, num_rels, s, True, device))
+                    g = build_sub_graph(num_nodes, num_rels, s, True, device)
+                    if shard != "none":
+                        from .parallel import ShardedGraph
+                        g = ShardedGraph(g, shard)
+                    graphs[key] = (s, g)
                 glist.append(graphs[key][1])
             tt = torch.from_numpy(np.asarray(test_snap, dtype=np.int64)).to(device)
-            test_triples, score, score_r = model.predict(glist, num_rels, None, tt, True)
-            _, _, rr, fr = ranking.get_total_rank(test_triples, score_r, all_ans_r_list[time_idx], 1000, 1)
+            if shard != "none":  # partitioned snapshots and candidate-sharded entity ranks
+                test_triples, (re_, fe), (rr, fr) = model.predict_ranks(
+                    glist, num_rels, None, tt, True, all_ans_list[time_idx], all_ans_r_list[time_idx])
+                score = score_r = None
+            else:
+                test_triples, score, score_r = model.predict(glist, num_rels, None, tt, True)
+                _, _, rr, fr = ranking.get_total_rank(test_triples, score_r, all_ans_r_list[time_idx], 1000, 1)
+                _, _, re_, fe = ranking.get_total_rank(test_triples, score, all_ans_list[time_idx], 1000, 0)
             ranks_raw_r.append(rr)
             ranks_filter_r.append(fr)
-            _, _, re_, fe = ranking.get_total_rank(test_triples, score, all_ans_list[time_idx], 1000, 0)
             ranks_raw.append(re_)
             ranks_filter.append(fe)
+            if args.multi_step and score is None:
+                raise SystemExit("--multi-step builds the next history from the full score matrix: not with --shard")
             if args.multi_step:
                 pred = (ranking.construct_snap_r(test_triples, num_nodes, num_rels, score_r, args.topk)
                         if args.relation_evaluation else
@@ -433,7 +450,8 @@ def main(argv=None):
     if not args.test:
         train_model(args, model, train_list, valid, num_nodes, num_rels, device, model_state_file)
         args.checkpoint = model_state_file if os.path.exists(model_state_file) else None
-    if world > 1:  # the test pass runs on rank 0
+    sharded_test = world > 1 and args.shard != "none"
+    if world > 1 and not sharded_test:  # the test pass runs on rank 0
         import torch.distributed as dist
         dist.barrier()
         rank = dist.get_rank()
@@ -447,6 +465,10 @@ def main(argv=None):
     t0 = time.time()
     res = test(model, train_list + valid_list, test_list, num_rels, num_nodes, device, all_ans, all_ans_r, args)
     logger.info("MRR raw %.6f filter %.6f | relation raw %.6f filter %.6f | %.2f s", *res, time.time() - t0)
+    if sharded_test:  # every rank took part in the partitioned test pass
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
     return res
 
 

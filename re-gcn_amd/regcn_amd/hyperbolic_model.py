@@ -763,6 +763,51 @@ class HyperbolicRecurrentRGCN(nn.Module):
             score, score_rel = self._decode_both(embedding, r_emb, at)
             return all_triples, score, score_rel
 
+    def predict_ranks(self, test_graph, num_rels, static_graph, test_triplets, use_cuda, all_ans=None,
+                      all_ans_r=None):
+        """predict followed by the evaluation loop's two get_total_rank calls
+        (hyperbolic_main.py:111-121, rgcn/utils.py:136-166).  Returns (all_triples,
+        (rank, filtered rank) of the entity queries, (rank, filtered rank) of the relation
+        queries), 1-based.  When the snapshots are partitioned over several ranks
+        (parallel.ShardedGraph), each rank scores only its contiguous slice of the entity
+        candidates (parallel.CandidateShard): the target score on every rank, the per-slice
+        count of candidates above it (raw and with the slice's part of the time-aware filter),
+        ONE all-reduce of 2B counts -- no rank scores all N entities (SURVEY.md §8(e) decoder).
+        The relation decoder (2R candidates) runs replicated.  Ranks equal the unsharded ones."""
+        from . import ranking
+        from .parallel import CandidateShard, ShardedGraph
+        sharded = [g for g in test_graph if isinstance(g, ShardedGraph) and g.world > 1]
+        if not sharded:
+            all_tr, score, score_rel = self.predict(test_graph, num_rels, static_graph, test_triplets, use_cuda)
+            r_e, f_e = ranking.get_total_rank(all_tr, score, all_ans, 1000, 0)[2:]
+            r_r, f_r = ranking.get_total_rank(all_tr, score_rel, all_ans_r, 1000, 1)[2:]
+            return all_tr, (r_e, f_e), (r_r, f_r)
+        dec = self.decoder_ob
+        if not hasattr(dec, "_query") or dec.use_relation_specific_curvature:
+            raise NotImplementedError("candidate-sharded ranking needs a MuRP / RotH / AttH decoder with the proxy "
+                                      "distance score")
+        sg = sharded[0]
+        with torch.no_grad():
+            c_val = self._c_float()
+            embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
+            emb = self._final_embedding(embs[-1], c_val).contiguous()
+            inv = test_triplets.flip(1)
+            inv[:, 1] = inv[:, 1] + num_rels
+            at = torch.cat([test_triplets, inv])
+            q = dec._query(emb, r_emb, at)
+            shard = CandidateShard(emb.shape[0], sg.rank, sg.world, sg.group)
+            kw = dict(scale=dec.score_scale_raw, margin=dec.score_margin, raw_scale=True)
+            # the candidates' entity_bias[n] as in the full scoring; the decoder's extra
+            # entity_bias[s] shifts a whole query row alike, so the ranks do not see it
+            bias = dec.entity_bias.detach() if dec.entity_bias is not None else None
+            local = shard.scores(q, emb, bias, dec.c, **kw)
+            ts = shard.target_scores(q, emb, bias, at[:, 2], dec.c, **kw)
+            fp, fi = ranking._filter_csr(at, all_ans, False)
+            r_e, f_e = shard.ranks(local, ts, fp, fi)
+            score_rel = self.rdecoder.forward(emb, r_emb, at, mode="test")
+            r_r, f_r = ranking.get_total_rank(at, score_rel, all_ans_r, 1000, 1)[2:]
+        return at, (r_e, f_e), (r_r, f_r)
+
     def _side(self, dev, k=1):
         """Side stream k of the calling stream (1: relation decoder / query triples / cold
         rows): keyed by the current stream, so predicts issued on different streams (e.g.

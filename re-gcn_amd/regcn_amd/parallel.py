@@ -36,24 +36,26 @@ class EdgePlan:
     `finish` = {row, row, row + 1} for every row with in-degree > 0 (identical on all ranks)."""
 
     def __init__(self, g, rank, world):
-        h = g._host
-        rowptr = h["rowptr"].astype(np.int64)
+        rowptr = g.work()["rowptr"].cpu().numpy().astype(np.int64) if g.dev is not None \
+            else g._host["rowptr"].astype(np.int64)
         V = g.number_of_nodes()
         E = int(rowptr[-1])
         self.e0, self.e1 = even_bounds(E, world)[rank:rank + 2]
         ce = g.chunk_edges
+        # the rows the slice touches, cut into chunks of <= ce edges (vectorised: ~1M rows
+        # at config 5), slots numbered in chunk order, one fix-up per touched row
         rows = np.nonzero((rowptr[:-1] < self.e1) & (rowptr[1:] > self.e0))[0]
         beg = np.maximum(rowptr[rows], self.e0)
         end = np.minimum(rowptr[rows + 1], self.e1)
-        chunks, fix, slot = [], [], 0
-        for r, b, e in zip(rows.tolist(), beg.tolist(), end.tolist()):
-            k = (e - b + ce - 1) // ce
-            for i in range(k):
-                chunks.append((r, b + i * ce, min(b + (i + 1) * ce, e), slot + i))
-            fix.append((r, slot, slot + k, 0))
-            slot += k
-        self.chunks = np.asarray(chunks, dtype=np.int32).reshape(-1, 4)
-        self.fixups, self.n_slots = group_fixups(fix, slot)
+        k = (end - beg + ce - 1) // ce
+        first = np.cumsum(k) - k
+        total = int(k.sum())
+        i = np.arange(total, dtype=np.int64) - np.repeat(first, k)
+        c_beg = np.repeat(beg, k) + i * ce
+        c_end = np.minimum(c_beg + ce, np.repeat(end, k))
+        self.chunks = np.stack([np.repeat(rows, k), c_beg, c_end, np.arange(total)], 1).astype(np.int32).reshape(-1, 4)
+        fix = np.stack([rows, first, first + k, np.zeros_like(k)], 1).astype(np.int32).reshape(-1, 4)
+        self.fixups, self.n_slots = group_fixups(fix, total)
         pos = np.nonzero(np.diff(rowptr) > 0)[0]
         self.finish = np.stack([pos, pos, pos + 1, np.zeros_like(pos)], 1).astype(np.int32).reshape(-1, 4)
         self.V = V
@@ -71,12 +73,15 @@ def owner_bounds(V, world):
 
 class OwnerView:
     """A rank's view of a snapshot under the owner partition: the global CSR and relation
-    spans, and the fused-kernel work lists of its node block only."""
+    spans, and the fused-kernel work lists of its node block only (or of rows [r0, r1) of
+    that block: a pipeline chunk, see ShardedGraph)."""
 
-    def __init__(self, g, rank, world):
+    def __init__(self, g, rank, world, r0=0, r1=None):
         self.g = g
         self.per, b = owner_bounds(g.number_of_nodes(), world)
-        self.v0, self.v1 = b[rank], b[rank + 1]
+        v0, v1 = b[rank], b[rank + 1]
+        self.v0 = min(v1, v0 + r0)
+        self.v1 = v1 if r1 is None else min(v1, v0 + r1)
         h = g._host
         fw = fused_work(np.arange(self.v0, self.v1), g.in_deg_np, h["rowptr"].astype(np.int64),
                         h["col_src"].astype(np.int64), h["col_type"].astype(np.int64), g.budget, g.pack_items,
@@ -112,8 +117,40 @@ def allgather_rows(full, per, group=None):
     if dist.is_initialized() and dist.get_world_size(group) > 1:
         rank = dist.get_rank(group)
         chunk = full[rank * per:(rank + 1) * per].clone()
-        dist.all_gather_into_tensor(full, chunk, group=group)
+        _all_gather_into(full, chunk, group)
     return full
+
+
+def _all_gather_into(out, chunk, group=None):
+    """all_gather_into_tensor; a gloo group (CPU tests, ranks sharing one GPU in the GPU
+    tests) gathers through host tensors."""
+    if dist.get_backend(group) == "gloo":
+        parts = [torch.empty_like(chunk, device="cpu") for _ in range(dist.get_world_size(group))]
+        dist.all_gather(parts, chunk.cpu(), group=group)
+        out.copy_(torch.cat(parts).to(out.device))
+    else:
+        dist.all_gather_into_tensor(out, chunk, group=group)
+
+
+def allgather_fused(tensors, per, rows=None, group=None):
+    """One collective for several row-aligned tensors (h, log0 h, |h| of the owner
+    partition): this rank's rows `rows` (a slice of its block, default all `per`) of every
+    tensor packed into one (n, W) buffer, ONE all_gather, unpacked into the same rows of
+    every rank's block.  Each tensor is (world * per, ...) ."""
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return tensors
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    a, b = (0, per) if rows is None else (rows.start, rows.stop)
+    flat = [t.view(world, per, -1) for t in tensors]
+    send = torch.cat([f[rank, a:b] for f in flat], 1).contiguous()
+    recv = torch.empty(world, b - a, send.shape[1], device=send.device, dtype=send.dtype)
+    _all_gather_into(recv.view(world * (b - a), -1), send, group)
+    off = 0
+    for f in flat:
+        w = f.shape[2]
+        f[:, a:b].copy_(recv[:, :, off:off + w])
+        off += w
+    return tensors
 
 
 # ---------------------------------------------------------------------- sharded layers
@@ -122,7 +159,11 @@ class ShardedGraph:
     Everything but the message-passing layers (relation spans, degrees, ...) is the
     wrapped graph's."""
 
-    def __init__(self, g, partition="owner", group=None, rank=None, world=None):
+    # owner partition: a rank's rows run as this many launches, each one's rows all-gathered
+    # on a side stream while the next launch computes (auto: 4 from 64k rows per rank)
+    pipeline_chunks = None
+
+    def __init__(self, g, partition="owner", group=None, rank=None, world=None, chunks=None):
         if partition not in ("edge", "owner"):
             raise ValueError("partition must be 'edge' or 'owner'")
         self.g, self.partition, self.group = g, partition, group
@@ -133,6 +174,14 @@ class ShardedGraph:
         self.rank, self.world = rank, world
         self.plan = EdgePlan(g, rank, world).to(g.device) if partition == "edge" else None
         self.view = OwnerView(g, rank, world) if partition == "owner" else None
+        self.views = []
+        if partition == "owner":
+            per = self.view.per
+            k = chunks or self.pipeline_chunks or (4 if per >= 65536 and world > 1 else 1)
+            cr = -(-per // k)
+            self.views = [(slice(j * cr, min(per, (j + 1) * cr)), OwnerView(g, rank, world, j * cr, (j + 1) * cr))
+                          for j in range(k) if j * cr < per] if k > 1 else [(slice(0, per), self.view)]
+        self._comm = None
 
     def __getattr__(self, name):  # delegate the DGL-visible surface and work lists
         return getattr(self.__dict__["g"], name)
@@ -211,10 +260,28 @@ class ShardedGraph:
         h = torch.empty(Vp, d, device=x.device, dtype=torch.float32)
         xn = torch.empty(Vp, d, device=x.device, dtype=torch.float32)
         rn = torch.empty(Vp, device=x.device, dtype=torch.float32)
-        run_layer(mode, self.view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                  drop_mask, c, euclid=euclid, step=step, out=(h[:V], xn[:V], rn[:V]))
-        for t in (h, xn, rn):
-            allgather_rows(t, per, self.group)
+        # the rank's rows in pipeline chunks: chunk j's rows (h | log0 h | |h|) are all-gathered
+        # in ONE collective on a side stream while chunk j + 1 computes (SURVEY.md §8(e):
+        # partitioning 2 with overlap)
+        cur = torch.cuda.current_stream(x.device) if x.is_cuda else None
+        comm = None
+        if cur is not None and len(self.views) > 1 and self.world > 1:
+            if self._comm is None:
+                self._comm = torch.cuda.Stream(x.device)
+            comm = self._comm
+        for rows, view in self.views:
+            run_layer(mode, view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
+                      drop_mask, c, euclid=euclid, step=step, out=(h[:V], xn[:V], rn[:V]))
+            if comm is None:
+                allgather_fused((h, xn, rn), per, rows, self.group)
+                continue
+            comm.wait_stream(cur)
+            with torch.cuda.stream(comm):
+                allgather_fused((h, xn, rn), per, rows, self.group)
+        if comm is not None:
+            cur.wait_stream(comm)
+            for t in (h, xn, rn):
+                t.record_stream(comm)
         return h[:V], xn[:V], rn[:V]
 
 
@@ -268,20 +335,22 @@ class CandidateShard:
         c = cand[self.n0:self.n1].contiguous()
         return c, (bias[self.n0:self.n1].contiguous() if bias is not None else None)
 
-    def scores(self, q, cand, bias, c, scale=None, margin=0.0):
-        """Scores of every query against this slice, (B, n1 - n0)."""
+    def scores(self, q, cand, bias, c, scale=None, margin=0.0, raw_scale=False):
+        """Scores of every query against this slice, (B, n1 - n0).  raw_scale: `scale` is
+        score_scale_raw (softplus on the device, as the unsharded predict scores)."""
         from .hyperbolic_decoder import _chunked_hyperbolic_dist_score
         cs, bs = self._slice(cand, bias)
-        return _chunked_hyperbolic_dist_score(q, cs, bs, c, 0, 0, score_scale=scale, score_margin=margin)
+        return _chunked_hyperbolic_dist_score(q, cs, bs, c, 0, 0, score_scale=scale, score_margin=margin,
+                                              _raw_scale=raw_scale)
 
-    def target_scores(self, q, cand, bias, target, c, scale=None, margin=0.0):
+    def target_scores(self, q, cand, bias, target, c, scale=None, margin=0.0, raw_scale=False):
         """S(q_b, e_{t_b}) for every query (the diagonal of a B x B scoring of the target rows:
         the same MFMA k-order and norm order as in the full scoring, so the same bits)."""
         from .hyperbolic_decoder import _chunked_hyperbolic_dist_score
         t = target.to(cand.device).long()
         tb = bias[t].contiguous() if bias is not None else None
         S = _chunked_hyperbolic_dist_score(q, cand[t].contiguous(), tb, c, 0, 0, score_scale=scale,
-                                           score_margin=margin)  # column j carries bias[t_j]
+                                           score_margin=margin, _raw_scale=raw_scale)  # column j carries bias[t_j]
         return torch.diagonal(S).contiguous()
 
     def local_lse(self, q, cand, bias, c, scale=None, margin=0.0):

@@ -109,6 +109,18 @@ def _worker(rank, world, port, result_q):
         buf[bounds[rank]:bounds[rank + 1]] = ref[bounds[rank]:bounds[rank + 1]]
         P.allgather_rows(buf, per)
         err_owner = float((buf[:V] - ref).abs().max())
+        # the owner partition's fused, pipelined exchange: (h | x | r) rows of two row chunks
+        # of the block, one collective each
+        h = torch.full((per * world, d), float("nan"))
+        xx = torch.full((per * world, d), float("nan"))
+        rr = torch.full((per * world,), float("nan"))
+        lo, hi = bounds[rank], bounds[rank + 1]
+        h[lo:hi], xx[lo:hi], rr[lo:hi] = ref[lo:hi], -ref[lo:hi], ref[lo:hi, 0]
+        half = per // 2
+        for rows in (slice(0, half), slice(half, per)):
+            P.allgather_fused((h, xx, rr), per, rows)
+        err_owner = max(err_owner, float((h[:V] - ref).abs().max()), float((xx[:V] + ref).abs().max()),
+                        float((rr[:V] - ref[:, 0]).abs().max()))
         result_q.put((rank, err_edge, err_owner))
     finally:
         dist.destroy_process_group()
