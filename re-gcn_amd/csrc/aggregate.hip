@@ -290,23 +290,38 @@ __global__ __launch_bounds__(256) void k_lorentz_sum(
         constexpr int EB = S == 4 ? 4 : 8;
         const uint32_t xoff = (uint32_t)min(col, d - 4) * 4u, woff = xoff * S;
         const float amask = active ? 1.f : 0.f;
+        // A batch inside one relation-type run (the row/type edge order makes a hub row's
+        // edges a few long runs) loads the run's block weights and relation row once for its
+        // EB edges: 0.8 KB + 2.4 KB / EB per edge from L2 instead of 3.2 KB (vector-memory
+        // request rate, not HBM, bounded it).  Same arithmetic per edge as the general path.
         for (; j + EB <= n; j += EB) {
-          f4 xs[EB], rv[EB];
-          WFrag<S> wf[EB];
+          f4 xs[EB], m[EB];
+          const int t_first = rl(my_t, j);
+          const uint64_t want = ((1ull << EB) - 1ull) << j;
+          if ((__ballot(my_t == t_first) & want) == want) {  // wave-uniform
+            WFrag<S> wr;
+            wr.load_row(W + (int64_t)t_first * wstride, woff);
+            const f4 rr = row_load4(rel + (int64_t)t_first * d, xoff);
 #pragma unroll
-          for (int u = 0; u < EB; ++u) {
-            const int src = rl(my_s, j + u), typ = rl(my_t, j + u);
-            xs[u] = row_load4(x + (int64_t)src * d, xoff);
-            rv[u] = row_load4(rel + (int64_t)typ * d, xoff);
-            wf[u].load_row(W + (int64_t)typ * wstride, woff);
+            for (int u = 0; u < EB; ++u) xs[u] = row_load4(x + (int64_t)rl(my_s, j + u) * d, xoff);
+#pragma unroll
+            for (int u = 0; u < EB; ++u) m[u] = wr.apply(xs[u]) + rr;
+          } else {
+            f4 rv[EB];
+            WFrag<S> wf[EB];
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+              const int src = rl(my_s, j + u), typ = rl(my_t, j + u);
+              xs[u] = row_load4(x + (int64_t)src * d, xoff);
+              rv[u] = row_load4(rel + (int64_t)typ * d, xoff);
+              wf[u].load_row(W + (int64_t)typ * wstride, woff);
+            }
+#pragma unroll
+            for (int u = 0; u < EB; ++u) m[u] = wf[u].apply(xs[u]) + rv[u];
           }
-          f4 m[EB];
           float q[EB];
 #pragma unroll
-          for (int u = 0; u < EB; ++u) {
-            m[u] = wf[u].apply(xs[u]) + rv[u];
-            q[u] = dot4(m[u], m[u]) * amask;
-          }
+          for (int u = 0; u < EB; ++u) q[u] = dot4(m[u], m[u]) * amask;
           const float n2l = batch_sums<EB>(q, lane);
           float p2;  // lorentz_accum (gather.h), lane-parallel over the batch
           const float f = exp0_factor(n2l, k, &p2);
