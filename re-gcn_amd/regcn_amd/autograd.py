@@ -14,7 +14,16 @@ with the gradients torch autograd would compute through the reference's op seque
     -> regcn_hyp_ce_lse_f32 / regcn_hyp_ce_bwd_f32 (+ dq, de on regcn_kreduce_gemm_f32);
   * the weight gradients of the (V x d) @ (d x d) products -> regcn_kreduce_gemm_f32.
 
-The curvature is a constant here (a learned curvature's gradient is not built).
+A learned curvature (--learn-curvature, hyperbolic_model.py:299-300, :673-679) arrives as a
+0-dim tensor `c` with requires_grad.  The reference lets its gradient flow through exp0,
+log0, mobius_add and the decoders' scores, not through the project / apply_radius bounds (they
+read c.item(), hyperbolic_ops.py:72, :228).  The row maps are radial (y = s(|x|, c) x) or, for
+mobius_add, y = alpha(c) x + beta(c) y per row, so the HIP kernels keep the x-gradients and
+the c-gradient is added by a zero-valued term (s(c) - s(c).detach()) x.detach() built from
+per-row scalars on the device; the cross entropy gets the same from the per-pair scalars
+(<q, e>, |q|^2, |e|^2) of its score.  The arctanh-distance score with per-query curvatures
+(--plus-relation-specific-curvature, hyperbolic_decoder.py:145-164, :257-283) trains through
+the same per-pair scalars in float64 (hyp_dist_ce_loss).
 """
 import ctypes
 import functools
@@ -33,11 +42,24 @@ def needs_grad(*ts):
 
 
 def _cf(c):
-    if torch.is_tensor(c):
-        if c.requires_grad:
-            raise NotImplementedError("the gradient of a learned curvature is not built (SURVEY.md §8(f) f1)")
-        return float(c.item())
-    return float(c)
+    return float(c.detach().item()) if torch.is_tensor(c) else float(c)
+
+
+def _c_grad(c):
+    """A learned curvature whose gradient this call must produce."""
+    return torch.is_tensor(c) and c.requires_grad and torch.is_grad_enabled()
+
+
+def _mx(c):
+    """The project / clamp_norm bound 1/sqrt(c) - 2 eps as a constant (the reference reads
+    c.item() there, hyperbolic_ops.py:72-74, :52)."""
+    return 1.0 / (_cf(c) ** 0.5) - 2 * EPS
+
+
+def _c_term(y, x, factor):
+    """y + (factor - factor.detach()) x.detach(): the value of y, plus d/dc of the radial factor."""
+    f = factor - factor.detach()
+    return y + (f.to(y.dtype).unsqueeze(-1) * x.detach().reshape(y.shape))
 
 
 def _rows(x):
@@ -127,11 +149,24 @@ class _Mobius(torch.autograd.Function):
 
 
 def log0(x, c):
-    return _Radial.apply(x, "log0", _cf(c))
+    y = _Radial.apply(x, "log0", _cf(c))
+    if _c_grad(c):  # atanh(min(sqrt(c) n, 1 - eps)) / (sqrt(c) n), n = max(|x|, eps)  (:97-116)
+        sc = torch.sqrt(c)
+        n = x.detach().norm(dim=-1).clamp(min=EPS)
+        y = _c_term(y, x, torch.atanh((sc * n).clamp(max=1.0 - EPS)) / (sc * n))
+    return y
 
 
 def exp0(x, c):
-    return _Radial.apply(x, "exp0", _cf(c))
+    y = _Radial.apply(x, "exp0", _cf(c))
+    if _c_grad(c):  # tanh(sqrt(c) n) / (sqrt(c) n), then project with a constant bound  (:76-95)
+        sc = torch.sqrt(c)
+        vn = x.detach().norm(dim=-1)
+        n = vn.clamp(min=EPS)
+        s = torch.tanh(sc * n) / (sc * n)
+        pn = (s * vn).clamp(min=EPS)
+        y = _c_term(y, x, s * pn.clamp(max=_mx(c)) / pn)
+    return y
 
 
 def project(x, c):
@@ -147,7 +182,20 @@ def get_radius(x):
 
 
 def mobius_add(x, y, c):
-    return _Mobius.apply(x, y.expand_as(x), _cf(c))
+    y = y.expand_as(x)
+    out = _Mobius.apply(x, y, _cf(c))
+    if _c_grad(c):  # out = p (a x + b y) / den, p the project factor of that row  (:118-143)
+        xd, yd = x.detach(), y.detach()
+        x2, y2, xy = (xd * xd).sum(-1), (yd * yd).sum(-1), (xd * yd).sum(-1)
+        a = 1 + 2 * c * xy + c * y2
+        b = 1 - c * x2
+        den = 1 + 2 * c * xy + c * c * x2 * y2 + EPS
+        rn = ((a * a * x2 + 2 * a * b * xy + b * b * y2).clamp(min=1e-30)).sqrt() / den.abs()
+        pn = rn.clamp(min=EPS)
+        pf = pn.clamp(max=_mx(c)) / pn
+        out = _c_term(out, x, pf * a / den)
+        out = _c_term(out, y, pf * b / den)
+    return out
 
 
 # ------------------------------------------------------------------------ edge aggregation
@@ -331,11 +379,84 @@ class _HypCE(torch.autograd.Function):
         return dq, de, dbias, dscale, dmargin, None, None
 
 
+def _const(v, like):
+    """A device scalar from a python number by a fill kernel (no host-to-device copy, so a
+    training step holding it stays capturable in a HIP graph)."""
+    return torch.full((), float(v), device=like.device, dtype=torch.float32)
+
+
+def _pair_terms(q, e, c):
+    """Per pair (b, n): |project((-q_b) (+)_c e_n)|^2 from the per-pair scalars <q, e>, |q|^2,
+    |e|^2 (float64; the bound of project a constant), with c a tensor."""
+    xy = -(q @ e.t())
+    x2 = (q * q).sum(1, keepdim=True)
+    y2 = (e * e).sum(1).unsqueeze(0)
+    a = 1 + 2 * c * xy + c * y2
+    b = 1 - c * x2
+    den = 1 + 2 * c * xy + c * c * x2 * y2 + EPS
+    n2 = (a * a * x2 + 2 * a * b * xy + b * b * y2) / (den * den)
+    pn = n2.clamp(min=1e-30).sqrt().clamp(min=EPS)
+    pf = pn.clamp(max=_mx(c)) / pn
+    return n2 * pf * pf
+
+
+def _ce_c_term(q, cand, target, c, bias, scale, margin, chunk=65536):
+    """Zero-valued term whose gradient is d(mean CE)/dc of the proxy score: sum_bn G_bn
+    (S_bn(c) - S_bn(c).detach()) / B with G = softmax - one-hot from the same scores."""
+    qd, ed = q.detach().double(), cand.detach().double()
+    cd = c.double()
+    sc = scale.detach().double()
+    mg = margin.detach().double()
+    B, N = qd.shape[0], ed.shape[0]
+    S = torch.empty(B, N, device=q.device, dtype=torch.float64)
+    parts = []
+    for n0 in range(0, N, chunk):
+        n1 = min(N, n0 + chunk)
+        Sc = sc * (mg - _pair_terms(qd, ed[n0:n1], cd))
+        if bias is not None:
+            Sc = Sc + bias.detach().double()[n0:n1]
+        S[:, n0:n1] = Sc.detach()
+        parts.append((n0, n1, Sc))
+    G = torch.softmax(S, dim=1)
+    G[torch.arange(B, device=q.device), target.long()] -= 1.0
+    G /= B
+    return sum((G[:, n0:n1] * (Sc - Sc.detach())).sum() for n0, n1, Sc in parts).float()
+
+
 def hyp_ce_loss(q, cand, target, c, bias=None, scale=None, margin=None):
     """mean over queries of the CE loss (hyperbolic_decoder.py:182-307, proxy score)."""
-    scale = scale if torch.is_tensor(scale) else q.new_tensor(1.0 if scale is None else float(scale))
-    margin = margin if torch.is_tensor(margin) else q.new_tensor(0.0 if margin is None else float(margin))
-    return _HypCE.apply(q, cand, bias, scale, margin, target, _cf(c)).mean()
+    scale = scale if torch.is_tensor(scale) else _const(1.0 if scale is None else scale, q)
+    margin = margin if torch.is_tensor(margin) else _const(0.0 if margin is None else margin, q)
+    loss = _HypCE.apply(q, cand, bias, scale, margin, target, _cf(c)).mean()
+    if _c_grad(c):
+        loss = loss + _ce_c_term(q, cand, target, c, bias, scale, margin)
+    return loss
+
+
+def hyp_dist_ce_loss(q, cand, target, c_r, bias=None, scale=None, margin=None):
+    """mean CE of the arctanh-distance score with per-query curvatures c_r
+    (hyperbolic_decoder.py:257-283): logits = scale (margin - d_{c_r}(q, e)) + bias,
+    d = 2 / (sqrt(c_r + eps) + eps) atanh(min(sqrt(c_r + eps) min(|n| / (den + eps), bound),
+    1 - eps)).  Per-pair scalars in float64, autograd through q, e, c_r, bias, scale, margin."""
+    qd, ed = q.double(), cand.double()
+    c = c_r.double().reshape(-1, 1)
+    sqrt_c = torch.sqrt(c + EPS)
+    x2 = (qd * qd).sum(1, keepdim=True)
+    y2 = (ed * ed).sum(1).unsqueeze(0)
+    xy = qd @ ed.t()
+    A = 1 - 2 * c * xy + c * y2  # num = A (-q) + B e
+    Bc = 1 - c * x2
+    num2 = A * A * x2 - 2 * A * Bc * xy + Bc * Bc * y2
+    den = 1 - 2 * c * xy + c * c * x2 * y2
+    n = (num2.clamp(min=1e-30).sqrt() / (den + EPS).abs()).clamp(min=EPS)
+    n = torch.min(n, 1.0 / (sqrt_c + EPS) - EPS)
+    dist = (2.0 / (sqrt_c + EPS)) * torch.atanh((sqrt_c * n).clamp(max=1.0 - EPS))
+    logits = margin.double() - dist if torch.is_tensor(margin) else (0.0 if margin is None else margin) - dist
+    if scale is not None:
+        logits = scale.double() * logits
+    if bias is not None:
+        logits = logits + bias.double()
+    return torch.nn.functional.cross_entropy(logits, target.long()).float()
 
 
 # ------------------------------------------------------------------ long-K products

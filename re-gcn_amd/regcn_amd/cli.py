@@ -19,8 +19,7 @@ validation every `--evaluate-every` epochs saving the best raw MRR to the checkp
 stop after 20 epochs without improvement, then the test set on the best checkpoint.  The
 forward and backward run on the HIP kernels (training.py / autograd.py); snapshot graphs
 are built once on the device and reused across epochs (the reference rebuilds them per
-sample, :560).  Out-of-scope features (static graph, EST, fhnn/hgat, Riemannian Adam) raise,
-as do the two whose gradients are not built (learned curvature, relation curvature).
+sample, :560).  Out-of-scope features (static graph, EST, fhnn/hgat, Riemannian Adam) raise.
 """
 import argparse
 import contextlib
@@ -311,9 +310,21 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
     best_mrr, best_epoch, patience = 0.0, 0, 20
     epoch_loss = []
     t_start = time.time()
+    initial_curvature = None
     for epoch in range(args.n_epochs):
         t0 = time.time()
         model.train()
+        if args.learn_curvature:  # hyperbolic_main.py:528-544: the upper bound warms up linearly
+            if initial_curvature is None:
+                initial_curvature = min(max(model.get_curvature().item(), args.curvature_min), args.curvature_max)
+            if args.curvature_warmup_epochs > 0 and epoch < args.curvature_warmup_epochs:
+                cmax = initial_curvature + (args.curvature_max - initial_curvature) * \
+                    (epoch + 1) / args.curvature_warmup_epochs
+            else:
+                cmax = args.curvature_max
+            model.set_curvature_bounds(curvature_max=cmax)
+            if args.plus_relation_specific_curvature:
+                model.set_relation_curvature_bounds(curvature_max=cmax)
         # per-sample losses accumulated on the device (the reference's four .item() per
         # mini-batch, :600-603, would synchronise every step): one read per epoch
         acc = torch.zeros(4, device=device, dtype=torch.float64)  # sum of e, r, rad; samples
@@ -400,12 +411,11 @@ def main(argv=None):
     bad = _unsupported(args)
     if bad:
         raise SystemExit("not supported in this build (SURVEY.md §2 out of scope): " + ", ".join(bad))
-    if not args.test and (args.learn_curvature or args.plus_relation_specific_curvature):
-        raise SystemExit("training with --learn-curvature / --plus-relation-specific-curvature is not supported "
-                         "in this build (their gradients are not built)")
-    if not args.test and args.hip_graph and args.decoder == "murp":
-        raise SystemExit("--hip-graph: the MuRP decoder's training step is not capturable yet "
-                         "(a host-synchronising op inside the step); train it without --hip-graph")
+    if args.curvature_warmup_epochs < 0:
+        raise ValueError("curvature_warmup_epochs must be non-negative")          # hyperbolic_main.py:212-213
+    if not args.test and args.hip_graph and args.learn_curvature:
+        raise SystemExit("--hip-graph with --learn-curvature: the curvature changes every step and the "
+                         "step reads it on the host (as the reference's c.item()); train it without --hip-graph")
     if args.radius_msg_gamma < 0:
         raise ValueError("--radius-msg-gamma must be non-negative (use 0 to disable the penalty)")
     if not 0.0 <= args.radius_anchor_beta <= 1.0:

@@ -40,11 +40,12 @@ def _relation_curvature_theta_init(global_c):
 
 def _clamp_relation_curvature(rel_c_raw, global_c, warmup_max=None):
     """hyperbolic_decoder.py:66-86."""
-    g = global_c if torch.is_tensor(global_c) else rel_c_raw.new_tensor(float(global_c))
+    # device scalars by fill kernels (new_full), not host copies: the step stays capturable
+    g = global_c if torch.is_tensor(global_c) else rel_c_raw.new_full((), float(global_c))
     upper = REL_CURVATURE_SAFETY_MARGIN * g.to(rel_c_raw.device, rel_c_raw.dtype)
     if warmup_max is not None:
-        upper = torch.min(upper, rel_c_raw.new_tensor(float(warmup_max)))
-    return torch.max(torch.min(rel_c_raw, upper), rel_c_raw.new_tensor(REL_CURVATURE_EPSILON))
+        upper = torch.min(upper, rel_c_raw.new_full((), float(warmup_max)))
+    return torch.max(torch.min(rel_c_raw, upper), rel_c_raw.new_full((), REL_CURVATURE_EPSILON))
 
 
 def _cf(c):
@@ -92,10 +93,13 @@ def _chunked_hyperbolic_ce_loss(query, candidates, target, c, c_chunk_size, cand
     B x N logits are never materialised).  query_bias cancels in CE and is ignored (:204-205)."""
     B, d = query.shape
     N = candidates.shape[0]
-    if _ag.needs_grad(query, candidates, candidate_bias, score_scale, score_margin):
-        if use_hyperbolic_distance or query_curvature is not None:
-            raise NotImplementedError("training with the arctanh-distance score (--plus-relation-specific-curvature) "
-                                      "is not built: its backward kernel is missing")
+    if _ag.needs_grad(query, candidates, candidate_bias, score_scale, score_margin, query_curvature, c):
+        if use_hyperbolic_distance and query_curvature is not None:  # --plus-relation-specific-curvature
+            return _ag.hyp_dist_ce_loss(query, candidates, target, query_curvature, bias=candidate_bias,
+                                        scale=score_scale, margin=score_margin)
+        if use_hyperbolic_distance:
+            raise NotImplementedError("the global-curvature arctanh-distance score has no caller in the reference "
+                                      "(its decoders pass per-relation curvatures)")
         return _ag.hyp_ce_loss(query, candidates, target, c, bias=candidate_bias, scale=score_scale,
                                margin=score_margin)
     q, e, b, cr, sc, mg = _score_operands(query, candidates, candidate_bias, score_scale, score_margin,

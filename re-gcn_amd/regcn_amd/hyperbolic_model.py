@@ -836,9 +836,17 @@ class HyperbolicRecurrentRGCN(nn.Module):
         score_rel.record_stream(main)
         return score, score_rel
 
+    def _loss_curvature(self):
+        """The curvature get_loss hands the decoders (hyperbolic_model.py:972-973): the learned
+        tensor while training it (its gradient flows through the decoders), else the float."""
+        c_val = self._c_float()
+        if self.learn_curvature and self._wants_grad():
+            return self.get_curvature()
+        return c_val
+
     def get_loss(self, glist, triples, static_graph, use_cuda, query_time=None):
         """hyperbolic_model.py:941-1088 (forward value of the four losses)."""
-        c_val = self._c_float()
+        c_val = self._loss_curvature()
         self.decoder_ob.c = c_val
         self.rdecoder.c = c_val
         evolve_embs, static_emb, r_emb, _, _ = self.forward(glist, static_graph, use_cuda)
@@ -864,21 +872,25 @@ class HyperbolicRecurrentRGCN(nn.Module):
         loss_radius), ...]."""
         if combine is None:
             combine = lambda le, lr, ls, lrad: le + lr + ls.sum() + lrad  # noqa: E731
-        c_val = self._c_float()
-        self.decoder_ob.c = c_val
-        self.rdecoder.c = c_val
+        c_val = self._loss_curvature()
         evolve_embs, static_emb, r_emb, _, _ = self.forward(glist, static_graph, use_cuda)
         pre_emb = self._final_embedding(evolve_embs[-1], c_val)
         grad_on = torch.is_grad_enabled()
-        cut = [t.detach().requires_grad_(grad_on and t.requires_grad) for t in (pre_emb, r_emb)]
+        srcs = (pre_emb, r_emb) + ((c_val,) if torch.is_tensor(c_val) else ())
+        # a learned curvature is cut too: the mini-batch decoders accumulate its gradient into
+        # the leaf, which the final encoder backward carries on to log_c
+        cut = [t.detach().requires_grad_(grad_on and t.requires_grad) for t in srcs]
+        c_dec = cut[2] if len(cut) > 2 else c_val
+        self.decoder_ob.c = c_dec
+        self.rdecoder.c = c_dec
         parts = []
         for b in range(0, triples.shape[0], batch_size):
-            losses = self._decode_losses(cut[0], cut[1], triples[b:b + batch_size], c_val)
+            losses = self._decode_losses(cut[0], cut[1], triples[b:b + batch_size], c_dec)
             total = combine(*losses)
             if grad_on and total.requires_grad:
                 total.backward()
             parts.append(tuple(t.detach() for t in losses))
-        roots = [(src, leaf.grad) for src, leaf in zip((pre_emb, r_emb), cut)
+        roots = [(src, leaf.grad) for src, leaf in zip(srcs, cut)
                  if src.requires_grad and leaf.grad is not None]
         if roots:
             torch.autograd.backward([r[0] for r in roots], [r[1] for r in roots])

@@ -3,7 +3,9 @@
 Same class names, method names, argument meaning and defaults as the reference; every
 method runs a hand-written gfx950 kernel (csrc/rowwise.hip) through the C-ABI.  Inputs
 must be fp32 HIP tensors; `c` may be a python float or a 0-dim tensor (read once, as the
-reference's `c.item()` does at hyperbolic_ops.py:72).  With autograd on, the row maps route to autograd.py (HIP backward kernels); these are the
+reference's `c.item()` does at hyperbolic_ops.py:72).  With autograd on (or a learned
+curvature tensor that requires grad), the row maps route to autograd.py (HIP backward
+kernels, the curvature's gradient where the reference has one); these are the
 inference/forward row maps of the hot path.
 """
 import math
@@ -46,7 +48,7 @@ class HyperbolicOps:
     def project_to_ball(x, c=0.01, eps=1e-6):
         """hyperbolic_ops.py:55-74."""
         _check_eps(eps)
-        if _ag.needs_grad(x):
+        if _ag.needs_grad(x, c):
             return _ag.project(x, c)
         return _rowmap("regcn_project_f32", x, c).view(x.shape)
 
@@ -54,7 +56,7 @@ class HyperbolicOps:
     def exp_map_zero(v, c=0.01, eps=1e-6):
         """hyperbolic_ops.py:76-95."""
         _check_eps(eps)
-        if _ag.needs_grad(v):
+        if _ag.needs_grad(v, c):
             return _ag.exp0(v, c)
         return _rowmap("regcn_exp0_f32", v, c).view(v.shape)
 
@@ -62,7 +64,7 @@ class HyperbolicOps:
     def log_map_zero(x, c=0.01, eps=1e-6):
         """hyperbolic_ops.py:97-116."""
         _check_eps(eps)
-        if _ag.needs_grad(x):
+        if _ag.needs_grad(x, c):
             return _ag.log0(x, c)
         return _rowmap("regcn_log0_f32", x, c).view(x.shape)
 
@@ -70,7 +72,7 @@ class HyperbolicOps:
     def mobius_add(x, y, c=0.01, eps=1e-6):
         """hyperbolic_ops.py:118-143."""
         _check_eps(eps)
-        if _ag.needs_grad(x, y):
+        if _ag.needs_grad(x, y, c):
             return _ag.mobius_add(x, y, c)
         x2, d = _rows(x)
         y2, _ = _rows(y.expand_as(x))
@@ -96,7 +98,7 @@ class HyperbolicOps:
         if radius is None:
             return x
         _check_eps(eps)
-        if _ag.needs_grad(x, radius):
+        if _ag.needs_grad(x, radius, c):
             r = radius.reshape(-1)
             n = x.reshape(-1, x.shape[-1]).shape[0]
             return _ag.apply_radius(x, r.expand(n) if r.numel() == 1 else r, c)
@@ -124,7 +126,7 @@ class HyperbolicOps:
     @staticmethod
     def layer_norm_roundtrip(x, c=0.01):
         """exp0(normalize(log0(x))) in one pass (hyperbolic_model.py:832-835, :926-929)."""
-        if _ag.needs_grad(x):
+        if _ag.needs_grad(x, c):
             return _ag.exp0(torch.nn.functional.normalize(_ag.log0(x, c)), c)
         return _rowmap("regcn_ln_roundtrip_f32", x, c).view(x.shape)
 

@@ -106,18 +106,22 @@ def relation_context(x, g, R2):
 def model_forward(model, g_list):
     """HyperbolicRecurrentRGCN.forward with autograd (hyperbolic_model.py:722-890)."""
     c = model._c_float()
+    # a learned curvature enters the model-level maps as the clamped exp(log_c) tensor, so its
+    # gradient flows (hyperbolic_model.py:753-756); the layers and the radius evolution keep
+    # their constructor-time float (hyperbolic_layers.py:195, hyperbolic_ops.py:385)
+    ct = model.get_curvature() if model.learn_curvature else c
     dev = model.dynamic_emb.device
     R2 = model.num_rels * 2
     r_static = model._static_radius(c)
     dyn = model.dynamic_emb
-    h = A.exp0(F.normalize(dyn) if model.layer_norm else dyn, c)                       # :775-780
+    h = A.exp0(F.normalize(dyn) if model.layer_norm else dyn, ct)                      # :775-780
     h = A.apply_radius(h, r_static, c)                                                 # :782
     trev = model.temporal_radius_evolution
     lorentz = model.encoder_name == "lgcn"
     history, h0 = [], None
     for i, g in enumerate(g_list):
         g = g.to(dev)
-        x_prev = A.log0(h, c)                                                          # :802
+        x_prev = A.log0(h, ct)                                                         # :802
         x_in = torch.cat([model.emb_rel, relation_context(x_prev, g, R2)], dim=1)
         h0 = model.relation_gru(x_in, model.emb_rel if i == 0 else h0)                 # :815-823
         if model.layer_norm:
@@ -125,11 +129,11 @@ def model_forward(model, g_list):
         cur = cell_forward(model.rgcn, g, h, [h0] * len(model.rgcn.layers), lorentz)   # :828
         cur = A.project(cur, c)                                                        # :829
         if model.layer_norm:
-            cur = A.exp0(F.normalize(A.log0(cur, c)), c)                              # :832-835
+            cur = A.exp0(F.normalize(A.log0(cur, ct)), ct)                            # :832-835
         pt = torch.clamp(x_prev, -10.0, 10.0)                                          # :841-846
         z = A.mm_weight(pt, model.time_gate_weight)                                    # tw = sigmoid(z + b)
-        mix = A.tail(A.log0(cur, c), z=z, bias=model.time_gate_bias, p=pt, flags=A.TAIL_CLAMP_IN)
-        h = A.project(A.exp0(mix, c), c)                                               # :859-860
+        mix = A.tail(A.log0(cur, ct), z=z, bias=model.time_gate_bias, p=pt, flags=A.TAIL_CLAMP_IN)
+        h = A.project(A.exp0(mix, ct), c)                                              # :859-860
         if model.use_residual_evolution:
             t = A.log0(h, trev.c)                                                      # hyperbolic_ops.py:395-435
             delta = torch.clamp(A.linear(trev.radius_mlp, t).squeeze(-1), -trev.epsilon, trev.epsilon)

@@ -58,8 +58,8 @@ def test_cli_rejects_out_of_scope_flags():
     from regcn_amd import cli
     with pytest.raises(SystemExit):
         cli.main(["-d", "synthetic:icews14s_lgcn_roth", "--test", "--gpu", "0", "--use-est"])
-    with pytest.raises(SystemExit):  # training needs the gradient of a learned curvature: not built
-        cli.main(["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0", "--learn-curvature"])
+    with pytest.raises(SystemExit):  # the learned curvature is read on the host every step: no graphs
+        cli.main(["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0", "--learn-curvature", "--hip-graph"])
 
 
 def test_cli_training_loop(tmp_path):
@@ -120,14 +120,17 @@ def test_cli_training_replicas(tmp_path):
     assert "MRR raw" in r.stdout + r.stderr
 
 
-@pytest.mark.parametrize("encoder,decoder", [("lgcn", "roth"), ("hyperbolic_uvrgcn", "atth")])
-def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder):
+@pytest.mark.parametrize("encoder,decoder,extra", [("lgcn", "roth", []), ("hyperbolic_uvrgcn", "atth", []),
+                                                   ("hyperbolic_uvrgcn", "murp", []),
+                                                   ("lgcn", "roth", ["--plus-relation-specific-curvature"])])
+def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder, extra):
     """--hip-graph (each sample's whole step captured after its first run and replayed:
     training.GraphedSteps) trains the same model as the eager loop: dropout off, the same
     seeds and sample order; epoch losses bit for bit and every parameter tensor to 1e-6 in
-    relative norm (epochs 2-3 are replays; measured: bitwise equal).  Not covered: ConvTransE
-    (its eager runs differ in the 6th digit: MIOpen convolution), MuRP (not capturable; the
-    CLI refuses --hip-graph with it)."""
+    relative norm (epochs 2-3 are replays; measured: bitwise equal).  MuRP's relation decoder
+    (no score scale / margin: device constants by fill kernels) and the per-relation curvature
+    score replay too.  Not covered: ConvTransE (its eager runs differ in the 6th digit: MIOpen
+    convolution)."""
     import random
     from regcn_amd import cli, ranking
     common = ["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0", "--encoder", encoder, "--decoder", decoder,
@@ -135,7 +138,7 @@ def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder):
               "--test-history-len", "3", "--relation-prediction", "--entity-prediction",
               "--checkpoint", str(tmp_path / "m.pth"), "--seed", "0", "--lr", "0.01", "--triple-batch-size", "64",
               "--dropout", "0", "--input-dropout", "0", "--hidden-dropout", "0", "--feat-dropout", "0",
-              "--n-epochs", "3", "--evaluate-every", "100"]
+              "--n-epochs", "3", "--evaluate-every", "100"] + extra
     dev = torch.device("cuda", 0)
     runs = []
     adam = torch.optim.Adam
@@ -240,3 +243,26 @@ def test_trained_model_mrr_matches_oracle(tmp_path):
     assert near_tie_flips <= 0.01 * n_queries
     print("trained MRR hip/oracle:", {k: round(v, 5) for k, v in mrr.items()}, "chance %.4f" % chance,
           "rank flips at near ties: %d of %d" % (near_tie_flips, n_queries))
+
+
+def test_cli_training_learned_curvature(tmp_path):
+    """--learn-curvature with a warm-up of the upper bound (hyperbolic_main.py:528-544) and
+    --plus-relation-specific-curvature train through the CLI: finite falling losses and a
+    curvature that moved away from its initial value."""
+    from regcn_amd import cli, ranking
+    args = cli.build_parser().parse_args(
+        ["-d", "synthetic:icews14s_lgcn_roth", "--gpu", "0", "--encoder", "hyperbolic_uvrgcn", "--decoder", "roth",
+         "--n-hidden", "64", "--n-bases", "32", "--synthetic-snapshots", "10", "--train-history-len", "3",
+         "--test-history-len", "3", "--relation-prediction", "--entity-prediction", "--seed", "0", "--lr", "0.01",
+         "--n-epochs", "4", "--evaluate-every", "2", "--learn-curvature", "--curvature-warmup-epochs", "2",
+         "--plus-relation-specific-curvature", "--checkpoint", str(tmp_path / "m.pth")])
+    dev = torch.device("cuda", 0)
+    V, R, train, valid, test = cli.load_dataset(args)
+    tl = ranking.split_by_time(train)
+    torch.manual_seed(0)
+    model = cli.build_model(args, V, R, tl, dev)
+    c0 = float(model.get_curvature())
+    out = cli.train_model(args, model, tl, valid, V, R, dev, str(tmp_path / "m.pth"))
+    assert all(np.isfinite(out["epoch_loss"])) and out["epoch_loss"][-1] < out["epoch_loss"][0], out["epoch_loss"]
+    assert abs(float(model.get_curvature()) - c0) > 1e-7
+    assert model.log_c.grad is not None and model.decoder_ob.rel_curvature_raw.grad is not None

@@ -25,6 +25,15 @@ CASES = {
                              radius_anchor_beta=0.5),
     "uvrgcn_convtranse": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="hyperbolic_convtranse",
                               layer_norm=True),
+    # the curvature features (tools/goldens/make_golden.py CURVATURE_TRAIN_CASES): a learned
+    # curvature (grad of log_c through exp0 / log0 / mobius_add and the decoder scores) and the
+    # per-relation curvature arctanh-distance score, alone and together
+    "uvrgcn_roth_lc": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False,
+                           learn_curvature=True),
+    "lgcn_roth_crel_bias": dict(encoder_name="lgcn", decoder_name="roth", layer_norm=False,
+                                use_relation_specific_curvature=True, use_entity_euclidean_bias=True),
+    "uvrgcn_atth_lc_crel_ln": dict(encoder_name="hyperbolic_uvrgcn", decoder_name="atth", layer_norm=True,
+                                   learn_curvature=True, use_relation_specific_curvature=True),
 }
 
 
@@ -77,6 +86,8 @@ def test_training_grads_vs_reference(golden, tag):
         assert err <= 2e-3, "%s: %.3g" % (k, err)
         n += 1
     assert n >= 20
+    if "lc" in tag.split("_"):
+        assert "grad_log_c" in z  # the learned curvature's gradient is among those checked
 
 
 ORACLE_CFG = {
@@ -110,7 +121,7 @@ def oracle_grads(z, tag, names):
     return {k: sd[k].grad for k in names}
 
 
-@pytest.mark.parametrize("tag", list(CASES))
+@pytest.mark.parametrize("tag", list(ORACLE_CFG))
 def test_training_grads_vs_fp64_oracle(golden, tag):
     """Every parameter gradient of one mini-batch against the fp64 oracle (the reference op
     sequence in double): |delta| <= 1e-4 * max(1e-3, max|ref|) per tensor (SURVEY.md §8(a)'s

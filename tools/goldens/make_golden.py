@@ -391,6 +391,72 @@ TRAIN_CASES = [
 ]
 
 
+CURVATURE_TRAIN_CASES = [
+    ("uvrgcn_roth_lc", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False,
+                            learn_curvature=True)),
+    ("lgcn_roth_crel_bias", dict(encoder_name="lgcn", decoder_name="roth", layer_norm=False,
+                                 use_relation_specific_curvature=True, use_entity_euclidean_bias=True)),
+    ("uvrgcn_atth_lc_crel_ln", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="atth", layer_norm=True,
+                                    learn_curvature=True, use_relation_specific_curvature=True)),
+]
+
+
+def gen_train_curvature():
+    """gen_train's mini-batch for the two curvature features whose gradients the build adds
+    this round: a learned curvature (log_c, hyperbolic_model.py:299-300, :673-679, :753-770)
+    and the per-relation curvature arctanh-distance score (hyperbolic_decoder.py:145-164,
+    :257-283), alone and together."""
+    V, R, T, d, tw = 256, 64, 3, 64, 0.7
+    snaps = snapshot_series(40, V, R, T + 1, 120)
+    rng = np.random.default_rng(41)
+    radius_target = rng.uniform(0.5, 3.0, size=V).astype(np.float32)
+    glist = [rutils.build_sub_graph(V, R, s, False, "cpu") for s in snaps[:T]]
+    batch = torch.from_numpy(snaps[T])
+    for i, (tag, kw) in enumerate(CURVATURE_TRAIN_CASES):
+        torch.manual_seed(350 + i)
+        base = dict(num_ents=V, num_rels=R, num_static_rels=0, num_words=0, h_dim=d, opn="sub",
+                    sequence_len=T, num_bases=d // 2, num_hidden_layers=2, dropout=0.0, c=C,
+                    self_loop=True, skip_connect=False, input_dropout=0.0, hidden_dropout=0.0,
+                    feat_dropout=0.0, entity_prediction=True, relation_prediction=True,
+                    use_cuda=False, gpu="cpu", radius_target=radius_target, radius_msg_gamma=0.15)
+        base.update(kw)
+        m = HyperbolicRecurrentRGCN(**base)
+        with torch.no_grad():
+            for mod in (m.decoder_ob, m.rdecoder):
+                if hasattr(mod, "score_margin"):
+                    mod.score_margin.fill_(0.7)
+                    mod.score_scale_raw.fill_(0.4)
+                if getattr(mod, "rel_bias", None) is not None:
+                    mod.rel_bias.normal_(0, 0.1)
+                if getattr(mod, "entity_bias", None) is not None:
+                    mod.entity_bias.normal_(0, 0.1)
+                if getattr(mod, "rel_curvature_raw", None) is not None:  # spread the curvatures
+                    mod.rel_curvature_raw.add_(torch.randn(mod.rel_curvature_raw.shape) * 0.5)
+                for lin in mod.modules():
+                    if isinstance(lin, torch.nn.Linear) and lin.weight.shape[0] == lin.weight.shape[1]:
+                        lin.weight.normal_(0, 0.05)
+            m.radius_static.add_(torch.randn(V) * 0.2)
+        sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        m.train()
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.eval()
+        m.zero_grad()
+        le, lr, ls, lrad = m.get_loss(glist, batch.clone(), None, False)
+        loss = tw * le + (1 - tw) * lr + ls + lrad
+        loss.backward()
+        out = {"meta": np.array([V, R, d, T]), "batch": snaps[T], "radius_target": radius_target,
+               "task_weight": np.array(tw), "losses": np.array([float(x) for x in (le, lr, ls, lrad, loss)])}
+        for t in range(T):
+            out["snap%d" % t] = snaps[t]
+        for k, v in sd.items():
+            out["sd_" + k] = v.numpy().copy()
+        for k, p in m.named_parameters():
+            if p.grad is not None:
+                out["grad_" + k] = p.grad.numpy().copy()
+        save("train_%s.npz" % tag, **out)
+
+
 def gen_train():
     """One training mini-batch (hyperbolic_main.py:585-598): get_loss on the snapshot's triples,
     loss = tw le + (1 - tw) lr + ls + lrad, backward; every parameter's gradient.  Dropout p = 0
@@ -625,7 +691,7 @@ if __name__ == "__main__":
     table = {"graph": gen_graph_indexing, "ops": gen_ops, "union": gen_layer_union,
              "euclid": gen_layer_euclid, "lorentz": gen_layer_lorentz, "models": gen_models,
              "rrgcn": gen_rrgcn, "score": gen_score, "rank": gen_rank, "train": gen_train,
-             "models_large": gen_models_large, "dataset": gen_dataset,
+             "models_large": gen_models_large, "dataset": gen_dataset, "train_curvature": gen_train_curvature,
              "multistep": gen_multistep}
     for w in which:
         table[w]()
