@@ -84,23 +84,73 @@ def cell_forward(cell, g, h, rel_embs, lorentz):
     return h
 
 
+class _RelationContext(torch.autograd.Function):
+    """x_input[r] = mean of x over r's r_to_e span, 0 for absent relations
+    (hyperbolic_model.py:802-812), forward and backward on the segment-mean kernel
+    (regcn_segment_mean_f32): deterministic (fixed summation orders, no atomics).
+
+    forward: the forward relations' spans (hyperbolic_model.relation_context; an inverse
+    relation's span repeats its forward relation's entities, so its mean is a copy).
+    backward: dx[e] = sum over the forward relations r whose span holds e of
+    (dy[r] + dy[r + R]) / count[r] -- a gather-sum over each entity's relation list (the
+    entity-sorted transpose of the spans, built once per snapshot and cached)."""
+
+    @staticmethod
+    def forward(ctx, x, g, R2):
+        from .hyperbolic_model import relation_context as rc_fwd
+        ctx.g, ctx.R2, ctx.V = g, R2, x.shape[0]
+        return rc_fwd(x.detach().contiguous(), g, R2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from . import _lib
+        g, R2, V = ctx.g, ctx.R2, ctx.V
+        R = R2 // 2
+        wk = g.work()
+        d = dy.shape[1]
+        tr = _entity_relation_lists(g, V, R)
+        gr = (dy[:R] + dy[R:]) / torch.clamp(wk["rel_count"][:R], min=1.0).unsqueeze(-1)
+        dx = torch.zeros(V, d, device=dy.device, dtype=torch.float32)
+        ch = tr["chunks"]
+        if ch.shape[0]:
+            _lib.call("regcn_segment_mean_f32", _lib.fptr(gr.contiguous(), "grad"), _lib.iptr(tr["rel"]),
+                      _lib.fptr(tr["ones"]), _lib.iptr(ch), ch.shape[0], None, 0, d, None, d, _lib.fptr(dx),
+                      _lib.stream())
+        return dx, None, None
+
+
+def _entity_relation_lists(g, V, R):
+    """Per entity, the forward relations whose r_to_e span holds it (entity-sorted, stable),
+    as chunk records {entity, begin, end, -1} over that list (one chunk per entity: an entity
+    touches at most R relations); cached on the graph."""
+    tr = g.__dict__.get("_ent_rel")
+    if tr is not None:
+        return tr
+    wk = g.work()
+    dev = wk["rel_idx"].device
+    cnt = wk["rel_count"][:R].long()
+    n_fwd = int(wk["rel_idx"].numel()) // 2
+    ent = wk["rel_idx"][:n_fwd].long()
+    rel = torch.repeat_interleave(torch.arange(R, device=dev), cnt)
+    order = torch.sort(ent, stable=True).indices
+    ent_s, rel_s = ent[order], rel[order].to(torch.int32)
+    per = torch.bincount(ent_s, minlength=V)
+    ptr = torch.zeros(V + 1, device=dev, dtype=torch.long)
+    ptr[1:] = torch.cumsum(per, 0)
+    rows = torch.nonzero(per > 0).flatten()
+    chunks = torch.stack([rows, ptr[rows], ptr[rows + 1], torch.full_like(rows, -1)], 1).to(torch.int32).contiguous()
+    tr = {"rel": rel_s.contiguous() if rel_s.numel() else torch.zeros(1, device=dev, dtype=torch.int32),
+          "chunks": chunks, "ones": torch.ones(V, device=dev, dtype=torch.float32)}
+    g.__dict__["_ent_rel"] = tr
+    return tr
+
+
 def relation_context(x, g, R2):
     """x_input[r] = mean of the rows of r's r_to_e span, 0 for absent relations
-    (hyperbolic_model.py:802-812).  Spans are laid out in relation-id order."""
-    wk = g.work()
-    idx = wk["rel_idx"]
-    out = torch.zeros(R2, x.shape[1], device=x.device, dtype=x.dtype)
-    if idx.numel() == 0:
-        return out
-    rel_of = g.__dict__.get("_rel_of_item")
-    if rel_of is None:
-        cnt = wk["rel_count"].long()
-        rel_of = torch.repeat_interleave(torch.arange(R2, device=x.device), cnt)
-        g.__dict__["_rel_of_item"] = rel_of
-    # advanced indexing + index_put(accumulate): sort-based, so forward and backward are
-    # deterministic (index_select / index_add accumulate with atomics)
-    out = out.index_put((rel_of,), x[idx.long()], accumulate=True)
-    return out / torch.clamp(wk["rel_count"], min=1.0).unsqueeze(-1)
+    (hyperbolic_model.py:802-812), HIP forward and backward (_RelationContext)."""
+    if g.work()["rel_idx"].numel() == 0:
+        return torch.zeros(R2, x.shape[1], device=x.device, dtype=x.dtype) + 0.0 * x.sum()
+    return _RelationContext.apply(x, g, R2)
 
 
 def model_forward(model, g_list):
