@@ -26,16 +26,22 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--modes", default="phases,layers")
     ap.add_argument("--encoder", default="hyperbolic_uvrgcn")
+    ap.add_argument("--budgets", default="0", help="fused-layer edge budgets to compare (0: the default)")
     a = ap.parse_args()
     cfg = dict(CONFIGS["synthetic_1m"], V=a.V, per_snap=a.triples, encoder=a.encoder)
     dev = torch.device("cuda", 0)
     t0 = time.time()
     snaps = snapshot_series(100, cfg["V"], cfg["R"], cfg["T"] + 1, cfg["per_snap"])
     print("generated %d snapshots in %.1f s" % (len(snaps), time.time() - t0), flush=True)
+    for budget in [int(b) for b in a.budgets.split(",")]:
+        run(a, cfg, snaps, dev, budget)
+
+
+def run(a, cfg, snaps, dev, budget):
     t0 = time.time()
-    glist = [G.build_sub_graph(cfg["V"], cfg["R"], s, True, dev) for s in snaps[:cfg["T"]]]
+    glist = [G.build_sub_graph(cfg["V"], cfg["R"], s, True, dev, tile_budget=budget or None) for s in snaps[:cfg["T"]]]
     torch.cuda.synchronize()
-    print("built in %.2f s" % (time.time() - t0), flush=True)
+    print("built in %.2f s (budget %s)" % (time.time() - t0, budget or "default"), flush=True)
     for g in glist:
         print("  E=%d n_pos=%d tiles=%d heavy=%d budget=%d chunk=%d rel_max_span=%d items=%d heavy_chunks=%d"
               % (g.number_of_edges(), g.n_pos, g.n_pos_tiles, g.n_heavy, g.budget, g.chunk_edges,
@@ -64,6 +70,8 @@ def main():
         print("%-7s %9.3f ms per predict (wall %.3f)  %.1f M edges/s   peak mem %.1f GB"
               % (mode, ms, (time.time() - t0) / a.reps * 1e3, edges / ms / 1e3,
                  torch.cuda.max_memory_allocated() / 1e9), flush=True)
+    del glist
+    torch.cuda.empty_cache()
     if len(outs) == 2:
         p, l = outs["phases"], outs["layers"]
         for name, x, y in (("score", p[1], l[1]), ("score_rel", p[2], l[2])):
