@@ -24,18 +24,22 @@
 namespace regcn {
 
 // ==================================================================================== layer
+// 4 waves per SIMD (VGPRs <= 128: a few spilled registers on the cold paths) and the LDS
+// rows of layer_part_rows: 4-5 workgroups per CU instead of 3, so more tiles' gathers are in
+// flight while others run their MFMA products.
 template <int AGG, int S, bool STEP>
-__global__ __launch_bounds__(NTHR) void k_layer(LayerArgs p) {
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void k_layer(LayerArgs p) {
   extern __shared__ float lds[];
-  const LdsLayout L = lds_layout(p.d, AGG == AGG_LORENTZ && S == 0);
+  const bool skip_op = p.prev_t != nullptr;
+  const LdsLayout L = lds_layout(p.d, AGG == AGG_LORENTZ && S == 0, layer_part_rows(skip_op, STEP));
   const int lda = L.lda;
   float* part = lds + L.part;
   float* X = lds + L.X;
   int* trow = reinterpret_cast<int*>(lds + L.ints);
   int* tmask = trow + TM;
   RowRed rr{lds + L.red, 0};
-  float* P1 = part + TM * lda;      // skip-connection operand
-  float* P2 = part + 2 * TM * lda;  // timestep: clamp(x_prev)
+  float* P1 = part + TM * lda;                        // skip-connection operand
+  float* P2 = part + (skip_op ? 2 : 1) * TM * lda;    // timestep: clamp(x_prev)
 
   auto mark = [&](int k) {
     trace_mark(p, k);
@@ -259,7 +263,7 @@ int layer(const LayerArgs& a, hipStream_t st) {
   const unsigned grid = (unsigned)(n_pos_tiles + (a.V - a.n_pos + TM - 1) / TM);
   const int s = mode == AGG_LORENTZ ? a.d / a.nb : 1;
   const bool gen = mode == AGG_LORENTZ && s != 1 && s != 2 && s != 4;
-  const size_t lds = (size_t)lds_layout(a.d, gen).total_bytes;
+  const size_t lds = (size_t)lds_layout(a.d, gen, layer_part_rows(a.prev_t != nullptr, a.fuse_step != 0)).total_bytes;
   switch (mode) {
     case AGG_NONE: launch_layer<AGG_NONE, 1>(b, dim3(grid), lds, st); break;
     case AGG_UNION: launch_layer<AGG_UNION, 1>(b, dim3(grid), lds, st); break;

@@ -17,11 +17,20 @@ struct LdsLayout {
   int part, X, red, ints, xsh, total_bytes;  // float offsets; total in bytes
 };
 
-__host__ __device__ inline LdsLayout lds_layout(int d, bool gen_s) {
+// Partial / operand rows one k_layer launch needs: the gather's TM + NWAVE - 1 partial slots,
+// reused after the finish for the aggregate tile, the skip operand (P1) and the timestep
+// operand (P2) -- only the ones the launch has, so a plain layer's tile fits more workgroups
+// per CU (LDS: 5 per CU without skip / timestep, 4 with one of them, 3 with both).
+__host__ __device__ inline int layer_part_rows(bool skip, bool step) {
+  const int ops = TM * (1 + (skip ? 1 : 0) + (step ? 1 : 0));
+  return ops > TM + NWAVE - 1 ? ops : TM + NWAVE - 1;
+}
+
+__host__ __device__ inline LdsLayout lds_layout(int d, bool gen_s, int part_rows = PART_ROWS) {
   LdsLayout L;
   L.lda = tile_lda(d);
   L.part = 0;
-  L.X = PART_ROWS * L.lda;
+  L.X = part_rows * L.lda;
   L.red = L.X + TM * L.lda;
   L.ints = L.red + RED_FLOATS;
   L.xsh = L.ints + 32;  // trow[16], tmask[NWAVE] (+pad)
