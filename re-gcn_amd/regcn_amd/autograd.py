@@ -400,9 +400,10 @@ def _pair_terms(q, e, c):
     return n2 * pf * pf
 
 
-def _ce_c_term(q, cand, target, c, bias, scale, margin, chunk=65536):
+def _ce_c_term(q, cand, target, c, bias, scale, margin, chunk=65536, per_query=False):
     """Zero-valued term whose gradient is d(mean CE)/dc of the proxy score: sum_bn G_bn
-    (S_bn(c) - S_bn(c).detach()) / B with G = softmax - one-hot from the same scores."""
+    (S_bn(c) - S_bn(c).detach()) / B with G = softmax - one-hot from the same scores
+    (per_query: the B per-query terms, without the 1 / B)."""
     qd, ed = q.detach().double(), cand.detach().double()
     cd = c.double()
     sc = scale.detach().double()
@@ -419,21 +420,27 @@ def _ce_c_term(q, cand, target, c, bias, scale, margin, chunk=65536):
         parts.append((n0, n1, Sc))
     G = torch.softmax(S, dim=1)
     G[torch.arange(B, device=q.device), target.long()] -= 1.0
+    if per_query:
+        return sum((G[:, n0:n1] * (Sc - Sc.detach())).sum(1) for n0, n1, Sc in parts).float()
     G /= B
     return sum((G[:, n0:n1] * (Sc - Sc.detach())).sum() for n0, n1, Sc in parts).float()
 
 
-def hyp_ce_loss(q, cand, target, c, bias=None, scale=None, margin=None):
-    """mean over queries of the CE loss (hyperbolic_decoder.py:182-307, proxy score)."""
+def hyp_ce_loss(q, cand, target, c, bias=None, scale=None, margin=None, reduction="mean"):
+    """mean over queries of the CE loss (hyperbolic_decoder.py:182-307, proxy score);
+    reduction="none": the per-query losses."""
     scale = scale if torch.is_tensor(scale) else _const(1.0 if scale is None else scale, q)
     margin = margin if torch.is_tensor(margin) else _const(0.0 if margin is None else margin, q)
-    loss = _HypCE.apply(q, cand, bias, scale, margin, target, _cf(c)).mean()
+    loss = _HypCE.apply(q, cand, bias, scale, margin, target, _cf(c))
+    per_query = reduction == "none"
+    if not per_query:
+        loss = loss.mean()
     if _c_grad(c):
-        loss = loss + _ce_c_term(q, cand, target, c, bias, scale, margin)
+        loss = loss + _ce_c_term(q, cand, target, c, bias, scale, margin, per_query=per_query)
     return loss
 
 
-def hyp_dist_ce_loss(q, cand, target, c_r, bias=None, scale=None, margin=None):
+def hyp_dist_ce_loss(q, cand, target, c_r, bias=None, scale=None, margin=None, reduction="mean"):
     """mean CE of the arctanh-distance score with per-query curvatures c_r
     (hyperbolic_decoder.py:257-283): logits = scale (margin - d_{c_r}(q, e)) + bias,
     d = 2 / (sqrt(c_r + eps) + eps) atanh(min(sqrt(c_r + eps) min(|n| / (den + eps), bound),
@@ -456,7 +463,7 @@ def hyp_dist_ce_loss(q, cand, target, c_r, bias=None, scale=None, margin=None):
         logits = scale.double() * logits
     if bias is not None:
         logits = logits + bias.double()
-    return torch.nn.functional.cross_entropy(logits, target.long()).float()
+    return torch.nn.functional.cross_entropy(logits, target.long(), reduction=reduction).float()
 
 
 # ------------------------------------------------------------------ long-K products

@@ -88,20 +88,21 @@ def _chunked_hyperbolic_dist_score(query, candidates, bias, c, q_chunk_size, c_c
 
 def _chunked_hyperbolic_ce_loss(query, candidates, target, c, c_chunk_size, candidate_bias=None, query_bias=None,
                                 q_chunk_size=None, score_scale=None, score_margin=0.0, query_curvature=None,
-                                use_hyperbolic_distance=False):
+                                use_hyperbolic_distance=False, reduction="mean"):
     """hyperbolic_decoder.py:182-307 -> regcn_hyp_ce_f32 (fused scores + log-sum-exp; the
-    B x N logits are never materialised).  query_bias cancels in CE and is ignored (:204-205)."""
+    B x N logits are never materialised).  query_bias cancels in CE and is ignored (:204-205).
+    reduction="none": the B per-query losses instead of their mean."""
     B, d = query.shape
     N = candidates.shape[0]
     if _ag.needs_grad(query, candidates, candidate_bias, score_scale, score_margin, query_curvature, c):
         if use_hyperbolic_distance and query_curvature is not None:  # --plus-relation-specific-curvature
             return _ag.hyp_dist_ce_loss(query, candidates, target, query_curvature, bias=candidate_bias,
-                                        scale=score_scale, margin=score_margin)
+                                        scale=score_scale, margin=score_margin, reduction=reduction)
         if use_hyperbolic_distance:
             raise NotImplementedError("the global-curvature arctanh-distance score has no caller in the reference "
                                       "(its decoders pass per-relation curvatures)")
         return _ag.hyp_ce_loss(query, candidates, target, c, bias=candidate_bias, scale=score_scale,
-                               margin=score_margin)
+                               margin=score_margin, reduction=reduction)
     q, e, b, cr, sc, mg = _score_operands(query, candidates, candidate_bias, score_scale, score_margin,
                                                     query_curvature if use_hyperbolic_distance else None)
     tgt = target.to(device=q.device, dtype=torch.int32).contiguous()
@@ -112,7 +113,7 @@ def _chunked_hyperbolic_ce_loss(query, candidates, target, c, c_chunk_size, cand
     _lib.call("regcn_hyp_ce_f32", f(q, "query"), f(e, "candidates"), f(b), f(cr), f(sc), f(mg),
               _lib.iptr(tgt, "target"), B, N, d, _cf(c), int(bool(use_hyperbolic_distance)), f(ws), f(loss),
               _lib.stream())
-    return loss.mean()
+    return loss if reduction == "none" else loss.mean()
 
 
 def _grad_path(mod, *ts):
@@ -202,13 +203,14 @@ class _EntityDecoderBase(nn.Module):
             scores = scores + self.entity_bias[triplets[:, 0]].unsqueeze(1)
         return scores
 
-    def loss(self, entity_embedding, rel_embedding, triplets):
+    def loss(self, entity_embedding, rel_embedding, triplets, reduction="mean"):
         q = self._query(entity_embedding, rel_embedding, triplets)
         rel_c = self._relation_curvature(triplets[:, 1])
         return _chunked_hyperbolic_ce_loss(
             q, entity_embedding, triplets[:, 2], self.c, self.candidate_chunk_size, candidate_bias=self.entity_bias,
             q_chunk_size=self.query_chunk_size, score_scale=self._score_scale(), score_margin=self.score_margin,
-            query_curvature=rel_c, use_hyperbolic_distance=self.use_relation_specific_curvature)
+            query_curvature=rel_c, use_hyperbolic_distance=self.use_relation_specific_curvature,
+            reduction=reduction)
 
 
 class HyperbolicMuRP(_EntityDecoderBase):
@@ -235,8 +237,9 @@ class HyperbolicMuRP(_EntityDecoderBase):
         r_idx = trip[:, 1]
         s_emb = HyperbolicOps.project_to_ball(ent[trip[:, 0]], c)
         s_tan = self.dropout(HyperbolicOps.log_map_zero(s_emb, c))
-        rot_s = HyperbolicOps.exp_map_zero((_ag.linear(self.rot_proj, rel[r_idx]) * s_tan).contiguous(), c)
-        t_r = HyperbolicOps.exp_map_zero(_ag.linear(self.trans_proj, rel[r_idx]).contiguous(), c)
+        rr = rel[r_idx]
+        rot_s = HyperbolicOps.exp_map_zero((_ag.linear(self.rot_proj, rr) * s_tan).contiguous(), c)
+        t_r = HyperbolicOps.exp_map_zero(_ag.linear(self.trans_proj, rr).contiguous(), c)
         return HyperbolicOps.mobius_add(HyperbolicOps.project_to_ball(rot_s, c),
                                         HyperbolicOps.project_to_ball(t_r, c), c)
 
@@ -288,8 +291,9 @@ class HyperbolicRotH(_EntityDecoderBase):
         r_idx = trip[:, 1]
         s_emb = HyperbolicOps.project_to_ball(ent[trip[:, 0]], c)
         s_tan = self._reshape_tangent(self.dropout(HyperbolicOps.log_map_zero(s_emb, c)))
-        rot_s = HyperbolicOps.exp_map_zero(givens_rotation(s_tan, _ag.linear(self.rot_proj, rel[r_idx])).contiguous(), c)
-        t_r = HyperbolicOps.exp_map_zero(_ag.linear(self.trans_proj, rel[r_idx]).contiguous(), c)
+        rr = rel[r_idx]  # one gather (and one index backward) for both projections
+        rot_s = HyperbolicOps.exp_map_zero(givens_rotation(s_tan, _ag.linear(self.rot_proj, rr)).contiguous(), c)
+        t_r = HyperbolicOps.exp_map_zero(_ag.linear(self.trans_proj, rr).contiguous(), c)
         return HyperbolicOps.mobius_add(HyperbolicOps.project_to_ball(rot_s, c),
                                         HyperbolicOps.project_to_ball(t_r, c), c)
 
@@ -419,12 +423,12 @@ class _RelDecoderBase(nn.Module):
         return _chunked_hyperbolic_dist_score(q, rel_hyp, self.rel_bias, self.c, self.query_chunk_size,
                                               self.candidate_chunk_size, **self._score_kw())
 
-    def loss(self, entity_embedding, rel_embedding, triplets):
+    def loss(self, entity_embedding, rel_embedding, triplets, reduction="mean"):
         q = self._query(entity_embedding, triplets)
         rel_hyp = HyperbolicOps.exp_map_zero(rel_embedding.contiguous(), self.c)
         return _chunked_hyperbolic_ce_loss(q, rel_hyp, triplets[:, 1], self.c, self.candidate_chunk_size,
                                            candidate_bias=self.rel_bias, q_chunk_size=self.query_chunk_size,
-                                           **self._score_kw())
+                                           reduction=reduction, **self._score_kw())
 
     def _score_kw(self):
         return dict(score_scale=self._score_scale(), score_margin=self.score_margin)

@@ -854,22 +854,24 @@ class HyperbolicRecurrentRGCN(nn.Module):
         return self._decode_losses(pre_emb, r_emb, triples, c_val)
 
     def get_loss_batches(self, glist, triples, static_graph, use_cuda, batch_size, query_time=None,
-                         combine=None):
+                         combine=None, group_budget=1 << 28):
         """One snapshot's training losses and gradients with ONE encoder forward (SURVEY.md
         §8(f) f1).  hyperbolic_main.py:585-598 recomputes the encoder for every
         `batch_size` mini-batch, back-propagates each mini-batch loss and steps once per
         snapshot, so the gradient is the sum over mini-batches.  Here the final entity and
-        relation embeddings are cut from the graph as leaf tensors; each mini-batch's
-        decoder loss is back-propagated as soon as it is formed (the reference's per
-        mini-batch peak memory: one (2*batch_size) x |V| score block alive at a time),
-        accumulating into those leaves and the decoder parameters, and one backward
-        through the encoder follows with the accumulated embedding gradients.  Same
-        gradients as the reference loop; the encoder dropout draws one mask per snapshot
-        instead of one per mini-batch.
+        relation embeddings are cut from the graph as leaf tensors; the decoders run once over
+        a GROUP of consecutive mini-batches (every mini-batch while the group's B x |V|
+        backward coefficient block stays under `group_budget` floats), each mini-batch's loss
+        is the mean of its own queries' losses (the decoder losses are per query, the radius
+        loss per mini-batch over its own distinct entities), the group back-propagates
+        sum_b combine(losses_b) once, and one backward through the encoder follows with the
+        accumulated embedding gradients.  Same gradients as the reference loop; the dropout
+        masks are drawn once per group (decoders) and once per snapshot (encoder) instead of
+        once per mini-batch.
 
         `combine(le, lr, ls, lrad)` -> the scalar each mini-batch back-propagates
         (default: the plain sum).  Returns the detached [(loss_ent, loss_rel, loss_static,
-        loss_radius), ...]."""
+        loss_radius), ...] per mini-batch."""
         if combine is None:
             combine = lambda le, lr, ls, lrad: le + lr + ls.sum() + lrad  # noqa: E731
         c_val = self._loss_curvature()
@@ -877,53 +879,83 @@ class HyperbolicRecurrentRGCN(nn.Module):
         pre_emb = self._final_embedding(evolve_embs[-1], c_val)
         grad_on = torch.is_grad_enabled()
         srcs = (pre_emb, r_emb) + ((c_val,) if torch.is_tensor(c_val) else ())
-        # a learned curvature is cut too: the mini-batch decoders accumulate its gradient into
-        # the leaf, which the final encoder backward carries on to log_c
+        # a learned curvature is cut too: the decoders accumulate its gradient into the leaf,
+        # which the final encoder backward carries on to log_c
         cut = [t.detach().requires_grad_(grad_on and t.requires_grad) for t in srcs]
         c_dec = cut[2] if len(cut) > 2 else c_val
         self.decoder_ob.c = c_dec
         self.rdecoder.c = c_dec
         parts = []
-        for b in range(0, triples.shape[0], batch_size):
-            losses = self._decode_losses(cut[0], cut[1], triples[b:b + batch_size], c_dec)
-            total = combine(*losses)
-            if grad_on and total.requires_grad:
-                total.backward()
-            parts.append(tuple(t.detach() for t in losses))
+        n = triples.shape[0]
+        per_group = max(1, int(group_budget) // max(1, 2 * batch_size * max(self.num_ents, 2 * self.num_rels)))
+        for g0 in range(0, n, per_group * batch_size):
+            g1 = min(n, g0 + per_group * batch_size)
+            vecs = self._decode_losses(cut[0], cut[1], triples[g0:g1], c_dec, batch_size=batch_size)
+            per_batch = list(zip(*(v.unbind(0) for v in vecs)))  # views; one stack in backward
+            if grad_on:
+                total = sum(combine(*losses) for losses in per_batch)
+                if total.requires_grad:
+                    total.backward()
+            parts.extend(tuple(t.detach() for t in losses) for losses in per_batch)
         roots = [(src, leaf.grad) for src, leaf in zip(srcs, cut)
                  if src.requires_grad and leaf.grad is not None]
         if roots:
             torch.autograd.backward([r[0] for r in roots], [r[1] for r in roots])
         return parts
 
-    def _decode_losses(self, pre_emb, r_emb, triples, c_val):
-        """hyperbolic_model.py:996-1073: decoders on the final embedding + radius loss."""
+    def _decode_losses(self, pre_emb, r_emb, triples, c_val, batch_size=None):
+        """hyperbolic_model.py:996-1073: decoders on the final embedding + radius loss.
+        batch_size: `triples` holds consecutive mini-batches of that size (the last may be
+        short); returns each loss as a vector with one entry per mini-batch, each the value
+        the mini-batch alone gives (the decoders' per-query losses averaged over the
+        mini-batch's queries by one small product, the radius loss over its own entities)."""
         dev = pre_emb.device
-        loss_ent = torch.zeros(1, device=dev)
-        loss_rel = torch.zeros(1, device=dev)
-        loss_static = torch.zeros(1, device=dev)
+        n = triples.shape[0]
+        nb = 1 if batch_size is None else (n + batch_size - 1) // batch_size
         inverse_triples = triples.flip(1)
         inverse_triples[:, 1] = inverse_triples[:, 1] + self.num_rels
         all_triples = torch.cat([triples, inverse_triples]).to(dev)
+        if batch_size is None:
+            red, avg, seg = "mean", None, None
+        else:
+            # query i (and its inverse n + i) belongs to mini-batch i // batch_size
+            seg = torch.arange(n, device=dev) // batch_size
+            seg = torch.cat([seg, seg])
+            onehot = (seg.unsqueeze(0) == torch.arange(nb, device=dev).unsqueeze(1)).float()
+            avg = onehot / onehot.sum(1, keepdim=True)  # nb x 2n, rows average a mini-batch
+            red = "none"
+        zero = torch.zeros(nb, device=dev) if batch_size is not None else torch.zeros(1, device=dev)
+        loss_ent, loss_rel = zero, zero
+        loss_static = torch.zeros(nb, 1, device=dev) if batch_size is not None else torch.zeros(1, device=dev)
         if self.entity_prediction:
             if hasattr(self.decoder_ob, "loss"):
-                loss_ent = self.decoder_ob.loss(pre_emb, r_emb, all_triples)
+                loss_ent = self.decoder_ob.loss(pre_emb, r_emb, all_triples, reduction=red)
             else:
                 scores_ob = self.decoder_ob.forward(pre_emb, r_emb, all_triples).view(-1, self.num_ents)
-                loss_ent = self.loss_e(scores_ob, all_triples[:, 2])
+                loss_ent = F.cross_entropy(scores_ob, all_triples[:, 2], reduction=red)
+            if avg is not None:
+                loss_ent = avg @ loss_ent
         if self.relation_prediction:
             if hasattr(self.rdecoder, "loss"):
-                loss_rel = self.rdecoder.loss(pre_emb, r_emb, all_triples)
+                loss_rel = self.rdecoder.loss(pre_emb, r_emb, all_triples, reduction=red)
             else:
                 score_rel = self.rdecoder.forward(pre_emb, r_emb, all_triples, mode="train").view(-1, 2 * self.num_rels)
-                loss_rel = self.loss_r(score_rel, all_triples[:, 1])
+                loss_rel = F.cross_entropy(score_rel, all_triples[:, 1], reduction=red)
+            if avg is not None:
+                loss_rel = avg @ loss_rel
         # MSE over the batch's distinct entities (hyperbolic_model.py:1067-1073 takes
         # torch.unique of them): a membership mask over all entities instead, so the loss has
         # a static shape and no host synchronisation (unique's output size is data-dependent)
-        seen = torch.zeros(self.num_ents, device=dev, dtype=torch.float32)
-        seen.index_fill_(0, all_triples[:, 0::2].reshape(-1), 1.0)  # s and o (a view)
         diff = self._static_radius(float(c_val)) - self.radius_target.to(dev)
-        loss_radius = self.radius_lambda * (seen * diff * diff).sum() / seen.sum()
+        ents = all_triples[:, 0::2]  # s and o (a view)
+        if batch_size is None:
+            seen = torch.zeros(self.num_ents, device=dev, dtype=torch.float32)
+            seen.index_fill_(0, ents.reshape(-1), 1.0)
+            loss_radius = self.radius_lambda * (seen * diff * diff).sum() / seen.sum()
+        else:
+            seen = torch.zeros(nb, self.num_ents, device=dev, dtype=torch.float32)
+            seen.index_put_((seg.repeat_interleave(2), ents.reshape(-1)), torch.ones((), device=dev))
+            loss_radius = self.radius_lambda * (seen @ (diff * diff)) / seen.sum(1)
         return loss_ent, loss_rel, loss_static, loss_radius
 
     def get_training_summary(self):

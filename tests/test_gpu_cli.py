@@ -163,8 +163,8 @@ def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder, extra)
     finally:
         torch.optim.Adam = adam
     (l0, s0), (l1, s1) = runs
-    # the step is deterministic (no atomics: relation_context and the embedding gathers
-    # accumulate through sort-based index_put, the HIP kernels sum in fixed orders), so the
+    # the step is deterministic (no atomics: the embedding gathers accumulate through
+    # sort-based index_put, the HIP kernels sum in fixed orders), so the
     # replays reproduce the eager run's losses bit for bit
     np.testing.assert_array_equal(l1, l0)
     worst = 0.0

@@ -52,7 +52,7 @@ def main():
                                 dropout=0.2, c=0.01, self_loop=True, layer_norm=False, input_dropout=0.2,
                                 hidden_dropout=0.2, feat_dropout=0.2, entity_prediction=True, relation_prediction=True,
                                 use_cuda=True, gpu=0, radius_target=rt, radius_msg_gamma=0.15).to(dev).train()
-    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5, capturable=a.graph)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-5, capturable=a.graph, fused=True)
     snaps = snapshot_series(1, V, R, T + 8, per)
     graphs = [G.build_sub_graph(V, R, s, True, dev) for s in snaps]
     samples = [(graphs[i:i + T], torch.from_numpy(snaps[i + T]).to(dev)) for i in range(8)]
