@@ -112,7 +112,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
   Frag v;
   v.zero();
   if (pos) {
-    if (p.w_n) mfma_tile_pf(v, part, lda, p.w_n, p.d, br);
+    if (p.w_n) mfma_tile_pf(v, part, lda, p.w_n, p.d, br, p.d);
     else frag_from_tile(v, part, lda, p.d);
     if (!p.euclid) {
 #pragma unroll
@@ -129,15 +129,15 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
     acc[1].zero();
     const float* Ts[2] = {X, P2};
     const float* Ws[2] = {wsel, p.step.w_g};
-    mfma_tiles<2, RING>(acc, Ts, Ws, lda, p.d);
+    mfma_tiles<2, RING>(acc, Ts, Ws, lda, p.d, p.d);
 #pragma unroll
     for (int j = 0; j < TPW; ++j) v.t[j] += acc[0].t[j];
     tw = acc[1];
   } else if (wsel) {
     Frag lp;
     lp.zero();
-    if (wfirst == wsel && !(pos && p.w_n)) mfma_tile_pf(lp, X, lda, wsel, p.d, br);
-    else mfma_tile(lp, X, lda, wsel, p.d);
+    if (wfirst == wsel && !(pos && p.w_n)) mfma_tile_pf(lp, X, lda, wsel, p.d, br, p.d);
+    else mfma_tile(lp, X, lda, wsel, p.d, p.d);
 #pragma unroll
     for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
   }
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
   if (p.prev_t) {  // v = g v + (1 - g) prev_t, g = sigmoid(prev_t @ W_skip + b)
     Frag g;
     g.zero();
-    mfma_tile(g, P1, lda, p.w_skip, p.d);
+    mfma_tile(g, P1, lda, p.w_skip, p.d, p.d);
     Frag pt;
     frag_from_tile(pt, P1, lda, p.d);
     float b[TPW];

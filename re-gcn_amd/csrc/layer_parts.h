@@ -144,7 +144,7 @@ __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4],
   if (tw_pre) return step_epilogue_tw(rr, ct, n2, P, lda, trow, n_valid, p, *tw_pre, trace);
   Frag tw;
   tw.zero();
-  mfma_tile(tw, P, lda, p.w_g, p.d);
+  mfma_tile(tw, P, lda, p.w_g, p.d, p.d);
   step_epilogue_tw(rr, ct, n2, P, lda, trow, n_valid, p, tw, trace);
 }
 

@@ -86,9 +86,17 @@ __device__ __forceinline__ void stage_rows(float* T, int lda, const float* __res
   }
 }
 
-__device__ __forceinline__ void mfma_tpw(Frag& acc, float a, bvec b) {
+// nt: this wave's column tiles that hold output columns (wave-uniform); the rest of the
+// packed weight is zero padding (d_out < 256), whose MFMAs are skipped.
+__device__ __forceinline__ void mfma_tpw(Frag& acc, float a, bvec b, int nt = TPW) {
 #pragma unroll
-  for (int j = 0; j < TPW; ++j) acc.t[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[j], acc.t[j], 0, 0, 0);
+  for (int j = 0; j < TPW; ++j)
+    if (j < nt) acc.t[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[j], acc.t[j], 0, 0, 0);
+}
+
+// column tiles of this wave below n_out output columns
+__device__ __forceinline__ int wave_tiles(int n_out) {
+  return min(TPW, max(0, (n_out - 16 * TPW * wave_id() + 15) >> 4));
 }
 
 // This wave's B fragments in the packed layout: k-step s lives at bsrc + s * B_STEP.
@@ -111,9 +119,11 @@ struct BRing {
 };
 
 // acc += T[16 x d] @ W (T in LDS, W packed with d_in = d), ring pre-filled by BRing::load.
+// n_out: W's output columns (the MFMAs of column tiles past it are skipped).
 __device__ __forceinline__ void mfma_tile_pf(Frag& acc, const float* T, int lda, const float* __restrict__ Wp, int d,
-                                             BRing& br) {
+                                             BRing& br, int n_out = MAX_D) {
   const int lane = threadIdx.x & 63;
+  const int nt = wave_tiles(n_out);
   const int S = d >> 2;
   const bvec* bsrc = bsrc_of(Wp);
   const float* arow = T + (lane & 15) * lda + (lane >> 4);
@@ -127,7 +137,7 @@ __device__ __forceinline__ void mfma_tile_pf(Frag& acc, const float* T, int lda,
   for (; s + RING <= S; s += RING) {
 #pragma unroll
     for (int i = 0; i < RING; ++i) {
-      mfma_tpw(acc, aring[i], ring[i]);
+      mfma_tpw(acc, aring[i], ring[i], nt);
       __builtin_amdgcn_sched_barrier(0);
       const int nx = min(s + i + RING, S - 1);
       ring[i] = bsrc[(int64_t)nx * B_STEP];  // unconditional: hipcc can count it
@@ -137,22 +147,25 @@ __device__ __forceinline__ void mfma_tile_pf(Frag& acc, const float* T, int lda,
   }
 #pragma unroll
   for (int i = 0; i < RING; ++i)
-    if (s + i < S) mfma_tpw(acc, aring[i], ring[i]);
+    if (s + i < S) mfma_tpw(acc, aring[i], ring[i], nt);
 }
 
 // acc += T[16 x d] @ W.  No barriers inside.
-__device__ __forceinline__ void mfma_tile(Frag& acc, const float* T, int lda, const float* __restrict__ Wp, int d) {
+__device__ __forceinline__ void mfma_tile(Frag& acc, const float* T, int lda, const float* __restrict__ Wp, int d,
+                                          int n_out = MAX_D) {
   BRing br;
   br.load(Wp, d);
-  mfma_tile_pf(acc, T, lda, Wp, d, br);
+  mfma_tile_pf(acc, T, lda, Wp, d, br, n_out);
 }
 
 // N independent GEMMs acc[n] += T[n] @ W[n] (same d) in one k-loop: N x TPW MFMA chains per
 // k-step, so each ring of R B fragments covers N times the latency one GEMM's ring does
 // (the weights of a small grid come from HBM, not a warm L2).
 template <int N, int R>
-__device__ __forceinline__ void mfma_tiles(Frag* acc, const float* const* T, const float* const* W, int lda, int d) {
+__device__ __forceinline__ void mfma_tiles(Frag* acc, const float* const* T, const float* const* W, int lda, int d,
+                                           int n_out = MAX_D) {
   const int lane = threadIdx.x & 63;
+  const int nt = wave_tiles(n_out);
   const int S = d >> 2;
   const bvec* bsrc[N];
   const float* arow[N];
@@ -175,7 +188,7 @@ __device__ __forceinline__ void mfma_tiles(Frag* acc, const float* const* T, con
 #pragma unroll
     for (int i = 0; i < R; ++i) {
 #pragma unroll
-      for (int n = 0; n < N; ++n) mfma_tpw(acc[n], aring[n][i], ring[n][i]);
+      for (int n = 0; n < N; ++n) mfma_tpw(acc[n], aring[n][i], ring[n][i], nt);
       __builtin_amdgcn_sched_barrier(0);
       const int nx = min(s + i + R, S - 1);
 #pragma unroll
@@ -190,7 +203,7 @@ __device__ __forceinline__ void mfma_tiles(Frag* acc, const float* const* T, con
   for (int i = 0; i < R; ++i)
     if (s + i < S) {
 #pragma unroll
-      for (int n = 0; n < N; ++n) mfma_tpw(acc[n], aring[n][i], ring[n][i]);
+      for (int n = 0; n < N; ++n) mfma_tpw(acc[n], aring[n][i], ring[n][i], nt);
     }
 }
 

@@ -130,7 +130,7 @@ __device__ __forceinline__ void skip_gate(Frag& v, const float* P, int lda, cons
                                           int d) {
   Frag g;
   g.zero();
-  mfma_tile(g, P, lda, w_skip, d);
+  mfma_tile(g, P, lda, w_skip, d, d);
   Frag pt;
   frag_from_tile(pt, P, lda, d);
   float b[TPW];
@@ -162,7 +162,7 @@ __device__ __forceinline__ void a_pos_rows(const PhaseArgs& p, int b, float* lds
   __syncthreads();
   Frag acc;
   acc.zero();
-  mfma_tile_pf(acc, X, lda, gate ? p.step.w_g : p.L[0].w_loop, p.d, br);
+  mfma_tile_pf(acc, X, lda, gate ? p.step.w_g : p.L[0].w_loop, p.d, br, p.d);
   frag_store(acc, gate ? p.tw : p.s1, trow, count, p.d);
 }
 
@@ -259,7 +259,7 @@ __device__ __forceinline__ int gather_tile(const PhaseArgs& p, const LayerArgs& 
 // loaded by the caller behind the gather.
 __device__ __forceinline__ void agg_term(Frag& v, const LayerArgs& l, const float* part, int lda, BRing& br) {
   v.zero();
-  if (l.w_n) mfma_tile_pf(v, part, lda, l.w_n, l.d, br);
+  if (l.w_n) mfma_tile_pf(v, part, lda, l.w_n, l.d, br, l.d);
   else frag_from_tile(v, part, lda, l.d);
 #pragma unroll
   for (int j = 0; j < TPW; ++j) v.t[j] = clamp4(v.t[j], -10.f, 10.f);
@@ -305,7 +305,7 @@ __device__ __forceinline__ void b_pos_tile(const PhaseArgs& p, int tile, float* 
     __syncthreads();
     Frag lp;
     lp.zero();
-    mfma_tile_pf(lp, X, L.lda, l1.w_loop, p.d, br1);
+    mfma_tile_pf(lp, X, L.lda, l1.w_loop, p.d, br1, p.d);
     mid_stamp(p, 6);
     frag_store(lp, p.s1, trow, count, p.d);
   }
@@ -376,7 +376,7 @@ __device__ __forceinline__ void a_zero_rows(const PhaseArgs& p, int b, float* ld
   if (l0.w_evolve) {
     Frag lp;
     lp.zero();
-    mfma_tile_pf(lp, X, lda, l0.w_evolve, p.d, br);
+    mfma_tile_pf(lp, X, lda, l0.w_evolve, p.d, br, p.d);
 #pragma unroll
     for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
   }
@@ -411,7 +411,7 @@ __device__ __forceinline__ void b_zero_rows(const PhaseArgs& p, int b, float* ld
   if (l.w_evolve) {
     Frag lp;
     lp.zero();
-    mfma_tile_pf(lp, X1, lda, l.w_evolve, p.d, br);
+    mfma_tile_pf(lp, X1, lda, l.w_evolve, p.d, br, p.d);
 #pragma unroll
     for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
   }
@@ -442,7 +442,7 @@ __device__ __forceinline__ void c_zero_rows(const PhaseArgs& p, int b, float* ld
   mid_stamp(p, 1);
   Frag tw;
   tw.zero();
-  mfma_tile_pf(tw, P2, lda, p.step.w_g, p.d, br);
+  mfma_tile_pf(tw, P2, lda, p.step.w_g, p.d, br, p.d);
   mid_stamp(p, 2);
   step_epilogue_tw(rr, v, n2, P2, lda, trow, count, p.step, tw);
 }

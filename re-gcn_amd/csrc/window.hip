@@ -131,8 +131,8 @@ __device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_r
       if (p.w_evolve0) {
         Frag lp;
         lp.zero();
-        if (t == 0) mfma_tile_pf(lp, XI, lda, p.w_evolve0, p.d, br);
-        else mfma_tile(lp, XI, lda, p.w_evolve0, p.d);
+        if (t == 0) mfma_tile_pf(lp, XI, lda, p.w_evolve0, p.d, br, p.d);
+        else mfma_tile(lp, XI, lda, p.w_evolve0, p.d, p.d);
 #pragma unroll
         for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
       }
@@ -157,31 +157,31 @@ __device__ __forceinline__ void chain_tile(const ChainArgs& p, int tile, int n_r
         if (p.w_evolve1) {
           Frag lp;
           lp.zero();
-          mfma_tile(lp, X1, lda, p.w_evolve1, p.d);
+          mfma_tile(lp, X1, lda, p.w_evolve1, p.d, p.d);
 #pragma unroll
           for (int j = 0; j < TPW; ++j) v.t[j] += lp.t[j];
         }
         tw.zero();
-        mfma_tile(tw, P2, lda, p.step.w_g, p.d);
+        mfma_tile(tw, P2, lda, p.step.w_g, p.d, p.d);
       } else if (p.w_evolve1) {
         Frag acc[2];
         acc[0].zero();
         acc[1].zero();
         const float* Ts[2] = {X1, P2};
         const float* Ws[2] = {p.w_evolve1, p.step.w_g};
-        mfma_tiles<2, RING>(acc, Ts, Ws, lda, p.d);
+        mfma_tiles<2, RING>(acc, Ts, Ws, lda, p.d, p.d);
 #pragma unroll
         for (int j = 0; j < TPW; ++j) v.t[j] += acc[0].t[j];
         tw = acc[1];
       } else {
         tw.zero();
-        mfma_tile(tw, P2, lda, p.step.w_g, p.d);
+        mfma_tile(tw, P2, lda, p.step.w_g, p.d, p.d);
       }
       stamp(4);
       if (p.w_skip1) {  // v = g v + (1 - g) x, g = sigmoid(x @ W_skip + b)
         Frag g;
         g.zero();
-        mfma_tile(g, XI, lda, p.w_skip1, p.d);
+        mfma_tile(g, XI, lda, p.w_skip1, p.d, p.d);
         Frag pt;
         frag_from_tile(pt, XI, lda, p.d);
         float b[TPW];
