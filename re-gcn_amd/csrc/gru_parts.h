@@ -71,6 +71,19 @@ __host__ __device__ inline int gru2_lda(int d, int parts) {
   return n + ((8 - n % 16) + 16) % 16;
 }
 
+// XCD-grouped order of a launch's GRU blocks: blocks g and g + 8 share an XCD (round-robin
+// dispatch), so class g % 8 takes a contiguous run of the (column tile, row tile) order and
+// each column tile's weight slice (read by every row tile) is fetched into one or two XCDs'
+// L2s instead of all eight.  The launch pads the GRU blocks to a multiple of 8 (the pads
+// return at once).
+__host__ __device__ inline int gru_blocks_padded(int n) { return (n + 7) & ~7; }
+__device__ __forceinline__ bool gru_block_xcd(int g, int n, int rt, int& bx, int& by) {
+  const int w = (g & 7) * ((n + 7) >> 3) + (g >> 3);
+  bx = w % rt;
+  by = w / rt;
+  return w < n;
+}
+
 inline size_t gru_pre_lds_bytes(int d) { return (size_t)TM * gru2_lda(d, 2) * 4 + (size_t)PRE_WAVES * 3 * 64 * 16; }
 
 // Workgroup (bx, by) of the pre-phase: relation rows 16 bx.., output column tile by.

@@ -473,8 +473,12 @@ __global__ __launch_bounds__(NTHR) void k_phase_a(PhaseArgs p) {
     return a_pos_rows(p, b, lds);
   }
   b -= 2 * p.n_pos_rt;
-  if (b < p.n_gru) return gru_x_block(p.gru, b % p.gru_rt, b / p.gru_rt, lds);
-  b -= p.n_gru;
+  if (b < gru_blocks_padded(p.n_gru)) {
+    int bx, by;
+    if (gru_block_xcd(b, p.n_gru, p.gru_rt, bx, by)) gru_x_block(p.gru, bx, by, lds);
+    return;
+  }
+  b -= gru_blocks_padded(p.n_gru);
   if (b < p.n_zero_rt) return a_zero_rows(p, b, lds);
   copy_block(p, b - p.n_zero_rt);
 }
@@ -493,7 +497,8 @@ __global__ __launch_bounds__(NTHR) void k_phase_b(PhaseArgs p) {
   b -= p.L[0].n_pos_tiles;
   if (b < p.n_zero_rt) return b_zero_rows(p, b, lds);
   b -= p.n_zero_rt;
-  gru_pre_block(p.gru, b % p.gru_rt, b / p.gru_rt, lds);
+  int bx, by;
+  if (gru_block_xcd(b, p.n_gru, p.gru_rt, bx, by)) gru_pre_block(p.gru, bx, by, lds);
 }
 
 template <int AGG, int S>
@@ -559,7 +564,7 @@ int timestep_phase(PhaseArgs a, int phase, hipStream_t st) {
     a.n_gru = a.gru.h_out ? gru_blocks : 0;
     if (a.n_gru && (!a.gru.h_prev || !a.gru.w_ih_x || !a.gru.pre || (!a.gru.x_mean && !a.gru.rel_start)))
       return set_error(REGCN_EINVAL, "GRU x-phase operands missing");
-    grid = (unsigned)(2 * a.n_pos_rt + a.n_gru + n_zero_rt + a.n_copy);
+    grid = (unsigned)(2 * a.n_pos_rt + gru_blocks_padded(a.n_gru) + n_zero_rt + a.n_copy);
     lds = std::max({2 * tile + TM * 4, tile + small, a.n_gru ? gru_x_lds_bytes(d) : 0});
     if (grid) hipLaunchKernelGGL(k_phase_a, dim3(grid), dim3(NTHR), lds, st, a);
     return grid ? check_launch("k_phase_a") : 0;
@@ -568,7 +573,7 @@ int timestep_phase(PhaseArgs a, int phase, hipStream_t st) {
     a.n_gru = a.gru.pre ? gru_blocks : 0;
     if (a.n_gru && (!a.gru.emb_rel || !a.gru.h_prev || !a.gru.w_ih_e || !a.gru.w_hh || !a.gru.b_ih || !a.gru.b_hh))
       return set_error(REGCN_EINVAL, "GRU pre-phase operands missing");
-    grid = (unsigned)(l0.n_pos_tiles + n_zero_rt + a.n_gru);
+    grid = (unsigned)(l0.n_pos_tiles + n_zero_rt + gru_blocks_padded(a.n_gru));
     lds = std::max({(size_t)glds(d, gen, GATHER_ROWS).total_bytes, 2 * tile + small,
                     a.n_gru ? gru_pre_lds_bytes(d) : 0});
   } else {
