@@ -778,11 +778,17 @@ def run_scale(args, cfg, world, rank, device, backend):
     from regcn_amd import _lib
     from regcn_amd import graph as G
     from regcn_amd.synthetic import snapshot_series
+    from regcn_amd.parallel import ShardedGraph
     d, T, V, R = args.d, cfg["T"], cfg["V"], cfg["R"]
     n_win = args.pool or 2
     t_setup = time.time()
-    snaps = snapshot_series(100 + 7919 * rank, V, R, T + n_win, cfg["per_snap"])  # replicas: own data per rank
+    # replicas: own data per rank; --shard edge|owner: every rank holds the same snapshots and
+    # processes its partition of each (strong scaling)
+    sharded = args.shard != "replica" and world > 1
+    snaps = snapshot_series(100 if sharded else 100 + 7919 * rank, V, R, T + n_win, cfg["per_snap"])
     graphs = [G.build_sub_graph(V, R, s, True, device) for s in snaps[:T + n_win - 1]]
+    if sharded:
+        graphs = [ShardedGraph(g, args.shard) for g in graphs]
     tests = [torch.from_numpy(np.ascontiguousarray(snaps[T + i][:args.queries // 2])).to(device)
              for i in range(n_win)]
     del snaps
@@ -816,11 +822,15 @@ def run_scale(args, cfg, world, rank, device, backend):
             _lib.EVENT_TRACE = None
 
     elapsed, edges_total = _timed(world, device, backend, run, edges_local)
+    if sharded:  # every rank processed its part of the same edges: count them once
+        edges_total = float(edges_local)
     value = edges_total / elapsed / 1e6
     out = None
     if rank == 0:
         calls = summarize_trace(trace, args.steps)
-        work, stats = scale_work(model, windows[0], B)
+        work, stats = scale_work(model, [getattr(g, "g", g) for g in windows[0]], B)
+        if sharded:  # a rank's launches do its partition's share: no per-launch roofline
+            work = {k: (0.0, 0.0) for k in work}
         kernels = {}
         for name, v in calls.items():
             flops, nbytes = work.get(name, (0.0, 0.0))
@@ -832,7 +842,7 @@ def run_scale(args, cfg, world, rank, device, backend):
                          frac=round(wv["frac"], 4))
             kernels[name] = e
         dom = max(calls, key=lambda k: calls[k]["ms"] * calls[k]["per_step"])
-        flops, nbytes = work[dom]
+        flops, nbytes = work.get(dom, (0.0, 0.0))
         wv = _work(flops, nbytes, calls[dom]["ms"])
         kname = SCALE_KERNEL.get(dom, dom)
         traffic, tsrc = pmc_for(kname, args.config, d)
@@ -848,7 +858,7 @@ def run_scale(args, cfg, world, rank, device, backend):
                      if k not in ("regcn_hyp_score_jobs_f32", "regcn_roth_queries_f32"))
         out = {"metric": METRIC, "value": round(value, 3), "unit": "M edges/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "f32",
                "data": "synthetic (config-5 snapshots: Zipf(1.1) subjects/objects, uniform relations, 60% "
                        "recurring triples; random-init weights)",
                "config": {"workload": cfg["label"] + " (BASELINE.json configs[4]) on 1 GPU per rank: "
@@ -858,7 +868,9 @@ def run_scale(args, cfg, world, rank, device, backend):
                           "edges_per_snapshot": 2 * cfg["per_snap"], "history_len": T, "n_layers": 2, "d": d,
                           "edges_per_step": int(np.mean(epw)), "queries_per_step": B, "windows": n_win,
                           "encoder_launches": "timestep phases" if model.use_phases else "per-layer",
-                          "hip_graph": False, "parallelism": "replicas x%d" % world,
+                          "hip_graph": False,
+                          "parallelism": ("%s-partitioned snapshots x%d" % (args.shard, world)) if sharded
+                          else "replicas x%d" % world,
                           "snapshot_stats": {k: round(v) for k, v in stats.items()}},
                "roofline": roof, "kernels": kernels,
                "breakdown": {"encoder_ms_per_step": round(enc_ms, 3),

@@ -310,6 +310,7 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
 
     best_mrr, best_epoch, patience = 0.0, 0, 20
     epoch_loss = []
+    valid_history = []  # (epoch, raw MRR, filtered MRR, raw rel MRR, filtered rel MRR) per validation
     t_start = time.time()
     initial_curvature = None
     for epoch in range(args.n_epochs):
@@ -388,6 +389,7 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
                     # initial state, memo) so validation scores the current weights
                     invalidate(model)
                 res = test(model, train_list, valid_list, num_rels, num_nodes, device, all_ans_v, all_ans_r_v, args)
+                valid_history.append((epoch,) + tuple(float(v) for v in res))
                 logger.info("Validation - MRR: raw=%.4f, filter=%.4f | Rel MRR: raw=%.4f, filter=%.4f", *res)
                 cur = res[2] if args.relation_evaluation else res[0]
                 if cur > best_mrr:
@@ -403,7 +405,7 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
             if float(stop) > 0:
                 break
     logger.info("Training completed in %.1f minutes", (time.time() - t_start) / 60)
-    return {"best_mrr": best_mrr, "best_epoch": best_epoch, "epoch_loss": epoch_loss}
+    return {"best_mrr": best_mrr, "best_epoch": best_epoch, "epoch_loss": epoch_loss, "valid": valid_history}
 
 
 def main(argv=None):

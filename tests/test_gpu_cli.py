@@ -126,8 +126,10 @@ def test_cli_training_replicas(tmp_path):
 def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder, extra):
     """--hip-graph (each sample's whole step captured after its first run and replayed:
     training.GraphedSteps) trains the same model as the eager loop: dropout off, the same
-    seeds and sample order; epoch losses bit for bit and every parameter tensor to 1e-6 in
-    relative norm (epochs 2-3 are replays; measured: bitwise equal).  MuRP's relation decoder
+    seeds and sample order; epoch losses bit for bit, every parameter tensor to 1e-6 in
+    relative norm (epochs 2-3 are replays; measured: bitwise equal) and the validation MRRs
+    after every epoch equal (validation under graphs must not score stale parameter-keyed
+    caches: a replay updates the weights without bumping their versions).  MuRP's relation decoder
     (no score scale / margin: device constants by fill kernels) and the per-relation curvature
     score replay too.  Not covered: ConvTransE (its eager runs differ in the 6th digit: MIOpen
     convolution)."""
@@ -138,7 +140,7 @@ def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder, extra)
               "--test-history-len", "3", "--relation-prediction", "--entity-prediction",
               "--checkpoint", str(tmp_path / "m.pth"), "--seed", "0", "--lr", "0.01", "--triple-batch-size", "64",
               "--dropout", "0", "--input-dropout", "0", "--hidden-dropout", "0", "--feat-dropout", "0",
-              "--n-epochs", "3", "--evaluate-every", "100"] + extra
+              "--n-epochs", "4", "--evaluate-every", "1"] + extra
     dev = torch.device("cuda", 0)
     runs = []
     adam = torch.optim.Adam
@@ -159,10 +161,12 @@ def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder, extra)
             random.seed(0)
             out = cli.train_model(args, model, tl, valid, V, R, dev, str(tmp_path / "m.pth"))
             torch.cuda.synchronize()
-            runs.append((out["epoch_loss"], {k: v.detach().clone() for k, v in model.state_dict().items()}))
+            runs.append((out["epoch_loss"], {k: v.detach().clone() for k, v in model.state_dict().items()},
+                         out["valid"]))
     finally:
         torch.optim.Adam = adam
-    (l0, s0), (l1, s1) = runs
+    (l0, s0, v0), (l1, s1, v1) = runs
+    assert len(v0) == 3 and v1 == v0, (v0, v1)
     # the step is deterministic (no atomics: the embedding gathers accumulate through
     # sort-based index_put, the HIP kernels sum in fixed orders), so the
     # replays reproduce the eager run's losses bit for bit
