@@ -255,6 +255,16 @@ def call_layer(desc):
           "regcn_layer_f32(step)" if desc.fuse_step else "regcn_layer_f32")
 
 
+def publish():
+    """Make device data just written on the current stream safe to read from any stream.
+    Lazily built caches (packed weights, a snapshot's edge orders, parameter-only states) are
+    read by whichever stream asks next -- another lane's predict may run on another stream --
+    so the builder waits for its kernels once.  Inside a HIP-graph capture the graph keeps its
+    own order and nothing is done."""
+    if not torch.cuda.is_current_stream_capturing():
+        torch.cuda.current_stream().synchronize()
+
+
 def stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 

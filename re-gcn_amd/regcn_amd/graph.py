@@ -258,6 +258,7 @@ class SnapshotGraph:
         for k, v in t.items():
             setattr(a, k, ctypes.c_void_p(v.data_ptr()))
         _lib.call_desc("regcn_snapshot_transpose_i32", a)
+        _lib.publish()  # cached: read next by whichever stream asks
         self.__dict__["_transposed"] = t
         return t
 
@@ -282,6 +283,7 @@ class SnapshotGraph:
             _lib.call("regcn_snapshot_row_type_order_i32", V, E, R2, _lib.iptr(wk["rowptr"]), _lib.iptr(wk["col_src"]),
                       _lib.iptr(wk["col_type"]), _lib.iptr(t[0]), _lib.iptr(t[1]), ws.data_ptr(), ws.numel(),
                       _lib.stream())
+            _lib.publish()  # cached: read next by whichever stream asks
         self.__dict__["_row_type"] = t
         return t
 

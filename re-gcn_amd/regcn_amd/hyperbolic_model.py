@@ -327,8 +327,9 @@ class HyperbolicRecurrentRGCN(nn.Module):
             return hit[1]  # parameter-only value: computed once per parameter version
         radius = torch.clamp(p, min=self.radius_min, max=self.radius_max)
         radius = torch.clamp(radius, max=1.0 / math.sqrt(c_val) - 1e-6)
-        if not torch.is_grad_enabled():
+        if not torch.is_grad_enabled() and self.param_caches:
             self._r_static_cache = (key, radius.detach().contiguous())
+            _lib.publish()
         return radius
 
     def _wants_grad(self):
@@ -405,7 +406,8 @@ class HyperbolicRecurrentRGCN(nn.Module):
         r = torch.empty(V, device=pe.device, dtype=torch.float32)
         _lib.call("regcn_init_entities_f32", _lib.fptr(dyn, "dynamic_emb"), _lib.fptr(r_static), V, d, c_val,
                   int(bool(self.layer_norm)), _lib.fptr(h), _lib.fptr(x), _lib.fptr(r), _lib.stream())
-        if not torch.cuda.is_current_stream_capturing():
+        if self.param_caches and not torch.cuda.is_current_stream_capturing():
+            _lib.publish()
             self.__dict__["_init_cache"] = (key, (h, x, r))
         return h, x, r
 
@@ -477,7 +479,8 @@ class HyperbolicRecurrentRGCN(nn.Module):
         if hit is not None and hit[0] == key and self.param_caches:
             return hit[1]
         pre = relation_gru_pre(gru, emb, emb)
-        if not torch.cuda.is_current_stream_capturing():
+        if self.param_caches and not torch.cuda.is_current_stream_capturing():
+            _lib.publish()
             self.__dict__["_gru_pre0"] = (key, pre)
         return pre
 
@@ -719,6 +722,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
             self.__dict__["_chain_operands"] = (rows, n_rows)
             return states
         if not torch.cuda.is_current_stream_capturing():
+            _lib.publish()
             self.__dict__["_pristine_cache"] = (key, states)
         else:
             self.__dict__.setdefault("_capture_keep", []).append((rows, n_rows, states))

@@ -15,6 +15,7 @@ normalize, GRUCell) as device torch ops.  The op sequence is the reference's:
 import torch
 import torch.nn.functional as F
 
+from . import _lib
 from . import autograd as A
 
 RRELU_SLOPE = (1.0 / 8 + 1.0 / 3) / 2  # F.rrelu(x) with training=False (hyperbolic_model.py:120)
@@ -25,6 +26,7 @@ def _pos_rows(g, device):
     pos = g.__dict__.get("_pos_u8")
     if pos is None or pos.device != device:
         pos = (g.in_degrees() > 0).to(device=device, dtype=torch.uint8).contiguous()
+        _lib.publish()
         g.__dict__["_pos_u8"] = pos
     return pos
 
@@ -141,6 +143,7 @@ def _entity_relation_lists(g, V, R):
     chunks = torch.stack([rows, ptr[rows], ptr[rows + 1], torch.full_like(rows, -1)], 1).to(torch.int32).contiguous()
     tr = {"rel": rel_s.contiguous() if rel_s.numel() else torch.zeros(1, device=dev, dtype=torch.int32),
           "chunks": chunks, "ones": torch.ones(V, device=dev, dtype=torch.float32)}
+    _lib.publish()
     g.__dict__["_ent_rel"] = tr
     return tr
 

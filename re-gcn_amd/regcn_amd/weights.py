@@ -3,7 +3,8 @@
 The layer tail and timestep kernels read their weights in v_mfma_f32_16x16x4_f32
 fragment order.  The packed copy is cached on the weight tensor itself and rebuilt only
 when its storage, shape or version counter changes (an optimizer step, an in-place edit,
-load_state_dict), so steady-state forwards launch no packing kernel.
+load_state_dict), so steady-state forwards launch no packing kernel.  A new packed copy is
+published (_lib.publish) before it is cached: a predict on another stream may read it next.
 """
 import torch
 
@@ -23,6 +24,7 @@ def packed(w):
     out = torch.empty(_lib.lib().regcn_packed_weight_floats(d_in), device=w.device, dtype=torch.float32)
     _lib.call("regcn_pack_weight_f32", _lib.fptr(wc, "weight"), d_in, d_out, _lib.fptr(out), _lib.stream())
     w._regcn_packed = (key, out)
+    _lib.publish()
     return out
 
 
@@ -40,6 +42,7 @@ def packed_linear(w, n_gates=1):
                       dtype=torch.float32)
     _lib.call("regcn_pack_linear_f32", _lib.fptr(wc, "weight"), n_gates, n_out, n_in, _lib.fptr(out), _lib.stream())
     w._regcn_packed_lin = (key, out)
+    _lib.publish()
     return out
 
 
@@ -58,6 +61,7 @@ def packed_linear_cols(w, n_gates, c0, c1):
                       dtype=torch.float32)
     _lib.call("regcn_pack_linear_f32", _lib.fptr(wc, "weight"), n_gates, n_out, n_in, _lib.fptr(out), _lib.stream())
     cache[(n_gates, c0, c1)] = (key, out, wc)  # keep wc alive until the packing kernel has run
+    _lib.publish()
     return out
 
 
@@ -73,6 +77,7 @@ def packed_t(w):
     out = torch.empty(_lib.lib().regcn_packed_weight_floats(n_in), device=w.device, dtype=torch.float32)
     _lib.call("regcn_pack_weight_f32", _lib.fptr(wt, "weight"), n_in, n_out, _lib.fptr(out), _lib.stream())
     w._regcn_packed_t = (key, out, wt)  # keep wt alive until the packing kernel has run
+    _lib.publish()
     return out
 
 
@@ -88,6 +93,7 @@ def packed_k4(w):
     out = torch.empty(_lib.lib().regcn_packed_k4_floats(n_out, n_in), device=w.device, dtype=torch.float32)
     _lib.call("regcn_pack_k4_f32", _lib.fptr(wc, "weight"), n_out, n_in, _lib.fptr(out), _lib.stream())
     w._regcn_packed_k4 = (key, out, wc)  # keep wc alive until the packing kernel has run
+    _lib.publish()
     return out
 
 

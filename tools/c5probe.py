@@ -27,11 +27,13 @@ def main():
     ap.add_argument("--modes", default="phases,layers")
     ap.add_argument("--encoder", default="hyperbolic_uvrgcn")
     ap.add_argument("--budgets", default="0", help="fused-layer edge budgets to compare (0: the default)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="independent predicts in flight on this many streams (two windows alternate)")
     a = ap.parse_args()
     cfg = dict(CONFIGS["synthetic_1m"], V=a.V, per_snap=a.triples, encoder=a.encoder)
     dev = torch.device("cuda", 0)
     t0 = time.time()
-    snaps = snapshot_series(100, cfg["V"], cfg["R"], cfg["T"] + 1, cfg["per_snap"])
+    snaps = snapshot_series(100, cfg["V"], cfg["R"], cfg["T"] + (2 if a.streams > 1 else 1), cfg["per_snap"])
     print("generated %d snapshots in %.1f s" % (len(snaps), time.time() - t0), flush=True)
     for budget in [int(b) for b in a.budgets.split(",")]:
         run(a, cfg, snaps, dev, budget)
@@ -40,6 +42,8 @@ def main():
 def run(a, cfg, snaps, dev, budget):
     t0 = time.time()
     glist = [G.build_sub_graph(cfg["V"], cfg["R"], s, True, dev, tile_budget=budget or None) for s in snaps[:cfg["T"]]]
+    if a.streams > 1:
+        return run_streams(a, cfg, snaps, dev, glist)
     torch.cuda.synchronize()
     print("built in %.2f s (budget %s)" % (time.time() - t0, budget or "default"), flush=True)
     for g in glist:
@@ -77,6 +81,47 @@ def run(a, cfg, snaps, dev, budget):
         for name, x, y in (("score", p[1], l[1]), ("score_rel", p[2], l[2])):
             print("%s equal=%s max|d|=%.3g finite=%s" % (name, bool(torch.equal(x, y)), float((x - y).abs().max()),
                                                         bool(torch.isfinite(x).all())), flush=True)
+
+
+def run_streams(a, cfg, snaps, dev, glist):
+    """Independent predicts on a.streams streams (windows: the first T snapshots and the next
+    T, alternating): the memory-bound aggregations of one overlap the MFMA-bound decoder and
+    the fused layers of another."""
+    T, R = cfg["T"], cfg["R"]
+    g2 = [G.build_sub_graph(cfg["V"], R, s, True, dev) for s in snaps[1:T + 1]]
+    wins = [glist, g2]
+    tests = [torch.from_numpy(snaps[T][:512]).to(dev), torch.from_numpy(snaps[T + 1][:512]).to(dev)]
+    model = build_model(cfg, 200, dev, seed=1234)
+    model.param_caches = False
+    model.memo_pristine = False
+    model.use_phases = False
+    streams = [torch.cuda.Stream(dev) for _ in range(a.streams)]
+    edges = 2 * sum(g.number_of_edges() for g in glist)
+    main = torch.cuda.current_stream(dev)
+
+    def run(n):
+        for k in range(n):
+            st = streams[k % len(streams)]
+            st.wait_stream(main) if k < len(streams) else None
+            with torch.cuda.stream(st):
+                model.predict(wins[k % 2], R, None, tests[k % 2], True)
+        for st in streams:
+            main.wait_stream(st)
+
+    with torch.no_grad():
+        run(2 * len(streams))
+        torch.cuda.synchronize()
+        for reps in (4 * len(streams),):
+            t0 = time.time()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            run(reps)
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / reps
+            print("streams %d: %9.3f ms per predict (wall %.3f)  %.1f M edges/s   peak mem %.1f GB"
+                  % (len(streams), ms, (time.time() - t0) / reps * 1e3, edges / ms / 1e3,
+                     torch.cuda.max_memory_allocated() / 1e9), flush=True)
 
 
 if __name__ == "__main__":
