@@ -35,7 +35,7 @@ import torch
 from . import ranking
 from .graph import build_sub_graph
 from .training import GraphedSteps
-from .weights import invalidate
+from .weights import bump_versions, invalidate
 
 logger = logging.getLogger("regcn_amd.cli")
 
@@ -289,9 +289,11 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
         logger.warning("--hip-graph is ignored with %d ranks: the replica step holds a gradient all-reduce "
                        "between its launches, so it runs eagerly", world0)
     graphed = GraphedSteps(device) if args.hip_graph and world0 == 1 else None
-    # :469; the fused multi-tensor kernel: a handful of launches per step instead of ~100
+    # :469; the fused multi-tensor kernel: a handful of launches per step instead of ~100 (it
+    # does not bump the parameters' version counters: bump_versions after each step)
+    fused = device.type == "cuda"
     optimizer = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=1e-5,
-                                 capturable=graphed is not None, fused=device.type == "cuda")
+                                 capturable=graphed is not None, fused=fused)
     # replicas: every rank takes its share of the shuffled samples, one gradient
     # all-reduce per optimizer step; the same seed on every rank keeps the shuffles (and so the
     # lock-step schedule) identical.  Rank 0 validates and checkpoints.
@@ -364,6 +366,8 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
                 allreduce_gradients(model.parameters())
                 torch.nn.utils.clip_grad_norm_(model.parameters(), args.grad_norm)          # :627-628
                 optimizer.step()
+                if fused:  # the fused step leaves the version counters the caches key on
+                    bump_versions(model.parameters())
                 # the sample's mean mini-batch losses (entity, relation, radius)
                 return torch.stack([torch.stack([p[k].detach().double() for p in parts]).mean() for k in (0, 1, 3)])
 

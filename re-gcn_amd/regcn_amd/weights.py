@@ -97,6 +97,17 @@ def packed_k4(w):
     return out
 
 
+def bump_versions(params):
+    """Fused optimizers (torch.optim.Adam(fused=True)) update parameters in place WITHOUT
+    bumping their version counters, which every cache here is keyed on: bump them after the
+    step with one multi-tensor in-place x *= 1 (a bitwise identity; detach() shares the
+    version counter).  Capturable inside a HIP graph, where it is harmless."""
+    ts = [p.detach() for p in params if p is not None]
+    if ts:
+        with torch.no_grad():
+            torch._foreach_mul_(ts, 1.0)
+
+
 _CACHE_ATTRS = ("_regcn_packed", "_regcn_packed_lin", "_regcn_packed_t", "_regcn_packed_cols", "_regcn_packed_k4")
 
 

@@ -124,12 +124,25 @@ def test_cli_training_replicas(tmp_path):
                                                    ("hyperbolic_uvrgcn", "murp", []),
                                                    ("lgcn", "roth", ["--plus-relation-specific-curvature"])])
 def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder, extra):
+    _graph_vs_eager(tmp_path, encoder, decoder, extra, epochs=3, every=100)
+
+
+def test_cli_hip_graph_validation_scores_current_weights(tmp_path):
+    """Validation after every epoch under --hip-graph scores the weights the replays produced
+    (a replay updates them without bumping their version counters; the CLI drops the
+    parameter-keyed caches first): the graphed run's validation MRRs equal the eager run's
+    within the north star's MRR tolerance (+-0.002).  Measured: equal to ~1e-4 -- with eager
+    work interleaved between replays (validation, or any allocation) the replays are no longer
+    bitwise the eager steps (~1e-5 relative on the epoch losses, independent of the values
+    written to free memory; tools/graphdbg.py), so this test is not bitwise."""
+    _graph_vs_eager(tmp_path, "lgcn", "roth", [], epochs=4, every=1)
+
+
+def _graph_vs_eager(tmp_path, encoder, decoder, extra, epochs, every):
     """--hip-graph (each sample's whole step captured after its first run and replayed:
     training.GraphedSteps) trains the same model as the eager loop: dropout off, the same
-    seeds and sample order; epoch losses bit for bit, every parameter tensor to 1e-6 in
-    relative norm (epochs 2-3 are replays; measured: bitwise equal) and the validation MRRs
-    after every epoch equal (validation under graphs must not score stale parameter-keyed
-    caches: a replay updates the weights without bumping their versions).  MuRP's relation decoder
+    seeds and sample order; epoch losses bit for bit and every parameter tensor to 1e-6 in
+    relative norm (epochs 2-3 are replays; measured: bitwise equal).  MuRP's relation decoder
     (no score scale / margin: device constants by fill kernels) and the per-relation curvature
     score replay too.  Not covered: ConvTransE (its eager runs differ in the 6th digit: MIOpen
     convolution)."""
@@ -140,13 +153,13 @@ def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder, extra)
               "--test-history-len", "3", "--relation-prediction", "--entity-prediction",
               "--checkpoint", str(tmp_path / "m.pth"), "--seed", "0", "--lr", "0.01", "--triple-batch-size", "64",
               "--dropout", "0", "--input-dropout", "0", "--hidden-dropout", "0", "--feat-dropout", "0",
-              "--n-epochs", "4", "--evaluate-every", "1"] + extra
+              "--n-epochs", str(epochs), "--evaluate-every", str(every)] + extra
     dev = torch.device("cuda", 0)
     runs = []
     adam = torch.optim.Adam
 
-    class CapturableAdam(adam):  # both runs step the same optimizer code (device step counter)
-        def __init__(self, *a, **k):
+    class CapturableAdam(adam):  # both runs step the same optimizer code (device step counter;
+        def __init__(self, *a, **k):  # fused as the CLI chooses: it bumps the version counters)
             k["capturable"] = True
             super().__init__(*a, **k)
 
@@ -166,7 +179,12 @@ def test_cli_training_hip_graph_matches_eager(tmp_path, encoder, decoder, extra)
     finally:
         torch.optim.Adam = adam
     (l0, s0, v0), (l1, s1, v1) = runs
-    assert len(v0) == 3 and v1 == v0, (v0, v1)
+    if every <= epochs:  # validation between the epochs: MRR parity, not bitwise (docstring above)
+        assert len(v0) == len(v1) == epochs - 1
+        for a, b in zip(v0, v1):
+            assert a[0] == b[0] and max(abs(x - y) for x, y in zip(a[1:], b[1:])) <= 2e-3, (v0, v1)
+        np.testing.assert_allclose(l1, l0, rtol=1e-3)
+        return
     # the step is deterministic (no atomics: the embedding gathers accumulate through
     # sort-based index_put, the HIP kernels sum in fixed orders), so the
     # replays reproduce the eager run's losses bit for bit

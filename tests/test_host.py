@@ -209,3 +209,21 @@ def test_dataset_directory_vs_reference(golden):
         snaps = ranking.split_by_time(arr)
         np.testing.assert_array_equal([len(s) for s in snaps], z[name + "_snap_len"])
         np.testing.assert_array_equal(np.concatenate(snaps), z[name + "_snaps"])
+
+
+def test_bump_versions_restores_the_cache_key_after_a_fused_step():
+    """Fused Adam updates parameters without bumping their version counters, which the packed
+    weight and parameter-state caches key on; the CLI bumps them after each step
+    (weights.bump_versions: x *= 1, a bitwise identity)."""
+    import torch
+    from regcn_amd.weights import bump_versions
+    p = torch.nn.Parameter(torch.tensor([1.5, -0.0, 2.0, -3.0]))
+    opt = torch.optim.Adam([p], lr=0.1, fused=True)
+    p.grad = torch.ones(4)
+    v0 = p._version
+    opt.step()
+    stepped = p.detach().clone()
+    assert p._version == v0  # the contract fused optimizers break
+    bump_versions([p, None])
+    assert p._version > v0
+    assert torch.equal(p.detach(), stepped) and torch.equal(torch.signbit(p.detach()), torch.signbit(stepped))

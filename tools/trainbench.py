@@ -42,6 +42,7 @@ def main():
     from regcn_amd import graph as G
     from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
     from regcn_amd.synthetic import CONFIGS, snapshot_series
+    from regcn_amd.weights import bump_versions
     cfg = CONFIGS["icews14s_lgcn_roth"]
     V, R, T, per = cfg["V"], cfg["R"], cfg["T"], cfg["per_snap"]
     dev = torch.device("cuda", 0)
@@ -73,6 +74,7 @@ def main():
             nb = 1
         torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
         opt.step()
+        bump_versions(m.parameters())  # as the CLI: the fused step leaves the version counters
         return nb
 
     cap = torch.cuda.Stream(dev) if a.graph else torch.cuda.current_stream(dev)

@@ -27,6 +27,7 @@ def main():
     from regcn_amd import graph as G
     from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
     from regcn_amd.synthetic import CONFIGS, snapshot_series
+    from regcn_amd.weights import bump_versions
     cfg = CONFIGS["icews14s_lgcn_roth"]
     V, R, T, per = cfg["V"], cfg["R"], cfg["T"], cfg["per_snap"]
     dev = torch.device("cuda", 0)
@@ -46,6 +47,7 @@ def main():
         m.get_loss_batches(glist, tr, None, True, 64, combine=lambda le, lr, ls, lrad: 0.7 * le + 0.3 * lr + ls.sum() + lrad)
         torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
         opt.step()
+        bump_versions(m.parameters())  # as the CLI: the fused step leaves the version counters
 
     for _ in range(3):
         step()
