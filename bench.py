@@ -352,8 +352,8 @@ def aggregation_at_scale(device):
     out = {"bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS}
     for tag, uniform, pmc_file in (("zipf_src", False, "pmc_traffic_agg.json"),
                                    ("uniform_src", True, "pmc_traffic_agg_uniform.json")):
-        res = measure(dev=device, which=("union_aggregate", "lorentz_aggregate"), log=lambda m: None,
-                      uniform_s=uniform)
+        res = measure(dev=device, which=("union_aggregate", "union_aggregate_src_runs", "lorentz_aggregate"),
+                      log=lambda m: None, uniform_s=uniform)
         try:  # HBM bytes per launch from the committed PMC passes of tools/aggbench.py
             with open(os.path.join(REPO, "profiles", pmc_file)) as fh:
                 pmc = json.load(fh)["kernels"]
@@ -362,11 +362,19 @@ def aggregation_at_scale(device):
         sub = {"config": "synthetic |V|=%d |E|=%d R2=%d d=%d, %s" % (res["V"], res["E"], res["R2"], res["d"],
                                                                    res["sources"]),
                "bytes_per_launch": res["b_agg_bytes"]}
-        for k, kern in (("union_aggregate", "k_union_runs<false>"), ("lorentz_aggregate", "k_lorentz_sum<2>")):
+        for k, kern in (("union_aggregate", "k_union_runs<false, false>"),
+                        ("union_aggregate_src_runs", "k_union_runs<false, true>"),
+                        ("lorentz_aggregate", "k_lorentz_sum<2>")):
             tr = pmc.get(kern, {}).get("hbm_bytes")
             e = {"achieved": res[k]["algorithmic_GBps"], "frac": res[k]["hbm_frac"],
                  "avg_launch_us": round(res[k]["ms"] * 1e3, 1), "G_edges_per_s": res[k]["edges_per_s_G"],
                  "kernel": kern, "traffic": tr}
+            if k == "union_aggregate_src_runs":  # its own algorithm's bytes: one row per distinct (row, source)
+                b = res["b_agg_src_runs_bytes"]
+                e["bytes_per_launch"] = b
+                e["distinct_row_sources"] = res["distinct_row_sources"]
+                e["achieved"] = round(b / (res[k]["ms"] * 1e-3) / 1e9, 1)
+                e["frac"] = round(e["achieved"] / HBM_PEAK_GBS, 4)
             if tr:
                 e["traffic_GBps"] = round(tr / (res[k]["ms"] * 1e-3) / 1e9, 1)
                 e["traffic_frac"] = round(e["traffic_GBps"] / HBM_PEAK_GBS, 4)
@@ -654,7 +662,8 @@ def run_small(args, cfg, world, rank, device, backend, extras=True):
 
 # --------------------------------------------------------------------------- config 5
 SCALE_KERNEL = {  # library call -> its main kernel (rocprof / PMC name)
-    "regcn_union_aggregate_f32": "k_union_runs<false>",
+    "regcn_union_aggregate_f32": "k_union_runs<false, false>",
+    "regcn_union_aggregate_src_runs_f32": "k_union_runs<false, true>",
     "regcn_segment_mean_f32": "k_gather_sum<1>",
     "regcn_layer_f32": "k_layer<0, 1, false>",
     "regcn_layer_f32(step)": "k_layer<0, 1, true>",
@@ -668,6 +677,26 @@ SCALE_KERNEL = {  # library call -> its main kernel (rocprof / PMC name)
     "regcn_relation_gru_pre_f32": "k_rel_gru_pre",
     "regcn_init_entities_f32": "k_init_entities",
 }
+
+
+def heavy_distinct_sources(g):
+    """Distinct (row, source) pairs over the hub rows (the pre-aggregated rows): the source
+    rows regcn_union_aggregate_src_runs_f32 gathers."""
+    wk = g.work()
+    hc = wk["heavy_chunks"]
+    if not hc.numel():
+        return 0
+    ss = g.row_src_cols()
+    rp = wk["rowptr"].long()
+    E, V = ss.numel(), rp.numel() - 1
+    head = torch.ones(E, dtype=torch.bool, device=ss.device)
+    head[1:] = ss[1:] != ss[:-1]
+    starts = rp[:-1]
+    head[starts[starts < E]] = True
+    mark = torch.zeros(V, dtype=torch.bool, device=ss.device)
+    mark[hc[:, 0].long()] = True
+    dst = torch.repeat_interleave(torch.arange(V, device=ss.device), rp[1:] - rp[:-1])
+    return int((head & mark[dst]).sum())
 
 
 def scale_work(model, glist, B):
@@ -685,12 +714,16 @@ def scale_work(model, glist, B):
         hc = wk["heavy_chunks"]
         e_heavy = int((hc[:, 2] - hc[:, 1]).sum()) if hc.numel() else 0
         st.append(dict(n_pos=g.n_pos, items=int(wk["item_src"].numel()), e_heavy=e_heavy, n_heavy=g.n_heavy,
-                       pairs=int(wk["rel_idx"].numel()) // 2))
+                       pairs=int(wk["rel_idx"].numel()) // 2, heavy_sources=heavy_distinct_sources(g)))
     m = {k: float(np.mean([x[k] for x in st])) for k in st[0]}
     per_edge = row + 12.0  # source row + col_src + col_type + radius[src]
     io_layer = V * (row + 4) + V * (2 * row + 4) + V * 4.0  # x, r in; h, x', r' out; norm
     w = {
         "regcn_union_aggregate_f32": (0.0, m["e_heavy"] * per_edge + m["n_heavy"] * (row + 12)),
+        # source runs: one gathered row per distinct (row, source); per edge (src, type) and
+        # radius[src] in type order, src and radius[src] in source order
+        "regcn_union_aggregate_src_runs_f32": (0.0, m["heavy_sources"] * row + m["e_heavy"] * 20.0
+                                               + m["n_heavy"] * (row + 12)),
         "regcn_segment_mean_f32": (0.0, m["pairs"] * (row + 4) + R2 * row),
         "regcn_layer_f32": (gemm * (m["n_pos"] + V), m["items"] * per_edge + m["n_heavy"] * row + io_layer),
         "regcn_layer_f32(step)": (gemm * (m["n_pos"] + 2 * V),

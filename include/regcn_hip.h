@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 6
+#define REGCN_ABI_VERSION 7
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -89,6 +89,20 @@ int regcn_union_aggregate_f32(const float* x, const float* radius, const float* 
                               const int32_t* col_type, const float* norm, const int32_t* chunks, int32_t n_chunks,
                               const int32_t* fixups, int32_t n_fix, float gamma, int32_t d, float* partial,
                               int32_t partial_stride, float* out, void* stream);
+/* The union (euclid = 0) or Euclidean (euclid = 1: w_e = 1, x = raw h, radius unused)
+ * aggregation over the same chunks with the source half summed over source runs:
+ * col_src / col_type in row/type order (regcn_snapshot_row_type_order_i32) carry the
+ * relation half, col_src_by_src (regcn_snapshot_row_src_order_i32) the source half, where
+ * a row's k in-edges from one source cost one gathered row, k * w_e * x[src] (w_e depends
+ * on the source and the row only).  Same sums as regcn_union_aggregate_f32 within fp32
+ * rounding (the DGL message sum of hyperbolic_layers.py:222-240 / rgcn/layers.py:257-279
+ * regrouped by linearity). */
+int regcn_union_aggregate_src_runs_f32(const float* x, const float* radius, const float* rel,
+                                       const int32_t* col_src, const int32_t* col_type,
+                                       const int32_t* col_src_by_src, const float* norm, const int32_t* chunks,
+                                       int32_t n_chunks, const int32_t* fixups, int32_t n_fix, float gamma,
+                                       int32_t euclid, int32_t d, float* partial, int32_t partial_stride,
+                                       float* out, void* stream);
 /* Euclidean UnionRGCNLayer aggregation (rgcn/layers.py:257-279): w_e = 1, x = raw h. */
 int regcn_euclid_aggregate_f32(const float* h, const float* rel, const int32_t* col_src, const int32_t* col_type,
                                const float* norm, const int32_t* chunks, int32_t n_chunks, const int32_t* fixups,
@@ -633,6 +647,12 @@ size_t regcn_row_type_order_workspace_bytes(int32_t E, int32_t V, int32_t R2);
 int regcn_snapshot_row_type_order_i32(int32_t V, int32_t E, int32_t R2, const int32_t* rowptr,
                                       const int32_t* col_src, const int32_t* col_type, int32_t* out_src,
                                       int32_t* out_type, void* workspace, size_t ws_bytes, void* stream);
+/* The CSR edges' sources with each destination row's edges in ascending source order
+ * (out_src [E]; same rows and row pointer as the CSR): a row's duplicate sources are
+ * adjacent for regcn_union_aggregate_src_runs_f32. */
+size_t regcn_row_src_order_workspace_bytes(int32_t E, int32_t V);
+int regcn_snapshot_row_src_order_i32(int32_t V, int32_t E, const int32_t* rowptr, const int32_t* col_src,
+                                     int32_t* out_src, void* workspace, size_t ws_bytes, void* stream);
 size_t regcn_snapshot_workspace_bytes(int64_t T, int32_t V, int32_t R);
 int64_t regcn_snapshot_capacity(int32_t what, int64_t T, int32_t V, int32_t R, int32_t chunk_edges);
 int regcn_snapshot_csr_i32(const regcn_snapshot_desc* desc, void* stream);

@@ -58,6 +58,39 @@ __global__ __launch_bounds__(256) void k_gather_sum(
   }
 }
 
+// One 64-edge batch of a chunk in source order (lane = edge, my_s its source): a head lane
+// starts a run of equal sources (cut at the batch end); its row is gathered once with weight
+// count * w.  8 distinct rows in flight; a short last group repeats its first row with weight 0.
+template <bool EUCLID>
+__device__ __forceinline__ void src_runs_batch(const float* __restrict__ x, const float* __restrict__ radius,
+                                               int my_s, float r_dst, float gamma, int d, uint32_t off, int lane,
+                                               int n, uint64_t upto, f4& acc) {
+  const float my_w = EUCLID ? 1.f : expf(-gamma * fabsf(radius[my_s] - r_dst));
+  const int prev_s = __shfl_up(my_s, 1);
+  const uint64_t hm = __ballot(lane < n && (lane == 0 || my_s != prev_s));
+  const uint64_t after = hm & ~upto;
+  const int nxt = after ? __builtin_ctzll(after) : n;
+  const float wc = my_w * (float)(nxt - lane);  // count * w on a head lane
+  uint64_t m = hm;
+  while (m) {
+    const int h0 = __builtin_ctzll(m);
+    int hs[8];
+    float wv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool ok = m != 0;
+      hs[u] = ok ? __builtin_ctzll(m) : h0;
+      wv[u] = ok ? rlf(wc, hs[u]) : 0.f;
+      if (ok) m &= m - 1;
+    }
+    f4 xs[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xs[u] = row_load4(x + (int64_t)rl(my_s, hs[u]) * d, off);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += wv[u] * xs[u];
+  }
+}
+
 // UNION / EUCLID with relation-type runs.  By linearity
 //   sum_e w_e (x[src_e] + rel[t_e]) = sum_e w_e x[src_e] + sum_runs (sum_{e in run} w_e) rel[t_run]
 // over the maximal runs of equal type in the chunk's edge order.  A hub row's edges in
@@ -68,12 +101,20 @@ __global__ __launch_bounds__(256) void k_gather_sum(
 // Per 64-edge batch, lane = edge: run heads by ballot, a segmented lane scan of the
 // weights, then each closed run's relation row once; the batch's last run stays open
 // into the next batch.  Deterministic (fixed lane and run order, no atomics).
-template <bool EUCLID>
+//
+// SRC_RUNS (col_src_s = the same rows' edges in source order, graph.row_src_cols): the
+// source half runs over source runs instead.  w_e depends on (src, dst) only, so a row's
+// duplicate sources (the same neighbour under several relations, or a repeated triple) sum
+// to count * w * x[src]: one gathered row per distinct source of the batch.  The type
+// pass then reads only (col_src, col_type) and radius[src] per edge (12 B, no rows).  Both
+// orders permute each row's CSR span, so a chunk [beg, end) covers a different edge subset
+// in each, and the row's chunks together still cover every edge exactly once per half.
+template <bool EUCLID, bool SRC_RUNS>
 __global__ __launch_bounds__(256) void k_union_runs(
     const float* __restrict__ x, const float* __restrict__ radius, const float* __restrict__ rel,
-    const int* __restrict__ col_src, const int* __restrict__ col_type, const float* __restrict__ rowscale,
-    const Chunk* __restrict__ chunks, int n_chunks, float gamma, int d, float* __restrict__ partial,
-    int pstride, float* __restrict__ out) {
+    const int* __restrict__ col_src, const int* __restrict__ col_type, const int* __restrict__ col_src_s,
+    const float* __restrict__ rowscale, const Chunk* __restrict__ chunks, int n_chunks, float gamma, int d,
+    float* __restrict__ partial, int pstride, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int col = lane * 4;
   // clamped column: lanes past d re-read the row's last quad (same cache lines, never
@@ -92,9 +133,13 @@ __global__ __launch_bounds__(256) void k_union_runs(
       const int ei = e0 + min(lane, n - 1);
       const int my_s = col_src[ei];
       const int my_t = col_type[ei];
+      // SRC_RUNS: the same batch positions in source order, loaded together with the type
+      // order's indices so both passes' index -> radius round trips overlap
+      const int my_ss = SRC_RUNS ? col_src_s[ei] : 0;
       const float my_w = EUCLID ? 1.f : expf(-gamma * fabsf(radius[my_s] - r_dst));
-      // gathered source rows
-      int j = 0;
+      if constexpr (SRC_RUNS) src_runs_batch<EUCLID>(x, radius, my_ss, r_dst, gamma, d, off, lane, n, upto, acc);
+      // gathered source rows (SRC_RUNS: src_runs_batch above)
+      int j = SRC_RUNS ? n : 0;
       for (; j + 8 <= n; j += 8) {
         f4 xs[8];
 #pragma unroll
@@ -389,22 +434,29 @@ static inline unsigned grid_for(int n_items) {
 int gather_sum(int mode, const float* x, const float* radius, const float* rel, const int* col_src,
                const int* col_type, const float* rowscale, const void* chunks, int n_chunks,
                const void* fixups, int n_fix, float gamma, int d, float* partial, int pstride, float* out,
-               hipStream_t st) {
+               hipStream_t st, const int* col_src_s) {
   if (d <= 0 || d > 256 || (d & 3)) return set_error(REGCN_EINVAL, "aggregation needs d %% 4 == 0 and d <= 256 (d=%d)", d);
   if (!x || !col_src || !rowscale || !out) return set_error(REGCN_EINVAL, "null pointer");
   if (mode != AGG_MEAN && (!col_type || !rel)) return set_error(REGCN_EINVAL, "null pointer");
+  if (col_src_s && mode == AGG_MEAN) return set_error(REGCN_EINVAL, "source runs apply to the union aggregations only");
   if (mode == AGG_UNION && !radius) return set_error(REGCN_EINVAL, "union aggregation needs radius");
   if (n_fix > 0 && !partial) return set_error(REGCN_EINVAL, "partial workspace required");
   const Chunk* ch = (const Chunk*)chunks;
   const Fixup* fx = (const Fixup*)fixups;
   if (n_chunks > 0) {
     dim3 g(grid_for(n_chunks)), b(256);
-    if (mode == AGG_UNION)
-      hipLaunchKernelGGL(k_union_runs<false>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,
-                         n_chunks, gamma, d, partial, pstride, out);
+    if (mode == AGG_UNION && col_src_s)
+      hipLaunchKernelGGL((k_union_runs<false, true>), g, b, 0, st, x, radius, rel, col_src, col_type, col_src_s,
+                         rowscale, ch, n_chunks, gamma, d, partial, pstride, out);
+    else if (mode == AGG_UNION)
+      hipLaunchKernelGGL((k_union_runs<false, false>), g, b, 0, st, x, radius, rel, col_src, col_type, nullptr,
+                         rowscale, ch, n_chunks, gamma, d, partial, pstride, out);
+    else if (mode == AGG_EUCLID && col_src_s)
+      hipLaunchKernelGGL((k_union_runs<true, true>), g, b, 0, st, x, radius, rel, col_src, col_type, col_src_s,
+                         rowscale, ch, n_chunks, gamma, d, partial, pstride, out);
     else if (mode == AGG_EUCLID)
-      hipLaunchKernelGGL(k_union_runs<true>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,
-                         n_chunks, gamma, d, partial, pstride, out);
+      hipLaunchKernelGGL((k_union_runs<true, false>), g, b, 0, st, x, radius, rel, col_src, col_type, nullptr,
+                         rowscale, ch, n_chunks, gamma, d, partial, pstride, out);
     else if (mode == AGG_MEAN)
       hipLaunchKernelGGL(k_gather_sum<AGG_MEAN>, g, b, 0, st, x, radius, rel, col_src, col_type, rowscale, ch,
                          n_chunks, gamma, d, partial, pstride, out);

@@ -84,6 +84,15 @@ int regcn_union_aggregate_f32(const float* x, const float* radius, const float* 
   return gather_sum(0, x, radius, rel, col_src, col_type, norm, chunks, n_chunks, fixups, n_fix, gamma, d, partial,
                     partial_stride, out, ST(s));
 }
+int regcn_union_aggregate_src_runs_f32(const float* x, const float* radius, const float* rel, const int32_t* col_src,
+                                       const int32_t* col_type, const int32_t* col_src_by_src, const float* norm,
+                                       const int32_t* chunks, int32_t n_chunks, const int32_t* fixups, int32_t n_fix,
+                                       float gamma, int32_t euclid, int32_t d, float* partial, int32_t partial_stride,
+                                       float* out, void* s) {
+  if (!col_src_by_src && n_chunks > 0) return set_error(REGCN_EINVAL, "null source-order column");
+  return gather_sum(euclid ? 2 : 0, x, radius, rel, col_src, col_type, norm, chunks, n_chunks, fixups, n_fix, gamma, d,
+                    partial, partial_stride, out, ST(s), col_src_by_src);
+}
 int regcn_euclid_aggregate_f32(const float* h, const float* rel, const int32_t* col_src, const int32_t* col_type,
                                const float* norm, const int32_t* chunks, int32_t n_chunks, const int32_t* fixups,
                                int32_t n_fix, int32_t d, float* partial, int32_t partial_stride, float* out,
@@ -643,6 +652,11 @@ int regcn_lorentz_aggregate_bwd_f32(const regcn_edge_bwd_desc* desc, int32_t num
 }
 size_t regcn_transpose_workspace_bytes(int32_t E, int32_t V, int32_t R2) { return transpose_ws_bytes(E, V, R2); }
 int regcn_snapshot_transpose_i32(const regcn_transpose_desc* desc, void* s) { return snapshot_transpose(desc, ST(s)); }
+size_t regcn_row_src_order_workspace_bytes(int32_t E, int32_t V) { return row_src_ws_bytes(E, V); }
+int regcn_snapshot_row_src_order_i32(int32_t V, int32_t E, const int32_t* rowptr, const int32_t* col_src, int32_t* out_src,
+                                     void* workspace, size_t ws_bytes, void* s) {
+  return row_src_order(V, E, rowptr, col_src, out_src, workspace, ws_bytes, ST(s));
+}
 size_t regcn_row_type_order_workspace_bytes(int32_t E, int32_t V, int32_t R2) { return row_type_ws_bytes(E, V, R2); }
 int regcn_snapshot_row_type_order_i32(int32_t V, int32_t E, int32_t R2, const int32_t* rowptr, const int32_t* col_src,
                                       const int32_t* col_type, int32_t* out_src, int32_t* out_type, void* workspace,

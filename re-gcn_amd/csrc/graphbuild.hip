@@ -921,6 +921,45 @@ int row_type_order(int V, int E, int R2, const int* rowptr, const int* col_src, 
   return check_launch("k_permute2");
 }
 
+// ----------------------------------------------------------------- row / source edge order
+namespace {
+__global__ __launch_bounds__(BT) void k_permute1(const uint32_t* __restrict__ perm, int n, const int* __restrict__ a,
+                                                 int* __restrict__ oa) {
+  const int i = blockIdx.x * BT + threadIdx.x;
+  if (i < n) oa[i] = a[perm[i]];
+}
+}  // namespace
+
+size_t row_src_ws_bytes(int E, int V) { return row_type_ws_bytes(E, V, 2); }
+
+// Stable LSD radix sort by source, then stably by destination row: each row's sources in
+// ascending order, so a row's duplicate sources are adjacent (k_union_runs<., true>).
+int row_src_order(int V, int E, const int* rowptr, const int* col_src, int* out_src, void* workspace, size_t ws_bytes,
+                  hipStream_t st) {
+  if (V <= 0 || E < 0) return set_error(REGCN_EINVAL, "bad row/source order sizes");
+  if (E == 0) return 0;
+  if (!rowptr || !col_src || !out_src) return set_error(REGCN_EINVAL, "null pointer");
+  if (!workspace || ws_bytes < row_src_ws_bytes(E, V)) return set_error(REGCN_EINVAL, "row/source order workspace too small");
+  const Layout L = tlayout(E, V, 2);
+  char* ws = (char*)workspace;
+  int* csr_dst = (int*)(ws + L.total);
+  int rc;
+  hipLaunchKernelGGL(k_csr_dst, dim3(std::min<unsigned>(blocks(V, 4), 65536)), dim3(BT), 0, st, rowptr, V, csr_dst);
+  if ((rc = check_launch("k_csr_dst"))) return rc;
+  hipLaunchKernelGGL(k_iota_keys, dim3(blocks(E)), dim3(BT), 0, st, col_src, E, (uint32_t*)(ws + L.k0),
+                     (uint32_t*)(ws + L.v0));
+  bool second;
+  if ((rc = radix_sort(ws, L, E, bitlen((uint64_t)V - 1), true, &second, st))) return rc;
+  hipLaunchKernelGGL(k_row_of, dim3(blocks(E)), dim3(BT), 0, st, csr_dst,
+                     (const uint32_t*)(ws + (second ? L.v1 : L.v0)), E, (uint32_t*)(ws + L.k0),
+                     (uint32_t*)(ws + L.v0));
+  if ((rc = check_launch("k_row_of"))) return rc;
+  if ((rc = radix_sort(ws, L, E, bitlen((uint64_t)V - 1), true, &second, st))) return rc;
+  hipLaunchKernelGGL(k_permute1, dim3(blocks(E)), dim3(BT), 0, st, (const uint32_t*)(ws + (second ? L.v1 : L.v0)), E,
+                     col_src, out_src);
+  return check_launch("k_permute1");
+}
+
 int64_t snapshot_capacity(int what, int64_t T, int V, int R, int C) {
   const int64_t E = 2 * T, EC = E / std::max(C, 1) + 1, R2 = 2 * (int64_t)R;
   switch (what) {

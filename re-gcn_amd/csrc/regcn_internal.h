@@ -34,7 +34,7 @@ int rowmap(int op, const float* a, const float* b, const float* vec, int64_t row
 int gather_sum(int mode, const float* x, const float* radius, const float* rel, const int* col_src,
                const int* col_type, const float* rowscale, const void* chunks, int n_chunks,
                const void* fixups, int n_fix, float gamma, int d, float* partial, int pstride, float* out,
-               hipStream_t st);
+               hipStream_t st, const int* col_src_s = nullptr);
 int partial_sum(float* partial, int pstride, const void* fixups, int n_fix, int width, float* out, int ostride,
                 hipStream_t st);
 int lorentz_sum(const float* x, const float* rel, const float* W, const int* col_src, const int* col_type,
@@ -55,6 +55,9 @@ size_t transpose_ws_bytes(int E, int V, int R2);
 size_t row_type_ws_bytes(int E, int V, int R2);
 int row_type_order(int V, int E, int R2, const int* rowptr, const int* col_src, const int* col_type, int* out_src,
                    int* out_type, void* ws, size_t ws_bytes, hipStream_t st);
+size_t row_src_ws_bytes(int E, int V);
+int row_src_order(int V, int E, const int* rowptr, const int* col_src, int* out_src, void* ws, size_t ws_bytes,
+                  hipStream_t st);
 int snapshot_csr(const regcn_snapshot_desc* d, hipStream_t st);
 int snapshot_work(const regcn_snapshot_desc* d, hipStream_t st);
 size_t snapshot_ws_bytes(int64_t T, int V, int R);

@@ -14,8 +14,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libregcn_hip.so")
-ABI_VERSION = 6
+LIB_PATH = os.environ.get("REGCN_HIP_LIB") or os.path.join(_HERE, "libregcn_hip.so")  # override: A/B builds
+ABI_VERSION = 7
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -39,6 +39,8 @@ _SIGS = {
     "regcn_init_entities_f32": [P, P, _c_i64, _c_int, _c_f, _c_int, P, P, P, P],
     "regcn_union_aggregate_f32": [P, P, P, P, P, P, P, _c_int, P, _c_int, _c_f, _c_int, P, _c_int, P, P],
     "regcn_euclid_aggregate_f32": [P, P, P, P, P, P, _c_int, P, _c_int, _c_int, P, _c_int, P, P],
+    "regcn_union_aggregate_src_runs_f32": [P, P, P, P, P, P, P, P, _c_int, P, _c_int, _c_f, _c_int, _c_int, P, _c_int,
+                                           P, P],
     "regcn_segment_mean_f32": [P, P, P, P, _c_int, P, _c_int, _c_int, P, _c_int, P, P],
     "regcn_lorentz_aggregate_f32": [P, P, P, P, P, P, _c_int, P, _c_int, _c_int, _c_f, _c_int, P, _c_int, P, P],
     "regcn_packed_weight_floats": [_c_int],
@@ -80,6 +82,8 @@ _SIGS = {
     "regcn_snapshot_transpose_i32": [P, P],
     "regcn_row_type_order_workspace_bytes": [_c_int, _c_int, _c_int],
     "regcn_snapshot_row_type_order_i32": [_c_int, _c_int, _c_int, P, P, P, P, P, P, _c_sz, P],
+    "regcn_row_src_order_workspace_bytes": [_c_int, _c_int],
+    "regcn_snapshot_row_src_order_i32": [_c_int, _c_int, P, P, P, P, _c_sz, P],
     "regcn_rowmap_bwd_f32": [_c_int, P, P, P, _c_i64, _c_int, _c_f, P, P, P],
     "regcn_union_aggregate_bwd_f32": [P, _c_f, P],
     "regcn_lorentz_sum_raw_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, P, P, P],
@@ -92,6 +96,7 @@ SCORE_DIST, SCORE_RAW_SCALE = 1, 2
 _RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz,
             "regcn_snapshot_workspace_bytes": _c_sz, "regcn_kreduce_workspace_floats": _c_sz, "regcn_snapshot_capacity": _c_i64,
             "regcn_transpose_workspace_bytes": _c_sz, "regcn_row_type_order_workspace_bytes": _c_sz,
+            "regcn_row_src_order_workspace_bytes": _c_sz,
             "regcn_packed_weight_floats": _c_sz, "regcn_packed_linear_floats": _c_sz,
             "regcn_packed_k4_floats": _c_sz}
 

@@ -287,6 +287,28 @@ class SnapshotGraph:
         self.__dict__["_row_type"] = t
         return t
 
+    def row_src_cols(self):
+        """col_src with each destination row's edges in ascending source order
+        (regcn_snapshot_row_src_order_i32), built on first use and cached: the source half of
+        the union hub-row aggregation gathers a row's duplicate sources once."""
+        t = self.__dict__.get("_row_src")
+        if t is not None:
+            return t
+        from . import _lib
+        wk = self.work()
+        dev = wk["rowptr"].device
+        V, E = self.num_nodes_, int(wk["col_src"].shape[0])
+        if E == 0:
+            t = wk["col_src"]
+        else:
+            ws = torch.empty(int(_lib.lib().regcn_row_src_order_workspace_bytes(E, V)), dtype=torch.uint8, device=dev)
+            t = torch.empty(E, dtype=torch.int32, device=dev)
+            _lib.call("regcn_snapshot_row_src_order_i32", V, E, _lib.iptr(wk["rowptr"]), _lib.iptr(wk["col_src"]),
+                      _lib.iptr(t), ws.data_ptr(), ws.numel(), _lib.stream())
+            _lib.publish()  # cached: read next by whichever stream asks
+        self.__dict__["_row_src"] = t
+        return t
+
     def work(self):
         """Device work lists (raises on a CPU graph: the HIP path has no CPU fallback)."""
         if self.dev is None:

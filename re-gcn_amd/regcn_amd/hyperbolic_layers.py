@@ -61,15 +61,13 @@ def _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c):
         cs, ct = g.row_type_cols()
         _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(cs), i(ct), i(hc),
                   hc.shape[0], i(hf), hf.shape[0], nb, float(c), d, f(part), stride, f(agg), _lib.stream())
-    elif mode == _lib.AGG_UNION:  # type order too: one relation-row read per same-type run
+    else:  # union / Euclid: relation half over type runs, source half over source runs
         cs, ct = g.row_type_cols()
-        _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(cs), i(ct),
-                  f(wk["norm"]), i(hc), hc.shape[0], i(hf), hf.shape[0], float(gamma), d, f(part), stride, f(agg),
-                  _lib.stream())
-    else:
-        cs, ct = g.row_type_cols()
-        _lib.call("regcn_euclid_aggregate_f32", f(x), f(rel), i(cs), i(ct), f(wk["norm"]),
-                  i(hc), hc.shape[0], i(hf), hf.shape[0], d, f(part), stride, f(agg), _lib.stream())
+        ss = g.row_src_cols()
+        euclid = mode != _lib.AGG_UNION
+        _lib.call("regcn_union_aggregate_src_runs_f32", f(x), None if euclid else f(r), f(rel), i(cs), i(ct), i(ss),
+                  f(wk["norm"]), i(hc), hc.shape[0], i(hf), hf.shape[0], float(gamma), int(euclid), d, f(part), stride,
+                  f(agg), _lib.stream())
     return agg
 
 

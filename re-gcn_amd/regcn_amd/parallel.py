@@ -94,6 +94,9 @@ class OwnerView:
     def row_type_cols(self):
         return self.g.row_type_cols()
 
+    def row_src_cols(self):
+        return self.g.row_src_cols()
+
     def work(self):
         if self._dev is None:
             wk = dict(self.g.work())

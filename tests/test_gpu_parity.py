@@ -362,6 +362,56 @@ def _zipf_snapshot(V, R, T, seed):
     return np.stack([perm[rng.choice(V, T, p=p)], rng.integers(0, R, T), perm[rng.choice(V, T, p=p)]], 1)
 
 
+@pytest.mark.parametrize("chunk", [2, 64, 4096])
+@pytest.mark.parametrize("euclid", [False, True])
+def test_union_source_runs_match_edge_sums(euclid, chunk):
+    """regcn_union_aggregate_src_runs_f32 (a hub row's duplicate sources gathered once:
+    count * w * x[src]) against regcn_union_aggregate_f32 over the CSR edge order on the same
+    hub chunks.  The snapshot repeats triples (one source 300 times into a hub under many
+    relations), so source runs cross 64-edge batches and chunk ends.  Also pins the
+    row/source order: each row's CSR span sorted by source."""
+    from regcn_amd import _lib
+    from regcn_amd import graph as G
+    V, R, d, gamma = 3000, 60, 200, 0.15
+    rng = np.random.default_rng(11)
+    tr = _zipf_snapshot(V, R, 20000, 5)
+    hub = int(np.bincount(tr[:, 2], minlength=V).argmax())
+    rep = np.stack([np.full(300, 17), rng.integers(0, R, 300), np.full(300, hub)], 1)
+    tr = np.concatenate([tr, rep, tr[:2000]])
+    g = G.build_sub_graph(V, R, tr, True, DEV, chunk_edges=chunk, tile_budget=64)
+    assert g.n_heavy > 0
+    wk = g.work()
+    rowptr = wk["rowptr"].cpu().numpy()
+    cs = wk["col_src"].cpu().numpy()
+    csr_dst = np.repeat(np.arange(V), np.diff(rowptr))
+    ss = g.row_src_cols()
+    np.testing.assert_array_equal(ss.cpu().numpy(), cs[np.lexsort((cs, csr_dst))])
+    gen = torch.Generator().manual_seed(2)
+    x = (torch.randn(V, d, generator=gen) * 0.3).to(DEV)
+    r = x.norm(dim=1).contiguous()
+    rel = (torch.randn(2 * R, d, generator=gen) * 0.1).to(DEV)
+    hc, hf = wk["heavy_chunks"], wk["heavy_fixups"]
+    part = torch.empty(max(g.heavy_slots, 1), d + 4, device=DEV)
+    f, i = _lib.fptr, _lib.iptr
+    ref = torch.zeros(V, d, device=DEV)
+    got = torch.zeros(V, d, device=DEV)
+    if euclid:
+        _lib.call("regcn_euclid_aggregate_f32", f(x), f(rel), i(wk["col_src"]), i(wk["col_type"]), f(wk["norm"]),
+                  i(hc), hc.shape[0], i(hf), hf.shape[0], d, f(part), d + 4, f(ref), _lib.stream())
+    else:
+        _lib.call("regcn_union_aggregate_f32", f(x), f(r), f(rel), i(wk["col_src"]), i(wk["col_type"]),
+                  f(wk["norm"]), i(hc), hc.shape[0], i(hf), hf.shape[0], gamma, d, f(part), d + 4, f(ref),
+                  _lib.stream())
+    ct_s, ct_t = g.row_type_cols()
+    _lib.call("regcn_union_aggregate_src_runs_f32", f(x), None if euclid else f(r), f(rel), i(ct_s), i(ct_t), i(ss),
+              f(wk["norm"]), i(hc), hc.shape[0], i(hf), hf.shape[0], gamma, int(euclid), d, f(part), d + 4, f(got),
+              _lib.stream())
+    torch.cuda.synchronize()
+    heavy = torch.from_numpy(np.unique(hc.cpu().numpy()[:, 0])).long().to(DEV)
+    assert got[heavy].abs().max() > 0
+    assert_close(got, ref, what="source-run union aggregation")
+
+
 @pytest.mark.parametrize("chunk", [None, 2])
 @pytest.mark.parametrize("kind", ["union", "lorentz", "euclid"])
 def test_layers_with_hubs_vs_oracle(kind, chunk):

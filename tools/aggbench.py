@@ -18,6 +18,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -75,6 +76,13 @@ def measure(V=1_000_000, R=256, triples=25_000_000, d=200, reps=3, dev=None,
                   f(wk["norm"]), i(ch), ch.shape[0], i(fx), fx.shape[0], 0.15, d, f(part), stride, f(out),
                   _lib.stream())
 
+    ss = g.row_src_cols()  # the source half's order (duplicate sources adjacent)
+
+    def union_agg_src_runs():
+        _lib.call("regcn_union_aggregate_src_runs_f32", f(x), f(r), f(rel), i(cs), i(ct), i(ss),
+                  f(wk["norm"]), i(ch), ch.shape[0], i(fx), fx.shape[0], 0.15, 0, d, f(part), stride, f(out),
+                  _lib.stream())
+
     def lorentz_agg(src=cs, typ=ct):
         _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(src), i(typ),
                   i(ch), ch.shape[0], i(fx), fx.shape[0], 100, float(C), d, f(part), stride, f(out), _lib.stream())
@@ -82,11 +90,22 @@ def measure(V=1_000_000, R=256, triples=25_000_000, d=200, reps=3, dev=None,
     fns = {"union_aggregate": union_agg, "union_layer": lambda: uni(g, h, rel),
            "lorentz_aggregate": lorentz_agg, "lorentz_layer": lambda: lor(g, h, rel),
            "lorentz_aggregate_csr": lambda: lorentz_agg(wk["col_src"], wk["col_type"]),  # edge-id order, for comparison
-           "union_aggregate_csr": lambda: union_agg(wk["col_src"], wk["col_type"])}
+           "union_aggregate_csr": lambda: union_agg(wk["col_src"], wk["col_type"]),
+           "union_aggregate_src_runs": union_agg_src_runs}
     st = torch.cuda.Stream(dev)
     b_agg = E * (4 * d + 12) + V * (4 * d + 12)
+    # distinct (row, source) pairs: the source half's gathered rows with source runs
+    s_np = ss.cpu().numpy()
+    rp = wk["rowptr"].cpu().numpy()
+    head = np.ones(len(s_np), bool)
+    head[1:] = s_np[1:] != s_np[:-1]
+    head[rp[:-1][rp[:-1] < len(s_np)]] = True
+    n_distinct = int(head.sum())
     res = {"V": V, "E": E, "R2": 2 * R, "d": d, "b_agg_bytes": b_agg, "hbm_peak_gbs": HBM_PEAK_GBS,
+           "distinct_row_sources": n_distinct,
+           "b_agg_src_runs_bytes": n_distinct * 4 * d + E * 24 + V * (4 * d + 12),
            "sources": "uniform subjects, Zipf objects" if uniform_s else "Zipf subjects and objects"}
+    log("distinct (row, source) pairs: %d of %d edges" % (n_distinct, E))
     with torch.no_grad():
         for name in which:
             ms = event_time(fns[name], reps, st, replays=3)
