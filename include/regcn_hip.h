@@ -263,6 +263,10 @@ typedef struct regcn_layer_desc {
   float* step_r_out;
   int64_t* trace;  /* optional: per-workgroup phase timestamps (s_memrealtime, 8 per
                       workgroup) for profiling; NULL in production */
+  int32_t item_src_runs; /* union / euclid: item_src / item_tl hold each row's items in ascending
+                            source order (regcn_snapshot_item_src_order_i32), so a row's k items
+                            from one source gather that source row once, k * w_e * x[src]
+                            (the relation rows still per item) */
 } regcn_layer_desc;
 int regcn_layer_f32(const regcn_layer_desc* desc, void* stream);
 
@@ -653,6 +657,14 @@ int regcn_snapshot_row_type_order_i32(int32_t V, int32_t E, int32_t R2, const in
 size_t regcn_row_src_order_workspace_bytes(int32_t E, int32_t V);
 int regcn_snapshot_row_src_order_i32(int32_t V, int32_t E, const int32_t* rowptr, const int32_t* col_src,
                                      int32_t* out_src, void* workspace, size_t ws_bytes, void* stream);
+/* The fused layer's inline items (tiles, item_ptr, item_src, item_tl of the snapshot's work
+ * lists) with each row's items in ascending source order (stable): out_src / out_tl
+ * [n_items], same tiles and item_ptr.  For regcn_layer_desc.item_src_runs. */
+size_t regcn_item_src_order_workspace_bytes(int32_t n_items, int32_t V);
+int regcn_snapshot_item_src_order_i32(int32_t V, int32_t n_tiles, int32_t n_items, const int32_t* tiles,
+                                      const int32_t* item_ptr, const int32_t* item_src, const int32_t* item_tl,
+                                      int32_t* out_src, int32_t* out_tl, void* workspace, size_t ws_bytes,
+                                      void* stream);
 size_t regcn_snapshot_workspace_bytes(int64_t T, int32_t V, int32_t R);
 int64_t regcn_snapshot_capacity(int32_t what, int64_t T, int32_t V, int32_t R, int32_t chunk_edges);
 int regcn_snapshot_csr_i32(const regcn_snapshot_desc* desc, void* stream);

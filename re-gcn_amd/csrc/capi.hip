@@ -400,6 +400,9 @@ int regcn_layer_f32(const regcn_layer_desc* g, void* s) {
   a.x_next = g->x_next;
   a.r_next = g->r_next;
   a.fuse_step = g->fuse_step;
+  a.item_src_runs = g->item_src_runs;
+  if (a.item_src_runs && a.agg_mode != REGCN_AGG_UNION && a.agg_mode != REGCN_AGG_EUCLID)
+    return set_error(REGCN_EINVAL, "item_src_runs applies to the union / euclid gathers only");
   if (g->fuse_step) {
     StepArgs& t = a.step;
     t.hc = nullptr;
@@ -652,6 +655,13 @@ int regcn_lorentz_aggregate_bwd_f32(const regcn_edge_bwd_desc* desc, int32_t num
 }
 size_t regcn_transpose_workspace_bytes(int32_t E, int32_t V, int32_t R2) { return transpose_ws_bytes(E, V, R2); }
 int regcn_snapshot_transpose_i32(const regcn_transpose_desc* desc, void* s) { return snapshot_transpose(desc, ST(s)); }
+size_t regcn_item_src_order_workspace_bytes(int32_t n_items, int32_t V) { return item_src_ws_bytes(n_items, V); }
+int regcn_snapshot_item_src_order_i32(int32_t V, int32_t n_tiles, int32_t n_items, const int32_t* tiles,
+                                      const int32_t* item_ptr, const int32_t* item_src, const int32_t* item_tl,
+                                      int32_t* out_src, int32_t* out_tl, void* workspace, size_t ws_bytes, void* s) {
+  return item_src_order(V, n_tiles, n_items, tiles, item_ptr, item_src, item_tl, out_src, out_tl, workspace, ws_bytes,
+                        ST(s));
+}
 size_t regcn_row_src_order_workspace_bytes(int32_t E, int32_t V) { return row_src_ws_bytes(E, V); }
 int regcn_snapshot_row_src_order_i32(int32_t V, int32_t E, const int32_t* rowptr, const int32_t* col_src, int32_t* out_src,
                                      void* workspace, size_t ws_bytes, void* s) {

@@ -25,6 +25,13 @@ __device__ __forceinline__ f4 row_load4(const float* row, uint32_t off) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
+// The same load with a wave-uniform record count: nrec = 0 makes every lane out of range, so
+// the load returns zeros without a memory request (a skipped duplicate row, branch-free).
+__device__ __forceinline__ f4 row_load4_n(const float* row, uint32_t off, int nrec) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row), (short)0, nrec, 0x00020000);
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
 __device__ __forceinline__ int rl(int v, int j) { return __builtin_amdgcn_readlane(v, j); }
 __device__ __forceinline__ float rlf(float v, int j) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));

@@ -932,6 +932,49 @@ __global__ __launch_bounds__(BT) void k_permute1(const uint32_t* __restrict__ pe
 
 size_t row_src_ws_bytes(int E, int V) { return row_type_ws_bytes(E, V, 2); }
 
+namespace {
+// per item: its row's position in rows[] (tile start + tile-local row), one wave per tile
+__global__ __launch_bounds__(BT) void k_item_rowpos(const int* __restrict__ tiles, const int* __restrict__ item_ptr,
+                                                    const int* __restrict__ item_tl, int n_tiles,
+                                                    int* __restrict__ rowpos) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * (BT / 64);
+  for (int t = blockIdx.x * (BT / 64) + (threadIdx.x >> 6); t < n_tiles; t += nw)
+    for (int i = item_ptr[t] + lane; i < item_ptr[t + 1]; i += 64) rowpos[i] = tiles[2 * t] + (item_tl[i] & 15);
+}
+}  // namespace
+
+size_t item_src_ws_bytes(int n_items, int V) { return row_type_ws_bytes(n_items, V, 2); }
+
+// Stable LSD radix sort of the items by source, then stably by row position: each row's
+// items in ascending source order (ties keep CSR order), rows and tiles unchanged.
+int item_src_order(int V, int n_tiles, int n_items, const int* tiles, const int* item_ptr, const int* item_src,
+                   const int* item_tl, int* out_src, int* out_tl, void* workspace, size_t ws_bytes, hipStream_t st) {
+  if (V <= 0 || n_tiles < 0 || n_items < 0) return set_error(REGCN_EINVAL, "bad item order sizes");
+  if (n_items == 0) return 0;
+  if (!tiles || !item_ptr || !item_src || !item_tl || !out_src || !out_tl) return set_error(REGCN_EINVAL, "null pointer");
+  if (!workspace || ws_bytes < item_src_ws_bytes(n_items, V)) return set_error(REGCN_EINVAL, "item order workspace too small");
+  const Layout L = tlayout(n_items, V, 2);
+  char* ws = (char*)workspace;
+  int* rowpos = (int*)(ws + L.total);
+  int rc;
+  hipLaunchKernelGGL(k_item_rowpos, dim3(std::min<unsigned>(blocks(n_tiles, 4), 65536)), dim3(BT), 0, st, tiles,
+                     item_ptr, item_tl, n_tiles, rowpos);
+  if ((rc = check_launch("k_item_rowpos"))) return rc;
+  hipLaunchKernelGGL(k_iota_keys, dim3(blocks(n_items)), dim3(BT), 0, st, item_src, n_items, (uint32_t*)(ws + L.k0),
+                     (uint32_t*)(ws + L.v0));
+  bool second;
+  if ((rc = radix_sort(ws, L, n_items, bitlen((uint64_t)V - 1), true, &second, st))) return rc;
+  hipLaunchKernelGGL(k_row_of, dim3(blocks(n_items)), dim3(BT), 0, st, rowpos,
+                     (const uint32_t*)(ws + (second ? L.v1 : L.v0)), n_items, (uint32_t*)(ws + L.k0),
+                     (uint32_t*)(ws + L.v0));
+  if ((rc = check_launch("k_row_of"))) return rc;
+  if ((rc = radix_sort(ws, L, n_items, bitlen((uint64_t)V - 1), true, &second, st))) return rc;
+  hipLaunchKernelGGL(k_permute2, dim3(blocks(n_items)), dim3(BT), 0, st, (const uint32_t*)(ws + (second ? L.v1 : L.v0)),
+                     n_items, item_src, item_tl, out_src, out_tl);
+  return check_launch("k_permute2");
+}
+
 // Stable LSD radix sort by source, then stably by destination row: each row's sources in
 // ascending order, so a row's duplicate sources are adjacent (k_union_runs<., true>).
 int row_src_order(int V, int E, const int* rowptr, const int* col_src, int* out_src, void* workspace, size_t ws_bytes,

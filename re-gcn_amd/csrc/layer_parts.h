@@ -227,20 +227,34 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
     // not one per edge.
     int j = 0;
     if constexpr (AGG == AGG_UNION || AGG == AGG_EUCLID) {
+      // With item_src_runs the items are in (row, source) order: a run of equal (row, source)
+      // in this window gathers the source row once, at its head, with weight count * w; the
+      // other items' x loads go through an empty buffer resource (no memory request, zero) and
+      // the relation rows stay per item.  Without it every item is its own head (count 1).
+      uint64_t hx = ~0ull;
+      float wx = my_w;
+      if (p.item_src_runs) {
+        const int ps = __shfl_up(my_s, 1), pi = __shfl_up(my_i, 1);
+        hx = __ballot(lane < n && (lane == 0 || my_s != ps || my_i != pi));
+        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+        const uint64_t after = hx & ~upto;
+        wx = my_w * (float)((after ? __builtin_ctzll(after) : n) - lane);
+      }
       for (; j < n; j += EB) {
         const int nv = n - j;
         f4 xs[EB], rv[EB];
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-          xs[u] = row4u(p.x, rl(my_s, j + u));
+          const int nrec = ((hx >> ((j + u) & 63)) & 1ull) ? 0x7FFFFFFF : 0;
+          xs[u] = row_load4_n(p.x + (int64_t)rl(my_s, j + u) * d, xoff, nrec);
           rv[u] = row4u(p.rel, rl(my_t, j + u));
         }
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
           if (u < nv) {
             take(rl(my_i, j + u));
-            if (AGG == AGG_EUCLID) acc += xs[u] + rv[u];
-            else acc += rlf(my_w, j + u) * (xs[u] + rv[u]);
+            if (AGG == AGG_EUCLID) acc += rlf(wx, j + u) * xs[u] + rv[u];
+            else acc += rlf(wx, j + u) * xs[u] + rlf(my_w, j + u) * rv[u];
           }
         }
       }

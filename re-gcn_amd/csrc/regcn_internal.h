@@ -55,6 +55,9 @@ size_t transpose_ws_bytes(int E, int V, int R2);
 size_t row_type_ws_bytes(int E, int V, int R2);
 int row_type_order(int V, int E, int R2, const int* rowptr, const int* col_src, const int* col_type, int* out_src,
                    int* out_type, void* ws, size_t ws_bytes, hipStream_t st);
+size_t item_src_ws_bytes(int n_items, int V);
+int item_src_order(int V, int n_tiles, int n_items, const int* tiles, const int* item_ptr, const int* item_src,
+                   const int* item_tl, int* out_src, int* out_tl, void* ws, size_t ws_bytes, hipStream_t st);
 size_t row_src_ws_bytes(int E, int V);
 int row_src_order(int V, int E, const int* rowptr, const int* col_src, int* out_src, void* ws, size_t ws_bytes,
                   hipStream_t st);
@@ -118,6 +121,7 @@ struct LayerArgs {
   int fuse_step;            // run the timestep on the layer output (step.hc unused)
   StepArgs step;
   int64_t* trace;           // debug: 8 phase timestamps per workgroup, or null
+  int item_src_runs;        // union / euclid items in (row, source) order: one x row per source run
 };
 
 struct ScoreArgs {

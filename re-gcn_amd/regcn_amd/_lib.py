@@ -83,6 +83,8 @@ _SIGS = {
     "regcn_row_type_order_workspace_bytes": [_c_int, _c_int, _c_int],
     "regcn_snapshot_row_type_order_i32": [_c_int, _c_int, _c_int, P, P, P, P, P, P, _c_sz, P],
     "regcn_row_src_order_workspace_bytes": [_c_int, _c_int],
+    "regcn_item_src_order_workspace_bytes": [_c_int, _c_int],
+    "regcn_snapshot_item_src_order_i32": [_c_int, _c_int, _c_int, P, P, P, P, P, P, P, _c_sz, P],
     "regcn_snapshot_row_src_order_i32": [_c_int, _c_int, P, P, P, P, _c_sz, P],
     "regcn_rowmap_bwd_f32": [_c_int, P, P, P, _c_i64, _c_int, _c_f, P, P, P],
     "regcn_union_aggregate_bwd_f32": [P, _c_f, P],
@@ -96,7 +98,7 @@ SCORE_DIST, SCORE_RAW_SCALE = 1, 2
 _RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_bytes": _c_sz,
             "regcn_snapshot_workspace_bytes": _c_sz, "regcn_kreduce_workspace_floats": _c_sz, "regcn_snapshot_capacity": _c_i64,
             "regcn_transpose_workspace_bytes": _c_sz, "regcn_row_type_order_workspace_bytes": _c_sz,
-            "regcn_row_src_order_workspace_bytes": _c_sz,
+            "regcn_row_src_order_workspace_bytes": _c_sz, "regcn_item_src_order_workspace_bytes": _c_sz,
             "regcn_packed_weight_floats": _c_sz, "regcn_packed_linear_floats": _c_sz,
             "regcn_packed_k4_floats": _c_sz}
 
@@ -116,7 +118,7 @@ class LayerDesc(ctypes.Structure):
         ("r_next", P), ("fuse_step", _c_int), ("step_x_prev", P), ("step_w_g", P), ("step_b_g", P),
         ("step_r_static", P), ("step_w_r", P), ("step_b_r", P), ("step_eps_r", _c_f), ("step_beta", _c_f),
         ("step_layer_norm", _c_int), ("step_residual", _c_int), ("step_c_radius", _c_f), ("step_h_out", P),
-        ("step_x_out", P), ("step_r_out", P), ("trace", P),
+        ("step_x_out", P), ("step_r_out", P), ("trace", P), ("item_src_runs", _c_int),
     ]
 
 

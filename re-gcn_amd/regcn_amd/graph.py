@@ -309,6 +309,42 @@ class SnapshotGraph:
         self.__dict__["_row_src"] = t
         return t
 
+    # fused-layer items in (row, source) order: on for snapshots with at least this many
+    # inline items (config 5), where a row's duplicate sources are common; the dataset-sized
+    # snapshots keep CSR item order (the phase launches read the same lists).  A graph's
+    # `item_src_runs` attribute (True / False) overrides the size rule.
+    ITEM_SRC_RUNS_MIN_ITEMS = 1 << 20
+    item_src_runs = None
+
+    def use_item_src_runs(self):
+        if self.item_src_runs is not None:
+            return bool(self.item_src_runs)
+        return int(self.work()["item_src"].numel()) >= self.ITEM_SRC_RUNS_MIN_ITEMS
+
+    def item_src_cols(self):
+        """(item_src, item_tl) with each row's inline items in ascending source order
+        (regcn_snapshot_item_src_order_i32), built on first use and cached: with
+        regcn_layer_desc.item_src_runs the fused gather loads a row's duplicate sources once."""
+        t = self.__dict__.get("_item_src")
+        if t is not None:
+            return t
+        from . import _lib
+        wk = self.work()
+        dev = wk["rowptr"].device
+        n_items, n_tiles = int(wk["item_src"].numel()), int(self.n_pos_tiles)
+        if n_items == 0:
+            t = (wk["item_src"], wk["item_tl"])
+        else:
+            ws = torch.empty(int(_lib.lib().regcn_item_src_order_workspace_bytes(n_items, self.num_nodes_)),
+                             dtype=torch.uint8, device=dev)
+            t = (torch.empty(n_items, dtype=torch.int32, device=dev), torch.empty(n_items, dtype=torch.int32, device=dev))
+            _lib.call("regcn_snapshot_item_src_order_i32", self.num_nodes_, n_tiles, n_items, _lib.iptr(wk["tiles"]),
+                      _lib.iptr(wk["item_ptr"]), _lib.iptr(wk["item_src"]), _lib.iptr(wk["item_tl"]), _lib.iptr(t[0]),
+                      _lib.iptr(t[1]), ws.data_ptr(), ws.numel(), _lib.stream())
+            _lib.publish()  # cached: read next by whichever stream asks
+        self.__dict__["_item_src"] = t
+        return t
+
     def work(self):
         """Device work lists (raises on a CPU graph: the HIP path has no CPU fallback)."""
         if self.dev is None:

@@ -126,8 +126,12 @@ def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_
     desc.tiles = a(wk["tiles"], torch.int32)
     desc.n_pos_tiles = g.n_pos_tiles
     desc.item_ptr = a(wk["item_ptr"], torch.int32)
-    desc.item_src = a(wk["item_src"], torch.int32) if wk["item_src"].numel() else None
-    desc.item_tl = a(wk["item_tl"], torch.int32) if wk["item_tl"].numel() else None
+    items = (wk["item_src"], wk["item_tl"])
+    if mode in (_lib.AGG_UNION, _lib.AGG_EUCLID) and getattr(g, "use_item_src_runs", None) and g.use_item_src_runs():
+        items = g.item_src_cols()  # a row's duplicate sources gathered once (regcn_layer_desc.item_src_runs)
+        desc.item_src_runs = 1
+    desc.item_src = a(items[0], torch.int32) if items[0].numel() else None
+    desc.item_tl = a(items[1], torch.int32) if items[1].numel() else None
     desc.agg = a(agg)
     desc.w_n, desc.w_loop, desc.w_evolve, desc.w_skip = (a(w) for w in pk)
     desc.prev_t = a(prev_t, what="prev_h")

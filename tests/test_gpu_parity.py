@@ -412,6 +412,65 @@ def test_union_source_runs_match_edge_sums(euclid, chunk):
     assert_close(got, ref, what="source-run union aggregation")
 
 
+@pytest.mark.parametrize("kind", ["union", "euclid"])
+def test_layer_item_source_runs(kind):
+    """The fused layer with its inline items in (row, source) order (regcn_layer_desc.
+    item_src_runs: a row's duplicate sources gathered once, count * w * x[src]) against the
+    oracle and against the CSR-order items; the snapshot repeats triples so light rows have
+    source runs, and crosses the hub budget.  Also pins the item order: each row's items
+    sorted by source, tiles unchanged."""
+    import torch.nn.functional as F
+    from oracle import graph as OG
+    from oracle import layers as OL
+    from oracle import ops as O
+    from regcn_amd import graph as G
+    from regcn_amd.hyperbolic_layers import HyperbolicUnionRGCNLayer
+    from regcn_amd.layers import UnionRGCNLayer
+    V, R, d = 3000, 60, 200
+    tr = _zipf_snapshot(V, R, 20000, 9)
+    tr = np.concatenate([tr, tr[:6000], tr[:1500, ::-1]])  # repeated triples and swapped pairs
+    tr[-1500:, 1] = tr[-1500:, 1] % R
+    g = G.build_sub_graph(V, R, tr, True, DEV)
+    assert g.n_heavy > 0
+    wk = g.work()
+    isrc, itl = g.item_src_cols()
+    tiles = wk["tiles"].cpu().numpy()
+    iptr = wk["item_ptr"].cpu().numpy()
+    rowpos = np.repeat(tiles[:, 0], np.diff(iptr)) + (wk["item_tl"].cpu().numpy() & 15)
+    order = np.lexsort((wk["item_src"].cpu().numpy(), rowpos))
+    np.testing.assert_array_equal(isrc.cpu().numpy(), wk["item_src"].cpu().numpy()[order])
+    np.testing.assert_array_equal(itl.cpu().numpy(), wk["item_tl"].cpu().numpy()[order])
+    s = isrc.cpu().numpy()
+    assert (s[1:] == s[:-1]).sum() > 1000  # source runs inside rows
+    og = OG.build_sub_graph(V, R, tr)
+    gen = torch.Generator().manual_seed(4)
+    rel = torch.randn(2 * R, d, generator=gen) * 0.1
+    torch.manual_seed(0)
+    if kind == "union":
+        h = O.exp0(torch.randn(V, d, generator=gen) * 0.5, C)
+        lay = HyperbolicUnionRGCNLayer(d, d, 2 * R, -1, c=C, activation=F.rrelu, self_loop=True,
+                                       radius_msg_gamma=0.15).eval()
+        ref = OL.union_layer(og, h, rel, lay.weight_neighbor.detach(), lay.loop_weight.detach(),
+                             lay.evolve_loop_weight.detach(), C, 0.15)
+        run = lambda: lay.to(DEV)(g, h.to(DEV), rel.to(DEV))  # noqa: E731
+    else:
+        lay = UnionRGCNLayer(d, d, 2 * R, -1, activation=F.rrelu, self_loop=True).eval()
+        hx = torch.randn(V, d, generator=gen) * 0.1
+        ref = OL.euclid_union_layer(og, hx, rel, lay.weight_neighbor.detach(), lay.loop_weight.detach(),
+                                    lay.evolve_loop_weight.detach())
+        def run():
+            g.ndata["h"] = hx.to(DEV)  # the layer replaces it with its output
+            return lay.to(DEV)(g, [], rel.to(DEV))
+    outs = {}
+    for on in (True, False):
+        g.item_src_runs = on
+        with torch.no_grad():
+            outs[on] = run().clone()
+    g.item_src_runs = None
+    assert_close(outs[True], ref, what=kind + " layer, item source runs")
+    assert_close(outs[True], outs[False], what=kind + " layer, item source runs vs CSR items")
+
+
 @pytest.mark.parametrize("chunk", [None, 2])
 @pytest.mark.parametrize("kind", ["union", "lorentz", "euclid"])
 def test_layers_with_hubs_vs_oracle(kind, chunk):
