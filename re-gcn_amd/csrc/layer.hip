@@ -87,7 +87,9 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
   const bool prefetch = wfirst && !(gate_with_loop && wfirst == wsel);
   BRing br;
   if (!inline_gather && prefetch) br.load(wfirst, p.d);
-  stage_rows<false>(X, lda, p.x, trow, p.d, count);
+  // inline gather: the self-loop rows stream into LDS while the gather's first indices load
+  if (inline_gather) stage_rows_async(X, lda, p.x, trow, p.d);
+  else stage_rows<false>(X, lda, p.x, trow, p.d, count);
   if (pos && AGG == AGG_NONE) stage_rows<false>(part, lda, p.agg, trow, p.d, count);
   if (!inline_gather) {
     if (STEP) stage_rows<true>(P2, lda, p.step.x_prev, trow, p.d, count);

@@ -86,6 +86,24 @@ __device__ __forceinline__ void stage_rows(float* T, int lda, const float* __res
   }
 }
 
+// Global -> LDS row staging with no VGPR round trip (global_load_lds, 16 B per lane, LDS
+// destination = wave-uniform row base + 16 B x lane): wave w issues rows w, w + NWAVE, ...;
+// lanes past d / 4 idle.  Asynchronous: the loads land while the caller goes on (the fused
+// layer issues the self-loop rows before its gather, whose first index wait retires them);
+// hipcc drains them (vmcnt) before the next barrier.  Every row is a real row (callers pad
+// `rows` with a valid row), so rows past the tile's count hold that row's values, not zeros.
+__device__ __forceinline__ void stage_rows_async(float* T, int lda, const float* __restrict__ A, const int* rows,
+                                                 int d) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = w; i < TM; i += NWAVE) {
+    const float* src = A + (int64_t)rows[i] * d;
+    if (lane < (d >> 2))
+      __builtin_amdgcn_global_load_lds((const void*)(src + lane * 4),
+                                       (__attribute__((address_space(3))) void*)(T + i * lda), 16, 0, 0);
+  }
+}
+
 // nt: this wave's column tiles that hold output columns (wave-uniform); the rest of the
 // packed weight is zero padding (d_out < 256), whose MFMAs are skipped.
 __device__ __forceinline__ void mfma_tpw(Frag& acc, float a, bvec b, int nt = TPW) {
