@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 case "$WHICH" in
   bench) T=c5; C="python bench.py --no-extras --no-scale --no-cpu-baseline --steps 6 --warmup 1";;
-  agg) T=agg${UNIFORM:+_uniform}; C="python tools/aggbench.py --reps 2 --which union_aggregate,lorentz_aggregate ${UNIFORM:+--uniform-src}";;
+  agg) T=agg${UNIFORM:+_uniform}; C="python tools/aggbench.py --reps 2 --which union_aggregate,union_aggregate_src_runs,lorentz_aggregate ${UNIFORM:+--uniform-src}";;
   icews) T=ic; C="python bench.py --config icews14s_lgcn_roth --no-scale --no-cpu-baseline --concurrent 1 --steps 48";;
 esac
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_prof -o run -- $C > gpurun_out/${T}_prof.log 2>&1 || { echo "rocprof failed"; exit 1; }

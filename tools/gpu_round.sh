@@ -19,7 +19,7 @@ B="python bench.py --no-extras --no-scale --no-cpu-baseline --steps 6 --warmup 1
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5_prof -o run -- $B > gpurun_out/c5_prof.log 2>&1 || { echo "rocprof c5 failed"; exit 1; }
 timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/c5_fetch -o run -- $B > gpurun_out/c5_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
 timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/c5_write -o run -- $B > gpurun_out/c5_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
-A="python tools/aggbench.py --reps 2 --which union_aggregate,lorentz_aggregate"
+A="python tools/aggbench.py --reps 2 --which union_aggregate,union_aggregate_src_runs,lorentz_aggregate"
 for u in "" "--uniform-src"; do
   t=agg${u:+_uniform}
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${t}_prof -o run -- $A $u > gpurun_out/${t}_prof.log 2>&1 || { echo "agg rocprof failed"; exit 1; }
