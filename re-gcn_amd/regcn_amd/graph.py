@@ -24,6 +24,8 @@ Built once per snapshot and cached across epochs: on the d
 csrc/graphbuild.hip when use_cuda (build_sub_graph_device), else with numpy here; both
 builds produce the same lists bit for bit (tests/test_gpu_graph.py).
 """
+import os
+
 import numpy as np
 import torch
 
@@ -463,6 +465,91 @@ def _chunk_rows_spans(start, length, chunk_edges):
     chunks = np.array(chunks_l, dtype=np.int32).reshape(-1, 4)
     fixups, nslot = group_fixups(fix_l, nslot)
     return chunks, fixups, nslot
+
+
+# Relation means over entity blocks (hyperbolic_model.relation_context at large snapshots).  A
+# relation's r_to_e list is ascending in entity id (np.unique), so cutting every forward
+# relation's span at multiples of REL_BLOCK entity ids gives chunks that touch one block of x
+# rows each.  The chunks of block k are dealt to the workgroups of XCD k % 8 (one wave per
+# chunk, 4 waves per workgroup, workgroup w on XCD w % 8), in block order, so a block's rows come
+# from HBM into that XCD's L2 once and serve every relation that lists them, instead of one HBM
+# read per (relation, entity) pair.  Same kernel (regcn_segment_mean_f32), same values up to the
+# fp32 association of each relation's partial sums (fixed order: deterministic).
+REL_BLOCK = int(os.environ.get("REGCN_REL_BLOCK", "4096"))  # entity ids per block; 0: CSR chunks
+REL_BLOCK_MIN_PAIRS = 1 << 20  # smaller snapshots keep the plain chunks (few rows, L2-resident)
+REL_BLOCK_CHUNK = 256          # pairs per chunk inside one (relation, block) segment
+_XCDS, _WAVES_PER_WG = 8, 4
+
+
+def rel_block_lists(rel_idx, rel_start, rel_len, block, chunk=REL_BLOCK_CHUNK):
+    """Chunks {rel, beg, end, slot} and fix-ups over the forward relations' spans
+    [rel_start[r], rel_start[r] + rel_len[r]) of `rel_idx`, cut at entity-block boundaries and
+    every `chunk` pairs, in XCD-dealt dispatch order (padding chunks: an empty span into the
+    spare last slot, which no fix-up reads).  Returns (chunks, fixups, n_slots incl. the spare)."""
+    rel_start = np.asarray(rel_start, dtype=np.int64)
+    rel_len = np.asarray(rel_len, dtype=np.int64)
+    R = len(rel_len)
+    total = int(rel_len.sum())
+    if total == 0:
+        return np.zeros((0, 4), np.int32), np.zeros((0, 4), np.int32), 0
+    r_of = np.repeat(np.arange(R, dtype=np.int64), rel_len)
+    first = np.cumsum(rel_len) - rel_len
+    pos = np.arange(total, dtype=np.int64) + np.repeat(rel_start - first, rel_len)
+    blk = np.asarray(rel_idx, dtype=np.int64)[pos] // block
+    new_seg = np.ones(total, dtype=bool)
+    new_seg[1:] = (r_of[1:] != r_of[:-1]) | (blk[1:] != blk[:-1])
+    seg_start = np.flatnonzero(new_seg)
+    seg_id = np.cumsum(new_seg) - 1
+    off = np.arange(total, dtype=np.int64) - seg_start[seg_id]
+    cs = np.flatnonzero(new_seg | (off % chunk == 0))
+    ce = np.append(cs[1:], total)
+    c_rel, c_blk = r_of[cs], blk[cs]
+    c_beg, c_end = pos[cs], pos[ce - 1] + 1
+    n_per = np.bincount(c_rel, minlength=R)
+    multi = n_per[c_rel] > 1
+    slot = np.full(len(cs), -1, dtype=np.int64)
+    slot[multi] = np.arange(int(multi.sum()))
+    nslot = int(multi.sum())
+    mr = np.flatnonzero(n_per > 1)
+    s_first = np.cumsum(n_per[mr]) - n_per[mr]
+    fix = np.stack([mr, s_first, s_first + n_per[mr], np.zeros_like(mr)], axis=1)
+    fixups, nslot = group_fixups(fix, nslot)
+    spare = nslot
+    chunks = np.stack([c_rel, c_beg, c_end, slot], axis=1)
+    # deal: position p belongs to XCD (p // 4) % 8; XCD x takes blocks x, x + 8, ... in order
+    order = np.argsort(c_blk, kind="stable")
+    xq = (c_blk[order] % _XCDS)
+    queues = [order[xq == x] for x in range(_XCDS)]
+    L = max(len(q) for q in queues)
+    L = (L + _WAVES_PER_WG - 1) // _WAVES_PER_WG * _WAVES_PER_WG
+    out = np.tile(np.array([0, 0, 0, spare], dtype=np.int64), (_XCDS * L, 1))
+    q = np.arange(L)
+    for x, qu in enumerate(queues):
+        p = ((q // _WAVES_PER_WG) * _XCDS + x) * _WAVES_PER_WG + q % _WAVES_PER_WG
+        out[p[:len(qu)]] = chunks[qu]
+    return out.astype(np.int32), np.asarray(fixups, dtype=np.int32).reshape(-1, 4), nslot + 1
+
+
+def rel_block_work(g, R):
+    """Device (chunks, fixups, n_slots) of rel_block_lists for snapshot `g` with R forward
+    relations, built on first use
+    and cached (None: the snapshot keeps the plain relation chunks)."""
+    hit = g.__dict__.get("_rel_block")
+    if hit is not None:
+        return hit[0]
+    wk = g.work()
+    res = None
+    if REL_BLOCK > 0 and int(wk["rel_idx"].numel()) // 2 >= REL_BLOCK_MIN_PAIRS:
+        idx = wk["rel_idx"].cpu().numpy()
+        start = wk["rel_start"][:R].cpu().numpy()
+        cnt = wk["rel_count"][:R].cpu().numpy().astype(np.int64)
+        ch, fx, ns = rel_block_lists(idx, start, cnt, REL_BLOCK)
+        dev = wk["rel_idx"].device
+        res = (torch.from_numpy(ch).to(dev), torch.from_numpy(fx).to(dev), ns)
+        from . import _lib
+        _lib.publish()
+    g.__dict__["_rel_block"] = (res,)
+    return res
 
 
 class DeviceSnapshotGraph(SnapshotGraph):

@@ -26,7 +26,7 @@ from . import _lib
 from .hyperbolic_decoder import (HyperbolicAttH, HyperbolicAttHRel, HyperbolicConvTransE, HyperbolicConvTransR,
                                  HyperbolicMuRP, HyperbolicMuRPRel, HyperbolicRotH, HyperbolicRotHRel,
                                  roth_pair_fusable, roth_pair_predict)
-from .graph import SnapshotGraph
+from .graph import SnapshotGraph, rel_block_work
 from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell, LorentzRGCNLayer, StepSpec, \
     _heavy_aggregate
 from .hyperbolic_ops import HyperbolicOps, TemporalRadiusEvolution
@@ -89,8 +89,12 @@ def relation_context(x, g, num_rels2):
     V, d = x.shape
     R = num_rels2 // 2
     out = torch.zeros(num_rels2, d, device=x.device, dtype=torch.float32)
-    ch, fx = wk["rel_chunks"], wk["rel_fixups"]
-    part = torch.empty(g.rel_slots, d, device=x.device, dtype=torch.float32) if g.rel_slots else None
+    blocks = rel_block_work(g, R)
+    if blocks is not None:  # large snapshot: entity-block chunks, XCD-dealt (graph.rel_block_lists)
+        ch, fx, n_slots = blocks
+    else:
+        ch, fx, n_slots = wk["rel_chunks"], wk["rel_fixups"], g.rel_slots
+    part = torch.empty(n_slots, d, device=x.device, dtype=torch.float32) if n_slots else None
     _lib.call("regcn_segment_mean_f32", _lib.fptr(x, "x"), _lib.iptr(wk["rel_idx"]), _lib.fptr(wk["rel_count"]),
               _lib.iptr(ch), ch.shape[0], _lib.iptr(fx), fx.shape[0], d, _lib.fptr(part), d, _lib.fptr(out),
               _lib.stream())

@@ -103,3 +103,41 @@ def test_lorentz_layer_config5(snapshot):
     if bool(zero.any()):
         assert_close(got[zero], ref[zero], what="rows without in-edges")
     np.testing.assert_array_equal(int(zero.sum()), V - g.n_pos)
+
+
+def test_relation_means_entity_blocks(snapshot):
+    """Relation means at config 5 over the entity-block chunks (graph.rel_block_lists: spans cut
+    at entity-block boundaries, a block's chunks dealt to one XCD) against a float64 segment
+    mean of the same r_to_e spans (hyperbolic_model.py:802-812) and against the plain relation
+    chunks: |delta| <= 1e-5 * max(1, |ref|); the inverse rows copy the forward ones."""
+    from regcn_amd import graph as G
+    from regcn_amd.hyperbolic_model import relation_context
+    g, h, rel = snapshot
+    R2, d = rel.shape[0], h.shape[1]
+    R = R2 // 2
+    g.__dict__.pop("_rel_block", None)
+    assert G.rel_block_work(g, R) is not None, "config 5 must take the entity-block lists"
+    with torch.no_grad():
+        got = relation_context(h, g, R2)
+        wk = g.work()
+        lens = wk["rel_count"][:R].long()
+        first = torch.cumsum(lens, 0) - lens
+        pos = torch.arange(int(lens.sum()), device=DEV) + torch.repeat_interleave(wk["rel_start"][:R].long() - first, lens)
+        ent = wk["rel_idx"].long()[pos]
+        rel_of = torch.repeat_interleave(torch.arange(R, device=DEV), lens)
+        ref = torch.zeros(R, d, device=DEV, dtype=torch.float64)
+        for c in range(0, ent.numel(), 1 << 20):
+            ref.index_add_(0, rel_of[c:c + (1 << 20)], h[ent[c:c + (1 << 20)]].double())
+        ref = ref / lens.clamp(min=1).double().unsqueeze(1)
+        saved = G.REL_BLOCK
+        try:
+            G.REL_BLOCK = 0
+            g.__dict__.pop("_rel_block", None)
+            plain = relation_context(h, g, R2)
+        finally:
+            G.REL_BLOCK = saved
+            g.__dict__.pop("_rel_block", None)
+    tol = 1e-5 * max(1.0, float(ref.abs().max()))
+    assert float((got[:R].double() - ref).abs().max()) <= tol
+    assert float((got[:R] - plain[:R]).abs().max()) <= tol
+    assert torch.equal(got[R:], got[:R])

@@ -227,3 +227,49 @@ def test_bump_versions_restores_the_cache_key_after_a_fused_step():
     bump_versions([p, None])
     assert p._version > v0
     assert torch.equal(p.detach(), stepped) and torch.equal(torch.signbit(p.detach()), torch.signbit(stepped))
+
+
+@pytest.mark.parametrize("block,chunk", [(512, 100), (64, 7), (100000, 256)])
+def test_relation_entity_block_lists(block, chunk):
+    """graph.rel_block_lists: every forward pair in exactly one chunk, a chunk inside one entity
+    block, block k's chunks at dispatch positions p with (p // 4) % 8 == k % 8, and the
+    chunk -> partial -> group -> fix-up walk (aggregate.hip k_gather_sum / k_fixup_groups /
+    k_gather_fixup) giving each relation's mean."""
+    rng = np.random.default_rng(block + chunk)
+    R, V = 9, 6000
+    lists = [np.unique(rng.integers(0, V, size=int(rng.integers(0, 4000)))) for _ in range(R)]
+    lists[3] = np.zeros(0, np.int64)  # a relation absent from the snapshot
+    lens = np.array([len(x) for x in lists])
+    idx = np.concatenate(lists + lists)  # forward spans, then the inverse copies
+    start = np.cumsum(lens) - lens
+    ch, fx, ns = G.rel_block_lists(idx, start, lens, block, chunk=chunk)
+    assert ch.dtype == np.int32 and fx.dtype == np.int32 and ch.shape[1] == 4
+    covered = np.zeros(int(lens.sum()), np.int64)
+    for r, b, e, s in ch:
+        if e == b:
+            assert s == ns - 1  # padding: the spare slot, read by no fix-up
+            continue
+        assert start[r] <= b < e <= start[r] + lens[r] and e - b <= chunk
+        assert idx[b] // block == idx[e - 1] // block
+        covered[b:e] += 1
+    assert (covered == 1).all()
+    p = np.arange(len(ch))
+    real = ch[:, 2] > ch[:, 1]
+    assert (((p // 4) % 8)[real] == (idx[ch[real, 1]] // block) % 8).all()
+    assert not ((fx[:, 1] <= ns - 1) & (fx[:, 2] > ns - 1)).any()
+    x = rng.standard_normal((V, 5))
+    part, out = np.zeros((ns, 5)), np.zeros((R, 5))
+    for r, b, e, s in ch:
+        acc = x[idx[b:e]].sum(0)
+        if s < 0:
+            out[r] = acc / lens[r]
+        else:
+            part[s] = acc
+    for r, b, e, pad in fx:
+        if pad > 0:
+            part[pad - 1] = part[b:e].sum(0)
+    for r, b, e, pad in fx:
+        if pad == 0:
+            out[r] = part[b:e].sum(0) / lens[r]
+    ref = np.stack([x[l].mean(0) if len(l) else np.zeros(5) for l in lists])
+    np.testing.assert_allclose(out, ref, rtol=1e-12, atol=1e-12)
