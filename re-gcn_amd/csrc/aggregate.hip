@@ -444,11 +444,11 @@ int gather_sum(int mode, const float* x, const float* radius, const float* rel, 
   const Chunk* ch = (const Chunk*)chunks;
   const Fixup* fx = (const Fixup*)fixups;
   if (n_chunks > 0) {
-    // the mean runs every chunk in one pass (one wave each, no grid-stride): chunk i sits on
-    // workgroup i / 4, XCD (i / 4) % 8, in dispatch order (graph.py rel_block_lists deals a
-    // block's chunks to one XCD)
+    // the mean and the source-run hub pass run every chunk in one pass (one wave each, no
+    // grid-stride): chunk i sits on workgroup i / 4, XCD (i / 4) % 8, in dispatch order
+    // (graph.py blocked_span_chunks deals a block's chunks to one XCD)
     const long gm = ((long)n_chunks + 3) / 4;
-    dim3 g(mode == AGG_MEAN && gm <= 0x7fffffffL ? (unsigned)gm : grid_for(n_chunks)), b(256);
+    dim3 g((mode == AGG_MEAN || col_src_s) && gm <= 0x7fffffffL ? (unsigned)gm : grid_for(n_chunks)), b(256);
     if (mode == AGG_UNION && col_src_s)
       hipLaunchKernelGGL((k_union_runs<false, true>), g, b, 0, st, x, radius, rel, col_src, col_type, col_src_s,
                          rowscale, ch, n_chunks, gamma, d, partial, pstride, out);

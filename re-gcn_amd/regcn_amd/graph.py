@@ -481,53 +481,62 @@ REL_BLOCK_CHUNK = 256          # pairs per chunk inside one (relation, block) se
 _XCDS, _WAVES_PER_WG = 8, 4
 
 
-def rel_block_lists(rel_idx, rel_start, rel_len, block, chunk=REL_BLOCK_CHUNK):
-    """Chunks {rel, beg, end, slot} and fix-ups over the forward relations' spans
-    [rel_start[r], rel_start[r] + rel_len[r]) of `rel_idx`, cut at entity-block boundaries and
-    every `chunk` pairs, in XCD-dealt dispatch order (padding chunks: an empty span into the
-    spare last slot, which no fix-up reads).  Returns (chunks, fixups, n_slots incl. the spare)."""
-    rel_start = np.asarray(rel_start, dtype=np.int64)
-    rel_len = np.asarray(rel_len, dtype=np.int64)
-    R = len(rel_len)
-    total = int(rel_len.sum())
+def blocked_span_chunks(span_rows, span_beg, span_len, keys, block, chunk, xcds=_XCDS, waves=_WAVES_PER_WG):
+    """Chunks {row, beg, end, slot} and fix-ups over spans [span_beg[i], span_beg[i] +
+    span_len[i]) of a position array whose `keys` (entity ids, ascending inside each span) pick
+    the block key // block; a span is cut at block boundaries and every `chunk` positions.  A
+    span's chunks get consecutive partial slots (none if it has one chunk: the wave finishes
+    the row).  Dispatch order: position p belongs to XCD (p // waves) % xcds and XCD x takes the
+    chunks of blocks x, x + xcds, ... in block order; padding chunks are empty spans into the
+    spare last slot, which no fix-up reads.  torch tensors (any device) in, (chunks int32
+    [n, 4], fixups int32 numpy [m, 4] after group_fixups, n_slots incl. the spare) out."""
+    dev = span_len.device
+    span_len = span_len.long()
+    n = int(span_len.numel())
+    total = int(span_len.sum()) if n else 0
     if total == 0:
-        return np.zeros((0, 4), np.int32), np.zeros((0, 4), np.int32), 0
-    r_of = np.repeat(np.arange(R, dtype=np.int64), rel_len)
-    first = np.cumsum(rel_len) - rel_len
-    pos = np.arange(total, dtype=np.int64) + np.repeat(rel_start - first, rel_len)
-    blk = np.asarray(rel_idx, dtype=np.int64)[pos] // block
-    new_seg = np.ones(total, dtype=bool)
-    new_seg[1:] = (r_of[1:] != r_of[:-1]) | (blk[1:] != blk[:-1])
-    seg_start = np.flatnonzero(new_seg)
-    seg_id = np.cumsum(new_seg) - 1
-    off = np.arange(total, dtype=np.int64) - seg_start[seg_id]
-    cs = np.flatnonzero(new_seg | (off % chunk == 0))
-    ce = np.append(cs[1:], total)
-    c_rel, c_blk = r_of[cs], blk[cs]
-    c_beg, c_end = pos[cs], pos[ce - 1] + 1
-    n_per = np.bincount(c_rel, minlength=R)
-    multi = n_per[c_rel] > 1
-    slot = np.full(len(cs), -1, dtype=np.int64)
-    slot[multi] = np.arange(int(multi.sum()))
+        return torch.zeros(0, 4, dtype=torch.int32, device=dev), np.zeros((0, 4), np.int32), 0
+    span_of = torch.repeat_interleave(torch.arange(n, device=dev), span_len)
+    first = torch.cumsum(span_len, 0) - span_len
+    pos = torch.arange(total, device=dev) + torch.repeat_interleave(span_beg.long() - first, span_len)
+    blk = keys[pos].long() // block
+    new_seg = torch.ones(total, dtype=torch.bool, device=dev)
+    new_seg[1:] = (span_of[1:] != span_of[:-1]) | (blk[1:] != blk[:-1])
+    seg_start = torch.nonzero(new_seg).squeeze(1)
+    off = torch.arange(total, device=dev) - seg_start[torch.cumsum(new_seg, 0) - 1]
+    cs = torch.nonzero(new_seg | (off % chunk == 0)).squeeze(1)
+    ce = torch.cat([cs[1:], torch.tensor([total], device=dev)])
+    c_span, c_blk = span_of[cs], blk[cs]
+    n_per = torch.bincount(c_span, minlength=n)
+    multi = n_per[c_span] > 1
+    slot = torch.full_like(cs, -1)
     nslot = int(multi.sum())
-    mr = np.flatnonzero(n_per > 1)
-    s_first = np.cumsum(n_per[mr]) - n_per[mr]
-    fix = np.stack([mr, s_first, s_first + n_per[mr], np.zeros_like(mr)], axis=1)
+    slot[multi] = torch.arange(nslot, device=dev)
+    mr = torch.nonzero(n_per > 1).squeeze(1)
+    s_first = torch.cumsum(n_per[mr], 0) - n_per[mr]
+    fix = torch.stack([span_rows.long()[mr], s_first, s_first + n_per[mr], torch.zeros_like(mr)], 1).cpu().numpy()
     fixups, nslot = group_fixups(fix, nslot)
-    spare = nslot
-    chunks = np.stack([c_rel, c_beg, c_end, slot], axis=1)
-    # deal: position p belongs to XCD (p // 4) % 8; XCD x takes blocks x, x + 8, ... in order
-    order = np.argsort(c_blk, kind="stable")
-    xq = (c_blk[order] % _XCDS)
-    queues = [order[xq == x] for x in range(_XCDS)]
-    L = max(len(q) for q in queues)
-    L = (L + _WAVES_PER_WG - 1) // _WAVES_PER_WG * _WAVES_PER_WG
-    out = np.tile(np.array([0, 0, 0, spare], dtype=np.int64), (_XCDS * L, 1))
-    q = np.arange(L)
+    chunks = torch.stack([span_rows.long()[c_span], pos[cs], pos[ce - 1] + 1, slot], 1)
+    order = torch.sort(c_blk, stable=True).indices
+    xq = c_blk[order] % xcds
+    queues = [order[xq == x] for x in range(xcds)]
+    L = max(int(q.numel()) for q in queues)
+    L = (L + waves - 1) // waves * waves
+    out = torch.tensor([0, 0, 0, nslot], dtype=torch.long, device=dev).repeat(xcds * L, 1)
+    q = torch.arange(L, device=dev)
     for x, qu in enumerate(queues):
-        p = ((q // _WAVES_PER_WG) * _XCDS + x) * _WAVES_PER_WG + q % _WAVES_PER_WG
-        out[p[:len(qu)]] = chunks[qu]
-    return out.astype(np.int32), np.asarray(fixups, dtype=np.int32).reshape(-1, 4), nslot + 1
+        p = ((q // waves) * xcds + x) * waves + q % waves
+        out[p[:qu.numel()]] = chunks[qu]
+    return out.to(torch.int32), np.asarray(fixups, dtype=np.int32).reshape(-1, 4), nslot + 1
+
+
+def rel_block_lists(rel_idx, rel_start, rel_len, block, chunk=REL_BLOCK_CHUNK):
+    """blocked_span_chunks over the forward relations' r_to_e spans (numpy in and out)."""
+    rel_len = np.asarray(rel_len, dtype=np.int64)
+    ch, fx, ns = blocked_span_chunks(torch.arange(len(rel_len)), torch.as_tensor(np.asarray(rel_start, np.int64)),
+                                     torch.from_numpy(rel_len), torch.as_tensor(np.asarray(rel_idx, np.int64)),
+                                     block, chunk)
+    return ch.numpy(), fx, ns
 
 
 def rel_block_work(g, R):
@@ -540,15 +549,45 @@ def rel_block_work(g, R):
     wk = g.work()
     res = None
     if REL_BLOCK > 0 and int(wk["rel_idx"].numel()) // 2 >= REL_BLOCK_MIN_PAIRS:
-        idx = wk["rel_idx"].cpu().numpy()
-        start = wk["rel_start"][:R].cpu().numpy()
-        cnt = wk["rel_count"][:R].cpu().numpy().astype(np.int64)
-        ch, fx, ns = rel_block_lists(idx, start, cnt, REL_BLOCK)
         dev = wk["rel_idx"].device
-        res = (torch.from_numpy(ch).to(dev), torch.from_numpy(fx).to(dev), ns)
+        ch, fx, ns = blocked_span_chunks(torch.arange(R, device=dev), wk["rel_start"][:R], wk["rel_count"][:R].long(),
+                                         wk["rel_idx"], REL_BLOCK, REL_BLOCK_CHUNK)
+        res = (ch, torch.from_numpy(fx).to(dev), ns)
         from . import _lib
         _lib.publish()
     g.__dict__["_rel_block"] = (res,)
+    return res
+
+
+# The union hub pass over source blocks (hyperbolic_layers._heavy_aggregate, source runs): a
+# hub row's edges in row/source order (row_src_cols) are ascending in source id, so the same
+# cut at source-block boundaries, dealt to XCDs by block, lets the hub rows that list a source
+# share its row from one L2.
+HUB_BLOCK = int(os.environ.get("REGCN_HUB_BLOCK", "16384"))  # source ids per block; 0: plain chunks
+HUB_BLOCK_MIN_EDGES = 1 << 20
+
+
+def hub_block_work(g):
+    """Device (chunks, fixups, n_slots) of the hub rows' edge spans cut at source blocks
+    (blocked_span_chunks over row_src_cols), built on first use and cached; None keeps the
+    plain heavy chunks."""
+    hit = g.__dict__.get("_hub_block")
+    if hit is not None:
+        return hit[0]
+    res = None
+    wk = g.work()
+    hc = wk["heavy_chunks"]
+    if HUB_BLOCK > 0 and g.n_heavy and hc.numel():
+        rows = wk["rows"][:g.n_heavy].long()
+        beg = wk["rowptr"].long()[rows]
+        ln = wk["rowptr"].long()[rows + 1] - beg
+        if int(ln.sum()) >= HUB_BLOCK_MIN_EDGES:
+            ss = g.row_src_cols()
+            ch, fx, ns = blocked_span_chunks(rows, beg, ln, ss, HUB_BLOCK, max(int(getattr(g, "chunk_edges", None) or 1024), 64))
+            res = (ch, torch.from_numpy(fx).to(ss.device), ns)
+            from . import _lib
+            _lib.publish()
+    g.__dict__["_hub_block"] = (res,)
     return res
 
 

@@ -17,6 +17,7 @@ from . import _lib
 from .parallel import ShardedGraph
 from .tangent import attach, tangent_of
 from .weights import packed
+from .graph import hub_block_work
 
 EPS = 1e-6
 TRACE = None  # int64 HIP tensor (>= 8 x workgroups) to record k_layer phase timestamps (profiling)
@@ -65,6 +66,10 @@ def _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c):
         cs, ct = g.row_type_cols()
         ss = g.row_src_cols()
         euclid = mode != _lib.AGG_UNION
+        hb = hub_block_work(g) if hasattr(g, "row_src_cols") else None
+        if hb is not None:  # large snapshot: spans cut at source blocks, XCD-dealt (graph.py)
+            hc, hf, n_slots = hb
+            part = torch.empty(n_slots, stride, device=x.device, dtype=torch.float32)
         _lib.call("regcn_union_aggregate_src_runs_f32", f(x), None if euclid else f(r), f(rel), i(cs), i(ct), i(ss),
                   f(wk["norm"]), i(hc), hc.shape[0], i(hf), hf.shape[0], float(gamma), int(euclid), d, f(part), stride,
                   f(agg), _lib.stream())

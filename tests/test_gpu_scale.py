@@ -141,3 +141,34 @@ def test_relation_means_entity_blocks(snapshot):
     assert float((got[:R].double() - ref).abs().max()) <= tol
     assert float((got[:R] - plain[:R]).abs().max()) <= tol
     assert torch.equal(got[R:], got[:R])
+
+
+@pytest.mark.parametrize("euclid", [False, True])
+def test_hub_pass_source_blocks(snapshot, euclid):
+    """The hub rows' pre-aggregation over source-block chunks (graph.hub_block_work: each hub
+    row's source-ordered span cut at source-id blocks, XCD-dealt) equals the plain heavy chunks'
+    within 1e-5 * max(1, |ref|) on every hub row (same sums, another fp32 association)."""
+    from oracle import ops
+    from regcn_amd import _lib
+    from regcn_amd import graph as G
+    from regcn_amd.hyperbolic_layers import _heavy_aggregate
+    g, h, rel = snapshot
+    mode = _lib.AGG_EUCLID if euclid else _lib.AGG_UNION
+    with torch.no_grad():
+        x = ops.log0(h, C).contiguous()
+        r = h.norm(dim=1).contiguous()
+        g.__dict__.pop("_hub_block", None)
+        assert G.hub_block_work(g) is not None, "config 5 must take the source-block hub lists"
+        got = _heavy_aggregate(mode, g, x, r, rel, None, 1, 0.15, C)
+        saved = G.HUB_BLOCK
+        try:
+            G.HUB_BLOCK = 0
+            g.__dict__.pop("_hub_block", None)
+            ref = _heavy_aggregate(mode, g, x, r, rel, None, 1, 0.15, C)
+        finally:
+            G.HUB_BLOCK = saved
+            g.__dict__.pop("_hub_block", None)
+    hubs = g.work()["rows"][:g.n_heavy].long()
+    a, b = got[hubs], ref[hubs]
+    assert torch.isfinite(a).all()
+    assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
