@@ -546,6 +546,8 @@ def rel_block_work(g, R):
     hit = g.__dict__.get("_rel_block")
     if hit is not None:
         return hit[0]
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        return None  # built with host round trips: not inside a HIP-graph capture (plain chunks)
     wk = g.work()
     res = None
     if REL_BLOCK > 0 and int(wk["rel_idx"].numel()) // 2 >= REL_BLOCK_MIN_PAIRS:
@@ -574,6 +576,8 @@ def hub_block_work(g):
     hit = g.__dict__.get("_hub_block")
     if hit is not None:
         return hit[0]
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+        return None  # built with host round trips: not inside a HIP-graph capture (plain chunks)
     res = None
     wk = g.work()
     hc = wk["heavy_chunks"]
