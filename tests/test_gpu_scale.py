@@ -172,3 +172,53 @@ def test_hub_pass_source_blocks(snapshot, euclid):
     a, b = got[hubs], ref[hubs]
     assert torch.isfinite(a).all()
     assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))
+
+
+def test_config5_predict_entity_blocks_vs_plain():
+    """The headline workload end to end (BASELINE.json configs[4]: 3 snapshots of |E| = 50M,
+    2 uvrgcn layers, RotH + RotHRel on 256 queries; bench.build_model) with the entity-block
+    relation and hub lists against the plain chunk lists: the same sums in another fp32
+    association, so the scores agree to 1e-4 * max(1, |ref|) and each target's raw rank moves
+    by at most its near-ties (candidates within twice the largest score change of it)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import bench
+    from regcn_amd import graph as G
+    from regcn_amd.synthetic import CONFIGS, snapshot_series
+    cfg = CONFIGS["synthetic_1m"]
+    snaps = snapshot_series(11, cfg["V"], cfg["R"], cfg["T"] + 1, cfg["per_snap"])
+    glist = [G.build_sub_graph(cfg["V"], cfg["R"], s, True, DEV) for s in snaps[:cfg["T"]]]
+    test = torch.from_numpy(snaps[cfg["T"]][:256]).to(DEV)
+    del snaps
+    model = bench.build_model(cfg, 200, DEV, seed=7)
+    model.param_caches = False
+    saved = (G.REL_BLOCK, G.HUB_BLOCK)
+    outs = []
+    try:
+        for rb, hb in (saved, (0, 0)):
+            G.REL_BLOCK, G.HUB_BLOCK = rb, hb
+            for g in glist:
+                g.__dict__.pop("_rel_block", None)
+                g.__dict__.pop("_hub_block", None)
+            with torch.no_grad():
+                r = model.predict(glist, cfg["R"], None, test, True)
+            outs.append([t.clone() for t in r[1:3]])
+            if rb:
+                assert all(G.rel_block_work(g, cfg["R"]) is not None and G.hub_block_work(g) is not None for g in glist)
+    finally:
+        G.REL_BLOCK, G.HUB_BLOCK = saved
+        for g in glist:
+            g.__dict__.pop("_rel_block", None)
+            g.__dict__.pop("_hub_block", None)
+    (s_b, sr_b), (s_p, sr_p) = outs
+    for a, b in ((s_b, s_p), (sr_b, sr_p)):
+        assert torch.isfinite(a).all()
+        assert float((a - b).abs().max()) <= 1e-4 * max(1.0, float(b.abs().max()))
+    tgt = torch.cat([test[:, 2], test[:, 0]]).long()  # queries and their inverses (predict)
+    assert s_b.shape[0] == tgt.numel()
+    # a candidate can swap order with the target only if their plain scores lie within twice
+    # the largest score change: the raw ranks differ by at most that many near-ties
+    rank = lambda s: (s > s.gather(1, tgt[:, None])).sum(1)
+    band = 2.0 * float((s_b - s_p).abs().max())
+    ties = ((s_p - s_p.gather(1, tgt[:, None])).abs() <= band).sum(1)
+    assert bool(((rank(s_b) - rank(s_p)).abs() <= ties).all())
