@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 7
+#define REGCN_ABI_VERSION 8
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -453,6 +453,17 @@ int regcn_timestep_f32(const float* hc, const float* x_prev, const float* w_g, c
                        const float* r_static, const float* w_r, const float* b_r, float eps_r, float beta,
                        int32_t layer_norm, int32_t residual, int32_t V, int32_t d, float c, float c_radius,
                        float* h_out, float* x_out, float* r_out, void* stream);
+/* The same timestep for --run-analysis (hyperbolic_main.py:716): also writes the time gate
+ * sigmoid(clamp(x_prev) @ W_g + b_g) of every element into gate_out (V x d: the reference's
+ * gate_list entry, hyperbolic_model.py:848-856) and, when residual != 0, the radius evolution's
+ * per-row terms into stat_out (3 x V, nullable): the clipped delta, the dynamic radius |h| and
+ * the base radius beta r_static + (1 - beta) |h| (TemporalRadiusEvolution's evolution stats,
+ * hyperbolic_ops.py:407-434).  h_out / x_out / r_out equal regcn_timestep_f32's bit for bit. */
+int regcn_timestep_analysis_f32(const float* hc, const float* x_prev, const float* w_g, const float* b_g,
+                                const float* r_static, const float* w_r, const float* b_r, float eps_r, float beta,
+                                int32_t layer_norm, int32_t residual, int32_t V, int32_t d, float c, float c_radius,
+                                float* h_out, float* x_out, float* r_out, float* gate_out, float* stat_out,
+                                void* stream);
 
 /* ---- a9/a10: decoder queries (one launch each) -------------------------------------- */
 /* Queries b < n_test use trip[b] = (s, r, o) (int64, n_test x 3); b >= n_test the inverse

@@ -44,8 +44,9 @@ def static_radius(sd, cfg):
     return torch.clamp(r, max=1.0 / math.sqrt(cfg["c"]) - 1e-6)
 
 
-def radius_evolution(h, r_static, sd, cfg):
-    """TemporalRadiusEvolution.forward, hyperbolic_ops.py:395-435."""
+def radius_evolution(h, r_static, sd, cfg, stats=None):
+    """TemporalRadiusEvolution.forward, hyperbolic_ops.py:395-435 (`stats`: a dict to receive
+    its last_evolution_stats, :426-434)."""
     c = cfg["c"]
     t = ops.log0(h, c)
     delta = F.linear(t, sd["temporal_radius_evolution.radius_mlp.weight"],
@@ -54,12 +55,18 @@ def radius_evolution(h, r_static, sd, cfg):
     dyn = ops.get_radius(h).unsqueeze(-1)
     beta = cfg["radius_anchor_beta"]
     base = beta * r_static.unsqueeze(-1) + (1.0 - beta) * dyn
+    if stats is not None:
+        stats.update(delta_mean=delta.mean().item(), delta_std=delta.std().item(),
+                     dynamic_radius_mean=dyn.mean().item(), static_radius_mean=r_static.mean().item(),
+                     base_radius_mean=base.mean().item(), anchor_beta=beta, epsilon=cfg["radius_epsilon"])
     return ops.apply_radius(h, base + delta, c)
 
 
-def hyperbolic_forward(sd, cfg, glist):
+def hyperbolic_forward(sd, cfg, glist, analysis=None):
     """HyperbolicRecurrentRGCN.forward, hyperbolic_model.py:722-890 (eval, no static
-    graph, no EST).  Returns (history_embs, h_0)."""
+    graph, no EST).  Returns (history_embs, h_0).  `analysis` (a dict, the --run-analysis
+    path): receives "gates" (each timestep's time_weight, :852-856), "time_gate_values"
+    (their means) and "evolution" (the last radius-evolution stats, hyperbolic_ops.py:426-434)."""
     c, ln = cfg["c"], cfg["layer_norm"]
     R2 = sd["emb_rel"].shape[0]
     dyn = sd["dynamic_emb"]
@@ -94,10 +101,14 @@ def hyperbolic_forward(sd, cfg, glist):
         ct = torch.clamp(ops.log0(cur, c), -10.0, 10.0)                    # :841-846
         pt = torch.clamp(ops.log0(h, c), -10.0, 10.0)
         tw = torch.sigmoid(torch.mm(pt, sd["time_gate_weight"]) + sd["time_gate_bias"])
+        if analysis is not None:
+            analysis.setdefault("gates", []).append(tw)
+            analysis.setdefault("time_gate_values", []).append(tw.mean().item())
         h = ops.project(ops.exp0(tw * ct + (1 - tw) * pt, c), c)           # :859-860
         sr = static_radius(sd, cfg)
         if cfg.get("use_residual_evolution", True):
-            h = radius_evolution(h, sr, sd, cfg)                           # :866-867
+            h = radius_evolution(h, sr, sd, cfg,
+                                 None if analysis is None else analysis.setdefault("evolution", {}))  # :866-867
         else:
             h = ops.apply_radius(h, sr, c)                                 # :869
         embs.append(h)

@@ -438,6 +438,16 @@ int regcn_timestep_f32(const float* hc, const float* x_prev, const float* w_g, c
   return timestep(a, ST(s));
 }
 
+int regcn_timestep_analysis_f32(const float* hc, const float* x_prev, const float* w_g, const float* b_g,
+                                const float* r_static, const float* w_r, const float* b_r, float eps_r, float beta,
+                                int32_t layer_norm, int32_t residual, int32_t V, int32_t d, float c, float c_radius,
+                                float* h_out, float* x_out, float* r_out, float* gate_out, float* stat_out, void* s) {
+  if (residual && !b_r) return set_error(REGCN_EINVAL, "residual radius needs b_r");
+  StepArgs a{hc, x_prev, w_g, b_g, r_static, w_r, b_r, eps_r, beta, layer_norm, residual, V, d,
+             make_curv(c), make_curv(c_radius), h_out, x_out, r_out, gate_out, stat_out};
+  return timestep(a, ST(s), true);
+}
+
 size_t regcn_packed_linear_floats(int32_t n_gates, int32_t n_out, int32_t n_in) {
   return packed_linear_floats(n_gates, n_out, n_in);
 }

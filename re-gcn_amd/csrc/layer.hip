@@ -190,6 +190,7 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(4))) void 
 }
 
 // ================================================================================ timestep
+template <bool ANA>
 __global__ __launch_bounds__(NTHR) void k_timestep(StepArgs p) {
   extern __shared__ float lds[];
   const int lda = tile_lda(p.d);
@@ -206,7 +207,7 @@ __global__ __launch_bounds__(NTHR) void k_timestep(StepArgs p) {
   __syncthreads();
   float n2[4];
   rr.sumsq(ct, n2);
-  step_epilogue(rr, ct, n2, P, lda, trow, n_valid, p);
+  step_epilogue<ANA>(rr, ct, n2, P, lda, trow, n_valid, p);
 }
 
 // ============================================================================ pack weights
@@ -279,14 +280,16 @@ int layer(const LayerArgs& a, hipStream_t st) {
   return check_launch("k_layer");
 }
 
-int timestep(const StepArgs& a, hipStream_t st) {
+int timestep(const StepArgs& a, hipStream_t st, bool analysis) {
   if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "timestep needs d %% 4 == 0, d <= 256");
   if (!a.hc || !a.x_prev || !a.w_g || !a.b_g || !a.r_static || !a.h_out) return set_error(REGCN_EINVAL, "null pointer");
   if (a.residual && (!a.w_r || !a.b_r)) return set_error(REGCN_EINVAL, "residual radius needs w_r and b_r");
+  if (analysis && !a.gate_out) return set_error(REGCN_EINVAL, "analysis needs gate_out");
   if (a.V == 0) return 0;
   const unsigned grid = (unsigned)((a.V + TM - 1) / TM);
   const size_t lds = (size_t)(TM * tile_lda(a.d) + RED_FLOATS + TM) * 4;
-  hipLaunchKernelGGL(k_timestep, dim3(grid), dim3(NTHR), lds, st, a);
+  if (analysis) hipLaunchKernelGGL(k_timestep<true>, dim3(grid), dim3(NTHR), lds, st, a);
+  else hipLaunchKernelGGL(k_timestep<false>, dim3(grid), dim3(NTHR), lds, st, a);
   return check_launch("k_timestep");
 }
 

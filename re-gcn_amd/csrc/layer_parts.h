@@ -59,6 +59,10 @@ __device__ __forceinline__ void frag_to_tile(const Frag& a, float* T, int lda, i
 // local Frag compared against null pins it in scratch memory, private null being nonzero).
 // h_out / x_out / r_out: the output rows (p's own, or per-timestep ones of a chain: passed
 // apart, since a local copy of StepArgs would live in scratch).
+// ANA (--run-analysis, k_timestep only): also the time gate per element into p.gate_out and,
+// with the residual evolution, per row {clipped delta, dynamic radius, base radius} into
+// p.stat_out[0 / V / 2V + row] (hyperbolic_model.py:852-856, hyperbolic_ops.py:426-434).
+template <bool ANA = false>
 __device__ __forceinline__ void step_epilogue_out(RowRed& rr, Frag& ct, float n2[4], const float* P, int lda,
                                                   const int* trow, int n_valid, const StepArgs& p, const Frag& tw,
                                                   float* h_out, float* x_out, float* r_out, int64_t* trace = nullptr,
@@ -78,15 +82,18 @@ __device__ __forceinline__ void step_epilogue_out(RowRed& rr, Frag& ct, float n2
   frag_from_tile(pt, P, lda, p.d);
   float bg[TPW];
   col_load(bg, p.b_g, p.d);
+  Frag gate;  // ANA only
 #pragma unroll
   for (int j = 0; j < TPW; ++j) {
     const f4 c4 = clamp4(ct.t[j], -10.f, 10.f);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float g = sigmoidf(tw.t[j][r] + bg[j]);
+      if constexpr (ANA) gate.t[j][r] = g;
       ct.t[j][r] = g * c4[r] + (1.f - g) * pt.t[j][r];
     }
   }
+  if constexpr (ANA) frag_store(gate, p.gate_out, trow, n_valid, p.d);
   rr.sumsq(ct, n2);
   exp0_known(ct, n2, p.k);
   project_known(ct, n2, p.k);  // hyperbolic_model.py:860
@@ -111,6 +118,14 @@ __device__ __forceinline__ void step_epilogue_out(RowRed& rr, Frag& ct, float n2
     const float delta = fminf(fmaxf(own_row(dl) + *p.b_r, -p.eps_r), p.eps_r);
     const float dyn = fmaxf(sqrtf(n2o), REGCN_EPS);
     newr = (p.beta * rs + (1.f - p.beta) * dyn) + delta;
+    if constexpr (ANA) {
+      if (p.stat_out && (threadIdx.x & 15) < 4 && wave_id() == 0 && ri < n_valid) {
+        const int64_t row = trow[ri];
+        p.stat_out[row] = delta;
+        p.stat_out[(int64_t)p.V + row] = dyn;
+        p.stat_out[2 * (int64_t)p.V + row] = p.beta * rs + (1.f - p.beta) * dyn;
+      }
+    }
   }
   const Curv kr = p.residual ? p.k_rad : p.k;  // by value: a pointer select would pin a local StepArgs in scratch
   float f[4];
@@ -138,6 +153,7 @@ __device__ __forceinline__ void step_epilogue_tw(RowRed& rr, Frag& ct, float n2[
 
 // The timestep epilogue computing the time-gate GEMM itself (tw_pre == nullptr) or taking the
 // caller's.
+template <bool ANA = false>
 __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4], const float* P, int lda,
                                               const int* trow, int n_valid, const StepArgs& p,
                                               int64_t* trace = nullptr, const Frag* tw_pre = nullptr) {
@@ -145,7 +161,10 @@ __device__ __forceinline__ void step_epilogue(RowRed& rr, Frag& ct, float n2[4],
   Frag tw;
   tw.zero();
   mfma_tile(tw, P, lda, p.w_g, p.d, p.d);
-  step_epilogue_tw(rr, ct, n2, P, lda, trow, n_valid, p, tw, trace);
+  if constexpr (ANA)
+    step_epilogue_out<true>(rr, ct, n2, P, lda, trow, n_valid, p, tw, p.h_out, p.x_out, p.r_out, trace);
+  else
+    step_epilogue_tw(rr, ct, n2, P, lda, trow, n_valid, p, tw, trace);
 }
 
 // Profiling hook: wall-clock phase stamps (100 MHz) of wave 0, 16 slots per workgroup.

@@ -82,6 +82,8 @@ struct StepArgs {
   float* h_out;
   float* x_out;
   float* r_out;
+  float* gate_out;  // --run-analysis (k_timestep<true>): V x d time gate
+  float* stat_out;  // 3 x V: clipped radius delta, dynamic radius, base radius (residual only)
 };
 
 // One message-passing layer: inline CSR gather + self-loop/neighbour GEMMs + epilogue,
@@ -298,7 +300,7 @@ int centroid(const float* S0, const float* Sv, int64_t V, int d, float c, float 
 int kreduce_gemm(const float* A, int a_kmajor, const float* B, int b_kmajor, int64_t K, int M, int N, const float* C0,
                  int64_t c0_ld, float* out, float* ws, hipStream_t st);
 int layer(const LayerArgs& a, hipStream_t st);
-int timestep(const StepArgs& a, hipStream_t st);
+int timestep(const StepArgs& a, hipStream_t st, bool analysis = false);
 int score(ScoreArgs& a, int mode, float* loss, hipStream_t st);
 int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st);
 // CE partial (max, sum exp) slots per query: one per candidate tile (generic kernel) or one per

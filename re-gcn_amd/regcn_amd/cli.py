@@ -288,7 +288,10 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
     if args.hip_graph and world0 > 1:
         logger.warning("--hip-graph is ignored with %d ranks: the replica step holds a gradient all-reduce "
                        "between its launches, so it runs eagerly", world0)
-    graphed = GraphedSteps(device) if args.hip_graph and world0 == 1 else None
+    if args.hip_graph and args.run_analysis:
+        logger.warning("--hip-graph is ignored with --run-analysis: the analysis statistics are produced per "
+                       "step on the host's schedule, so the steps run eagerly")
+    graphed = GraphedSteps(device) if args.hip_graph and world0 == 1 and not args.run_analysis else None
     # :469; the fused multi-tensor kernel: a handful of launches per step instead of ~100 (it
     # does not bump the parameters' version counters: bump_versions after each step)
     fused = device.type == "cuda"
@@ -313,6 +316,7 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
     best_mrr, best_epoch, patience = 0.0, 0, 20
     epoch_loss = []
     valid_history = []  # (epoch, raw MRR, filtered MRR, raw rel MRR, filtered rel MRR) per validation
+    summaries = []  # --run-analysis: get_training_summary() per epoch
     t_start = time.time()
     initial_curvature = None
     for epoch in range(args.n_epochs):
@@ -364,6 +368,8 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
                         loss.backward()
                         parts.append((le, lr, ls, lrad))
                 allreduce_gradients(model.parameters())
+                if args.run_analysis and n % 100 == 0 and hasattr(model, "log_gradient_stats"):   # :623-625
+                    model.log_gradient_stats()
                 torch.nn.utils.clip_grad_norm_(model.parameters(), args.grad_norm)          # :627-628
                 optimizer.step()
                 if fused:  # the fused step leaves the version counters the caches key on
@@ -384,6 +390,12 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
         if epoch % args.log_interval == 0:
             logger.info("Epoch %04d | Loss: %.4f | E/R/S/Rad: %.4f/%.4f/%.4f/%.4f | Best MRR: %.4f | Time: %.1fs",
                         epoch, epoch_loss[-1], me, mr, 0.0, mrad, best_mrr, time.time() - t0)
+        if args.run_analysis:                                                                # :617-621
+            logger.debug("Radius loss: %.4f", mrad)
+            if hasattr(model, "get_training_summary"):                                    # :655-657
+                summary = model.get_training_summary()
+                summaries.append(summary)
+                logger.info("Training summary: %s", summary)
         if epoch and epoch % args.evaluate_every == 0:                                      # :660-681
             stop = torch.zeros(1, device=device)
             if rank == 0:
@@ -409,7 +421,8 @@ def train_model(args, model, train_list, valid, num_nodes, num_rels, device, mod
             if float(stop) > 0:
                 break
     logger.info("Training completed in %.1f minutes", (time.time() - t_start) / 60)
-    return {"best_mrr": best_mrr, "best_epoch": best_epoch, "epoch_loss": epoch_loss, "valid": valid_history}
+    return {"best_mrr": best_mrr, "best_epoch": best_epoch, "epoch_loss": epoch_loss, "valid": valid_history,
+            "summaries": summaries}
 
 
 def main(argv=None):

@@ -23,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from . import analysis as _ana
 from .hyperbolic_decoder import (HyperbolicAttH, HyperbolicAttHRel, HyperbolicConvTransE, HyperbolicConvTransR,
                                  HyperbolicMuRP, HyperbolicMuRPRel, HyperbolicRotH, HyperbolicRotHRel,
                                  roth_pair_fusable, roth_pair_predict)
@@ -228,8 +229,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
             self.log_c = nn.Parameter(torch.tensor(math.log(c)))
         else:
             self.register_buffer("c", torch.tensor(c))
-        self.training_stats = {"embedding_norms": [], "gradient_norms": [], "loss_components": [],
-                               "time_gate_values": []}
+        self.training_stats = _ana.TrainingStats()  # device values, read on access (analysis.py)
         self.dynamic_emb = nn.Parameter(torch.Tensor(num_ents, h_dim))
         nn.init.normal_(self.dynamic_emb, std=1.0)
         self.emb_rel = nn.Parameter(torch.Tensor(num_rels * 2, h_dim))
@@ -366,6 +366,10 @@ class HyperbolicRecurrentRGCN(nn.Module):
         wg, bg, w_r, b_r = self._step_tensors()
         if self._phases_ok(g_list):
             return self._forward_phases(g_list, c_val, r_static, wg, bg, w_r, b_r)
+        ana = self.run_analysis
+        if ana and self.training:  # hyperbolic_model.py:791-792
+            _ana.log_embedding(self, h, "init_embeddings", c_val)
+        gate_list, gate_means = [], []
         for i, g in enumerate(g_list):
             g = g.to(dev)
             x_prev, _ = tangent_of(self.h, c_val)
@@ -383,14 +387,29 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 h_new = torch.empty_like(x_prev)
                 x_new = torch.empty_like(x_prev)
                 r_new = torch.empty(V, device=dev, dtype=torch.float32)
-                _lib.call("regcn_timestep_f32", _lib.fptr(current_h.contiguous(), "current_h"), _lib.fptr(x_prev),
-                          _lib.fptr(wg), _lib.fptr(bg), _lib.fptr(r_static), _lib.fptr(w_r), _lib.fptr(b_r),
-                          float(trev.epsilon), float(trev.anchor_beta), int(bool(self.layer_norm)),
-                          int(bool(self.use_residual_evolution)), V, d, c_val, float(trev.c), _lib.fptr(h_new),
-                          _lib.fptr(x_new), _lib.fptr(r_new), _lib.stream())
+                args = (_lib.fptr(current_h.contiguous(), "current_h"), _lib.fptr(x_prev), _lib.fptr(wg),
+                        _lib.fptr(bg), _lib.fptr(r_static), _lib.fptr(w_r), _lib.fptr(b_r), float(trev.epsilon),
+                        float(trev.anchor_beta), int(bool(self.layer_norm)), int(bool(self.use_residual_evolution)),
+                        V, d, c_val, float(trev.c), _lib.fptr(h_new), _lib.fptr(x_new), _lib.fptr(r_new))
+                if ana:  # the time gate and the radius terms come out of the timestep launch
+                    gate = torch.empty_like(x_prev)
+                    stat = torch.empty(3, V, device=dev, dtype=torch.float32) \
+                        if self.use_residual_evolution else None
+                    _lib.call("regcn_timestep_analysis_f32", *args, _lib.fptr(gate), _lib.fptr(stat), _lib.stream())
+                    gate_list.append(gate)                                      # :852-856
+                    gate_means.append(gate.mean())
+                    if stat is not None:                                        # hyperbolic_ops.py:426-434
+                        trev.last_evolution_stats = _ana.evolution_terms(stat[0], stat[1], stat[2], r_static,
+                                                                             trev.anchor_beta, trev.epsilon)
+                    _ana.log_timestep(i, gate_means[-1], trev.__dict__.get("_ev"))
+                else:
+                    _lib.call("regcn_timestep_f32", *args, _lib.stream())
                 self.h = attach(h_new, x_new, r_new, c_val)
             history_embs.append(self.h)
-        return history_embs, None, self.h_0, [], []
+        if ana:  # hyperbolic_model.py:887-888
+            dict.__setitem__(self.training_stats, "time_gate_values",
+                             torch.stack(gate_means) if gate_means else [])
+        return history_embs, None, self.h_0, gate_list, []
 
     def _initial_state(self, c_val, r_static):
         """(h, x, r) of the initial entity state (hyperbolic_model.py:775-782): a function of
@@ -748,6 +767,8 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 # (queries + candidates + all_triples, then both scores in one launch)
                 evolve_embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
                 embedding = self._final_embedding(evolve_embs[-1], c_val)
+                if self.run_analysis:  # hyperbolic_model.py:932-933
+                    _ana.log_embedding(self, embedding, "predict_embeddings", c_val)
                 return roth_pair_predict(self.decoder_ob, self.rdecoder, embedding, r_emb, test_triplets, num_rels)
             # the query triples do not depend on the encoder: on a HIP device they are built on
             # the side stream while the encoder runs (joined in _decode_both)
@@ -767,6 +788,8 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 torch.cuda.current_stream(dev).wait_event(built)
                 all_triples.record_stream(torch.cuda.current_stream(dev))
             embedding = self._final_embedding(evolve_embs[-1], c_val)
+            if self.run_analysis:  # hyperbolic_model.py:932-933
+                _ana.log_embedding(self, embedding, "predict_embeddings", c_val)
             at = all_triples.to(embedding.device)
             score, score_rel = self._decode_both(embedding, r_emb, at)
             return all_triples, score, score_rel
@@ -859,7 +882,10 @@ class HyperbolicRecurrentRGCN(nn.Module):
         self.rdecoder.c = c_val
         evolve_embs, static_emb, r_emb, _, _ = self.forward(glist, static_graph, use_cuda)
         pre_emb = self._final_embedding(evolve_embs[-1], c_val)
-        return self._decode_losses(pre_emb, r_emb, triples, c_val)
+        losses = self._decode_losses(pre_emb, r_emb, triples, c_val)
+        if self.run_analysis:  # hyperbolic_model.py:1076-1086
+            _ana.record_losses(self, *losses)
+        return losses
 
     def get_loss_batches(self, glist, triples, static_graph, use_cuda, batch_size, query_time=None,
                          combine=None, group_budget=1 << 28):
@@ -905,6 +931,9 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 if total.requires_grad:
                     total.backward()
             parts.extend(tuple(t.detach() for t in losses) for losses in per_batch)
+            if self.run_analysis:  # one loss-components entry per mini-batch (hyperbolic_model.py:1076-1086)
+                for losses in per_batch:
+                    _ana.record_losses(self, *losses)
         roots = [(src, leaf.grad) for src, leaf in zip(srcs, cut)
                  if src.requires_grad and leaf.grad is not None]
         if roots:
@@ -966,5 +995,10 @@ class HyperbolicRecurrentRGCN(nn.Module):
             loss_radius = self.radius_lambda * (seen @ (diff * diff)) / seen.sum(1)
         return loss_ent, loss_rel, loss_static, loss_radius
 
+    def log_gradient_stats(self):
+        """hyperbolic_model.py:1090-1108 (the total gradient norm, kept on the device)."""
+        return _ana.gradient_stats(self)
+
     def get_training_summary(self):
-        return {"curvature": float(self.get_curvature())}
+        """hyperbolic_model.py:1110-1127."""
+        return _ana.training_summary(self)

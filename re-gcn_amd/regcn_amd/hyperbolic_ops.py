@@ -131,6 +131,15 @@ class HyperbolicOps:
         return _rowmap("regcn_ln_roundtrip_f32", x, c).view(x.shape)
 
     @staticmethod
+    def log_embedding_stats(x, name="embeddings", c=0.01):
+        """hyperbolic_ops.py:235-269: norm statistics of `x` as a host dict (the reference's own
+        return value; one device read).  The model keeps them on the device instead
+        (analysis.log_embedding)."""
+        from .analysis import embedding_dict, embedding_stats
+        with torch.no_grad():
+            return embedding_dict(embedding_stats(HyperbolicOps.get_radius(x), _cf(c)), name, _cf(c))
+
+    @staticmethod
     def sumsq(x):
         x2, d = _rows(x)
         out = torch.empty(x2.shape[0], device=x.device, dtype=torch.float32)
@@ -199,12 +208,27 @@ class TemporalRadiusEvolution(nn.Module):
         nn.init.zeros_(self.radius_mlp.bias)
         self.last_evolution_stats = None
 
+    # The statistics of the last evolution (hyperbolic_ops.py:426-434) are kept as one device
+    # vector (analysis.evolution_terms) and read on the host when looked at.
+    @property
+    def last_evolution_stats(self):
+        from .analysis import evolution_dict
+        return evolution_dict(self.__dict__.get("_ev"))
+
+    @last_evolution_stats.setter
+    def last_evolution_stats(self, ev):
+        self.__dict__["_ev"] = ev
+
     def forward(self, x, static_radius):
+        from .analysis import evolution_terms
         t = HyperbolicOps.log_map_zero(x, self.c)
         delta = torch.clamp(self.radius_mlp(t).squeeze(-1), -self.epsilon, self.epsilon)
         dyn = HyperbolicOps.get_radius(x)
-        base = dyn if static_radius is None else self.anchor_beta * static_radius + (1.0 - self.anchor_beta) * dyn
+        st = dyn if static_radius is None else static_radius
+        base = self.anchor_beta * st + (1.0 - self.anchor_beta) * dyn
+        self.last_evolution_stats = evolution_terms(delta, dyn, base, st, self.anchor_beta, self.epsilon)
         return HyperbolicOps.apply_radius(x, base + delta, self.c)
 
     def get_evolution_stats(self):
+        """hyperbolic_ops.py:437-439 (a host dict; one device read)."""
         return self.last_evolution_stats

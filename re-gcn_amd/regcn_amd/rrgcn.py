@@ -42,6 +42,8 @@ class RGCNCell(BaseRGCN):
         if self.encoder_name != "uvrgcn":
             raise NotImplementedError
         sc = (idx != 0) if self.skip_connect else False
+        if self.run_analysis:  # src/rrgcn.py:19-20
+            print("activate function: {}".format(F.rrelu))
         return UnionRGCNLayer(self.h_dim, self.h_dim, self.num_rels, self.num_bases, activation=F.rrelu,
                               dropout=self.dropout, self_loop=self.self_loop, skip_connect=sc, rel_emb=self.rel_emb)
 

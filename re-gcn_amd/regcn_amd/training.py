@@ -16,6 +16,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _lib
+from . import analysis
 from . import autograd as A
 
 RRELU_SLOPE = (1.0 / 8 + 1.0 / 3) / 2  # F.rrelu(x) with training=False (hyperbolic_model.py:120)
@@ -171,7 +172,10 @@ def model_forward(model, g_list):
     h = A.apply_radius(h, r_static, c)                                                 # :782
     trev = model.temporal_radius_evolution
     lorentz = model.encoder_name == "lgcn"
-    history, h0 = [], None
+    ana = model.run_analysis
+    if ana and model.training:                                                         # :791-792
+        analysis.log_embedding(model, h, "init_embeddings", c)
+    history, h0, gate_list, gate_means = [], None, [], []
     for i, g in enumerate(g_list):
         g = g.to(dev)
         x_prev = A.log0(h, ct)                                                         # :802
@@ -185,17 +189,30 @@ def model_forward(model, g_list):
             cur = A.exp0(F.normalize(A.log0(cur, ct)), ct)                            # :832-835
         pt = torch.clamp(x_prev, -10.0, 10.0)                                          # :841-846
         z = A.mm_weight(pt, model.time_gate_weight)                                    # tw = sigmoid(z + b)
+        if ana:                                                                        # :852-856
+            with torch.no_grad():
+                gate_list.append(torch.sigmoid(z.detach() + model.time_gate_bias.detach()))
+                gate_means.append(gate_list[-1].mean())
         mix = A.tail(A.log0(cur, ct), z=z, bias=model.time_gate_bias, p=pt, flags=A.TAIL_CLAMP_IN)
         h = A.project(A.exp0(mix, ct), c)                                              # :859-860
         if model.use_residual_evolution:
             t = A.log0(h, trev.c)                                                      # hyperbolic_ops.py:395-435
             delta = torch.clamp(A.linear(trev.radius_mlp, t).squeeze(-1), -trev.epsilon, trev.epsilon)
-            base = trev.anchor_beta * r_static + (1.0 - trev.anchor_beta) * A.get_radius(h)
+            dyn = A.get_radius(h)
+            base = trev.anchor_beta * r_static + (1.0 - trev.anchor_beta) * dyn
             h = A.apply_radius(h, base + delta, trev.c)
+            if ana:  # TemporalRadiusEvolution's stats of this evolution (hyperbolic_ops.py:426-434)
+                with torch.no_grad():
+                    trev.last_evolution_stats = analysis.evolution_terms(
+                        delta.detach(), dyn.detach(), base.detach(), r_static.detach(), trev.anchor_beta, trev.epsilon)
         else:
             h = A.apply_radius(h, r_static, c)                                         # :869
+        if ana:
+            analysis.log_timestep(i, gate_means[-1], trev.__dict__.get("_ev"))
         history.append(h)
-    return history, None, h0, [], []
+    if ana:                                                                            # :887-888
+        dict.__setitem__(model.training_stats, "time_gate_values", torch.stack(gate_means) if gate_means else [])
+    return history, None, h0, gate_list, []
 
 
 def euclid_layer(layer, g, h, rel):

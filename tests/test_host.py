@@ -2,6 +2,7 @@
 indexing), work-list invariants, and that the C-ABI library loads and exports every
 symbol include/regcn_hip.h declares (no compute call: there is no GPU here)."""
 import ctypes
+import math
 import os
 import re
 
@@ -273,3 +274,37 @@ def test_relation_entity_block_lists(block, chunk):
             out[r] = part[b:e].sum(0) / lens[r]
     ref = np.stack([x[l].mean(0) if len(l) else np.zeros(5) for l in lists])
     np.testing.assert_allclose(out, ref, rtol=1e-12, atol=1e-12)
+
+
+def test_analysis_containers_on_host():
+    """--run-analysis bookkeeping (regcn_amd/analysis.py) without a GPU: training_stats keeps the
+    reference's keys and reads device-kept values as python numbers; the radius evolution's
+    stats and the embedding stats are computed from per-row vectors like the reference's."""
+    import torch
+    from regcn_amd import analysis as A
+    from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
+    m = HyperbolicRecurrentRGCN("roth", "hyperbolic_uvrgcn", 16, 4, 0, 0, 8, "sub", 3, num_bases=4,
+                                num_hidden_layers=2, analysis=True)
+    assert set(m.training_stats) == {"embedding_norms", "gradient_norms", "loss_components", "time_gate_values"}
+    A.record_losses(m, torch.tensor([1.5]), torch.tensor([0.25]), torch.zeros(1), torch.tensor(0.125))
+    assert m.training_stats["loss_components"] == [{"loss_ent": 1.5, "loss_rel": 0.25, "loss_static": 0.0,
+                                                    "loss_radius": 0.125}]
+    dict.__setitem__(m.training_stats, "time_gate_values", torch.tensor([0.25, 0.75]))
+    assert m.training_stats["time_gate_values"] == [0.25, 0.75]
+    delta, dyn, st = torch.tensor([0.1, -0.1, 0.05]), torch.tensor([1.0, 2.0, 3.0]), torch.tensor([2.0, 2.0, 2.0])
+    base = 0.5 * st + 0.5 * dyn
+    m.temporal_radius_evolution.last_evolution_stats = A.evolution_terms(delta, dyn, base, st, 0.5, 0.1)
+    ev = m.temporal_radius_evolution.get_evolution_stats()
+    assert abs(ev["delta_std"] - float(delta.std())) < 1e-7 and ev["base_radius_mean"] == 2.0
+    s = m.get_training_summary()
+    assert list(s) == ["curvature", "radius_delta_mean", "radius_delta_std", "dynamic_radius_mean",
+                       "static_radius_mean", "base_radius_mean", "anchor_beta", "avg_time_gate"]
+    assert abs(s["avg_time_gate"] - 0.5) < 1e-12 and abs(s["curvature"] - 0.01) < 1e-9
+    r = torch.tensor([1.0, 9.5, 3.0])
+    e = A.embedding_dict(A.embedding_stats(r, 0.01), "x", 0.01)
+    assert abs(e["pct_near_boundary"] - 100.0 / 3) < 1e-4 and e["max_norm"] == 9.5
+    for p in m.parameters():
+        p.grad = torch.ones_like(p)
+    gn = m.log_gradient_stats()
+    assert abs(float(gn) - math.sqrt(sum(p.numel() for p in m.parameters()))) < 1e-3
+    assert len(m.training_stats["gradient_norms"]) == 1

@@ -252,3 +252,44 @@ def test_oracle_euclid_training_grads_vs_reference(golden, tag):
             assert err <= 1e-3, "%s: %.3g" % (k, err)
             n += 1
     assert n >= 15
+
+
+ANALYSIS_CASES = {
+    "uvrgcn_roth_beta": dict(encoder="hyperbolic_uvrgcn", decoder="roth", layer_norm=False, radius_anchor_beta=0.5),
+    "lgcn_roth_ln": dict(encoder="lgcn", decoder="roth", layer_norm=True),
+    "uvrgcn_murp_nores": dict(encoder="hyperbolic_uvrgcn", decoder="murp", layer_norm=False,
+                              use_residual_evolution=False),
+}
+_BUFFERS = ("c", "radius_target")
+
+
+@pytest.mark.parametrize("tag", list(ANALYSIS_CASES))
+def test_oracle_analysis_vs_reference(golden, tag):
+    """N1 pin (--run-analysis): the oracle's time gates, their means and the last radius-evolution
+    stats of the eval forward, and the total gradient norm of one mini-batch (log_gradient_stats
+    over the parameters that get a gradient) equal the reference's (analysis_*.npz)."""
+    z = golden("analysis_%s.npz" % tag)
+    V, R, d, T = (int(v) for v in z["meta"])
+    cfg = dict(c=C, n_layers=2, n_bases=d // 2, radius_min=0.5, radius_max=3.0, radius_epsilon=0.1,
+               radius_anchor_beta=1.0, radius_msg_gamma=0.15, use_residual_evolution=True)
+    cfg.update(ANALYSIS_CASES[tag])
+    sd = {k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("sd_")}
+    glist = [og.build_sub_graph(V, R, z["snap%d" % t]) for t in range(T)]
+    ana = {}
+    om.hyperbolic_forward(sd, cfg, glist, analysis=ana)
+    close(torch.stack(ana["gates"]), z["eval_gates"])
+    close(ana["time_gate_values"], z["eval_time_gate_values"])
+    if z["eval_evolution"].size:
+        ev = ana["evolution"]
+        close([ev[k] for k in ("delta_mean", "delta_std", "dynamic_radius_mean", "static_radius_mean",
+                               "base_radius_mean", "anchor_beta")], z["eval_evolution"])
+    else:
+        assert "evolution" not in ana
+    sd64 = {k: (v.double().requires_grad_(k not in _BUFFERS and "running" not in k) if v.dtype == torch.float32
+                else v) for k, v in sd.items()}
+    le, lr, ls, lrad = om.hyperbolic_get_loss(sd64, cfg, glist, torch.from_numpy(z["batch"]), z["radius_target"])
+    close([float(le), float(lr), 0.0, float(lrad)], z["loss_components"], 1e-5)
+    tw = float(z["task_weight"])
+    (tw * le + (1 - tw) * lr + ls.sum() + lrad).backward()
+    norms = [float(v.grad.norm()) for v in sd64.values() if torch.is_tensor(v) and v.grad is not None]
+    np.testing.assert_allclose(float(np.sqrt(np.sum(np.square(norms)))), float(z["grad_norm"]), rtol=1e-4)

@@ -23,6 +23,10 @@ Each fixture pins one row of SURVEY.md §8(a):
                            (the --multi-step history roll)   rgcn/utils.py:51-75, 367-405;
                                                              hyperbolic_main.py:116-149
   train_*.npz          f1  get_loss + backward: every parameter gradient   hyperbolic_main.py:585-598
+  analysis_*.npz       N1  --run-analysis: gate_list, time-gate means, radius-evolution stats,
+                           embedding stats, loss components, gradient norm, training summary
+                                                             hyperbolic_model.py:747-890, :1076-1127;
+                                                             hyperbolic_ops.py:235-269, :426-439
   tkg_tiny/ + dataset_tiny.npz  f4  load_from_local + split_by_time on a dataset directory
                                                              knowledge_graph.py:189-206, 526-555;
                                                              rgcn/utils.py:306-339
@@ -661,6 +665,96 @@ def gen_dataset():
     save("dataset_tiny.npz", **out)
 
 
+ANALYSIS_CASES = [
+    ("uvrgcn_roth_beta", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="roth", layer_norm=False,
+                              radius_anchor_beta=0.5)),
+    ("lgcn_roth_ln", dict(encoder_name="lgcn", decoder_name="roth", layer_norm=True)),
+    ("uvrgcn_murp_nores", dict(encoder_name="hyperbolic_uvrgcn", decoder_name="murp", layer_norm=False,
+                               use_residual_evolution=False)),
+]
+SUMMARY_KEYS = ("curvature", "radius_delta_mean", "radius_delta_std", "dynamic_radius_mean", "static_radius_mean",
+                "base_radius_mean", "anchor_beta", "avg_time_gate")
+EVO_KEYS = ("delta_mean", "delta_std", "dynamic_radius_mean", "static_radius_mean", "base_radius_mean",
+            "anchor_beta")
+EMB_KEYS = ("mean_norm", "max_norm", "min_norm", "std_norm", "max_allowed", "pct_near_boundary")
+
+
+def gen_analysis():
+    """--run-analysis (analysis=True): the eval forward's gate_list and time-gate means, the
+    radius-evolution stats, the predict embeddings' stats (log_embedding_stats, captured), then
+    one training mini-batch (dropout 0): the init embeddings' stats, the loss components, the
+    total gradient norm of log_gradient_stats and get_training_summary."""
+    from hyperbolic_src import hyperbolic_model as hm
+    V, R, T, d, tw = 256, 64, 3, 64, 0.7
+    snaps = snapshot_series(60, V, R, T + 1, 120)
+    rng = np.random.default_rng(61)
+    radius_target = rng.uniform(0.5, 3.0, size=V).astype(np.float32)
+    glist = [rutils.build_sub_graph(V, R, s, False, "cpu") for s in snaps[:T]]
+    batch = torch.from_numpy(snaps[T])
+    logged = {}
+    orig = HyperbolicOps.log_embedding_stats
+
+    def capture(x, name="embeddings", c=0.01):
+        logged[name] = orig(x, name, c)
+        return logged[name]
+
+    for i, (tag, kw) in enumerate(ANALYSIS_CASES):
+        torch.manual_seed(600 + i)
+        base = dict(num_ents=V, num_rels=R, num_static_rels=0, num_words=0, h_dim=d, opn="sub",
+                    sequence_len=T, num_bases=d // 2, num_hidden_layers=2, dropout=0.0, c=C,
+                    self_loop=True, skip_connect=False, input_dropout=0.0, hidden_dropout=0.0,
+                    feat_dropout=0.0, entity_prediction=True, relation_prediction=True,
+                    use_cuda=False, gpu="cpu", radius_target=radius_target, radius_msg_gamma=0.15,
+                    analysis=True)
+        base.update(kw)
+        m = HyperbolicRecurrentRGCN(**base)
+        with torch.no_grad():
+            for mod in (m.decoder_ob, m.rdecoder):
+                if hasattr(mod, "score_margin"):
+                    mod.score_margin.fill_(0.7)
+                    mod.score_scale_raw.fill_(0.4)
+            m.radius_static.add_(torch.randn(V) * 0.2)
+            m.time_gate_bias.normal_(0, 0.5)  # gates away from one value
+        sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        out = {"meta": np.array([V, R, d, T]), "batch": snaps[T], "radius_target": radius_target,
+               "task_weight": np.array(tw)}
+        for t in range(T):
+            out["snap%d" % t] = snaps[t]
+        for k, v in sd.items():
+            out["sd_" + k] = v.numpy().copy()
+        logged.clear()
+        hm.HyperbolicOps.log_embedding_stats = staticmethod(capture)
+        try:
+            m.eval()
+            with torch.no_grad():
+                _, _, _, gate_list, degree_list = m.forward(glist, None, False)
+                out["eval_gates"] = torch.stack(gate_list).numpy()
+                out["eval_time_gate_values"] = np.array(m.training_stats["time_gate_values"])
+                ev = m.temporal_radius_evolution.get_evolution_stats()
+                out["eval_evolution"] = np.array([ev[k] for k in EVO_KEYS] if ev else [])
+                m.predict(glist, R, None, batch.clone(), False)
+            out["predict_emb_stats"] = np.array([logged["predict_embeddings"][k] for k in EMB_KEYS])
+            m.train()
+            for mod in m.modules():
+                if isinstance(mod, torch.nn.BatchNorm1d):
+                    mod.eval()
+            m.zero_grad()
+            le, lr, ls, lrad = m.get_loss(glist, batch.clone(), None, False)
+            (tw * le + (1 - tw) * lr + ls + lrad).backward()
+            out["init_emb_stats"] = np.array([logged["init_embeddings"][k] for k in EMB_KEYS])
+        finally:
+            hm.HyperbolicOps.log_embedding_stats = staticmethod(orig)
+        lc = m.training_stats["loss_components"][-1]
+        out["loss_components"] = np.array([lc[k] for k in ("loss_ent", "loss_rel", "loss_static", "loss_radius")])
+        out["grad_norm"] = np.array(m.log_gradient_stats())
+        out["train_time_gate_values"] = np.array(m.training_stats["time_gate_values"])
+        summ = m.get_training_summary()
+        out["summary_keys"] = np.array([k for k in SUMMARY_KEYS if k in summ])
+        out["summary"] = np.array([float(summ[k]) for k in SUMMARY_KEYS if k in summ])
+        assert set(summ) <= set(SUMMARY_KEYS), summ
+        save("analysis_%s.npz" % tag, **out)
+
+
 def gen_multistep():
     """get_total_rank filters `score` in place; --multi-step builds the next history
     snapshot from those filtered scores (hyperbolic_main.py:116-149)."""
@@ -692,6 +786,6 @@ if __name__ == "__main__":
              "euclid": gen_layer_euclid, "lorentz": gen_layer_lorentz, "models": gen_models,
              "rrgcn": gen_rrgcn, "score": gen_score, "rank": gen_rank, "train": gen_train,
              "models_large": gen_models_large, "dataset": gen_dataset, "train_curvature": gen_train_curvature,
-             "multistep": gen_multistep}
+             "multistep": gen_multistep, "analysis": gen_analysis}
     for w in which:
         table[w]()
