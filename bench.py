@@ -16,7 +16,16 @@ fragment packing); the snapshot graphs are built once, in HBM, before the timed 
 metric = million directed message edges aggregated per second (edges after inverse
 doubling x GCN layers x history snapshots = 300M per step), whole job:
 K steps timed exactly, between barriers + device synchronisation, max over ranks.
-Multi-GPU: one process per GPU; each rank runs its own windows (replicas, weak scaling).
+Multi-GPU: one process per GPU.  At config 5 with --gpus > 1 the default is the owner
+partition (SURVEY.md §8(e) partitioning 2, strong scaling): the entity ids are relabelled so
+each rank's rows carry an equal share of the edges (parallel.EntityRelabel), every rank runs
+its rows of every layer and all-gathers their tangent rows and radii (804 B per row) on a
+side stream while its next row chunk computes, the relation means are partitioned (one
+all_reduce of R x d), and the step ends in the candidate-sharded decoder (predict_ranks: each
+rank scores its own rows as candidates, one all_reduce of the 2B rank counts).  The replica
+mode (independent windows per rank, weak scaling) rides along as the `replicas` key.  At N = 1
+the line carries `owner_simulation`: the 8 ranks' launches run one after another on the one
+GPU, each rank's device time measured, plus the replicated work and the exchange volume.
 
 Per-call device times come from HIP events recorded on the launching stream after every
 library call during the timed steps (`_lib.EVENT_TRACE`); `roofline` reports the call
@@ -87,10 +96,13 @@ def parse(argv=None):
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work")
     ap.add_argument("--no-scale", action="store_true",
                     help="skip the config-5 aggregation and decoder rooflines (N=1 only)")
-    ap.add_argument("--shard", default="replica", choices=["replica", "edge", "owner"],
+    ap.add_argument("--shard", default="auto", choices=["auto", "replica", "edge", "owner"],
                     help="multi-GPU: independent samples per rank (weak scaling), or every snapshot "
                          "partitioned across the ranks by edges (all-reduce) / destination owner "
-                         "(all-gather) (strong scaling, SURVEY.md §8(e))")
+                         "(all-gather) (strong scaling, SURVEY.md §8(e)); auto: owner at config 5 with "
+                         "--gpus > 1 (+ a replica leg), replica for the dataset configs")
+    ap.add_argument("--sim-ranks", type=int, default=8,
+                    help="config 5 at N = 1: ranks of the one-GPU owner-partition simulation (0: skip)")
     a = ap.parse_args(argv)
     if a.per_layer:
         a.encoder_launches = "layers"
@@ -393,6 +405,7 @@ def cpu_baseline(cfg, d, model, sample, budget):
     from oracle import model as OM
     hist, glist, _, test_np = sample
     V, R = cfg["V"], cfg["R"]
+    torch.set_num_threads(cpu_threads())
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     ocfg = dict(c=0.01, n_layers=2, n_bases=cfg["n_bases"], radius_min=0.5, radius_max=3.0, radius_epsilon=0.1,
                 radius_anchor_beta=1.0, radius_msg_gamma=0.15, use_residual_evolution=True, layer_norm=False,
@@ -473,6 +486,18 @@ def _timed(world, device, backend, run, edges_local):
     return elapsed, float(edges_local)
 
 
+def cpu_threads():
+    """Threads for the CPU baseline: every core this process may use.  On the GPU box one
+    GPU's job gets a share of the host (the harness sets OMP_NUM_THREADS to it, 16 per GPU)
+    while os.cpu_count() reports the whole machine, which the other GPUs' jobs share."""
+    share = os.environ.get("OMP_NUM_THREADS")
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    return max(1, min(aff, int(share))) if share and share.isdigit() else aff
+
+
 def cpu_info():
     """Host CPU model and the threads the CPU baseline used (lscpu model
     and core count)."""
@@ -485,7 +510,9 @@ def cpu_info():
                     break
     except OSError:
         pass
-    return {"cpu_model": model, "host_logical_cpus": os.cpu_count()}
+    return {"cpu_model": model, "host_logical_cpus": os.cpu_count(),
+            "threads_note": "cores = the CPU share this process is given (OMP_NUM_THREADS / affinity); the "
+                            "host's logical CPUs serve all of its GPUs' jobs"}
 
 
 # ------------------------------------------------------------------------- dataset configs
@@ -777,7 +804,7 @@ def cpu_baseline_scale(cfg, d, budget):
     from oracle import graph as OG
     from oracle import model as OM
     from regcn_amd.synthetic import snapshot_series
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    torch.set_num_threads(cpu_threads())
     V, R = cfg["V"], cfg["R"]
     triples = 2_500_000
     snap = snapshot_series(7, V, R, 1, triples)[0]
@@ -806,12 +833,130 @@ def cpu_baseline_scale(cfg, d, budget):
                        % (len(times), V, 2 * triples, 2 * R, d, edges, per), **cpu_info())
 
 
+def prepare_snapshot(V, R, triples, device, prep=None):
+    """One config-5 snapshot in HBM with every list a predict reads (graph build on the device,
+    then the row/type and row/source orders, inline items in source order, the entity-block
+    relation and hub lists -- otherwise built lazily by the first predict); `prep` collects
+    the build and list times in ms (synchronised)."""
+    from regcn_amd import graph as G
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    g = G.build_sub_graph(V, R, triples, True, device)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    g.row_type_cols()
+    g.row_src_cols()
+    if g.use_item_src_runs():
+        g.item_src_cols()
+    G.rel_block_work(g, R)
+    G.hub_block_work(g)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    if prep is not None:
+        prep.append((1e3 * (t1 - t0), 1e3 * (t2 - t1)))
+    return g
+
+
+def owner_simulation(args, cfg, device, world):
+    """The config-5 owner partition for `world` GPUs, simulated on this one:
+    entity ids relabelled for equal edge loads (EntityRelabel.balanced), every snapshot a
+    parallel.RankSimulation, so each layer runs rank 0's chunk launches, then rank 1's, ...
+    (each rank's device time from HIP events around its launches), the relation means sum the
+    ranks' partials, and the decoder scores each rank's own rows as its candidates.  Reports
+    the per-rank device ms per step, the replicated ms (what every rank runs: initial state,
+    relation GRU, queries, target scores, relation decoder), the all-gather volume, and the
+    step a rank would take with the exchange hidden under its compute."""
+    from regcn_amd.graph import hub_block_work  # noqa: F401
+    from regcn_amd.parallel import CandidateShard, EntityRelabel, RankSimulation
+    from regcn_amd.synthetic import snapshot_series
+    d, T, V, R = args.d, cfg["T"], cfg["V"], cfg["R"]
+    snaps = snapshot_series(100, V, R, T + 1, cfg["per_snap"])
+    rl = EntityRelabel.balanced(snaps[:T], V, world)
+    loads = rl.loads(snaps[:T], world)
+    loads_plain = EntityRelabel(np.arange(V)).loads(snaps[:T], world)
+    snaps = [rl.triples(x) for x in snaps]
+    t0 = time.time()
+    sims = [RankSimulation(prepare_snapshot(V, R, x, device), world) for x in snaps[:T]]
+    setup_s = time.time() - t0
+    test = torch.from_numpy(np.ascontiguousarray(snaps[T][:args.queries // 2])).to(device)
+    del snaps
+    model = build_model(cfg, d, device, seed=1234)
+    rl.model(model)
+    model.memo_pristine = model.param_caches = False
+    dec = model.decoder_ob
+    lay = sims[-1].layout
+    shards = [CandidateShard(V, k, world, None, ranges=lay.ranges(k)) for k in range(world)]
+    kw = dict(scale=dec.score_scale_raw, margin=dec.score_margin, raw_scale=True)
+    dec_times = [[] for _ in range(world)]
+
+    def step():
+        embs, _, r_emb, _, _ = model.forward(sims, None, True)
+        inv = test.flip(1)
+        inv[:, 1] = inv[:, 1] + R
+        at = torch.cat([test, inv])
+        emb = embs[-1]
+        q = dec._query(emb, r_emb, at)
+        ts = shards[0].target_scores(q, emb, None, at[:, 2], dec.c, **kw)
+        for k, sh in enumerate(shards):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            sh.range_ranks(q, emb, None, dec.c, ts, **kw)
+            b.record()
+            dec_times[k].append((a, b))
+        model.rdecoder.forward(emb, r_emb, at, mode="test")
+
+    reps = 3
+    with torch.no_grad():
+        step()
+        torch.cuda.synchronize()
+        for sm in sims:
+            sm.times = [[] for _ in range(world)]
+        for k in range(world):
+            dec_times[k].clear()
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record()
+        for _ in range(reps):
+            step()
+        end.record()
+        torch.cuda.synchronize()
+    total = start.elapsed_time(end) / reps
+    enc = np.sum([sm.per_rank_ms() for sm in sims], axis=0) / reps
+    dec_ms = np.array([sum(a.elapsed_time(b) for a, b in t) for t in dec_times]) / reps
+    per_rank = enc + dec_ms
+    replicated = total - float(per_rank.sum())
+    layers = 2 * T
+    xbytes = (world - 1) * lay.cr * lay.chunks * (d + 1) * 4  # received per rank per layer
+    link_gbs, links = 153.0, world - 1  # xGMI: 7 links x ~153 GB/s per MI355X (SURVEY.md §5)
+    xchg_ms = xbytes / (links * link_gbs * 1e9) * 1e3
+    edges = 2 * sum(sm.number_of_edges() for sm in sims)
+    pred = float(per_rank.max()) + replicated
+    return {
+        "world": world, "chunks_per_rank": lay.chunks, "rows_per_chunk": lay.cr,
+        "per_rank_ms": [round(float(x), 3) for x in per_rank],
+        "per_rank_encoder_ms": [round(float(x), 3) for x in enc],
+        "per_rank_decoder_ms": [round(float(x), 3) for x in dec_ms],
+        "max_rank_ms": round(float(per_rank.max()), 3), "mean_rank_ms": round(float(per_rank.mean()), 3),
+        "replicated_ms": round(replicated, 3), "single_gpu_equivalent_ms": round(total, 3),
+        "exchange_bytes_per_layer_per_rank": int(xbytes), "exchange_gb_per_step_per_rank": round(xbytes * layers / 1e9, 3),
+        "exchange_ms_per_layer_at_7_links": round(xchg_ms, 3),
+        "edge_loads_per_rank": loads, "edge_loads_contiguous_ids": loads_plain,
+        "predicted_step_ms": round(pred, 3),
+        "predicted_M_edges_per_s": round(edges / pred / 1e3, 1),
+        "predicted_speedup_vs_this_run": round(total / pred, 2),
+        "setup_s": round(setup_s, 1),
+        "note": "ranks run one after another on one MI355X (parallel.RankSimulation); per-rank = device time "
+                "of its own launches (layer chunks incl. hub pass, relation-mean partials, its candidate "
+                "slice); replicated = the rest of the step; predicted step = max rank + replicated, with the "
+                "all-gathers (exchange_ms_per_layer, nominal link rate) hidden under the next chunk's compute",
+    }
+
+
 def run_scale(args, cfg, world, rank, device, backend):
     """Config 5 headline (see the module docstring)."""
     from regcn_amd import _lib
     from regcn_amd import graph as G
     from regcn_amd.synthetic import snapshot_series
-    from regcn_amd.parallel import ShardedGraph
+    from regcn_amd.parallel import EntityRelabel, ShardedGraph
     d, T, V, R = args.d, cfg["T"], cfg["V"], cfg["R"]
     n_win = args.pool or 2
     t_setup = time.time()
@@ -819,7 +964,13 @@ def run_scale(args, cfg, world, rank, device, backend):
     # processes its partition of each (strong scaling)
     sharded = args.shard != "replica" and world > 1
     snaps = snapshot_series(100 if sharded else 100 + 7919 * rank, V, R, T + n_win, cfg["per_snap"])
-    graphs = [G.build_sub_graph(V, R, s, True, device) for s in snaps[:T + n_win - 1]]
+    relabel = None
+    if sharded and args.shard == "owner":  # equal edge loads per rank (parallel.EntityRelabel)
+        relabel = EntityRelabel.balanced(snaps[:T + n_win - 1], V, world)
+        snaps = [relabel.triples(s) for s in snaps]
+    graphs, prep = [], []
+    for s in snaps[:T + n_win - 1]:
+        graphs.append(prepare_snapshot(V, R, s, device, prep))
     if sharded:
         graphs = [ShardedGraph(g, args.shard) for g in graphs]
     tests = [torch.from_numpy(np.ascontiguousarray(snaps[T + i][:args.queries // 2])).to(device)
@@ -827,6 +978,8 @@ def run_scale(args, cfg, world, rank, device, backend):
     del snaps
     windows = [graphs[i:i + T] for i in range(n_win)]
     model = build_model(cfg, d, device, seed=1234)
+    if relabel is not None:
+        relabel.model(model)
     model.use_phases = args.encoder_launches == "phases"
     model.memo_pristine = model.param_caches = False  # every step computes everything
     B = 2 * tests[0].shape[0]
@@ -834,6 +987,8 @@ def run_scale(args, cfg, world, rank, device, backend):
     def step(k):
         i = k % n_win
         _lib.trace_mark("__step__")
+        if sharded:  # the candidate-sharded decoder: every rank ranks its own candidates
+            return model.predict_ranks(windows[i], R, None, tests[i], True)
         return model.predict(windows[i], R, None, tests[i], True)
 
     with torch.no_grad():
@@ -886,6 +1041,16 @@ def run_scale(args, cfg, world, rank, device, backend):
         if traffic:
             roof["traffic_GBps"] = round(traffic / (calls[dom]["ms"] * 1e-3) / 1e9, 1)
             roof["traffic_frac"] = round(roof["traffic_GBps"] / HBM_PEAK_GBS, 4)
+        if dom.startswith("regcn_layer_f32") and not sharded:
+            # SURVEY.md §8(d)'s count alone: 812 B per unit (gathered row + col_src + col_type +
+            # radius per edge; row write + rowptr + norm + radius per node) x the launch's units
+            # (its inline in-edges + every row); `achieved` above adds the timestep's row I/O
+            units = stats["items"] + V
+            b8 = units * (4.0 * d + 12)
+            roof["s8d_bytes_per_launch"] = b8
+            roof["s8d_units_per_launch"] = units
+            roof["s8d_achieved_GBps"] = round(b8 / (calls[dom]["ms"] * 1e-3) / 1e9, 1)
+            roof["s8d_frac"] = round(roof["s8d_achieved_GBps"] / HBM_PEAK_GBS, 4)
         ms = elapsed / args.steps * 1e3
         enc_ms = sum(v["ms"] * v["per_step"] for k, v in calls.items()
                      if k not in ("regcn_hyp_score_jobs_f32", "regcn_roth_queries_f32"))
@@ -911,7 +1076,17 @@ def run_scale(args, cfg, world, rank, device, backend):
                              "decoder_ms_per_step": round(sum(calls[k]["ms"] * calls[k]["per_step"] for k in calls
                                                               if k in ("regcn_hyp_score_jobs_f32",
                                                                        "regcn_roth_queries_f32")), 3),
+                             "encoder_M_edges_per_s_note": "with Zipf(1.1) sources the hub rows' gathered "
+                                 "rows are L2 / MALL hits (830 rows hold ~65 % of the edges): this rate is cache "
+                                 "reuse on top of HBM streaming; the HBM figure is aggregation_roofline.uniform_src "
+                                 "(fabric traffic with uniformly spread sources)",
                              "setup_s": round(setup_s, 1),
+                             "snapshot_prep_ms": {
+                                 "graph_build": round(float(np.mean([p[0] for p in prep])), 1),
+                                 "lists": round(float(np.mean([p[1] for p in prep])), 1),
+                                 "note": "per snapshot, once (cached for every predict that reads it): the device "
+                                         "CSR / r2e / tile build, then the row/type and row/source orders, inline "
+                                         "items in source order and the entity-block relation and hub lists"},
                              "note": "per-call device time from HIP events recorded after each library call on "
                                      "the launching stream during the timed steps"}}
     del windows, graphs, tests, model, trace
@@ -925,10 +1100,22 @@ def main():
     world, rank, device, backend = _ctx()
     from regcn_amd.synthetic import CONFIGS
     cfg = CONFIGS[args.config]
+    if args.shard == "auto":
+        args.shard = "owner" if cfg.get("scale") and world > 1 else "replica"
     if args.encoder_launches == "auto":
         args.encoder_launches = "layers" if cfg.get("scale") else "phases"
     if cfg.get("scale"):
         out = run_scale(args, cfg, world, rank, device, backend)
+        if world > 1 and args.shard != "replica" and not args.no_extras:
+            # the replica mode beside the partitioned headline (independent windows per rank)
+            rep_args = parse(["--shard", "replica", "--steps", str(max(4, args.steps // 2)), "--warmup", "1",
+                              "--no-extras"])
+            r = run_scale(rep_args, cfg, world, rank, device, backend)
+            if rank == 0:
+                out["replicas"] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps", "scaling")}
+                out["replicas"]["parallelism"] = r["config"]["parallelism"]
+        if rank == 0 and world == 1 and args.sim_ranks > 1 and not args.no_extras:
+            out["owner_simulation"] = owner_simulation(args, cfg, device, args.sim_ranks)
         if rank == 0 and world == 1:
             if not args.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline_scale(cfg, args.d, args.cpu_budget)

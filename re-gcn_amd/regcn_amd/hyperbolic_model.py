@@ -86,6 +86,8 @@ def relation_context(x, g, num_rels2):
     work lists chunk the forward relations' spans only: r2e gives an inverse id r + R the
     same entity list as r, in the same order (rgcn/utils.py:88-89), so its mean is the
     same sum of the same rows, copied instead of recomputed (half the row gathers)."""
+    if getattr(g, "partition", None) == "owner" and g.world > 1:  # partitioned pairs (parallel.py)
+        return g.relation_means(x, num_rels2)
     wk = g.work()
     V, d = x.shape
     R = num_rels2 // 2
@@ -766,7 +768,10 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 # one stream end to end: encoder, then the two-launch RotH/RotHRel front
                 # (queries + candidates + all_triples, then both scores in one launch)
                 evolve_embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
-                embedding = self._final_embedding(evolve_embs[-1], c_val)
+                last = evolve_embs[-1]
+                if getattr(last, "_regcn_owner", None) is not None:  # owner partition: rank-local rows
+                    last._regcn_owner[0].complete_rows(last)
+                embedding = self._final_embedding(last, c_val)
                 if self.run_analysis:  # hyperbolic_model.py:932-933
                     _ana.log_embedding(self, embedding, "predict_embeddings", c_val)
                 return roth_pair_predict(self.decoder_ob, self.rdecoder, embedding, r_emb, test_triplets, num_rels)
@@ -787,7 +792,10 @@ class HyperbolicRecurrentRGCN(nn.Module):
             if side is not None:
                 torch.cuda.current_stream(dev).wait_event(built)
                 all_triples.record_stream(torch.cuda.current_stream(dev))
-            embedding = self._final_embedding(evolve_embs[-1], c_val)
+            last = evolve_embs[-1]
+            if getattr(last, "_regcn_owner", None) is not None:  # owner partition: rank-local rows
+                last._regcn_owner[0].complete_rows(last)
+            embedding = self._final_embedding(last, c_val)
             if self.run_analysis:  # hyperbolic_model.py:932-933
                 _ana.log_embedding(self, embedding, "predict_embeddings", c_val)
             at = all_triples.to(embedding.device)
@@ -817,26 +825,35 @@ class HyperbolicRecurrentRGCN(nn.Module):
         if not hasattr(dec, "_query") or dec.use_relation_specific_curvature:
             raise NotImplementedError("candidate-sharded ranking needs a MuRP / RotH / AttH decoder with the proxy "
                                       "distance score")
-        sg = sharded[0]
+        sg = sharded[-1]
         with torch.no_grad():
             c_val = self._c_float()
             embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
-            emb = self._final_embedding(embs[-1], c_val).contiguous()
             inv = test_triplets.flip(1)
             inv[:, 1] = inv[:, 1] + num_rels
             at = torch.cat([test_triplets, inv])
+            last = embs[-1]
+            if getattr(last, "_regcn_owner", None) is not None:
+                # owner partition: every rank holds its own rows of the last state; the queries'
+                # subjects / objects come from their owners (one all_reduce of 2B x d rows)
+                sg.fetch_rows(last, test_triplets[:, [0, 2]].reshape(-1))
+            emb = self._final_embedding(last, c_val).contiguous()
             q = dec._query(emb, r_emb, at)
-            shard = CandidateShard(emb.shape[0], sg.rank, sg.world, sg.group)
+            N = emb.shape[0]
+            shard = CandidateShard(N, sg.rank, sg.world, sg.group, ranges=sg.candidate_ranges(N))
             kw = dict(scale=dec.score_scale_raw, margin=dec.score_margin, raw_scale=True)
             # the candidates' entity_bias[n] as in the full scoring; the decoder's extra
             # entity_bias[s] shifts a whole query row alike, so the ranks do not see it
             bias = dec.entity_bias.detach() if dec.entity_bias is not None else None
-            local = shard.scores(q, emb, bias, dec.c, **kw)
             ts = shard.target_scores(q, emb, bias, at[:, 2], dec.c, **kw)
-            fp, fi = ranking._filter_csr(at, all_ans, False)
-            r_e, f_e = shard.ranks(local, ts, fp, fi)
+            # without answer lists (a benchmark step) no host round trip: raw ranks only
+            fp, fi = ranking._filter_csr(at, all_ans, False) if all_ans is not None else (None, None)
+            r_e, f_e = shard.range_ranks(q, emb, bias, dec.c, ts, fp, fi, **kw)
             score_rel = self.rdecoder.forward(emb, r_emb, at, mode="test")
-            r_r, f_r = ranking.get_total_rank(at, score_rel, all_ans_r, 1000, 1)[2:]
+            if all_ans_r is None:
+                r_r = f_r = ranking.ranks(score_rel, at[:, 1])[0]
+            else:
+                r_r, f_r = ranking.get_total_rank(at, score_rel, all_ans_r, 1000, 1)[2:]
         return at, (r_e, f_e), (r_r, f_r)
 
     def _side(self, dev, k=1):

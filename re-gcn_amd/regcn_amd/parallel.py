@@ -7,9 +7,18 @@ Two partitionings of a message-passing layer over `world` ranks:
   sums (union: sum_e w_e (x_src + rel); Lorentz: the summed Lorentz points plus their
   time coordinate); one ``all_reduce(SUM)`` of the V x (d + 1) partials; every rank
   finishes the rows (norm / centroid -> log0) and runs the MFMA tail on all rows.
-* ``"owner"`` — rank k owns the k-th contiguous block of ceil(V / world) destination nodes
-  and runs the fused layer kernel on them only (gather + GEMMs + epilogue, rank-local);
-  an ``all_gather`` of the owned rows of (h, log0 h, |h|) rebuilds the full state.
+* ``"owner"`` — rank k owns a set of destination nodes (OwnerLayout: `chunks` groups of
+  contiguous ids per rank, chunk-major so that chunk j of every rank is one contiguous id
+  range) and runs the fused layer kernel on them only (gather + GEMMs + epilogue,
+  rank-local).  The next layer reads only the tangent rows x = log0 h and the radii |h|, so
+  after each chunk's launch ONE in-place ``all_gather`` per array (804 B per row) rebuilds x
+  and |h| on every rank, on a side stream while the next chunk computes; the Poincare rows h
+  stay rank-local (the decoder fetches the rows it needs, `fetch_rows`, and scores each
+  rank's own rows as its candidates, CandidateShard).  The relation-context means are
+  partitioned the same way (per-rank partial sums over owned entities, one all_reduce of
+  R x d).  Which node goes to which rank is a relabelling of the entity ids
+  (`EntityRelabel.balanced`): LPT on the per-entity in-degrees, so the ranks carry equal
+  edge loads under power-law skew (partitioning 2).
 
 `ShardedGraph` wraps a `SnapshotGraph` with one of the two; the HIP layers dispatch on it,
 so `HyperbolicRecurrentRGCN.forward(g_list=[ShardedGraph, ...])` runs sharded.  The
@@ -71,17 +80,46 @@ def owner_bounds(V, world):
     return per, [min(V, per * k) for k in range(world + 1)]
 
 
+def owner_chunks(V, world):
+    """Pipeline chunks per rank of the owner partition (auto): 4 from 64k rows per rank."""
+    return 4 if world > 1 and -(-V // world) >= 65536 else 1
+
+
+class OwnerLayout:
+    """Node ids of the owner partition: [0, Vp) in chunks x world groups of cr ids; group
+    g = j * world + k, ids [g cr, (g + 1) cr) clipped to V, is rank k's pipeline chunk j.
+    Chunk j of all ranks is the contiguous range [j world cr, (j + 1) world cr), so its
+    all_gather lands in place (no pack / unpack).  One chunk: rank k owns [k cr, (k + 1) cr).
+    Arrays exchanged this way are Vp rows long (rows >= V are padding nobody reads)."""
+
+    def __init__(self, V, world, chunks=1):
+        self.V, self.world, self.chunks = int(V), int(world), int(chunks)
+        self.cr = max(1, -(-self.V // (self.world * self.chunks)))
+        self.Vp = self.cr * self.world * self.chunks
+
+    def group(self, rank, j):
+        a = (j * self.world + rank) * self.cr
+        return min(a, self.V), min(a + self.cr, self.V)
+
+    def ranges(self, rank):
+        return [self.group(rank, j) for j in range(self.chunks)]
+
+    def owner(self, ids):
+        return (ids // self.cr) % self.world
+
+    def sizes(self):
+        """Rows per group, g = j * world + k."""
+        return [self.group(g % self.world, g // self.world) for g in range(self.world * self.chunks)]
+
+
 class OwnerView:
     """A rank's view of a snapshot under the owner partition: the global CSR and relation
-    spans, and the fused-kernel work lists of its node block only (or of rows [r0, r1) of
-    that block: a pipeline chunk, see ShardedGraph)."""
+    spans, and the fused-kernel work lists of the node ids [lo, hi) only (one pipeline
+    chunk of the rank's rows, see ShardedGraph)."""
 
-    def __init__(self, g, rank, world, r0=0, r1=None):
+    def __init__(self, g, lo, hi):
         self.g = g
-        self.per, b = owner_bounds(g.number_of_nodes(), world)
-        v0, v1 = b[rank], b[rank + 1]
-        self.v0 = min(v1, v0 + r0)
-        self.v1 = v1 if r1 is None else min(v1, v0 + r1)
+        self.v0, self.v1 = int(lo), int(hi)
         h = g._host
         fw = fused_work(np.arange(self.v0, self.v1), g.in_deg_np, h["rowptr"].astype(np.int64),
                         h["col_src"].astype(np.int64), h["col_type"].astype(np.int64), g.budget, g.pack_items,
@@ -104,6 +142,129 @@ class OwnerView:
             wk.update({k: torch.from_numpy(v).to(dev) for k, v in self.fw.host.items()})
             self._dev = wk
         return self._dev
+
+
+# ------------------------------------------------------------- balanced entity relabel
+def _lpt(load, caps, head=None):
+    """Group (0 .. len(caps) - 1) of every item: longest-processing-time first -- items by
+    descending load, each to the least-loaded group with room (caps[g] items) -- for the
+    `head` heaviest items; the light tail dealt round-robin, heaviest first, over the groups
+    in ascending load order, each up to its room.  sum(caps) == len(load)."""
+    import heapq
+    load = np.asarray(load, dtype=np.float64)
+    caps = np.asarray(caps, dtype=np.int64)
+    n, G = len(load), len(caps)
+    if int(caps.sum()) != n:
+        raise ValueError("group capacities must sum to the item count")
+    order = np.argsort(-load, kind="stable")
+    out = np.empty(n, dtype=np.int64)
+    cnt = np.zeros(G, dtype=np.int64)
+    tot = np.zeros(G)
+    K = min(n, head if head is not None else 4096 * G)
+    heap = [(0.0, g) for g in range(G) if caps[g] > 0]
+    heapq.heapify(heap)
+    for i in order[:K]:
+        lo, g = heapq.heappop(heap)
+        out[i] = g
+        cnt[g] += 1
+        tot[g] = lo + load[i]
+        if cnt[g] < caps[g]:
+            heapq.heappush(heap, (tot[g], g))
+    rest = order[K:]
+    if len(rest):
+        room = caps - cnt
+        pos = np.empty(G, dtype=np.int64)
+        pos[np.argsort(tot, kind="stable")] = np.arange(G)
+        g_rep = np.repeat(np.arange(G), room)
+        r_idx = np.arange(len(g_rep)) - np.repeat(np.cumsum(room) - room, room)
+        out[rest] = g_rep[np.argsort(r_idx * G + pos[g_rep], kind="stable")]
+    return out
+
+
+class EntityRelabel:
+    """A permutation of the entity ids (old id -> new id) that balances the owner partition:
+    the model is equivariant under it (entity-indexed parameters permuted alike, the triples
+    relabelled), so every MRR is unchanged while rank k's rows -- the ids OwnerLayout gives it
+    -- carry ~1/world of the edges under power-law skew (a Zipf(1.1) hub holds ~9 % of a
+    snapshot's edges; equal contiguous id blocks leave the hubs wherever the ids put them)."""
+
+    ENTITY_TENSORS = ("dynamic_emb", "radius_static", "radius_target", "decoder_ob.entity_bias")
+
+    def __init__(self, perm):
+        self.perm = np.asarray(perm, dtype=np.int64)
+        self.inv = np.empty_like(self.perm)
+        self.inv[self.perm] = np.arange(len(self.perm))
+        self._dev = {}
+
+    @classmethod
+    def balanced(cls, snapshots, V, world, chunks=None):
+        """LPT over the entities' in-degrees in the doubled snapshot graphs (one per subject and
+        object occurrence, rgcn/utils.py:116-118) summed over `snapshots` (triple arrays): first
+        to ranks (equal row counts), then inside each rank to its pipeline chunks."""
+        chunks = chunks or owner_chunks(V, world)
+        lay = OwnerLayout(V, world, chunks)
+        deg = np.zeros(V, dtype=np.float64)
+        for tr in snapshots:
+            tr = np.asarray(tr)
+            deg += np.bincount(tr[:, 0], minlength=V) + np.bincount(tr[:, 2], minlength=V)
+        size = np.array([hi - lo for lo, hi in lay.sizes()], dtype=np.int64)  # g = j * world + k
+        rank_cap = size.reshape(chunks, world).sum(0)
+        rank_of = _lpt(deg, rank_cap)
+        perm = np.empty(V, dtype=np.int64)
+        for k in range(world):
+            mine = np.nonzero(rank_of == k)[0]
+            caps = size.reshape(chunks, world)[:, k]
+            chunk_of = _lpt(deg[mine], caps) if chunks > 1 else np.zeros(len(mine), np.int64)
+            for j in range(chunks):
+                rows = mine[chunk_of == j]  # ascending old ids
+                lo, _ = lay.group(k, j)
+                perm[rows] = lo + np.arange(len(rows))
+        return cls(perm)
+
+    def loads(self, snapshots, world, chunks=None):
+        """Per-rank directed in-edges of each snapshot under this relabel ([n_snap][world])."""
+        V = len(self.perm)
+        lay = OwnerLayout(V, world, chunks or owner_chunks(V, world))
+        out = []
+        for tr in snapshots:
+            tr = np.asarray(tr)
+            own = lay.owner(self.perm[np.concatenate([tr[:, 0], tr[:, 2]])])
+            out.append(np.bincount(own, minlength=world).tolist())
+        return out
+
+    def _t(self, which, device):
+        key = (which, str(device))
+        if key not in self._dev:
+            self._dev[key] = torch.from_numpy(getattr(self, which)).to(device)
+        return self._dev[key]
+
+    def triples(self, tr):
+        """(s, r, o) rows with s and o relabelled (numpy or torch, a copy)."""
+        if torch.is_tensor(tr):
+            p = self._t("perm", tr.device)
+            out = tr.clone()
+            out[:, 0] = p[tr[:, 0].long()].to(tr.dtype)
+            out[:, 2] = p[tr[:, 2].long()].to(tr.dtype)
+            return out
+        tr = np.asarray(tr)
+        out = tr.copy()
+        out[:, 0] = self.perm[tr[:, 0]]
+        out[:, 2] = self.perm[tr[:, 2]]
+        return out
+
+    def model(self, m):
+        """Permute the entity-indexed parameters / buffers of a model in place (new row
+        perm[i] = old row i); in-place writes bump the version counters the caches key on."""
+        names = dict(m.named_parameters())
+        names.update(dict(m.named_buffers()))
+        with torch.no_grad():
+            for n in self.ENTITY_TENSORS:
+                t = names.get(n)
+                if t is not None:
+                    t.copy_(t[self._t("inv", t.device)])
+        from .weights import invalidate
+        invalidate(m)
+        return m
 
 
 # -------------------------------------------------------------------------- collectives
@@ -157,6 +318,25 @@ def allgather_fused(tensors, per, rows=None, group=None):
 
 
 # ---------------------------------------------------------------------- sharded layers
+def owned_rel_spans(rel_idx, rel_count, ranges, Vp):
+    """The forward relations' r_to_e spans (consecutive in rel_idx, relation r holding
+    rel_count[r] entries, ascending entity ids) cut to the entity id ranges [lo, hi): span
+    r * len(ranges) + q holds relation r's entities in range q.  Returns (rows, beg, len)
+    tensors (span row = r * n_ranges + q) on rel_idx's device."""
+    dev = rel_idx.device
+    cnt = rel_count.long()
+    R, nq = int(cnt.numel()), len(ranges)
+    ids = rel_idx[:int(cnt.sum())].long()
+    Vk = int(Vp) + 1  # key = relation * Vk + id ascends over the whole forward list
+    key = torch.repeat_interleave(torch.arange(R, device=dev), cnt) * Vk + ids
+    lo = torch.tensor([a for a, _ in ranges], device=dev, dtype=torch.long).repeat(R)
+    hi = torch.tensor([b for _, b in ranges], device=dev, dtype=torch.long).repeat(R)
+    rr = torch.arange(R, device=dev).repeat_interleave(nq)
+    beg = torch.searchsorted(key, rr * Vk + lo)
+    end = torch.searchsorted(key, rr * Vk + hi)
+    return torch.arange(R * nq, device=dev), beg, end - beg
+
+
 class ShardedGraph:
     """A SnapshotGraph partitioned across the ranks of `group` (see module docstring).
     Everything but the message-passing layers (relation spans, degrees, ...) is the
@@ -175,16 +355,20 @@ class ShardedGraph:
         if world is None:
             world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank, self.world = rank, world
+        self.chunks = chunks
         self.plan = EdgePlan(g, rank, world).to(g.device) if partition == "edge" else None
-        self.view = OwnerView(g, rank, world) if partition == "owner" else None
-        self.views = []
+        self.layout, self.views = None, []
         if partition == "owner":
-            per = self.view.per
-            k = chunks or self.pipeline_chunks or (4 if per >= 65536 and world > 1 else 1)
-            cr = -(-per // k)
-            self.views = [(slice(j * cr, min(per, (j + 1) * cr)), OwnerView(g, rank, world, j * cr, (j + 1) * cr))
-                          for j in range(k) if j * cr < per] if k > 1 else [(slice(0, per), self.view)]
+            V = g.number_of_nodes()
+            k = chunks or self.pipeline_chunks or owner_chunks(V, world)
+            self.layout = OwnerLayout(V, world, k)
+            self.views = [((lo, hi), OwnerView(g, lo, hi)) for lo, hi in self.layout.ranges(rank)]
         self._comm = None
+        self._rel = None
+        # collectives only inside a process group of world > 1 (a single-process simulation of
+        # one rank, bench.py's owner_simulation, runs the rank's launches alone)
+        self.collective = dist.is_initialized() and dist.get_world_size(group) > 1
+        self.exchanged_bytes = 0  # bytes this rank received in the owner all-gathers (bench)
 
     def __getattr__(self, name):  # delegate the DGL-visible surface and work lists
         return getattr(self.__dict__["g"], name)
@@ -196,7 +380,15 @@ class ShardedGraph:
         device = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
         if device == self.g.device:
             return self
-        return ShardedGraph(self.g.to(device), self.partition, self.group, self.rank, self.world)
+        return ShardedGraph(self.g.to(device), self.partition, self.group, self.rank, self.world, self.chunks)
+
+    def candidate_ranges(self, N):
+        """The entity ids this rank scores as candidates: its own rows (owner partition: the
+        rows whose Poincare embedding it computed), an even slice otherwise."""
+        if self.partition == "owner" and self.layout.V == N:
+            return [r for r in self.layout.ranges(self.rank) if r[1] > r[0]]
+        b = even_bounds(N, self.world)
+        return [(b[self.rank], b[self.rank + 1])]
 
     # ---- edge partition pieces (also used by the single-GPU rank simulation in tests)
     def edge_partials(self, mode, x, r, rel, w_rel, nb, gamma, c):
@@ -258,34 +450,173 @@ class ShardedGraph:
             agg = self.edge_finish(mode, P, x, r, rel, w_rel, nb, gamma, c)
             return run_layer(_lib.AGG_NONE, self.g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t,
                              w_skip, b_skip, drop_mask, c, euclid=euclid, step=step, agg=agg)
-        per = self.view.per
-        Vp = per * self.world
-        h = torch.empty(Vp, d, device=x.device, dtype=torch.float32)
-        xn = torch.empty(Vp, d, device=x.device, dtype=torch.float32)
-        rn = torch.empty(Vp, device=x.device, dtype=torch.float32)
-        # the rank's rows in pipeline chunks: chunk j's rows (h | log0 h | |h|) are all-gathered
-        # in ONE collective on a side stream while chunk j + 1 computes (SURVEY.md §8(e):
-        # partitioning 2 with overlap)
+        lay = self.layout
+        W, cr = self.world, lay.cr
+        h = torch.empty(lay.Vp, d, device=x.device, dtype=torch.float32)
+        xn = torch.empty(lay.Vp, d, device=x.device, dtype=torch.float32)
+        rn = torch.empty(lay.Vp, device=x.device, dtype=torch.float32)
+        # the rank's rows in pipeline chunks: after chunk j's launch, chunk j of every rank --
+        # one contiguous id range -- is all-gathered in place, x and |h| (804 B per row), on a
+        # side stream while chunk j + 1 computes (partitioning 2 with overlap)
         cur = torch.cuda.current_stream(x.device) if x.is_cuda else None
         comm = None
-        if cur is not None and len(self.views) > 1 and self.world > 1:
+        if cur is not None and len(self.views) > 1 and W > 1:
             if self._comm is None:
                 self._comm = torch.cuda.Stream(x.device)
             comm = self._comm
-        for rows, view in self.views:
+        for j, (_, view) in enumerate(self.views):
             run_layer(mode, view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
                       drop_mask, c, euclid=euclid, step=step, out=(h[:V], xn[:V], rn[:V]))
+            if W == 1:
+                continue
+            a, b, k = j * W * cr, (j + 1) * W * cr, (j * W + self.rank) * cr
+            self.exchanged_bytes += (W - 1) * cr * (d + 1) * 4
+            if not self.collective:
+                continue
             if comm is None:
-                allgather_fused((h, xn, rn), per, rows, self.group)
+                _all_gather_into(xn[a:b], xn[k:k + cr], self.group)
+                _all_gather_into(rn[a:b], rn[k:k + cr], self.group)
                 continue
             comm.wait_stream(cur)
             with torch.cuda.stream(comm):
-                allgather_fused((h, xn, rn), per, rows, self.group)
+                _all_gather_into(xn[a:b], xn[k:k + cr], self.group)
+                _all_gather_into(rn[a:b], rn[k:k + cr], self.group)
         if comm is not None:
             cur.wait_stream(comm)
-            for t in (h, xn, rn):
+            for t in (xn, rn):
                 t.record_stream(comm)
+        hv = h[:V]
+        if self.collective:  # only this rank's rows of h are computed (complete_rows / fetch_rows)
+            hv._regcn_owner = (self, h)
+        return hv, xn[:V], rn[:V]
+
+    # ---- owner partition: the rows other ranks computed, when a consumer needs them
+    def relation_means(self, x, R2):
+        """Relation-context means (hyperbolic_model.relation_context) with the pairs
+        partitioned like the rows: this rank sums the x rows of its own entities in every
+        forward relation's r_to_e span (one sub-span per pipeline chunk), ONE all_reduce of the
+        R x d sums, then / count; inverse relations copy their forward row."""
+        R = R2 // 2
+        V, d = x.shape
+        wk = self.g.work()
+        if self._rel is None:
+            self._rel = self._relation_lists(R)
+        ch, fx, ns, nq = self._rel
+        out = torch.zeros(R * nq, d, device=x.device, dtype=torch.float32)
+        part = torch.empty(max(ns, 1), d, device=x.device, dtype=torch.float32)
+        ones = torch.ones(R * nq, device=x.device, dtype=torch.float32)
+        _lib.call("regcn_segment_mean_f32", _lib.fptr(x, "x"), _lib.iptr(wk["rel_idx"]), _lib.fptr(ones),
+                  _lib.iptr(ch), ch.shape[0], _lib.iptr(fx), fx.shape[0], d, _lib.fptr(part), d, _lib.fptr(out),
+                  _lib.stream())
+        sums = out.view(R, nq, d).sum(1) if nq > 1 else out
+        if self.collective:
+            allreduce_partials(sums, self.group)
+        mean = torch.zeros(R2, d, device=x.device, dtype=torch.float32)
+        cnt = wk["rel_count"][:R].clamp(min=1.0).unsqueeze(1)
+        torch.div(sums, cnt, out=mean[:R])
+        mean[R:].copy_(mean[:R])
+        return mean
+
+    def _relation_lists(self, R):
+        """(chunks, fixups, n_slots, n_ranges): every forward relation's r_to_e span cut to this
+        rank's id ranges (span rows r * n_ranges + q), then at entity blocks and every 256
+        pairs (graph.blocked_span_chunks)."""
+        from .graph import REL_BLOCK, REL_BLOCK_CHUNK, blocked_span_chunks
+        wk = self.g.work()
+        dev = wk["rel_idx"].device
+        ranges = self.layout.ranges(self.rank)
+        rows, beg, ln = owned_rel_spans(wk["rel_idx"], wk["rel_count"][:R], ranges, self.layout.Vp)
+        ch, fx, ns = blocked_span_chunks(rows, beg, ln, wk["rel_idx"], max(REL_BLOCK, 1), REL_BLOCK_CHUNK)
+        _lib.publish()
+        return ch, torch.from_numpy(fx).to(dev), ns, len(ranges)
+
+    def fetch_rows(self, h, ids):
+        """Make h[ids] valid on every rank (owner partition: each id's row lives on its
+        owner): the owners' rows in one all_reduce of len(ids) x d (exact: every entry is
+        one rank's value plus zeros), written into h."""
+        meta = getattr(h, "_regcn_owner", None)
+        if meta is None:
+            return h
+        ids = ids.to(h.device).long()
+        mine = self.layout.owner(ids) == self.rank
+        buf = torch.zeros(ids.numel(), h.shape[1], device=h.device, dtype=h.dtype)
+        buf[mine] = h[ids[mine]]
+        allreduce_partials(buf, self.group)
+        h[ids] = buf
+        return h
+
+    def complete_rows(self, h):
+        """All rows of a rank-local h on every rank (the full-score predict): the pipeline
+        chunks' in-place all-gathers of h."""
+        meta = getattr(h, "_regcn_owner", None)
+        if meta is None:
+            return h
+        full = meta[1]
+        W, cr = self.world, self.layout.cr
+        for j in range(self.layout.chunks):
+            a, b, k = j * W * cr, (j + 1) * W * cr, (j * W + self.rank) * cr
+            _all_gather_into(full[a:b], full[k:k + cr], self.group)
+        del h._regcn_owner
+        return h
+
+
+def complete(h):
+    """h with every row valid on every rank: a rank-local state of the owner partition (the
+    Poincare rows only its own launches wrote) is all-gathered in place; anything else is
+    returned as is."""
+    meta = getattr(h, "_regcn_owner", None)
+    return meta[0].complete_rows(h) if meta is not None else h
+
+
+class RankSimulation(ShardedGraph):
+    """All `world` ranks of the owner partition run one after another on ONE device, for
+    measurement (bench.py owner_simulation): every layer runs rank 0's chunk launches, then
+    rank 1's, ... into the same output arrays (so the next layer reads valid rows, as after
+    the all-gathers), each rank's launches bracketed by HIP events; the relation means sum the
+    ranks' partials.  `times[k]` collects rank k's (start, end) event pairs; what a step spends
+    outside them is the work every rank repeats (replicated)."""
+
+    def __init__(self, g, world, chunks=None):
+        super().__init__(g, "owner", None, 0, world, chunks)
+        self.ranks = [self] + [ShardedGraph(g, "owner", None, k, world, chunks) for k in range(1, world)]
+        for r in self.ranks:
+            r.collective = False
+        self.times = [[] for _ in range(world)]
+
+    def _timed(self, k, fn):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = fn()
+        b.record()
+        self.times[k].append((a, b))
+        return out
+
+    def run_layer(self, mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
+                  drop_mask, c, euclid=False, step=None):
+        from .hyperbolic_layers import run_layer
+        V, d = x.shape
+        lay = self.layout
+        h = torch.empty(lay.Vp, d, device=x.device, dtype=torch.float32)
+        xn = torch.empty(lay.Vp, d, device=x.device, dtype=torch.float32)
+        rn = torch.empty(lay.Vp, device=x.device, dtype=torch.float32)
+
+        def rank_launches(sg):
+            for _, view in sg.views:
+                run_layer(mode, view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
+                          drop_mask, c, euclid=euclid, step=step, out=(h[:V], xn[:V], rn[:V]))
+        for k, sg in enumerate(self.ranks):
+            self._timed(k, lambda: rank_launches(sg))
+            sg.exchanged_bytes += (self.world - 1) * lay.cr * lay.chunks * (d + 1) * 4
         return h[:V], xn[:V], rn[:V]
+
+    def relation_means(self, x, R2):
+        means = [self._timed(k, lambda: ShardedGraph.relation_means(sg, x, R2)) for k, sg in enumerate(self.ranks)]
+        cnt = self.g.work()["rel_count"].clamp(min=1.0).unsqueeze(1)
+        tot = sum(m * cnt for m in means)  # each rank's sums (mean x count), added as the all_reduce would
+        return tot / cnt
+
+    def per_rank_ms(self):
+        return [sum(a.elapsed_time(b) for a, b in t) for t in self.times]
 
 
 # ------------------------------------------------------------------- sharded decoder
@@ -321,18 +652,19 @@ def shard_filters(filt_ptr, filt_idx, n0, n1):
 class CandidateShard:
     """Rank `rank`'s contiguous slice [n0, n1) of the N all-entity candidates (SURVEY.md §8(e):
     the decoder shards its candidates; the cross entropy and the ranks need only B-sized
-    exchanges).  Every rank holds the full candidate rows (the owner partition all-gathers
-    them), scores its slice with the HIP scorer and combines:
+    exchanges), or the id `ranges` it owns (owner partition: the rows it computed).  It
+    scores its candidates with the HIP scorer and combines:
       * cross entropy: per-slice log-sum-exp (regcn_hyp_ce_lse_f32 on the slice) -> combine_lse;
         the target logit is the pair score of (q_b, e_{t_b}) computed on every rank;
       * ranks: the target's score as threshold, per-slice count-greater with the slice-local
         filter list (regcn_rank_count_f32) -> combine_counts, + 1.
     With group=None the collectives are skipped (a single-process simulation of one rank)."""
 
-    def __init__(self, N, rank, world, group=None):
+    def __init__(self, N, rank, world, group=None, ranges=None):
         b = even_bounds(N, world)
         self.N, self.rank, self.world, self.group = N, rank, world, group
         self.n0, self.n1 = b[rank], b[rank + 1]
+        self.ranges = ranges if ranges is not None else [(self.n0, self.n1)]
 
     def _slice(self, cand, bias):
         c = cand[self.n0:self.n1].contiguous()
@@ -401,6 +733,20 @@ class CandidateShard:
         both = torch.stack([raw, flt if flt is not None else raw])
         both = combine_counts(both, self.group)
         return both[0].long() + 1, both[1].long() + 1
+
+    def range_ranks(self, q, cand, bias, c, ts, filt_ptr=None, filt_idx=None, **kw):
+        """ranks() over every id range of this shard (one scorer launch and one count launch
+        per range, the counts summed), then ONE all_reduce of the 2B counts."""
+        tot = None
+        for n0, n1 in self.ranges:
+            self.n0, self.n1 = n0, n1
+            raw, flt = self.local_counts(self.scores(q, cand, bias, c, **kw), ts, filt_ptr, filt_idx)
+            both = torch.stack([raw, flt if flt is not None else raw])
+            tot = both if tot is None else tot + both
+        if tot is None:
+            tot = torch.zeros(2, q.shape[0], device=q.device, dtype=torch.int32)
+        tot = combine_counts(tot, self.group)
+        return tot[0].long() + 1, tot[1].long() + 1
 
 
 # ------------------------------------------------------------------ training replicas

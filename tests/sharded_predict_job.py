@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(HERE), "re-gcn_amd"))
 def main(out_path, tag):
     from gpu_helpers import build_hyperbolic_model
     from regcn_amd import ranking
-    from regcn_amd.parallel import ShardedGraph
+    from regcn_amd.parallel import ShardedGraph, complete
     dist.init_process_group(os.environ.get("REGCN_DIST_BACKEND", "gloo"))
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = torch.device("cuda", 0)
@@ -38,6 +38,7 @@ def main(out_path, tag):
             for chunks in ((1, 3) if part == "owner" else (1,)):
                 sg = [ShardedGraph(g, part, chunks=chunks) for g in glist]
                 e2, _, h02, _, _ = m.forward(sg, None, True)
+                complete(e2[-1])  # owner partition: the other ranks' rows of the last state
                 _, (re2, fe2), (rr2, fr2) = m.predict_ranks(sg, R, None, test, True, ans, ans_r)
                 # the candidate-sharded decoder alone, on the unsharded encoder outputs: the
                 # same ranks bit for bit (the partitions sum rows in another order, so the

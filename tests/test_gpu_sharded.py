@@ -71,3 +71,36 @@ def test_cli_sharded_evaluation_world2():
     for got in found:
         for a, b in zip((float(v) for v in got), single):
             assert abs(a - b) <= 0.002, (got, single)
+
+
+@pytest.mark.parametrize("tag,world,chunks", [("uvrgcn_roth_r512_d200", 8, 2), ("lgcn_roth_h7_d200", 3, 1),
+                                              ("uvrgcn_roth_e80k_d200", 4, 3)])
+def test_rank_simulation_matches_unsharded(golden, tag, world, chunks):
+    """The owner partition's per-rank work, all ranks run one after another on the GPU
+    (parallel.RankSimulation, bench.py's owner_simulation): each rank's chunk views of every
+    layer and its partial relation means, combined, give the unsharded history embeddings
+    (1e-4 * max(1, |ref|)) and relation states; a balanced relabel of the entities
+    (EntityRelabel) changes nothing but the row order."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import numpy as np
+    from gpu_helpers import assert_close, build_hyperbolic_model
+    from regcn_amd import graph as G
+    from regcn_amd.parallel import EntityRelabel, RankSimulation
+    dev = torch.device("cuda", 0)
+    z = golden("model_%s.npz" % tag)
+    m, glist, (V, R, d, T) = build_hyperbolic_model(z, tag, dev)
+    with torch.no_grad():
+        embs, _, h0, _, _ = m.forward(glist, None, True)
+        ref = embs[-1].clone()
+        sims = [RankSimulation(g, world, chunks) for g in glist]
+        e2, _, h02, _, _ = m.forward(sims, None, True)
+        assert_close(e2[-1], ref, what="simulated ranks")
+        assert_close(h02, h0, 1e-5, "relation state")
+        assert all(len(t) for sm in sims for t in sm.times)
+        snaps = [z["snap%d" % t] for t in range(T)]
+        rl = EntityRelabel.balanced(snaps, V, world, chunks)
+        rl.model(m)
+        gl = [G.build_sub_graph(V, R, rl.triples(s).astype(np.int64), True, dev) for s in snaps]
+        e3 = m.forward([RankSimulation(g, world, chunks) for g in gl], None, True)[0]
+        assert_close(e3[-1][torch.from_numpy(rl.perm).to(dev)], ref, what="relabelled simulated ranks")

@@ -56,22 +56,92 @@ def test_edge_plan_covers_every_edge_once(world):
     assert (cov == 1).all()
 
 
-@pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_owner_views_partition_the_nodes(world):
+@pytest.mark.parametrize("world,chunks", [(1, 1), (2, 1), (3, 2), (8, 4)])
+def test_owner_views_partition_the_nodes(world, chunks):
     g = _snapshot()
     V = g.number_of_nodes()
+    lay = P.OwnerLayout(V, world, chunks)
     seen = []
-    per, bounds = P.owner_bounds(V, world)
     for rank in range(world):
-        v = P.OwnerView(g, rank, world)
-        rows = v.fw.host["rows"]
-        assert ((rows >= v.v0) & (rows < v.v1)).all() and v.v1 - v.v0 <= per
-        assert v.n_pos == int((g.in_deg_np[rows] > 0).sum())
-        # the view's items are exactly the in-edges of its inline rows
-        n_inline = int(np.where(g.in_deg_np[rows[:v.n_pos]] > g.budget, 0, g.in_deg_np[rows[:v.n_pos]]).sum())
-        assert v.fw.host["item_ptr"][-1] == n_inline
-        seen += rows.tolist()
+        for j, (lo, hi) in enumerate(lay.ranges(rank)):
+            assert (lo, hi) == lay.group(rank, j) and hi - lo <= lay.cr
+            assert lo == hi or (lo // lay.cr == j * world + rank and (P.OwnerLayout(V, world, chunks).owner(
+                np.arange(lo, hi)) == rank).all())
+            v = P.OwnerView(g, lo, hi)
+            rows = v.fw.host["rows"]
+            assert ((rows >= lo) & (rows < hi)).all()
+            assert v.n_pos == int((g.in_deg_np[rows] > 0).sum())
+            # the view's items are exactly the in-edges of its inline rows
+            n_inline = int(np.where(g.in_deg_np[rows[:v.n_pos]] > g.budget, 0, g.in_deg_np[rows[:v.n_pos]]).sum())
+            assert v.fw.host["item_ptr"][-1] == n_inline
+            seen += rows.tolist()
     assert sorted(seen) == list(range(V))
+    # chunk j of every rank is one contiguous id range (its all-gather lands in place)
+    for j in range(chunks):
+        rs = [lay.group(k, j) for k in range(world)]
+        for (a0, b0), (a1, b1) in zip(rs, rs[1:]):
+            assert b0 == a1 or a1 == b1
+
+
+def test_lpt_balances_and_respects_capacities():
+    rng = np.random.default_rng(3)
+    n = 80_000
+    load = np.floor(1e6 / np.arange(1, n + 1) ** 1.1)[rng.permutation(n)]
+    caps = np.array([n // 4] * 3 + [n - 3 * (n // 4)])
+    g = P._lpt(load, caps, head=4000)
+    assert (np.bincount(g, minlength=4) == caps).all()
+    tot = np.bincount(g, weights=load, minlength=4)
+    # the heaviest item is below a fair share here: every group within 2 % of the mean
+    assert load.max() < load.sum() / 4 and tot.max() <= 1.02 * load.sum() / 4, tot / (load.sum() / 4)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_entity_relabel_balances_edges(world):
+    """EntityRelabel.balanced: a permutation; per-rank in-edge loads of every snapshot within a
+    few percent of the mean under Zipf(1.1) (equal contiguous id blocks are far off); the model
+    tensors and triples relabel consistently (new row perm[i] = old row i)."""
+    from regcn_amd.synthetic import snapshot_series
+    V = 200_000
+    snaps = snapshot_series(1, V, 16, 2, 400_000)
+    rl = P.EntityRelabel.balanced(snaps, V, world)
+    assert np.array_equal(np.sort(rl.perm), np.arange(V))
+    for row in rl.loads(snaps, world):
+        assert max(row) <= 1.03 * np.mean(row), row
+    plain = P.EntityRelabel(np.arange(V)).loads(snaps, world)
+    imb = lambda rows: max(max(r) / np.mean(r) for r in rows)  # noqa: E731
+    assert imb(rl.loads(snaps, world)) < imb(plain) and (world < 8 or imb(plain) > 1.1)
+    tr = rl.triples(snaps[0][:50])
+    assert (tr[:, 0] == rl.perm[snaps[0][:50, 0]]).all() and (tr[:, 1] == snaps[0][:50, 1]).all()
+    m = torch.nn.Module()
+    m.dynamic_emb = torch.nn.Parameter(torch.arange(V, dtype=torch.float32).unsqueeze(1).repeat(1, 2))
+    m.register_buffer("radius_target", torch.arange(V, dtype=torch.float32))
+    rl.model(m)
+    assert torch.equal(m.radius_target[torch.from_numpy(rl.perm)], torch.arange(V, dtype=torch.float32))
+    assert torch.equal(m.dynamic_emb[torch.from_numpy(rl.perm), 0], torch.arange(V, dtype=torch.float32))
+
+
+def test_owned_relation_spans_cover_each_pair_once():
+    """The partitioned relation means: every forward (relation, entity) pair lies in exactly one
+    rank's spans, each span inside its id range (the ranks' partial sums add up to the sums)."""
+    rng = np.random.default_rng(0)
+    R, V = 6, 500
+    spans = [np.unique(rng.integers(0, V, rng.integers(0, 80))) for _ in range(R)]
+    idx = torch.from_numpy(np.concatenate(spans + spans)).int()  # forward lists, then inverse copies
+    cnt = torch.tensor([len(x) for x in spans], dtype=torch.float32)
+    start = np.concatenate([[0], np.cumsum([len(x) for x in spans])])
+    for world, chunks in ((2, 1), (3, 2), (8, 4)):
+        lay = P.OwnerLayout(V, world, chunks)
+        hit = np.zeros(int(cnt.sum()), np.int64)
+        for k in range(world):
+            ranges = lay.ranges(k)
+            rows, beg, ln = P.owned_rel_spans(idx, cnt, ranges, lay.Vp)
+            for row, b, n in zip(rows.tolist(), beg.tolist(), ln.tolist()):
+                r, q = divmod(row, len(ranges))
+                assert start[r] <= b and b + n <= start[r + 1]
+                lo, hi = ranges[q]
+                assert ((idx[b:b + n] >= lo) & (idx[b:b + n] < hi)).all()
+                hit[b:b + n] += 1
+        assert (hit == 1).all()
 
 
 def _segment_sum_slice(g, pl, x, rel):
@@ -109,18 +179,25 @@ def _worker(rank, world, port, result_q):
         buf[bounds[rank]:bounds[rank + 1]] = ref[bounds[rank]:bounds[rank + 1]]
         P.allgather_rows(buf, per)
         err_owner = float((buf[:V] - ref).abs().max())
-        # the owner partition's fused, pipelined exchange: (h | x | r) rows of two row chunks
-        # of the block, one collective each
-        h = torch.full((per * world, d), float("nan"))
-        xx = torch.full((per * world, d), float("nan"))
-        rr = torch.full((per * world,), float("nan"))
-        lo, hi = bounds[rank], bounds[rank + 1]
-        h[lo:hi], xx[lo:hi], rr[lo:hi] = ref[lo:hi], -ref[lo:hi], ref[lo:hi, 0]
-        half = per // 2
-        for rows in (slice(0, half), slice(half, per)):
-            P.allgather_fused((h, xx, rr), per, rows)
-        err_owner = max(err_owner, float((h[:V] - ref).abs().max()), float((xx[:V] + ref).abs().max()),
-                        float((rr[:V] - ref[:, 0]).abs().max()))
+        # the pipelined exchange of ShardedGraph.run_layer: OwnerLayout with 3 chunks per rank,
+        # after each chunk the in-place all-gather of chunk j of every rank (x rows and radii)
+        lay = P.OwnerLayout(V, world, 3)
+        xx = torch.full((lay.Vp, d), float("nan"))
+        rr = torch.full((lay.Vp,), float("nan"))
+        cr = lay.cr
+        for j, (lo, hi) in enumerate(lay.ranges(rank)):
+            xx[lo:hi], rr[lo:hi] = -ref[lo:hi], ref[lo:hi, 0]
+            a, b, k = j * world * cr, (j + 1) * world * cr, (j * world + rank) * cr
+            P._all_gather_into(xx[a:b], xx[k:k + cr])
+            P._all_gather_into(rr[a:b], rr[k:k + cr])
+        err_owner = max(err_owner, float((xx[:V] + ref).abs().max()), float((rr[:V] - ref[:, 0]).abs().max()))
+        # fetch_rows' exchange: the owner's rows in one all_reduce with zeros elsewhere
+        ids = torch.tensor([0, V - 1, 17, 123, 17])
+        got = torch.zeros(len(ids), d)
+        mine = lay.owner(ids) == rank
+        got[mine] = ref[ids[mine]]
+        P.allreduce_partials(got)
+        err_owner = max(err_owner, float((got - ref[ids]).abs().max()))
         result_q.put((rank, err_edge, err_owner))
     finally:
         dist.destroy_process_group()

@@ -81,6 +81,24 @@ def main():
             from regcn_amd.graph import build_sub_graph
             model.eval()
             T = 3
+            if kind == "junk_only":
+                junk = [torch.full((1 << 26,), 3.0, device=device) for _ in range(16)]
+                del junk
+                torch.cuda.synchronize()
+                return (0.0, 0.0, 0.0, 0.0)
+            if kind in ("host_build", "device_build"):
+                gl = [build_sub_graph(num_nodes, num_rels, s, kind == "device_build", device)
+                      for s in history_list[-T:]]
+                if kind == "host_build":
+                    gl = [g.to(device) for g in gl]
+                del gl
+                torch.cuda.synchronize()
+                return (0.0, 0.0, 0.0, 0.0)
+            if kind == "h2d":
+                tt = torch.from_numpy(np.asarray(test_list[0], dtype=np.int64)).to(device)
+                del tt
+                torch.cuda.synchronize()
+                return (0.0, 0.0, 0.0, 0.0)
             glist = [build_sub_graph(num_nodes, num_rels, s, True, device) for s in history_list[-T:]]
             tt = torch.from_numpy(np.asarray(test_list[0], dtype=np.int64)).to(device)
             with torch.no_grad():
@@ -168,12 +186,39 @@ def main():
             print("     %3d x %s" % (n, label[:260]), flush=True)
         return (0.0, 0.0, 0.0, 0.0)
 
-    run("eager", [])
-    run("eager, garbage 3", [], test=variant("garbage:3"))
-    run("eager, predict", [], test=variant("predict"))
-    run("graph, garbage 0", ["--hip-graph"], test=variant("garbage:0"))
-    run("graph, garbage 3", ["--hip-graph"], test=variant("garbage:3"))
-    run("graph, garbage nan", ["--hip-graph"], test=variant("garbage:nan"))
+    which = os.environ.get("VARIANTS", "base")
+    if which == "base":
+        run("eager", [])
+        run("eager, garbage 3", [], test=variant("garbage:3"))
+        run("eager, predict", [], test=variant("predict"))
+        run("graph, garbage 0", ["--hip-graph"], test=variant("garbage:0"))
+        run("graph, garbage 3", ["--hip-graph"], test=variant("garbage:3"))
+        run("graph, garbage nan", ["--hip-graph"], test=variant("garbage:nan"))
+    else:  # bisect the trigger: what between the replays makes them drift
+        from regcn_amd import weights as W
+        noop = lambda m: None  # noqa: E731
+
+        def inv_only(attrs):
+            def f(module):
+                for t in list(module.parameters()) + list(module.buffers()):
+                    for a in attrs:
+                        if hasattr(t, a):
+                            delattr(t, a)
+            return f
+
+        def inv_model(keys):
+            def f(module):
+                for m in module.modules():
+                    for a in keys:
+                        m.__dict__.pop(a, None)
+            return f
+        run("eager", [])
+        if which == "report":  # captured operands sitting in free default-pool blocks at validation
+            with mode:
+                run("graph, report", ["--hip-graph"], test=report, inv=noop)
+        else:
+            for kind in ("junk_only", "device_build", "host_build", "h2d"):
+                run("graph, %s" % kind, ["--hip-graph"], test=variant(kind), inv=noop)
     torch.optim.Adam = adam
 
 
