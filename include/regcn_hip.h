@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 8
+#define REGCN_ABI_VERSION 9
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -267,8 +267,29 @@ typedef struct regcn_layer_desc {
                             source order (regcn_snapshot_item_src_order_i32), so a row's k items
                             from one source gather that source row once, k * w_e * x[src]
                             (the relation rows still per item) */
+  /* regcn_layer_rowtail_f32 only (NULL elsewhere): */
+  const float* gate_w;   /* a cell's first layer: also the timestep's time-gate pre-activation */
+  float* gate_out;       /*   clamp(x) @ gate_w (kp-packed W_g) of every row -> gate_out (V x d) */
+  const float* step_tw;  /* the step layer: those rows (else the gate product runs in-kernel) */
 } regcn_layer_desc;
 int regcn_layer_f32(const regcn_layer_desc* desc, void* stream);
+
+/* The same layer for snapshots with many rows, as two launches (csrc/rowtail.hip):
+ *   1. the inline in-edge rows of every tile (desc->tiles / items) gathered and finished into
+ *      `agg` (V x d; on entry it holds the rows over the budget, pre-aggregated by the chunked
+ *      kernels: those rows are left as they are), desc->agg ignored;
+ *   2. a 64-row MFMA tail over desc->rows[0 .. desc->V): one wave per 16 rows and all columns
+ *      (in-wave row reductions; the four waves of a workgroup share each weight fragment), the
+ *      same epilogue / timestep as regcn_layer_f32.
+ * desc->w_n / w_loop / w_evolve / step_w_g are packed by regcn_pack_weight_kp_f32 for this
+ * call (a k-permuted fragment order the tail's direct global A loads need).  No skip gate, no
+ * dropout mask.  Values equal regcn_layer_f32's up to the fp32 order of the products' sums. */
+int regcn_layer_rowtail_f32(const regcn_layer_desc* desc, float* agg, void* stream);
+/* Packing of a d_in x d_out weight for regcn_layer_rowtail_f32:
+ * packed[s][jq][lane][e] = W[16 (s / 4) + 4 (lane / 16) + s % 4][16 (4 jq + e) + lane % 16],
+ * s < 4 ceil(d_in / 16), zero outside W; regcn_packed_weight_kp_floats(d_in) floats. */
+size_t regcn_packed_weight_kp_floats(int32_t d_in);
+int regcn_pack_weight_kp_f32(const float* w, int32_t d_in, int32_t d_out, float* packed, void* stream);
 
 /* ---- a4-a9: history-window schedule ------------------------------------------------- */
 /* A row without in-edges in any snapshot of the window ("cold") evolves through the T

@@ -362,9 +362,30 @@ int regcn_timestep_phase_f32(const regcn_phase_desc* g, int32_t phase, void* s) 
   return timestep_phase(a, phase, ST(s));
 }
 
+static int layer_args(const regcn_layer_desc* g, LayerArgs& a);
+
 int regcn_layer_f32(const regcn_layer_desc* g, void* s) {
   if (!g) return set_error(REGCN_EINVAL, "null descriptor");
   LayerArgs a{};
+  const int rc = layer_args(g, a);
+  if (rc == -1) return set_error(REGCN_EINVAL, "gate_w / gate_out / step_tw are regcn_layer_rowtail_f32 fields");
+  return rc ? rc : layer(a, ST(s));
+}
+
+int regcn_layer_rowtail_f32(const regcn_layer_desc* g, float* agg, void* s) {
+  if (!g) return set_error(REGCN_EINVAL, "null descriptor");
+  LayerArgs a{};
+  const int rc = layer_args(g, a);
+  return (rc && rc != -1) ? rc : layer_rowtail(a, agg, ST(s));
+}
+
+size_t regcn_packed_weight_kp_floats(int32_t d_in) { return packed_weight_kp_floats(d_in); }
+
+int regcn_pack_weight_kp_f32(const float* w, int32_t d_in, int32_t d_out, float* packed, void* s) {
+  return pack_weight_kp(w, d_in, d_out, packed, ST(s));
+}
+
+static int layer_args(const regcn_layer_desc* g, LayerArgs& a) {
   a.agg_mode = g->agg_mode;
   a.x = g->x;
   a.radius = g->radius;
@@ -423,9 +444,14 @@ int regcn_layer_f32(const regcn_layer_desc* g, void* s) {
     t.h_out = g->step_h_out;
     t.x_out = g->step_x_out;
     t.r_out = g->step_r_out;
+    t.tw = g->step_tw;
   }
+  a.w_gate = g->gate_w;
+  a.gate_out = g->gate_out;
   a.trace = g->trace;
-  return layer(a, ST(s));
+  if (g->gate_w || g->gate_out || g->step_tw)
+    return -1;  // marker: only regcn_layer_rowtail_f32 reads these (checked there)
+  return 0;
 }
 
 int regcn_timestep_f32(const float* hc, const float* x_prev, const float* w_g, const float* b_g,

@@ -340,10 +340,12 @@ __device__ __forceinline__ void tile_gather(const LayerArgs& p, float* part, int
 
 // Combine the wave partials of row i (wave w does rows w, w + NWAVE) and finish it:
 // Lorentz centroid -> log0, or norm-scaled sum; rows over budget read the pre-aggregated
-// row.  The result overwrites slot i (the A operand / agg fragment source).
+// row.  Row w + NWAVE q of the tile ends in out[q] (heavy[q]: pre[q] holds its pre-aggregated
+// row instead).
 template <int AGG>
-__device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int lda, const int* trow, int count,
-                                            const int* tmask, int rdeg, float rnorm) {
+__device__ __forceinline__ void tile_finish_rows(const LayerArgs& p, const float* part, int lda, const int* trow,
+                                                 int count, const int* tmask, int rdeg, float rnorm,
+                                                 f4 out[TM / NWAVE], f4 pre[TM / NWAVE], bool heavy[TM / NWAVE]) {
   const int lane = threadIdx.x & 63, w = wave_id();
   const int d = p.d;
   const int col = lane * 4, colc = min(col, d - 4);
@@ -351,9 +353,8 @@ __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int
   const f4 zero = {0.f, 0.f, 0.f, 0.f};
   // the wave's rows side by side: independent loads and reductions
   constexpr int RPW = TM / NWAVE;  // rows per wave
-  f4 acc[RPW], pre[RPW];
+  f4 acc[RPW];
   float acc0[RPW];
-  bool heavy[RPW];
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
     const int i = w + NWAVE * q;
@@ -376,7 +377,6 @@ __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int
       }
     }
   }
-  f4 out[RPW];
   if constexpr (AGG == AGG_LORENTZ) {
     // Centroid -> Poincare -> log0 of the wave's RPW rows with the per-row scalar chain run
     // once, lane-parallel (row q in lane batch_lane<RPW>(q)): |acc_q|^2 from one transposing
@@ -407,6 +407,20 @@ __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int
       out[q] = acc[q] * rlane(rnorm, i);
     }
   }
+}
+
+// tile_finish_rows, the result overwriting slot i (the A operand / agg fragment source).
+template <int AGG>
+__device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int lda, const int* trow, int count,
+                                            const int* tmask, int rdeg, float rnorm) {
+  const int lane = threadIdx.x & 63, w = wave_id();
+  const int col = lane * 4;
+  const bool active = col < p.d;
+  const f4 zero = {0.f, 0.f, 0.f, 0.f};
+  constexpr int RPW = TM / NWAVE;
+  f4 out[RPW], pre[RPW];
+  bool heavy[RPW];
+  tile_finish_rows<AGG>(p, part, lda, trow, count, tmask, rdeg, rnorm, out, pre, heavy);
   __syncthreads();  // every partial slot is read before any slot is overwritten
 #pragma unroll
   for (int q = 0; q < RPW; ++q) {
@@ -422,6 +436,5 @@ __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int
     }
   }
 }
-
 
 }  // namespace regcn

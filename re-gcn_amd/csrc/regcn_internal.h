@@ -84,6 +84,7 @@ struct StepArgs {
   float* r_out;
   float* gate_out;  // --run-analysis (k_timestep<true>): V x d time gate
   float* stat_out;  // 3 x V: clipped radius delta, dynamic radius, base radius (residual only)
+  const float* tw;  // rowtail: precomputed gate pre-activation rows clamp(x_prev) @ W_g, or null
 };
 
 // One message-passing layer: inline CSR gather + self-loop/neighbour GEMMs + epilogue,
@@ -124,6 +125,8 @@ struct LayerArgs {
   StepArgs step;
   int64_t* trace;           // debug: 8 phase timestamps per workgroup, or null
   int item_src_runs;        // union / euclid items in (row, source) order: one x row per source run
+  const float* w_gate;      // rowtail, a cell's first layer: W_g (kp-packed) ...
+  float* gate_out;          // ... and the V x d rows clamp(x) @ W_g it writes for the timestep
 };
 
 struct ScoreArgs {
@@ -300,6 +303,10 @@ int centroid(const float* S0, const float* Sv, int64_t V, int d, float c, float 
 int kreduce_gemm(const float* A, int a_kmajor, const float* B, int b_kmajor, int64_t K, int M, int N, const float* C0,
                  int64_t c0_ld, float* out, float* ws, hipStream_t st);
 int layer(const LayerArgs& a, hipStream_t st);
+// rowtail.hip: large snapshots' layer as an agg gather + a 64-row MFMA tail (k-permuted packing)
+size_t packed_weight_kp_floats(int d_in);
+int pack_weight_kp(const float* W, int d_in, int d_out, float* Wp, hipStream_t st);
+int layer_rowtail(const LayerArgs& a, float* agg, hipStream_t st);
 int timestep(const StepArgs& a, hipStream_t st, bool analysis = false);
 int score(ScoreArgs& a, int mode, float* loss, hipStream_t st);
 int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st);

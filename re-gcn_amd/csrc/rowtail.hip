@@ -1,0 +1,481 @@
+// Large-snapshot layers in two launches: the in-edge gather, then
+// a 64-row MFMA tail.
+//
+// The fused layer kernel (layer.hip) runs a 16-row tile's gather and then its three d x d
+// products serially, and every 16-row tile streams each d x d weight from L2 once per product:
+// at config 5 that is 38 GB of L1 <- L2 weight traffic per launch (16x re-read per 256 rows),
+// and a tile's life is gather (24 us) then products (12 us) with ~4 tiles per CU to overlap
+// them.  Here, for snapshots with many rows:
+//   1. k_gather_agg: the same per-tile gather (layer_parts.h tile_gather / tile_finish_rows) of
+//      the inline in-edge rows, finished rows written to an agg buffer that already holds the
+//      hub rows' chunked pre-aggregation (no products, no weights: small LDS and register
+//      footprint, many tiles in flight);
+//   2. k_rowtail: one workgroup = 4 waves = 64 rows, each wave 16 rows x ALL columns, so a
+//      row's reductions (norms, dots of the row maps and the timestep) are in-wave (a DPP row
+//      sum, no LDS, no barrier) and the four waves of a workgroup read the same weight
+//      fragments at the same k-step (served once from L2, 4x less weight traffic per row).
+//      The A operands come straight from global memory: lane l loads 4 consecutive columns
+//      16 b + 4 (l / 16) .. + 3 of its row (l % 16) per 16-column block b, and the weights are
+//      packed in the matching k order (k_pack_weight_kp: the k index of a 16-deep block is
+//      permuted, which a contraction does not see), so neither operand is staged in LDS.
+// Epilogues are the fused kernel's (clamp, self loop, rrelu, exp0, the timestep with the time
+// gate and the radius evolution), in fp32 with the same formulas; the products accumulate in
+// another k order (1e-7-relative differences, not bitwise the fused kernel).
+#include "layer_parts.h"
+
+namespace regcn {
+
+// ------------------------------------------------------------------------------ packing
+// Wp[s][jq][lane][e] = W[16 (s / 4) + 4 (lane / 16) + s % 4][16 (4 jq + e) + lane % 16], zero
+// outside d_in x d_out; s < 4 * ceil(d_in / 16).
+__global__ void k_pack_weight_kp(const float* __restrict__ W, int d_in, int d_out, int S, float* __restrict__ Wp) {
+  const int total = S * 4 * 64 * 4;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int e = idx & 3, lane = (idx >> 2) & 63, jq = (idx >> 8) & 3, s = idx >> 10;
+    const int k = 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3), n = 16 * (4 * jq + e) + (lane & 15);
+    Wp[idx] = (k < d_in && n < d_out) ? W[(int64_t)k * d_out + n] : 0.f;
+  }
+}
+
+size_t packed_weight_kp_floats(int d_in) { return (size_t)((d_in + 15) / 16) * 4 * 4 * 64 * 4; }
+
+int pack_weight_kp(const float* W, int d_in, int d_out, float* Wp, hipStream_t st) {
+  if (!W || !Wp) return set_error(REGCN_EINVAL, "null pointer");
+  if (d_in <= 0 || d_out <= 0 || d_out > MAX_D) return set_error(REGCN_EINVAL, "pack_weight_kp needs d_out <= 256");
+  const int S = 4 * ((d_in + 15) / 16);
+  const int total = S * 4 * 64 * 4;
+  hipLaunchKernelGGL(k_pack_weight_kp, dim3((total + 255) / 256), dim3(256), 0, st, W, d_in, d_out, S, Wp);
+  return check_launch("k_pack_weight_kp");
+}
+
+// ------------------------------------------------------------------------------- gather
+// The inline in-edge rows of every in-degree > 0 tile (the tiles / items of the fused kernel),
+// finished (norm-scaled sum, or Lorentz centroid -> log0) and written to out[row]; rows over
+// the budget are skipped (out already holds them).
+template <int AGG, int S>
+__global__ __launch_bounds__(NTHR) void k_gather_agg(LayerArgs p, float* __restrict__ out) {
+  extern __shared__ float lds[];
+  const int lda = tile_lda(p.d);
+  float* part = lds;
+  int* trow = reinterpret_cast<int*>(lds + (TM + NWAVE - 1) * lda);
+  int* tmask = trow + TM;
+  float* xsh = lds + (TM + NWAVE - 1) * lda + 32;
+  const int start = p.tiles[2 * blockIdx.x], count = p.tiles[2 * blockIdx.x + 1];
+  if (threadIdx.x < TM) trow[threadIdx.x] = p.rows[start + ((int)threadIdx.x < count ? threadIdx.x : 0)];
+  __syncthreads();
+  const int lrow = trow[min((int)(threadIdx.x & 63), TM - 1)];
+  const int rdeg = p.rowptr[lrow + 1] - p.rowptr[lrow];
+  const float rnorm = AGG != AGG_LORENTZ ? p.norm[lrow] : 1.f;
+  tile_gather<AGG, S>(p, part, lda, trow, blockIdx.x, tmask, xsh);
+  __syncthreads();
+  constexpr int RPW = TM / NWAVE;
+  f4 o[RPW], pre[RPW];
+  bool heavy[RPW];
+  tile_finish_rows<AGG>(p, part, lda, trow, count, tmask, rdeg, rnorm, o, pre, heavy);
+  const int lane = threadIdx.x & 63, w = wave_id(), col = lane * 4;
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int i = w + NWAVE * q;
+    if (i < count && !heavy[q] && col < p.d) *reinterpret_cast<f4*>(out + (int64_t)trow[i] * p.d + col) = o[q];
+  }
+}
+
+// --------------------------------------------------------------------------- 64-row tail
+constexpr int RT_ROWS = 64;
+
+template <int NT>
+struct RAcc {
+  f4 t[NT];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) t[j] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+};
+
+// acc += A[16 rows x K] @ W for the wave's rows: A row of lane l = arow (row l % 16 of the
+// wave), columns >= d and rows with !aok read as 0 (clamped loads, then a select), CLAMP:
+// A clamped to +-10 (the time gate's operand); Wp packed by k_pack_weight_kp.  B fragments of
+// the next P k-steps are in flight while a k-step's NT MFMAs issue.
+template <int NT, bool CLAMP>
+__device__ __forceinline__ void rt_mm(RAcc<NT>& acc, const float* __restrict__ arow, bool aok,
+                                      const float* __restrict__ Wp, int d, int KB) {
+  constexpr int P = 2;
+  const int lane = threadIdx.x & 63, q = lane >> 4;
+  const f4* __restrict__ B = reinterpret_cast<const f4*>(Wp) + lane;
+  const int S = 4 * KB;
+  auto load_a = [&](int kb) {
+    const int col = 16 * kb + 4 * q;
+    f4 v = *reinterpret_cast<const f4*>(arow + min(col, d - 4));
+    if (CLAMP) v = clamp4(v, -10.f, 10.f);
+    return (aok & (col < d)) ? v : f4{0.f, 0.f, 0.f, 0.f};
+  };
+  f4 ring[P][4];
+#pragma unroll
+  for (int i = 0; i < P; ++i)
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq) ring[i][jq] = B[(int64_t)(min(i, S - 1) * 4 + jq) * 64];
+  f4 a = load_a(0);
+  for (int kb = 0; kb < KB; ++kb) {
+    const f4 an = load_a(min(kb + 1, KB - 1));
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int slot = s % P;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc.t[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], ring[slot][t >> 2][t & 3], acc.t[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      const int nx = min(4 * kb + s + P, S - 1);
+#pragma unroll
+      for (int jq = 0; jq < 4; ++jq) ring[slot][jq] = B[(int64_t)(nx * 4 + jq) * 64];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    a = an;
+  }
+}
+
+// ---- per-row maps on the wave's 16 rows (lane l: rows 4 (l / 16) + r, column 16 t + l % 16)
+template <int NT>
+__device__ __forceinline__ void rt_sumsq(const RAcc<NT>& a, float n2[4]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) s += a.t[t][r] * a.t[t][r];
+    n2[r] = row16_sum(s);
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void rt_scale(RAcc<NT>& a, const float f[4]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a.t[t][r] *= f[r];
+}
+
+template <int NT>
+__device__ __forceinline__ void rt_scale_known(RAcc<NT>& a, float n2[4], const float f[4]) {
+  rt_scale(a, f);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) n2[r] *= f[r] * f[r];
+}
+
+template <int NT>
+__device__ __forceinline__ void rt_project(RAcc<NT>& a, float n2[4], const Curv& k) {
+  float f[4];
+  spread_rows(project_factor(own_row(n2), k), f);
+  rt_scale_known(a, n2, f);
+}
+
+template <int NT>
+__device__ __forceinline__ void rt_log0(RAcc<NT>& a, float n2[4], const Curv& k) {
+  float f[4];
+  spread_rows(log0_factor(own_row(n2), k), f);
+  rt_scale_known(a, n2, f);
+}
+
+template <int NT>
+__device__ __forceinline__ void rt_exp0(RAcc<NT>& a, float n2[4], const Curv& k) {  // exp0 + project
+  float f[4], o;
+  spread_rows(exp0_factor(own_row(n2), k, &o), f);
+  rt_scale(a, f);
+  spread_rows(o, n2);
+}
+
+template <int NT>
+__device__ __forceinline__ void rt_normalize(RAcc<NT>& a, float n2[4]) {  // F.normalize, eps 1e-12
+  float f[4];
+  spread_rows(1.0f / fmaxf(sqrtf(own_row(n2)), 1e-12f), f);
+  rt_scale_known(a, n2, f);
+}
+
+// C-layout rows of a row-major matrix (columns >= d and rows past n_valid read 0)
+template <int NT>
+__device__ __forceinline__ void rt_load(RAcc<NT>& a, const float* __restrict__ M, const int crow[4], int n_valid,
+                                        int d) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool ok = 4 * (lane >> 4) + r < n_valid;
+    const int64_t base = (int64_t)crow[r] * d;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = 16 * t + (lane & 15);
+      const float v = M[base + min(col, d - 1)];
+      a.t[t][r] = (ok & (col < d)) ? v : 0.f;
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void rt_store(const RAcc<NT>& a, float* __restrict__ M, const int crow[4], int n_valid,
+                                         int d) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (4 * (lane >> 4) + r >= n_valid) continue;
+    const int64_t base = (int64_t)crow[r] * d;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = 16 * t + (lane & 15);
+      if (col < d) M[base + col] = a.t[t][r];
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void rt_col(float out[NT], const float* __restrict__ v, int d) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int col = 16 * t + (lane & 15);
+    const float x = v[min(col, d - 1)];
+    out[t] = col < d ? x : 0.f;
+  }
+}
+
+__device__ __forceinline__ void rt_store_radius(const float n2[4], float* __restrict__ rad, const int crow[4],
+                                                int n_valid) {
+  const int lane = threadIdx.x & 63;
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (4 * (lane >> 4) + r < n_valid) rad[crow[r]] = fmaxf(sqrtf(n2[r]), REGCN_EPS);
+  }
+}
+
+__device__ __forceinline__ int own_int(const int v[4]) {
+  const bool b0 = threadIdx.x & 1, b1 = threadIdx.x & 2;
+  const int lo = b0 ? v[1] : v[0], hi = b0 ? v[3] : v[2];
+  return b1 ? hi : lo;
+}
+
+// The layer of the rows rows[64 b + 16 w ...] (wave w of workgroup b): v = clamp(agg @ W_n)
+// (or clamp(agg): Lorentz; no clamps: euclid) + x @ (W_loop | W_evolve) -> clamp -> rrelu ->
+// exp0; then the next layer's x / |h|, or the timestep (hyperbolic_model.py:829-869: project,
+// layer norm, time gate, exp0, project, radius evolution / static radius).
+// MODE: RT_LAYER; RT_GATE = RT_LAYER + the timestep's time-gate pre-activation clamp(x) @ W_g
+// into gate_out (a cell's first layer: x is the timestep input); RT_STEP = the last layer with
+// the timestep, its gate product in-kernel; RT_STEP_PRE = with the gate rows from RT_GATE (the
+// blend reads them per column tile: no second accumulator set, half the registers).
+enum { RT_LAYER = 0, RT_GATE = 1, RT_STEP = 2, RT_STEP_PRE = 3 };
+template <int NT, int MODE>
+__global__ __launch_bounds__(NTHR) void k_rowtail(LayerArgs p) {
+  constexpr bool STEP = MODE >= RT_STEP;
+  const int lane = threadIdx.x & 63, w = wave_id(), q = lane >> 4;
+  const int base = blockIdx.x * RT_ROWS + 16 * w;
+  const int n_valid = min(16, p.V - base);  // p.V: the length of the row list
+  if (n_valid <= 0) return;
+  const int d = p.d, KB = (d + 15) >> 4;
+  const int my_i = lane & 15;
+  const int arow_id = p.rows[base + min(my_i, n_valid - 1)];
+  const bool a_valid = my_i < n_valid;
+  const bool a_pos = a_valid & (base + my_i < p.n_pos);
+  int crow[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) crow[r] = __shfl(arow_id, 4 * q + r);
+  const int npos_w = min(max(p.n_pos - base, 0), n_valid);  // wave-uniform
+  const float* xrow = p.x + (int64_t)arow_id * d;
+
+  RAcc<NT> v;
+  if constexpr (MODE == RT_GATE) {  // the timestep's gate pre-activation, stored as is
+    v.zero();
+    rt_mm<NT, true>(v, xrow, a_valid, p.w_gate, d, KB);
+    rt_store<NT>(v, p.gate_out, crow, n_valid, d);
+  }
+  v.zero();
+  // The products into v, one call site (one copy of the MFMA loop, one accumulator set):
+  // pass 0 = agg @ W_n (in-edge rows), then x @ W_loop / x @ W_evolve -- both in the one wave
+  // where the in-edge rows end (rows masked), one of them everywhere else.
+  const bool p1 = npos_w > 0 && p.agg != nullptr;
+  if (p1 && !p.w_n) rt_load<NT>(v, p.agg, crow, npos_w, d);  // Lorentz: the centroid rows as is
+  const bool mixed = npos_w > 0 && npos_w < n_valid;
+  const int first = (p1 && p.w_n) ? 0 : 1;
+  const int last = p.w_loop ? (mixed ? 3 : 2) : 1;
+  for (int pass = first; pass < last; ++pass) {
+    if (pass == 1 && p1 && !p.euclid) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
+    }
+    if (pass == last) break;
+    const float* arow = pass == 0 ? p.agg + (int64_t)arow_id * d : xrow;
+    const bool ok = pass == 0 ? a_pos : (mixed ? (pass == 1 ? a_pos : a_valid & !a_pos) : a_valid);
+    const float* W = pass == 0 ? p.w_n : (pass == 1 && npos_w > 0 ? p.w_loop : p.w_evolve);
+    rt_mm<NT, false>(v, arow, ok, W, d, KB);
+  }
+  if (first == 0 && last == 1 && !p.euclid) {  // agg @ W_n without a self loop
+#pragma unroll
+    for (int t = 0; t < NT; ++t) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
+  }
+  if (first == 1 && p1 && !p.euclid) {  // Lorentz rows without a W_n product
+    // (clamped above when a self-loop pass followed; else here)
+    if (last == 1) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    if (!p.euclid) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
+    v.t[t] = leaky4(v.t[t]);
+  }
+  float n2[4];
+  if (!p.euclid || p.r_next) rt_sumsq<NT>(v, n2);
+  if (!p.euclid) rt_exp0<NT>(v, n2, p.k);
+
+  if constexpr (!STEP) {
+    rt_store<NT>(v, p.h_out, crow, n_valid, d);
+    if (p.r_next) rt_store_radius(n2, p.r_next, crow, n_valid);
+    if (p.x_next) {
+      if (!p.euclid) rt_log0<NT>(v, n2, p.k);
+      rt_store<NT>(v, p.x_next, crow, n_valid, d);
+    }
+  } else {
+    const StepArgs& s = p.step;
+    const Curv k = s.k;
+    rt_project<NT>(v, n2, k);
+    if (s.layer_norm) {
+      rt_log0<NT>(v, n2, k);
+      rt_normalize<NT>(v, n2);
+      rt_exp0<NT>(v, n2, k);
+    }
+    rt_log0<NT>(v, n2, k);
+    RAcc<NT> g;  // the time gate pre-activation clamp(x_prev) @ W_g (RT_STEP), then its blend
+    if constexpr (MODE == RT_STEP) {
+      g.zero();
+      rt_mm<NT, true>(g, s.x_prev + (int64_t)arow_id * d, a_valid, s.w_g, d, KB);
+    }
+    float bg[NT];
+    rt_col<NT>(bg, s.b_g, d);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int col = 16 * t + (lane & 15), colc = min(col, d - 1);
+      const f4 c4 = clamp4(v.t[t], -10.f, 10.f);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool ok = (4 * q + r < n_valid) & (col < d);
+        const float xp = s.x_prev[(int64_t)crow[r] * d + colc];
+        const float pr = fminf(fmaxf(ok ? xp : 0.f, -10.f), 10.f);
+        float z;
+        if constexpr (MODE == RT_STEP_PRE) {
+          const float zt = s.tw[(int64_t)crow[r] * d + colc];
+          z = ok ? zt : 0.f;
+        } else {
+          z = g.t[t][r];
+        }
+        const float gg = sigmoidf(z + bg[t]);
+        v.t[t][r] = gg * c4[r] + (1.f - gg) * pr;
+      }
+    }
+    rt_sumsq<NT>(v, n2);
+    rt_exp0<NT>(v, n2, k);
+    rt_project<NT>(v, n2, k);  // hyperbolic_model.py:860
+    // radius: per-row scalars once per lane, for its own row r = lane & 3 (own_row)
+    const float rs = s.r_static[own_int(crow)];
+    const float n2o = own_row(n2);
+    float newr = rs;
+    if (s.residual) {
+      float wr[NT], lf[4], dl[4];
+      rt_col<NT>(wr, s.w_r, d);
+      spread_rows(log0_factor(n2o, s.k_rad), lf);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float acc = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc += wr[t] * (v.t[t][r] * lf[r]);
+        dl[r] = row16_sum(acc);
+      }
+      const float delta = fminf(fmaxf(own_row(dl) + *s.b_r, -s.eps_r), s.eps_r);
+      const float dyn = fmaxf(sqrtf(n2o), REGCN_EPS);
+      newr = (s.beta * rs + (1.f - s.beta) * dyn) + delta;
+    }
+    const Curv kr = s.residual ? s.k_rad : s.k;
+    float f[4];
+    spread_rows(fminf(fmaxf(newr, REGCN_EPS), kr.rmax) / fmaxf(sqrtf(n2o), REGCN_EPS), f);
+    rt_scale_known<NT>(v, n2, f);
+    rt_store<NT>(v, s.h_out, crow, n_valid, d);
+    if (s.r_out) rt_store_radius(n2, s.r_out, crow, n_valid);
+    if (s.x_out) {
+      rt_log0<NT>(v, n2, k);
+      rt_store<NT>(v, s.x_out, crow, n_valid, d);
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- launchers
+template <int AGG, int S>
+static void launch_gather(const LayerArgs& a, float* out, size_t lds, hipStream_t st) {
+  hipLaunchKernelGGL((k_gather_agg<AGG, S>), dim3(a.n_pos_tiles), dim3(NTHR), lds, st, a, out);
+}
+
+template <int NT>
+static void launch_tail(const LayerArgs& a, unsigned grid, hipStream_t st) {
+  if (a.fuse_step && a.step.tw)
+    hipLaunchKernelGGL((k_rowtail<NT, RT_STEP_PRE>), dim3(grid), dim3(NTHR), 0, st, a);
+  else if (a.fuse_step)
+    hipLaunchKernelGGL((k_rowtail<NT, RT_STEP>), dim3(grid), dim3(NTHR), 0, st, a);
+  else if (a.gate_out)
+    hipLaunchKernelGGL((k_rowtail<NT, RT_GATE>), dim3(grid), dim3(NTHR), 0, st, a);
+  else
+    hipLaunchKernelGGL((k_rowtail<NT, RT_LAYER>), dim3(grid), dim3(NTHR), 0, st, a);
+}
+
+int layer_rowtail(const LayerArgs& a, float* agg, hipStream_t st) {
+  const int mode = a.agg_mode;
+  if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "rowtail needs d %% 4 == 0, d <= 256");
+  if (!a.x || !a.rows || (!a.h_out && !a.fuse_step)) return set_error(REGCN_EINVAL, "null pointer");
+  if ((a.w_loop == nullptr) != (a.w_evolve == nullptr)) return set_error(REGCN_EINVAL, "self-loop weights must come in pairs");
+  if (a.prev_t || a.drop_mask) return set_error(REGCN_EINVAL, "rowtail has no skip gate / dropout mask (use regcn_layer_f32)");
+  if (a.n_pos < 0 || a.n_pos > a.V) return set_error(REGCN_EINVAL, "bad n_pos");
+  if (mode != AGG_NONE && mode != AGG_UNION && mode != AGG_EUCLID && mode != AGG_LORENTZ)
+    return set_error(REGCN_EINVAL, "unknown aggregation mode %d", mode);
+  if (a.n_pos > 0 && !agg) return set_error(REGCN_EINVAL, "rowtail needs the agg buffer");
+  if ((mode == AGG_UNION || mode == AGG_EUCLID) && !a.w_n && a.n_pos > 0)
+    return set_error(REGCN_EINVAL, "union / euclid rowtail needs w_n");
+  if ((mode == AGG_UNION || mode == AGG_LORENTZ) && a.euclid) return set_error(REGCN_EINVAL, "hyperbolic gather with euclid tail");
+  if ((a.gate_out == nullptr) != (a.w_gate == nullptr)) return set_error(REGCN_EINVAL, "gate_w and gate_out come in pairs");
+  if (a.gate_out && a.fuse_step) return set_error(REGCN_EINVAL, "gate_out is for a cell's first layer, not the step layer");
+  if (a.fuse_step) {
+    const StepArgs& s = a.step;
+    if (a.euclid) return set_error(REGCN_EINVAL, "the fused timestep is hyperbolic only");
+    if (!s.x_prev || !s.w_g || !s.b_g || !s.r_static || !s.h_out) return set_error(REGCN_EINVAL, "null timestep pointer");
+    if (s.residual && (!s.w_r || !s.b_r)) return set_error(REGCN_EINVAL, "residual radius needs w_r and b_r");
+  }
+  if (a.V == 0) return 0;
+  if (mode != AGG_NONE && a.n_pos_tiles > 0) {
+    if (!a.rowptr || !a.col_src || !a.col_type || !a.rel || !a.tiles || !a.item_ptr)
+      return set_error(REGCN_EINVAL, "gather needs CSR, rel, tiles and item lists");
+    if (mode == AGG_UNION && !a.radius) return set_error(REGCN_EINVAL, "union gather needs radius");
+    if (mode != AGG_LORENTZ && !a.norm) return set_error(REGCN_EINVAL, "gather needs norm");
+    if (mode == AGG_LORENTZ && (!a.w_rel || a.nb <= 0 || a.d % a.nb))
+      return set_error(REGCN_EINVAL, "lorentz gather needs weights and d %% num_bases == 0");
+    LayerArgs g = a;
+    g.agg = agg;  // hub rows: read back (skipped) by the finish
+    const int s = mode == AGG_LORENTZ ? a.d / a.nb : 1;
+    const bool gen = mode == AGG_LORENTZ && s != 1 && s != 2 && s != 4;
+    const size_t lds = (size_t)(((TM + NWAVE - 1) * tile_lda(a.d) + 32) + (gen ? NWAVE * MAX_D : 0)) * 4;
+    switch (mode) {
+      case AGG_UNION: launch_gather<AGG_UNION, 1>(g, agg, lds, st); break;
+      case AGG_EUCLID: launch_gather<AGG_EUCLID, 1>(g, agg, lds, st); break;
+      default:
+        if (s == 1) launch_gather<AGG_LORENTZ, 1>(g, agg, lds, st);
+        else if (s == 2) launch_gather<AGG_LORENTZ, 2>(g, agg, lds, st);
+        else if (s == 4) launch_gather<AGG_LORENTZ, 4>(g, agg, lds, st);
+        else launch_gather<AGG_LORENTZ, 0>(g, agg, lds, st);
+    }
+    const int rc = check_launch("k_gather_agg");
+    if (rc) return rc;
+  }
+  LayerArgs t = a;
+  t.agg = agg;
+  if (mode == AGG_LORENTZ) t.w_n = nullptr;  // the centroid rows are the aggregation itself
+  const unsigned grid = (unsigned)((a.V + RT_ROWS - 1) / RT_ROWS);
+  const int nt = (a.d + 15) / 16;
+  if (nt <= 4) launch_tail<4>(t, grid, st);
+  else if (nt <= 8) launch_tail<8>(t, grid, st);
+  else if (nt <= 13) launch_tail<13>(t, grid, st);
+  else launch_tail<16>(t, grid, st);
+  return check_launch("k_rowtail");
+}
+
+}  // namespace regcn

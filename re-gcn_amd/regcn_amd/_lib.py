@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REGCN_HIP_LIB") or os.path.join(_HERE, "libregcn_hip.so")  # override: A/B builds
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -60,6 +60,9 @@ _SIGS = {
     "regcn_rank_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
     "regcn_rank_count_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
     "regcn_layer_f32": [P, P],
+    "regcn_layer_rowtail_f32": [P, P, P],
+    "regcn_packed_weight_kp_floats": [_c_int],
+    "regcn_pack_weight_kp_f32": [P, _c_int, _c_int, P, P],
     "regcn_timestep_phase_f32": [P, _c_int, P],
     "regcn_window_plan_i32": [_c_int, P, P, _c_int, P, P, P, P, _c_int, P, P],
     "regcn_cold_chain_f32": [P, P],
@@ -101,6 +104,7 @@ _RESTYPE = {"regcn_last_error_string": ctypes.c_char_p, "regcn_hyp_ce_workspace_
             "regcn_snapshot_workspace_bytes": _c_sz, "regcn_kreduce_workspace_floats": _c_sz, "regcn_snapshot_capacity": _c_i64,
             "regcn_transpose_workspace_bytes": _c_sz, "regcn_row_type_order_workspace_bytes": _c_sz,
             "regcn_row_src_order_workspace_bytes": _c_sz, "regcn_item_src_order_workspace_bytes": _c_sz,
+            "regcn_packed_weight_kp_floats": _c_sz,
             "regcn_packed_weight_floats": _c_sz, "regcn_packed_linear_floats": _c_sz,
             "regcn_packed_k4_floats": _c_sz}
 
@@ -121,6 +125,7 @@ class LayerDesc(ctypes.Structure):
         ("step_r_static", P), ("step_w_r", P), ("step_b_r", P), ("step_eps_r", _c_f), ("step_beta", _c_f),
         ("step_layer_norm", _c_int), ("step_residual", _c_int), ("step_c_radius", _c_f), ("step_h_out", P),
         ("step_x_out", P), ("step_r_out", P), ("trace", P), ("item_src_runs", _c_int),
+        ("gate_w", P), ("gate_out", P), ("step_tw", P),
     ]
 
 

@@ -9,6 +9,9 @@ signatures follow the reference; forward runs three gfx950 kernels per layer:
 With autograd on (training) the model runs training.py instead, the differentiable
 composition of the same layers; FHNN/HGAT encoders are outside this build's scope.
 """
+import ctypes
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -16,11 +19,14 @@ import torch.nn.functional as F
 from . import _lib
 from .parallel import ShardedGraph
 from .tangent import attach, tangent_of
-from .weights import packed
+from .weights import packed, packed_kp
 from .graph import hub_block_work
 
 EPS = 1e-6
 TRACE = None  # int64 HIP tensor (>= 8 x workgroups) to record k_layer phase timestamps (profiling)
+# Snapshots with at least this many rows run a layer as the agg gather + the 64-row MFMA tail
+# (regcn_layer_rowtail_f32, csrc/rowtail.hip) instead of the fused 16-row kernel; 0 disables.
+ROWTAIL_MIN_ROWS = int(os.environ.get("REGCN_ROWTAIL_MIN_ROWS", "65536"))
 
 
 def _drop_mask(layer, like):
@@ -77,37 +83,56 @@ def _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c):
 
 
 class StepSpec:
-    """Timestep operands fused behind the last layer (regcn_layer_desc step_* fields)."""
+    """Timestep operands fused behind the last layer (regcn_layer_desc step_* fields).
+    w_g_param: the time-gate weight itself (the 64-row tail packs it its own way); tw: the
+    gate pre-activation rows clamp(x_prev) @ W_g when the cell's first layer computed them
+    (the 64-row tail, `gate=` of run_layer), else None."""
 
-    def __init__(self, x_prev, w_g, b_g, r_static, w_r, b_r, eps_r, beta, layer_norm, residual, c_radius):
+    def __init__(self, x_prev, w_g, b_g, r_static, w_r, b_r, eps_r, beta, layer_norm, residual, c_radius,
+                 w_g_param=None):
         self.x_prev, self.w_g, self.b_g, self.r_static = x_prev, w_g, b_g, r_static
         self.w_r, self.b_r, self.eps_r, self.beta = w_r, b_r, eps_r, beta
         self.layer_norm, self.residual, self.c_radius = layer_norm, residual, c_radius
+        self.w_g_param, self.tw = w_g_param, None
+
+
+def _use_rowtail(V, n_rows, d, prev_t, drop_mask, pos_only):
+    """The 64-row tail serves large snapshots' layers (V rows; a rank's view of one runs its
+    own n_rows) without a skip gate or dropout mask."""
+    return (ROWTAIL_MIN_ROWS > 0 and V >= ROWTAIL_MIN_ROWS and n_rows >= 1024 and prev_t is None
+            and drop_mask is None and not pos_only and d % 4 == 0 and d <= 256)
 
 
 def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip, drop_mask, c,
-              euclid=False, step=None, agg=None, out=None, pos_only=False):
+              euclid=False, step=None, agg=None, out=None, pos_only=False, gate=None):
     """One fused layer launch (regcn_layer_f32): inline gather + GEMMs + epilogue, or with
     `step` the timestep too.  Returns (h, x_next, r_next) of the layer (or of the step).
     `g` may be a rank's view of a snapshot (parallel.py): the launch covers its rows only,
     writing them into full-size outputs (`out`, optional preallocated (h, x, r)).
     agg (with mode AGG_NONE): the finished aggregation of every in-degree > 0 row.
-    pos_only: the launch covers the rows with in-edges only (rows[:n_pos])."""
+    pos_only: the launch covers the rows with in-edges only (rows[:n_pos]).
+    Large snapshots run regcn_layer_rowtail_f32 instead (the agg gather, then the 64-row MFMA
+    tail); `gate` (a StepSpec, the cell's first layer): that path also writes the timestep's
+    gate pre-activation rows into gate.tw for the step layer."""
     if isinstance(g, ShardedGraph):  # multi-GPU partition of the snapshot (parallel.py)
         if agg is not None or out is not None or pos_only:
             raise ValueError("agg/out are managed by the sharded layer")
         return g.run_layer(mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                           drop_mask, c, euclid=euclid, step=step)
+                           drop_mask, c, euclid=euclid, step=step, gate=gate)
     wk = g.work()
     V, d = x.shape
     n_rows = int(wk["rows"].shape[0])
     a = _lib.addr
+    rowtail = _use_rowtail(V, n_rows, d, prev_t, drop_mask, pos_only) and (agg is None or mode == _lib.AGG_NONE)
     if agg is None:
         agg = _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c)
     elif mode != _lib.AGG_NONE:
         raise ValueError("a precomputed aggregation needs mode AGG_NONE")
     if g.n_pos == 0:  # an edgeless snapshot: nothing to gather, every row takes the evolve loop
         mode = _lib.AGG_NONE
+    if rowtail:
+        return _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c, euclid, step, agg, out,
+                            gate, n_rows)
     if out is None:
         h = torch.empty_like(x)
         xn = torch.empty_like(x)
@@ -162,6 +187,74 @@ def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_
     return h, xn, rn
 
 
+def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c, euclid, step, agg, out, gate,
+                 n_rows):
+    """regcn_layer_rowtail_f32: the inline in-edge rows gathered into `agg` (which holds the hub
+    rows already), then the 64-row tail over all rows (csrc/rowtail.hip)."""
+    wk = g.work()
+    V, d = x.shape
+    a = _lib.addr
+    if out is None:
+        h = torch.empty_like(x)
+        xn = torch.empty_like(x)
+        rn = torch.empty(V, device=x.device, dtype=torch.float32)
+    else:
+        h, xn, rn = out
+    if agg is None and g.n_pos:
+        agg = torch.empty_like(x)
+    desc = _lib.LayerDesc()
+    desc.agg_mode = mode
+    desc.x = a(x, what="x")
+    desc.radius = a(r, what="radius")
+    desc.rel = a(rel, what="rel_emb")
+    desc.w_rel = a(w_rel, what="weight")
+    desc.num_bases = int(nb)
+    desc.gamma = float(gamma)
+    desc.rowptr = a(wk["rowptr"], torch.int32)
+    desc.col_src = a(wk["col_src"], torch.int32)
+    desc.col_type = a(wk["col_type"], torch.int32)
+    desc.norm = a(wk["norm"])
+    desc.budget = g.budget
+    desc.tiles = a(wk["tiles"], torch.int32)
+    desc.n_pos_tiles = g.n_pos_tiles
+    desc.item_ptr = a(wk["item_ptr"], torch.int32)
+    items = (wk["item_src"], wk["item_tl"])
+    if mode in (_lib.AGG_UNION, _lib.AGG_EUCLID) and getattr(g, "use_item_src_runs", None) and g.use_item_src_runs():
+        items = g.item_src_cols()
+        desc.item_src_runs = 1
+    desc.item_src = a(items[0], torch.int32) if items[0].numel() else None
+    desc.item_tl = a(items[1], torch.int32) if items[1].numel() else None
+    desc.w_n, desc.w_loop, desc.w_evolve = (a(packed_kp(w)) for w in (w_n, w_loop, w_evolve))
+    desc.rows = a(wk["rows"], torch.int32)
+    desc.n_pos, desc.V, desc.d, desc.euclid = g.n_pos, n_rows, d, int(bool(euclid))
+    desc.c = float(c)
+    keep = []
+    if step is None:
+        desc.h_out, desc.x_next, desc.r_next = a(h), a(xn), a(rn)
+        if gate is not None and gate.w_g_param is not None:
+            if gate.tw is None:
+                gate.tw = torch.empty_like(x)
+            desc.gate_w, desc.gate_out = a(packed_kp(gate.w_g_param)), a(gate.tw)
+    else:
+        desc.fuse_step = 1
+        desc.step_x_prev = a(step.x_prev, what="x_prev")
+        wg = packed_kp(step.w_g_param) if step.w_g_param is not None else None
+        if wg is None:
+            raise ValueError("the 64-row tail needs StepSpec.w_g_param")
+        desc.step_w_g, desc.step_b_g = a(wg), a(step.b_g)
+        desc.step_r_static, desc.step_w_r, desc.step_b_r = a(step.r_static), a(step.w_r), a(step.b_r)
+        desc.step_eps_r, desc.step_beta = float(step.eps_r), float(step.beta)
+        desc.step_layer_norm, desc.step_residual = int(bool(step.layer_norm)), int(bool(step.residual))
+        desc.step_c_radius = float(step.c_radius)
+        desc.step_h_out, desc.step_x_out, desc.step_r_out = a(h), a(xn), a(rn)
+        if step.tw is not None:
+            desc.step_tw = a(step.tw)
+            keep.append(step.tw)
+    _lib.check(_lib.lib().regcn_layer_rowtail_f32(ctypes.byref(desc), _lib.fptr(agg), _lib.stream()),
+               "regcn_layer_rowtail_f32(step)" if step is not None else "regcn_layer_rowtail_f32")
+    return h, xn, rn
+
+
 def _partial(g, d, device, lorentz=False):
     if g.n_slots == 0:
         return None, 0
@@ -196,9 +289,9 @@ class HyperbolicUnionRGCNLayer(nn.Module):
             self.skip_bias = nn.Parameter(torch.zeros(out_feat))
         self.dropout = nn.Dropout(dropout) if dropout > 0 else None
 
-    def forward(self, g, h_hyper, rel_emb, prev_h=None, step=None, pos_only=False, out=None):
+    def forward(self, g, h_hyper, rel_emb, prev_h=None, step=None, pos_only=False, out=None, gate=None):
         """hyperbolic_layers.py:242-323 (one fused launch; `step` fuses the timestep;
-        pos_only/out: see run_layer)."""
+        pos_only/out/gate: see run_layer)."""
         if self.activation is None:
             raise NotImplementedError("the fused tail applies rrelu; activation=None is not supported")
         self.rel_emb = rel_emb
@@ -213,7 +306,7 @@ class HyperbolicUnionRGCNLayer(nn.Module):
                               self.weight_neighbor, wl, we, prev_t,
                               self.skip_weight if prev_t is not None else None,
                               self.skip_bias.detach() if prev_t is not None else None,
-                              _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only)
+                              _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only, gate=gate)
         return attach(h, xn, rn, c)
 
 
@@ -248,9 +341,9 @@ class LorentzRGCNLayer(nn.Module):
         self.dropout = nn.Dropout(dropout) if dropout > 0 else None
         self.rel_emb = None
 
-    def forward(self, g, h_hyper, rel_emb=None, prev_h=None, step=None, pos_only=False, out=None):
+    def forward(self, g, h_hyper, rel_emb=None, prev_h=None, step=None, pos_only=False, out=None, gate=None):
         """hyperbolic_layers.py:627-694 (one fused launch; `step` fuses the timestep;
-        pos_only/out: see run_layer)."""
+        pos_only/out/gate: see run_layer)."""
         if self.activation is None:
             raise NotImplementedError("the fused tail applies rrelu; activation=None is not supported")
         if self.submat_in * self.num_bases != self.in_feat:
@@ -274,7 +367,7 @@ class LorentzRGCNLayer(nn.Module):
                               None, wl, we, prev_t,
                               self.skip_weight if prev_t is not None else None,
                               self.skip_bias.detach() if prev_t is not None else None,
-                              _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only)
+                              _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only, gate=gate)
         return attach(h, xn, rn, c)
 
 
@@ -303,7 +396,7 @@ class LorentzRGCNCell(nn.Module):
         for i, layer in enumerate(self.layers):
             last = i == n - 1
             h_new = layer(g, h, rel_embs[i], prev_h=prev_h, step=step if last else None, pos_only=pos_only,
-                          out=out if last else None)
+                          out=out if last else None, gate=step if (i == 0 and not last) else None)
             prev_h = h
             h = h_new
         return h

@@ -77,7 +77,8 @@ class HyperbolicRGCNCell(HyperbolicBaseRGCN):
         for i, layer in enumerate(self.layers):
             # prev_h is never passed (hyperbolic_model.py:152)
             last = i == n - 1
-            h = layer(g, h, rel_embs[i], step=step if last else None, pos_only=pos_only, out=out if last else None)
+            h = layer(g, h, rel_embs[i], step=step if last else None, pos_only=pos_only, out=out if last else None,
+                      gate=step if (i == 0 and not last) else None)
         return h
 
 
@@ -382,7 +383,8 @@ class HyperbolicRecurrentRGCN(nn.Module):
             if len(self.rgcn.layers) and not self.run_analysis:
                 # cell + timestep: the last layer's launch runs the timestep on its output
                 step = StepSpec(x_prev, wg, bg, r_static, w_r, b_r, trev.epsilon, trev.anchor_beta,
-                                self.layer_norm, self.use_residual_evolution, trev.c)
+                                self.layer_norm, self.use_residual_evolution, trev.c,
+                                w_g_param=self.time_gate_weight)
                 self.h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0], step=step)
             else:
                 current_h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0])

@@ -440,7 +440,7 @@ class ShardedGraph:
         return agg
 
     def run_layer(self, mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                  drop_mask, c, euclid=False, step=None):
+                  drop_mask, c, euclid=False, step=None, gate=None):
         """The sharded counterpart of hyperbolic_layers.run_layer (same arguments/returns)."""
         from .hyperbolic_layers import run_layer
         V, d = x.shape
@@ -466,7 +466,7 @@ class ShardedGraph:
             comm = self._comm
         for j, (_, view) in enumerate(self.views):
             run_layer(mode, view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                      drop_mask, c, euclid=euclid, step=step, out=(h[:V], xn[:V], rn[:V]))
+                      drop_mask, c, euclid=euclid, step=step, out=(h[:V], xn[:V], rn[:V]), gate=gate)
             if W == 1:
                 continue
             a, b, k = j * W * cr, (j + 1) * W * cr, (j * W + self.rank) * cr
@@ -592,7 +592,7 @@ class RankSimulation(ShardedGraph):
         return out
 
     def run_layer(self, mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                  drop_mask, c, euclid=False, step=None):
+                  drop_mask, c, euclid=False, step=None, gate=None):
         from .hyperbolic_layers import run_layer
         V, d = x.shape
         lay = self.layout
@@ -603,7 +603,7 @@ class RankSimulation(ShardedGraph):
         def rank_launches(sg):
             for _, view in sg.views:
                 run_layer(mode, view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                          drop_mask, c, euclid=euclid, step=step, out=(h[:V], xn[:V], rn[:V]))
+                          drop_mask, c, euclid=euclid, step=step, out=(h[:V], xn[:V], rn[:V]), gate=gate)
         for k, sg in enumerate(self.ranks):
             self._timed(k, lambda: rank_launches(sg))
             sg.exchanged_bytes += (self.world - 1) * lay.cr * lay.chunks * (d + 1) * 4

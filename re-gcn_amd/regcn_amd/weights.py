@@ -28,6 +28,24 @@ def packed(w):
     return out
 
 
+def packed_kp(w):
+    """Packed copy of a (d_in, d_out) weight in the k-permuted fragment order of the 64-row
+    tail (regcn_pack_weight_kp_f32, csrc/rowtail.hip), cached like `packed`."""
+    if w is None:
+        return None
+    key = (w.data_ptr(), w._version, tuple(w.shape))
+    hit = getattr(w, "_regcn_packed_kp", None)
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    d_in, d_out = w.shape
+    wc = w.detach().contiguous()
+    out = torch.empty(_lib.lib().regcn_packed_weight_kp_floats(d_in), device=w.device, dtype=torch.float32)
+    _lib.call("regcn_pack_weight_kp_f32", _lib.fptr(wc, "weight"), d_in, d_out, _lib.fptr(out), _lib.stream())
+    w._regcn_packed_kp = (key, out, wc)  # keep wc alive until the packing kernel has run
+    _lib.publish()
+    return out
+
+
 def packed_linear(w, n_gates=1):
     """Per-16-column-tile packing of an nn.Linear-layout weight ((n_gates*n_out) x n_in,
     regcn_pack_linear_f32), cached like `packed`."""
@@ -108,7 +126,8 @@ def bump_versions(params):
             torch._foreach_mul_(ts, 1.0)
 
 
-_CACHE_ATTRS = ("_regcn_packed", "_regcn_packed_lin", "_regcn_packed_t", "_regcn_packed_cols", "_regcn_packed_k4")
+_CACHE_ATTRS = ("_regcn_packed", "_regcn_packed_lin", "_regcn_packed_t", "_regcn_packed_cols", "_regcn_packed_k4",
+                "_regcn_packed_kp")
 
 
 def invalidate(module):
