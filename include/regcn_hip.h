@@ -285,6 +285,12 @@ int regcn_layer_f32(const regcn_layer_desc* desc, void* stream);
  * call (a k-permuted fragment order the tail's direct global A loads need).  No skip gate, no
  * dropout mask.  Values equal regcn_layer_f32's up to the fp32 order of the products' sums. */
 int regcn_layer_rowtail_f32(const regcn_layer_desc* desc, float* agg, void* stream);
+/* One part of regcn_layer_rowtail_f32, so a caller can pipeline row chunks on two streams
+ * (the gather of chunk i + 1 beside the tail of chunk i): which = 1: the gather of tiles
+ * [lo, hi); which = 2: the tail of desc->rows[lo .. hi) (their in-edge rows' agg complete:
+ * gathered, or hub rows pre-aggregated); which = 3: both, everything (= the call above). */
+int regcn_layer_rowtail_part_f32(const regcn_layer_desc* desc, float* agg, int32_t which, int32_t lo, int32_t hi,
+                                 void* stream);
 /* Packing of a d_in x d_out weight for regcn_layer_rowtail_f32:
  * packed[s][jq][lane][e] = W[16 (s / 4) + 4 (lane / 16) + s % 4][16 (4 jq + e) + lane % 16],
  * s < 4 ceil(d_in / 16), zero outside W; regcn_packed_weight_kp_floats(d_in) floats. */

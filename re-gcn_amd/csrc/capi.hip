@@ -379,6 +379,14 @@ int regcn_layer_rowtail_f32(const regcn_layer_desc* g, float* agg, void* s) {
   return (rc && rc != -1) ? rc : layer_rowtail(a, agg, ST(s));
 }
 
+int regcn_layer_rowtail_part_f32(const regcn_layer_desc* g, float* agg, int32_t which, int32_t lo, int32_t hi,
+                                 void* s) {
+  if (!g) return set_error(REGCN_EINVAL, "null descriptor");
+  LayerArgs a{};
+  const int rc = layer_args(g, a);
+  return (rc && rc != -1) ? rc : layer_rowtail_part(a, agg, which, lo, hi, ST(s));
+}
+
 size_t regcn_packed_weight_kp_floats(int32_t d_in) { return packed_weight_kp_floats(d_in); }
 
 int regcn_pack_weight_kp_f32(const float* w, int32_t d_in, int32_t d_out, float* packed, void* s) {

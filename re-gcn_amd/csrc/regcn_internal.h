@@ -307,6 +307,7 @@ int layer(const LayerArgs& a, hipStream_t st);
 size_t packed_weight_kp_floats(int d_in);
 int pack_weight_kp(const float* W, int d_in, int d_out, float* Wp, hipStream_t st);
 int layer_rowtail(const LayerArgs& a, float* agg, hipStream_t st);
+int layer_rowtail_part(const LayerArgs& a, float* agg, int which, int lo, int hi, hipStream_t st);
 int timestep(const StepArgs& a, hipStream_t st, bool analysis = false);
 int score(ScoreArgs& a, int mode, float* loss, hipStream_t st);
 int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st);

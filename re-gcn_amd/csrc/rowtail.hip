@@ -53,20 +53,21 @@ int pack_weight_kp(const float* W, int d_in, int d_out, float* Wp, hipStream_t s
 // finished (norm-scaled sum, or Lorentz centroid -> log0) and written to out[row]; rows over
 // the budget are skipped (out already holds them).
 template <int AGG, int S>
-__global__ __launch_bounds__(NTHR) void k_gather_agg(LayerArgs p, float* __restrict__ out) {
+__global__ __launch_bounds__(NTHR) void k_gather_agg(LayerArgs p, float* __restrict__ out, int tile0) {
   extern __shared__ float lds[];
+  const int tile = tile0 + blockIdx.x;
   const int lda = tile_lda(p.d);
   float* part = lds;
   int* trow = reinterpret_cast<int*>(lds + (TM + NWAVE - 1) * lda);
   int* tmask = trow + TM;
   float* xsh = lds + (TM + NWAVE - 1) * lda + 32;
-  const int start = p.tiles[2 * blockIdx.x], count = p.tiles[2 * blockIdx.x + 1];
+  const int start = p.tiles[2 * tile], count = p.tiles[2 * tile + 1];
   if (threadIdx.x < TM) trow[threadIdx.x] = p.rows[start + ((int)threadIdx.x < count ? threadIdx.x : 0)];
   __syncthreads();
   const int lrow = trow[min((int)(threadIdx.x & 63), TM - 1)];
   const int rdeg = p.rowptr[lrow + 1] - p.rowptr[lrow];
   const float rnorm = AGG != AGG_LORENTZ ? p.norm[lrow] : 1.f;
-  tile_gather<AGG, S>(p, part, lda, trow, blockIdx.x, tmask, xsh);
+  tile_gather<AGG, S>(p, part, lda, trow, tile, tmask, xsh);
   __syncthreads();
   constexpr int RPW = TM / NWAVE;
   f4 o[RPW], pre[RPW];
@@ -96,41 +97,63 @@ struct RAcc {
 // wave), columns >= d and rows with !aok read as 0 (clamped loads, then a select), CLAMP:
 // A clamped to +-10 (the time gate's operand); Wp packed by k_pack_weight_kp.  B fragments of
 // the next P k-steps are in flight while a k-step's NT MFMAs issue.
+// Masked A lanes (rows !aok, columns >= d) load from this zero row instead of their row: the
+// loaded value then needs no select, which would make the compiler wait for the load right
+// where it is issued (an s_waitcnt vmcnt(0) per k-block, no prefetch).
+__device__ const f4 kZeroRow[1] = {{0.f, 0.f, 0.f, 0.f}};
+
+constexpr int RT_KB_BYTES = 4 * 4 * 64 * 16;  // one 16-deep k-block of a packed weight: 16 KB
+
+// acc += A[16 rows x K] @ W for the wave's rows: A row of lane l = arow (row l % 16 of the
+// wave), columns >= d and rows with !aok read as 0, CLAMP: A clamped to +-10 (the time gate's
+// operand); Wp packed by k_pack_weight_kp.  The weight streams through LDS: k-block kb + 1
+// (16 KB) is copied by the workgroup's four waves with LDS-DMA (global_load_lds, one quarter
+// each) into the other half of a double buffer while k-block kb's MFMAs run, so each fragment
+// leaves L2 once per workgroup (64 rows), and the waves read it with ds_read_b128.  Every wave
+// of the workgroup must call this with the same Wp and KB (one barrier per k-block).
 template <int NT, bool CLAMP>
 __device__ __forceinline__ void rt_mm(RAcc<NT>& acc, const float* __restrict__ arow, bool aok,
-                                      const float* __restrict__ Wp, int d, int KB) {
-  constexpr int P = 2;
-  const int lane = threadIdx.x & 63, q = lane >> 4;
-  const f4* __restrict__ B = reinterpret_cast<const f4*>(Wp) + lane;
-  const int S = 4 * KB;
-  auto load_a = [&](int kb) {
+                                      const float* __restrict__ Wp, int d, int KB, char* lds) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, w = wave_id();
+  typedef const __attribute__((address_space(1))) f4* gptr;
+  const gptr zrow = (gptr)kZeroRow;
+  auto aptr = [&](int kb) -> gptr {
     const int col = 16 * kb + 4 * q;
-    f4 v = *reinterpret_cast<const f4*>(arow + min(col, d - 4));
-    if (CLAMP) v = clamp4(v, -10.f, 10.f);
-    return (aok & (col < d)) ? v : f4{0.f, 0.f, 0.f, 0.f};
+    return (aok & (col < d)) ? (gptr)(arow + col) : zrow;
   };
-  f4 ring[P][4];
+  const char* wsrc = reinterpret_cast<const char*>(Wp);
+  auto dma = [&](int kb) {  // this wave's quarter of k-block kb into buffer kb & 1
+    char* dst = lds + (kb & 1) * RT_KB_BYTES + w * (RT_KB_BYTES / 4);
+    const char* src = wsrc + (int64_t)kb * RT_KB_BYTES + w * (RT_KB_BYTES / 4) + lane * 16;
 #pragma unroll
-  for (int i = 0; i < P; ++i)
-#pragma unroll
-    for (int jq = 0; jq < 4; ++jq) ring[i][jq] = B[(int64_t)(min(i, S - 1) * 4 + jq) * 64];
-  f4 a = load_a(0);
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
+                                       (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+  };
+  dma(0);
+  f4 a = *aptr(0);
   for (int kb = 0; kb < KB; ++kb) {
-    const f4 an = load_a(min(kb + 1, KB - 1));
+    __syncthreads();  // k-block kb landed (each wave drained its own copies); buffer (kb + 1) & 1 is free
+    if (kb + 1 < KB) dma(kb + 1);
+    const f4 an = *aptr(min(kb + 1, KB - 1));
+    const f4* buf = reinterpret_cast<const f4*>(lds + (kb & 1) * RT_KB_BYTES) + lane;
+    f4 b[2][4];
+#pragma unroll
+    for (int jq = 0; jq < 4; ++jq) b[0][jq] = buf[jq * 64];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int slot = s % P;
+      if (s + 1 < 4) {
+#pragma unroll
+        for (int jq = 0; jq < 4; ++jq) b[(s + 1) & 1][jq] = buf[((s + 1) * 4 + jq) * 64];
+      }
+      const float as = CLAMP ? fminf(fmaxf(a[s], -10.f), 10.f) : a[s];
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        acc.t[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], ring[slot][t >> 2][t & 3], acc.t[t], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      const int nx = min(4 * kb + s + P, S - 1);
-#pragma unroll
-      for (int jq = 0; jq < 4; ++jq) ring[slot][jq] = B[(int64_t)(nx * 4 + jq) * 64];
-      __builtin_amdgcn_sched_barrier(0);
+        acc.t[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(as, b[s & 1][t >> 2][t & 3], acc.t[t], 0, 0, 0);
     }
     a = an;
   }
+  __syncthreads();  // the last buffer is read before a following call refills buffer 0
 }
 
 // ---- per-row maps on the wave's 16 rows (lane l: rows 4 (l / 16) + r, column 16 t + l % 16)
@@ -260,36 +283,40 @@ __device__ __forceinline__ int own_int(const int v[4]) {
 // blend reads them per column tile: no second accumulator set, half the registers).
 enum { RT_LAYER = 0, RT_GATE = 1, RT_STEP = 2, RT_STEP_PRE = 3 };
 template <int NT, int MODE>
-__global__ __launch_bounds__(NTHR) void k_rowtail(LayerArgs p) {
+__global__ __launch_bounds__(NTHR) void k_rowtail(LayerArgs p, int row0) {
   constexpr bool STEP = MODE >= RT_STEP;
+  extern __shared__ char rt_lds[];
   const int lane = threadIdx.x & 63, w = wave_id(), q = lane >> 4;
-  const int base = blockIdx.x * RT_ROWS + 16 * w;
-  const int n_valid = min(16, p.V - base);  // p.V: the length of the row list
-  if (n_valid <= 0) return;
+  const int wg0 = row0 + blockIdx.x * RT_ROWS;
+  const int base = wg0 + 16 * w;
+  const int n_valid = max(0, min(16, p.V - base));  // p.V: the length of the row list
   const int d = p.d, KB = (d + 15) >> 4;
   const int my_i = lane & 15;
-  const int arow_id = p.rows[base + min(my_i, n_valid - 1)];
+  const int arow_id = p.rows[min(base + min(my_i, max(n_valid - 1, 0)), p.V - 1)];
   const bool a_valid = my_i < n_valid;
   const bool a_pos = a_valid & (base + my_i < p.n_pos);
   int crow[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) crow[r] = __shfl(arow_id, 4 * q + r);
-  const int npos_w = min(max(p.n_pos - base, 0), n_valid);  // wave-uniform
+  const int npos_w = min(max(p.n_pos - base, 0), n_valid);
+  // the passes are the workgroup's (every wave takes part in each weight's LDS stream)
+  const int n_wg = min(RT_ROWS, p.V - wg0);
+  const int npos_wg = min(max(p.n_pos - wg0, 0), n_wg);
   const float* xrow = p.x + (int64_t)arow_id * d;
 
   RAcc<NT> v;
   if constexpr (MODE == RT_GATE) {  // the timestep's gate pre-activation, stored as is
     v.zero();
-    rt_mm<NT, true>(v, xrow, a_valid, p.w_gate, d, KB);
+    rt_mm<NT, true>(v, xrow, a_valid, p.w_gate, d, KB, rt_lds);
     rt_store<NT>(v, p.gate_out, crow, n_valid, d);
   }
   v.zero();
   // The products into v, one call site (one copy of the MFMA loop, one accumulator set):
-  // pass 0 = agg @ W_n (in-edge rows), then x @ W_loop / x @ W_evolve -- both in the one wave
-  // where the in-edge rows end (rows masked), one of them everywhere else.
-  const bool p1 = npos_w > 0 && p.agg != nullptr;
+  // pass 0 = agg @ W_n (in-edge rows), then x @ W_loop / x @ W_evolve -- both in the one
+  // workgroup where the in-edge rows end (rows masked), one of them everywhere else.
+  const bool p1 = npos_wg > 0 && p.agg != nullptr;
   if (p1 && !p.w_n) rt_load<NT>(v, p.agg, crow, npos_w, d);  // Lorentz: the centroid rows as is
-  const bool mixed = npos_w > 0 && npos_w < n_valid;
+  const bool mixed = npos_wg > 0 && npos_wg < n_wg;
   const int first = (p1 && p.w_n) ? 0 : 1;
   const int last = p.w_loop ? (mixed ? 3 : 2) : 1;
   for (int pass = first; pass < last; ++pass) {
@@ -297,22 +324,18 @@ __global__ __launch_bounds__(NTHR) void k_rowtail(LayerArgs p) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
     }
-    if (pass == last) break;
     const float* arow = pass == 0 ? p.agg + (int64_t)arow_id * d : xrow;
     const bool ok = pass == 0 ? a_pos : (mixed ? (pass == 1 ? a_pos : a_valid & !a_pos) : a_valid);
-    const float* W = pass == 0 ? p.w_n : (pass == 1 && npos_w > 0 ? p.w_loop : p.w_evolve);
-    rt_mm<NT, false>(v, arow, ok, W, d, KB);
+    const float* W = pass == 0 ? p.w_n : (pass == 1 && npos_wg > 0 ? p.w_loop : p.w_evolve);
+    rt_mm<NT, false>(v, arow, ok, W, d, KB, rt_lds);
   }
   if (first == 0 && last == 1 && !p.euclid) {  // agg @ W_n without a self loop
 #pragma unroll
     for (int t = 0; t < NT; ++t) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
   }
-  if (first == 1 && p1 && !p.euclid) {  // Lorentz rows without a W_n product
-    // (clamped above when a self-loop pass followed; else here)
-    if (last == 1) {
+  if (first == 1 && last == 1 && p1 && !p.euclid) {  // Lorentz rows, no self loop
 #pragma unroll
-      for (int t = 0; t < NT; ++t) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
-    }
+    for (int t = 0; t < NT; ++t) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -343,7 +366,7 @@ __global__ __launch_bounds__(NTHR) void k_rowtail(LayerArgs p) {
     RAcc<NT> g;  // the time gate pre-activation clamp(x_prev) @ W_g (RT_STEP), then its blend
     if constexpr (MODE == RT_STEP) {
       g.zero();
-      rt_mm<NT, true>(g, s.x_prev + (int64_t)arow_id * d, a_valid, s.w_g, d, KB);
+      rt_mm<NT, true>(g, s.x_prev + (int64_t)arow_id * d, a_valid, s.w_g, d, KB, rt_lds);
     }
     float bg[NT];
     rt_col<NT>(bg, s.b_g, d);
@@ -404,23 +427,32 @@ __global__ __launch_bounds__(NTHR) void k_rowtail(LayerArgs p) {
 
 // ----------------------------------------------------------------------------- launchers
 template <int AGG, int S>
-static void launch_gather(const LayerArgs& a, float* out, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((k_gather_agg<AGG, S>), dim3(a.n_pos_tiles), dim3(NTHR), lds, st, a, out);
+static void launch_gather(const LayerArgs& a, float* out, int t0, int t1, size_t lds, hipStream_t st) {
+  hipLaunchKernelGGL((k_gather_agg<AGG, S>), dim3(t1 - t0), dim3(NTHR), lds, st, a, out, t0);
 }
 
 template <int NT>
-static void launch_tail(const LayerArgs& a, unsigned grid, hipStream_t st) {
+static void launch_tail(const LayerArgs& a, int row0, unsigned grid, hipStream_t st) {
+  const size_t lds = 2 * RT_KB_BYTES;
   if (a.fuse_step && a.step.tw)
-    hipLaunchKernelGGL((k_rowtail<NT, RT_STEP_PRE>), dim3(grid), dim3(NTHR), 0, st, a);
+    hipLaunchKernelGGL((k_rowtail<NT, RT_STEP_PRE>), dim3(grid), dim3(NTHR), lds, st, a, row0);
   else if (a.fuse_step)
-    hipLaunchKernelGGL((k_rowtail<NT, RT_STEP>), dim3(grid), dim3(NTHR), 0, st, a);
+    hipLaunchKernelGGL((k_rowtail<NT, RT_STEP>), dim3(grid), dim3(NTHR), lds, st, a, row0);
   else if (a.gate_out)
-    hipLaunchKernelGGL((k_rowtail<NT, RT_GATE>), dim3(grid), dim3(NTHR), 0, st, a);
+    hipLaunchKernelGGL((k_rowtail<NT, RT_GATE>), dim3(grid), dim3(NTHR), lds, st, a, row0);
   else
-    hipLaunchKernelGGL((k_rowtail<NT, RT_LAYER>), dim3(grid), dim3(NTHR), 0, st, a);
+    hipLaunchKernelGGL((k_rowtail<NT, RT_LAYER>), dim3(grid), dim3(NTHR), lds, st, a, row0);
 }
 
+// which == 1: the gather over tiles [lo, hi); which == 2: the tail over rows[lo, hi) (hi <= a.V);
+// which == 3: both, all tiles and rows.
+int layer_rowtail_part(const LayerArgs& a, float* agg, int which, int lo, int hi, hipStream_t st);
+
 int layer_rowtail(const LayerArgs& a, float* agg, hipStream_t st) {
+  return layer_rowtail_part(a, agg, 3, 0, 0, st);
+}
+
+int layer_rowtail_part(const LayerArgs& a, float* agg, int which, int lo, int hi, hipStream_t st) {
   const int mode = a.agg_mode;
   if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "rowtail needs d %% 4 == 0, d <= 256");
   if (!a.x || !a.rows || (!a.h_out && !a.fuse_step)) return set_error(REGCN_EINVAL, "null pointer");
@@ -430,6 +462,7 @@ int layer_rowtail(const LayerArgs& a, float* agg, hipStream_t st) {
   if (mode != AGG_NONE && mode != AGG_UNION && mode != AGG_EUCLID && mode != AGG_LORENTZ)
     return set_error(REGCN_EINVAL, "unknown aggregation mode %d", mode);
   if (a.n_pos > 0 && !agg) return set_error(REGCN_EINVAL, "rowtail needs the agg buffer");
+  if (which < 1 || which > 3) return set_error(REGCN_EINVAL, "bad rowtail part");
   if ((mode == AGG_UNION || mode == AGG_EUCLID) && !a.w_n && a.n_pos > 0)
     return set_error(REGCN_EINVAL, "union / euclid rowtail needs w_n");
   if ((mode == AGG_UNION || mode == AGG_LORENTZ) && a.euclid) return set_error(REGCN_EINVAL, "hyperbolic gather with euclid tail");
@@ -442,7 +475,17 @@ int layer_rowtail(const LayerArgs& a, float* agg, hipStream_t st) {
     if (s.residual && (!s.w_r || !s.b_r)) return set_error(REGCN_EINVAL, "residual radius needs w_r and b_r");
   }
   if (a.V == 0) return 0;
-  if (mode != AGG_NONE && a.n_pos_tiles > 0) {
+  int t0 = 0, t1 = a.n_pos_tiles, r0 = 0, r1 = a.V;
+  if (which == 1) {
+    if (lo < 0 || hi > a.n_pos_tiles || lo > hi) return set_error(REGCN_EINVAL, "bad tile range");
+    t0 = lo;
+    t1 = hi;
+  } else if (which == 2) {
+    if (lo < 0 || hi > a.V || lo > hi) return set_error(REGCN_EINVAL, "bad row range");
+    r0 = lo;
+    r1 = hi;
+  }
+  if ((which & 1) && mode != AGG_NONE && t1 > t0) {
     if (!a.rowptr || !a.col_src || !a.col_type || !a.rel || !a.tiles || !a.item_ptr)
       return set_error(REGCN_EINVAL, "gather needs CSR, rel, tiles and item lists");
     if (mode == AGG_UNION && !a.radius) return set_error(REGCN_EINVAL, "union gather needs radius");
@@ -455,26 +498,28 @@ int layer_rowtail(const LayerArgs& a, float* agg, hipStream_t st) {
     const bool gen = mode == AGG_LORENTZ && s != 1 && s != 2 && s != 4;
     const size_t lds = (size_t)(((TM + NWAVE - 1) * tile_lda(a.d) + 32) + (gen ? NWAVE * MAX_D : 0)) * 4;
     switch (mode) {
-      case AGG_UNION: launch_gather<AGG_UNION, 1>(g, agg, lds, st); break;
-      case AGG_EUCLID: launch_gather<AGG_EUCLID, 1>(g, agg, lds, st); break;
+      case AGG_UNION: launch_gather<AGG_UNION, 1>(g, agg, t0, t1, lds, st); break;
+      case AGG_EUCLID: launch_gather<AGG_EUCLID, 1>(g, agg, t0, t1, lds, st); break;
       default:
-        if (s == 1) launch_gather<AGG_LORENTZ, 1>(g, agg, lds, st);
-        else if (s == 2) launch_gather<AGG_LORENTZ, 2>(g, agg, lds, st);
-        else if (s == 4) launch_gather<AGG_LORENTZ, 4>(g, agg, lds, st);
-        else launch_gather<AGG_LORENTZ, 0>(g, agg, lds, st);
+        if (s == 1) launch_gather<AGG_LORENTZ, 1>(g, agg, t0, t1, lds, st);
+        else if (s == 2) launch_gather<AGG_LORENTZ, 2>(g, agg, t0, t1, lds, st);
+        else if (s == 4) launch_gather<AGG_LORENTZ, 4>(g, agg, t0, t1, lds, st);
+        else launch_gather<AGG_LORENTZ, 0>(g, agg, t0, t1, lds, st);
     }
     const int rc = check_launch("k_gather_agg");
     if (rc) return rc;
   }
+  if (!(which & 2) || r1 <= r0) return 0;
   LayerArgs t = a;
   t.agg = agg;
+  t.V = r1;
   if (mode == AGG_LORENTZ) t.w_n = nullptr;  // the centroid rows are the aggregation itself
-  const unsigned grid = (unsigned)((a.V + RT_ROWS - 1) / RT_ROWS);
+  const unsigned grid = (unsigned)((r1 - r0 + RT_ROWS - 1) / RT_ROWS);
   const int nt = (a.d + 15) / 16;
-  if (nt <= 4) launch_tail<4>(t, grid, st);
-  else if (nt <= 8) launch_tail<8>(t, grid, st);
-  else if (nt <= 13) launch_tail<13>(t, grid, st);
-  else launch_tail<16>(t, grid, st);
+  if (nt <= 4) launch_tail<4>(t, r0, grid, st);
+  else if (nt <= 8) launch_tail<8>(t, r0, grid, st);
+  else if (nt <= 13) launch_tail<13>(t, r0, grid, st);
+  else launch_tail<16>(t, r0, grid, st);
   return check_launch("k_rowtail");
 }
 

@@ -61,6 +61,7 @@ _SIGS = {
     "regcn_rank_count_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
     "regcn_layer_f32": [P, P],
     "regcn_layer_rowtail_f32": [P, P, P],
+    "regcn_layer_rowtail_part_f32": [P, P, _c_int, _c_int, _c_int, P],
     "regcn_packed_weight_kp_floats": [_c_int],
     "regcn_pack_weight_kp_f32": [P, _c_int, _c_int, P, P],
     "regcn_timestep_phase_f32": [P, _c_int, P],

@@ -27,6 +27,41 @@ TRACE = None  # int64 HIP tensor (>= 8 x workgroups) to record k_layer phase tim
 # Snapshots with at least this many rows run a layer as the agg gather + the 64-row MFMA tail
 # (regcn_layer_rowtail_f32, csrc/rowtail.hip) instead of the fused 16-row kernel; 0 disables.
 ROWTAIL_MIN_ROWS = int(os.environ.get("REGCN_ROWTAIL_MIN_ROWS", "65536"))
+# ... in this many row chunks: the gather of chunk i + 1 runs on a side stream beside the tail of
+# chunk i (the L2-bound gather beside the MFMA-bound tail); 1 = one stream, no pipelining
+ROWTAIL_CHUNKS = int(os.environ.get("REGCN_ROWTAIL_CHUNKS", "1"))
+
+
+def _rowtail_chunks(g, k):
+    """[(tile0, tile1, row0, row1)]: k chunks of the rows list, cut at tile starts (each chunk's
+    gather covers exactly the in-edge rows its tail needs), the rows without in-edges in the
+    last; cached on the graph (one host copy of the tile starts)."""
+    hit = g.__dict__.get("_rt_chunks")
+    if hit is not None and hit[0] == k:
+        return hit[1]
+    if torch.cuda.is_current_stream_capturing():
+        return None  # no host copy inside a capture: this launch runs unchunked
+    wk = g.work()
+    n_t, n_rows = int(g.n_pos_tiles), int(wk["rows"].shape[0])
+    starts = wk["tiles"][:n_t, 0].cpu().tolist() if n_t else []
+    k = max(1, min(k, n_t)) if n_t else 1
+    tb = [round(i * n_t / k) for i in range(k + 1)]
+    rb = [starts[t] if t < n_t else n_rows for t in tb]
+    rb[0], rb[-1] = 0, n_rows
+    out = [(tb[i], tb[i + 1], rb[i], rb[i + 1]) for i in range(k)]
+    g.__dict__["_rt_chunks"] = (k, out)
+    return out
+
+
+_RT_STREAMS = {}
+
+
+def _rowtail_stream(dev):
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    st = _RT_STREAMS.get(key)
+    if st is None:
+        st = _RT_STREAMS[key] = torch.cuda.Stream(dev)
+    return st
 
 
 def _drop_mask(layer, like):
@@ -250,8 +285,30 @@ def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c,
         if step.tw is not None:
             desc.step_tw = a(step.tw)
             keep.append(step.tw)
-    _lib.check(_lib.lib().regcn_layer_rowtail_f32(ctypes.byref(desc), _lib.fptr(agg), _lib.stream()),
-               "regcn_layer_rowtail_f32(step)" if step is not None else "regcn_layer_rowtail_f32")
+    name = "regcn_layer_rowtail_f32(step)" if step is not None else "regcn_layer_rowtail_f32"
+    chunks = _rowtail_chunks(g, ROWTAIL_CHUNKS) if (ROWTAIL_CHUNKS > 1 and g.n_pos_tiles > 1
+                                                     and mode != _lib.AGG_NONE) else None
+    if chunks is None or len(chunks) < 2:
+        _lib.check(_lib.lib().regcn_layer_rowtail_f32(ctypes.byref(desc), _lib.fptr(agg), _lib.stream()), name)
+        return h, xn, rn
+    # gathers on the side stream, chunk by chunk; each tail chunk waits for its gather only
+    part = _lib.lib().regcn_layer_rowtail_part_f32
+    cur = torch.cuda.current_stream(x.device)
+    side = _rowtail_stream(x.device)
+    side.wait_stream(cur)
+    events = []
+    with torch.cuda.stream(side):
+        for t0, t1, _, _ in chunks:
+            _lib.check(part(ctypes.byref(desc), _lib.fptr(agg), 1, t0, t1, _lib.stream()), name + "[gather]")
+            ev = torch.cuda.Event()
+            ev.record(side)
+            events.append(ev)
+    for (_, _, r0, r1), ev in zip(chunks, events):
+        cur.wait_event(ev)
+        _lib.check(part(ctypes.byref(desc), _lib.fptr(agg), 2, r0, r1, _lib.stream()), name)
+    # the last tail waited for the last gather event, so every side-stream read is joined into
+    # `cur` here: x, r, rel and agg may be freed on `cur` afterwards (and, under capture, the
+    # fork joins back into the captured stream)
     return h, xn, rn
 
 
