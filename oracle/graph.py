@@ -32,6 +32,34 @@ def r2e(triples, num_rels):
     return uniq_r.astype(np.int64), np.asarray(spans, dtype=np.int64).reshape(-1, 2), r_to_e
 
 
+def row_subgraph(num_nodes, num_rels, triples, rows):
+    """build_sub_graph restricted to the in-edges of `rows` (for pinning single rows of a graph
+    too large for the whole-graph oracle): the edges whose destination is in `rows`, in the
+    reference's order, relabelled onto the compact node list `nodes` = rows followed by the
+    other sources; in_deg / norm are the full graph's (rgcn/utils.py:110-114), so the rows'
+    layer outputs equal the whole-graph ones.  Returns (g, nodes)."""
+    triples = np.asarray(triples, dtype=np.int64).reshape(-1, 3)
+    rows = np.asarray(rows, dtype=np.int64)
+    s, r, o = triples[:, 0], triples[:, 1], triples[:, 2]
+    in_deg = np.bincount(o, minlength=num_nodes) + np.bincount(s, minlength=num_nodes)
+    pick = np.zeros(num_nodes, bool)
+    pick[rows] = True
+    fwd, inv = pick[o], pick[s]
+    src = np.concatenate([s[fwd], o[inv]])
+    dst = np.concatenate([o[fwd], s[inv]])
+    etype = np.concatenate([r[fwd], r[inv] + num_rels])
+    extra = np.setdiff1d(np.unique(src), rows)
+    nodes = np.concatenate([rows, extra])
+    pos = np.full(num_nodes, -1, np.int64)
+    pos[nodes] = np.arange(nodes.size)
+    deg = in_deg[nodes].astype(np.int64)
+    deg_f = deg.astype(np.float32)
+    deg_f[deg_f == 0] = 1.0
+    norm = (np.float32(1.0) / deg_f).astype(np.float32)
+    return {"num_nodes": int(nodes.size), "src": pos[src], "dst": pos[dst], "type": etype, "in_deg": deg,
+            "norm": norm}, nodes
+
+
 def build_sub_graph(num_nodes, num_rels, triples):
     """rgcn/utils.py:100-134 restated without DGL.
 

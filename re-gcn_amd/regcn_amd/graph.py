@@ -530,6 +530,13 @@ def blocked_span_chunks(span_rows, span_beg, span_len, keys, block, chunk, xcds=
     return out.to(torch.int32), np.asarray(fixups, dtype=np.int32).reshape(-1, 4), nslot + 1
 
 
+def spread_block(num_keys, block, xcds=_XCDS, per_xcd=2):
+    """The block size blocked_span_chunks uses over `num_keys` key ids: `block`, shrunk so the
+    key range holds at least per_xcd * xcds blocks (otherwise a small key range lands every
+    chunk in a few XCD queues and pads the others with empty chunks)."""
+    return max(64, min(int(block), -(-int(num_keys) // (per_xcd * xcds))))
+
+
 def rel_block_lists(rel_idx, rel_start, rel_len, block, chunk=REL_BLOCK_CHUNK):
     """blocked_span_chunks over the forward relations' r_to_e spans (numpy in and out)."""
     rel_len = np.asarray(rel_len, dtype=np.int64)
@@ -547,13 +554,16 @@ def rel_block_work(g, R):
     if hit is not None:
         return hit[0]
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-        return None  # built with host round trips: not inside a HIP-graph capture (plain chunks)
+        # built with host round trips, so not inside a HIP-graph capture: the plain chunks, and
+        # cached, so later eager runs sum in the same order as the captured graph
+        g.__dict__["_rel_block"] = (None,)
+        return None
     wk = g.work()
     res = None
     if REL_BLOCK > 0 and int(wk["rel_idx"].numel()) // 2 >= REL_BLOCK_MIN_PAIRS:
         dev = wk["rel_idx"].device
         ch, fx, ns = blocked_span_chunks(torch.arange(R, device=dev), wk["rel_start"][:R], wk["rel_count"][:R].long(),
-                                         wk["rel_idx"], REL_BLOCK, REL_BLOCK_CHUNK)
+                                         wk["rel_idx"], spread_block(g.number_of_nodes(), REL_BLOCK), REL_BLOCK_CHUNK)
         res = (ch, torch.from_numpy(fx).to(dev), ns)
         from . import _lib
         _lib.publish()
@@ -577,7 +587,8 @@ def hub_block_work(g):
     if hit is not None:
         return hit[0]
     if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
-        return None  # built with host round trips: not inside a HIP-graph capture (plain chunks)
+        g.__dict__["_hub_block"] = (None,)  # as rel_block_work: plain chunks, cached
+        return None
     res = None
     wk = g.work()
     hc = wk["heavy_chunks"]
@@ -587,7 +598,7 @@ def hub_block_work(g):
         ln = wk["rowptr"].long()[rows + 1] - beg
         if int(ln.sum()) >= HUB_BLOCK_MIN_EDGES:
             ss = g.row_src_cols()
-            ch, fx, ns = blocked_span_chunks(rows, beg, ln, ss, HUB_BLOCK, max(int(getattr(g, "chunk_edges", None) or 1024), 64))
+            ch, fx, ns = blocked_span_chunks(rows, beg, ln, ss, spread_block(g.number_of_nodes(), HUB_BLOCK), max(int(getattr(g, "chunk_edges", None) or 1024), 64))
             res = (ch, torch.from_numpy(fx).to(ss.device), ns)
             from . import _lib
             _lib.publish()

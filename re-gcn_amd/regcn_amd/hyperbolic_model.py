@@ -940,7 +940,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
         self.rdecoder.c = c_dec
         parts = []
         n = triples.shape[0]
-        per_group = max(1, int(group_budget) // max(1, 2 * batch_size * max(self.num_ents, 2 * self.num_rels)))
+        per_group = self._loss_group_size(batch_size, group_budget, torch.is_tensor(c_dec) and c_dec.requires_grad)
         for g0 in range(0, n, per_group * batch_size):
             g1 = min(n, g0 + per_group * batch_size)
             vecs = self._decode_losses(cut[0], cut[1], triples[g0:g1], c_dec, batch_size=batch_size)
@@ -958,6 +958,22 @@ class HyperbolicRecurrentRGCN(nn.Module):
         if roots:
             torch.autograd.backward([r[0] for r in roots], [r[1] for r in roots])
         return parts
+
+    # per-element footprint (in fp32 words) of the B x N decoder blocks a group holds: the fused
+    # fp32 CE keeps one backward coefficient per element; the dense fp64 paths (a learned
+    # curvature's _ce_c_term S matrix and its retained pair terms, the relation-specific
+    # curvature's arctanh-distance score) keep fp64 intermediates and their autograd state,
+    # measured at ~150 B per element (tests/test_gpu_training.py::test_loss_batches_memory_dense_fp64)
+    DENSE_FP64_WORDS = 40
+
+    def _loss_group_size(self, batch_size, group_budget, learned_c):
+        """Mini-batches decoded together by get_loss_batches: the group's B x max(|V|, 2R)
+        blocks (queries and their inverses) stay under `group_budget` fp32 words."""
+        words = 1
+        if learned_c or self.use_relation_specific_curvature:
+            words = self.DENSE_FP64_WORDS
+        per_elem = 2 * batch_size * max(self.num_ents, 2 * self.num_rels) * words
+        return max(1, int(group_budget) // max(1, per_elem))
 
     def _decode_losses(self, pre_emb, r_emb, triples, c_val, batch_size=None):
         """hyperbolic_model.py:996-1073: decoders on the final embedding + radius loss.

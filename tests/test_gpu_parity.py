@@ -303,14 +303,15 @@ def test_get_loss_vs_golden(golden, tag):
     assert_close(got, z["losses"], what="losses")
 
 
-@pytest.mark.parametrize("tag", ["noln", "ln"])
+@pytest.mark.parametrize("tag", ["noln", "ln", "ln_d200"])
 def test_euclid_model_vs_golden(golden, tag):
+    """RecurrentRGCN + ConvTransE (src/rrgcn.py:142-194); ln_d200: d = 200 at ICEWS14s' R = 230."""
     from regcn_amd import graph as G
     from regcn_amd.rrgcn import RecurrentRGCN
     z = golden("rrgcn_%s.npz" % tag)
     V, R, d, T = (int(v) for v in z["meta"])
     m = RecurrentRGCN("convtranse", "uvrgcn", V, R, 0, 0, d, "sub", T, num_bases=100, num_basis=100,
-                      num_hidden_layers=2, dropout=0.2, self_loop=True, layer_norm=(tag == "ln"),
+                      num_hidden_layers=2, dropout=0.2, self_loop=True, layer_norm=tag.startswith("ln"),
                       input_dropout=0.2, hidden_dropout=0.2, feat_dropout=0.2, entity_prediction=True,
                       relation_prediction=True, use_cuda=True, gpu=0)
     m.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in z.items() if k.startswith("sd_")})

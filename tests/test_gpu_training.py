@@ -247,3 +247,33 @@ def test_encoder_reuse_same_gradients(golden, tag):
         if k in ref:
             err = float((p.grad - ref[k]).abs().max()) / max(1e-3, float(ref[k].abs().max()))
             assert err <= 1e-4, (k, err)
+
+
+@pytest.mark.parametrize("learned_c,crel", [(True, False), (False, True)])
+def test_loss_batches_memory_dense_fp64(learned_c, crel):
+    """get_loss_batches' mini-batch groups on the dense fp64 decoder paths (a learned
+    curvature's S matrix, the relation-specific curvature's arctanh-distance score) are sized
+    for their fp64 B x N intermediates: at ICEWS18's |V| = 23,033 and batch 1024 one mini-batch
+    per group (5 before), and the peak stays near one group's budgeted footprint."""
+    from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
+    from regcn_amd.synthetic import zipf_triples
+    V, R, d, bs = 23_033, 256, 64, 1024
+    rng = np.random.default_rng(9)
+    torch.manual_seed(9)
+    m = HyperbolicRecurrentRGCN("roth", "hyperbolic_uvrgcn", V, R, 0, 0, d, "sub", 2, num_bases=d // 2,
+                                num_hidden_layers=2, dropout=0.0, c=C, self_loop=True, entity_prediction=True,
+                                relation_prediction=True, use_cuda=True, gpu=0, learn_curvature=learned_c,
+                                use_relation_specific_curvature=crel).to(DEV).train()
+    glist = [G.build_sub_graph(V, R, zipf_triples(rng, V, R, 20_000), True, DEV) for _ in range(2)]
+    batch = torch.from_numpy(zipf_triples(rng, V, R, 4 * bs)).to(DEV)
+    assert m._loss_group_size(bs, 1 << 28, learned_c) == 1
+    assert m._loss_group_size(bs, 1 << 28, False) == (1 if crel else 5)
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats()
+    base = torch.cuda.memory_allocated()
+    parts = m.get_loss_batches(glist, batch, None, True, bs)
+    torch.cuda.synchronize()
+    peak = torch.cuda.max_memory_allocated() - base
+    assert len(parts) == 4
+    one_group = 2 * bs * V * 4 * m.DENSE_FP64_WORDS  # the budgeted bytes of one mini-batch
+    assert peak < 1.25 * one_group, "peak %.2f GB over one group's %.2f GB" % (peak / 2 ** 30, one_group / 2 ** 30)

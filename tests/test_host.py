@@ -308,3 +308,37 @@ def test_analysis_containers_on_host():
     gn = m.log_gradient_stats()
     assert abs(float(gn) - math.sqrt(sum(p.numel() for p in m.parameters()))) < 1e-3
     assert len(m.training_stats["gradient_norms"]) == 1
+
+
+def test_loss_group_size_dense_fp64():
+    """the dense fp64 decoder paths group DENSE_FP64_WORDS x fewer mini-batches than the fused CE."""
+    import types
+    from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN as M
+    ns = types.SimpleNamespace(num_ents=23033, num_rels=256, use_relation_specific_curvature=False,
+                               DENSE_FP64_WORDS=M.DENSE_FP64_WORDS)
+    assert M._loss_group_size(ns, 1024, 1 << 28, False) == 5
+    assert M._loss_group_size(ns, 1024, 1 << 28, True) == 1
+    ns.use_relation_specific_curvature = True
+    assert M._loss_group_size(ns, 1024, 1 << 28, False) == 1
+    ns.num_ents = 500
+    assert M._loss_group_size(ns, 64, 1 << 28, False) == (1 << 28) // (2 * 64 * 512 * M.DENSE_FP64_WORDS)
+
+
+def test_spread_block_fills_every_xcd_queue():
+    """a small key range (V < 8 blocks) with many pairs spreads its chunks over all 8
+    XCD queues once the block is shrunk by graph.spread_block (the default block put them all in
+    one queue and padded the other seven)."""
+    rng = np.random.default_rng(1)
+    V, R = 20000, 4
+    lists = [np.unique(rng.integers(0, V, size=15000)) for _ in range(R)]
+    lens = np.array([len(x) for x in lists])
+    idx = np.concatenate(lists + lists)
+    start = np.cumsum(lens) - lens
+    fill = []
+    for block in (G.REL_BLOCK * 8, G.spread_block(V, G.REL_BLOCK * 8)):
+        ch, _, _ = G.rel_block_lists(idx, start, lens, block, chunk=256)
+        p = np.arange(len(ch))
+        real = ch[:, 2] > ch[:, 1]
+        fill.append((np.bincount(((p // 4) % 8)[real], minlength=8) > 0).sum())
+    assert fill == [1, 8], fill
+    assert G.spread_block(V, 64) == 64 and G.spread_block(10 ** 6, 4096) == 4096

@@ -17,6 +17,7 @@ Each fixture pins one row of SURVEY.md §8(a):
   model_*.npz          a9  HyperbolicRecurrentRGCN.predict / get_loss   hyperbolic_model.py:722-1088
                            (models_large: d = 200 at the ICEWS18 / GDELT shapes, predict only)
   rrgcn_*.npz          a9  RecurrentRGCN.predict             src/rrgcn.py:142-194
+                           (rrgcn_ln_d200: d = 200 at ICEWS14s' R = 230; "rrgcn_large")
   score.npz            a11/a12 chunked dist score / CE       hyperbolic_decoder.py:89-307
   rank.npz             f2  get_total_rank / filter_score     rgcn/utils.py:21-166
   multistep.npz        f2  filtered scores left by get_total_rank -> construct_snap(_r)
@@ -542,12 +543,14 @@ def gen_train():
     torch.Tensor.cuda = lambda self, *a, **k: self  # noqa: E731
 
 
-def gen_rrgcn():
-    V, R, d, T = 256, 64, 64, 3
-    snaps = snapshot_series(30, V, R, T + 1, 120)
+def gen_rrgcn(large=False):
+    """rrgcn_{noln,ln}: V 256, R 64, d 64; large: rrgcn_ln_d200 at ICEWS14s' relation count
+    (R = 230) and the paper's d = 200, V 1500, 3000 triples per snapshot."""
+    V, R, d, T = (1500, 230, 200, 3) if large else (256, 64, 64, 3)
+    snaps = snapshot_series(31 if large else 30, V, R, T + 1, 3000 if large else 120)
     glist = [rutils.build_sub_graph(V, R, s, False, "cpu") for s in snaps[:T]]
-    test = torch.from_numpy(snaps[T])
-    for i, ln in enumerate((False, True)):
+    test = torch.from_numpy(snaps[T][:200] if large else snaps[T])
+    for i, ln in enumerate((True,) if large else (False, True)):
         torch.manual_seed(200 + i)
         m = RecurrentRGCN("convtranse", "uvrgcn", V, R, 0, 0, d, "sub", T, num_bases=100,
                           num_basis=100, num_hidden_layers=2, dropout=0.2, self_loop=True,
@@ -558,14 +561,14 @@ def gen_rrgcn():
         with torch.no_grad():
             embs, _, h0, _, _ = m.forward(glist, None, False)
             all_tr, score, score_rel = m.predict(glist, R, None, test.clone(), False)
-        out = {"meta": np.array([V, R, d, T]), "test": snaps[T], "all_triples": all_tr.numpy(),
+        out = {"meta": np.array([V, R, d, T]), "test": test.numpy(), "all_triples": all_tr.numpy(),
                "score": score.numpy(), "score_rel": score_rel.numpy(), "h0": h0.numpy(),
                "embs": torch.stack(embs).numpy()}
         for t in range(T):
             out["snap%d" % t] = snaps[t]
         for k, v in m.state_dict().items():
             out["sd_" + k] = v.numpy().copy()
-        save("rrgcn_%s.npz" % ("ln" if ln else "noln"), **out)
+        save("rrgcn_%s%s.npz" % ("ln" if ln else "noln", "_d200" if large else ""), **out)
 
 
 def gen_score():
@@ -784,7 +787,7 @@ if __name__ == "__main__":
                              "score", "rank", "train"]
     table = {"graph": gen_graph_indexing, "ops": gen_ops, "union": gen_layer_union,
              "euclid": gen_layer_euclid, "lorentz": gen_layer_lorentz, "models": gen_models,
-             "rrgcn": gen_rrgcn, "score": gen_score, "rank": gen_rank, "train": gen_train,
+             "rrgcn": gen_rrgcn, "rrgcn_large": lambda: gen_rrgcn(True), "score": gen_score, "rank": gen_rank, "train": gen_train,
              "models_large": gen_models_large, "dataset": gen_dataset, "train_curvature": gen_train_curvature,
              "multistep": gen_multistep, "analysis": gen_analysis}
     for w in which:
