@@ -16,6 +16,7 @@
 // LDS in 16-deep chunks.  Epilogues: write S (score), or per-tile (max, sum exp)
 // partials + target logit for a fused cross entropy (never materialising B x N).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "regcn_internal.h"
@@ -584,6 +585,230 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   stamp(2);
 }
 
+// Wave-specialised fp32 scorer: the same workgroup tile (128 queries, strips of 64-candidate
+// tiles, XCD-aware order) with the roles split so the epilogue never holds the matrix core.
+// Waves 0-3 (one per SIMD) are MFMA waves: wave w keeps queries [32w, 32w + 32) in registers
+// (two 16-row A groups sharing every B fragment) and only multiplies, handing each tile's
+// accumulators to LDS.  Waves 4-7 (the other wave of each SIMD) are epilogue waves: wave 4 + w
+// reads MFMA wave w's accumulators, stages the next candidate tiles (global -> registers -> LDS)
+// and runs the score / cross-entropy epilogue of tile i - 1 and its stores while the MFMA waves
+// multiply tile i, so their VALU work and stores issue beside the MFMAs.  Two barriers per
+// tile: B' (after MFMA block WS_MID: the previous accumulators have been read, the next tile
+// may be staged) and B (tile i multiplied, its accumulators in LDS, tile i + 1 staged).
+constexpr int WS_MID = 2;
+__host__ __device__ inline size_t score_ws_exch_floats() { return (size_t)4 * 8 * 4 * 64; }  // waves x acc f4 x lanes
+inline size_t score_ws_lds(int d) { return score_f32_lds(d) + score_ws_exch_floats() * 4; }
+
+template <int MODE>
+__device__ __forceinline__ void score_ws_body(ScoreArgs p, const int blk, const int nblk) {
+  extern __shared__ float Es[];  // 2 x SN x SE candidate rows | 2 x SN |e|^2 | exchange
+  p.scale = p.scale_p ? *p.scale_p : 1.f;
+  if (p.scale_raw && p.scale_p) p.scale = (p.scale > 20.f ? p.scale : log1pf(expf(p.scale))) + 1e-6f;
+  p.margin = p.margin_p ? *p.margin_p : 0.f;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool mfma_wave = wv < 4;  // wave-uniform role
+  const int grpw = wv & 3;        // the 32-query group of this wave (MFMA wave and its epilogue wave)
+  const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
+  const int nbn = (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
+  const int S = nblk / (8 * nbq);
+  const int xcd = blk & 7, rk = blk >> 3;
+  const int bq = rk % nbq, stripe = rk / nbq;
+  auto tile_of = [&](int i) { return xcd + 8 * (stripe + S * i); };
+  const int q0 = bq * SQ2 + 32 * grpw;
+  const int g4 = 4 * (lane >> 4);
+  float* e2s = Es + 2 * SN * SE;
+  f4* exch = reinterpret_cast<f4*>(Es + 2 * SN * SE + 2 * SN) + (size_t)grpw * 8 * 64;  // [8 acc][64 lanes]
+  const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  float run_m[2][4], run_se[2][4];
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) run_m[g][r] = -INFINITY, run_se[g][r] = 0.f;
+  auto ce_flush = [&]() {  // epilogue waves: this wave's 32 queries, partial xcd + 8 stripe
+    const int np = 8 * S, pidx = xcd + 8 * stripe;
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = q0 + 16 * g + 4 * (lane >> 4) + r;
+        const float M = row16_max(run_m[g][r]);
+        const float Ml = (M == -INFINITY ? 0.f : M) * LOG2E;
+        const float se = row16_sum(run_se[g][r] * __builtin_amdgcn_exp2f(fmaf(run_m[g][r], LOG2E, -Ml)));
+        if ((lane & 15) == 0 && q < p.B) {
+          float* o = p.part + ((int64_t)q * np + pidx) * 2;
+          o[0] = M;
+          o[1] = se;
+        }
+      }
+  };
+  int bn = tile_of(0);
+  if (bn >= nbn) {  // no work for this stripe (whole workgroup, before any barrier)
+    if (MODE == 1 && !mfma_wave) ce_flush();
+    return;
+  }
+  if (mfma_wave) {
+    // ---------------------------------------------------------------- MFMA waves
+    f4 a[2][KB_MAX];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int qr = q0 + 16 * g + (lane & 15);
+      const bool q_ok = qr < p.B;
+      const float* qrow = p.q + (int64_t)min(qr, p.B - 1) * d;
+#pragma unroll
+      for (int b = 0; b < KB_MAX; ++b) {
+        const f4 v = *reinterpret_cast<const f4*>(qrow + min(16 * b + g4, d - 4));
+        a[g][b] = (q_ok & (b < KB) & (16 * b + g4 < d)) ? v : z4;
+      }
+    }
+    __syncthreads();  // P: tile 0 staged
+    int cur = 0;
+    for (int i = 0;; ++i) {
+      const bool more = tile_of(i + 1) < nbn;
+      const float* brow = Es + cur * SN * SE + (lane & 15) * SE + g4;
+      f4 acc[2][4] = {{z4, z4, z4, z4}, {z4, z4, z4, z4}};
+      f4 bb[2][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bb[0][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE);
+#pragma unroll
+      for (int b = 0; b < KB_MAX; ++b) {
+        if (b < KB) {  // wave-uniform
+          const int bnx = min(b + 1, KB - 1);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            bb[(b + 1) & 1][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE + 16 * bnx);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int g = 0; g < 2; ++g)
+                acc[g][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][b][e], bb[b & 1][j][e], acc[g][j], 0, 0, 0);
+        }
+        if (b == min(WS_MID, KB - 1)) __syncthreads();  // B': the previous accumulators were read
+      }
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) exch[(g * 4 + j) * 64 + lane] = acc[g][j];
+      __syncthreads();  // B: accumulators in LDS, next tile staged
+      if (!more) break;
+      cur ^= 1;
+    }
+    return;
+  }
+  // ------------------------------------------------------------------ epilogue waves
+  const int et = tid - 256;  // 0..255
+  // |q|^2 of this lane's C rows (queries q0 + 16 g + 4 (lane >> 4) + r)
+  float x2[2][4];
+  int qi[2][4];
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    const int qr = q0 + 16 * g + (lane & 15);
+    const bool q_ok = qr < p.B;
+    const float* qrow = p.q + (int64_t)min(qr, p.B - 1) * d;
+    float xs = 0.f;
+    for (int b = 0; b < KB; ++b) {
+      const f4 v = *reinterpret_cast<const f4*>(qrow + min(16 * b + g4, d - 4));
+      const f4 w = (q_ok & (16 * b + g4 < d)) ? v : z4;
+      xs += dot4(w, w);
+    }
+    xs += __shfl_xor(xs, 16);
+    xs += __shfl_xor(xs, 32);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int li = 4 * (lane >> 4) + r;
+      x2[g][r] = __shfl(xs, li);
+      qi[g][r] = q0 + 16 * g + li;
+    }
+  }
+  // staging map: 4 epilogue threads per candidate row, float4 units sub + 4 it
+  constexpr int IT = KB_MAX;
+  const int sr = et >> 2, sub = et & 3, per_row = 4 * KB;
+  f4 v[IT];
+  auto fetch = [&](int t) {
+    const float* erow = p.e + (int64_t)min(t * SN + sr, p.N - 1) * d;
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+      if (it < KB) v[it] = *reinterpret_cast<const f4*>(erow + min((sub + 4 * it) * 4, d - 4));
+  };
+  auto stash = [&](int buf, int t) {
+    const bool row_ok = t * SN + sr < p.N;
+    float* lrow = Es + buf * SN * SE + sr * SE;
+    float ss = 0.f;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      if (it < KB) {
+        const int u = sub + 4 * it;
+        const f4 w = (row_ok & (4 * u < d)) ? v[it] : z4;
+        ss += dot4(w, w);
+        if (u < per_row) *reinterpret_cast<f4*>(lrow + 4 * u) = w;
+      }
+    }
+    ss += __shfl_xor(ss, 1);
+    ss += __shfl_xor(ss, 2);
+    if (sub == 0) e2s[buf * SN + sr] = ss;
+  };
+  fetch(bn);
+  stash(0, bn);
+  if (tile_of(1) < nbn) fetch(tile_of(1));
+  __syncthreads();  // P
+  int cur = 0;
+  // tile i - 1's accumulators and candidate factors, read right after B(i - 1) (its LDS buffer
+  // is restaged with tile i + 1 after B'(i))
+  f4 acc[2][4];
+  float y2[4], bn_[4];
+  int ni[4], prev_bn = -1;
+  auto take = [&](int tb, int buf) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[g][j] = exch[(g * 4 + j) * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      ni[j] = tb * SN + 16 * j + (lane & 15);
+      y2[j] = e2s[buf * SN + 16 * j + (lane & 15)];
+      bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
+    }
+    prev_bn = tb;
+  };
+  auto epilogue = [&]() {
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+      score_epilogue_fast<MODE>(p, acc[g], x2[g], y2, bn_, qi[g], ni, lane, prev_bn, run_m[g], run_se[g]);
+  };
+  for (int i = 0;; ++i) {
+    const int bn_next = tile_of(i + 1), bn_next2 = tile_of(i + 2);
+    const bool more = bn_next < nbn;
+    __syncthreads();  // B'
+    if (more) {
+      stash(cur ^ 1, bn_next);  // tile i - 1's buffer: read by the MFMA waves before B(i - 1)
+      if (MODE != 2 && bn_next2 < nbn) fetch(bn_next2);
+    }
+    if (prev_bn >= 0) epilogue();  // tile i - 1
+    if (MODE == 2 && more && bn_next2 < nbn) fetch(bn_next2);
+    __syncthreads();  // B: tile i's accumulators in LDS
+    take(bn, cur);
+    if (!more) break;
+    cur ^= 1;
+    bn = bn_next;
+  }
+  epilogue();
+  if (MODE == 1) ce_flush();
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_score_ws(ScoreArgs p) {
+  score_ws_body<MODE>(p, blockIdx.x, gridDim.x);
+}
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_score_ws_jobs(ScoreArgs p0, ScoreArgs p1,
+                                                                                             int g0) {
+  if ((int)blockIdx.x < g0) score_ws_body<0>(p0, blockIdx.x, g0);
+  else score_ws_body<0>(p1, blockIdx.x - g0, gridDim.x - g0);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32(ScoreArgs p) {
   score_f32_body<MODE>(p, blockIdx.x, gridDim.x);
@@ -657,6 +882,19 @@ __global__ __launch_bounds__(256) void k_rank(const float* __restrict__ S, int B
   }
 }
 
+// REGCN_SCORE_WS=1 selects the wave-specialised scorer (k_score_ws) for A/B measurement; the
+// default is the uniform-wave k_score_f32 (config 5, 5 predicts: 4.15 ms vs 5.35 ms per call
+// for k_score_ws_jobs, profiles/r4_score_ws_kernel_stats.csv).
+constexpr size_t SCORE_LDS_MAX = 160 * 1024;  // gfx950 LDS per workgroup (d > 224 keeps k_score_f32)
+static bool score_ws() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("REGCN_SCORE_WS");
+    v = e ? atoi(e) : 0;
+  }
+  return v != 0;
+}
+
 int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   if (a.d <= 0 || (a.d & 3)) return set_error(REGCN_EINVAL, "score needs d %% 4 == 0");
   if (!a.q || !a.e) return set_error(REGCN_EINVAL, "null pointer");
@@ -670,15 +908,18 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   const bool fast = !a.use_dist && a.d <= 16 * KB_MAX;
   const dim3 g2(score_f32_grid(a.B, nbn)), b2(64 * SW2);
   const size_t lds2 = score_f32_lds(a.d);
+  const bool ws = fast && score_ws() && score_ws_lds(a.d) <= SCORE_LDS_MAX;
   if (mode == 0) {
     if (!a.out) return set_error(REGCN_EINVAL, "null output");
-    if (fast) hipLaunchKernelGGL((k_score_f32<0>), g2, b2, lds2, st, a);
+    if (ws) hipLaunchKernelGGL((k_score_ws<0>), g2, dim3(512), score_ws_lds(a.d), st, a);
+    else if (fast) hipLaunchKernelGGL((k_score_f32<0>), g2, b2, lds2, st, a);
     else if (a.use_dist) hipLaunchKernelGGL((k_score<0, true>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_score<0, false>), g, b, 0, st, a);
     return check_launch("k_score");
   }
   if (!a.target || !a.part || !a.tgt_logit || !loss) return set_error(REGCN_EINVAL, "CE needs target/workspace/loss");
-  if (fast) hipLaunchKernelGGL((k_score_f32<1>), g2, b2, lds2, st, a);
+  if (ws) hipLaunchKernelGGL((k_score_ws<1>), g2, dim3(512), score_ws_lds(a.d), st, a);
+  else if (fast) hipLaunchKernelGGL((k_score_f32<1>), g2, b2, lds2, st, a);
   else if (a.use_dist) hipLaunchKernelGGL((k_score<1, true>), g, b, 0, st, a);
   else hipLaunchKernelGGL((k_score<1, false>), g, b, 0, st, a);
   int rc = check_launch("k_score_ce");
@@ -703,7 +944,10 @@ int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st) {
     return 0;
   }
   const unsigned g0 = score_f32_grid(a0.B, (a0.N + SN - 1) / SN), g1 = score_f32_grid(a1.B, (a1.N + SN - 1) / SN);
-  hipLaunchKernelGGL(k_score_f32_jobs, dim3(g0 + g1), dim3(64 * SW2), score_f32_lds(a0.d), st, a0, a1, (int)g0);
+  if (score_ws() && score_ws_lds(a0.d) <= SCORE_LDS_MAX)
+    hipLaunchKernelGGL(k_score_ws_jobs, dim3(g0 + g1), dim3(512), score_ws_lds(a0.d), st, a0, a1, (int)g0);
+  else
+    hipLaunchKernelGGL(k_score_f32_jobs, dim3(g0 + g1), dim3(64 * SW2), score_f32_lds(a0.d), st, a0, a1, (int)g0);
   return check_launch("k_score_f32_jobs");
 }
 
@@ -719,6 +963,8 @@ int score_ce_bwd(ScoreArgs& a, hipStream_t st) {
   const int nbn = (a.N + SN - 1) / SN;
   const dim3 g2(score_f32_grid(a.B, nbn)), b2(64 * SW2);
   const size_t lds2 = score_f32_lds(a.d);
+  // (the uniform-wave kernel: the backward epilogue's registers beside the wave-specialised
+  // kernel's two A groups would spill)
   hipLaunchKernelGGL((k_score_f32<2>), g2, b2, lds2, st, a);
   return check_launch("k_score_ce_bwd");
 }

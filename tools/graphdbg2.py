@@ -34,10 +34,16 @@ def main():
             super().__init__(*a, **k)
             opts.append(self)
 
+    steps = {}
+
     class RecGS(training.GraphedSteps):
         def __init__(self, *a, **k):
             super().__init__(*a, **k)
             gss.append(self)
+
+        def run(self, key, step):
+            steps.setdefault(key, step)
+            return super().run(key, step)
 
     torch.optim.Adam = CapturableAdam
     cli.GraphedSteps = RecGS
@@ -83,12 +89,22 @@ def main():
             restore()
             return out
 
+        def eager(key):
+            restore()
+            with torch.cuda.stream(gs.stream):
+                o = steps[key]()
+            torch.cuda.synchronize()
+            out = ({kk: v.detach().clone() for kk, v in tensors.items()}, o.detach().clone())
+            restore()
+            return out
+
         def diff(x, y):
             out = []
             for kk in x[0]:
                 if not torch.equal(x[0][kk], y[0][kk]):
                     dd = float((x[0][kk].double() - y[0][kk].double()).abs().max())
-                    out.append("%s(%.2e)" % (kk, dd))
+                    rr = dd / max(float(x[0][kk].double().abs().max()), 1e-30)
+                    out.append("%s(%.2e rel %.1e)" % (kk, dd, rr))
             head = "losses %s vs %s; " % (x[1].tolist(), y[1].tolist()) if not torch.equal(x[1], y[1]) else ""
             return head + ("%d tensors differ: %s" % (len(out), " ".join(out[:40])) if out else "all equal")
 
@@ -114,6 +130,19 @@ def main():
 
         keys = sorted(gs.graphs)
         print("graphs:", len(keys), "keys", keys[:5], flush=True)
+        for key in keys[:2]:
+            e0 = eager(key)
+            print("key %s: eager twice         -> %s" % (key, diff(e0, eager(key))), flush=True)
+            junk()
+            print("key %s: eager after junk    -> %s" % (key, diff(e0, eager(key))), flush=True)
+            print("key %s: replay vs eager     -> %s" % (key, diff(e0, replay(key))), flush=True)
+        import warnings
+        torch.use_deterministic_algorithms(True, warn_only=True)
+        with warnings.catch_warnings(record=True) as wl:
+            warnings.simplefilter("always")
+            eager(keys[0])
+        torch.use_deterministic_algorithms(False)
+        print("nondeterministic ops:", sorted({str(w.message)[:160] for w in wl}), flush=True)
         for key in keys[:2]:
             base = replay(key)
             print("key %s: replay twice        -> %s" % (key, diff(base, replay(key))), flush=True)
