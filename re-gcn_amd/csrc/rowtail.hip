@@ -103,57 +103,75 @@ struct RAcc {
 __device__ const f4 kZeroRow[1] = {{0.f, 0.f, 0.f, 0.f}};
 
 constexpr int RT_KB_BYTES = 4 * 4 * 64 * 16;  // one 16-deep k-block of a packed weight: 16 KB
+constexpr int RT_A_BYTES = 4 * 64 * 16;        // one k-block of the workgroup's 64 A rows: 4 KB
+constexpr int RT_A_RING = 3;
+constexpr size_t RT_LDS = 2 * RT_KB_BYTES + RT_A_RING * RT_A_BYTES;  // 44 KB
 
 // acc += A[16 rows x K] @ W for the wave's rows: A row of lane l = arow (row l % 16 of the
 // wave), columns >= d and rows with !aok read as 0, CLAMP: A clamped to +-10 (the time gate's
-// operand); Wp packed by k_pack_weight_kp.  The weight streams through LDS: k-block kb + 1
-// (16 KB) is copied by the workgroup's four waves with LDS-DMA (global_load_lds, one quarter
-// each) into the other half of a double buffer while k-block kb's MFMAs run, so each fragment
-// leaves L2 once per workgroup (64 rows), and the waves read it with ds_read_b128.  Every wave
-// of the workgroup must call this with the same Wp and KB (one barrier per k-block).
+// operand); Wp packed by k_pack_weight_kp.  Both operands stream through LDS by DMA
+// (global_load_lds), nothing through registers: k-block kb + 1 of the weight (16 KB, a quarter
+// per wave, double-buffered) and k-block kb + 2 of the wave's own A fragments (1 KB per wave,
+// each lane DMAs the 16 bytes it later reads: a 3-deep ring) are in flight while k-block kb's
+// MFMAs run.  Masked A lanes DMA from a zero row.  One raw barrier per k-block after a counted
+// vmcnt (the A block two ahead may stay in flight across it; __syncthreads would drain it).
+// Every wave of the workgroup must call this with the same Wp and KB.
 template <int NT, bool CLAMP>
 __device__ __forceinline__ void rt_mm(RAcc<NT>& acc, const float* __restrict__ arow, bool aok,
                                       const float* __restrict__ Wp, int d, int KB, char* lds) {
   const int lane = threadIdx.x & 63, q = lane >> 4, w = wave_id();
-  typedef const __attribute__((address_space(1))) f4* gptr;
-  const gptr zrow = (gptr)kZeroRow;
-  auto aptr = [&](int kb) -> gptr {
-    const int col = 16 * kb + 4 * q;
-    return (aok & (col < d)) ? (gptr)(arow + col) : zrow;
-  };
+  char* wbuf = lds;
+  char* abuf = lds + 2 * RT_KB_BYTES + w * 1024;
   const char* wsrc = reinterpret_cast<const char*>(Wp);
-  auto dma = [&](int kb) {  // this wave's quarter of k-block kb into buffer kb & 1
-    char* dst = lds + (kb & 1) * RT_KB_BYTES + w * (RT_KB_BYTES / 4);
+  const float* zrow = reinterpret_cast<const float*>(kZeroRow);
+  auto dma_w = [&](int kb) {  // this wave's quarter of k-block kb into buffer kb & 1
+    char* dst = wbuf + (kb & 1) * RT_KB_BYTES + w * (RT_KB_BYTES / 4);
     const char* src = wsrc + (int64_t)kb * RT_KB_BYTES + w * (RT_KB_BYTES / 4) + lane * 16;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
                                        (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
   };
-  dma(0);
-  f4 a = *aptr(0);
+  auto dma_a = [&](int kb) {  // lane l: A[row l % 16][16 kb + 4 (l / 16) ...] into ring slot kb % 3
+    const int col = 16 * kb + 4 * q;
+    const float* src = (aok & (col < d)) ? arow + col : zrow;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(abuf + (kb % RT_A_RING) * RT_A_BYTES),
+                                     16, 0, 0);
+  };
+  dma_a(0);
+  dma_w(0);
+  if (KB > 1) dma_a(1);
   for (int kb = 0; kb < KB; ++kb) {
-    __syncthreads();  // k-block kb landed (each wave drained its own copies); buffer (kb + 1) & 1 is free
-    if (kb + 1 < KB) dma(kb + 1);
-    const f4 an = *aptr(min(kb + 1, KB - 1));
-    const f4* buf = reinterpret_cast<const f4*>(lds + (kb & 1) * RT_KB_BYTES) + lane;
+    // this wave's copies of k-block kb have landed (A of kb + 1, issued after them, may not);
+    // after the barrier every wave's have, and every wave has read buffers kb - 1
+    if (kb + 1 < KB) asm volatile("s_waitcnt vmcnt(1)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kb + 1 < KB) dma_w(kb + 1);
+    if (kb + 2 < KB) dma_a(kb + 2);
+    const f4 a = *reinterpret_cast<const f4*>(abuf + (kb % RT_A_RING) * RT_A_BYTES + lane * 16);
+    const f4* buf = reinterpret_cast<const f4*>(wbuf + (kb & 1) * RT_KB_BYTES) + lane;
+    constexpr int JQ = (NT + 3) / 4;  // fragment quads a k-step reads
     f4 b[2][4];
 #pragma unroll
-    for (int jq = 0; jq < 4; ++jq) b[0][jq] = buf[jq * 64];
+    for (int jq = 0; jq < JQ; ++jq) b[0][jq] = buf[jq * 64];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       if (s + 1 < 4) {
 #pragma unroll
-        for (int jq = 0; jq < 4; ++jq) b[(s + 1) & 1][jq] = buf[((s + 1) * 4 + jq) * 64];
+        for (int jq = 0; jq < JQ; ++jq) b[(s + 1) & 1][jq] = buf[((s + 1) * 4 + jq) * 64];
       }
+      // k-step s + 1's fragment reads stay ahead of k-step s's MFMAs (the scheduler would
+      // otherwise sink each read to its first use and wait for it there)
+      __builtin_amdgcn_sched_barrier(0);
       const float as = CLAMP ? fminf(fmaxf(a[s], -10.f), 10.f) : a[s];
 #pragma unroll
       for (int t = 0; t < NT; ++t)
         acc.t[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(as, b[s & 1][t >> 2][t & 3], acc.t[t], 0, 0, 0);
     }
-    a = an;
   }
-  __syncthreads();  // the last buffer is read before a following call refills buffer 0
+  // every wave has read the last buffers before a following call refills them
+  asm volatile("s_barrier" ::: "memory");
 }
 
 // ---- per-row maps on the wave's 16 rows (lane l: rows 4 (l / 16) + r, column 16 t + l % 16)
@@ -283,7 +301,7 @@ __device__ __forceinline__ int own_int(const int v[4]) {
 // blend reads them per column tile: no second accumulator set, half the registers).
 enum { RT_LAYER = 0, RT_GATE = 1, RT_STEP = 2, RT_STEP_PRE = 3 };
 template <int NT, int MODE>
-__global__ __launch_bounds__(NTHR) void k_rowtail(LayerArgs p, int row0) {
+__device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
   constexpr bool STEP = MODE >= RT_STEP;
   extern __shared__ char rt_lds[];
   const int lane = threadIdx.x & 63, w = wave_id(), q = lane >> 4;
@@ -425,6 +443,18 @@ __global__ __launch_bounds__(NTHR) void k_rowtail(LayerArgs p, int row0) {
   }
 }
 
+template <int NT, int MODE>
+__global__ __launch_bounds__(NTHR) void k_rowtail(LayerArgs p, int row0) {
+  rowtail_body<NT, MODE>(p, row0);
+}
+
+// the timestep variant with the gate rows precomputed at three waves per SIMD (the compiler
+// otherwise keeps ~170 VGPRs of blend loads in flight and the kernel runs at two)
+template <int NT, int MODE>
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) void k_rowtail3(LayerArgs p, int row0) {
+  rowtail_body<NT, MODE>(p, row0);
+}
+
 // ----------------------------------------------------------------------------- launchers
 template <int AGG, int S>
 static void launch_gather(const LayerArgs& a, float* out, int t0, int t1, size_t lds, hipStream_t st) {
@@ -433,9 +463,9 @@ static void launch_gather(const LayerArgs& a, float* out, int t0, int t1, size_t
 
 template <int NT>
 static void launch_tail(const LayerArgs& a, int row0, unsigned grid, hipStream_t st) {
-  const size_t lds = 2 * RT_KB_BYTES;
+  const size_t lds = RT_LDS;
   if (a.fuse_step && a.step.tw)
-    hipLaunchKernelGGL((k_rowtail<NT, RT_STEP_PRE>), dim3(grid), dim3(NTHR), lds, st, a, row0);
+    hipLaunchKernelGGL((k_rowtail3<NT, RT_STEP_PRE>), dim3(grid), dim3(NTHR), lds, st, a, row0);
   else if (a.fuse_step)
     hipLaunchKernelGGL((k_rowtail<NT, RT_STEP>), dim3(grid), dim3(NTHR), lds, st, a, row0);
   else if (a.gate_out)

@@ -135,6 +135,9 @@ class OwnerView:
     def row_src_cols(self):
         return self.g.row_src_cols()
 
+    def number_of_nodes(self):  # the key range of the source-blocked hub lists: every node
+        return self.g.number_of_nodes()
+
     def work(self):
         if self._dev is None:
             wk = dict(self.g.work())
