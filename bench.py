@@ -694,6 +694,9 @@ SCALE_KERNEL = {  # library call -> its main kernel (rocprof / PMC name)
     "regcn_segment_mean_f32": "k_gather_sum<1>",
     "regcn_layer_f32": "k_layer<0, 1, false>",
     "regcn_layer_f32(step)": "k_layer<0, 1, true>",
+    "regcn_layer_rowtail_f32(gather)": "k_gather_agg<0, 1>",
+    "regcn_layer_rowtail_f32": "k_rowtail2<13, 1>",
+    "regcn_layer_rowtail_f32(step)": "k_rowtail3<13, 3>",
     "regcn_timestep_phase_f32(A)": "k_phase_a",
     "regcn_timestep_phase_f32(B)": "k_phase_b<0, 1>",
     "regcn_timestep_phase_f32(C)": "k_phase_c<0, 1>",
@@ -755,6 +758,14 @@ def scale_work(model, glist, B):
         "regcn_layer_f32": (gemm * (m["n_pos"] + V), m["items"] * per_edge + m["n_heavy"] * row + io_layer),
         "regcn_layer_f32(step)": (gemm * (m["n_pos"] + 2 * V),
                                   m["items"] * per_edge + m["n_heavy"] * row + io_layer + V * (2 * row + 4)),
+        # the large-snapshot layer as two launches (csrc/rowtail.hip): the inline rows' gather
+        # into the agg buffer, then the 64-row tail (the first layer also computes the time-gate
+        # product and writes it; the step layer reads it back with x_prev for the blend)
+        "regcn_layer_rowtail_f32(gather)": (0.0, m["items"] * per_edge + (m["n_pos"] - m["n_heavy"]) * (row + 8)),
+        "regcn_layer_rowtail_f32": (gemm * (m["n_pos"] + 2 * V), m["n_pos"] * row + V * (row + 4) + V * row
+                                    + V * (2 * row + 4)),
+        "regcn_layer_rowtail_f32(step)": (gemm * (m["n_pos"] + V), m["n_pos"] * row + V * (row + 4) + 2 * V * row
+                                          + V * (2 * row + 8)),
         "regcn_timestep_phase_f32(A)": (2 * gemm * m["n_pos"] + 2.0 * R2 * 3 * d * d,
                                         V * row + 2 * m["n_pos"] * row + 4.0 * R2 * d * 3 + 4.0 * 3 * d * d),
         "regcn_timestep_phase_f32(B)": (2 * gemm * m["n_pos"], m["items"] * per_edge + m["n_heavy"] * row
@@ -1041,6 +1052,15 @@ def run_scale(args, cfg, world, rank, device, backend):
         if traffic:
             roof["traffic_GBps"] = round(traffic / (calls[dom]["ms"] * 1e-3) / 1e9, 1)
             roof["traffic_frac"] = round(roof["traffic_GBps"] / HBM_PEAK_GBS, 4)
+        gname = "regcn_layer_rowtail_f32(gather)"
+        if gname in calls and not sharded:
+            # the aggregation launch under SURVEY.md §8(d)'s count: 812 B per unit x its units
+            # (inline in-edges + the rows it finishes)
+            units = stats["items"] + stats["n_pos"] - stats["n_heavy"]
+            b8 = units * (4.0 * d + 12)
+            kernels[gname].update(s8d_bytes_per_launch=b8, s8d_units_per_launch=units,
+                                  s8d_achieved_GBps=round(b8 / (calls[gname]["ms"] * 1e-3) / 1e9, 1))
+            kernels[gname]["s8d_frac"] = round(kernels[gname]["s8d_achieved_GBps"] / HBM_PEAK_GBS, 4)
         if dom.startswith("regcn_layer_f32") and not sharded:
             # SURVEY.md §8(d)'s count alone: 812 B per unit (gathered row + col_src + col_type +
             # radius per edge; row write + rowptr + norm + radius per node) x the launch's units

@@ -10,17 +10,21 @@
 //      the inline in-edge rows, finished rows written to an agg buffer that already holds the
 //      hub rows' chunked pre-aggregation (no products, no weights: small LDS and register
 //      footprint, many tiles in flight);
-//   2. k_rowtail: one workgroup = 4 waves = 64 rows, each wave 16 rows x ALL columns, so a
-//      row's reductions (norms, dots of the row maps and the timestep) are in-wave (a DPP row
-//      sum, no LDS, no barrier) and the four waves of a workgroup read the same weight
-//      fragments at the same k-step (served once from L2, 4x less weight traffic per row).
-//      The A operands come straight from global memory: lane l loads 4 consecutive columns
-//      16 b + 4 (l / 16) .. + 3 of its row (l % 16) per 16-column block b, and the weights are
-//      packed in the matching k order (k_pack_weight_kp: the k index of a 16-deep block is
-//      permuted, which a contraction does not see), so neither operand is staged in LDS.
+//   2. k_rowtail: one workgroup = 4 waves = 64 RG rows, each wave RG groups of 16 rows x ALL
+//      columns, so a row's reductions (norms, dots of the row maps and the timestep) are
+//      in-wave (a DPP row sum, no LDS, no barrier) and the four waves of a workgroup share the
+//      weight fragments of each k-block (one L2 read per workgroup, 4 RG x less weight traffic
+//      per row).  Both operands arrive in LDS by DMA (global_load_lds) two / one k-blocks
+//      ahead: lane l of a group DMAs the 4 consecutive columns 16 b + 4 (l / 16) .. + 3 of its
+//      row (l % 16) of k-block b -- exactly the A fragment it later reads -- and the weights
+//      are packed in the matching k order (k_pack_weight_kp: the k index of a 16-deep block is
+//      permuted, which a contraction does not see), so a k-block is 16 KB of weight, copied
+//      as is.
 // Epilogues are the fused kernel's (clamp, self loop, rrelu, exp0, the timestep with the time
 // gate and the radius evolution), in fp32 with the same formulas; the products accumulate in
 // another k order (1e-7-relative differences, not bitwise the fused kernel).
+#include <cstdlib>
+
 #include "layer_parts.h"
 
 namespace regcn {
@@ -103,25 +107,28 @@ struct RAcc {
 __device__ const f4 kZeroRow[1] = {{0.f, 0.f, 0.f, 0.f}};
 
 constexpr int RT_KB_BYTES = 4 * 4 * 64 * 16;  // one 16-deep k-block of a packed weight: 16 KB
-constexpr int RT_A_BYTES = 4 * 64 * 16;        // one k-block of the workgroup's 64 A rows: 4 KB
 constexpr int RT_A_RING = 3;
-constexpr size_t RT_LDS = 2 * RT_KB_BYTES + RT_A_RING * RT_A_BYTES;  // 44 KB
+// LDS of a workgroup whose waves hold RG 16-row groups each: the weight double buffer and the
+// A ring (3 k-blocks x 4 waves x RG groups x 1 KB)
+__host__ __device__ constexpr size_t rt_lds_bytes(int RG) { return 2 * RT_KB_BYTES + RT_A_RING * 4 * RG * 1024; }
 
-// acc += A[16 rows x K] @ W for the wave's rows: A row of lane l = arow (row l % 16 of the
-// wave), columns >= d and rows with !aok read as 0, CLAMP: A clamped to +-10 (the time gate's
-// operand); Wp packed by k_pack_weight_kp.  Both operands stream through LDS by DMA
-// (global_load_lds), nothing through registers: k-block kb + 1 of the weight (16 KB, a quarter
-// per wave, double-buffered) and k-block kb + 2 of the wave's own A fragments (1 KB per wave,
-// each lane DMAs the 16 bytes it later reads: a 3-deep ring) are in flight while k-block kb's
-// MFMAs run.  Masked A lanes DMA from a zero row.  One raw barrier per k-block after a counted
-// vmcnt (the A block two ahead may stay in flight across it; __syncthreads would drain it).
-// Every wave of the workgroup must call this with the same Wp and KB.
-template <int NT, bool CLAMP>
-__device__ __forceinline__ void rt_mm(RAcc<NT>& acc, const float* __restrict__ arow, bool aok,
+// acc[g] += A_g[16 rows x K] @ W for the wave's RG row groups: A row of lane l in group g =
+// arow[g] (row l % 16 of the group), columns >= d and rows with !aok[g] read as 0, CLAMP: A
+// clamped to +-10 (the time gate's operand); Wp packed by k_pack_weight_kp.  Both operands
+// stream through LDS by DMA (global_load_lds), nothing through registers: k-block kb + 1 of
+// the weight (16 KB, a quarter per wave, double-buffered) and k-block kb + 2 of the wave's own
+// A fragments (1 KB per group, each lane DMAs the 16 bytes it later reads: a 3-deep ring) are
+// in flight while k-block kb's MFMAs run; every B fragment read feeds RG MFMAs.  Masked A
+// lanes DMA from a zero row.  One raw barrier per k-block after a counted vmcnt (the A block
+// two ahead may stay in flight across it; __syncthreads would drain it).  Every wave of the
+// workgroup must call this with the same Wp and KB.
+template <int NT, int RG, bool CLAMP>
+__device__ __forceinline__ void rt_mm(RAcc<NT> (&acc)[RG], const float* const (&arow)[RG], const bool (&aok)[RG],
                                       const float* __restrict__ Wp, int d, int KB, char* lds) {
   const int lane = threadIdx.x & 63, q = lane >> 4, w = wave_id();
+  constexpr int A_SLOT = 4 * RG * 1024;
   char* wbuf = lds;
-  char* abuf = lds + 2 * RT_KB_BYTES + w * 1024;
+  char* abuf = lds + 2 * RT_KB_BYTES + w * RG * 1024;
   const char* wsrc = reinterpret_cast<const char*>(Wp);
   const float* zrow = reinterpret_cast<const float*>(kZeroRow);
   auto dma_w = [&](int kb) {  // this wave's quarter of k-block kb into buffer kb & 1
@@ -132,12 +139,15 @@ __device__ __forceinline__ void rt_mm(RAcc<NT>& acc, const float* __restrict__ a
       __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
                                        (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
   };
-  auto dma_a = [&](int kb) {  // lane l: A[row l % 16][16 kb + 4 (l / 16) ...] into ring slot kb % 3
+  auto dma_a = [&](int kb) {  // lane l: A_g[row l % 16][16 kb + 4 (l / 16) ...] into ring slot kb % 3
     const int col = 16 * kb + 4 * q;
-    const float* src = (aok & (col < d)) ? arow + col : zrow;
-    __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (__attribute__((address_space(3))) void*)(abuf + (kb % RT_A_RING) * RT_A_BYTES),
-                                     16, 0, 0);
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      const float* src = (aok[g] & (col < d)) ? arow[g] + col : zrow;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)src, (__attribute__((address_space(3))) void*)(abuf + (kb % RT_A_RING) * A_SLOT + g * 1024), 16,
+          0, 0);
+    }
   };
   dma_a(0);
   dma_w(0);
@@ -145,11 +155,18 @@ __device__ __forceinline__ void rt_mm(RAcc<NT>& acc, const float* __restrict__ a
   for (int kb = 0; kb < KB; ++kb) {
     // this wave's copies of k-block kb have landed (A of kb + 1, issued after them, may not);
     // after the barrier every wave's have, and every wave has read buffers kb - 1
-    if (kb + 1 < KB) asm volatile("s_waitcnt vmcnt(1)\n\ts_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (kb + 1 < KB) {
+      if constexpr (RG == 1) asm volatile("s_waitcnt vmcnt(1)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    }
     if (kb + 1 < KB) dma_w(kb + 1);
     if (kb + 2 < KB) dma_a(kb + 2);
-    const f4 a = *reinterpret_cast<const f4*>(abuf + (kb % RT_A_RING) * RT_A_BYTES + lane * 16);
+    f4 a[RG];
+#pragma unroll
+    for (int g = 0; g < RG; ++g)
+      a[g] = *reinterpret_cast<const f4*>(abuf + (kb % RT_A_RING) * A_SLOT + g * 1024 + lane * 16);
     const f4* buf = reinterpret_cast<const f4*>(wbuf + (kb & 1) * RT_KB_BYTES) + lane;
     constexpr int JQ = (NT + 3) / 4;  // fragment quads a k-step reads
     f4 b[2][4];
@@ -164,10 +181,14 @@ __device__ __forceinline__ void rt_mm(RAcc<NT>& acc, const float* __restrict__ a
       // k-step s + 1's fragment reads stay ahead of k-step s's MFMAs (the scheduler would
       // otherwise sink each read to its first use and wait for it there)
       __builtin_amdgcn_sched_barrier(0);
-      const float as = CLAMP ? fminf(fmaxf(a[s], -10.f), 10.f) : a[s];
+      float as[RG];
+#pragma unroll
+      for (int g = 0; g < RG; ++g) as[g] = CLAMP ? fminf(fmaxf(a[g][s], -10.f), 10.f) : a[g][s];
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        acc.t[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(as, b[s & 1][t >> 2][t & 3], acc.t[t], 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < RG; ++g)
+          acc[g].t[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(as[g], b[s & 1][t >> 2][t & 3], acc[g].t[t], 0, 0, 0);
     }
   }
   // every wave has read the last buffers before a following call refills them
@@ -300,61 +321,36 @@ __device__ __forceinline__ int own_int(const int v[4]) {
 // the timestep, its gate product in-kernel; RT_STEP_PRE = with the gate rows from RT_GATE (the
 // blend reads them per column tile: no second accumulator set, half the registers).
 enum { RT_LAYER = 0, RT_GATE = 1, RT_STEP = 2, RT_STEP_PRE = 3 };
-template <int NT, int MODE>
-__device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
-  constexpr bool STEP = MODE >= RT_STEP;
-  extern __shared__ char rt_lds[];
-  const int lane = threadIdx.x & 63, w = wave_id(), q = lane >> 4;
-  const int wg0 = row0 + blockIdx.x * RT_ROWS;
-  const int base = wg0 + 16 * w;
-  const int n_valid = max(0, min(16, p.V - base));  // p.V: the length of the row list
-  const int d = p.d, KB = (d + 15) >> 4;
-  const int my_i = lane & 15;
-  const int arow_id = p.rows[min(base + min(my_i, max(n_valid - 1, 0)), p.V - 1)];
-  const bool a_valid = my_i < n_valid;
-  const bool a_pos = a_valid & (base + my_i < p.n_pos);
-  int crow[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) crow[r] = __shfl(arow_id, 4 * q + r);
-  const int npos_w = min(max(p.n_pos - base, 0), n_valid);
-  // the passes are the workgroup's (every wave takes part in each weight's LDS stream)
-  const int n_wg = min(RT_ROWS, p.V - wg0);
-  const int npos_wg = min(max(p.n_pos - wg0, 0), n_wg);
-  const float* xrow = p.x + (int64_t)arow_id * d;
 
-  RAcc<NT> v;
-  if constexpr (MODE == RT_GATE) {  // the timestep's gate pre-activation, stored as is
-    v.zero();
-    rt_mm<NT, true>(v, xrow, a_valid, p.w_gate, d, KB, rt_lds);
-    rt_store<NT>(v, p.gate_out, crow, n_valid, d);
-  }
-  v.zero();
-  // The products into v, one call site (one copy of the MFMA loop, one accumulator set):
-  // pass 0 = agg @ W_n (in-edge rows), then x @ W_loop / x @ W_evolve -- both in the one
-  // workgroup where the in-edge rows end (rows masked), one of them everywhere else.
-  const bool p1 = npos_wg > 0 && p.agg != nullptr;
-  if (p1 && !p.w_n) rt_load<NT>(v, p.agg, crow, npos_w, d);  // Lorentz: the centroid rows as is
-  const bool mixed = npos_wg > 0 && npos_wg < n_wg;
-  const int first = (p1 && p.w_n) ? 0 : 1;
-  const int last = p.w_loop ? (mixed ? 3 : 2) : 1;
-  for (int pass = first; pass < last; ++pass) {
-    if (pass == 1 && p1 && !p.euclid) {
+// One 16-row group of a wave: its row ids (C layout), counts and A-operand row.
+struct RtRows {
+  int base, n_valid, arow_id, npos_w;
+  bool a_valid, a_pos;
+  int crow[4];
+};
+
+__device__ __forceinline__ RtRows rt_rows(const LayerArgs& p, int base) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, my_i = lane & 15;
+  RtRows R;
+  R.base = base;
+  R.n_valid = max(0, min(16, p.V - base));  // p.V: the length of the row list
+  R.arow_id = p.rows[min(base + min(my_i, max(R.n_valid - 1, 0)), p.V - 1)];
+  R.a_valid = my_i < R.n_valid;
+  R.a_pos = R.a_valid & (base + my_i < p.n_pos);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
-    }
-    const float* arow = pass == 0 ? p.agg + (int64_t)arow_id * d : xrow;
-    const bool ok = pass == 0 ? a_pos : (mixed ? (pass == 1 ? a_pos : a_valid & !a_pos) : a_valid);
-    const float* W = pass == 0 ? p.w_n : (pass == 1 && npos_wg > 0 ? p.w_loop : p.w_evolve);
-    rt_mm<NT, false>(v, arow, ok, W, d, KB, rt_lds);
-  }
-  if (first == 0 && last == 1 && !p.euclid) {  // agg @ W_n without a self loop
-#pragma unroll
-    for (int t = 0; t < NT; ++t) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
-  }
-  if (first == 1 && last == 1 && p1 && !p.euclid) {  // Lorentz rows, no self loop
-#pragma unroll
-    for (int t = 0; t < NT; ++t) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
-  }
+  for (int r = 0; r < 4; ++r) R.crow[r] = __shfl(R.arow_id, 4 * q + r);
+  R.npos_w = min(max(p.n_pos - base, 0), R.n_valid);
+  return R;
+}
+
+// Everything after the products for one 16-row group: clamps, rrelu, exp0, then the next
+// layer's x / |h| or the timestep.  `g` (RT_STEP) holds the in-kernel gate product.
+template <int NT, int MODE>
+__device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const RtRows& R, const RAcc<NT>* g) {
+  constexpr bool STEP = MODE >= RT_STEP;
+  const int lane = threadIdx.x & 63, q = lane >> 4, d = p.d;
+  const int* crow = R.crow;
+  const int n_valid = R.n_valid;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (!p.euclid) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
@@ -381,11 +377,6 @@ __device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
       rt_exp0<NT>(v, n2, k);
     }
     rt_log0<NT>(v, n2, k);
-    RAcc<NT> g;  // the time gate pre-activation clamp(x_prev) @ W_g (RT_STEP), then its blend
-    if constexpr (MODE == RT_STEP) {
-      g.zero();
-      rt_mm<NT, true>(g, s.x_prev + (int64_t)arow_id * d, a_valid, s.w_g, d, KB, rt_lds);
-    }
     float bg[NT];
     rt_col<NT>(bg, s.b_g, d);
 #pragma unroll
@@ -402,7 +393,7 @@ __device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
           const float zt = s.tw[(int64_t)crow[r] * d + colc];
           z = ok ? zt : 0.f;
         } else {
-          z = g.t[t][r];
+          z = g->t[t][r];
         }
         const float gg = sigmoidf(z + bg[t]);
         v.t[t][r] = gg * c4[r] + (1.f - gg) * pr;
@@ -443,16 +434,106 @@ __device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
   }
 }
 
-template <int NT, int MODE>
+// The layer of the rows rows[64 RG b + 16 (RG w + g) ...] (wave w of workgroup b, group g): v =
+// clamp(agg @ W_n) (or clamp(agg): Lorentz; no clamps: euclid) + x @ (W_loop | W_evolve) ->
+// clamp -> rrelu -> exp0; then the next layer's x / |h|, or the timestep
+// (hyperbolic_model.py:829-869: project, layer norm, time gate, exp0, project, radius
+// evolution / static radius).  MODE: RT_LAYER; RT_GATE = RT_LAYER + the timestep's time-gate
+// pre-activation clamp(x) @ W_g into gate_out (a cell's first layer: x is the timestep input);
+// RT_STEP = the last layer with the timestep, its gate product in-kernel (RG = 1 only);
+// RT_STEP_PRE = with the gate rows from RT_GATE (the blend reads them per column tile).
+template <int NT, int MODE, int RG>
+__device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
+  static_assert(MODE != RT_STEP || RG == 1, "the in-kernel gate product runs on one row group");
+  extern __shared__ char rt_lds[];
+  const int w = wave_id();
+  const int wg0 = row0 + blockIdx.x * RT_ROWS * RG;
+  const int d = p.d, KB = (d + 15) >> 4;
+  RtRows R[RG];
+#pragma unroll
+  for (int g = 0; g < RG; ++g) R[g] = rt_rows(p, wg0 + 16 * (RG * w + g));
+  // the passes are the workgroup's (every wave takes part in each weight's LDS stream)
+  const int n_wg = min(RT_ROWS * RG, p.V - wg0);
+  const int npos_wg = min(max(p.n_pos - wg0, 0), n_wg);
+  const float* xrow[RG];
+  bool valid[RG];
+#pragma unroll
+  for (int g = 0; g < RG; ++g) xrow[g] = p.x + (int64_t)R[g].arow_id * d, valid[g] = R[g].a_valid;
+
+  RAcc<NT> v[RG];
+  if constexpr (MODE == RT_GATE) {  // the timestep's gate pre-activation, stored as is
+#pragma unroll
+    for (int g = 0; g < RG; ++g) v[g].zero();
+    rt_mm<NT, RG, true>(v, xrow, valid, p.w_gate, d, KB, rt_lds);
+#pragma unroll
+    for (int g = 0; g < RG; ++g) rt_store<NT>(v[g], p.gate_out, R[g].crow, R[g].n_valid, d);
+  }
+#pragma unroll
+  for (int g = 0; g < RG; ++g) v[g].zero();
+  // The products into v, one call site (one copy of the MFMA loop, one accumulator set):
+  // pass 0 = agg @ W_n (in-edge rows), then x @ W_loop / x @ W_evolve -- both in the one
+  // workgroup where the in-edge rows end (rows masked), one of them everywhere else.
+  const bool p1 = npos_wg > 0 && p.agg != nullptr;
+  if (p1 && !p.w_n) {  // Lorentz: the centroid rows as is
+#pragma unroll
+    for (int g = 0; g < RG; ++g) rt_load<NT>(v[g], p.agg, R[g].crow, R[g].npos_w, d);
+  }
+  const bool mixed = npos_wg > 0 && npos_wg < n_wg;
+  const int first = (p1 && p.w_n) ? 0 : 1;
+  const int last = p.w_loop ? (mixed ? 3 : 2) : 1;
+  for (int pass = first; pass < last; ++pass) {
+    if (pass == 1 && p1 && !p.euclid) {
+#pragma unroll
+      for (int g = 0; g < RG; ++g)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) v[g].t[t] = clamp4(v[g].t[t], -10.f, 10.f);
+    }
+    const float* arow[RG];
+    bool ok[RG];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      arow[g] = pass == 0 ? p.agg + (int64_t)R[g].arow_id * d : xrow[g];
+      ok[g] = pass == 0 ? R[g].a_pos : (mixed ? (pass == 1 ? R[g].a_pos : R[g].a_valid & !R[g].a_pos) : R[g].a_valid);
+    }
+    const float* W = pass == 0 ? p.w_n : (pass == 1 && npos_wg > 0 ? p.w_loop : p.w_evolve);
+    rt_mm<NT, RG, false>(v, arow, ok, W, d, KB, rt_lds);
+  }
+  if (((first == 0 && last == 1) || (first == 1 && last == 1 && p1)) && !p.euclid) {
+    // agg @ W_n without a self loop, or Lorentz rows without one
+#pragma unroll
+    for (int g = 0; g < RG; ++g)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) v[g].t[t] = clamp4(v[g].t[t], -10.f, 10.f);
+  }
+  if constexpr (MODE == RT_STEP) {  // the time gate pre-activation clamp(x_prev) @ W_g
+    RAcc<NT> gt[1];
+    gt[0].zero();
+    const float* xp[1] = {p.step.x_prev + (int64_t)R[0].arow_id * d};
+    const bool okp[1] = {R[0].a_valid};
+    rt_mm<NT, 1, true>(gt, xp, okp, p.step.w_g, d, KB, rt_lds);
+    rt_finish<NT, MODE>(p, v[0], R[0], &gt[0]);
+  } else {
+#pragma unroll
+    for (int g = 0; g < RG; ++g) rt_finish<NT, MODE>(p, v[g], R[g], nullptr);
+  }
+}
+
+template <int NT, int MODE, int RG>
 __global__ __launch_bounds__(NTHR) void k_rowtail(LayerArgs p, int row0) {
-  rowtail_body<NT, MODE>(p, row0);
+  rowtail_body<NT, MODE, RG>(p, row0);
+}
+
+// two row groups per wave at two waves per SIMD
+template <int NT, int MODE>
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(2))) void k_rowtail2(LayerArgs p, int row0) {
+  rowtail_body<NT, MODE, 2>(p, row0);
 }
 
 // the timestep variant with the gate rows precomputed at three waves per SIMD (the compiler
 // otherwise keeps ~170 VGPRs of blend loads in flight and the kernel runs at two)
 template <int NT, int MODE>
 __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) void k_rowtail3(LayerArgs p, int row0) {
-  rowtail_body<NT, MODE>(p, row0);
+  rowtail_body<NT, MODE, 1>(p, row0);
 }
 
 // ----------------------------------------------------------------------------- launchers
@@ -461,17 +542,38 @@ static void launch_gather(const LayerArgs& a, float* out, int t0, int t1, size_t
   hipLaunchKernelGGL((k_gather_agg<AGG, S>), dim3(t1 - t0), dim3(NTHR), lds, st, a, out, t0);
 }
 
+// Row groups per wave of the layer tails (d > 128): 2 (default) = every B fragment feeds two
+// MFMAs at 2 waves / SIMD; REGCN_ROWTAIL_RG=1: one group at 3 waves / SIMD.  Config 5
+// (profiles/r4_rowtail_rg_kernel_stats.csv): first-layer tail 2.41 vs 2.55 ms; the step
+// layer's tail is the same either way (1.99 ms) and keeps its one-group kernel.
+static int rowtail_rg() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("REGCN_ROWTAIL_RG");
+    v = e ? atoi(e) : 2;
+  }
+  return v;
+}
+
 template <int NT>
-static void launch_tail(const LayerArgs& a, int row0, unsigned grid, hipStream_t st) {
-  const size_t lds = RT_LDS;
-  if (a.fuse_step && a.step.tw)
-    hipLaunchKernelGGL((k_rowtail3<NT, RT_STEP_PRE>), dim3(grid), dim3(NTHR), lds, st, a, row0);
-  else if (a.fuse_step)
-    hipLaunchKernelGGL((k_rowtail<NT, RT_STEP>), dim3(grid), dim3(NTHR), lds, st, a, row0);
-  else if (a.gate_out)
-    hipLaunchKernelGGL((k_rowtail<NT, RT_GATE>), dim3(grid), dim3(NTHR), lds, st, a, row0);
-  else
-    hipLaunchKernelGGL((k_rowtail<NT, RT_LAYER>), dim3(grid), dim3(NTHR), lds, st, a, row0);
+static int launch_tail(const LayerArgs& a, int r0, int r1, hipStream_t st) {
+  const int rg = (NT > 8 && rowtail_rg() == 2) ? 2 : 1;
+  const unsigned grid = (unsigned)((r1 - r0 + RT_ROWS * rg - 1) / (RT_ROWS * rg));
+  const size_t lds = rt_lds_bytes(rg);
+  if (a.fuse_step && a.step.tw) {
+    hipLaunchKernelGGL((k_rowtail3<NT, RT_STEP_PRE>), dim3((r1 - r0 + RT_ROWS - 1) / RT_ROWS), dim3(NTHR),
+                       rt_lds_bytes(1), st, a, r0);
+  } else if (a.fuse_step) {
+    hipLaunchKernelGGL((k_rowtail<NT, RT_STEP, 1>), dim3((r1 - r0 + RT_ROWS - 1) / RT_ROWS), dim3(NTHR),
+                       rt_lds_bytes(1), st, a, r0);
+  } else if (a.gate_out) {
+    if (rg == 2) hipLaunchKernelGGL((k_rowtail2<NT, RT_GATE>), dim3(grid), dim3(NTHR), lds, st, a, r0);
+    else hipLaunchKernelGGL((k_rowtail<NT, RT_GATE, 1>), dim3(grid), dim3(NTHR), lds, st, a, r0);
+  } else {
+    if (rg == 2) hipLaunchKernelGGL((k_rowtail2<NT, RT_LAYER>), dim3(grid), dim3(NTHR), lds, st, a, r0);
+    else hipLaunchKernelGGL((k_rowtail<NT, RT_LAYER, 1>), dim3(grid), dim3(NTHR), lds, st, a, r0);
+  }
+  return 0;
 }
 
 // which == 1: the gather over tiles [lo, hi); which == 2: the tail over rows[lo, hi) (hi <= a.V);
@@ -544,12 +646,11 @@ int layer_rowtail_part(const LayerArgs& a, float* agg, int which, int lo, int hi
   t.agg = agg;
   t.V = r1;
   if (mode == AGG_LORENTZ) t.w_n = nullptr;  // the centroid rows are the aggregation itself
-  const unsigned grid = (unsigned)((r1 - r0 + RT_ROWS - 1) / RT_ROWS);
   const int nt = (a.d + 15) / 16;
-  if (nt <= 4) launch_tail<4>(t, r0, grid, st);
-  else if (nt <= 8) launch_tail<8>(t, r0, grid, st);
-  else if (nt <= 13) launch_tail<13>(t, r0, grid, st);
-  else launch_tail<16>(t, r0, grid, st);
+  if (nt <= 4) launch_tail<4>(t, r0, r1, st);
+  else if (nt <= 8) launch_tail<8>(t, r0, r1, st);
+  else if (nt <= 13) launch_tail<13>(t, r0, r1, st);
+  else launch_tail<16>(t, r0, r1, st);
   return check_launch("k_rowtail");
 }
 

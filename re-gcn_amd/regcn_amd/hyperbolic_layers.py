@@ -39,7 +39,7 @@ def _rowtail_chunks(g, k):
     hit = g.__dict__.get("_rt_chunks")
     if hit is not None and hit[0] == k:
         return hit[1]
-    if torch.cuda.is_current_stream_capturing():
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
         return None  # no host copy inside a capture: this launch runs unchunked
     wk = g.work()
     n_t, n_rows = int(g.n_pos_tiles), int(wk["rows"].shape[0])
@@ -289,7 +289,13 @@ def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c,
     chunks = _rowtail_chunks(g, ROWTAIL_CHUNKS) if (ROWTAIL_CHUNKS > 1 and g.n_pos_tiles > 1
                                                      and mode != _lib.AGG_NONE) else None
     if chunks is None or len(chunks) < 2:
-        _lib.check(_lib.lib().regcn_layer_rowtail_f32(ctypes.byref(desc), _lib.fptr(agg), _lib.stream()), name)
+        # the gather and the tail as two calls (the same two launches regcn_layer_rowtail_f32
+        # makes), so a trace times each kernel on its own
+        part = _lib.lib().regcn_layer_rowtail_part_f32
+        if mode != _lib.AGG_NONE and g.n_pos_tiles:
+            _lib.check(part(ctypes.byref(desc), _lib.fptr(agg), 1, 0, int(g.n_pos_tiles), _lib.stream()),
+                       "regcn_layer_rowtail_f32(gather)")
+        _lib.check(part(ctypes.byref(desc), _lib.fptr(agg), 2, 0, int(n_rows), _lib.stream()), name)
         return h, xn, rn
     # gathers on the side stream, chunk by chunk; each tail chunk waits for its gather only
     part = _lib.lib().regcn_layer_rowtail_part_f32

@@ -342,3 +342,35 @@ def test_spread_block_fills_every_xcd_queue():
         fill.append((np.bincount(((p // 4) % 8)[real], minlength=8) > 0).sum())
     assert fill == [1, 8], fill
     assert G.spread_block(V, 64) == 64 and G.spread_block(10 ** 6, 4096) == 4096
+
+
+def test_rowtail_chunks_partition_tiles_and_rows():
+    """hyperbolic_layers._rowtail_chunks (the two-stream rowtail pipeline): k chunks whose tile
+    ranges partition the in-edge tiles and whose row ranges partition the row list, each row
+    boundary at a tile start (a chunk's tail reads only rows its own gather finished)."""
+    from regcn_amd import graph as G
+    import torch
+    from regcn_amd.hyperbolic_layers import _rowtail_chunks
+    from regcn_amd.synthetic import zipf_triples
+    rng = np.random.default_rng(2)
+    V, R = 5000, 8
+    host = G.build_sub_graph(V, R, zipf_triples(rng, V, R, 20000), False, "cpu")
+    wk = {k: torch.from_numpy(np.asarray(host._host[k])) for k in ("tiles", "rows")}
+
+    class Lists:  # the host lists behind the work() a device snapshot would give
+        n_pos_tiles = host.n_pos_tiles
+
+        def work(self):
+            return wk
+
+    g = Lists()
+    n_t, n_rows = int(g.n_pos_tiles), int(wk["rows"].shape[0])
+    starts = wk["tiles"][:n_t, 0].tolist()
+    for k in (1, 3, 6):
+        ch = _rowtail_chunks(g, k)
+        assert len(ch) == min(k, n_t)
+        assert ch[0][0] == 0 and ch[-1][1] == n_t and ch[0][2] == 0 and ch[-1][3] == n_rows
+        for (t0, t1, r0, r1), nxt in zip(ch, ch[1:] + [None]):
+            assert t0 < t1 and r0 <= r1
+            if nxt is not None:
+                assert nxt[0] == t1 and nxt[2] == r1 and r1 == starts[t1]
