@@ -555,9 +555,13 @@ static int rowtail_rg() {
   return v;
 }
 
+constexpr int RT_RG2_MIN_ROWS = 256 * 1024;
+
 template <int NT>
 static int launch_tail(const LayerArgs& a, int r0, int r1, hipStream_t st) {
-  const int rg = (NT > 8 && rowtail_rg() == 2) ? 2 : 1;
+  // two groups only when the launch still fills the chip with 128-row workgroups (a rank's
+  // slice of an owner-partitioned snapshot runs one group per wave: more, shorter workgroups)
+  const int rg = (NT > 8 && rowtail_rg() == 2 && r1 - r0 >= RT_RG2_MIN_ROWS) ? 2 : 1;
   const unsigned grid = (unsigned)((r1 - r0 + RT_ROWS * rg - 1) / (RT_ROWS * rg));
   const size_t lds = rt_lds_bytes(rg);
   if (a.fuse_step && a.step.tw) {

@@ -370,7 +370,7 @@ class _HypCE(torch.autograd.Function):
         _lib.call("regcn_hyp_ce_bwd_f32", f(q), f(cand), f(b) if ctx.has_bias else None, f(sc), f(mg),
                   _lib.iptr(tgt), f(lse), f(gl), B, N, d, ctx.c, 0, f(coef), f(rsum), f(csum), _lib.stream())
         rs = rsum.sum(1, keepdim=True)
-        cs = csum.sum(0)
+        cs = colsum(csum.reshape(ng, -1)).reshape(N, 3)
         dq = kreduce_mm(coef, cand, False, 2.0 * rs * q)            # coef E + 2 q sum_n G dS/d|q|^2
         de = kreduce_mm(coef, q, True, 2.0 * cs[:, :1] * cand)      # coef^T Q + 2 e sum_b G dS/d|e|^2
         dbias = cs[:, 1].clone() if ctx.has_bias else None
@@ -499,6 +499,18 @@ def kreduce_mm(a, b, a_kmajor, c0=None, b_kmajor=True):
     return out
 
 
+def colsum(x):
+    """x.sum(0) of a 2-D fp32 device tensor on regcn_kreduce_gemm_f32 (ones^T x: K = rows split
+    over workgroups, partials summed by a second launch in a fixed order).  torch's column sum
+    of a tall matrix finishes in the kernel's last workgroup after an atomic ticket, reading
+    the other workgroups' partials through the XCDs' separate L2s; in replayed HIP graphs it
+    returned different sums for the same input (tools/graphdbg3.py: the time-gate bias
+    gradient), so the training backward sums columns here."""
+    x = x.contiguous().float()
+    ones = torch.ones(x.shape[0], 1, device=x.device, dtype=torch.float32)
+    return kreduce_mm(ones, x, True).reshape(x.shape[1])
+
+
 class _Linear(torch.autograd.Function):
     """F.linear(x, W, bias) for a mini-batch of query rows: y = x W^T + bias, dx = dy W,
     dW = dy^T x, dbias = sum dy, all three products on regcn_kreduce_gemm_f32."""
@@ -516,7 +528,7 @@ class _Linear(torch.autograd.Function):
         gy = gy.contiguous()
         gx = kreduce_mm(gy, w, False) if ctx.needs_input_grad[0] else None
         gw = kreduce_mm(gy, x, True) if ctx.needs_input_grad[1] else None
-        gb = gy.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        gb = colsum(gy) if ctx.has_bias and ctx.needs_input_grad[2] else None
         return gx, gw, gb
 
 
@@ -617,7 +629,7 @@ class _Tail(torch.autograd.Function):
         _lib.call("regcn_tail_f32", f(agg), lx, ex, 2 * d, _lib.dptr(pos, torch.uint8), f(z), f(bias), f(p),
                   agg.shape[0], d, ctx.flags, float(ctx.slope), f(gy), None, f(dagg), dlx, dex, f(dz), f(dp),
                   _lib.stream())
-        dbias = dz.sum(0) if bias is not None and need[3] else None
+        dbias = colsum(dz) if bias is not None and need[3] else None
         return dagg, dloop, dz if need[2] else None, dbias, dp, None, None, None
 
 

@@ -222,8 +222,21 @@ def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_
     return h, xn, rn
 
 
+def run_layer_chunked(mode, g, tail_views, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c, euclid, step, out,
+                      gate, after):
+    """The large-snapshot layer over a rank's rows in pipeline chunks (parallel.ShardedGraph,
+    owner partition): the hub pass and the gather run once over `g` (all of the rank's rows),
+    then each tail view's 64-row tail, `after(j)` following chunk j's tail (its rows' x and |h|
+    are final: the caller all-gathers them while the next chunk's tail runs)."""
+    agg = _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c)
+    if g.n_pos == 0:
+        mode = _lib.AGG_NONE
+    return _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c, euclid, step, agg, out, gate,
+                        int(g.work()["rows"].shape[0]), tail_views=tail_views, after=after)
+
+
 def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c, euclid, step, agg, out, gate,
-                 n_rows):
+                 n_rows, tail_views=None, after=None):
     """regcn_layer_rowtail_f32: the inline in-edge rows gathered into `agg` (which holds the hub
     rows already), then the 64-row tail over all rows (csrc/rowtail.hip)."""
     wk = g.work()
@@ -286,6 +299,20 @@ def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c,
             desc.step_tw = a(step.tw)
             keep.append(step.tw)
     name = "regcn_layer_rowtail_f32(step)" if step is not None else "regcn_layer_rowtail_f32"
+    if tail_views is not None:  # gather over g, then one tail per view (run_layer_chunked)
+        part = _lib.lib().regcn_layer_rowtail_part_f32
+        if mode != _lib.AGG_NONE and g.n_pos_tiles:
+            _lib.check(part(ctypes.byref(desc), _lib.fptr(agg), 1, 0, int(g.n_pos_tiles), _lib.stream()),
+                       "regcn_layer_rowtail_f32(gather)")
+        for j, tv in enumerate(tail_views):
+            tw = tv.work()
+            nr = int(tw["rows"].shape[0])
+            if nr:
+                keep.append(tw["rows"])
+                desc.rows, desc.n_pos, desc.V = a(tw["rows"], torch.int32), tv.n_pos, nr
+                _lib.check(part(ctypes.byref(desc), _lib.fptr(agg), 2, 0, nr, _lib.stream()), name)
+            after(j)
+        return h, xn, rn
     chunks = _rowtail_chunks(g, ROWTAIL_CHUNKS) if (ROWTAIL_CHUNKS > 1 and g.n_pos_tiles > 1
                                                      and mode != _lib.AGG_NONE) else None
     if chunks is None or len(chunks) < 2:

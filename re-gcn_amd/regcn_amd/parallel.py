@@ -81,7 +81,11 @@ def owner_bounds(V, world):
 
 
 def owner_chunks(V, world):
-    """Pipeline chunks per rank of the owner partition (auto): 4 from 64k rows per rank."""
+    """Pipeline chunks per rank of the owner partition (auto): 4 from 64k rows per rank.  The
+    8-rank config-5 simulation (bench owner_simulation, round 4; the hub pass and the gather
+    over all of a rank's rows, only the tails per chunk): per-rank compute 5.9 / 6.1 / 6.4 ms
+    at 1 / 2 / 4 chunks against 3.9 ms of all-gather per step, of which all but the last
+    chunk's of each layer (1/4) hides under the next chunk's tail."""
     return 4 if world > 1 and -(-V // world) >= 65536 else 1
 
 
@@ -117,11 +121,15 @@ class OwnerView:
     spans, and the fused-kernel work lists of the node ids [lo, hi) only (one pipeline
     chunk of the rank's rows, see ShardedGraph)."""
 
-    def __init__(self, g, lo, hi):
+    def __init__(self, g, lo, hi, ranges=None):
+        """Node ids [lo, hi), or the union of `ranges` (a rank's pipeline chunks: one gather
+        launch over all of them, ShardedGraph.run_layer)."""
         self.g = g
-        self.v0, self.v1 = int(lo), int(hi)
+        ranges = [(int(lo), int(hi))] if ranges is None else [(int(a), int(b)) for a, b in ranges]
+        self.v0, self.v1 = ranges[0][0], ranges[-1][1]
+        nodes = np.concatenate([np.arange(a, b) for a, b in ranges]) if ranges else np.zeros(0, np.int64)
         h = g._host
-        fw = fused_work(np.arange(self.v0, self.v1), g.in_deg_np, h["rowptr"].astype(np.int64),
+        fw = fused_work(nodes, g.in_deg_np, h["rowptr"].astype(np.int64),
                         h["col_src"].astype(np.int64), h["col_type"].astype(np.int64), g.budget, g.pack_items,
                         g.chunk_edges)
         self.fw = fw
@@ -345,8 +353,8 @@ class ShardedGraph:
     Everything but the message-passing layers (relation spans, degrees, ...) is the
     wrapped graph's."""
 
-    # owner partition: a rank's rows run as this many launches, each one's rows all-gathered
-    # on a side stream while the next launch computes (auto: 4 from 64k rows per rank)
+    # owner partition: a rank's rows run in this many chunks, each one's rows all-gathered on a
+    # side stream while the next chunk computes (auto: owner_chunks)
     pipeline_chunks = None
 
     def __init__(self, g, partition="owner", group=None, rank=None, world=None, chunks=None):
@@ -360,12 +368,15 @@ class ShardedGraph:
         self.rank, self.world = rank, world
         self.chunks = chunks
         self.plan = EdgePlan(g, rank, world).to(g.device) if partition == "edge" else None
-        self.layout, self.views = None, []
+        self.layout, self.views, self.rank_view = None, [], None
         if partition == "owner":
             V = g.number_of_nodes()
             k = chunks or self.pipeline_chunks or owner_chunks(V, world)
             self.layout = OwnerLayout(V, world, k)
             self.views = [((lo, hi), OwnerView(g, lo, hi)) for lo, hi in self.layout.ranges(rank)]
+            # all of the rank's rows as one view: with the large-snapshot layer path the hub
+            # pass and the gather run once over them, only the tails per chunk
+            self.rank_view = OwnerView(g, 0, 0, ranges=self.layout.ranges(rank)) if len(self.views) > 1 else None
         self._comm = None
         self._rel = None
         # collectives only inside a process group of world > 1 (a single-process simulation of
@@ -442,6 +453,24 @@ class ShardedGraph:
                       f(wk["norm"]), None, 0, i(fn), fn.shape[0], d, f(P), stride, f(agg), _lib.stream())
         return agg
 
+    def _rank_launches(self, mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
+                       drop_mask, c, euclid, step, out, gate, exchange):
+        """This rank's launches of one layer into `out`, exchange(j) after chunk j's rows are
+        final.  Large snapshots: the hub pass and the gather once over all of the rank's rows,
+        then each chunk's tail (full-size launches but the tails); otherwise each chunk's whole
+        layer launch."""
+        from .hyperbolic_layers import _use_rowtail, run_layer, run_layer_chunked
+        V, d = x.shape
+        rv = self.rank_view
+        if rv is not None and _use_rowtail(V, int(rv.fw.host["rows"].shape[0]), d, prev_t, drop_mask, False):
+            run_layer_chunked(mode, rv, [v for _, v in self.views], x, r, rel, w_rel, nb, gamma, w_n, w_loop,
+                              w_evolve, c, euclid, step, out, gate, exchange)
+            return
+        for j, (_, view) in enumerate(self.views):
+            run_layer(mode, view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
+                      drop_mask, c, euclid=euclid, step=step, out=out, gate=gate)
+            exchange(j)
+
     def run_layer(self, mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
                   drop_mask, c, euclid=False, step=None, gate=None):
         """The sharded counterpart of hyperbolic_layers.run_layer (same arguments/returns)."""
@@ -467,23 +496,24 @@ class ShardedGraph:
             if self._comm is None:
                 self._comm = torch.cuda.Stream(x.device)
             comm = self._comm
-        for j, (_, view) in enumerate(self.views):
-            run_layer(mode, view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                      drop_mask, c, euclid=euclid, step=step, out=(h[:V], xn[:V], rn[:V]), gate=gate)
+        def exchange(j):  # chunk j of every rank, in place, once this rank's rows are written
             if W == 1:
-                continue
+                return
             a, b, k = j * W * cr, (j + 1) * W * cr, (j * W + self.rank) * cr
             self.exchanged_bytes += (W - 1) * cr * (d + 1) * 4
             if not self.collective:
-                continue
+                return
             if comm is None:
                 _all_gather_into(xn[a:b], xn[k:k + cr], self.group)
                 _all_gather_into(rn[a:b], rn[k:k + cr], self.group)
-                continue
+                return
             comm.wait_stream(cur)
             with torch.cuda.stream(comm):
                 _all_gather_into(xn[a:b], xn[k:k + cr], self.group)
                 _all_gather_into(rn[a:b], rn[k:k + cr], self.group)
+
+        self._rank_launches(mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
+                            drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, exchange)
         if comm is not None:
             cur.wait_stream(comm)
             for t in (xn, rn):
@@ -596,7 +626,6 @@ class RankSimulation(ShardedGraph):
 
     def run_layer(self, mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
                   drop_mask, c, euclid=False, step=None, gate=None):
-        from .hyperbolic_layers import run_layer
         V, d = x.shape
         lay = self.layout
         h = torch.empty(lay.Vp, d, device=x.device, dtype=torch.float32)
@@ -604,9 +633,8 @@ class RankSimulation(ShardedGraph):
         rn = torch.empty(lay.Vp, device=x.device, dtype=torch.float32)
 
         def rank_launches(sg):
-            for _, view in sg.views:
-                run_layer(mode, view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                          drop_mask, c, euclid=euclid, step=step, out=(h[:V], xn[:V], rn[:V]), gate=gate)
+            sg._rank_launches(mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
+                              drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, lambda j: None)
         for k, sg in enumerate(self.ranks):
             self._timed(k, lambda: rank_launches(sg))
             sg.exchanged_bytes += (self.world - 1) * lay.cr * lay.chunks * (d + 1) * 4

@@ -73,16 +73,24 @@ def test_cli_sharded_evaluation_world2():
             assert abs(a - b) <= 0.002, (got, single)
 
 
-@pytest.mark.parametrize("tag,world,chunks", [("uvrgcn_roth_r512_d200", 8, 2), ("lgcn_roth_h7_d200", 3, 1),
-                                              ("uvrgcn_roth_e80k_d200", 4, 3)])
-def test_rank_simulation_matches_unsharded(golden, tag, world, chunks):
+@pytest.mark.parametrize("tag,world,chunks,rowtail", [("uvrgcn_roth_r512_d200", 8, 2, False),
+                                                      ("lgcn_roth_h7_d200", 3, 1, False),
+                                                      ("uvrgcn_roth_e80k_d200", 4, 3, False),
+                                                      ("uvrgcn_roth_e80k_d200", 4, 3, True),
+                                                      ("lgcn_roth_h7_d200", 2, 2, True)])
+def test_rank_simulation_matches_unsharded(golden, tag, world, chunks, rowtail, monkeypatch):
     """The owner partition's per-rank work, all ranks run one after another on the GPU
     (parallel.RankSimulation, bench.py's owner_simulation): each rank's chunk views of every
     layer and its partial relation means, combined, give the unsharded history embeddings
     (1e-4 * max(1, |ref|)) and relation states; a balanced relabel of the entities
-    (EntityRelabel) changes nothing but the row order."""
+    (EntityRelabel) changes nothing but the row order.  rowtail: the large-snapshot layer path
+    (threshold lowered), where a rank's hub pass and gather run once over all of its rows and
+    only the tails per chunk (hyperbolic_layers.run_layer_chunked)."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
+    if rowtail:
+        from regcn_amd import hyperbolic_layers as HL
+        monkeypatch.setattr(HL, "ROWTAIL_MIN_ROWS", 1)
     import numpy as np
     from gpu_helpers import assert_close, build_hyperbolic_model
     from regcn_amd import graph as G
