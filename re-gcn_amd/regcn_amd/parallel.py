@@ -767,8 +767,20 @@ class CandidateShard:
 
     def range_ranks(self, q, cand, bias, c, ts, filt_ptr=None, filt_idx=None, **kw):
         """ranks() over every id range of this shard (one scorer launch and one count launch
-        per range, the counts summed), then ONE all_reduce of the 2B counts."""
+        per range, the counts summed; without a filter the ranges' rows are scored together, as
+        one candidate block), then ONE all_reduce of the 2B counts."""
         tot = None
+        if filt_ptr is None and len(self.ranges) > 1:
+            rows = torch.cat([torch.arange(a, b, device=cand.device) for a, b in self.ranges])
+            cs = cand.index_select(0, rows)
+            bs = bias.index_select(0, rows) if bias is not None else None
+            from .hyperbolic_decoder import _chunked_hyperbolic_dist_score
+            S = _chunked_hyperbolic_dist_score(q, cs, bs, c, 0, 0, score_scale=kw.get("scale"),
+                                               score_margin=kw.get("margin", 0.0), _raw_scale=kw.get("raw_scale", False))
+            self.n0, self.n1 = 0, int(rows.numel())
+            raw, _ = self.local_counts(S, ts)
+            tot = combine_counts(torch.stack([raw, raw]), self.group)
+            return tot[0].long() + 1, tot[1].long() + 1
         for n0, n1 in self.ranges:
             self.n0, self.n1 = n0, n1
             raw, flt = self.local_counts(self.scores(q, cand, bias, c, **kw), ts, filt_ptr, filt_idx)
