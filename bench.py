@@ -1144,7 +1144,11 @@ def main():
                 out["replicas"] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps", "scaling")}
                 out["replicas"]["parallelism"] = r["config"]["parallelism"]
         if rank == 0 and world == 1 and args.sim_ranks > 1 and not args.no_extras:
-            out["owner_simulation"] = owner_simulation(args, cfg, device, args.sim_ranks)
+            sim = owner_simulation(args, cfg, device, args.sim_ranks)
+            # against this run's measured one-GPU step (the simulation's own sum of the ranks'
+            # launches is larger: many short launches)
+            sim["predicted_speedup_vs_headline"] = round(out["ms_per_step"] / sim["predicted_step_ms"], 2)
+            out["owner_simulation"] = sim
         if rank == 0 and world == 1:
             if not args.no_cpu_baseline:
                 out["cpu_baseline"] = cpu_baseline_scale(cfg, args.d, args.cpu_budget)

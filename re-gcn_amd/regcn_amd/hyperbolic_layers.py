@@ -27,6 +27,8 @@ TRACE = None  # int64 HIP tensor (>= 8 x workgroups) to record k_layer phase tim
 # Snapshots with at least this many rows run a layer as the agg gather + the 64-row MFMA tail
 # (regcn_layer_rowtail_f32, csrc/rowtail.hip) instead of the fused 16-row kernel; 0 disables.
 ROWTAIL_MIN_ROWS = int(os.environ.get("REGCN_ROWTAIL_MIN_ROWS", "65536"))
+# ... and a view (a rank's rows of a partitioned snapshot) of at least this many rows
+ROWTAIL_MIN_VIEW_ROWS = int(os.environ.get("REGCN_ROWTAIL_MIN_VIEW_ROWS", "1024"))
 # ... in this many row chunks: the gather of chunk i + 1 runs on a side stream beside the tail of
 # chunk i (the L2-bound gather beside the MFMA-bound tail); 1 = one stream, no pipelining
 ROWTAIL_CHUNKS = int(os.environ.get("REGCN_ROWTAIL_CHUNKS", "1"))
@@ -134,7 +136,7 @@ class StepSpec:
 def _use_rowtail(V, n_rows, d, prev_t, drop_mask, pos_only):
     """The 64-row tail serves large snapshots' layers (V rows; a rank's view of one runs its
     own n_rows) without a skip gate or dropout mask."""
-    return (ROWTAIL_MIN_ROWS > 0 and V >= ROWTAIL_MIN_ROWS and n_rows >= 1024 and prev_t is None
+    return (ROWTAIL_MIN_ROWS > 0 and V >= ROWTAIL_MIN_ROWS and n_rows >= ROWTAIL_MIN_VIEW_ROWS and prev_t is None
             and drop_mask is None and not pos_only and d % 4 == 0 and d <= 256)
 
 

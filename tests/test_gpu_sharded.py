@@ -17,8 +17,12 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("tag", ["uvrgcn_roth_r512_d200", "lgcn_roth_h7_d200"])
-def test_sharded_predict_world2(tmp_path, tag):
+@pytest.mark.parametrize("tag,rowtail", [("uvrgcn_roth_r512_d200", False), ("lgcn_roth_h7_d200", False),
+                                         ("uvrgcn_roth_e80k_d200", True)])
+def test_sharded_predict_world2(tmp_path, tag, rowtail):
+    """rowtail: the large-snapshot layer path (REGCN_ROWTAIL_MIN_ROWS lowered in the ranks),
+    where a rank's hub pass and gather run once and each chunk's tail is followed by its
+    all-gather (hyperbolic_layers.run_layer_chunked)."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -28,6 +32,9 @@ def test_sharded_predict_world2(tmp_path, tag):
     out = str(tmp_path / "res.json")
     env = dict(os.environ, PYTHONPATH=os.path.join(repo, "re-gcn_amd") + os.pathsep + repo,
                REGCN_DIST_BACKEND="gloo")
+    if rowtail:
+        env["REGCN_ROWTAIL_MIN_ROWS"] = "1"
+        env["REGCN_ROWTAIL_MIN_VIEW_ROWS"] = "1"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(repo, "tests", "sharded_predict_job.py"), out, tag]
@@ -91,6 +98,7 @@ def test_rank_simulation_matches_unsharded(golden, tag, world, chunks, rowtail, 
     if rowtail:
         from regcn_amd import hyperbolic_layers as HL
         monkeypatch.setattr(HL, "ROWTAIL_MIN_ROWS", 1)
+        monkeypatch.setattr(HL, "ROWTAIL_MIN_VIEW_ROWS", 1)
     import numpy as np
     from gpu_helpers import assert_close, build_hyperbolic_model
     from regcn_amd import graph as G
