@@ -901,7 +901,11 @@ def owner_simulation(args, cfg, device, world):
     dec_times = [[] for _ in range(world)]
 
     def step():
-        embs, _, r_emb, _, _ = model.forward(sims, None, True)
+        model.__dict__["_owner_rows_only"] = True  # as predict_ranks: no exchange after the last layer
+        try:
+            embs, _, r_emb, _, _ = model.forward(sims, None, True)
+        finally:
+            model.__dict__.pop("_owner_rows_only", None)
         inv = test.flip(1)
         inv[:, 1] = inv[:, 1] + R
         at = torch.cat([test, inv])
@@ -922,6 +926,9 @@ def owner_simulation(args, cfg, device, world):
         torch.cuda.synchronize()
         for sm in sims:
             sm.times = [[] for _ in range(world)]
+            sm.chunk_marks = [[] for _ in range(world)]
+            for sg in sm.ranks:
+                sg.exchanged_bytes = 0
         for k in range(world):
             dec_times[k].clear()
         start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -936,13 +943,19 @@ def owner_simulation(args, cfg, device, world):
     per_rank = enc + dec_ms
     replicated = total - float(per_rank.sum())
     layers = 2 * T
-    xbytes = (world - 1) * lay.cr * lay.chunks * (d + 1) * 4  # received per rank per layer
     link_gbs, links = 153.0, world - 1  # xGMI: 7 links x ~153 GB/s per MI355X
+    # received per rank per step (the sparse exchange: the rows the next layer reads; none
+    # after the last layer), and the all-gather it replaces
+    recv = np.array([sum(sm.ranks[k].exchanged_bytes for sm in sims) for k in range(world)]) / reps
+    full_bytes = (world - 1) * lay.cr * lay.chunks * (d + 1) * 4
+    xbytes = float(recv.max()) / layers
     xchg_ms = xbytes / (links * link_gbs * 1e9) * 1e3
     edges = 2 * sum(sm.number_of_edges() for sm in sims)
-    # the last chunk's all-gather of each layer has no next chunk to hide under
-    exposed = xchg_ms * layers / lay.chunks
-    pred = float(per_rank.max()) + replicated + exposed
+    # per rank: chunk j's exchange starts when chunk j's rows are final and the link is free;
+    # the next layer waits for the last one (RankSimulation.exposed_exchange_ms)
+    exp_k = np.sum([sm.exposed_exchange_ms(link_gbs) for sm in sims], axis=0) / reps
+    exposed = float(exp_k[int(np.argmax(per_rank + exp_k))])
+    pred = float((per_rank + exp_k).max()) + replicated
     return {
         "world": world, "chunks_per_rank": lay.chunks, "rows_per_chunk": lay.cr,
         "per_rank_ms": [round(float(x), 3) for x in per_rank],
@@ -950,8 +963,10 @@ def owner_simulation(args, cfg, device, world):
         "per_rank_decoder_ms": [round(float(x), 3) for x in dec_ms],
         "max_rank_ms": round(float(per_rank.max()), 3), "mean_rank_ms": round(float(per_rank.mean()), 3),
         "replicated_ms": round(replicated, 3), "single_gpu_equivalent_ms": round(total, 3),
-        "exchange_bytes_per_layer_per_rank": int(xbytes), "exchange_gb_per_step_per_rank": round(xbytes * layers / 1e9, 3),
+        "exchange_bytes_per_layer_per_rank": int(xbytes), "exchange_gb_per_step_per_rank": round(float(recv.max()) / 1e9, 3),
+        "allgather_bytes_per_layer_per_rank": int(full_bytes),
         "exchange_ms_per_layer_at_7_links": round(xchg_ms, 3),
+        "exposed_exchange_ms_per_rank": [round(float(x), 3) for x in exp_k],
         "exposed_exchange_ms_per_step": round(exposed, 3),
         "edge_loads_per_rank": loads, "edge_loads_contiguous_ids": loads_plain,
         "predicted_step_ms": round(pred, 3),
@@ -960,9 +975,11 @@ def owner_simulation(args, cfg, device, world):
         "setup_s": round(setup_s, 1),
         "note": "ranks run one after another on one MI355X (parallel.RankSimulation); per-rank = device time "
                 "of its own launches (layer chunks incl. hub pass, relation-mean partials, its candidate "
-                "slice); replicated = the rest of the step; predicted step = max rank + replicated + the "
-                "exposed all-gathers (exchange_ms_per_layer at the nominal link rate, each layer's last "
-                "chunk: the others hide under the next chunk's tail)",
+                "slice; the pack / unpack of its exchanges); replicated = the rest of the step; predicted "
+                "step = max over ranks of (rank + its exposed exchange) + replicated.  Exchange: per chunk one "
+                "all_to_all of the rows the next layer reads (ExchangePlan), its time = the busiest peer "
+                "link's bytes at the nominal 153 GB/s, starting when the chunk's rows are final and the "
+                "previous chunk's exchange is done; a layer exposes what runs past its last chunk",
     }
 
 

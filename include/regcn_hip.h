@@ -584,6 +584,14 @@ int regcn_rank_f32(const float* score, int32_t B, int32_t N, const int32_t* targ
  * regcn_rank_f32's ranks, threshold = the target's score. */
 int regcn_rank_count_f32(const float* score, int32_t B, int32_t N, const float* threshold, const int32_t* filt_ptr,
                          const int32_t* filt_idx, int32_t* count_raw, int32_t* count_filt, void* stream);
+/* e: the owner partition's exchange (the reference runs on one GPU, so no
+ * reference call site): rows ids[i] of x (n_rows x d) and radius packed as records of stride
+ * d + 4 floats (x row, radius, 3 pad) for one all_to_all, and the received records written back
+ * to rows ids[i].  d % 4 == 0, d <= 252, x and the record buffer 16-B aligned. */
+int regcn_pack_rows_f32(const float* x, const float* radius, const int64_t* ids, int64_t n, int32_t d, float* out,
+                        void* stream);
+int regcn_unpack_rows_f32(const float* in, const int64_t* ids, int64_t n, int32_t d, float* x, float* radius,
+                          void* stream);
 
 /* ---- a1 / f3: snapshot construction on the device ------------------------------------
  * build_sub_graph + r2e (rgcn/utils.py:78-134) and the kernel work lists of

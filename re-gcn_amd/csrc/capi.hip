@@ -648,6 +648,14 @@ int regcn_rank_count_f32(const float* score_m, int32_t B, int32_t N, const float
   return rank(score_m, B, N, nullptr, threshold, filt_ptr, filt_idx, 0, count_raw, count_filt, ST(s));
 }
 
+int regcn_pack_rows_f32(const float* x, const float* radius, const int64_t* ids, int64_t n, int32_t d, float* out,
+                        void* s) {
+  return exchange_rows(1, const_cast<float*>(x), const_cast<float*>(radius), ids, n, d, out, ST(s));
+}
+int regcn_unpack_rows_f32(const float* in, const int64_t* ids, int64_t n, int32_t d, float* x, float* radius, void* s) {
+  return exchange_rows(0, x, radius, ids, n, d, const_cast<float*>(in), ST(s));
+}
+
 size_t regcn_snapshot_workspace_bytes(int64_t T, int32_t V, int32_t R) { return snapshot_ws_bytes(T, V, R); }
 int64_t regcn_snapshot_capacity(int32_t what, int64_t T, int32_t V, int32_t R, int32_t chunk_edges) {
   return snapshot_capacity(what, T, V, R, chunk_edges);

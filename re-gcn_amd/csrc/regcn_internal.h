@@ -315,6 +315,7 @@ int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st);
 // workgroup of the query's tile (persistent fp32 kernel, <= 8 x 32).
 inline size_t ce_partial_slots(int N) { return std::max<size_t>(((size_t)N + 63) / 64, 256); }
 int score_ce_bwd(ScoreArgs& a, hipStream_t st);
+int exchange_rows(int pack, float* x, float* r, const int64_t* idx, int64_t n, int d, float* buf, hipStream_t st);
 int rank(const float* S, int B, int N, const int* target, const float* ts, const int* filt_ptr, const int* filt_idx,
          int add, int* rank_raw, int* rank_filt, hipStream_t st);
 

@@ -196,4 +196,54 @@ int rowmap(int op, const float* a, const float* b, const float* vec, int64_t row
   return set_error(REGCN_EINVAL, "unknown row op %d", op);
 }
 
+
+// ------------------------------------------------------- owner-partition row exchange
+// The rows of x (d floats) and |h| (1 float) the next layer of another rank reads, packed as
+// one record of stride d + 4 floats (16-B aligned records: the x part moves as 16-B vectors;
+// float d holds |h|, d+1..d+3 are padding) for one all_to_all (parallel.ExchangePlan); the
+// unpack scatters the received records back.  One 64-lane wave per record, lane l moves the
+// 16-B group l (d <= 252), lane d/4 the radius: HBM-bound, 2 x 816 B of traffic per row.
+__global__ __launch_bounds__(256) void k_pack_rows(const float* __restrict__ x, const float* __restrict__ r,
+                                                   const int64_t* __restrict__ idx, int64_t n, int d,
+                                                   float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int lane = threadIdx.x & 63, q = d >> 2;
+  const int64_t src = idx[i];
+  float* o = out + i * (d + 4);
+  if (lane < q) {
+    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x + src * d) + lane);
+    reinterpret_cast<f4*>(o)[lane] = v;
+  } else if (lane == q) {
+    reinterpret_cast<f4*>(o)[lane] = f4{r[src], 0.f, 0.f, 0.f};
+  }
+}
+
+__global__ __launch_bounds__(256) void k_unpack_rows(const float* __restrict__ in, const int64_t* __restrict__ idx,
+                                                     int64_t n, int d, float* __restrict__ x, float* __restrict__ r) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int lane = threadIdx.x & 63, q = d >> 2;
+  const int64_t dst = idx[i];
+  const float* s = in + i * (d + 4);
+  if (lane < q) {
+    reinterpret_cast<f4*>(x + dst * d)[lane] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(s) + lane);
+  } else if (lane == q) {
+    r[dst] = s[d];
+  }
+}
+
+int exchange_rows(int pack, float* x, float* r, const int64_t* idx, int64_t n, int d, float* buf, hipStream_t st) {
+  if (n == 0) return 0;
+  if (!x || !r || !idx || !buf) return set_error(REGCN_EINVAL, "null pointer");
+  if (d <= 0 || (d & 3) || d > 4 * (WAVE - 1)) return set_error(REGCN_EINVAL, "row exchange needs d %% 4 == 0, d <= 252");
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(buf)) & 15)
+    return set_error(REGCN_EINVAL, "row exchange needs 16-B aligned x and buffer");
+  const int64_t blocks = (n + 3) / 4;
+  if (blocks > 0x7fffffffL) return set_error(REGCN_EINVAL, "row exchange grid too large");
+  if (pack) hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)blocks), dim3(256), 0, st, x, r, idx, n, d, buf);
+  else hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)blocks), dim3(256), 0, st, buf, idx, n, d, x, r);
+  return check_launch(pack ? "k_pack_rows" : "k_unpack_rows");
+}
+
 }  // namespace regcn

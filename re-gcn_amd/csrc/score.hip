@@ -849,36 +849,54 @@ __global__ __launch_bounds__(256) void k_ce_combine(const float* __restrict__ pa
 // and the same count excluding the other true answers of the snapshot (time-aware
 // filter, rgcn/utils.py:51-75 sets them to -1e7).  filt_ptr/filt_idx: CSR of the
 // entities to exclude per query (target itself excluded by the host).
-__global__ __launch_bounds__(256) void k_rank(const float* __restrict__ S, int B, int N, const int* __restrict__ target,
-                                              const float* __restrict__ ts_in, const int* __restrict__ filt_ptr,
-                                              const int* __restrict__ filt_idx, int add, int* __restrict__ rank_raw,
-                                              int* __restrict__ rank_filt) {
-  const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
+// One workgroup (4 waves) per query row: the row is a streaming read (N floats), so every
+// thread keeps RANK_UNROLL 16-B loads in flight over the 16-B aligned body (a scalar head and
+// tail around it: rows start anywhere when N % 4 != 0).  Integer counts, so any split is exact.
+constexpr int RANK_THR = 256, RANK_UNROLL = 4;
+__global__ __launch_bounds__(RANK_THR) void k_rank(const float* __restrict__ S, int B, int N, const int* __restrict__ target,
+                                                   const float* __restrict__ ts_in, const int* __restrict__ filt_ptr,
+                                                   const int* __restrict__ filt_idx, int add, int* __restrict__ rank_raw,
+                                                   int* __restrict__ rank_filt) {
+  __shared__ int red[2][RANK_THR / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int b = blockIdx.x;
   const float* row = S + (int64_t)b * N;
   const float ts = ts_in ? ts_in[b] : row[target[b]];
+  const int head = min(N, (int)((16 - (reinterpret_cast<uintptr_t>(row) & 15)) & 15) / 4);
+  const int nb4 = (N - head) / 4;  // aligned 4-float groups
+  const f4* body = reinterpret_cast<const f4*>(row + head);
   int cnt = 0;
-  for (int n = lane * 4; n < N; n += 256) {
-    if (n + 3 < N && ((reinterpret_cast<uintptr_t>(row + n) & 15) == 0)) {
-      f4 v = *reinterpret_cast<const f4*>(row + n);
-      cnt += (v.x > ts) + (v.y > ts) + (v.z > ts) + (v.w > ts);
-    } else {
-      for (int u = 0; u < 4 && n + u < N; ++u) cnt += row[n + u] > ts;
-    }
+  if (tid < head) cnt += row[tid] > ts;
+  for (int i = head + 4 * nb4 + tid; i < N; i += RANK_THR) cnt += row[i] > ts;
+  int i = tid;
+  for (; i + (RANK_UNROLL - 1) * RANK_THR < nb4; i += RANK_UNROLL * RANK_THR) {
+    f4 v[RANK_UNROLL];
+#pragma unroll
+    for (int u = 0; u < RANK_UNROLL; ++u) v[u] = __builtin_nontemporal_load(body + i + u * RANK_THR);
+#pragma unroll
+    for (int u = 0; u < RANK_UNROLL; ++u) cnt += (v[u].x > ts) + (v[u].y > ts) + (v[u].z > ts) + (v[u].w > ts);
+  }
+  for (; i < nb4; i += RANK_THR) {
+    const f4 v = body[i];
+    cnt += (v.x > ts) + (v.y > ts) + (v.z > ts) + (v.w > ts);
   }
   int f = 0;
   if (filt_ptr) {
-    for (int i = filt_ptr[b] + lane; i < filt_ptr[b + 1]; i += 64) f += row[filt_idx[i]] > ts;
+    for (int j = filt_ptr[b] + tid; j < filt_ptr[b + 1]; j += RANK_THR) f += row[filt_idx[j]] > ts;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     cnt += __shfl_xor(cnt, o);
     f += __shfl_xor(f, o);
   }
-  if (lane == 0) {
-    rank_raw[b] = cnt + add;
-    if (rank_filt) rank_filt[b] = cnt - f + add;
+  if (lane == 0) red[0][w] = cnt, red[1][w] = f;
+  __syncthreads();
+  if (tid == 0) {
+    int c = 0, ff = 0;
+#pragma unroll
+    for (int k = 0; k < RANK_THR / 64; ++k) c += red[0][k], ff += red[1][k];
+    rank_raw[b] = c + add;
+    if (rank_filt) rank_filt[b] = c - ff + add;
   }
 }
 
@@ -973,7 +991,7 @@ int rank(const float* S, int B, int N, const int* target, const float* ts, const
          int add, int* rank_raw, int* rank_filt, hipStream_t st) {
   if (!S || (!target && !ts) || !rank_raw) return set_error(REGCN_EINVAL, "null pointer");
   if (B == 0) return 0;
-  hipLaunchKernelGGL(k_rank, dim3((B + 3) / 4), dim3(256), 0, st, S, B, N, target, ts, filt_ptr, filt_idx, add,
+  hipLaunchKernelGGL(k_rank, dim3(B), dim3(RANK_THR), 0, st, S, B, N, target, ts, filt_ptr, filt_idx, add,
                      rank_raw, rank_filt);
   return check_launch("k_rank");
 }

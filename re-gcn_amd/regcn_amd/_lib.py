@@ -59,6 +59,8 @@ _SIGS = {
     "regcn_hyp_ce_f32": [P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P, P],
     "regcn_rank_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
     "regcn_rank_count_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
+    "regcn_pack_rows_f32": [P, P, P, ctypes.c_int64, _c_int, P, P],
+    "regcn_unpack_rows_f32": [P, P, ctypes.c_int64, _c_int, P, P, P],
     "regcn_layer_f32": [P, P],
     "regcn_layer_rowtail_f32": [P, P, P],
     "regcn_layer_rowtail_part_f32": [P, P, _c_int, _c_int, _c_int, P],

@@ -577,6 +577,19 @@ def rel_block_work(g, R):
 # share its row from one L2.
 HUB_BLOCK = int(os.environ.get("REGCN_HUB_BLOCK", "16384"))  # source ids per block; 0: plain chunks
 HUB_BLOCK_MIN_EDGES = 1 << 20
+HUB_CHUNK = int(os.environ.get("REGCN_HUB_CHUNK", "0"))  # edges per hub chunk; 0: hub_chunk()
+HUB_CHUNKS_MIN = 16384
+
+
+def hub_chunk(total_edges, chunk_edges):
+    """Edges per hub-pass chunk (one wave each): the snapshot's chunk size, shrunk (not below
+    256) so the pass has at least HUB_CHUNKS_MIN chunks.  An owner-partitioned rank holds ~1/8
+    of the hub edges: config 5's 8-rank simulation at 1024 / 256 edges per chunk runs 5.42 /
+    5.21 ms of encoder per rank (profiles/r4_hub_chunk_sweep.txt); the whole snapshot keeps 1024."""
+    if HUB_CHUNK:
+        return max(HUB_CHUNK, 64)
+    base = max(int(chunk_edges or 1024), 64)
+    return min(base, max(256, -(-int(total_edges) // HUB_CHUNKS_MIN)))
 
 
 def hub_block_work(g):
@@ -596,9 +609,11 @@ def hub_block_work(g):
         rows = wk["rows"][:g.n_heavy].long()
         beg = wk["rowptr"].long()[rows]
         ln = wk["rowptr"].long()[rows + 1] - beg
-        if int(ln.sum()) >= HUB_BLOCK_MIN_EDGES:
+        total = int(ln.sum())
+        if total >= HUB_BLOCK_MIN_EDGES:
             ss = g.row_src_cols()
-            ch, fx, ns = blocked_span_chunks(rows, beg, ln, ss, spread_block(g.number_of_nodes(), HUB_BLOCK), max(int(getattr(g, "chunk_edges", None) or 1024), 64))
+            ch, fx, ns = blocked_span_chunks(rows, beg, ln, ss, spread_block(g.number_of_nodes(), HUB_BLOCK),
+                                             hub_chunk(total, getattr(g, "chunk_edges", None)))
             res = (ch, torch.from_numpy(fx).to(ss.device), ns)
             from . import _lib
             _lib.publish()

@@ -31,6 +31,7 @@ from .graph import SnapshotGraph, rel_block_work
 from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell, LorentzRGCNLayer, StepSpec, \
     _heavy_aggregate
 from .hyperbolic_ops import HyperbolicOps, TemporalRadiusEvolution
+from .parallel import FULL_EXCHANGE, ShardedGraph
 from .tangent import attach, tangent_of
 from .weights import invalidate, packed
 
@@ -109,13 +110,20 @@ def relation_context(x, g, num_rels2):
 REL_INLINE_MAX_SPAN = 64  # longer r_to_e spans are averaged by the chunked segment-mean kernel first
 
 
+def _means_first(g):
+    """The relation means as their own launch: long r_to_e spans, or an owner-partitioned
+    snapshot (a rank holds only the rows the exchange sent it: the partitioned sums, never the
+    GRU's inline means over every entity)."""
+    return g.rel_max_span > REL_INLINE_MAX_SPAN or (getattr(g, "partition", None) == "owner" and g.world > 1)
+
+
 def relation_gru_step(gru, emb_rel, x, g, h_prev):
     """h_0' = GRUCell([emb_rel | mean_{r_to_e} x], h_prev) in one launch
     (regcn_relation_gru_f32; hyperbolic_model.py:797-818, src/rrgcn.py:161-174)."""
     from .weights import packed_linear
     wk = g.work()
     R2, d = emb_rel.shape
-    x_mean = relation_context(x, g, R2) if g.rel_max_span > REL_INLINE_MAX_SPAN else None
+    x_mean = relation_context(x, g, R2) if _means_first(g) else None
     zeros = None
     if gru.bias_ih is None:
         zeros = torch.zeros(3 * d, device=emb_rel.device, dtype=torch.float32)
@@ -159,7 +167,7 @@ def relation_gru_x(gru, x, g, h_prev, pre):
     from .weights import packed_linear_cols
     wk = g.work()
     R2, d = h_prev.shape
-    x_mean = relation_context(x, g, R2) if g.rel_max_span > REL_INLINE_MAX_SPAN else None
+    x_mean = relation_context(x, g, R2) if _means_first(g) else None
     out = torch.empty(R2, d, device=h_prev.device, dtype=torch.float32)
     f = _lib.fptr
     _lib.call("regcn_relation_gru_x_f32", f(x, "x"), _lib.iptr(wk["rel_idx"]) if wk["rel_idx"].numel() else None,
@@ -373,8 +381,16 @@ class HyperbolicRecurrentRGCN(nn.Module):
         if ana and self.training:  # hyperbolic_model.py:791-792
             _ana.log_embedding(self, h, "init_embeddings", c_val)
         gate_list, gate_means = [], []
+        fused_step = len(self.rgcn.layers) > 0 and not self.run_analysis
         for i, g in enumerate(g_list):
             g = g.to(dev)
+            if isinstance(g, ShardedGraph) and g.partition == "owner":
+                # the owner partition sends each layer's new rows only to the ranks whose next
+                # layer reads them: this snapshot's sources, then the next timestep's; after the
+                # last timestep all rows, unless the caller reads only its own (predict_ranks)
+                nxt = g_list[i + 1] if i + 1 < len(g_list) else \
+                    (None if self.__dict__.get("_owner_rows_only") else FULL_EXCHANGE)
+                g.consumers = (g, nxt) if fused_step else None
             x_prev, _ = tangent_of(self.h, c_val)
             h_prev = self.emb_rel if i == 0 else self.h_0  # the two-phase GRU, as _forward_phases runs it
             self.h_0 = relation_gru_x(self.relation_gru, x_prev, g, h_prev,
@@ -830,7 +846,13 @@ class HyperbolicRecurrentRGCN(nn.Module):
         sg = sharded[-1]
         with torch.no_grad():
             c_val = self._c_float()
-            embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
+            # every rank reads only its own rows of the last state (its candidates) plus the
+            # queries' rows, fetched below: the last layer's exchange is skipped
+            self.__dict__["_owner_rows_only"] = True
+            try:
+                embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
+            finally:
+                self.__dict__.pop("_owner_rows_only", None)
             inv = test_triplets.flip(1)
             inv[:, 1] = inv[:, 1] + num_rels
             at = torch.cat([test_triplets, inv])

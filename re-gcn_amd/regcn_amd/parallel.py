@@ -155,6 +155,96 @@ class OwnerView:
         return self._dev
 
 
+# ------------------------------------------------------------------ sparse exchange
+def exchange_keys(g, layout):
+    """The (receiver, row) pairs of the owner partition's exchange for consumer snapshot `g`:
+    rank m needs row s of another rank when s is the source of an in-edge of one of m's rows
+    (the next layer reads x[s] and |h|[s] for its messages; its own rows it computed itself).
+    Returns (m, s) int64 tensors sorted by (m, s), on the graph's device; cached on `g`."""
+    key = (layout.world, layout.chunks, layout.cr)
+    hit = g.__dict__.get("_xkeys")
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    if getattr(g, "dev", None) is not None:
+        wk = g.work()
+        rowptr, src = wk["rowptr"].long(), wk["col_src"].long()
+    else:
+        rowptr = torch.from_numpy(g._host["rowptr"].astype(np.int64))
+        src = torch.from_numpy(g._host["col_src"].astype(np.int64))
+    V = g.number_of_nodes()
+    E = int(rowptr[-1])
+    src = src[:E]
+    dev = src.device
+    dst_owner = torch.repeat_interleave(layout.owner(torch.arange(V, device=dev)), rowptr[1:] - rowptr[:-1])
+    remote = layout.owner(src) != dst_owner
+    pairs = torch.unique(dst_owner[remote] * layout.Vp + src[remote])  # sorted: by receiver, then row
+    out = (pairs // layout.Vp, pairs % layout.Vp)
+    g.__dict__["_xkeys"] = (key, out)
+    return out
+
+
+class ExchangePlan:
+    """Rank `rank`'s part of the owner partition's exchange for one consumer snapshot, per
+    pipeline chunk j: the ids of its own chunk-j rows that each other rank needs (grouped by
+    receiver in rank order, ascending inside a group), the ids it receives (grouped by sender,
+    ascending), and the split sizes of ONE all_to_all_single (x | |h| packed, 804 B per row at
+    d = 200).  Every rank derives its lists from the same global snapshot (exchange_keys), so a
+    sender's group for m and m's group from that sender hold the same ids in the same order.
+    Config 5 at 8 ranks: a rank needs ~46 % of the other ranks' rows (Zipf sources), against
+    all of them in the all-gather (a direct full-mesh exchange over xGMI)."""
+
+    def __init__(self, g, layout, rank):
+        m, s = exchange_keys(g, layout)
+        W, cr = layout.world, layout.cr
+        k = layout.owner(s)
+        j = (s // cr) // W
+        self.world, self.chunks = W, []
+        for jj in range(layout.chunks):
+            sm = (k == rank) & (j == jj)
+            rm = (m == rank) & (j == jj)
+            send, recv = s[sm], s[rm]
+            self.chunks.append((send, torch.bincount(m[sm], minlength=W).tolist(),
+                                recv, torch.bincount(k[rm], minlength=W).tolist()))
+
+    def rows_received(self):
+        return sum(sum(c[3]) for c in self.chunks)
+
+    def link_rows(self, j):
+        """The largest per-peer row count of chunk j's exchange, either direction (each peer
+        pair has its own xGMI link, so the exchange takes max over links)."""
+        _, ss, _, rs = self.chunks[j]
+        return max(max(ss), max(rs)) if ss else 0
+
+
+def pack_rows(xn, rn, ids):
+    """(len(ids), d + 4) records [x row, |h|, pad] of rows `ids` (regcn_pack_rows_f32)."""
+    d = xn.shape[1]
+    out = torch.empty(ids.numel(), d + 4, device=xn.device, dtype=torch.float32)
+    _lib.call("regcn_pack_rows_f32", _lib.fptr(xn, "x"), _lib.fptr(rn, "radius"), _lib.dptr(ids, torch.int64, "ids"),
+              ids.numel(), d, _lib.fptr(out), _lib.stream())
+    return out
+
+
+def unpack_rows(buf, ids, xn, rn):
+    """Records of pack_rows written back to rows `ids` of xn / rn (regcn_unpack_rows_f32)."""
+    _lib.call("regcn_unpack_rows_f32", _lib.fptr(buf, "records"), _lib.dptr(ids, torch.int64, "ids"), ids.numel(),
+              xn.shape[1], _lib.fptr(xn, "x"), _lib.fptr(rn, "radius"), _lib.stream())
+
+
+def exchange_rows(chunk, xn, rn, group=None, pack=pack_rows, unpack=unpack_rows):
+    """One chunk of an ExchangePlan: this rank's rows other ranks read (x | |h| records),
+    ONE all_to_all_single, the received records written into xn / rn in place.  `pack` /
+    `unpack`: the HIP kernels (a CPU test of the plan passes torch stand-ins)."""
+    sidx, ss, ridx, rs = chunk
+    send = pack(xn, rn, sidx)
+    recv = torch.empty(ridx.numel(), send.shape[1], device=xn.device, dtype=xn.dtype)
+    _all_to_all_into(recv, send, rs, ss, group)
+    unpack(recv, ridx, xn, rn)
+
+
+FULL_EXCHANGE = "all rows"  # ShardedGraph.consumers: the next consumer is unknown -> all-gather
+
+
 # ------------------------------------------------------------- balanced entity relabel
 def _lpt(load, caps, head=None):
     """Group (0 .. len(caps) - 1) of every item: longest-processing-time first -- items by
@@ -307,6 +397,16 @@ def _all_gather_into(out, chunk, group=None):
         dist.all_gather_into_tensor(out, chunk, group=group)
 
 
+def _all_to_all_into(out, inp, out_splits, in_splits, group=None):
+    """all_to_all_single with split sizes (rows); gloo through host tensors."""
+    if dist.get_backend(group) == "gloo":
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(o.to(out.device))
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
 def allgather_fused(tensors, per, rows=None, group=None):
     """One collective for several row-aligned tensors (h, log0 h, |h| of the owner
     partition): this rank's rows `rows` (a slice of its block, default all `per`) of every
@@ -382,7 +482,36 @@ class ShardedGraph:
         # collectives only inside a process group of world > 1 (a single-process simulation of
         # one rank, bench.py's owner_simulation, runs the rank's launches alone)
         self.collective = dist.is_initialized() and dist.get_world_size(group) > 1
-        self.exchanged_bytes = 0  # bytes this rank received in the owner all-gathers (bench)
+        self.exchanged_bytes = 0  # bytes this rank received in the owner exchanges (bench)
+        # (after a non-step layer, after the step layer) the snapshot whose layer reads the new
+        # rows next, set per timestep by HyperbolicRecurrentRGCN.forward: a ShardedGraph (the
+        # sparse exchange of its ExchangePlan), None (nothing reads them: no exchange) or
+        # FULL_EXCHANGE; unset (None): every layer all-gathers every row
+        self.consumers = None
+
+    def exchange_plan(self, step):
+        """None: all-gather every row; False: no exchange; else the ExchangePlan of the layer's
+        consumer (self for a cell's inner layer, the next timestep's snapshot after the step)."""
+        if self.consumers is None:
+            return None
+        target = self.consumers[1] if step is not None else self.consumers[0]
+        if target is None:
+            return False
+        if target is FULL_EXCHANGE:
+            return None
+        plans = target.__dict__.setdefault("_xplans", {})
+        key = (self.rank, self.world, self.layout.chunks)
+        if key not in plans:
+            plans[key] = ExchangePlan(target.g, self.layout, self.rank)
+        return plans[key]
+
+    def link_bytes(self, plan, j, d):
+        """Bytes on the busiest peer link in chunk j's exchange (the all-gather: one chunk of
+        rows from every peer)."""
+        if plan is False:
+            return 0
+        rows = self.layout.cr if plan is None else plan.link_rows(j)
+        return rows * (d + 1) * 4
 
     def __getattr__(self, name):  # delegate the DGL-visible surface and work lists
         return getattr(self.__dict__["g"], name)
@@ -496,21 +625,29 @@ class ShardedGraph:
             if self._comm is None:
                 self._comm = torch.cuda.Stream(x.device)
             comm = self._comm
-        def exchange(j):  # chunk j of every rank, in place, once this rank's rows are written
-            if W == 1:
-                return
+        plan = self.exchange_plan(step) if W > 1 else False
+
+        def gather_all(j):  # chunk j of every rank, in place
             a, b, k = j * W * cr, (j + 1) * W * cr, (j * W + self.rank) * cr
-            self.exchanged_bytes += (W - 1) * cr * (d + 1) * 4
+            _all_gather_into(xn[a:b], xn[k:k + cr], self.group)
+            _all_gather_into(rn[a:b], rn[k:k + cr], self.group)
+
+        def gather_needed(j):  # the rows the consumer reads
+            exchange_rows(plan.chunks[j], xn, rn, self.group)
+
+        def exchange(j):  # once this rank's chunk-j rows are written
+            if plan is False:
+                return
+            self.exchanged_bytes += ((W - 1) * cr if plan is None else sum(plan.chunks[j][3])) * (d + 1) * 4
             if not self.collective:
                 return
+            fn = gather_all if plan is None else gather_needed
             if comm is None:
-                _all_gather_into(xn[a:b], xn[k:k + cr], self.group)
-                _all_gather_into(rn[a:b], rn[k:k + cr], self.group)
+                fn(j)
                 return
             comm.wait_stream(cur)
             with torch.cuda.stream(comm):
-                _all_gather_into(xn[a:b], xn[k:k + cr], self.group)
-                _all_gather_into(rn[a:b], rn[k:k + cr], self.group)
+                fn(j)
 
         self._rank_launches(mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
                             drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, exchange)
@@ -615,6 +752,7 @@ class RankSimulation(ShardedGraph):
         for r in self.ranks:
             r.collective = False
         self.times = [[] for _ in range(world)]
+        self.chunk_marks = [[] for _ in range(world)]  # per rank: (chunk-end events, link bytes) per layer
 
     def _timed(self, k, fn):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -632,13 +770,50 @@ class RankSimulation(ShardedGraph):
         xn = torch.empty(lay.Vp, d, device=x.device, dtype=torch.float32)
         rn = torch.empty(lay.Vp, device=x.device, dtype=torch.float32)
 
-        def rank_launches(sg):
+        def rank_launches(sg, plan, marks):
+            def after(j):  # chunk j's rows final: its exchange's pack / unpack on this stream
+                if plan:
+                    sidx, _, ridx, _ = plan.chunks[j]
+                    del sidx
+                    # the receive side's records (same count and traffic as the send side's),
+                    # written back: the rows already hold these values in the simulation
+                    unpack_rows(pack_rows(xn, rn, ridx), ridx, xn, rn)
+                    pack_rows(xn, rn, plan.chunks[j][0])
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                marks.append(e)
             sg._rank_launches(mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                              drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, lambda j: None)
+                              drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, after)
         for k, sg in enumerate(self.ranks):
-            self._timed(k, lambda: rank_launches(sg))
-            sg.exchanged_bytes += (self.world - 1) * lay.cr * lay.chunks * (d + 1) * 4
+            sg.consumers = self.consumers
+            plan = sg.exchange_plan(step)
+            marks = []
+            self._timed(k, lambda: rank_launches(sg, plan, marks))
+            rows = 0 if plan is False else ((self.world - 1) * lay.cr * lay.chunks if plan is None
+                                            else plan.rows_received())
+            sg.exchanged_bytes += rows * (d + 1) * 4
+            self.chunk_marks[k].append((marks, [sg.link_bytes(plan, j, d) for j in range(len(marks))]))
         return h[:V], xn[:V], rn[:V]
+
+    def exposed_exchange_ms(self, link_gbs=153.0):
+        """Per rank: the exchange time no compute hides, summed over the layers run since
+        `chunk_marks` was cleared.  Chunk j's exchange (its busiest peer link's bytes at
+        `link_gbs`) starts when chunk j's rows are final and the previous exchange is done; the
+        next layer starts when the last one is done, so a layer exposes end(last exchange) -
+        end(last chunk)."""
+        out = []
+        for marks_k in self.chunk_marks:
+            tot = 0.0
+            for marks, nbytes in marks_k:
+                if not marks:
+                    continue
+                t = [marks[0].elapsed_time(e) for e in marks]
+                end = 0.0
+                for tj, bj in zip(t, nbytes):
+                    end = max(end, tj) + bj / (link_gbs * 1e6)
+                tot += max(0.0, end - t[-1])
+            out.append(tot)
+        return out
 
     def relation_means(self, x, R2):
         means = [self._timed(k, lambda: ShardedGraph.relation_means(sg, x, R2)) for k, sg in enumerate(self.ranks)]

@@ -707,3 +707,57 @@ def test_candidate_sharded_decoder(world):
     loss = (lse - full[torch.arange(B, device=DEV), tgt]).mean()
     ref = _chunked_hyperbolic_ce_loss(q, e, tgt, C, 0, candidate_bias=bias, score_scale=scale, score_margin=margin)
     assert abs(float(loss) - float(ref)) <= 1e-5 * max(1.0, abs(float(ref)))
+
+
+@pytest.mark.parametrize("N", [1, 3, 7, 1023, 4099, 130001])
+def test_rank_counts_vs_torch(N):
+    """regcn_rank_f32 (k_rank: one workgroup per query, 16-B body loads between a scalar head
+    and tail -- a row starts anywhere when N % 4 != 0) against torch's count of the scores above
+    the target's, raw and filtered; quantised scores, so ties with the target occur."""
+    from regcn_amd import ranking
+    g = torch.Generator().manual_seed(N)
+    B = 37
+    S = (torch.randint(0, 64, (B, N), generator=g).float() / 8.0).to(DEV)
+    tgt = torch.randint(0, N, (B,), generator=g)
+    rng = np.random.default_rng(N)
+    ptr, idx = [0], []
+    for b in range(B):
+        o = rng.integers(0, N, size=rng.integers(0, 9))
+        idx.extend(sorted(set(o.tolist()) - {int(tgt[b])}))
+        ptr.append(len(idx))
+    fp, fi = np.asarray(ptr, np.int32), np.asarray(idx, np.int32)
+    raw, flt = ranking.ranks(S, tgt, fp, fi)
+    Sc = S.cpu()
+    ts = Sc[torch.arange(B), tgt].unsqueeze(1)
+    want = 1 + (Sc > ts).sum(1)
+    wf = want.clone()
+    for b in range(B):
+        cols = torch.from_numpy(fi[fp[b]:fp[b + 1]].astype(np.int64))
+        wf[b] -= int((Sc[b, cols] > ts[b]).sum())
+    assert torch.equal(raw.cpu(), want) and torch.equal(flt.cpu(), wf)
+
+
+@pytest.mark.parametrize("d", [8, 200, 252])
+def test_pack_unpack_rows(d):
+    """regcn_pack_rows_f32 / regcn_unpack_rows_f32 (the owner partition's exchange records):
+    records [x row, |h|, 0, 0, 0] of the listed rows, bit for bit, and the unpack writes exactly
+    the listed rows back."""
+    from regcn_amd.parallel import pack_rows, unpack_rows
+    g = torch.Generator().manual_seed(d)
+    V = 5000
+    x = torch.randn(V, d, generator=g).to(DEV)
+    r = torch.rand(V, generator=g).to(DEV)
+    ids = torch.randperm(V, generator=g)[:1237].to(DEV)
+    buf = pack_rows(x, r, ids)
+    assert buf.shape == (1237, d + 4)
+    assert torch.equal(buf[:, :d], x[ids]) and torch.equal(buf[:, d], r[ids])
+    assert torch.equal(buf[:, d + 1:], torch.zeros(1237, 3, device=DEV))
+    x2 = torch.full_like(x, float("nan"))
+    r2 = torch.full_like(r, float("nan"))
+    unpack_rows(buf, ids, x2, r2)
+    hit = torch.zeros(V, dtype=torch.bool, device=DEV)
+    hit[ids] = True
+    assert torch.equal(x2[hit], x[hit]) and torch.equal(r2[hit], r[hit])
+    assert torch.isnan(x2[~hit]).all() and torch.isnan(r2[~hit]).all()
+    empty = torch.zeros(0, dtype=torch.int64, device=DEV)
+    assert pack_rows(x, r, empty).shape == (0, d + 4)

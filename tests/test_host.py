@@ -374,3 +374,12 @@ def test_rowtail_chunks_partition_tiles_and_rows():
             assert t0 < t1 and r0 <= r1
             if nxt is not None:
                 assert nxt[0] == t1 and nxt[2] == r1 and r1 == starts[t1]
+
+
+def test_hub_chunk_size():
+    """graph.hub_chunk: the snapshot's chunk size for a whole config-5 snapshot's hubs (32.7M
+    edges), shrunk towards 256 for an owner rank's eighth so the pass keeps >= 16k chunks."""
+    assert G.hub_chunk(32_700_000, 1024) == 1024
+    assert G.hub_chunk(4_100_000, 1024) == 256
+    assert G.hub_chunk(8_000_000, 1024) == 489
+    assert G.hub_chunk(1 << 20, None) == 256

@@ -323,3 +323,66 @@ def test_replica_gradients_gloo():
         opt.step()
     for a, b in zip(m.parameters(), p0):
         assert float((a.detach() - torch.from_numpy(b)).abs().max()) < 1e-6
+
+
+def _pack_cpu(xn, rn, ids):  # torch stand-ins for regcn_pack_rows_f32 / regcn_unpack_rows_f32
+    d = xn.shape[1]
+    out = torch.zeros(ids.numel(), d + 4)
+    out[:, :d], out[:, d] = xn[ids], rn[ids]
+    return out
+
+
+def _unpack_cpu(buf, ids, xn, rn):
+    d = xn.shape[1]
+    xn[ids], rn[ids] = buf[:, :d], buf[:, d]
+
+
+def _exchange_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = _snapshot(V=400, T=3000, seed=world)
+        V, d = g.number_of_nodes(), 6
+        ref = torch.arange(V * d, dtype=torch.float32).view(V, d) + 0.5
+        ok = True
+        for chunks in (1, 3):
+            lay = P.OwnerLayout(V, world, chunks)
+            plan = P.ExchangePlan(g, lay, rank)
+            xn = torch.full((lay.Vp, d), float("nan"))
+            rn = torch.full((lay.Vp,), float("nan"))
+            for j, (lo, hi) in enumerate(lay.ranges(rank)):
+                xn[lo:hi], rn[lo:hi] = ref[lo:hi], -ref[lo:hi, 0]
+                P.exchange_rows(plan.chunks[j], xn, rn, pack=_pack_cpu, unpack=_unpack_cpu)
+            # every source of an in-edge of this rank's rows is valid, and nothing else arrived
+            rowptr = g._host["rowptr"].astype(np.int64)
+            src = g._host["col_src"].astype(np.int64)[:rowptr[-1]]
+            dst = np.repeat(np.arange(V), np.diff(rowptr))
+            mine = lay.owner(np.arange(V)) == rank
+            need = np.zeros(V, bool)
+            need[src[mine[dst]]] = True
+            need |= mine
+            got = ~torch.isnan(xn[:V, 0]).numpy()
+            ok &= bool((got == need).all())
+            ok &= bool(torch.equal(xn[:V][need], ref[need]) and torch.equal(rn[:V][need], -ref[need, 0]))
+            ok &= plan.rows_received() == int((need & ~mine).sum())
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sparse_exchange_gloo(world):
+    """ExchangePlan + exchange_rows (the owner partition's per-chunk all_to_all): after every
+    chunk's exchange a rank holds exactly its own rows and the sources of its rows' in-edges,
+    with the owners' values; senders and receivers agree on the order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    res = sorted(q.get() for _ in range(world))
+    assert all(ok for _, ok in res), res
