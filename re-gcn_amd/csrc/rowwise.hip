@@ -201,35 +201,46 @@ int rowmap(int op, const float* a, const float* b, const float* vec, int64_t row
 // The rows of x (d floats) and |h| (1 float) the next layer of another rank reads, packed as
 // one record of stride d + 4 floats (16-B aligned records: the x part moves as 16-B vectors;
 // float d holds |h|, d+1..d+3 are padding) for one all_to_all (parallel.ExchangePlan); the
-// unpack scatters the received records back.  One 64-lane wave per record, lane l moves the
-// 16-B group l (d <= 252), lane d/4 the radius: HBM-bound, 2 x 816 B of traffic per row.
+// unpack scatters the received records back.  HBM-bound, 2 x 816 B of traffic per row: a wave
+// moves XR_ROWS records, all loads issued before the stores (lane l: the 16-B group l of each,
+// d <= 252; lane d/4 the radius).
+constexpr int XR_ROWS = 4;
 __global__ __launch_bounds__(256) void k_pack_rows(const float* __restrict__ x, const float* __restrict__ r,
                                                    const int64_t* __restrict__ idx, int64_t n, int d,
                                                    float* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= n) return;
+  const int64_t i0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * XR_ROWS;
   const int lane = threadIdx.x & 63, q = d >> 2;
-  const int64_t src = idx[i];
-  float* o = out + i * (d + 4);
-  if (lane < q) {
-    const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x + src * d) + lane);
-    reinterpret_cast<f4*>(o)[lane] = v;
-  } else if (lane == q) {
-    reinterpret_cast<f4*>(o)[lane] = f4{r[src], 0.f, 0.f, 0.f};
+  f4 v[XR_ROWS];
+#pragma unroll
+  for (int u = 0; u < XR_ROWS; ++u) {
+    const int64_t i = min(i0 + u, n - 1);
+    const int64_t src = idx[i];
+    if (lane < q) v[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x + src * d) + lane);
+    else v[u] = f4{lane == q ? r[src] : 0.f, 0.f, 0.f, 0.f};
   }
+#pragma unroll
+  for (int u = 0; u < XR_ROWS; ++u)
+    if (i0 + u < n && lane <= q) reinterpret_cast<f4*>(out + (i0 + u) * (d + 4))[lane] = v[u];
 }
 
 __global__ __launch_bounds__(256) void k_unpack_rows(const float* __restrict__ in, const int64_t* __restrict__ idx,
                                                      int64_t n, int d, float* __restrict__ x, float* __restrict__ r) {
-  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= n) return;
+  const int64_t i0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * XR_ROWS;
   const int lane = threadIdx.x & 63, q = d >> 2;
-  const int64_t dst = idx[i];
-  const float* s = in + i * (d + 4);
-  if (lane < q) {
-    reinterpret_cast<f4*>(x + dst * d)[lane] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(s) + lane);
-  } else if (lane == q) {
-    r[dst] = s[d];
+  f4 v[XR_ROWS];
+  int64_t dst[XR_ROWS];
+#pragma unroll
+  for (int u = 0; u < XR_ROWS; ++u) {
+    const int64_t i = min(i0 + u, n - 1);
+    dst[u] = idx[i];
+    v[u] = lane <= q ? __builtin_nontemporal_load(reinterpret_cast<const f4*>(in + i * (d + 4)) + lane)
+                     : f4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int u = 0; u < XR_ROWS; ++u) {
+    if (i0 + u >= n) continue;
+    if (lane < q) reinterpret_cast<f4*>(x + dst[u] * d)[lane] = v[u];
+    else if (lane == q) r[dst[u]] = v[u].x;
   }
 }
 
@@ -239,7 +250,7 @@ int exchange_rows(int pack, float* x, float* r, const int64_t* idx, int64_t n, i
   if (d <= 0 || (d & 3) || d > 4 * (WAVE - 1)) return set_error(REGCN_EINVAL, "row exchange needs d %% 4 == 0, d <= 252");
   if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(buf)) & 15)
     return set_error(REGCN_EINVAL, "row exchange needs 16-B aligned x and buffer");
-  const int64_t blocks = (n + 3) / 4;
+  const int64_t blocks = (n + 4 * XR_ROWS - 1) / (4 * XR_ROWS);
   if (blocks > 0x7fffffffL) return set_error(REGCN_EINVAL, "row exchange grid too large");
   if (pack) hipLaunchKernelGGL(k_pack_rows, dim3((unsigned)blocks), dim3(256), 0, st, x, r, idx, n, d, buf);
   else hipLaunchKernelGGL(k_unpack_rows, dim3((unsigned)blocks), dim3(256), 0, st, buf, idx, n, d, x, r);

@@ -15,6 +15,7 @@ encoders and geoopt manifold parameters are out of scope and rai
 """
 import contextlib
 import ctypes
+import os
 import logging
 import math
 
@@ -106,6 +107,10 @@ def relation_context(x, g, num_rels2):
     out[R:].copy_(out[:R])
     return out
 
+
+# the owner partition's exchange: the rows the next layer reads (parallel.ExchangePlan); 0: every
+# row after every layer (in-place all-gathers)
+SPARSE_EXCHANGE = os.environ.get("REGCN_SPARSE_EXCHANGE", "1") != "0"
 
 REL_INLINE_MAX_SPAN = 64  # longer r_to_e spans are averaged by the chunked segment-mean kernel first
 
@@ -390,7 +395,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 # last timestep all rows, unless the caller reads only its own (predict_ranks)
                 nxt = g_list[i + 1] if i + 1 < len(g_list) else \
                     (None if self.__dict__.get("_owner_rows_only") else FULL_EXCHANGE)
-                g.consumers = (g, nxt) if fused_step else None
+                g.consumers = (g, nxt) if fused_step and SPARSE_EXCHANGE else None
             x_prev, _ = tangent_of(self.h, c_val)
             h_prev = self.emb_rel if i == 0 else self.h_0  # the two-phase GRU, as _forward_phases runs it
             self.h_0 = relation_gru_x(self.relation_gru, x_prev, g, h_prev,

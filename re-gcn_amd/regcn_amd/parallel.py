@@ -772,18 +772,20 @@ class RankSimulation(ShardedGraph):
 
         def rank_launches(sg, plan, marks):
             def after(j):  # chunk j's rows final: its exchange's pack / unpack on this stream
-                if plan:
-                    sidx, _, ridx, _ = plan.chunks[j]
-                    del sidx
-                    # the receive side's records (same count and traffic as the send side's),
-                    # written back: the rows already hold these values in the simulation
-                    unpack_rows(pack_rows(xn, rn, ridx), ridx, xn, rn)
-                    pack_rows(xn, rn, plan.chunks[j][0])
+                if plan:  # the rank's two kernels: its send records, and the received records
+                    sidx, _, ridx, _ = plan.chunks[j]  # scattered (into scratch rows here: the
+                    send = pack_rows(xn, rn, sidx)      # simulated rows hold their values already)
+                    recv = torch.empty(ridx.numel(), d + 4, device=x.device, dtype=torch.float32)
+                    del send
+                    unpack_rows(recv, ridx, scratch[0], scratch[1])
                 e = torch.cuda.Event(enable_timing=True)
                 e.record()
                 marks.append(e)
             sg._rank_launches(mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
                               drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, after)
+        scratch = self.__dict__.get("_scratch")
+        if scratch is None or scratch[0].shape != xn.shape:
+            scratch = self.__dict__["_scratch"] = (torch.empty_like(xn), torch.empty_like(rn))
         for k, sg in enumerate(self.ranks):
             sg.consumers = self.consumers
             plan = sg.exchange_plan(step)
