@@ -738,6 +738,16 @@ def complete(h):
     return meta[0].complete_rows(h) if meta is not None else h
 
 
+def exposed_after(chunk_end_ms, xchg_ms):
+    """The exchange time a layer exposes: exchange j starts at max(chunk j's end, exchange j-1's
+    end) and takes xchg_ms[j]; the next layer starts after the last one, so the layer exposes
+    end(last exchange) - end(last chunk)."""
+    end = 0.0
+    for tj, aj in zip(chunk_end_ms, xchg_ms):
+        end = max(end, tj) + aj
+    return max(0.0, end - chunk_end_ms[-1]) if chunk_end_ms else 0.0
+
+
 class RankSimulation(ShardedGraph):
     """All `world` ranks of the owner partition run one after another on ONE device, for
     measurement (bench.py owner_simulation): every layer runs rank 0's chunk launches, then
@@ -807,15 +817,12 @@ class RankSimulation(ShardedGraph):
         for marks_k in self.chunk_marks:
             tot = 0.0
             for marks, nbytes in marks_k:
-                if not marks:
-                    continue
-                t = [marks[0].elapsed_time(e) for e in marks]
-                end = 0.0
-                for tj, bj in zip(t, nbytes):
-                    end = max(end, tj) + bj / (link_gbs * 1e6)
-                tot += max(0.0, end - t[-1])
+                if marks:
+                    tot += exposed_after([marks[0].elapsed_time(e) for e in marks],
+                                         [b / (link_gbs * 1e6) for b in nbytes])
             out.append(tot)
         return out
+
 
     def relation_means(self, x, R2):
         means = [self._timed(k, lambda: ShardedGraph.relation_means(sg, x, R2)) for k, sg in enumerate(self.ranks)]

@@ -386,3 +386,14 @@ def test_sparse_exchange_gloo(world):
         assert p.exitcode == 0
     res = sorted(q.get() for _ in range(world))
     assert all(ok for _, ok in res), res
+
+
+def test_exposed_exchange_model():
+    """The rank simulation's link model (parallel.exposed_after): exchanges shorter than the
+    next chunk's compute hide except the last; longer ones queue on the link."""
+    assert P.exposed_after([0.0, 1.0, 2.0, 3.0], [0.5] * 4) == pytest.approx(0.5)
+    # 4 chunks of 0.09 ms compute, 0.164 ms exchanges: 0.657 - 3 * 0.09 exposed
+    t = [0.0, 0.09, 0.18, 0.27]
+    assert P.exposed_after(t, [0.164] * 4) == pytest.approx(4 * 0.164 - 0.27)
+    assert P.exposed_after([0.0], [0.2]) == pytest.approx(0.2)
+    assert P.exposed_after([0.0, 1.0], [0.0, 0.0]) == 0.0
