@@ -1041,7 +1041,10 @@ def run_scale(args, cfg, world, rank, device, backend):
         finally:
             _lib.EVENT_TRACE = None
 
+    for g in graphs if sharded else ():
+        g.exchanged_bytes = 0
     elapsed, edges_total = _timed(world, device, backend, run, edges_local)
+    xbytes = sum(getattr(g, "exchanged_bytes", 0) for g in graphs) / max(args.steps, 1) if sharded else 0
     if sharded:  # every rank processed its part of the same edges: count them once
         edges_total = float(edges_local)
     value = edges_total / elapsed / 1e6
@@ -1116,6 +1119,7 @@ def run_scale(args, cfg, world, rank, device, backend):
                           "parallelism": ("%s-partitioned snapshots x%d" % (args.shard, world)) if sharded
                           else "replicas x%d" % world,
                           "snapshot_stats": {k: round(v) for k, v in stats.items()}},
+               "exchange_gb_per_step_rank0": round(xbytes / 1e9, 3) if sharded else None,
                "roofline": roof, "kernels": kernels,
                "breakdown": {"encoder_ms_per_step": round(enc_ms, 3),
                              "encoder_M_edges_per_s": round(np.mean(epw) / enc_ms / 1e3, 1),

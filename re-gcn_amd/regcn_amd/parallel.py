@@ -10,9 +10,10 @@ Two partitionings of a message-passing layer over `world` ranks:
 * ``"owner"`` — rank k owns a set of destination nodes (OwnerLayout: `chunks` groups of
   contiguous ids per rank, chunk-major so that chunk j of every rank is one contiguous id
   range) and runs the fused layer kernel on them only (gather + GEMMs + epilogue,
-  rank-local).  The next layer reads only the tangent rows x = log0 h and the radii |h|, so
-  after each chunk's launch ONE in-place ``all_gather`` per array (804 B per row) rebuilds x
-  and |h| on every rank, on a side stream while the next chunk computes; the Poincare rows h
+  rank-local).  The next layer reads only the tangent rows x = log0 h and the radii |h| of
+  its rows' in-edge sources, so after each chunk's launch ONE ``all_to_all`` sends every rank
+  exactly those rows (ExchangePlan; records of 816 B), on a side stream while the next chunk
+  computes (without a known consumer: in-place ``all_gather`` of every row); the Poincare rows h
   stay rank-local (the decoder fetches the rows it needs, `fetch_rows`, and scores each
   rank's own rows as its candidates, CandidateShard).  The relation-context means are
   partitioned the same way (per-rank partial sums over owned entities, one all_reduce of
@@ -83,9 +84,8 @@ def owner_bounds(V, world):
 def owner_chunks(V, world):
     """Pipeline chunks per rank of the owner partition (auto): 4 from 64k rows per rank.  The
     8-rank config-5 simulation (bench owner_simulation, round 4; the hub pass and the gather
-    over all of a rank's rows, only the tails per chunk): per-rank compute 5.9 / 6.1 / 6.4 ms
-    at 1 / 2 / 4 chunks against 3.9 ms of all-gather per step, of which all but the last
-    chunk's of each layer (1/4) hides under the next chunk's tail."""
+    over all of a rank's rows, only the tails per chunk; the sparse exchange): 9.26 / 9.45 ms
+    per step predicted at 4 / 2 chunks (profiles/r4_owner_sim_sparse.txt)."""
     return 4 if world > 1 and -(-V // world) >= 65536 else 1
 
 
