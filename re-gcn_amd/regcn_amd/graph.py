@@ -481,6 +481,13 @@ REL_BLOCK_CHUNK = 256          # pairs per chunk inside one (relation, block) se
 _XCDS, _WAVES_PER_WG = 8, 4
 
 
+# How blocked_span_chunks deals the block-ordered chunks to the XCD queues: "even" = xcds equal
+# contiguous runs (a queue holds consecutive blocks; a block may straddle two queues), "mod" =
+# block k to XCD k % xcds (a Zipf-hot source block makes its XCD's queue the longest)
+XCD_DEAL = os.environ.get("REGCN_XCD_DEAL", "cost")
+XCD_RUN_COST = int(os.environ.get("REGCN_XCD_RUN_COST", "7"))  # ~ L2 lines of a gathered row / an index
+
+
 def blocked_span_chunks(span_rows, span_beg, span_len, keys, block, chunk, xcds=_XCDS, waves=_WAVES_PER_WG):
     """Chunks {row, beg, end, slot} and fix-ups over spans [span_beg[i], span_beg[i] +
     span_len[i]) of a position array whose `keys` (entity ids, ascending inside each span) pick
@@ -518,7 +525,23 @@ def blocked_span_chunks(span_rows, span_beg, span_len, keys, block, chunk, xcds=
     fixups, nslot = group_fixups(fix, nslot)
     chunks = torch.stack([span_rows.long()[c_span], pos[cs], pos[ce - 1] + 1, slot], 1)
     order = torch.sort(c_blk, stable=True).indices
-    xq = c_blk[order] % xcds
+    if XCD_DEAL == "even":  # the block-ordered chunks cut into xcds equal contiguous runs
+        xq = torch.arange(order.numel(), device=dev) * xcds // max(order.numel(), 1)
+    elif XCD_DEAL == "cost":  # ... with equal work per run: positions + XCD_RUN_COST per key run
+        kv = keys[pos].long()
+        head = new_seg.clone()
+        head[1:] |= kv[1:] != kv[:-1]
+        hc = torch.cat([torch.zeros(1, dtype=torch.long, device=dev), torch.cumsum(head.long(), 0)])
+        first = torch.zeros(total, dtype=torch.bool, device=dev)
+        first[cs] = True  # a chunk's first position starts a run in that chunk
+        hc2 = torch.cat([torch.zeros(1, dtype=torch.long, device=dev), torch.cumsum((head | first).long(), 0)])
+        runs = hc2[ce] - hc2[cs]
+        del hc
+        w = ((ce - cs) + XCD_RUN_COST * runs)[order]
+        mid = torch.cumsum(w, 0) - w // 2
+        xq = torch.clamp(mid * xcds // max(int(w.sum()), 1), max=xcds - 1)
+    else:  # whole blocks round-robin
+        xq = c_blk[order] % xcds
     queues = [order[xq == x] for x in range(xcds)]
     L = max(int(q.numel()) for q in queues)
     L = (L + waves - 1) // waves * waves

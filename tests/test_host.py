@@ -256,7 +256,16 @@ def test_relation_entity_block_lists(block, chunk):
     assert (covered == 1).all()
     p = np.arange(len(ch))
     real = ch[:, 2] > ch[:, 1]
-    assert (((p // 4) % 8)[real] == (idx[ch[real, 1]] // block) % 8).all()
+    xcd, q = (p // 4) % 8, (p // 32) * 4 + p % 4  # the XCD a position's workgroup lands on, queue index
+    blk = idx[ch[:, 1]] // block
+    # the default deal (graph.XCD_DEAL = "cost"): each XCD's queue is a contiguous run of the
+    # block-ordered chunks, the runs in XCD order
+    last = -1
+    for x in range(8):
+        sel = real & (xcd == x)
+        b = blk[sel][np.argsort(q[sel], kind="stable")]
+        assert (np.diff(b) >= 0).all() and (len(b) == 0 or b[0] >= last)
+        last = b[-1] if len(b) else last
     assert not ((fx[:, 1] <= ns - 1) & (fx[:, 2] > ns - 1)).any()
     x = rng.standard_normal((V, 5))
     part, out = np.zeros((ns, 5)), np.zeros((R, 5))
@@ -340,8 +349,39 @@ def test_spread_block_fills_every_xcd_queue():
         p = np.arange(len(ch))
         real = ch[:, 2] > ch[:, 1]
         fill.append((np.bincount(((p // 4) % 8)[real], minlength=8) > 0).sum())
-    assert fill == [1, 8], fill
+    assert fill[1] == 8, fill
     assert G.spread_block(V, 64) == 64 and G.spread_block(10 ** 6, 4096) == 4096
+
+
+@pytest.mark.parametrize("deal", ["mod", "cost"])
+def test_xcd_deal_balances_work(deal, monkeypatch):
+    """graph.blocked_span_chunks' XCD queues over Zipf-skewed spans (one hot key block): "mod"
+    puts block k on XCD k % 8 (every chunk of a block on one XCD); "cost" cuts the block-ordered
+    chunks into 8 runs of equal positions + XCD_RUN_COST x key runs (config 5's hub pass:
+    804 -> 750 us per launch), each XCD within one chunk's cost of the mean."""
+    import torch
+    monkeypatch.setattr(G, "XCD_DEAL", deal)
+    rng = np.random.default_rng(7)
+    V, n_spans = 50_000, 40
+    p = 1.0 / np.arange(1, V + 1) ** 1.1
+    p /= p.sum()
+    spans = [np.sort(rng.choice(V, size=int(rng.integers(2000, 9000)), p=p)) for _ in range(n_spans)]
+    lens = np.array([len(x) for x in spans])
+    keys = torch.from_numpy(np.concatenate(spans))
+    beg = torch.from_numpy(np.cumsum(lens) - lens)
+    ch, _, _ = G.blocked_span_chunks(torch.arange(n_spans), beg, torch.from_numpy(lens), keys, 4096, 256)
+    ch = ch.numpy().astype(np.int64)
+    k = keys.numpy()
+    pos = np.arange(len(ch))
+    real = ch[:, 2] > ch[:, 1]
+    xcd = (pos // 4) % 8
+    if deal == "mod":
+        assert (xcd[real] == (k[ch[real, 1]] // 4096) % 8).all()
+        return
+    runs = np.array([len(np.unique(k[b:e])) if e > b else 0 for _, b, e, _ in ch])
+    cost = (ch[:, 2] - ch[:, 1]) + G.XCD_RUN_COST * runs
+    per = np.bincount(xcd, weights=cost, minlength=8)
+    assert per.max() - per.mean() <= cost.max(), (per, cost.max())
 
 
 def test_rowtail_chunks_partition_tiles_and_rows():
