@@ -343,14 +343,43 @@ __device__ __forceinline__ RtRows rt_rows(const LayerArgs& p, int base) {
   return R;
 }
 
+// The step layer's blend operands (x_prev and the gate rows) in column stages of RT_SC_COLS:
+// each wave DMAs its 16 rows' columns [RT_SC_COLS s, ...) of both arrays into its own LDS
+// region (row stride = the stage's width; 16-B pieces, global_load_lds, 5 instructions per
+// array), then reads them in C layout -- instead of 2 x NT x 4 scattered 4-B loads per lane.
+// The region is the products' LDS (free after rt_mm's final barrier): 4 waves x 2 arrays x 5 KB.
+constexpr int RT_SC_COLS = 80, RT_SC_TILES = RT_SC_COLS / 16, RT_SC_BYTES = 16 * RT_SC_COLS * 4;
+static_assert(4 * 2 * RT_SC_BYTES <= rt_lds_bytes(1), "blend staging must fit the tail's LDS");
+
+__device__ __forceinline__ void rt_stage_blend(const StepArgs& s, const RtRows& R, int d, int stage, char* lds) {
+  const int lane = threadIdx.x & 63, w = wave_id();
+  const int c0 = RT_SC_COLS * stage, ncols = min(RT_SC_COLS, d - c0), f4pr = ncols >> 2;
+  const float* zrow = reinterpret_cast<const float*>(kZeroRow);
+  char* base = lds + w * 2 * RT_SC_BYTES;
+#pragma unroll
+  for (int i = 0; i < RT_SC_BYTES / 1024; ++i) {
+    const int slot = 64 * i + lane, sr = slot / max(f4pr, 1), sc = slot - sr * f4pr;
+    const int rid = __shfl(R.arow_id, min(sr, 15));
+    const bool ok = (slot < 16 * f4pr) & (sr < R.n_valid);
+    const int64_t off = (int64_t)rid * d + c0 + 4 * sc;
+    __builtin_amdgcn_global_load_lds((const void*)(ok ? s.x_prev + off : zrow),
+                                     (__attribute__((address_space(3))) void*)(base + i * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(ok ? s.tw + off : zrow),
+                                     (__attribute__((address_space(3))) void*)(base + RT_SC_BYTES + i * 1024), 16, 0, 0);
+  }
+}
+
 // Everything after the products for one 16-row group: clamps, rrelu, exp0, then the next
 // layer's x / |h| or the timestep.  `g` (RT_STEP) holds the in-kernel gate product.
 template <int NT, int MODE>
-__device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const RtRows& R, const RAcc<NT>* g) {
+__device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const RtRows& R, const RAcc<NT>* g,
+                                          char* lds) {
   constexpr bool STEP = MODE >= RT_STEP;
   const int lane = threadIdx.x & 63, q = lane >> 4, d = p.d;
   const int* crow = R.crow;
   const int n_valid = R.n_valid;
+  // the first blend stage's copies fly under the epilogue's row maps
+  if constexpr (MODE == RT_STEP_PRE) rt_stage_blend(p.step, R, d, 0, lds);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (!p.euclid) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
@@ -379,24 +408,45 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     rt_log0<NT>(v, n2, k);
     float bg[NT];
     rt_col<NT>(bg, s.b_g, d);
+    if constexpr (MODE == RT_STEP_PRE) {
+      const float* xs = reinterpret_cast<const float*>(lds + wave_id() * 2 * RT_SC_BYTES);
+      const float* zs = xs + RT_SC_BYTES / 4;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = 16 * t + (lane & 15), colc = min(col, d - 1);
-      const f4 c4 = clamp4(v.t[t], -10.f, 10.f);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool ok = (4 * q + r < n_valid) & (col < d);
-        const float xp = s.x_prev[(int64_t)crow[r] * d + colc];
-        const float pr = fminf(fmaxf(ok ? xp : 0.f, -10.f), 10.f);
-        float z;
-        if constexpr (MODE == RT_STEP_PRE) {
-          const float zt = s.tw[(int64_t)crow[r] * d + colc];
-          z = ok ? zt : 0.f;
-        } else {
-          z = g->t[t][r];
+      for (int t = 0; t < NT; ++t) {
+        const int stage = t / RT_SC_TILES;
+        if (t % RT_SC_TILES == 0) {
+          if (stage > 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the last stage
+            rt_stage_blend(s, R, d, stage, lds);
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stage's copies have landed
         }
-        const float gg = sigmoidf(z + bg[t]);
-        v.t[t][r] = gg * c4[r] + (1.f - gg) * pr;
+        const int col = 16 * t + (lane & 15);
+        const int ncols = min(RT_SC_COLS, d - RT_SC_COLS * stage), cl = min(col - RT_SC_COLS * stage, ncols - 1);
+        const f4 c4 = clamp4(v.t[t], -10.f, 10.f);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = (4 * q + r < n_valid) & (col < d);
+          const float xp = xs[(4 * q + r) * ncols + cl];
+          const float zt = zs[(4 * q + r) * ncols + cl];
+          const float pr = fminf(fmaxf(ok ? xp : 0.f, -10.f), 10.f);
+          const float gg = sigmoidf((ok ? zt : 0.f) + bg[t]);
+          v.t[t][r] = gg * c4[r] + (1.f - gg) * pr;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int col = 16 * t + (lane & 15), colc = min(col, d - 1);
+        const f4 c4 = clamp4(v.t[t], -10.f, 10.f);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = (4 * q + r < n_valid) & (col < d);
+          const float xp = s.x_prev[(int64_t)crow[r] * d + colc];
+          const float pr = fminf(fmaxf(ok ? xp : 0.f, -10.f), 10.f);
+          const float gg = sigmoidf(g->t[t][r] + bg[t]);
+          v.t[t][r] = gg * c4[r] + (1.f - gg) * pr;
+        }
       }
     }
     rt_sumsq<NT>(v, n2);
@@ -511,10 +561,10 @@ __device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
     const float* xp[1] = {p.step.x_prev + (int64_t)R[0].arow_id * d};
     const bool okp[1] = {R[0].a_valid};
     rt_mm<NT, 1, true>(gt, xp, okp, p.step.w_g, d, KB, rt_lds);
-    rt_finish<NT, MODE>(p, v[0], R[0], &gt[0]);
+    rt_finish<NT, MODE>(p, v[0], R[0], &gt[0], rt_lds);
   } else {
 #pragma unroll
-    for (int g = 0; g < RG; ++g) rt_finish<NT, MODE>(p, v[g], R[g], nullptr);
+    for (int g = 0; g < RG; ++g) rt_finish<NT, MODE>(p, v[g], R[g], nullptr, rt_lds);
   }
 }
 
