@@ -369,6 +369,38 @@ __device__ __forceinline__ void rt_stage_blend(const StepArgs& s, const RtRows& 
   }
 }
 
+// C-layout rows stored through the wave's LDS region in the same 80-column stages: written
+// there per element, read back as 16-B row pieces, stored as whole 16-B vectors (5 per lane per
+// stage) instead of NT x 4 scattered 4-B stores.  In-order LDS within the wave: no barrier.
+template <int NT>
+__device__ __forceinline__ void rt_store_staged(const RAcc<NT>& a, float* __restrict__ M, const RtRows& R, int d,
+                                                char* lds) {
+  const int lane = threadIdx.x & 63, q = lane >> 4;
+  float* st = reinterpret_cast<float*>(lds + wave_id() * 2 * RT_SC_BYTES);
+  constexpr int NS = (NT + RT_SC_TILES - 1) / RT_SC_TILES;
+#pragma unroll
+  for (int stage = 0; stage < NS; ++stage) {
+    const int c0 = RT_SC_COLS * stage;
+    if (c0 >= d) break;
+    const int ncols = min(RT_SC_COLS, d - c0), f4pr = ncols >> 2;
+#pragma unroll
+    for (int t = stage * RT_SC_TILES; t < min(NT, (stage + 1) * RT_SC_TILES); ++t) {
+      const int cl = 16 * t + (lane & 15) - c0;
+      if (cl < ncols) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[(4 * q + r) * ncols + cl] = a.t[t][r];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RT_SC_BYTES / 1024; ++i) {
+      const int slot = 64 * i + lane, sr = slot / f4pr, sc = slot - sr * f4pr;
+      const int rid = __shfl(R.arow_id, min(sr, 15));
+      if (slot < 16 * f4pr && sr < R.n_valid)
+        *reinterpret_cast<f4*>(M + (int64_t)rid * d + c0 + 4 * sc) = *reinterpret_cast<const f4*>(st + 4 * slot);
+    }
+  }
+}
+
 // Everything after the products for one 16-row group: clamps, rrelu, exp0, then the next
 // layer's x / |h| or the timestep.  `g` (RT_STEP) holds the in-kernel gate product.
 template <int NT, int MODE>
@@ -390,6 +422,8 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
   if (!p.euclid) rt_exp0<NT>(v, n2, p.k);
 
   if constexpr (!STEP) {
+    // (element stores: staging them as in the step layer made the two-group first layer's
+    // tail 2.5 % slower at config 5)
     rt_store<NT>(v, p.h_out, crow, n_valid, d);
     if (p.r_next) rt_store_radius(n2, p.r_next, crow, n_valid);
     if (p.x_next) {
@@ -475,11 +509,11 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     float f[4];
     spread_rows(fminf(fmaxf(newr, REGCN_EPS), kr.rmax) / fmaxf(sqrtf(n2o), REGCN_EPS), f);
     rt_scale_known<NT>(v, n2, f);
-    rt_store<NT>(v, s.h_out, crow, n_valid, d);
+    rt_store_staged<NT>(v, s.h_out, R, d, lds);
     if (s.r_out) rt_store_radius(n2, s.r_out, crow, n_valid);
     if (s.x_out) {
       rt_log0<NT>(v, n2, k);
-      rt_store<NT>(v, s.x_out, crow, n_valid, d);
+      rt_store_staged<NT>(v, s.x_out, R, d, lds);
     }
   }
 }
