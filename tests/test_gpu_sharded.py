@@ -1,7 +1,8 @@
 """A whole sharded predict (-m gpu): two ranks launched like the driver launches bench.py
 (torch.distributed.run), sharing the box's one GPU through a gloo group (on a node each rank
 owns a GPU and the group is RCCL).  Both partitions of SURVEY.md §8(e) -- owner (with and
-without the pipelined all-gather) and edge -- against the same model unsharded: history
+without the pipelined exchange: per chunk one all_to_all of the rows the next layer reads,
+parallel.ExchangePlan) and edge -- against the same model unsharded: history
 embeddings within 1e-4 * max(1, |ref|), relation states within 1e-5; the candidate-sharded
 decoder on the unsharded embeddings gives the unsharded ranks bit for bit, and end to end the
 entity ranks differ (near ties) for at most 1% of the queries, by at most 2."""
@@ -22,7 +23,7 @@ pytestmark = pytest.mark.gpu
 def test_sharded_predict_world2(tmp_path, tag, rowtail):
     """rowtail: the large-snapshot layer path (REGCN_ROWTAIL_MIN_ROWS lowered in the ranks),
     where a rank's hub pass and gather run once and each chunk's tail is followed by its
-    all-gather (hyperbolic_layers.run_layer_chunked)."""
+    exchange (hyperbolic_layers.run_layer_chunked)."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
