@@ -1177,18 +1177,39 @@ def main():
                 out["aggregation_roofline"] = aggregation_at_scale(device)
                 out["decoder_roofline"] = decoder_at_scale()
         if world == 1 and not args.no_extras:
-            for key, name in (("icews14s", "icews14s_lgcn_roth"), ("icews18", "icews18_roth")):
+            # the dataset configs (BASELINE.json configs[1..3]) as legs of the N = 1 line; GDELT
+            # (configs[3], history 7) for both encoders, each with its CPU baseline
+            for key, name, enc in (("icews14s", "icews14s_lgcn_roth", None), ("icews18", "icews18_roth", None),
+                                   ("gdelt", "gdelt", None), ("gdelt_lgcn", "gdelt", "lgcn")):
                 sub = parse(["--config", name, "--steps", "64", "--warmup", "4", "--cpu-budget", "10"]
-                            + (["--no-cpu-baseline"] if name != "icews14s_lgcn_roth" else []))
-                r = run_small(sub, CONFIGS[name], world, rank, device, backend)
+                            + (["--no-cpu-baseline"] if name == "icews18_roth" else []))
+                c = dict(CONFIGS[name])
+                if enc:
+                    c.update(encoder=enc, label=c["label"] + ", encoder=" + enc)
+                r = run_small(sub, c, world, rank, device, backend)
                 if rank == 0:
                     out[key] = {k: r[k] for k in ("value", "unit", "ms_per_step", "latency_ms_per_predict",
-                                                  "steps", "config", "roofline", "kernels")}
-                    if r.get("mrr_parity"):
-                        out["mrr_parity"] = dict(r["mrr_parity"], workload=CONFIGS[name]["label"])
+                                                  "steps", "config", "roofline", "kernels", "breakdown")}
+                    if r.get("cpu_baseline"):
                         out[key]["cpu_baseline"] = r["cpu_baseline"]
+                    if r.get("mrr_parity"):
+                        mp = dict(r["mrr_parity"], workload=c["label"])
+                        if key == "icews14s":
+                            out["mrr_parity"] = mp
+                        else:
+                            out[key]["mrr_parity"] = mp
     else:
         out = run_small(args, cfg, world, rank, device, backend)
+        if world > 1 and args.shard == "replica" and not args.no_extras:
+            # the north star's literal scheme beside the replicas: every snapshot's edges split
+            # across the ranks, one all_reduce of the destination partials per layer (SURVEY.md
+            # §8(e) partitioning 1; latency-bound at dataset sizes, reported as measured)
+            sub = parse(["--config", args.config, "--shard", "edge", "--steps", str(max(8, args.steps // 4)),
+                         "--warmup", "2", "--no-cpu-baseline", "--pool", "4"])
+            r = run_small(sub, cfg, world, rank, device, backend, extras=False)
+            if rank == 0:
+                out["edge_partition"] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps", "scaling")}
+                out["edge_partition"]["parallelism"] = r["config"]["parallelism"]
         if rank == 0 and world == 1 and not args.no_scale:
             out["aggregation_roofline"] = aggregation_at_scale(device)
             out["decoder_roofline"] = decoder_at_scale()

@@ -608,7 +608,9 @@ def hub_chunk(total_edges, chunk_edges):
     """Edges per hub-pass chunk (one wave each): the snapshot's chunk size, shrunk (not below
     256) so the pass has at least HUB_CHUNKS_MIN chunks.  An owner-partitioned rank holds ~1/8
     of the hub edges: config 5's 8-rank simulation at 1024 / 256 edges per chunk runs 5.42 /
-    5.21 ms of encoder per rank (profiles/r4_hub_chunk_sweep.txt); the whole snapshot keeps 1024."""
+    5.21 ms of encoder per rank (profiles/r4_hub_chunk_sweep.txt).  The whole config-5 snapshot
+    keeps 1024: its hub rows hold ~32.7M of the 50M directed edges, ceil(32.7M / 16384) = 1,996
+    > 1024 (a rank's ~4.1M give 250 -> the 256 floor)."""
     if HUB_CHUNK:
         return max(HUB_CHUNK, 64)
     base = max(int(chunk_edges or 1024), 64)

@@ -32,7 +32,7 @@ from .graph import SnapshotGraph, rel_block_work
 from .hyperbolic_layers import HyperbolicUnionRGCNLayer, LorentzRGCNCell, LorentzRGCNLayer, StepSpec, \
     _heavy_aggregate
 from .hyperbolic_ops import HyperbolicOps, TemporalRadiusEvolution
-from .parallel import FULL_EXCHANGE, ShardedGraph
+from .parallel import FULL_EXCHANGE, ShardedGraph, complete
 from .tangent import attach, tangent_of
 from .weights import invalidate, packed
 
@@ -408,7 +408,10 @@ class HyperbolicRecurrentRGCN(nn.Module):
                                 w_g_param=self.time_gate_weight)
                 self.h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0], step=step)
             else:
-                current_h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0])
+                # the timestep kernel reads every row of current_h (and recomputes x, |h| from
+                # it): under the owner partition only this rank's rows are written, so gather
+                # the rest first (the all-gather of h the fused step's sparse exchange avoids)
+                current_h = complete(self.rgcn.forward(g, self.h, [self.h_0, self.h_0]))
                 h_new = torch.empty_like(x_prev)
                 x_new = torch.empty_like(x_prev)
                 r_new = torch.empty(V, device=dev, dtype=torch.float32)
@@ -431,6 +434,17 @@ class HyperbolicRecurrentRGCN(nn.Module):
                     _lib.call("regcn_timestep_f32", *args, _lib.stream())
                 self.h = attach(h_new, x_new, r_new, c_val)
             history_embs.append(self.h)
+        if history_embs and not self.__dict__.get("_owner_rows_only"):
+            # owner partition: the last state holds this rank's rows only until its h rows are
+            # all-gathered (its x and |h| already were: the last exchange is FULL_EXCHANGE), so
+            # every caller of forward (predict, get_loss, ...) sees complete rows; the earlier
+            # history entries stay rank-local (parallel.complete fills one in when needed)
+            last = history_embs[-1]
+            xr = getattr(last, "_regcn_xr", None)
+            if getattr(last, "_regcn_owner", None) is not None:
+                complete(last)
+                if xr is not None:  # the in-place gather bumped h's version: same x and |h|
+                    attach(last, xr[0], xr[1], xr[2])
         if ana:  # hyperbolic_model.py:887-888
             dict.__setitem__(self.training_stats, "time_gate_values",
                              torch.stack(gate_means) if gate_means else [])

@@ -242,6 +242,12 @@ def exchange_rows(chunk, xn, rn, group=None, pack=pack_rows, unpack=unpack_rows)
     unpack(recv, ridx, xn, rn)
 
 
+def record_bytes(plan, d):
+    """Bytes per exchanged row: the sparse all_to_all moves pack_rows' (d + 4)-float records,
+    the in-place all-gathers (plan None) x and |h| alone, (d + 1) floats."""
+    return (d + 1) * 4 if plan is None else (d + 4) * 4
+
+
 FULL_EXCHANGE = "all rows"  # ShardedGraph.consumers: the next consumer is unknown -> all-gather
 
 
@@ -289,7 +295,10 @@ class EntityRelabel:
     -- carry ~1/world of the edges under power-law skew (a Zipf(1.1) hub holds ~9 % of a
     snapshot's edges; equal contiguous id blocks leave the hubs wherever the ids put them)."""
 
-    ENTITY_TENSORS = ("dynamic_emb", "radius_static", "radius_target", "decoder_ob.entity_bias")
+    # every entity-indexed parameter / buffer of the hyperbolic and Euclidean models: the
+    # embedding table, the radii, the scorers' per-entity bias (RotH / MuRP / AttH `entity_bias`,
+    # hyperbolic_decoder.py:166; ConvTransE's `b`, hyperbolic_decoder.py:568, rrgcn.py:71)
+    ENTITY_TENSORS = ("dynamic_emb", "radius_static", "radius_target", "decoder_ob.entity_bias", "decoder_ob.b")
 
     def __init__(self, perm):
         self.perm = np.asarray(perm, dtype=np.int64)
@@ -358,10 +367,13 @@ class EntityRelabel:
         perm[i] = old row i); in-place writes bump the version counters the caches key on."""
         names = dict(m.named_parameters())
         names.update(dict(m.named_buffers()))
+        V = len(self.perm)
         with torch.no_grad():
             for n in self.ENTITY_TENSORS:
                 t = names.get(n)
                 if t is not None:
+                    if t.shape[0] != V:
+                        raise ValueError("%s has %d rows, the relabel %d entities" % (n, t.shape[0], V))
                     t.copy_(t[self._t("inv", t.device)])
         from .weights import invalidate
         invalidate(m)
@@ -511,7 +523,7 @@ class ShardedGraph:
         if plan is False:
             return 0
         rows = self.layout.cr if plan is None else plan.link_rows(j)
-        return rows * (d + 1) * 4
+        return rows * record_bytes(plan, d)
 
     def __getattr__(self, name):  # delegate the DGL-visible surface and work lists
         return getattr(self.__dict__["g"], name)
@@ -638,7 +650,7 @@ class ShardedGraph:
         def exchange(j):  # once this rank's chunk-j rows are written
             if plan is False:
                 return
-            self.exchanged_bytes += ((W - 1) * cr if plan is None else sum(plan.chunks[j][3])) * (d + 1) * 4
+            self.exchanged_bytes += ((W - 1) * cr if plan is None else sum(plan.chunks[j][3])) * record_bytes(plan, d)
             if not self.collective:
                 return
             fn = gather_all if plan is None else gather_needed
@@ -803,7 +815,7 @@ class RankSimulation(ShardedGraph):
             self._timed(k, lambda: rank_launches(sg, plan, marks))
             rows = 0 if plan is False else ((self.world - 1) * lay.cr * lay.chunks if plan is None
                                             else plan.rows_received())
-            sg.exchanged_bytes += rows * (d + 1) * 4
+            sg.exchanged_bytes += rows * record_bytes(plan, d)
             self.chunk_marks[k].append((marks, [sg.link_bytes(plan, j, d) for j in range(len(marks))]))
         return h[:V], xn[:V], rn[:V]
 

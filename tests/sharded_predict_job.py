@@ -37,8 +37,8 @@ def main(out_path, tag):
         for part in ("owner", "edge"):
             for chunks in ((1, 3) if part == "owner" else (1,)):
                 sg = [ShardedGraph(g, part, chunks=chunks) for g in glist]
+                # forward itself completes the last state (the owner partition's other rows)
                 e2, _, h02, _, _ = m.forward(sg, None, True)
-                complete(e2[-1])  # owner partition: the other ranks' rows of the last state
                 _, (re2, fe2), (rr2, fr2) = m.predict_ranks(sg, R, None, test, True, ans, ans_r)
                 # the candidate-sharded decoder alone, on the unsharded encoder outputs: the
                 # same ranks bit for bit (the partitions sum rows in another order, so the
@@ -56,6 +56,23 @@ def main(out_path, tag):
                     "ent_rank_queries_differing": int((d_e > 0).sum()), "queries": int(d_e.numel()),
                     "ent_rank_max_diff": int(d_e.max()),
                 }
+        # --run-analysis under the owner partition: the non-fused timestep reads every row of
+        # the cell output, which the sharded forward completes first
+        m.run_analysis = True
+        try:
+            ea, _, _, ga, _ = m.forward(glist, None, True)
+            ref_a = ea[-1].clone()
+            ref_g = [g.clone() for g in ga]
+            sg = [ShardedGraph(g, "owner", chunks=2) for g in glist]
+            eb, _, _, gb, _ = m.forward(sg, None, True)
+            hist = [complete(e) for e in eb]
+            res["owner_analysis"] = {
+                "emb_err": float(((eb[-1] - ref_a).abs() / ref_a.abs().clamp_min(1.0)).max()),
+                "hist_err": float(max(((a - b).abs() / b.abs().clamp_min(1.0)).max() for a, b in zip(hist, ea))),
+                "gate_err": float(max((a - b).abs().max() for a, b in zip(gb, ref_g))) if ref_g else 0.0,
+            }
+        finally:
+            m.run_analysis = False
     if rank == 0:
         with open(out_path, "w") as f:
             json.dump(res, f)

@@ -49,6 +49,8 @@ def test_sharded_predict_world2(tmp_path, tag, rowtail):
         assert v["h0_err"] <= 1e-5, (key, v)
         assert v["dec_ent_rank_equal"] and v["dec_rel_rank_equal"], (key, v)
         assert v["ent_rank_queries_differing"] <= 0.01 * v["queries"] and v["ent_rank_max_diff"] <= 2, (key, v)
+    a = res["owner_analysis"]  # --run-analysis (the non-fused timestep) under the owner partition
+    assert a["emb_err"] <= 1e-4 and a["hist_err"] <= 1e-4 and a["gate_err"] <= 1e-4, a
     print(res)
 
 
@@ -121,3 +123,27 @@ def test_rank_simulation_matches_unsharded(golden, tag, world, chunks, rowtail, 
         gl = [G.build_sub_graph(V, R, rl.triples(s).astype(np.int64), True, dev) for s in snaps]
         e3 = m.forward([RankSimulation(g, world, chunks) for g in gl], None, True)[0]
         assert_close(e3[-1][torch.from_numpy(rl.perm).to(dev)], ref, what="relabelled simulated ranks")
+
+
+def test_rccl_device_branches_world1(tmp_path):
+    """The RCCL branches of the owner exchange (parallel._all_to_all_into's all_to_all_single
+    and _all_gather_into's all_gather_into_tensor on device tensors, launched on the comm
+    stream as ShardedGraph.run_layer launches them) in a one-rank "nccl" group: exact against
+    the known one-rank result and equal bit for bit to the gloo branch of the same calls
+    (tests/nccl_world1_job.py).  Two ranks cannot share the box's one GPU under RCCL."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "res.json")
+    env = dict(os.environ, PYTHONPATH=os.path.join(repo, "re-gcn_amd") + os.pathsep + repo)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(repo, "tests", "nccl_world1_job.py"),
+           out]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.load(open(out))
+    assert res["backend"] == "nccl" and res["world"] == 1, res
+    assert res["nccl_exchange_exact"] and res["nccl_allgather_exact"] and res["nccl_equals_gloo"], res

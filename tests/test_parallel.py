@@ -397,3 +397,36 @@ def test_exposed_exchange_model():
     assert P.exposed_after(t, [0.164] * 4) == pytest.approx(4 * 0.164 - 0.27)
     assert P.exposed_after([0.0], [0.2]) == pytest.approx(0.2)
     assert P.exposed_after([0.0, 1.0], [0.0, 0.0]) == 0.0
+
+
+@pytest.mark.parametrize("decoder", ["hyperbolic_convtranse", "roth"])
+def test_entity_relabel_permutes_every_entity_tensor(decoder):
+    """EntityRelabel.model permutes every parameter / buffer indexed by entity id of a real
+    model -- incl. HyperbolicConvTransE's per-entity bias `decoder_ob.b` (hyperbolic_decoder.py
+    :568) and RotH's Euclidean `decoder_ob.entity_bias` -- so a relabelled model scores entity
+    perm[i] exactly as the original scores entity i; every other tensor is unchanged."""
+    from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
+    V, R = 40, 3
+    torch.manual_seed(0)
+    m = HyperbolicRecurrentRGCN(decoder, "hyperbolic_uvrgcn", V, R, 0, 0, 8, "sub", 3, num_bases=4,
+                                num_hidden_layers=2, self_loop=True, entity_prediction=True, relation_prediction=True,
+                                use_entity_euclidean_bias=decoder == "roth")
+    with torch.no_grad():
+        for t in list(m.parameters()) + list(m.buffers()):
+            if t.is_floating_point():
+                t.copy_(torch.randn_like(t))
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    perm = np.random.default_rng(2).permutation(V)
+    P.EntityRelabel(perm).model(m)
+    after = m.state_dict()
+    p = torch.from_numpy(perm)
+    moved = set()
+    for k, v in before.items():
+        if k in P.EntityRelabel.ENTITY_TENSORS:
+            assert torch.equal(after[k][p], v), k
+            moved.add(k)
+        else:
+            assert torch.equal(after[k], v), k
+    per_entity = {k for k, v in before.items() if v.dim() >= 1 and v.shape[0] == V}
+    assert per_entity == moved, per_entity ^ moved
+    assert ("decoder_ob.b" in moved) == (decoder == "hyperbolic_convtranse")
