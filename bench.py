@@ -53,6 +53,7 @@ sys.path.insert(0, os.path.join(REPO, "re-gcn_amd"))
 
 METRIC = "million edges aggregated/sec at d=200 history_len=3; MRR parity vs ref"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SIM_BLOCKER_CYCLES = int(os.environ.get("BENCH_SIM_BLOCKER_CYCLES", str(400_000_000)))  # ~0.2 s device wait
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix peak (MI355X_MICROARCH.md)
 
 
@@ -921,27 +922,51 @@ def owner_simulation(args, cfg, device, world):
         model.rdecoder.forward(emb, r_emb, at, mode="test")
 
     reps = 3
-    with torch.no_grad():
-        step()
-        torch.cuda.synchronize()
+
+    def reset():
         for sm in sims:
             sm.times = [[] for _ in range(world)]
             sm.chunk_marks = [[] for _ in range(world)]
+            sm.delivery = []
             for sg in sm.ranks:
                 sg.exchanged_bytes = 0
         for k in range(world):
             dec_times[k].clear()
-        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        start.record()
+
+    def timed(blocker):
+        """reps simulated steps; blocker: a device-side wait before each step, during which
+        the host enqueues the whole step, so the step's launches run back to back (device
+        time, no host-issue gaps).  Returns the mean ms per step."""
+        reset()
+        tot = 0.0
         for _ in range(reps):
+            if blocker:
+                torch.cuda._sleep(SIM_BLOCKER_CYCLES)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
             step()
-        end.record()
+            b.record()
+            if not blocker:
+                continue
+            torch.cuda.synchronize()
+            tot += a.elapsed_time(b)
         torch.cuda.synchronize()
-    total = start.elapsed_time(end) / reps
+        return tot / reps if blocker else a.elapsed_time(b)
+
+    with torch.no_grad():
+        step()
+        torch.cuda.synchronize()
+        t_host = time.perf_counter()
+        timed(False)  # as issued (the host's launch rate included): reported beside
+        host_issued_ms = (time.perf_counter() - t_host) * 1e3 / reps
+        issued_rank = np.sum([sm.per_rank_ms() for sm in sims], axis=0) / reps
+        issued_dec = np.array([sum(a.elapsed_time(b) for a, b in t) for t in dec_times]) / reps
+        total = timed(True)
     enc = np.sum([sm.per_rank_ms() for sm in sims], axis=0) / reps
     dec_ms = np.array([sum(a.elapsed_time(b) for a, b in t) for t in dec_times]) / reps
     per_rank = enc + dec_ms
-    replicated = total - float(per_rank.sum())
+    delivery = sum(sm.delivery_ms() for sm in sims) / reps
+    replicated = total - float(per_rank.sum()) - delivery
     layers = 2 * T
     link_gbs, links = 153.0, world - 1  # xGMI: 7 links x ~153 GB/s per MI355X (SURVEY.md §5)
     # received per rank per step (the sparse exchange: the rows the next layer reads; none
@@ -971,15 +996,23 @@ def owner_simulation(args, cfg, device, world):
         "edge_loads_per_rank": loads, "edge_loads_contiguous_ids": loads_plain,
         "predicted_step_ms": round(pred, 3),
         "predicted_M_edges_per_s": round(edges / pred / 1e3, 1),
-        "predicted_speedup_vs_this_run": round(total / pred, 2),
+        "halo_delivery_ms_excluded": round(delivery, 3),
+        "as_issued": {"host_ms_per_step": round(host_issued_ms, 3),
+                      "max_rank_ms": round(float((issued_rank + issued_dec).max()), 3),
+                      "note": "the same steps without the device-side wait: the one host issues all 8 ranks' "
+                              "launches (~8x a real rank's), so ranks see its launch-rate gaps"},
         "setup_s": round(setup_s, 1),
         "note": "ranks run one after another on one MI355X (parallel.RankSimulation); per-rank = device time "
                 "of its own launches (layer chunks incl. hub pass, relation-mean partials, its candidate "
-                "slice; the pack / unpack of its exchanges); replicated = the rest of the step; predicted "
-                "step = max over ranks of (rank + its exposed exchange) + replicated.  Exchange: per chunk one "
-                "all_to_all of the rows the next layer reads (ExchangePlan), its time = the busiest peer "
-                "link's bytes at the nominal 153 GB/s, starting when the chunk's rows are final and the "
-                "previous chunk's exchange is done; a layer exposes what runs past its last chunk",
+                "slice with the fused score + rank count; the send-side gather of its exchanges); "
+                "replicated = the rest of the step (initial state, relation GRU, queries, relation "
+                "decoder; the halo delivery of the simulated all_to_alls, RCCL's work on a node, is in it "
+                "too); each timed step starts behind a device-side wait so that its launches run back to "
+                "back (device time; `as_issued` without it); predicted step = max over ranks of (rank + "
+                "its exposed exchange) + replicated.  Exchange: per chunk two all_to_alls (x rows, |h|) of "
+                "the rows the next layer reads (ExchangePlan) into the receivers' halo rows, its time = the "
+                "busiest peer link's bytes at the nominal 153 GB/s, starting when the chunk's rows are final "
+                "and the previous chunk's exchange is done; a layer exposes what runs past its last chunk",
     }
 
 

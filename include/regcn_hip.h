@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 9
+#define REGCN_ABI_VERSION 10
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -584,6 +584,15 @@ int regcn_rank_f32(const float* score, int32_t B, int32_t N, const int32_t* targ
  * regcn_rank_f32's ranks, threshold = the target's score. */
 int regcn_rank_count_f32(const float* score, int32_t B, int32_t N, const float* threshold, const int32_t* filt_ptr,
                          const int32_t* filt_idx, int32_t* count_raw, int32_t* count_filt, void* stream);
+/* e / f2: the fused form of regcn_hyp_score_f32 + regcn_rank_count_f32 for the proxy score
+ * (flags: REGCN_SCORE_RAW_SCALE only; d % 4 == 0, d <= 256): counts[b] = #{n : S[b,n] >
+ * threshold[b]} over the N candidate rows, S bit for bit what regcn_hyp_score_f32 writes, with
+ * no B x N score matrix (rgcn/utils.py:21-50 sort_and_rank's position = this count + 1 when
+ * the target has no tie).  accumulate != 0 adds to counts (a candidate set scored as several
+ * row ranges).  workspace: regcn_hyp_ce_workspace_bytes(B, N) bytes. */
+int regcn_hyp_rank_fused_f32(const float* q, const float* cand, const float* bias, const float* scale,
+                             const float* margin, const float* threshold, int32_t B, int32_t N, int32_t d, float c,
+                             int32_t flags, void* workspace, int32_t accumulate, int32_t* counts, void* stream);
 /* e: the owner partition's exchange (the reference runs on one GPU, so no
  * reference call site): rows ids[i] of x (n_rows x d) and radius packed as records of stride
  * d + 4 floats (x row, radius, 3 pad) for one all_to_all, and the received records written back
@@ -592,6 +601,13 @@ int regcn_pack_rows_f32(const float* x, const float* radius, const int64_t* ids,
                         void* stream);
 int regcn_unpack_rows_f32(const float* in, const int64_t* ids, int64_t n, int32_t d, float* x, float* radius,
                           void* stream);
+/* e: the send side of the halo exchange: rows ids[i] of x and radius gathered into x_out
+ * (n x d, contiguous) and r_out (n), which two all_to_alls deliver straight into the
+ * receiving ranks' halo rows (the rows after the Vp owned ids, which that rank's consumer
+ * work lists name instead of the remote ids: no scatter).  d % 4 == 0, d <= 252, x and x_out
+ * 16-B aligned. */
+int regcn_gather_rows_f32(const float* x, const float* radius, const int64_t* ids, int64_t n, int32_t d,
+                          float* x_out, float* r_out, void* stream);
 
 /* ---- a1 / f3: snapshot construction on the device ------------------------------------
  * build_sub_graph + r2e (rgcn/utils.py:78-134) and the kernel work lists of

@@ -648,9 +648,24 @@ int regcn_rank_count_f32(const float* score_m, int32_t B, int32_t N, const float
   return rank(score_m, B, N, nullptr, threshold, filt_ptr, filt_idx, 0, count_raw, count_filt, ST(s));
 }
 
+int regcn_hyp_rank_fused_f32(const float* q, const float* cand, const float* bias, const float* scale,
+                             const float* margin, const float* threshold, int32_t B, int32_t N, int32_t d, float c,
+                             int32_t flags, void* workspace, int32_t accumulate, int32_t* counts, void* s) {
+  if (flags & ~REGCN_SCORE_RAW_SCALE) return set_error(REGCN_ENOTSUP, "fused rank count: proxy score flags only");
+  if (!workspace && B > 0) return set_error(REGCN_EINVAL, "null workspace");
+  ScoreArgs a = score_args(q, cand, bias, nullptr, scale, margin, B, N, d, c, flags);
+  a.thr = threshold;
+  a.part = (float*)workspace;
+  return rank_fused(a, accumulate, counts, ST(s));
+}
+
 int regcn_pack_rows_f32(const float* x, const float* radius, const int64_t* ids, int64_t n, int32_t d, float* out,
                         void* s) {
   return exchange_rows(1, const_cast<float*>(x), const_cast<float*>(radius), ids, n, d, out, ST(s));
+}
+int regcn_gather_rows_f32(const float* x, const float* radius, const int64_t* ids, int64_t n, int32_t d, float* x_out,
+                          float* r_out, void* s) {
+  return gather_rows(x, radius, ids, n, d, x_out, r_out, ST(s));
 }
 int regcn_unpack_rows_f32(const float* in, const int64_t* ids, int64_t n, int32_t d, float* x, float* radius, void* s) {
   return exchange_rows(0, x, radius, ids, n, d, const_cast<float*>(in), ST(s));

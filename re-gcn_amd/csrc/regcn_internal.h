@@ -153,6 +153,8 @@ struct ScoreArgs {
   float* coef;           // [B, N]: G dS/dxy
   float* rsum;           // [B, nblk]: per candidate block, sum_n G dS/dx2
   float* csum;           // [ngroups16, N, 3]: per 16-query group, sum_b (G dS/dy2, G, G (margin - n^2))
+  // fused rank count (MODE 3): per query #{n : S[b,n] > thr[b]}, partial counts in `part`
+  const float* thr;      // [B]
 };
 
 // Relation GRU of one timestep (relgru.hip).
@@ -316,6 +318,9 @@ int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st);
 inline size_t ce_partial_slots(int N) { return std::max<size_t>(((size_t)N + 63) / 64, 256); }
 int score_ce_bwd(ScoreArgs& a, hipStream_t st);
 int exchange_rows(int pack, float* x, float* r, const int64_t* idx, int64_t n, int d, float* buf, hipStream_t st);
+int gather_rows(const float* x, const float* r, const int64_t* idx, int64_t n, int d, float* x_out, float* r_out,
+                hipStream_t st);
+int rank_fused(ScoreArgs& a, int accumulate, int* counts, hipStream_t st);
 int rank(const float* S, int B, int N, const int* target, const float* ts, const int* filt_ptr, const int* filt_idx,
          int add, int* rank_raw, int* rank_filt, hipStream_t st);
 

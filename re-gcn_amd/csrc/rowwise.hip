@@ -244,7 +244,46 @@ __global__ __launch_bounds__(256) void k_unpack_rows(const float* __restrict__ i
   }
 }
 
+// The send side of the halo exchange: rows idx[i] of x and |h| gathered into a contiguous x
+// block (stride d) and |h| vector, which two all_to_alls deliver straight into the receivers'
+// halo rows (no scatter on the receiving side; parallel.ExchangePlan).
+__global__ __launch_bounds__(256) void k_gather_rows(const float* __restrict__ x, const float* __restrict__ r,
+                                                     const int64_t* __restrict__ idx, int64_t n, int d,
+                                                     float* __restrict__ x_out, float* __restrict__ r_out) {
+  const int64_t i0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * XR_ROWS;
+  const int lane = threadIdx.x & 63, q = d >> 2;
+  f4 v[XR_ROWS];
+#pragma unroll
+  for (int u = 0; u < XR_ROWS; ++u) {
+    const int64_t i = min(i0 + u, n - 1);
+    const int64_t src = idx[i];
+    if (lane < q) v[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x + src * d) + lane);
+    else v[u] = f4{lane == q ? r[src] : 0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int u = 0; u < XR_ROWS; ++u) {
+    if (i0 + u >= n) continue;
+    if (lane < q) reinterpret_cast<f4*>(x_out + (i0 + u) * d)[lane] = v[u];
+    else if (lane == q) r_out[i0 + u] = v[u].x;
+  }
+}
+
+int gather_rows(const float* x, const float* r, const int64_t* idx, int64_t n, int d, float* x_out, float* r_out,
+                hipStream_t st) {
+  if (n < 0) return set_error(REGCN_EINVAL, "negative row count");
+  if (n == 0) return 0;
+  if (!x || !r || !idx || !x_out || !r_out) return set_error(REGCN_EINVAL, "null pointer");
+  if (d <= 0 || (d & 3) || d > 4 * (WAVE - 1)) return set_error(REGCN_EINVAL, "row gather needs d %% 4 == 0, d <= 252");
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(x_out)) & 15)
+    return set_error(REGCN_EINVAL, "row gather needs 16-B aligned x and output");
+  const int64_t blocks = (n + 4 * XR_ROWS - 1) / (4 * XR_ROWS);
+  if (blocks > 0x7fffffffL) return set_error(REGCN_EINVAL, "row gather grid too large");
+  hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)blocks), dim3(256), 0, st, x, r, idx, n, d, x_out, r_out);
+  return check_launch("k_gather_rows");
+}
+
 int exchange_rows(int pack, float* x, float* r, const int64_t* idx, int64_t n, int d, float* buf, hipStream_t st) {
+  if (n < 0) return set_error(REGCN_EINVAL, "negative row count");
   if (n == 0) return 0;
   if (!x || !r || !idx || !buf) return set_error(REGCN_EINVAL, "null pointer");
   if (d <= 0 || (d & 3) || d > 4 * (WAVE - 1)) return set_error(REGCN_EINVAL, "row exchange needs d %% 4 == 0, d <= 252");

@@ -357,6 +357,18 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
       run_m[r] = mn;
       run_se[r] = se;
     }
+  } else if (MODE == 3) {  // fused rank count: this lane's running #{S > thr} per query row
+    // (the same S bits as MODE 0 writes, so the count equals k_rank's over the score matrix)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float t = qi[r] < p.B ? p.thr[qi[r]] : INFINITY;
+      float cnt = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ni[j] < p.N)
+          cnt += fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb) > t ? 1.f : 0.f;
+      run_se[r] += cnt;  // an exact integer (< 2^24 per lane)
+    }
   } else {  // MODE 2: CE backward coefficients
     const int nblk = (p.N + SN - 1) / SN;
     const float c = p.c, m2c = -2.f * c;
@@ -461,6 +473,15 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   // cross entropy: per-lane running (max, sum exp) over every tile of the strip, reduced over the
   // 16 lanes of each query row and written once, as partial xcd + 8 stripe of the query
   float run_m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY}, run_se[4] = {0.f, 0.f, 0.f, 0.f};
+  auto count_flush = [&]() {  // MODE 3: the 16 lanes of a query row summed, partial xcd + 8 stripe
+    const int np = 8 * S, pidx = xcd + 8 * stripe;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + 16 * wv + 4 * (lane >> 4) + r;
+      const float cnt = row16_sum(run_se[r]);
+      if ((lane & 15) == 0 && q < p.B) p.part[(int64_t)q * np + pidx] = cnt;
+    }
+  };
   auto ce_flush = [&]() {
     const int np = 8 * S, pidx = xcd + 8 * stripe;
 #pragma unroll
@@ -478,6 +499,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   };
   if (bn >= nbn) {  // no work for this stripe (whole workgroup, before any barrier)
     if (MODE == 1) ce_flush();
+    if (MODE == 3) count_flush();
     return;
   }
   const f4 z4 = {0.f, 0.f, 0.f, 0.f};
@@ -582,6 +604,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     bn = bn_next;
   }
   if (MODE == 1) ce_flush();
+  if (MODE == 3) count_flush();
   stamp(2);
 }
 
@@ -845,6 +868,21 @@ __global__ __launch_bounds__(256) void k_ce_combine(const float* __restrict__ pa
   }
 }
 
+// Sum of the fused rank count's per-strip partial counts (exact integers held in fp32) into
+// counts[b] (added to its value when `accumulate`: a candidate set scored in several ranges).
+__global__ __launch_bounds__(256) void k_count_combine(const float* __restrict__ part, int B, int np, int accumulate,
+                                                       int* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float* pb = part + (int64_t)b * np;
+  int s = 0;
+  for (int i = lane; i < np; i += 64) s += (int)pb[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) counts[b] = (accumulate ? counts[b] : 0) + s;
+}
+
 // Rank of the target under a descending sort, as 1 + #{n : S[b,n] > S[b,t]} (raw)
 // and the same count excluding the other true answers of the snapshot (time-aware
 // filter, rgcn/utils.py:51-75 sets them to -1e7).  filt_ptr/filt_idx: CSR of the
@@ -985,6 +1023,34 @@ int score_ce_bwd(ScoreArgs& a, hipStream_t st) {
   // kernel's two A groups would spill)
   hipLaunchKernelGGL((k_score_f32<2>), g2, b2, lds2, st, a);
   return check_launch("k_score_ce_bwd");
+}
+
+// Fused score + rank count (no B x N score matrix): counts[b] (+)= #{n : S[b,n] > thr[b]} with S
+// the proxy score k_score_f32<0> would write, bit for bit.  workspace: >= B * 8 * stripes floats
+// (regcn_hyp_ce_workspace_bytes(B, N) suffices).
+int rank_fused(ScoreArgs& a, int accumulate, int* counts, hipStream_t st) {
+  if (a.d <= 0 || (a.d & 3) || a.d > 16 * KB_MAX)
+    return set_error(REGCN_ENOTSUP, "fused rank count needs d %% 4 == 0, d <= 256 (d=%d)", a.d);
+  if (a.use_dist || a.c_r) return set_error(REGCN_ENOTSUP, "fused rank count computes the proxy score only");
+  if (a.B < 0 || a.N < 0) return set_error(REGCN_EINVAL, "negative size");
+  if (a.B > 0 && (!a.q || !a.thr || !counts || !a.part)) return set_error(REGCN_EINVAL, "null pointer");
+  if (a.B > 0 && a.N > 0 && !a.e) return set_error(REGCN_EINVAL, "null candidates");
+  if (a.B == 0) return 0;
+  if (a.N == 0) {  // nothing to count: counts stay (accumulate) or become 0
+    if (!accumulate) {
+      hipLaunchKernelGGL(k_count_combine, dim3((a.B + 3) / 4), dim3(256), 0, st, a.part, a.B, 0, 0, counts);
+      return check_launch("k_count_combine");
+    }
+    return 0;
+  }
+  a.trace = g_trace;
+  const int nbn = (a.N + SN - 1) / SN;
+  hipLaunchKernelGGL((k_score_f32<3>), dim3(score_f32_grid(a.B, nbn)), dim3(64 * SW2), score_f32_lds(a.d), st, a);
+  const int rc = check_launch("k_score_f32<3>");
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_count_combine, dim3((a.B + 3) / 4), dim3(256), 0, st, a.part, a.B,
+                     8 * score_f32_stripes(a.B, nbn), accumulate, counts);
+  return check_launch("k_count_combine");
 }
 
 int rank(const float* S, int B, int N, const int* target, const float* ts, const int* filt_ptr, const int* filt_idx,

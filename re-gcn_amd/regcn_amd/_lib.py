@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REGCN_HIP_LIB") or os.path.join(_HERE, "libregcn_hip.so")  # override: A/B builds
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -59,8 +59,10 @@ _SIGS = {
     "regcn_hyp_ce_f32": [P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P, P],
     "regcn_rank_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
     "regcn_rank_count_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
+    "regcn_hyp_rank_fused_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, _c_int, P, P],
     "regcn_pack_rows_f32": [P, P, P, ctypes.c_int64, _c_int, P, P],
     "regcn_unpack_rows_f32": [P, P, ctypes.c_int64, _c_int, P, P, P],
+    "regcn_gather_rows_f32": [P, P, P, ctypes.c_int64, _c_int, P, P, P],
     "regcn_layer_f32": [P, P],
     "regcn_layer_rowtail_f32": [P, P, P],
     "regcn_layer_rowtail_part_f32": [P, P, _c_int, _c_int, _c_int, P],

@@ -27,6 +27,8 @@ collective helpers (`allreduce_partials`, `allgather_rows`) and the plans are pl
 torch.distributed / numpy, covered on CPU with gloo (tests/test_parallel.py); the compute
 between them is the HIP library (tests/test_gpu_parity.py simulates the ranks on one GPU).
 """
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -155,6 +157,39 @@ class OwnerView:
         return self._dev
 
 
+class HaloView:
+    """A rank's OwnerView read through its halo numbering: every source id in the view's work
+    lists that another rank owns is replaced by the index of its row in the rank's halo (the
+    rows after the Vp owned ids, where the sparse exchange's all_to_alls land the received x
+    and |h| rows in place: no scatter on the receiving side).  Owned ids are unchanged.  The
+    hub pass keeps the base view's chunk lists (positions, cut at the ORIGINAL source blocks:
+    `hub_owner`) and reads the remapped row/type and row/source columns (`gather_cols`)."""
+
+    def __init__(self, view, remap):
+        self.v, self.remap = view, remap
+        self.hub_owner = view
+        self._work = self._cols = None
+
+    def __getattr__(self, name):
+        return getattr(self.__dict__["v"], name)
+
+    def work(self):
+        if self._work is None:
+            wk = dict(self.v.work())
+            if wk["item_src"].numel():
+                wk["item_src"] = self.remap[wk["item_src"].long()].to(torch.int32)
+            self._work = wk
+        return self._work
+
+    def gather_cols(self, cs, ss):
+        """(row/type order sources, row/source order sources) remapped (full-length copies;
+        the hub pass reads its rows' spans of them)."""
+        if self._cols is None:
+            self._cols = (self.remap[cs.long()].to(torch.int32), self.remap[ss.long()].to(torch.int32))
+            _lib.publish()
+        return self._cols
+
+
 # ------------------------------------------------------------------ sparse exchange
 def exchange_keys(g, layout):
     """The (receiver, row) pairs of the owner partition's exchange for consumer snapshot `g`:
@@ -205,6 +240,22 @@ class ExchangePlan:
             send, recv = s[sm], s[rm]
             self.chunks.append((send, torch.bincount(m[sm], minlength=W).tolist(),
                                 recv, torch.bincount(k[rm], minlength=W).tolist()))
+        # the halo: every received id, chunk by chunk (inside a chunk by sender, ascending) --
+        # the order in which the all_to_alls deliver the rows into the rows after the owned ids
+        self.halo = torch.cat([c[2] for c in self.chunks]) if self.chunks else s[:0]
+        off = np.cumsum([0] + [int(c[2].numel()) for c in self.chunks])
+        self.halo_off = [int(v) for v in off]
+
+    def remap(self, V, base):
+        """Global id -> the index a consumer reads it at: owned and unreceived ids unchanged,
+        received id halo[i] -> base + i (int64, on the plan's device; cached per base)."""
+        hit = self.__dict__.get("_remap")
+        if hit is not None and hit[0] == base:
+            return hit[1]
+        m = torch.arange(V, device=self.halo.device, dtype=torch.int64)
+        m[self.halo] = base + torch.arange(self.halo.numel(), device=self.halo.device, dtype=torch.int64)
+        self.__dict__["_remap"] = (base, m)
+        return m
 
     def rows_received(self):
         return sum(sum(c[3]) for c in self.chunks)
@@ -242,10 +293,40 @@ def exchange_rows(chunk, xn, rn, group=None, pack=pack_rows, unpack=unpack_rows)
     unpack(recv, ridx, xn, rn)
 
 
+# The sparse exchange delivers into the receiver's halo rows (HaloView; two all_to_alls per
+# chunk, x rows and |h|, no receive-side scatter); 0: one all_to_all of pack_rows' (d + 4)-float
+# records scattered into the global rows by unpack_rows (round 4)
+HALO = os.environ.get("REGCN_HALO", "1") != "0"
+
+
 def record_bytes(plan, d):
-    """Bytes per exchanged row: the sparse all_to_all moves pack_rows' (d + 4)-float records,
-    the in-place all-gathers (plan None) x and |h| alone, (d + 1) floats."""
-    return (d + 1) * 4 if plan is None else (d + 4) * 4
+    """Bytes per exchanged row: x and |h|, (d + 1) floats (the in-place all-gathers, plan None,
+    and the halo exchange); pack_rows' (d + 4)-float records without the halo."""
+    return (d + 1) * 4 if (plan is None or HALO) else (d + 4) * 4
+
+
+def exchange_halo(plan, j, xn, rn, base, group=None, gather=None):
+    """Chunk j of an ExchangePlan through the halo: this rank's rows other ranks read gathered
+    into a contiguous x block and |h| vector (regcn_gather_rows_f32), two all_to_all_singles
+    landing the received rows at rows base + halo_off[j] .. of xn / rn (the consumer's HaloView
+    numbering): no scatter.  `gather`: a stand-in for the HIP gather (CPU tests)."""
+    sidx, ss, _, rs = plan.chunks[j]
+    d = xn.shape[1]
+    xs, r1 = (gather or gather_rows)(xn, rn, sidx)
+    a, b = base + plan.halo_off[j], base + plan.halo_off[j + 1]
+    _all_to_all_into(xn[a:b], xs, rs, ss, group)
+    _all_to_all_into(rn[a:b], r1, rs, ss, group)
+    return d
+
+
+def gather_rows(xn, rn, ids):
+    """(x rows, |h| values) of rows `ids`, contiguous (regcn_gather_rows_f32)."""
+    d = xn.shape[1]
+    xs = torch.empty(ids.numel(), d, device=xn.device, dtype=torch.float32)
+    r1 = torch.empty(ids.numel(), device=xn.device, dtype=torch.float32)
+    _lib.call("regcn_gather_rows_f32", _lib.fptr(xn, "x"), _lib.fptr(rn, "radius"), _lib.dptr(ids, torch.int64, "ids"),
+              ids.numel(), d, _lib.fptr(xs), _lib.fptr(r1), _lib.stream())
+    return xs, r1
 
 
 FULL_EXCHANGE = "all rows"  # ShardedGraph.consumers: the next consumer is unknown -> all-gather
@@ -511,11 +592,32 @@ class ShardedGraph:
             return False
         if target is FULL_EXCHANGE:
             return None
-        plans = target.__dict__.setdefault("_xplans", {})
-        key = (self.rank, self.world, self.layout.chunks)
+        return target.plan_for(self.rank)
+
+    def exchange_target(self, step):
+        """The consumer object of this layer's rows (see exchange_plan), or None."""
+        if self.consumers is None:
+            return None
+        t = self.consumers[1] if step is not None else self.consumers[0]
+        return None if t is FULL_EXCHANGE else t
+
+    def plan_for(self, rank):
+        """Rank `rank`'s ExchangePlan with this snapshot as the consumer (cached)."""
+        plans = self.__dict__.setdefault("_xplans", {})
+        key = (rank, self.world, self.layout.chunks)
         if key not in plans:
-            plans[key] = ExchangePlan(target.g, self.layout, self.rank)
+            plans[key] = ExchangePlan(self.g, self.layout, rank)
         return plans[key]
+
+    def halo_views(self, plan, base):
+        """(the rank's whole-rows view, its chunk views) read through the halo numbering of
+        `plan` (this snapshot as the consumer) with the halo at rows [base, base + H)."""
+        cache = self.__dict__.setdefault("_halo_views", {})
+        if base not in cache:
+            remap = plan.remap(self.g.number_of_nodes(), base)
+            rv = HaloView(self.rank_view, remap) if self.rank_view is not None else None
+            cache[base] = (rv, [HaloView(v, remap) for _, v in self.views])
+        return cache[base]
 
     def link_bytes(self, plan, j, d):
         """Bytes on the busiest peer link in chunk j's exchange (the all-gather: one chunk of
@@ -595,19 +697,20 @@ class ShardedGraph:
         return agg
 
     def _rank_launches(self, mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                       drop_mask, c, euclid, step, out, gate, exchange):
+                       drop_mask, c, euclid, step, out, gate, exchange, views=None):
         """This rank's launches of one layer into `out`, exchange(j) after chunk j's rows are
         final.  Large snapshots: the hub pass and the gather once over all of the rank's rows,
         then each chunk's tail (full-size launches but the tails); otherwise each chunk's whole
-        layer launch."""
+        layer launch.  views: (whole-rows view, chunk views) to read x / r through (the halo
+        views when the input came through the halo exchange; default the plain views)."""
         from .hyperbolic_layers import _use_rowtail, run_layer, run_layer_chunked
         V, d = x.shape
-        rv = self.rank_view
+        rv, cvs = views if views is not None else (self.rank_view, [v for _, v in self.views])
         if rv is not None and _use_rowtail(V, int(rv.fw.host["rows"].shape[0]), d, prev_t, drop_mask, False):
-            run_layer_chunked(mode, rv, [v for _, v in self.views], x, r, rel, w_rel, nb, gamma, w_n, w_loop,
+            run_layer_chunked(mode, rv, cvs, x, r, rel, w_rel, nb, gamma, w_n, w_loop,
                               w_evolve, c, euclid, step, out, gate, exchange)
             return
-        for j, (_, view) in enumerate(self.views):
+        for j, view in enumerate(cvs):
             run_layer(mode, view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
                       drop_mask, c, euclid=euclid, step=step, out=out, gate=gate)
             exchange(j)
@@ -625,9 +728,19 @@ class ShardedGraph:
                              w_skip, b_skip, drop_mask, c, euclid=euclid, step=step, agg=agg)
         lay = self.layout
         W, cr = self.world, lay.cr
+        # the input came through the halo exchange for this snapshot: read the full buffers
+        # (owned rows + halo) through the halo views
+        tag = getattr(x, "_regcn_halo", None)
+        views, xin, rin = None, x, r
+        if tag is not None and tag[0] is self:
+            xin, rin = tag[1], tag[2]
+            views = self.halo_views(self.plan_for(self.rank), lay.Vp)
+        plan = self.exchange_plan(step) if W > 1 else False
+        halo_out = HALO and isinstance(plan, ExchangePlan) and self.collective
+        H = plan.halo.numel() if halo_out else 0
         h = torch.empty(lay.Vp, d, device=x.device, dtype=torch.float32)
-        xn = torch.empty(lay.Vp, d, device=x.device, dtype=torch.float32)
-        rn = torch.empty(lay.Vp, device=x.device, dtype=torch.float32)
+        xn = torch.empty(lay.Vp + H, d, device=x.device, dtype=torch.float32)
+        rn = torch.empty(lay.Vp + H, device=x.device, dtype=torch.float32)
         # the rank's rows in pipeline chunks: after chunk j's launch, chunk j of every rank --
         # one contiguous id range -- is all-gathered in place, x and |h| (804 B per row), on a
         # side stream while chunk j + 1 computes (partitioning 2 with overlap)
@@ -637,7 +750,6 @@ class ShardedGraph:
             if self._comm is None:
                 self._comm = torch.cuda.Stream(x.device)
             comm = self._comm
-        plan = self.exchange_plan(step) if W > 1 else False
 
         def gather_all(j):  # chunk j of every rank, in place
             a, b, k = j * W * cr, (j + 1) * W * cr, (j * W + self.rank) * cr
@@ -645,7 +757,10 @@ class ShardedGraph:
             _all_gather_into(rn[a:b], rn[k:k + cr], self.group)
 
         def gather_needed(j):  # the rows the consumer reads
-            exchange_rows(plan.chunks[j], xn, rn, self.group)
+            if halo_out:  # straight into the consumer's halo rows
+                exchange_halo(plan, j, xn, rn, lay.Vp, self.group)
+            else:
+                exchange_rows(plan.chunks[j], xn, rn, self.group)
 
         def exchange(j):  # once this rank's chunk-j rows are written
             if plan is False:
@@ -661,16 +776,18 @@ class ShardedGraph:
             with torch.cuda.stream(comm):
                 fn(j)
 
-        self._rank_launches(mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                            drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, exchange)
+        self._rank_launches(mode, xin, rin, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
+                            drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, exchange, views=views)
         if comm is not None:
             cur.wait_stream(comm)
             for t in (xn, rn):
                 t.record_stream(comm)
-        hv = h[:V]
+        hv, xv = h[:V], xn[:V]
         if self.collective:  # only this rank's rows of h are computed (complete_rows / fetch_rows)
             hv._regcn_owner = (self, h)
-        return hv, xn[:V], rn[:V]
+        if halo_out:  # the consumer reads the received rows at rows Vp.. (HaloView)
+            xv._regcn_halo = (self.exchange_target(step), xn, rn)
+        return hv, xv, rn[:V]
 
     # ---- owner partition: the rows other ranks computed, when a consumer needs them
     def relation_means(self, x, R2):
@@ -775,6 +892,7 @@ class RankSimulation(ShardedGraph):
             r.collective = False
         self.times = [[] for _ in range(world)]
         self.chunk_marks = [[] for _ in range(world)]  # per rank: (chunk-end events, link bytes) per layer
+        self.delivery = []  # event pairs around the simulated halo deliveries (the all_to_alls' data)
 
     def _timed(self, k, fn):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -784,40 +902,79 @@ class RankSimulation(ShardedGraph):
         self.times[k].append((a, b))
         return out
 
+    def halo_bases(self):
+        """[Vp, Vp + H_0, Vp + H_0 + H_1, ...]: with every simulated rank's layers writing one
+        shared buffer, rank k's halo (this snapshot as the consumer) sits at rows
+        [bases[k], bases[k + 1])."""
+        hit = self.__dict__.get("_halo_bases")
+        if hit is None:
+            sizes = [self.plan_for(k).halo.numel() for k in range(self.world)]
+            hit = self.__dict__["_halo_bases"] = [self.layout.Vp + int(v) for v in np.cumsum([0] + sizes)]
+        return hit
+
     def run_layer(self, mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
                   drop_mask, c, euclid=False, step=None, gate=None):
         V, d = x.shape
         lay = self.layout
+        tag = getattr(x, "_regcn_halo", None)
+        halo_in = tag is not None and tag[0] is self
+        xin, rin = (tag[1], tag[2]) if halo_in else (x, r)
+        in_bases = self.halo_bases() if halo_in else None
+        for sg in self.ranks:
+            sg.consumers = self.consumers
+        plans = [sg.exchange_plan(step) for sg in self.ranks]
+        target = self.ranks[0].exchange_target(step)
+        halo_out = HALO and all(isinstance(p, ExchangePlan) for p in plans)
+        out_bases = target.halo_bases() if halo_out else None
         h = torch.empty(lay.Vp, d, device=x.device, dtype=torch.float32)
-        xn = torch.empty(lay.Vp, d, device=x.device, dtype=torch.float32)
-        rn = torch.empty(lay.Vp, device=x.device, dtype=torch.float32)
+        xn = torch.empty(out_bases[-1] if halo_out else lay.Vp, d, device=x.device, dtype=torch.float32)
+        rn = torch.empty(xn.shape[0], device=x.device, dtype=torch.float32)
 
-        def rank_launches(sg, plan, marks):
-            def after(j):  # chunk j's rows final: its exchange's pack / unpack on this stream
-                if plan:  # the rank's two kernels: its send records, and the received records
-                    sidx, _, ridx, _ = plan.chunks[j]  # scattered (into scratch rows here: the
-                    send = pack_rows(xn, rn, sidx)      # simulated rows hold their values already)
+        def rank_launches(k, sg, plan, marks):
+            def after(j):  # chunk j's rows final: the rank's send-side kernel(s) of its exchange
+                if plan and halo_out:  # its send block (delivered into the halos below)
+                    gather_rows(xn, rn, plan.chunks[j][0])
+                elif plan:  # the records, and the received records scattered (into scratch rows
+                    sidx, _, ridx, _ = plan.chunks[j]  # here: the simulated rows hold their
+                    send = pack_rows(xn, rn, sidx)      # values already)
                     recv = torch.empty(ridx.numel(), d + 4, device=x.device, dtype=torch.float32)
                     del send
                     unpack_rows(recv, ridx, scratch[0], scratch[1])
                 e = torch.cuda.Event(enable_timing=True)
                 e.record()
                 marks.append(e)
-            sg._rank_launches(mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                              drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, after)
-        scratch = self.__dict__.get("_scratch")
-        if scratch is None or scratch[0].shape != xn.shape:
-            scratch = self.__dict__["_scratch"] = (torch.empty_like(xn), torch.empty_like(rn))
+            views = sg.halo_views(self.plan_for(k), in_bases[k]) if halo_in else None
+            sg._rank_launches(mode, xin, rin, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
+                              drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, after, views=views)
+        scratch = None
+        if not halo_out:
+            scratch = self.__dict__.get("_scratch")
+            if scratch is None or scratch[0].shape != xn.shape:
+                scratch = self.__dict__["_scratch"] = (torch.empty_like(xn), torch.empty_like(rn))
         for k, sg in enumerate(self.ranks):
-            sg.consumers = self.consumers
-            plan = sg.exchange_plan(step)
+            plan = plans[k]
             marks = []
-            self._timed(k, lambda: rank_launches(sg, plan, marks))
+            self._timed(k, lambda: rank_launches(k, sg, plan, marks))
             rows = 0 if plan is False else ((self.world - 1) * lay.cr * lay.chunks if plan is None
                                             else plan.rows_received())
             sg.exchanged_bytes += rows * record_bytes(plan, d)
             self.chunk_marks[k].append((marks, [sg.link_bytes(plan, j, d) for j in range(len(marks))]))
-        return h[:V], xn[:V], rn[:V]
+        xv = xn[:V]
+        if halo_out:
+            # what the ranks' all_to_alls deliver on a node (RCCL over xGMI, which the link model
+            # times): rank k's halo rows from their owners' rows, for the consumer's halo views;
+            # bracketed so the measurement can leave it out (`delivery`)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for k, p in enumerate(plans):
+                a, n = out_bases[k], p.halo.numel()
+                if n:
+                    xn[a:a + n] = xn.index_select(0, p.halo)
+                    rn[a:a + n] = rn.index_select(0, p.halo)
+            e1.record()
+            self.delivery.append((e0, e1))
+            xv._regcn_halo = (target, xn, rn)
+        return h[:V], xv, rn[:V]
 
     def exposed_exchange_ms(self, link_gbs=153.0):
         """Per rank: the exchange time no compute hides, summed over the layers run since
@@ -844,6 +1001,9 @@ class RankSimulation(ShardedGraph):
 
     def per_rank_ms(self):
         return [sum(a.elapsed_time(b) for a, b in t) for t in self.times]
+
+    def delivery_ms(self):
+        return sum(a.elapsed_time(b) for a, b in self.delivery)
 
 
 # ------------------------------------------------------------------- sharded decoder
@@ -883,8 +1043,9 @@ class CandidateShard:
     scores its candidates with the HIP scorer and combines:
       * cross entropy: per-slice log-sum-exp (regcn_hyp_ce_lse_f32 on the slice) -> combine_lse;
         the target logit is the pair score of (q_b, e_{t_b}) computed on every rank;
-      * ranks: the target's score as threshold, per-slice count-greater with the slice-local
-        filter list (regcn_rank_count_f32) -> combine_counts, + 1.
+      * ranks: the target's score as threshold, the count of candidates above it fused into
+        the scorer (regcn_hyp_rank_fused_f32: no score matrix), minus the listed answers above
+        it for the filtered rank -> combine_counts, + 1.
     With group=None the collectives are skipped (a single-process simulation of one rank)."""
 
     def __init__(self, N, rank, world, group=None, ranges=None):
@@ -961,22 +1122,73 @@ class CandidateShard:
         both = combine_counts(both, self.group)
         return both[0].long() + 1, both[1].long() + 1
 
+    def fused_counts(self, q, cand, bias, c, ts, scale=None, margin=0.0, raw_scale=False):
+        """#{n in this shard's id ranges : S(q_b, e_n) > ts_b} with no score matrix: one
+        regcn_hyp_rank_fused_f32 launch per range (a range's rows are contiguous in `cand`: no
+        copy), the counts accumulated on the device.  S is bit for bit the full scoring's, so
+        the counts equal regcn_rank_count_f32's over the score matrix.  None when the fused
+        scorer does not apply (d % 4 != 0 or d > 256)."""
+        from .hyperbolic_decoder import _scalar
+        B, d = q.shape
+        if d % 4 or d > 256:
+            return None
+        dev = q.device
+        q = q.contiguous().float()
+        cand = cand.contiguous()
+        ts = ts.contiguous().float()
+        counts = torch.zeros(B, device=dev, dtype=torch.int32)
+        spans = [(a, b) for a, b in self.ranges if b > a]
+        if not spans or B == 0:
+            return counts
+        lib = _lib.lib()
+        ws = torch.empty((max(lib.regcn_hyp_ce_workspace_bytes(B, b - a) for a, b in spans) + 3) // 4, device=dev)
+        sc = _scalar(scale if scale is not None else 1.0, q)
+        mg = _scalar(margin, q)
+        flags = _lib.SCORE_RAW_SCALE if raw_scale else 0
+        f = _lib.fptr
+        for k, (a, b) in enumerate(spans):
+            _lib.call("regcn_hyp_rank_fused_f32", f(q, "query"), f(cand[a:b], "candidates"),
+                      f(bias[a:b]) if bias is not None else None, f(sc), f(mg), f(ts, "threshold"), B, b - a, d,
+                      float(c), flags, f(ws), int(k > 0), _lib.iptr(counts), _lib.stream())
+        return counts
+
+    def filter_hits(self, q, cand, bias, c, ts, filt_ptr, filt_idx, **kw):
+        """#{f in query b's filter list, f in this shard's ranges : S(q_b, e_f) > ts_b}: the
+        filtered count is the raw count minus these.  The listed candidates are scored as one
+        block (the same per-pair bits as the full scoring) and compared on the device."""
+        from .hyperbolic_decoder import _chunked_hyperbolic_dist_score
+        ptr = np.asarray(filt_ptr, dtype=np.int64)
+        idx = np.asarray(filt_idx, dtype=np.int64)
+        row = np.repeat(np.arange(len(ptr) - 1), np.diff(ptr))
+        keep = np.zeros(len(idx), dtype=bool)
+        for a, b in self.ranges:
+            keep |= (idx >= a) & (idx < b)
+        B = q.shape[0]
+        dev = q.device
+        if not keep.any():
+            return torch.zeros(B, device=dev, dtype=torch.int32)
+        row, idx = row[keep], idx[keep]
+        uniq, pos = np.unique(idx, return_inverse=True)
+        u = torch.from_numpy(uniq).to(dev)
+        S = _chunked_hyperbolic_dist_score(q, cand.index_select(0, u), bias.index_select(0, u) if bias is not None
+                                           else None, c, 0, 0, score_scale=kw.get("scale"),
+                                           score_margin=kw.get("margin", 0.0), _raw_scale=kw.get("raw_scale", False))
+        rt = torch.from_numpy(row).to(dev)
+        hit = (S[rt, torch.from_numpy(pos).to(dev)] > ts.float()[rt]).to(torch.int32)
+        return torch.zeros(B, device=dev, dtype=torch.int32).index_add_(0, rt, hit)
+
     def range_ranks(self, q, cand, bias, c, ts, filt_ptr=None, filt_idx=None, **kw):
-        """ranks() over every id range of this shard (one scorer launch and one count launch
-        per range, the counts summed; without a filter the ranges' rows are scored together, as
-        one candidate block), then ONE all_reduce of the 2B counts."""
-        tot = None
-        if filt_ptr is None and len(self.ranges) > 1:
-            rows = torch.cat([torch.arange(a, b, device=cand.device) for a, b in self.ranges])
-            cs = cand.index_select(0, rows)
-            bs = bias.index_select(0, rows) if bias is not None else None
-            from .hyperbolic_decoder import _chunked_hyperbolic_dist_score
-            S = _chunked_hyperbolic_dist_score(q, cs, bs, c, 0, 0, score_scale=kw.get("scale"),
-                                               score_margin=kw.get("margin", 0.0), _raw_scale=kw.get("raw_scale", False))
-            self.n0, self.n1 = 0, int(rows.numel())
-            raw, _ = self.local_counts(S, ts)
-            tot = combine_counts(torch.stack([raw, raw]), self.group)
+        """(rank, filtered rank) over all N candidates, 1-based, replicated: this shard's counts
+        over its id ranges (fused_counts: no score matrix; the filtered count subtracts
+        filter_hits), then ONE all_reduce of the 2B counts.  Without the fused scorer: one
+        scorer launch and one count launch per range."""
+        raw = self.fused_counts(q, cand, bias, c, ts, **kw)
+        if raw is not None:
+            flt = raw - self.filter_hits(q, cand, bias, c, ts, filt_ptr, filt_idx, **kw) if filt_ptr is not None \
+                else raw
+            tot = combine_counts(torch.stack([raw, flt]), self.group)
             return tot[0].long() + 1, tot[1].long() + 1
+        tot = None
         for n0, n1 in self.ranges:
             self.n0, self.n1 = n0, n1
             raw, flt = self.local_counts(self.scores(q, cand, bias, c, **kw), ts, filt_ptr, filt_idx)

@@ -355,6 +355,44 @@ def test_score_shapes_vs_oracle(B, N, d):
     assert_close(sc(q.to(DEV), e.to(DEV), None, C, 128, 256), OM.dist_score(q, e, None, C), what="score")
 
 
+@pytest.mark.parametrize("B,N,d,ranges", [(1, 1, 4, [(0, 1)]), (5, 700, 12, [(0, 300), (300, 301), (500, 700)]),
+                                           (130, 3000, 200, [(0, 1000), (1000, 3000)]), (1024, 20000, 256, [(0, 20000)])])
+def test_fused_rank_count_matches_score_matrix(B, N, d, ranges):
+    """regcn_hyp_rank_fused_f32 (score + count-greater in one launch, no score matrix) against
+    regcn_hyp_score_f32 + the count over the score matrix: equal counts for thresholds at
+    existing scores (ties at the threshold are not counted: strictly greater) and in between,
+    over several candidate ranges accumulated (CandidateShard.fused_counts), with a per-
+    candidate bias and the raw score scale; filter_hits: the listed answers above the threshold."""
+    from regcn_amd.hyperbolic_decoder import _chunked_hyperbolic_dist_score as sc
+    from regcn_amd.parallel import CandidateShard
+    from oracle import ops as O
+    g = torch.Generator().manual_seed(B + N + d)
+    q = O.exp0(torch.randn(B, d, generator=g), C).to(DEV)
+    e = O.exp0(torch.randn(N, d, generator=g), C).to(DEV)
+    bias = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    scale_raw = torch.tensor(0.7, device=DEV)
+    margin = torch.tensor(1.3, device=DEV)
+    S = sc(q, e, bias, C, 0, 0, score_scale=scale_raw, score_margin=margin, _raw_scale=True)
+    pick = torch.randint(0, N, (B,), generator=g).to(DEV)
+    thr = S.gather(1, pick[:, None]).flatten()
+    thr[::3] = thr[::3] + 1e-3  # thresholds between scores too
+    sh = CandidateShard(N, 0, 1, None, ranges=ranges)
+    kw = dict(scale=scale_raw, margin=margin, raw_scale=True)
+    got = sh.fused_counts(q, e, bias, C, thr, **kw)
+    mask = torch.zeros(N, dtype=torch.bool, device=DEV)
+    for a, b in ranges:
+        mask[a:b] = True
+    want = ((S > thr[:, None]) & mask[None, :]).sum(1).to(torch.int32)
+    assert torch.equal(got, want)
+    # filtered: 3 listed answers per query
+    fl = torch.randint(0, N, (B, 3), generator=g)
+    fp = np.arange(0, 3 * B + 1, 3)
+    hits = sh.filter_hits(q, e, bias, C, thr, fp, fl.flatten().numpy(), **kw)
+    fl = fl.to(DEV)
+    want_h = ((S.gather(1, fl) > thr[:, None]) & mask[fl]).sum(1).to(torch.int32)
+    assert torch.equal(hits, want_h)
+
+
 def _zipf_snapshot(V, R, T, seed):
     rng = np.random.default_rng(seed)
     p = 1.0 / np.arange(1, V + 1) ** 1.1

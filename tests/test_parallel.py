@@ -365,6 +365,19 @@ def _exchange_worker(rank, world, port, q):
             ok &= bool((got == need).all())
             ok &= bool(torch.equal(xn[:V][need], ref[need]) and torch.equal(rn[:V][need], -ref[need, 0]))
             ok &= plan.rows_received() == int((need & ~mine).sum())
+            # the halo exchange: the received rows land at rows Vp + halo_off[j] .. in the plan's
+            # halo order, and the remap sends every in-edge source of this rank's rows there
+            H = plan.halo.numel()
+            xh = torch.full((lay.Vp + H, d), float("nan"))
+            rh = torch.full((lay.Vp + H,), float("nan"))
+            for j, (lo, hi) in enumerate(lay.ranges(rank)):
+                xh[lo:hi], rh[lo:hi] = ref[lo:hi], -ref[lo:hi, 0]
+                P.exchange_halo(plan, j, xh, rh, lay.Vp, gather=lambda x_, r_, i_: (x_[i_], r_[i_]))
+            m = plan.remap(V, lay.Vp).numpy()
+            srcs = src[mine[dst]]
+            ok &= bool(torch.equal(xh[torch.from_numpy(m[srcs])], ref[srcs]))
+            ok &= bool(torch.equal(rh[torch.from_numpy(m[srcs])], -ref[srcs, 0]))
+            ok &= bool((m[mine] == np.nonzero(mine)[0]).all()) and bool((m[need & ~mine] >= lay.Vp).all())
         q.put((rank, ok))
     finally:
         dist.destroy_process_group()
@@ -374,7 +387,9 @@ def _exchange_worker(rank, world, port, q):
 def test_sparse_exchange_gloo(world):
     """ExchangePlan + exchange_rows (the owner partition's per-chunk all_to_all): after every
     chunk's exchange a rank holds exactly its own rows and the sources of its rows' in-edges,
-    with the owners' values; senders and receivers agree on the order."""
+    with the owners' values; senders and receivers agree on the order.  The
+    halo exchange (exchange_halo: two all_to_alls straight into the rows after Vp) delivers the
+    same rows where ExchangePlan.remap points the consumer's source ids."""
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()

@@ -5,7 +5,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 900 python -u -m pytest -v --timeout 400 --timeout-method thread tests/test_gpu_dataset_full.py tests/test_gpu_decoder_c5.py tests/test_gpu_sharded.py > gpurun_out/r5a_pytest.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/r5a_pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest -v --timeout 400 --timeout-method thread tests/test_gpu_parity.py::test_fused_rank_count_matches_score_matrix tests/test_gpu_dataset_full.py tests/test_gpu_decoder_c5.py tests/test_gpu_sharded.py > gpurun_out/r5a_pytest.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/r5a_pytest.log; exit 1; }
 tail -3 gpurun_out/r5a_pytest.log
 timeout -k 10 300 python -u bench.py --config gdelt --steps 32 > gpurun_out/r5a_gdelt.json 2> gpurun_out/r5a_gdelt.err || { echo "gdelt bench failed"; tail -20 gpurun_out/r5a_gdelt.err; exit 1; }
 echo "gdelt bench ok"
