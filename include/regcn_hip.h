@@ -586,13 +586,16 @@ int regcn_rank_count_f32(const float* score, int32_t B, int32_t N, const float* 
                          const int32_t* filt_idx, int32_t* count_raw, int32_t* count_filt, void* stream);
 /* e / f2: the fused form of regcn_hyp_score_f32 + regcn_rank_count_f32 for the proxy score
  * (flags: REGCN_SCORE_RAW_SCALE only; d % 4 == 0, d <= 256): counts[b] = #{n : S[b,n] >
- * threshold[b]} over the N candidate rows, S bit for bit what regcn_hyp_score_f32 writes, with
+ * threshold[b]} over the candidate rows, S bit for bit what regcn_hyp_score_f32 writes, with
  * no B x N score matrix (rgcn/utils.py:21-50 sort_and_rank's position = this count + 1 when
- * the target has no tie).  accumulate != 0 adds to counts (a candidate set scored as several
- * row ranges).  workspace: regcn_hyp_ce_workspace_bytes(B, N) bytes. */
+ * the target has no tie).  The candidates are rows [0, N) of cand, or with n_ranges > 0 the
+ * union of the row ranges {ranges[2r], ranges[2r+1]} (a HOST array, <= 8 ranges inside [0, N):
+ * a rank's owner ranges in one launch; bias indexed by row).  accumulate != 0 adds to counts.
+ * workspace: regcn_hyp_ce_workspace_bytes(B, N) bytes. */
 int regcn_hyp_rank_fused_f32(const float* q, const float* cand, const float* bias, const float* scale,
                              const float* margin, const float* threshold, int32_t B, int32_t N, int32_t d, float c,
-                             int32_t flags, void* workspace, int32_t accumulate, int32_t* counts, void* stream);
+                             int32_t flags, const int32_t* ranges, int32_t n_ranges, void* workspace,
+                             int32_t accumulate, int32_t* counts, void* stream);
 /* e: the owner partition's exchange (the reference runs on one GPU, so no
  * reference call site): rows ids[i] of x (n_rows x d) and radius packed as records of stride
  * d + 4 floats (x row, radius, 3 pad) for one all_to_all, and the received records written back

@@ -650,10 +650,27 @@ int regcn_rank_count_f32(const float* score_m, int32_t B, int32_t N, const float
 
 int regcn_hyp_rank_fused_f32(const float* q, const float* cand, const float* bias, const float* scale,
                              const float* margin, const float* threshold, int32_t B, int32_t N, int32_t d, float c,
-                             int32_t flags, void* workspace, int32_t accumulate, int32_t* counts, void* s) {
+                             int32_t flags, const int32_t* ranges, int32_t n_ranges, void* workspace,
+                             int32_t accumulate, int32_t* counts, void* s) {
   if (flags & ~REGCN_SCORE_RAW_SCALE) return set_error(REGCN_ENOTSUP, "fused rank count: proxy score flags only");
   if (!workspace && B > 0) return set_error(REGCN_EINVAL, "null workspace");
+  if (n_ranges < 0 || n_ranges > SCORE_MAX_RANGES || (n_ranges > 0 && !ranges))
+    return set_error(REGCN_EINVAL, "fused rank count takes 0..%d candidate ranges", SCORE_MAX_RANGES);
   ScoreArgs a = score_args(q, cand, bias, nullptr, scale, margin, B, N, d, c, flags);
+  int tiles = 0, k = 0;
+  for (int r = 0; r < n_ranges; ++r) {  // host array {start, end} per range; empty ranges dropped
+    const int lo = ranges[2 * r], hi = ranges[2 * r + 1];
+    if (lo < 0 || hi < lo || hi > N) return set_error(REGCN_EINVAL, "candidate range [%d, %d) outside [0, %d)", lo, hi, N);
+    if (hi == lo) continue;
+    a.rng_start[k] = lo;
+    a.rng_len[k] = hi - lo;
+    a.rng_tile[k] = tiles;
+    tiles += (hi - lo + 63) / 64;
+    ++k;
+  }
+  a.n_rng = n_ranges ? k : 0;
+  a.rng_tile[a.n_rng] = tiles;
+  if (n_ranges && !k) a.N = 0;  // every range empty
   a.thr = threshold;
   a.part = (float*)workspace;
   return rank_fused(a, accumulate, counts, ST(s));

@@ -155,7 +155,14 @@ struct ScoreArgs {
   float* csum;           // [ngroups16, N, 3]: per 16-query group, sum_b (G dS/dy2, G, G (margin - n^2))
   // fused rank count (MODE 3): per query #{n : S[b,n] > thr[b]}, partial counts in `part`
   const float* thr;      // [B]
+  // candidate row ranges (n_rng > 0): the candidates are rows [rng_start[r], rng_start[r] +
+  // rng_len[r]) of e, tiled range by range (range r's tiles [rng_tile[r], rng_tile[r + 1])),
+  // so one launch covers a rank's owner ranges; n_rng == 0: rows [0, N)
+  int n_rng;
+  int rng_start[8], rng_len[8], rng_tile[9];
 };
+
+constexpr int SCORE_MAX_RANGES = 8;
 
 // Relation GRU of one timestep (relgru.hip).
 struct RelGruArgs {

@@ -639,13 +639,22 @@ static int rowtail_rg() {
   return v;
 }
 
-constexpr int RT_RG2_MIN_ROWS = 256 * 1024;
+// Rows from which a launch takes two groups per wave (REGCN_RT_RG2_MIN_ROWS overrides: a rank's
+// chunk tails that run two at a time on two streams fill the chip with fewer rows each).
+static int rt_rg2_min_rows() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("REGCN_RT_RG2_MIN_ROWS");
+    v = e ? atoi(e) : 256 * 1024;
+  }
+  return v;
+}
 
 template <int NT>
 static int launch_tail(const LayerArgs& a, int r0, int r1, hipStream_t st) {
   // two groups only when the launch still fills the chip with 128-row workgroups (a rank's
   // slice of an owner-partitioned snapshot runs one group per wave: more, shorter workgroups)
-  const int rg = (NT > 8 && rowtail_rg() == 2 && r1 - r0 >= RT_RG2_MIN_ROWS) ? 2 : 1;
+  const int rg = (NT > 8 && rowtail_rg() == 2 && r1 - r0 >= rt_rg2_min_rows()) ? 2 : 1;
   const unsigned grid = (unsigned)((r1 - r0 + RT_ROWS * rg - 1) / (RT_ROWS * rg));
   const size_t lds = rt_lds_bytes(rg);
   if (a.fuse_step && a.step.tw) {

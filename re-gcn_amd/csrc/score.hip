@@ -462,7 +462,20 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   };
   stamp(0);
   const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
-  const int nbn = (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
+  const int nbn = p.n_rng ? p.rng_tile[p.n_rng] : (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
+  // candidate tile t -> its first row and valid rows (row ranges: a tile never spans two)
+  auto tile_rows = [&](int t, int& row0, int& nvalid) {
+    if (!p.n_rng) {
+      row0 = t * SN;
+      nvalid = min(SN, p.N - row0);
+      return;
+    }
+    int r = 0;
+    while (r + 1 < p.n_rng && t >= p.rng_tile[r + 1]) ++r;
+    const int off = (t - p.rng_tile[r]) * SN;
+    row0 = p.rng_start[r] + off;
+    nvalid = min(SN, p.rng_len[r] - off);
+  };
   const int S = nblk / (8 * nbq);
   const int xcd = blk & 7, rk = blk >> 3;
   const int bq = rk % nbq, stripe = rk / nbq;
@@ -532,14 +545,18 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   const int sr = tid >> 3, sub = tid & 7, per_row = 4 * KB;
   f4 v[IT];
   auto fetch = [&](int t) {  // unconditional clamped loads (a conditional load drains vmcnt)
-    const float* erow = p.e + (int64_t)min(t * SN + sr, p.N - 1) * d;
+    int row0, nv;
+    tile_rows(t, row0, nv);
+    const float* erow = p.e + (int64_t)(row0 + min(sr, max(nv - 1, 0))) * d;
 #pragma unroll
     for (int it = 0; it < IT; ++it) v[it] = *reinterpret_cast<const f4*>(erow + min((sub + 8 * it) * 4, d - 4));
   };
   // |e|^2 of each staged row, summed over its 8 staging lanes (xor 1, 2, 4), next to the tile
   float* e2s = Es + 2 * SN * SE;  // [2][SN]
   auto stash = [&](int buf, int t) {
-    const bool row_ok = t * SN + sr < p.N;
+    int row0, nv;
+    tile_rows(t, row0, nv);
+    const bool row_ok = sr < nv;
     float* lrow = Es + buf * SN * SE + sr * SE;
     float ss = 0.f;
 #pragma unroll
@@ -565,7 +582,6 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     // next tile's rows in flight under this tile's MFMAs (MODE 2: after its epilogue, whose
     // live registers would otherwise spill)
     if (MODE != 2) fetch(min(bn_next, nbn - 1));
-    const int n0 = bn * SN;
     const float* brow = Es + cur * SN * SE + (lane & 15) * SE + g4;
     f4 acc[4] = {z4, z4, z4, z4};
     // B fragments of block b + 1 are read while block b's MFMAs run (register double buffer;
@@ -588,10 +604,11 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
       }
     }
     float y2[4], bn_[4];
-    int ni[4];
+    int ni[4], row0, nv;
+    tile_rows(bn, row0, nv);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      ni[j] = n0 + 16 * j + (lane & 15);
+      ni[j] = 16 * j + (lane & 15) < nv ? row0 + 16 * j + (lane & 15) : 0x7fffffff;  // invalid: >= N
       y2[j] = e2s[cur * SN + 16 * j + (lane & 15)];
       bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
     }
@@ -633,7 +650,20 @@ __device__ __forceinline__ void score_ws_body(ScoreArgs p, const int blk, const 
   const bool mfma_wave = wv < 4;  // wave-uniform role
   const int grpw = wv & 3;        // the 32-query group of this wave (MFMA wave and its epilogue wave)
   const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
-  const int nbn = (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
+  const int nbn = p.n_rng ? p.rng_tile[p.n_rng] : (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
+  // candidate tile t -> its first row and valid rows (row ranges: a tile never spans two)
+  auto tile_rows = [&](int t, int& row0, int& nvalid) {
+    if (!p.n_rng) {
+      row0 = t * SN;
+      nvalid = min(SN, p.N - row0);
+      return;
+    }
+    int r = 0;
+    while (r + 1 < p.n_rng && t >= p.rng_tile[r + 1]) ++r;
+    const int off = (t - p.rng_tile[r]) * SN;
+    row0 = p.rng_start[r] + off;
+    nvalid = min(SN, p.rng_len[r] - off);
+  };
   const int S = nblk / (8 * nbq);
   const int xcd = blk & 7, rk = blk >> 3;
   const int bq = rk % nbq, stripe = rk / nbq;
@@ -751,13 +781,17 @@ __device__ __forceinline__ void score_ws_body(ScoreArgs p, const int blk, const 
   const int sr = et >> 2, sub = et & 3, per_row = 4 * KB;
   f4 v[IT];
   auto fetch = [&](int t) {
-    const float* erow = p.e + (int64_t)min(t * SN + sr, p.N - 1) * d;
+    int row0, nv;
+    tile_rows(t, row0, nv);
+    const float* erow = p.e + (int64_t)(row0 + min(sr, max(nv - 1, 0))) * d;
 #pragma unroll
     for (int it = 0; it < IT; ++it)
       if (it < KB) v[it] = *reinterpret_cast<const f4*>(erow + min((sub + 4 * it) * 4, d - 4));
   };
   auto stash = [&](int buf, int t) {
-    const bool row_ok = t * SN + sr < p.N;
+    int row0, nv;
+    tile_rows(t, row0, nv);
+    const bool row_ok = sr < nv;
     float* lrow = Es + buf * SN * SE + sr * SE;
     float ss = 0.f;
 #pragma unroll
@@ -1036,7 +1070,8 @@ int rank_fused(ScoreArgs& a, int accumulate, int* counts, hipStream_t st) {
   if (a.B > 0 && (!a.q || !a.thr || !counts || !a.part)) return set_error(REGCN_EINVAL, "null pointer");
   if (a.B > 0 && a.N > 0 && !a.e) return set_error(REGCN_EINVAL, "null candidates");
   if (a.B == 0) return 0;
-  if (a.N == 0) {  // nothing to count: counts stay (accumulate) or become 0
+  const int nbn = a.n_rng ? a.rng_tile[a.n_rng] : (a.N + SN - 1) / SN;
+  if (nbn == 0) {  // nothing to count: counts stay (accumulate) or become 0
     if (!accumulate) {
       hipLaunchKernelGGL(k_count_combine, dim3((a.B + 3) / 4), dim3(256), 0, st, a.part, a.B, 0, 0, counts);
       return check_launch("k_count_combine");
@@ -1044,7 +1079,6 @@ int rank_fused(ScoreArgs& a, int accumulate, int* counts, hipStream_t st) {
     return 0;
   }
   a.trace = g_trace;
-  const int nbn = (a.N + SN - 1) / SN;
   hipLaunchKernelGGL((k_score_f32<3>), dim3(score_f32_grid(a.B, nbn)), dim3(64 * SW2), score_f32_lds(a.d), st, a);
   const int rc = check_launch("k_score_f32<3>");
   if (rc) return rc;

@@ -59,7 +59,8 @@ _SIGS = {
     "regcn_hyp_ce_f32": [P, P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, P, P],
     "regcn_rank_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
     "regcn_rank_count_f32": [P, _c_int, _c_int, P, P, P, P, P, P],
-    "regcn_hyp_rank_fused_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, _c_int, P, P],
+    "regcn_hyp_rank_fused_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, _c_int, P, _c_int, P, _c_int, P,
+                                 P],
     "regcn_pack_rows_f32": [P, P, P, ctypes.c_int64, _c_int, P, P],
     "regcn_unpack_rows_f32": [P, P, ctypes.c_int64, _c_int, P, P, P],
     "regcn_gather_rows_f32": [P, P, P, ctypes.c_int64, _c_int, P, P, P],

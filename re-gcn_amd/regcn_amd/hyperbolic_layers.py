@@ -32,6 +32,8 @@ ROWTAIL_MIN_VIEW_ROWS = int(os.environ.get("REGCN_ROWTAIL_MIN_VIEW_ROWS", "1024"
 # ... in this many row chunks: the gather of chunk i + 1 runs on a side stream beside the tail of
 # chunk i (the L2-bound gather beside the MFMA-bound tail); 1 = one stream, no pipelining
 ROWTAIL_CHUNKS = int(os.environ.get("REGCN_ROWTAIL_CHUNKS", "1"))
+# A rank's pipeline-chunk tails (owner partition) on this many streams (1: one after another)
+CHUNK_TAIL_STREAMS = int(os.environ.get("REGCN_CHUNK_TAIL_STREAMS", "2"))
 
 
 def _rowtail_chunks(g, k):
@@ -312,14 +314,26 @@ def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c,
         if mode != _lib.AGG_NONE and g.n_pos_tiles:
             _lib.check(part(ctypes.byref(desc), _lib.fptr(agg), 1, 0, int(g.n_pos_tiles), _lib.stream()),
                        "regcn_layer_rowtail_f32(gather)")
+        # chunk tails alternate between the calling stream and a side stream, so chunk j + 1's
+        # tail fills the CUs chunk j's drains from (a chunk is ~500 workgroups) while each
+        # chunk's completion still orders its exchange (after(j) runs on the chunk's stream)
+        cur = torch.cuda.current_stream(x.device)
+        lanes = [cur]
+        if CHUNK_TAIL_STREAMS > 1 and len(tail_views) > 1:
+            side = _rowtail_stream(x.device)
+            side.wait_stream(cur)
+            lanes.append(side)
         for j, tv in enumerate(tail_views):
-            tw = tv.work()
-            nr = int(tw["rows"].shape[0])
-            if nr:
-                keep.append(tw["rows"])
-                desc.rows, desc.n_pos, desc.V = a(tw["rows"], torch.int32), tv.n_pos, nr
-                _lib.check(part(ctypes.byref(desc), _lib.fptr(agg), 2, 0, nr, _lib.stream()), name)
-            after(j)
+            with torch.cuda.stream(lanes[j % len(lanes)]):
+                tw = tv.work()
+                nr = int(tw["rows"].shape[0])
+                if nr:
+                    keep.append(tw["rows"])
+                    desc.rows, desc.n_pos, desc.V = a(tw["rows"], torch.int32), tv.n_pos, nr
+                    _lib.check(part(ctypes.byref(desc), _lib.fptr(agg), 2, 0, nr, _lib.stream()), name)
+                after(j)
+        for ln in lanes[1:]:  # every side-stream read and write joined back (frees on `cur` are safe)
+            cur.wait_stream(ln)
         return h, xn, rn
     chunks = _rowtail_chunks(g, ROWTAIL_CHUNKS) if (ROWTAIL_CHUNKS > 1 and g.n_pos_tiles > 1
                                                      and mode != _lib.AGG_NONE) else None

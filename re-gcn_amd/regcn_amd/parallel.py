@@ -27,6 +27,7 @@ collective helpers (`allreduce_partials`, `allgather_rows`) and the plans are pl
 torch.distributed / numpy, covered on CPU with gloo (tests/test_parallel.py); the compute
 between them is the HIP library (tests/test_gpu_parity.py simulates the ranks on one GPU).
 """
+import ctypes
 import os
 
 import numpy as np
@@ -772,7 +773,7 @@ class ShardedGraph:
             if comm is None:
                 fn(j)
                 return
-            comm.wait_stream(cur)
+            comm.wait_stream(torch.cuda.current_stream(x.device))  # the stream chunk j's tail ran on
             with torch.cuda.stream(comm):
                 fn(j)
 
@@ -1123,11 +1124,11 @@ class CandidateShard:
         return both[0].long() + 1, both[1].long() + 1
 
     def fused_counts(self, q, cand, bias, c, ts, scale=None, margin=0.0, raw_scale=False):
-        """#{n in this shard's id ranges : S(q_b, e_n) > ts_b} with no score matrix: one
-        regcn_hyp_rank_fused_f32 launch per range (a range's rows are contiguous in `cand`: no
-        copy), the counts accumulated on the device.  S is bit for bit the full scoring's, so
-        the counts equal regcn_rank_count_f32's over the score matrix.  None when the fused
-        scorer does not apply (d % 4 != 0 or d > 256)."""
+        """#{n in this shard's id ranges : S(q_b, e_n) > ts_b} with no score matrix and no copy
+        of the candidate rows: regcn_hyp_rank_fused_f32 over the ranges (up to 8 per launch, the
+        counts accumulated on the device).  S is bit for bit the full scoring's, so the counts
+        equal regcn_rank_count_f32's over the score matrix.  None when the fused scorer does
+        not apply (d % 4 != 0 or d > 256)."""
         from .hyperbolic_decoder import _scalar
         B, d = q.shape
         if d % 4 or d > 256:
@@ -1140,16 +1141,18 @@ class CandidateShard:
         spans = [(a, b) for a, b in self.ranges if b > a]
         if not spans or B == 0:
             return counts
-        lib = _lib.lib()
-        ws = torch.empty((max(lib.regcn_hyp_ce_workspace_bytes(B, b - a) for a, b in spans) + 3) // 4, device=dev)
+        N = cand.shape[0]
+        ws = torch.empty((_lib.lib().regcn_hyp_ce_workspace_bytes(B, N) + 3) // 4, device=dev)
         sc = _scalar(scale if scale is not None else 1.0, q)
         mg = _scalar(margin, q)
         flags = _lib.SCORE_RAW_SCALE if raw_scale else 0
         f = _lib.fptr
-        for k, (a, b) in enumerate(spans):
-            _lib.call("regcn_hyp_rank_fused_f32", f(q, "query"), f(cand[a:b], "candidates"),
-                      f(bias[a:b]) if bias is not None else None, f(sc), f(mg), f(ts, "threshold"), B, b - a, d,
-                      float(c), flags, f(ws), int(k > 0), _lib.iptr(counts), _lib.stream())
+        for k in range(0, len(spans), 8):
+            part = spans[k:k + 8]
+            rng = (ctypes.c_int32 * (2 * len(part)))(*[v for ab in part for v in ab])
+            _lib.call("regcn_hyp_rank_fused_f32", f(q, "query"), f(cand, "candidates"), f(bias), f(sc), f(mg),
+                      f(ts, "threshold"), B, N, d, float(c), flags, rng, len(part), f(ws), int(k > 0),
+                      _lib.iptr(counts), _lib.stream())
         return counts
 
     def filter_hits(self, q, cand, bias, c, ts, filt_ptr, filt_idx, **kw):

@@ -356,12 +356,14 @@ def test_score_shapes_vs_oracle(B, N, d):
 
 
 @pytest.mark.parametrize("B,N,d,ranges", [(1, 1, 4, [(0, 1)]), (5, 700, 12, [(0, 300), (300, 301), (500, 700)]),
-                                           (130, 3000, 200, [(0, 1000), (1000, 3000)]), (1024, 20000, 256, [(0, 20000)])])
+                                           (130, 3000, 200, [(0, 1000), (1000, 3000)]), (1024, 20000, 256, [(0, 20000)]),
+                                           (256, 5000, 200, [(k * 500, k * 500 + 40 * k + 1) for k in range(10)])])
 def test_fused_rank_count_matches_score_matrix(B, N, d, ranges):
     """regcn_hyp_rank_fused_f32 (score + count-greater in one launch, no score matrix) against
     regcn_hyp_score_f32 + the count over the score matrix: equal counts for thresholds at
     existing scores (ties at the threshold are not counted: strictly greater) and in between,
-    over several candidate ranges accumulated (CandidateShard.fused_counts), with a per-
+    over several candidate ranges (one launch for up to 8, accumulated past that:
+    CandidateShard.fused_counts), with a per-
     candidate bias and the raw score scale; filter_hits: the listed answers above the threshold."""
     from regcn_amd.hyperbolic_decoder import _chunked_hyperbolic_dist_score as sc
     from regcn_amd.parallel import CandidateShard
