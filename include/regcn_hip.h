@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 10
+#define REGCN_ABI_VERSION 11
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -271,6 +271,15 @@ typedef struct regcn_layer_desc {
   const float* gate_w;   /* a cell's first layer: also the timestep's time-gate pre-activation */
   float* gate_out;       /*   clamp(x) @ gate_w (kp-packed W_g) of every row -> gate_out (V x d) */
   const float* step_tw;  /* the step layer: those rows (else the gate product runs in-kernel) */
+  /* regcn_layer_rowtail_* gather, union / euclid (0 elsewhere): tiles [0, crel_tiles) take the
+   * relation half sum_e w_e rel[t_e] = sum_t C[row][t] rel[t] as one [16 x R2] @ [R2 x d] MFMA
+   * product per tile, reading the relation table once per tile instead of once per item
+   * (hyperbolic_layers.py:222-240 by linearity) */
+  int32_t crel_tiles;
+  const int32_t* crel_item_src; /* those tiles' items in (row, type) order (item_type_order) */
+  const int32_t* crel_item_tl;
+  const float* rel_t;    /* 16 ceil(d / 16) x kpad: rel transposed, zero padded, kpad = R2 rounded up to 16 */
+  int32_t n_types;       /* R2 <= 512 */
 } regcn_layer_desc;
 int regcn_layer_f32(const regcn_layer_desc* desc, void* stream);
 
@@ -730,6 +739,15 @@ int regcn_snapshot_item_src_order_i32(int32_t V, int32_t n_tiles, int32_t n_item
                                       const int32_t* item_ptr, const int32_t* item_src, const int32_t* item_tl,
                                       int32_t* out_src, int32_t* out_tl, void* workspace, size_t ws_bytes,
                                       void* stream);
+/* The same items with each row's items in ascending relation-type order (stable; workspace:
+ * regcn_item_src_order_workspace_bytes(n_items, V)).  For regcn_layer_desc.item_crel: a row's
+ * same-type items are adjacent, so the gather sums their weights per (row, type) and applies the
+ * relation rows as one [16 x R2] @ [R2 x d] product per tile (hyperbolic_layers.py:222-240 by
+ * linearity: sum_e w_e rel[t_e] = sum_t (sum_{e: t_e = t} w_e) rel[t]). */
+int regcn_snapshot_item_type_order_i32(int32_t V, int32_t R2, int32_t n_tiles, int32_t n_items, const int32_t* tiles,
+                                       const int32_t* item_ptr, const int32_t* item_src, const int32_t* item_tl,
+                                       int32_t* out_src, int32_t* out_tl, void* workspace, size_t ws_bytes,
+                                       void* stream);
 size_t regcn_snapshot_workspace_bytes(int64_t T, int32_t V, int32_t R);
 int64_t regcn_snapshot_capacity(int32_t what, int64_t T, int32_t V, int32_t R, int32_t chunk_edges);
 int regcn_snapshot_csr_i32(const regcn_snapshot_desc* desc, void* stream);

@@ -430,6 +430,11 @@ static int layer_args(const regcn_layer_desc* g, LayerArgs& a) {
   a.r_next = g->r_next;
   a.fuse_step = g->fuse_step;
   a.item_src_runs = g->item_src_runs;
+  a.crel_tiles = g->crel_tiles;
+  a.crel_item_src = g->crel_item_src;
+  a.crel_item_tl = g->crel_item_tl;
+  a.rel_t = g->rel_t;
+  a.n_types = g->n_types;
   if (a.item_src_runs && a.agg_mode != REGCN_AGG_UNION && a.agg_mode != REGCN_AGG_EUCLID)
     return set_error(REGCN_EINVAL, "item_src_runs applies to the union / euclid gathers only");
   if (g->fuse_step) {
@@ -670,6 +675,7 @@ int regcn_hyp_rank_fused_f32(const float* q, const float* cand, const float* bia
   }
   a.n_rng = n_ranges ? k : 0;
   a.rng_tile[a.n_rng] = tiles;
+  a.rng_total = tiles;
   if (n_ranges && !k) a.N = 0;  // every range empty
   a.thr = threshold;
   a.part = (float*)workspace;
@@ -745,6 +751,12 @@ int regcn_snapshot_item_src_order_i32(int32_t V, int32_t n_tiles, int32_t n_item
                                       int32_t* out_src, int32_t* out_tl, void* workspace, size_t ws_bytes, void* s) {
   return item_src_order(V, n_tiles, n_items, tiles, item_ptr, item_src, item_tl, out_src, out_tl, workspace, ws_bytes,
                         ST(s));
+}
+int regcn_snapshot_item_type_order_i32(int32_t V, int32_t R2, int32_t n_tiles, int32_t n_items, const int32_t* tiles,
+                                       const int32_t* item_ptr, const int32_t* item_src, const int32_t* item_tl,
+                                       int32_t* out_src, int32_t* out_tl, void* workspace, size_t ws_bytes, void* s) {
+  return item_type_order(V, R2, n_tiles, n_items, tiles, item_ptr, item_src, item_tl, out_src, out_tl, workspace,
+                         ws_bytes, ST(s));
 }
 size_t regcn_row_src_order_workspace_bytes(int32_t E, int32_t V) { return row_src_ws_bytes(E, V); }
 int regcn_snapshot_row_src_order_i32(int32_t V, int32_t E, const int32_t* rowptr, const int32_t* col_src, int32_t* out_src,

@@ -946,10 +946,14 @@ __global__ __launch_bounds__(BT) void k_item_rowpos(const int* __restrict__ tile
 
 size_t item_src_ws_bytes(int n_items, int V) { return row_type_ws_bytes(n_items, V, 2); }
 
-// Stable LSD radix sort of the items by source, then stably by row position: each row's
-// items in ascending source order (ties keep CSR order), rows and tiles unchanged.
-int item_src_order(int V, int n_tiles, int n_items, const int* tiles, const int* item_ptr, const int* item_src,
-                   const int* item_tl, int* out_src, int* out_tl, void* workspace, size_t ws_bytes, hipStream_t st) {
+// Stable LSD radix sort of the items by a key, then stably by row position: each row's items in
+// ascending key order (ties keep CSR order), rows and tiles unchanged.  by_type = 0: the key is
+// the source id (a row's duplicate sources adjacent, regcn_layer_desc.item_src_runs); 1: the
+// item_tl word (type << 4 | local row; within a row: the relation type), a row's same-type
+// items adjacent (regcn_layer_desc.item_crel: their weights summed per (row, type)).
+static int item_order(int V, int key_bits, int by_type, int n_tiles, int n_items, const int* tiles,
+                      const int* item_ptr, const int* item_src, const int* item_tl, int* out_src, int* out_tl,
+                      void* workspace, size_t ws_bytes, hipStream_t st) {
   if (V <= 0 || n_tiles < 0 || n_items < 0) return set_error(REGCN_EINVAL, "bad item order sizes");
   if (n_items == 0) return 0;
   if (!tiles || !item_ptr || !item_src || !item_tl || !out_src || !out_tl) return set_error(REGCN_EINVAL, "null pointer");
@@ -961,10 +965,10 @@ int item_src_order(int V, int n_tiles, int n_items, const int* tiles, const int*
   hipLaunchKernelGGL(k_item_rowpos, dim3(std::min<unsigned>(blocks(n_tiles, 4), 65536)), dim3(BT), 0, st, tiles,
                      item_ptr, item_tl, n_tiles, rowpos);
   if ((rc = check_launch("k_item_rowpos"))) return rc;
-  hipLaunchKernelGGL(k_iota_keys, dim3(blocks(n_items)), dim3(BT), 0, st, item_src, n_items, (uint32_t*)(ws + L.k0),
-                     (uint32_t*)(ws + L.v0));
+  hipLaunchKernelGGL(k_iota_keys, dim3(blocks(n_items)), dim3(BT), 0, st, by_type ? item_tl : item_src, n_items,
+                     (uint32_t*)(ws + L.k0), (uint32_t*)(ws + L.v0));
   bool second;
-  if ((rc = radix_sort(ws, L, n_items, bitlen((uint64_t)V - 1), true, &second, st))) return rc;
+  if ((rc = radix_sort(ws, L, n_items, key_bits, true, &second, st))) return rc;
   hipLaunchKernelGGL(k_row_of, dim3(blocks(n_items)), dim3(BT), 0, st, rowpos,
                      (const uint32_t*)(ws + (second ? L.v1 : L.v0)), n_items, (uint32_t*)(ws + L.k0),
                      (uint32_t*)(ws + L.v0));
@@ -973,6 +977,21 @@ int item_src_order(int V, int n_tiles, int n_items, const int* tiles, const int*
   hipLaunchKernelGGL(k_permute2, dim3(blocks(n_items)), dim3(BT), 0, st, (const uint32_t*)(ws + (second ? L.v1 : L.v0)),
                      n_items, item_src, item_tl, out_src, out_tl);
   return check_launch("k_permute2");
+}
+
+int item_src_order(int V, int n_tiles, int n_items, const int* tiles, const int* item_ptr, const int* item_src,
+                   const int* item_tl, int* out_src, int* out_tl, void* workspace, size_t ws_bytes, hipStream_t st) {
+  if (V <= 0) return set_error(REGCN_EINVAL, "bad item order sizes");
+  return item_order(V, bitlen((uint64_t)V - 1), 0, n_tiles, n_items, tiles, item_ptr, item_src, item_tl, out_src,
+                    out_tl, workspace, ws_bytes, st);
+}
+
+int item_type_order(int V, int R2, int n_tiles, int n_items, const int* tiles, const int* item_ptr,
+                    const int* item_src, const int* item_tl, int* out_src, int* out_tl, void* workspace,
+                    size_t ws_bytes, hipStream_t st) {
+  if (R2 <= 0 || R2 >= (1 << 27)) return set_error(REGCN_EINVAL, "bad relation count %d", R2);
+  return item_order(V, bitlen((uint64_t)R2 * 16 - 1), 1, n_tiles, n_items, tiles, item_ptr, item_src, item_tl,
+                    out_src, out_tl, workspace, ws_bytes, st);
 }
 
 // Stable LSD radix sort by source, then stably by destination row: each row's sources in

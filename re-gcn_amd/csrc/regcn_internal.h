@@ -58,6 +58,9 @@ int row_type_order(int V, int E, int R2, const int* rowptr, const int* col_src, 
 size_t item_src_ws_bytes(int n_items, int V);
 int item_src_order(int V, int n_tiles, int n_items, const int* tiles, const int* item_ptr, const int* item_src,
                    const int* item_tl, int* out_src, int* out_tl, void* ws, size_t ws_bytes, hipStream_t st);
+int item_type_order(int V, int R2, int n_tiles, int n_items, const int* tiles, const int* item_ptr,
+                    const int* item_src, const int* item_tl, int* out_src, int* out_tl, void* workspace,
+                    size_t ws_bytes, hipStream_t st);
 size_t row_src_ws_bytes(int E, int V);
 int row_src_order(int V, int E, const int* rowptr, const int* col_src, int* out_src, void* ws, size_t ws_bytes,
                   hipStream_t st);
@@ -127,6 +130,13 @@ struct LayerArgs {
   int item_src_runs;        // union / euclid items in (row, source) order: one x row per source run
   const float* w_gate;      // rowtail, a cell's first layer: W_g (kp-packed) ...
   float* gate_out;          // ... and the V x d rows clamp(x) @ W_g it writes for the timestep
+  // rowtail gather, union / euclid: tiles [0, crel_tiles) sum their relation weights per (row,
+  // type) and apply the relation rows as one MFMA product per tile (rowtail.hip k_gather_crel)
+  int crel_tiles;
+  const int* crel_item_src;  // those tiles' items in (row, type) order
+  const int* crel_item_tl;
+  const float* rel_t;        // ceil(d / 16) 16 x crel_kpad(n_types): rel transposed, zero padded
+  int n_types;               // R2 <= 512
 };
 
 struct ScoreArgs {
@@ -158,7 +168,7 @@ struct ScoreArgs {
   // candidate row ranges (n_rng > 0): the candidates are rows [rng_start[r], rng_start[r] +
   // rng_len[r]) of e, tiled range by range (range r's tiles [rng_tile[r], rng_tile[r + 1])),
   // so one launch covers a rank's owner ranges; n_rng == 0: rows [0, N)
-  int n_rng;
+  int n_rng, rng_total;  // rng_total = rng_tile[n_rng] (device code indexes the arrays statically only)
   int rng_start[8], rng_len[8], rng_tile[9];
 };
 

@@ -85,6 +85,202 @@ __global__ __launch_bounds__(NTHR) void k_gather_agg(LayerArgs p, float* __restr
   }
 }
 
+// ---------------------------------------------------------------- relation half as a product
+// Tiles [0, crel_tiles) of a union / euclid gather (item_crel): the tile's items in (row, type)
+// order (regcn_snapshot_item_type_order_i32).  By linearity (hyperbolic_layers.py:222-240)
+//   sum_e w_e (x[src_e] + rel[t_e]) = sum_e w_e x[src_e] + sum_t C[row][t] rel[t],
+//   C[row][t] = sum of w_e over the row's type-t items,
+// so the per-item loads are the source rows only; the weights of a row's same-type items are
+// summed in registers (a segmented lane scan per 64-item window, the window's last run carried
+// into the next) into an LDS matrix C[16][n_types], and the relation rows enter as one
+// [16 x n_types] @ [n_types x d] MFMA product per tile: the relation table is read once per tile
+// instead of once per item.  Deterministic: a wave stores the sum of every run it owns (plain
+// stores: a (row, type) run lies in one wave's item range but for its pieces at range
+// boundaries); each wave's FIRST run -- possibly the tail of the previous wave's last run -- is
+// parked and added by one thread in wave order after the barrier.
+constexpr int CREL_MAX_TYPES = 512;
+
+__host__ __device__ inline int crel_kpad(int n_types) { return (n_types + 15) & ~15; }
+__host__ __device__ inline int crel_ld(int n_types) { return crel_kpad(n_types) + 4; }  // C row stride (floats)
+__host__ __device__ inline size_t crel_lds_bytes(int d, int n_types) {
+  return (size_t)((TM + NWAVE - 1) * tile_lda(d) + 32 + 2 * NWAVE + TM * crel_ld(n_types)) * 4;
+}
+
+template <int AGG>
+__global__ __launch_bounds__(NTHR) void k_gather_crel(LayerArgs p, float* __restrict__ out, int tile0) {
+  extern __shared__ float lds[];
+  const int tile = tile0 + blockIdx.x;
+  const int d = p.d, lda = tile_lda(d);
+  float* part = lds;
+  int* trow = reinterpret_cast<int*>(lds + (TM + NWAVE - 1) * lda);
+  int* tmask = trow + TM;
+  int* bkey = reinterpret_cast<int*>(lds + (TM + NWAVE - 1) * lda + 32);  // parked first runs
+  float* bval = reinterpret_cast<float*>(bkey + NWAVE);
+  float* cl = lds + (TM + NWAVE - 1) * lda + 32 + 2 * NWAVE;
+  const int cld = crel_ld(p.n_types), kpad = crel_kpad(p.n_types);
+  const int start = p.tiles[2 * tile], count = p.tiles[2 * tile + 1];
+  const int lane = threadIdx.x & 63, w = wave_id();
+  if (threadIdx.x < TM) trow[threadIdx.x] = p.rows[start + ((int)threadIdx.x < count ? threadIdx.x : 0)];
+  if (lane == 0) bkey[w] = -1;
+  for (int i = threadIdx.x; i < TM * cld; i += NTHR) cl[i] = 0.f;
+  __syncthreads();
+  const int lrow = trow[min(lane, TM - 1)];
+  const int rdeg = p.rowptr[lrow + 1] - p.rowptr[lrow];
+  const float rnorm = p.norm[lrow];
+  // ---- the items: source rows per item, relation weights per (row, type) run (16 source rows
+  // in flight per wave: no relation rows in the loop, and 3 workgroups per CU for the LDS C)
+  constexpr int EB = 16;
+  const int col = lane * 4, colc = min(col, d - 4);
+  const bool active = col < d;
+  const int i0 = p.item_ptr[tile], n_items = p.item_ptr[tile + 1] - i0;
+  const int ib = i0 + (n_items * w) / NWAVE, ie = i0 + (n_items * (w + 1)) / NWAVE;
+  const f4 zero = {0.f, 0.f, 0.f, 0.f};
+  int cur = -1;
+  unsigned mask = 0;
+  f4 acc = zero;
+  auto flush = [&]() {
+    if (cur >= 0) {
+      float* dst = part + (cur + w) * lda;
+      if (active) {
+        dst[col] = acc.x;
+        dst[col + 1] = acc.y;
+        dst[col + 2] = acc.z;
+        dst[col + 3] = acc.w;
+      }
+      mask |= 1u << cur;
+    }
+  };
+  auto take = [&](int li) {
+    if (li != cur) {
+      flush();
+      cur = li;
+      acc = zero;
+    }
+  };
+  const uint32_t xoff = (uint32_t)colc * 4u;
+  bool first_pending = true;  // the wave's first run is parked, not stored
+  int ck = -1;                // the carried (open) run of the previous window: key, weight sum
+  float cw = 0.f;
+  auto emit1 = [&](int key, float v) {  // one run's sum, from lane 0
+    if (first_pending) {
+      if (lane == 0) bkey[w] = key, bval[w] = v;
+      first_pending = false;
+    } else if (lane == 0) {
+      cl[(key >> 16) * cld + (key & 0xffff)] = v;
+    }
+  };
+  for (int t0 = ib; t0 < ie; t0 += 64) {
+    const int n = min(64, ie - t0);
+    const int t = t0 + min(lane, n - 1);
+    const int my_s = p.item_src[t];
+    const int tl = p.item_tl[t];
+    const int my_t = tl >> 4, my_i = tl & 15;
+    float my_w = 1.f;
+    if (AGG == AGG_UNION) my_w = expf(-p.gamma * fabsf(p.radius[my_s] - p.radius[trow[my_i]]));
+    const bool valid = lane < n;
+    const int key = (my_i << 16) | my_t;
+    const int key0 = __builtin_amdgcn_readfirstlane(key);
+    if (ck >= 0 && key0 != ck) {  // the carried run ended with the last window
+      emit1(ck, cw);
+      ck = -1;
+    }
+    float v = valid ? my_w : 0.f;
+    if (lane == 0 && ck >= 0) v += cw;  // ... or continues here
+    const int pk = __shfl_up(key, 1);
+    const uint64_t heads = __ballot(valid && (lane == 0 || key != pk)) | 1ull;
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    const int sstart = 63 - __builtin_clzll(heads & upto);
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {  // inclusive segmented sum, fixed order
+      const float u = __shfl_up(v, off);
+      if (lane - off >= sstart) v += u;
+    }
+    uint64_t ends = __ballot(valid && lane != n - 1 && ((heads >> ((lane + 1) & 63)) & 1ull));
+    if (first_pending && ends) {  // the lowest closed run is the wave's first
+      const int l0 = __builtin_ctzll(ends);
+      const float v0 = __shfl(v, l0);
+      const int k0 = __shfl(key, l0);
+      if (lane == 0) bkey[w] = k0, bval[w] = v0;
+      ends &= ends - 1;
+      first_pending = false;
+    }
+    if ((ends >> lane) & 1ull) cl[my_i * cld + my_t] = v;
+    ck = __shfl(key, n - 1);
+    cw = __shfl(v, n - 1);
+    // the source half, EB rows in flight per wave
+    for (int j = 0; j < n; j += EB) {
+      const int nv = n - j;
+      f4 xs[EB];
+#pragma unroll
+      for (int u = 0; u < EB; ++u) xs[u] = row_load4(p.x + (int64_t)rl(my_s, j + u) * d, xoff);
+#pragma unroll
+      for (int u = 0; u < EB; ++u) {
+        if (u < nv) {
+          take(rl(my_i, j + u));
+          acc += rlf(my_w, j + u) * xs[u];
+        }
+      }
+    }
+  }
+  if (ck >= 0) emit1(ck, cw);
+  flush();
+  if (lane == 0) tmask[w] = (int)mask;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // the parked first runs, in wave order
+#pragma unroll
+    for (int w2 = 0; w2 < NWAVE; ++w2)
+      if (bkey[w2] >= 0) cl[(bkey[w2] >> 16) * cld + (bkey[w2] & 0xffff)] += bval[w2];
+  }
+  __syncthreads();
+  // ---- the relation half: C[16 x kpad] @ rel_t^T, k-permuted operands (16-deep block b, MFMA
+  // step e: k = 16 b + 4 (lane / 16) + e for both A and B), wave w: column tiles w + NWAVE j
+  {
+    const int nt = (d + 15) >> 4, q = lane >> 4, r16 = lane & 15;
+    const float* arow = cl + r16 * cld + 4 * q;
+    constexpr int JMAX = (MAX_D / 16 + NWAVE - 1) / NWAVE;
+    f4 racc[JMAX];
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j) racc[j] = zero;
+    for (int b = 0; b < kpad / 16; ++b) {
+      const f4 a = *reinterpret_cast<const f4*>(arow + 16 * b);
+#pragma unroll
+      for (int j = 0; j < JMAX; ++j) {
+        const int ct = w + NWAVE * j;
+        if (ct < nt) {  // wave-uniform
+          const f4 bv = *reinterpret_cast<const f4*>(p.rel_t + (int64_t)(16 * ct + r16) * kpad + 16 * b + 4 * q);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) racc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], bv[e], racc[j], 0, 0, 0);
+        }
+      }
+    }
+    // add row i's relation sum into the slot its first writing wave used
+#pragma unroll
+    for (int j = 0; j < JMAX; ++j) {
+      const int ct = w + NWAVE * j, c = 16 * ct + r16;
+      if (ct >= nt || c >= d) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * q + r;
+        int wf = -1;
+#pragma unroll
+        for (int w2 = NWAVE - 1; w2 >= 0; --w2)
+          if ((tmask[w2] >> i) & 1) wf = w2;
+        if (i < count && wf >= 0) part[(i + wf) * lda + c] += racc[j][r];
+      }
+    }
+  }
+  __syncthreads();
+  constexpr int RPW = TM / NWAVE;
+  f4 o[RPW], pre[RPW];
+  bool heavy[RPW];
+  tile_finish_rows<AGG>(p, part, lda, trow, count, tmask, rdeg, rnorm, o, pre, heavy);
+#pragma unroll
+  for (int q2 = 0; q2 < RPW; ++q2) {
+    const int i = w + NWAVE * q2;
+    if (i < count && !heavy[q2] && col < d) *reinterpret_cast<f4*>(out + (int64_t)trow[i] * d + col) = o[q2];
+  }
+}
+
 // --------------------------------------------------------------------------- 64-row tail
 constexpr int RT_ROWS = 64;
 
@@ -723,10 +919,30 @@ int layer_rowtail_part(const LayerArgs& a, float* agg, int which, int lo, int hi
       return set_error(REGCN_EINVAL, "lorentz gather needs weights and d %% num_bases == 0");
     LayerArgs g = a;
     g.agg = agg;  // hub rows: read back (skipped) by the finish
+    if ((mode == AGG_UNION || mode == AGG_EUCLID) && a.crel_tiles > 0 && t0 < a.crel_tiles) {
+      if (!a.crel_item_src || !a.crel_item_tl || !a.rel_t) return set_error(REGCN_EINVAL, "crel needs its items and rel_t");
+      if (a.n_types <= 0 || a.n_types > CREL_MAX_TYPES)
+        return set_error(REGCN_ENOTSUP, "crel takes 1..%d relation types (got %d)", CREL_MAX_TYPES, a.n_types);
+      if (a.crel_tiles > a.n_pos_tiles) return set_error(REGCN_EINVAL, "crel_tiles > n_pos_tiles");
+      const int tc = std::min(t1, a.crel_tiles);
+      LayerArgs c = g;
+      c.item_src = a.crel_item_src;
+      c.item_tl = a.crel_item_tl;
+      const size_t lds_c = crel_lds_bytes(a.d, a.n_types);
+      if (mode == AGG_UNION) {
+        if (!a.radius) return set_error(REGCN_EINVAL, "union gather needs radius");
+        hipLaunchKernelGGL((k_gather_crel<AGG_UNION>), dim3(tc - t0), dim3(NTHR), lds_c, st, c, agg, t0);
+      } else {
+        hipLaunchKernelGGL((k_gather_crel<AGG_EUCLID>), dim3(tc - t0), dim3(NTHR), lds_c, st, c, agg, t0);
+      }
+      const int rc = check_launch("k_gather_crel");
+      if (rc) return rc;
+      t0 = tc;
+    }
     const int s = mode == AGG_LORENTZ ? a.d / a.nb : 1;
     const bool gen = mode == AGG_LORENTZ && s != 1 && s != 2 && s != 4;
     const size_t lds = (size_t)(((TM + NWAVE - 1) * tile_lda(a.d) + 32) + (gen ? NWAVE * MAX_D : 0)) * 4;
-    switch (mode) {
+    if (t1 > t0) switch (mode) {
       case AGG_UNION: launch_gather<AGG_UNION, 1>(g, agg, t0, t1, lds, st); break;
       case AGG_EUCLID: launch_gather<AGG_EUCLID, 1>(g, agg, t0, t1, lds, st); break;
       default:

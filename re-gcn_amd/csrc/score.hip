@@ -462,7 +462,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   };
   stamp(0);
   const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
-  const int nbn = p.n_rng ? p.rng_tile[p.n_rng] : (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
+  const int nbn = p.n_rng ? p.rng_total : (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
   // candidate tile t -> its first row and valid rows (row ranges: a tile never spans two)
   auto tile_rows = [&](int t, int& row0, int& nvalid) {
     if (!p.n_rng) {
@@ -470,11 +470,14 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
       nvalid = min(SN, p.N - row0);
       return;
     }
-    int r = 0;
-    while (r + 1 < p.n_rng && t >= p.rng_tile[r + 1]) ++r;
-    const int off = (t - p.rng_tile[r]) * SN;
-    row0 = p.rng_start[r] + off;
-    nvalid = min(SN, p.rng_len[r] - off);
+    // static indices only (a dynamic index would put the argument struct in scratch)
+    int st = p.rng_start[0], tb = p.rng_tile[0], ln = p.rng_len[0];
+#pragma unroll
+    for (int r = 1; r < SCORE_MAX_RANGES; ++r)
+      if (r < p.n_rng && t >= p.rng_tile[r]) st = p.rng_start[r], tb = p.rng_tile[r], ln = p.rng_len[r];
+    const int off = (t - tb) * SN;
+    row0 = st + off;
+    nvalid = min(SN, ln - off);
   };
   const int S = nblk / (8 * nbq);
   const int xcd = blk & 7, rk = blk >> 3;
@@ -650,7 +653,7 @@ __device__ __forceinline__ void score_ws_body(ScoreArgs p, const int blk, const 
   const bool mfma_wave = wv < 4;  // wave-uniform role
   const int grpw = wv & 3;        // the 32-query group of this wave (MFMA wave and its epilogue wave)
   const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
-  const int nbn = p.n_rng ? p.rng_tile[p.n_rng] : (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
+  const int nbn = p.n_rng ? p.rng_total : (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
   // candidate tile t -> its first row and valid rows (row ranges: a tile never spans two)
   auto tile_rows = [&](int t, int& row0, int& nvalid) {
     if (!p.n_rng) {
@@ -658,11 +661,14 @@ __device__ __forceinline__ void score_ws_body(ScoreArgs p, const int blk, const 
       nvalid = min(SN, p.N - row0);
       return;
     }
-    int r = 0;
-    while (r + 1 < p.n_rng && t >= p.rng_tile[r + 1]) ++r;
-    const int off = (t - p.rng_tile[r]) * SN;
-    row0 = p.rng_start[r] + off;
-    nvalid = min(SN, p.rng_len[r] - off);
+    // static indices only (a dynamic index would put the argument struct in scratch)
+    int st = p.rng_start[0], tb = p.rng_tile[0], ln = p.rng_len[0];
+#pragma unroll
+    for (int r = 1; r < SCORE_MAX_RANGES; ++r)
+      if (r < p.n_rng && t >= p.rng_tile[r]) st = p.rng_start[r], tb = p.rng_tile[r], ln = p.rng_len[r];
+    const int off = (t - tb) * SN;
+    row0 = st + off;
+    nvalid = min(SN, ln - off);
   };
   const int S = nblk / (8 * nbq);
   const int xcd = blk & 7, rk = blk >> 3;
@@ -1070,7 +1076,7 @@ int rank_fused(ScoreArgs& a, int accumulate, int* counts, hipStream_t st) {
   if (a.B > 0 && (!a.q || !a.thr || !counts || !a.part)) return set_error(REGCN_EINVAL, "null pointer");
   if (a.B > 0 && a.N > 0 && !a.e) return set_error(REGCN_EINVAL, "null candidates");
   if (a.B == 0) return 0;
-  const int nbn = a.n_rng ? a.rng_tile[a.n_rng] : (a.N + SN - 1) / SN;
+  const int nbn = a.n_rng ? a.rng_total : (a.N + SN - 1) / SN;
   if (nbn == 0) {  // nothing to count: counts stay (accumulate) or become 0
     if (!accumulate) {
       hipLaunchKernelGGL(k_count_combine, dim3((a.B + 3) / 4), dim3(256), 0, st, a.part, a.B, 0, 0, counts);

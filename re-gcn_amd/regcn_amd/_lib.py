@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REGCN_HIP_LIB") or os.path.join(_HERE, "libregcn_hip.so")  # override: A/B builds
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -97,6 +97,7 @@ _SIGS = {
     "regcn_item_src_order_workspace_bytes": [_c_int, _c_int],
     "regcn_snapshot_item_src_order_i32": [_c_int, _c_int, _c_int, P, P, P, P, P, P, P, _c_sz, P],
     "regcn_snapshot_row_src_order_i32": [_c_int, _c_int, P, P, P, P, _c_sz, P],
+    "regcn_snapshot_item_type_order_i32": [_c_int, _c_int, _c_int, _c_int, P, P, P, P, P, P, P, _c_sz, P],
     "regcn_rowmap_bwd_f32": [_c_int, P, P, P, _c_i64, _c_int, _c_f, P, P, P],
     "regcn_union_aggregate_bwd_f32": [P, _c_f, P],
     "regcn_lorentz_sum_raw_f32": [P, P, P, P, P, P, _c_int, _c_int, _c_int, _c_f, P, P, P],
@@ -132,6 +133,7 @@ class LayerDesc(ctypes.Structure):
         ("step_layer_norm", _c_int), ("step_residual", _c_int), ("step_c_radius", _c_f), ("step_h_out", P),
         ("step_x_out", P), ("step_r_out", P), ("trace", P), ("item_src_runs", _c_int),
         ("gate_w", P), ("gate_out", P), ("step_tw", P),
+        ("crel_tiles", _c_int), ("crel_item_src", P), ("crel_item_tl", P), ("rel_t", P), ("n_types", _c_int),
     ]
 
 

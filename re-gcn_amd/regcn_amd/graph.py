@@ -347,6 +347,32 @@ class SnapshotGraph:
         self.__dict__["_item_src"] = t
         return t
 
+    def item_type_cols(self):
+        """(item_src, item_tl) with each row's inline items in ascending relation-type order
+        (regcn_snapshot_item_type_order_i32), built on first use and cached: with
+        regcn_layer_desc.item_crel the gather sums a row's same-type item weights and applies the
+        relation rows as one MFMA product per tile."""
+        t = self.__dict__.get("_item_type")
+        if t is not None:
+            return t
+        from . import _lib
+        wk = self.work()
+        dev = wk["rowptr"].device
+        n_items, n_tiles = int(wk["item_src"].numel()), int(self.n_pos_tiles)
+        if n_items == 0:
+            t = (wk["item_src"], wk["item_tl"])
+        else:
+            ws = torch.empty(int(_lib.lib().regcn_item_src_order_workspace_bytes(n_items, self.num_nodes_)),
+                             dtype=torch.uint8, device=dev)
+            t = (torch.empty(n_items, dtype=torch.int32, device=dev), torch.empty(n_items, dtype=torch.int32, device=dev))
+            _lib.call("regcn_snapshot_item_type_order_i32", self.num_nodes_, 2 * self.num_rels, n_tiles, n_items,
+                      _lib.iptr(wk["tiles"]), _lib.iptr(wk["item_ptr"]), _lib.iptr(wk["item_src"]),
+                      _lib.iptr(wk["item_tl"]), _lib.iptr(t[0]), _lib.iptr(t[1]), ws.data_ptr(), ws.numel(),
+                      _lib.stream())
+            _lib.publish()
+        self.__dict__["_item_type"] = t
+        return t
+
     def work(self):
         """Device work lists (raises on a CPU graph: the HIP path has no CPU fallback)."""
         if self.dev is None:

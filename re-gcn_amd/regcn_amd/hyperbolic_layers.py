@@ -12,6 +12,7 @@ composition of the same layers; FHNN/HGAT encoders are outside this build's scop
 import ctypes
 import os
 
+import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -32,6 +33,9 @@ ROWTAIL_MIN_VIEW_ROWS = int(os.environ.get("REGCN_ROWTAIL_MIN_VIEW_ROWS", "1024"
 # ... in this many row chunks: the gather of chunk i + 1 runs on a side stream beside the tail of
 # chunk i (the L2-bound gather beside the MFMA-bound tail); 1 = one stream, no pipelining
 ROWTAIL_CHUNKS = int(os.environ.get("REGCN_ROWTAIL_CHUNKS", "1"))
+# Inline tiles with at least this many items take their relation half as one MFMA product per
+# tile (regcn_layer_desc.crel_tiles, csrc/rowtail.hip k_gather_crel); 0 disables
+CREL_MIN_ITEMS = int(os.environ.get("REGCN_CREL_MIN_ITEMS", "512"))
 # A rank's pipeline-chunk tails (owner partition) on this many streams (1: one after another)
 CHUNK_TAIL_STREAMS = int(os.environ.get("REGCN_CHUNK_TAIL_STREAMS", "2"))
 
@@ -287,6 +291,12 @@ def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c,
     desc.n_pos, desc.V, desc.d, desc.euclid = g.n_pos, n_rows, d, int(bool(euclid))
     desc.c = float(c)
     keep = []
+    cr = _crel(g, mode, rel) if g.n_pos else None
+    if cr is not None:  # the big tiles' relation half as one product per tile
+        desc.crel_tiles, desc.n_types = cr[0], rel.shape[0]
+        desc.crel_item_src, desc.crel_item_tl = a(cr[1][0], torch.int32), a(cr[1][1], torch.int32)
+        desc.rel_t = a(cr[2])
+        keep.append(cr[2])
     if step is None:
         desc.h_out, desc.x_next, desc.r_next = a(h), a(xn), a(rn)
         if gate is not None and gate.w_g_param is not None:
@@ -365,6 +375,40 @@ def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c,
     # `cur` here: x, r, rel and agg may be freed on `cur` afterwards (and, under capture, the
     # fork joins back into the captured stream)
     return h, xn, rn
+
+
+def _rel_t(rel):
+    """rel (R2 x d) transposed into the crel gather's B operand: 16 ceil(d / 16) rows of kpad =
+    R2 rounded up to 16 floats, zero padded; cached on the tensor per version (both layers of a
+    timestep read the same relation rows)."""
+    hit = getattr(rel, "_regcn_relt", None)
+    if hit is not None and hit[0] == rel._version:
+        return hit[1]
+    R2, d = rel.shape
+    t = torch.zeros(-(-d // 16) * 16, -(-R2 // 16) * 16, device=rel.device, dtype=torch.float32)
+    t[:d, :R2] = rel.t()
+    rel._regcn_relt = (rel._version, t)
+    return t
+
+
+def _crel(g, mode, rel):
+    """(tiles, (item_src, item_tl) in (row, type) order, rel_t) of the rowtail gather's leading
+    tiles with >= CREL_MIN_ITEMS items (tiles come in descending row-degree order: the big ones
+    first), or None: union / euclid, R2 <= 512, a whole snapshot (rank views keep per-item rows)."""
+    if CREL_MIN_ITEMS <= 0 or mode not in (_lib.AGG_UNION, _lib.AGG_EUCLID) or not hasattr(g, "item_type_cols"):
+        return None
+    if rel.shape[0] > 512 or not g.n_pos_tiles:
+        return None
+    hit = g.__dict__.get("_crel_tiles")
+    if hit is None or hit[0] != CREL_MIN_ITEMS:
+        if torch.cuda.is_current_stream_capturing():
+            return None  # no host copy inside a capture: this launch gathers per item
+        ip = g.work()["item_ptr"][:g.n_pos_tiles + 1].cpu().numpy()
+        small = np.nonzero(np.diff(ip) < CREL_MIN_ITEMS)[0]
+        hit = g.__dict__["_crel_tiles"] = (CREL_MIN_ITEMS, int(small[0]) if len(small) else len(ip) - 1)
+    if hit[1] == 0:
+        return None
+    return hit[1], g.item_type_cols(), _rel_t(rel)
 
 
 def _partial(g, d, device, lorentz=False):

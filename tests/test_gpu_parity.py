@@ -801,3 +801,53 @@ def test_pack_unpack_rows(d):
     assert torch.isnan(x2[~hit]).all() and torch.isnan(r2[~hit]).all()
     empty = torch.zeros(0, dtype=torch.int64, device=DEV)
     assert pack_rows(x, r, empty).shape == (0, d + 4)
+
+
+@pytest.mark.parametrize("skew", [False, True])
+@pytest.mark.parametrize("euclid", [False, True])
+def test_crel_gather_matches_per_item(skew, euclid, monkeypatch):
+    """The rowtail gather's relation half as one [16 x R2] @ [R2 x d] MFMA product per tile
+    (k_gather_crel: items in (row, type) order, per-(row, type) weight sums in LDS) against the
+    per-item relation rows (REGCN_CREL_MIN_ITEMS=0): the same agg rows within 1e-5 * max|ref|
+    (another fp32 association), on a snapshot whose leading tiles carry thousands of items;
+    skew: one relation type takes 90 % of the edges, so (row, type) runs cross the waves' item
+    ranges (the parked first runs).  Two runs are bitwise equal (no atomics)."""
+    from regcn_amd import _lib
+    from regcn_amd import graph as G
+    from regcn_amd import hyperbolic_layers as HL
+    V, R, d = 3000, 250, 200
+    rng = np.random.default_rng(7)
+    tr = _zipf_snapshot(V, R, 60000, 9)
+    if skew:
+        tr[:, 1] = np.where(rng.random(len(tr)) < 0.9, 3, tr[:, 1])
+    g = G.build_sub_graph(V, R, tr, True, DEV, tile_budget=4096)
+    wk = g.work()
+    ip = wk["item_ptr"][:g.n_pos_tiles + 1].cpu().numpy()
+    assert np.diff(ip).max() >= 2048
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    x = (torch.randn(V, d, device=DEV, generator=gen) * 0.3).contiguous()
+    r = (torch.rand(V, device=DEV, generator=gen) * 2.5 + 0.5).contiguous()
+    rel = (torch.randn(2 * R, d, device=DEV, generator=gen) * 0.3).contiguous()
+    mode = _lib.AGG_EUCLID if euclid else _lib.AGG_UNION
+    w = torch.randn(d, d, device=DEV, generator=gen) * 0.05
+
+    def gather(min_items):
+        monkeypatch.setattr(HL, "CREL_MIN_ITEMS", min_items)
+        g.__dict__.pop("_crel_tiles", None)
+        agg = HL._heavy_aggregate(mode, g, x, r, rel, None, 1, 0.15, 0.01)
+        if agg is None:
+            agg = torch.zeros_like(x)
+        h, xn, rn = HL._run_rowtail(mode, g, x, r, rel, None, 1, 0.15, w, w, w, 0.01, euclid, None, agg, None,
+                                    None, int(wk["rows"].shape[0]))
+        torch.cuda.synchronize()
+        return agg.clone(), h.clone()
+
+    a_ref, h_ref = gather(0)
+    a1, h1 = gather(512)
+    a2, h2 = gather(512)
+    assert g.__dict__["_crel_tiles"][1] > 0
+    rows = wk["rows"][:g.n_pos].long()
+    ref = a_ref[rows]
+    assert float((a1[rows] - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
+    assert torch.equal(a1, a2) and torch.equal(h1, h2)
+    assert float((h1 - h_ref).abs().max()) <= 1e-4
