@@ -120,6 +120,8 @@ __global__ __launch_bounds__(NTHR) void k_gather_crel(LayerArgs p, float* __rest
   const int cld = crel_ld(p.n_types), kpad = crel_kpad(p.n_types);
   const int start = p.tiles[2 * tile], count = p.tiles[2 * tile + 1];
   const int lane = threadIdx.x & 63, w = wave_id();
+  const int i0 = p.item_ptr[tile], n_items = p.item_ptr[tile + 1] - i0;
+  if (n_items == 0) return;  // a tile of hub rows only (pre-aggregated): nothing to write
   if (threadIdx.x < TM) trow[threadIdx.x] = p.rows[start + ((int)threadIdx.x < count ? threadIdx.x : 0)];
   if (lane == 0) bkey[w] = -1;
   for (int i = threadIdx.x; i < TM * cld; i += NTHR) cl[i] = 0.f;
@@ -132,7 +134,6 @@ __global__ __launch_bounds__(NTHR) void k_gather_crel(LayerArgs p, float* __rest
   constexpr int EB = 16;
   const int col = lane * 4, colc = min(col, d - 4);
   const bool active = col < d;
-  const int i0 = p.item_ptr[tile], n_items = p.item_ptr[tile + 1] - i0;
   const int ib = i0 + (n_items * w) / NWAVE, ie = i0 + (n_items * (w + 1)) / NWAVE;
   const f4 zero = {0.f, 0.f, 0.f, 0.f};
   int cur = -1;

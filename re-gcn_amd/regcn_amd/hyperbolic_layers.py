@@ -393,8 +393,9 @@ def _rel_t(rel):
 
 def _crel(g, mode, rel):
     """(tiles, (item_src, item_tl) in (row, type) order, rel_t) of the rowtail gather's leading
-    tiles with >= CREL_MIN_ITEMS items (tiles come in descending row-degree order: the big ones
-    first), or None: union / euclid, R2 <= 512, a whole snapshot (rank views keep per-item rows)."""
+    tiles up to the last of the first run of tiles with >= CREL_MIN_ITEMS items (tiles come in
+    descending row-degree order: the hub rows' item-less tiles, then the big ones), or None:
+    union / euclid, R2 <= 512, a whole snapshot (rank views keep per-item rows)."""
     if CREL_MIN_ITEMS <= 0 or mode not in (_lib.AGG_UNION, _lib.AGG_EUCLID) or not hasattr(g, "item_type_cols"):
         return None
     if rel.shape[0] > 512 or not g.n_pos_tiles:
@@ -403,9 +404,13 @@ def _crel(g, mode, rel):
     if hit is None or hit[0] != CREL_MIN_ITEMS:
         if torch.cuda.is_current_stream_capturing():
             return None  # no host copy inside a capture: this launch gathers per item
-        ip = g.work()["item_ptr"][:g.n_pos_tiles + 1].cpu().numpy()
-        small = np.nonzero(np.diff(ip) < CREL_MIN_ITEMS)[0]
-        hit = g.__dict__["_crel_tiles"] = (CREL_MIN_ITEMS, int(small[0]) if len(small) else len(ip) - 1)
+        big = np.diff(g.work()["item_ptr"][:g.n_pos_tiles + 1].cpu().numpy()) >= CREL_MIN_ITEMS
+        k = 0
+        if big.any():  # the big tiles follow the hub rows' tiles (no inline items: skipped in-kernel)
+            first = int(np.argmax(big))
+            rest = np.nonzero(~big[first:])[0]
+            k = first + (int(rest[0]) if len(rest) else len(big) - first)
+        hit = g.__dict__["_crel_tiles"] = (CREL_MIN_ITEMS, k)
     if hit[1] == 0:
         return None
     return hit[1], g.item_type_cols(), _rel_t(rel)

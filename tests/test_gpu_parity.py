@@ -850,4 +850,5 @@ def test_crel_gather_matches_per_item(skew, euclid, monkeypatch):
     ref = a_ref[rows]
     assert float((a1[rows] - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
     assert torch.equal(a1, a2) and torch.equal(h1, h2)
+    assert not torch.equal(a1[rows], ref)  # the product path ran (another fp32 association)
     assert float((h1 - h_ref).abs().max()) <= 1e-4
