@@ -99,6 +99,15 @@ __global__ __launch_bounds__(NTHR) void k_gather_agg(LayerArgs p, float* __restr
 // boundaries); each wave's FIRST run -- possibly the tail of the previous wave's last run -- is
 // parked and added by one thread in wave order after the barrier.
 constexpr int CREL_MAX_TYPES = 512;
+// source rows in flight per wave in the crel gather: 32 (default) or 16 (REGCN_CREL_EB)
+static int crel_eb() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("REGCN_CREL_EB");
+    v = e ? atoi(e) : 32;
+  }
+  return v;
+}
 
 __host__ __device__ inline int crel_kpad(int n_types) { return (n_types + 15) & ~15; }
 __host__ __device__ inline int crel_ld(int n_types) { return crel_kpad(n_types) + 4; }  // C row stride (floats)
@@ -106,8 +115,10 @@ __host__ __device__ inline size_t crel_lds_bytes(int d, int n_types) {
   return (size_t)((TM + NWAVE - 1) * tile_lda(d) + 32 + 2 * NWAVE + TM * crel_ld(n_types)) * 4;
 }
 
-template <int AGG>
-__global__ __launch_bounds__(NTHR) void k_gather_crel(LayerArgs p, float* __restrict__ out, int tile0) {
+template <int AGG, int EB>
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) void k_gather_crel(LayerArgs p,
+                                                                                          float* __restrict__ out,
+                                                                                          int tile0) {
   extern __shared__ float lds[];
   const int tile = tile0 + blockIdx.x;
   const int d = p.d, lda = tile_lda(d);
@@ -129,9 +140,8 @@ __global__ __launch_bounds__(NTHR) void k_gather_crel(LayerArgs p, float* __rest
   const int lrow = trow[min(lane, TM - 1)];
   const int rdeg = p.rowptr[lrow + 1] - p.rowptr[lrow];
   const float rnorm = p.norm[lrow];
-  // ---- the items: source rows per item, relation weights per (row, type) run (16 source rows
+  // ---- the items: source rows per item, relation weights per (row, type) run (EB source rows
   // in flight per wave: no relation rows in the loop, and 3 workgroups per CU for the LDS C)
-  constexpr int EB = 16;
   const int col = lane * 4, colc = min(col, d - 4);
   const bool active = col < d;
   const int ib = i0 + (n_items * w) / NWAVE, ie = i0 + (n_items * (w + 1)) / NWAVE;
@@ -930,11 +940,14 @@ int layer_rowtail_part(const LayerArgs& a, float* agg, int which, int lo, int hi
       c.item_src = a.crel_item_src;
       c.item_tl = a.crel_item_tl;
       const size_t lds_c = crel_lds_bytes(a.d, a.n_types);
+      const bool eb32 = crel_eb() == 32;
       if (mode == AGG_UNION) {
         if (!a.radius) return set_error(REGCN_EINVAL, "union gather needs radius");
-        hipLaunchKernelGGL((k_gather_crel<AGG_UNION>), dim3(tc - t0), dim3(NTHR), lds_c, st, c, agg, t0);
+        if (eb32) hipLaunchKernelGGL((k_gather_crel<AGG_UNION, 32>), dim3(tc - t0), dim3(NTHR), lds_c, st, c, agg, t0);
+        else hipLaunchKernelGGL((k_gather_crel<AGG_UNION, 16>), dim3(tc - t0), dim3(NTHR), lds_c, st, c, agg, t0);
       } else {
-        hipLaunchKernelGGL((k_gather_crel<AGG_EUCLID>), dim3(tc - t0), dim3(NTHR), lds_c, st, c, agg, t0);
+        if (eb32) hipLaunchKernelGGL((k_gather_crel<AGG_EUCLID, 32>), dim3(tc - t0), dim3(NTHR), lds_c, st, c, agg, t0);
+        else hipLaunchKernelGGL((k_gather_crel<AGG_EUCLID, 16>), dim3(tc - t0), dim3(NTHR), lds_c, st, c, agg, t0);
       }
       const int rc = check_launch("k_gather_crel");
       if (rc) return rc;

@@ -395,7 +395,8 @@ def _crel(g, mode, rel):
     """(tiles, (item_src, item_tl) in (row, type) order, rel_t) of the rowtail gather's leading
     tiles up to the last of the first run of tiles with >= CREL_MIN_ITEMS items (tiles come in
     descending row-degree order: the hub rows' item-less tiles, then the big ones), or None:
-    union / euclid, R2 <= 512, a whole snapshot (rank views keep per-item rows)."""
+    union / euclid, R2 <= 512 (a snapshot, or a rank's view of one: parallel.OwnerView /
+    HaloView build their own type-ordered items)."""
     if CREL_MIN_ITEMS <= 0 or mode not in (_lib.AGG_UNION, _lib.AGG_EUCLID) or not hasattr(g, "item_type_cols"):
         return None
     if rel.shape[0] > 512 or not g.n_pos_tiles:

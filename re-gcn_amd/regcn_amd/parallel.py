@@ -157,6 +157,30 @@ class OwnerView:
             self._dev = wk
         return self._dev
 
+    def item_type_cols(self):
+        """The view's inline items with each row's items in relation-type order (the crel
+        gather's lists, regcn_snapshot_item_type_order_i32 over the view's tiles), cached."""
+        t = self.__dict__.get("_item_type")
+        if t is None:
+            t = self.__dict__["_item_type"] = type_ordered_items(self.work(), self.n_pos_tiles,
+                                                                self.g.number_of_nodes(), 2 * self.g.num_rels)
+        return t
+
+
+def type_ordered_items(wk, n_tiles, V, R2):
+    """(item_src, item_tl) of work lists `wk` with each row's items in relation-type order."""
+    n_items = int(wk["item_src"].numel())
+    if n_items == 0:
+        return wk["item_src"], wk["item_tl"]
+    dev = wk["item_src"].device
+    ws = torch.empty(int(_lib.lib().regcn_item_src_order_workspace_bytes(n_items, V)), dtype=torch.uint8, device=dev)
+    out = (torch.empty(n_items, dtype=torch.int32, device=dev), torch.empty(n_items, dtype=torch.int32, device=dev))
+    _lib.call("regcn_snapshot_item_type_order_i32", V, R2, int(n_tiles), n_items, _lib.iptr(wk["tiles"]),
+              _lib.iptr(wk["item_ptr"]), _lib.iptr(wk["item_src"]), _lib.iptr(wk["item_tl"]), _lib.iptr(out[0]),
+              _lib.iptr(out[1]), ws.data_ptr(), ws.numel(), _lib.stream())
+    _lib.publish()
+    return out
+
 
 class HaloView:
     """A rank's OwnerView read through its halo numbering: every source id in the view's work
@@ -181,6 +205,16 @@ class HaloView:
                 wk["item_src"] = self.remap[wk["item_src"].long()].to(torch.int32)
             self._work = wk
         return self._work
+
+    def item_type_cols(self):
+        """The base view's type-ordered items with the sources remapped (the crel gather)."""
+        t = self.__dict__.get("_item_type")
+        if t is None:
+            src, tl = self.v.item_type_cols()
+            if src.numel():
+                src = self.remap[src.long()].to(torch.int32)
+            t = self.__dict__["_item_type"] = (src, tl)
+        return t
 
     def gather_cols(self, cs, ss):
         """(row/type order sources, row/source order sources) remapped (full-length copies;
