@@ -7,6 +7,8 @@
 #include "rowtile.h"
 
 namespace regcn {
+// per wave count (rowtile.h): units built with different REGCN_ROWTILE_WAVES never share a definition
+inline namespace REGCN_RT_CAT(rowtile_w, REGCN_ROWTILE_WAVES) {
 
 constexpr int GR4 = 4;  // k-blocks (16 k-steps each) of operands in flight per wave
 
@@ -303,4 +305,5 @@ __device__ __forceinline__ void gru_x_block(const RelGru2Args& p, int bx, int by
 }
 
 
+}  // inline namespace
 }  // namespace regcn

@@ -8,6 +8,8 @@
 #include "rowtile.h"
 
 namespace regcn {
+// per wave count (rowtile.h): units built with different REGCN_ROWTILE_WAVES never share a definition
+inline namespace REGCN_RT_CAT(rowtile_w, REGCN_ROWTILE_WAVES) {
 
 // partial slots of the gather (TM + NWAVE - 1), reused for the three operand tiles after it
 constexpr int PART_ROWS = (TM + NWAVE - 1) > 3 * TM ? (TM + NWAVE - 1) : 3 * TM;
@@ -437,4 +439,5 @@ __device__ __forceinline__ void tile_finish(const LayerArgs& p, float* part, int
   }
 }
 
+}  // inline namespace
 }  // namespace regcn
