@@ -35,6 +35,7 @@ def main():
     del snaps
     model = bench.build_model(cfg, 200, dev, seed=1234)
     model.param_caches = model.memo_pristine = False
+    model.use_phases = False  # config 5 runs per-layer launches (bench.py)
     out = {"crel_eb": os.environ.get("REGCN_CREL_EB", "32")}
     for m in [int(v) for v in a.mins.split(",")]:
         HL.CREL_MIN_ITEMS = m
