@@ -808,6 +808,25 @@ def pmc_for(kernel, config, d):
         config, k["launches"])
 
 
+L2_GATHER_CEILING_TBPS = 16.8  # rows gathered from the XCD's L2, chip-wide (MI355X_MICROARCH.md, lower end)
+
+
+def l2_request_stream(config, ms):
+    """The inline gather against the L2-gather ceiling: L1 <- L2 read requests per launch of its
+    kernels (rocprofv3 TCP_TCC_READ_REQ_sum, summed over the gather's kernels, from
+    profiles/pmc_l2req_<config>.json) x 128 B over the call's measured time."""
+    path = os.path.join(REPO, "profiles", "pmc_l2req_%s.json" % config)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pm = json.load(f)
+    req = float(pm["gather_requests_per_launch"])
+    tbps = req * 128.0 / (ms * 1e-3) / 1e12
+    return {"requests_per_launch": req, "bytes_per_launch": req * 128.0, "achieved_TBps": round(tbps, 2),
+            "ceiling_TBps": L2_GATHER_CEILING_TBPS, "frac": round(tbps / L2_GATHER_CEILING_TBPS, 4),
+            "kernels": pm.get("kernels"), "source": "profiles/pmc_l2req_%s.json" % config}
+
+
 def cpu_baseline_scale(cfg, d, budget):
     """The CPU oracle's encoder forward (oracle/model.py hyperbolic_forward, the reference op
     sequence with per-edge message materialisation) over ONE snapshot at |V| = 1M with a
@@ -1123,6 +1142,9 @@ def run_scale(args, cfg, world, rank, device, backend):
             kernels[gname].update(s8d_bytes_per_launch=b8, s8d_units_per_launch=units,
                                   s8d_achieved_GBps=round(b8 / (calls[gname]["ms"] * 1e-3) / 1e9, 1))
             kernels[gname]["s8d_frac"] = round(kernels[gname]["s8d_achieved_GBps"] / HBM_PEAK_GBS, 4)
+            l2 = l2_request_stream(args.config, calls[gname]["ms"])
+            if l2:  # the bound that applies: rows gathered from the XCD's L2 (MI355X_MICROARCH.md)
+                kernels[gname]["l2_request_stream"] = l2
         if dom.startswith("regcn_layer_f32") and not sharded:
             # SURVEY.md §8(d)'s count alone: 812 B per unit (gathered row + col_src + col_type +
             # radius per edge; row write + rowptr + norm + radius per node) x the launch's units

@@ -252,15 +252,38 @@ __global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(3))) void 
     f4 racc[JMAX];
 #pragma unroll
     for (int j = 0; j < JMAX; ++j) racc[j] = zero;
-    for (int b = 0; b < kpad / 16; ++b) {
-      const f4 a = *reinterpret_cast<const f4*>(arow + 16 * b);
+    // B fragments stream from L2 (the relation table is L2-resident): a ring of CR_DEPTH k-blocks
+    // in flight ahead of the MFMAs (one block's MFMAs ~512 cycles, an L2 round trip ~1-2k);
+    // unconditional loads (column tiles past nt read row 16 ct + r16 of the zero-padded rows)
+    constexpr int CR_DEPTH = 4;
+    const int nkb = kpad / 16;
+    const float* bbase = p.rel_t + (int64_t)r16 * kpad + 4 * q;
+    auto bload = [&](f4 (&dst)[JMAX], int b) {
+      const int bb = min(b, nkb - 1);
 #pragma unroll
       for (int j = 0; j < JMAX; ++j) {
-        const int ct = w + NWAVE * j;
-        if (ct < nt) {  // wave-uniform
-          const f4 bv = *reinterpret_cast<const f4*>(p.rel_t + (int64_t)(16 * ct + r16) * kpad + 16 * b + 4 * q);
+        const int ct = min(w + NWAVE * j, nt - 1);
+        dst[j] = *reinterpret_cast<const f4*>(bbase + (int64_t)(16 * ct) * kpad + 16 * bb);
+      }
+    };
+    f4 ring[CR_DEPTH][JMAX];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) racc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], bv[e], racc[j], 0, 0, 0);
+    for (int i = 0; i < CR_DEPTH; ++i) bload(ring[i], i);
+    for (int b0 = 0; b0 < nkb; b0 += CR_DEPTH) {
+#pragma unroll
+      for (int i = 0; i < CR_DEPTH; ++i) {
+        const int b = b0 + i;
+        if (b < nkb) {  // wave-uniform
+          const f4 a = *reinterpret_cast<const f4*>(arow + 16 * b);
+#pragma unroll
+          for (int j = 0; j < JMAX; ++j) {
+            if (w + NWAVE * j < nt) {  // wave-uniform
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                racc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[e], ring[i][j][e], racc[j], 0, 0, 0);
+            }
+          }
+          bload(ring[i], b + CR_DEPTH);  // block b + CR_DEPTH into the slot just consumed
         }
       }
     }
