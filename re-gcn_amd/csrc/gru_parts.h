@@ -95,6 +95,11 @@ __device__ __forceinline__ void gru_pre_block(const RelGru2Args& p, int bx, int 
   f4* red = reinterpret_cast<f4*>(lds + TM * lda);  // [PRE_WAVES][3][64]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w >= PRE_WAVES) {  // waves beyond the part's four (a wider phase launch) only meet its barriers
+    __syncthreads();
+    __syncthreads();
+    return;
+  }
   const int r0 = bx * TM, jt = by;
   const int n_valid = min(TM, p.R2 - r0);
   {  // [emb_rel | h_prev] rows as float4s, every load issued before the first LDS store
@@ -253,6 +258,12 @@ __device__ __forceinline__ void gru_x_block(const RelGru2Args& p, int bx, int by
   int* tmask = reinterpret_cast<int*>(red + X_WAVES * 3 * 64);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w >= X_WAVES) {  // as in gru_pre_block: three barriers on either staging path
+    __syncthreads();
+    __syncthreads();
+    __syncthreads();
+    return;
+  }
   const int r0 = bx * TM, jt = by;
   const int n_valid = min(TM, p.R2 - r0);
   const int NB = dp >> 4, NT = dp >> 4;

@@ -247,22 +247,26 @@ __global__ __launch_bounds__(256) void k_unpack_rows(const float* __restrict__ i
 // The send side of the halo exchange: rows idx[i] of x and |h| gathered into a contiguous x
 // block (stride d) and |h| vector, which two all_to_alls deliver straight into the receivers'
 // halo rows (no scatter on the receiving side; parallel.ExchangePlan).
+constexpr int GR_ROWS = 8;  // rows in flight per wave in the halo gather
 __global__ __launch_bounds__(256) void k_gather_rows(const float* __restrict__ x, const float* __restrict__ r,
                                                      const int64_t* __restrict__ idx, int64_t n, int d,
                                                      float* __restrict__ x_out, float* __restrict__ r_out) {
-  const int64_t i0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * XR_ROWS;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t i0 = ((int64_t)blockIdx.x * 4 + wv) * GR_ROWS;
   const int lane = threadIdx.x & 63, q = d >> 2;
-  f4 v[XR_ROWS];
+  // the wave's GR_ROWS source ids in one load (lane u), then broadcast: one round trip
+  const int64_t my = idx[min(i0 + min(lane, GR_ROWS - 1), n - 1)];
+  f4 v[GR_ROWS];
 #pragma unroll
-  for (int u = 0; u < XR_ROWS; ++u) {
-    const int64_t i = min(i0 + u, n - 1);
-    const int64_t src = idx[i];
-    if (lane < q) v[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x + src * d) + lane);
+  for (int u = 0; u < GR_ROWS; ++u) {
+    const int64_t src = __builtin_amdgcn_readlane((int)my, u) | ((int64_t)__builtin_amdgcn_readlane((int)(my >> 32), u) << 32);
+    // plain loads: the rows were just written by the chunk's tail and are served by the caches
+    if (lane < q) v[u] = reinterpret_cast<const f4*>(x + src * d)[lane];
     else v[u] = f4{lane == q ? r[src] : 0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
-  for (int u = 0; u < XR_ROWS; ++u) {
-    if (i0 + u >= n) continue;
+  for (int u = 0; u < GR_ROWS; ++u) {
+    if (i0 + u >= n) break;
     if (lane < q) reinterpret_cast<f4*>(x_out + (i0 + u) * d)[lane] = v[u];
     else if (lane == q) r_out[i0 + u] = v[u].x;
   }
@@ -276,7 +280,7 @@ int gather_rows(const float* x, const float* r, const int64_t* idx, int64_t n, i
   if (d <= 0 || (d & 3) || d > 4 * (WAVE - 1)) return set_error(REGCN_EINVAL, "row gather needs d %% 4 == 0, d <= 252");
   if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(x_out)) & 15)
     return set_error(REGCN_EINVAL, "row gather needs 16-B aligned x and output");
-  const int64_t blocks = (n + 4 * XR_ROWS - 1) / (4 * XR_ROWS);
+  const int64_t blocks = (n + 4 * GR_ROWS - 1) / (4 * GR_ROWS);
   if (blocks > 0x7fffffffL) return set_error(REGCN_EINVAL, "row gather grid too large");
   hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)blocks), dim3(256), 0, st, x, r, idx, n, d, x_out, r_out);
   return check_launch("k_gather_rows");

@@ -34,8 +34,9 @@ ROWTAIL_MIN_VIEW_ROWS = int(os.environ.get("REGCN_ROWTAIL_MIN_VIEW_ROWS", "1024"
 # chunk i (the L2-bound gather beside the MFMA-bound tail); 1 = one stream, no pipelining
 ROWTAIL_CHUNKS = int(os.environ.get("REGCN_ROWTAIL_CHUNKS", "1"))
 # Inline tiles with at least this many items take their relation half as one MFMA product per
-# tile (regcn_layer_desc.crel_tiles, csrc/rowtail.hip k_gather_crel); 0 disables
-CREL_MIN_ITEMS = int(os.environ.get("REGCN_CREL_MIN_ITEMS", "512"))
+# tile (regcn_layer_desc.crel_tiles, csrc/rowtail.hip k_gather_crel); 0 disables.  Config-5 sweep
+# (profiles/r5_crel_sweep.log, gather call ms): off 1.623, 512 1.657, 1024 1.596, 2048 1.580, 4096 1.667
+CREL_MIN_ITEMS = int(os.environ.get("REGCN_CREL_MIN_ITEMS", "2048"))
 # A rank's pipeline-chunk tails (owner partition) on this many streams (1: one after another)
 CHUNK_TAIL_STREAMS = int(os.environ.get("REGCN_CHUNK_TAIL_STREAMS", "2"))
 

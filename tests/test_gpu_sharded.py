@@ -147,3 +147,21 @@ def test_rccl_device_branches_world1(tmp_path):
     res = json.load(open(out))
     assert res["backend"] == "nccl" and res["world"] == 1, res
     assert res["nccl_exchange_exact"] and res["nccl_allgather_exact"] and res["nccl_equals_gloo"], res
+
+
+@pytest.mark.parametrize("n,d", [(1, 200), (37, 200), (5000, 200), (129, 12)])
+def test_gather_rows_matches_index_select(n, d):
+    """The halo exchange's send-side gather (regcn_gather_rows_f32): rows `ids` of x and |h|,
+    repeated and unsorted ids included, equal index_select bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from regcn_amd import parallel as P
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(n + d)
+    V = 3 * n + 7
+    x = torch.randn(V, d, generator=g).to(dev)
+    r = torch.rand(V, generator=g).to(dev)
+    ids = torch.randint(0, V, (n,), generator=g).to(dev)
+    xs, r1 = P.gather_rows(x, r, ids)
+    torch.cuda.synchronize()
+    assert torch.equal(xs, x.index_select(0, ids)) and torch.equal(r1, r.index_select(0, ids))

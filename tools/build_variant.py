@@ -28,7 +28,7 @@ def main():
     for src in G.SOURCES:
         if src in special:
             obj = os.path.join(out_dir, src.replace(".hip", ".o"))
-            subprocess.run([G.HIPCC, *G.FLAGS, *a.flags, "-c", os.path.join(G.CSRC, src), "-o", obj], check=True)
+            subprocess.run([G.HIPCC, *G.FLAGS, *G.SOURCE_FLAGS.get(src, []), *a.flags, "-c", os.path.join(G.CSRC, src), "-o", obj], check=True)
         else:
             obj = os.path.join(G.CSRC, "build", src.replace(".hip", ".o"))
         objs.append(obj)
