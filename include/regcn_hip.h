@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 11
+#define REGCN_ABI_VERSION 12
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -280,6 +280,17 @@ typedef struct regcn_layer_desc {
   const int32_t* crel_item_tl;
   const float* rel_t;    /* 16 ceil(d / 16) x kpad: rel transposed, zero padded, kpad = R2 rounded up to 16 */
   int32_t n_types;       /* R2 <= 512 */
+  /* regcn_layer_rowtail_* tail (NULL send_x elsewhere): the send block of the owner partition's
+   * halo exchange written by the tail itself (instead of regcn_gather_rows_f32 after it): row id
+   * i of the launch (send_lo <= i < send_lo + send_n) also goes to the slots
+   * send_pos[send_ptr[i - send_lo] .. send_ptr[i - send_lo + 1]) -- its x row (the x_next /
+   * step_x_out value) to send_x + slot * d, its |h| to send_r[slot] */
+  int64_t send_lo;
+  int32_t send_n;
+  const int32_t* send_ptr; /* send_n + 1 */
+  const int32_t* send_pos;
+  float* send_x;
+  float* send_r;
 } regcn_layer_desc;
 int regcn_layer_f32(const regcn_layer_desc* desc, void* stream);
 

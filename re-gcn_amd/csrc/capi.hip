@@ -435,6 +435,14 @@ static int layer_args(const regcn_layer_desc* g, LayerArgs& a) {
   a.crel_item_tl = g->crel_item_tl;
   a.rel_t = g->rel_t;
   a.n_types = g->n_types;
+  a.send_lo = g->send_lo;
+  a.send_n = g->send_n;
+  a.send_ptr = g->send_ptr;
+  a.send_pos = g->send_pos;
+  a.send_x = g->send_x;
+  a.send_r = g->send_r;
+  if (a.send_x && (!a.send_ptr || !a.send_pos || !a.send_r || a.send_n < 0 || a.send_lo < 0))
+    return set_error(REGCN_EINVAL, "send block needs send_ptr, send_pos, send_r and send_n >= 0");
   if (a.item_src_runs && a.agg_mode != REGCN_AGG_UNION && a.agg_mode != REGCN_AGG_EUCLID)
     return set_error(REGCN_EINVAL, "item_src_runs applies to the union / euclid gathers only");
   if (g->fuse_step) {

@@ -137,6 +137,14 @@ struct LayerArgs {
   const int* crel_item_tl;
   const float* rel_t;        // ceil(d / 16) 16 x crel_kpad(n_types): rel transposed, zero padded
   int n_types;               // R2 <= 512
+  // rowtail tail: the halo exchange's send block written alongside x_next / step.x_out (row id
+  // i -> slots send_pos[send_ptr[i - send_lo] ..]), send_x null when off
+  int64_t send_lo;
+  int send_n;
+  const int* send_ptr;
+  const int* send_pos;
+  float* send_x;
+  float* send_r;
 };
 
 struct ScoreArgs {

@@ -536,6 +536,51 @@ __device__ __forceinline__ void rt_store_radius(const float n2[4], float* __rest
   }
 }
 
+// The halo exchange's send block (regcn_layer_desc.send_*): row id i of the launch also goes to
+// slots send_pos[send_ptr[i - send_lo] ..] -- its |h| and, after log0, its x row -- so no gather
+// kernel re-reads the rows after the tail (parallel.exchange_halo).  Rows outside the block's
+// id range have no slots.
+__device__ __forceinline__ void rt_send_span(const LayerArgs& p, int rid, int& s0, int& s1) {
+  const int64_t li = (int64_t)rid - p.send_lo;
+  const bool in = li >= 0 && li < p.send_n;
+  s0 = in ? p.send_ptr[li] : 0;
+  s1 = in ? p.send_ptr[li + 1] : 0;
+}
+
+__device__ __forceinline__ void rt_send_radius(const LayerArgs& p, const float n2[4], const int crow[4], int n_valid) {
+  const int lane = threadIdx.x & 63;
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (4 * (lane >> 4) + r >= n_valid) continue;
+      int s0, s1;
+      rt_send_span(p, crow[r], s0, s1);
+      const float v = fmaxf(sqrtf(n2[r]), REGCN_EPS);  // = rt_store_radius's value
+      for (int sl = s0; sl < s1; ++sl) p.send_r[p.send_pos[sl]] = v;
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void rt_send_rows(const RAcc<NT>& a, const LayerArgs& p, const int crow[4], int n_valid,
+                                             int d) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (4 * (lane >> 4) + r >= n_valid) continue;
+    int s0, s1;
+    rt_send_span(p, crow[r], s0, s1);
+    for (int sl = s0; sl < s1; ++sl) {
+      float* dst = p.send_x + (int64_t)p.send_pos[sl] * d;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int col = 16 * t + (lane & 15);
+        if (col < d) dst[col] = a.t[t][r];
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ int own_int(const int v[4]) {
   const bool b0 = threadIdx.x & 1, b1 = threadIdx.x & 2;
   const int lo = b0 ? v[1] : v[0], hi = b0 ? v[3] : v[2];
@@ -602,9 +647,10 @@ __device__ __forceinline__ void rt_stage_blend(const StepArgs& s, const RtRows& 
 // C-layout rows stored through the wave's LDS region in the same 80-column stages: written
 // there per element, read back as 16-B row pieces, stored as whole 16-B vectors (5 per lane per
 // stage) instead of NT x 4 scattered 4-B stores.  In-order LDS within the wave: no barrier.
+// send: also into p's send block (as rt_send_rows)
 template <int NT>
 __device__ __forceinline__ void rt_store_staged(const RAcc<NT>& a, float* __restrict__ M, const RtRows& R, int d,
-                                                char* lds) {
+                                                char* lds, const LayerArgs& p, bool send) {
   const int lane = threadIdx.x & 63, q = lane >> 4;
   float* st = reinterpret_cast<float*>(lds + wave_id() * 2 * RT_SC_BYTES);
   constexpr int NS = (NT + RT_SC_TILES - 1) / RT_SC_TILES;
@@ -625,8 +671,16 @@ __device__ __forceinline__ void rt_store_staged(const RAcc<NT>& a, float* __rest
     for (int i = 0; i < RT_SC_BYTES / 1024; ++i) {
       const int slot = 64 * i + lane, sr = slot / f4pr, sc = slot - sr * f4pr;
       const int rid = __shfl(R.arow_id, min(sr, 15));
-      if (slot < 16 * f4pr && sr < R.n_valid)
-        *reinterpret_cast<f4*>(M + (int64_t)rid * d + c0 + 4 * sc) = *reinterpret_cast<const f4*>(st + 4 * slot);
+      if (slot < 16 * f4pr && sr < R.n_valid) {
+        const f4 val = *reinterpret_cast<const f4*>(st + 4 * slot);
+        *reinterpret_cast<f4*>(M + (int64_t)rid * d + c0 + 4 * sc) = val;
+        if (send) {
+          int s0, s1;
+          rt_send_span(p, rid, s0, s1);
+          for (int sl = s0; sl < s1; ++sl)
+            *reinterpret_cast<f4*>(p.send_x + (int64_t)p.send_pos[sl] * d + c0 + 4 * sc) = val;
+        }
+      }
     }
   }
 }
@@ -656,9 +710,11 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     // tail 2.5 % slower at config 5)
     rt_store<NT>(v, p.h_out, crow, n_valid, d);
     if (p.r_next) rt_store_radius(n2, p.r_next, crow, n_valid);
+    if (p.send_x) rt_send_radius(p, n2, crow, n_valid);
     if (p.x_next) {
       if (!p.euclid) rt_log0<NT>(v, n2, p.k);
       rt_store<NT>(v, p.x_next, crow, n_valid, d);
+      if (p.send_x) rt_send_rows<NT>(v, p, crow, n_valid, d);
     }
   } else {
     const StepArgs& s = p.step;
@@ -739,11 +795,12 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     float f[4];
     spread_rows(fminf(fmaxf(newr, REGCN_EPS), kr.rmax) / fmaxf(sqrtf(n2o), REGCN_EPS), f);
     rt_scale_known<NT>(v, n2, f);
-    rt_store_staged<NT>(v, s.h_out, R, d, lds);
+    rt_store_staged<NT>(v, s.h_out, R, d, lds, p, false);
     if (s.r_out) rt_store_radius(n2, s.r_out, crow, n_valid);
+    if (p.send_x) rt_send_radius(p, n2, crow, n_valid);
     if (s.x_out) {
       rt_log0<NT>(v, n2, k);
-      rt_store_staged<NT>(v, s.x_out, R, d, lds);
+      rt_store_staged<NT>(v, s.x_out, R, d, lds, p, p.send_x != nullptr);
     }
   }
 }

@@ -316,23 +316,23 @@ __device__ __forceinline__ float row16_max(float v) {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
-template <int MODE>
+template <int MODE, int J>
 __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4* acc, const float* x2,
                                                     const float* y2, const float* bn_, const int* qi, const int* ni,
                                                     int lane, int bn, float* run_m, float* run_se) {
   RowK rk[4];
-  ColK ck[4];
+  ColK ck[J];
 #pragma unroll
   for (int r = 0; r < 4; ++r) rk[r] = row_k(x2[r], p);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) ck[j] = col_k(y2[j], bn_[j], p);
+  for (int j = 0; j < J; ++j) ck[j] = col_k(y2[j], bn_[j], p);
   const float mx2 = p.mx * p.mx;
   if (MODE == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (qi[r] >= p.B) continue;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < J; ++j)
         if (ni[j] < p.N)
           p.out[(int64_t)qi[r] * p.N + ni[j]] =
               fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb);
@@ -340,10 +340,10 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
   } else if (MODE == 1) {  // this lane's running (max, sum exp) per query row, across tiles
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float sv[4], m = -INFINITY;
+      float sv[J], m = -INFINITY;
       const int t = qi[r] < p.B ? p.target[qi[r]] : -1;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < J; ++j) {
         sv[j] = ni[j] < p.N ? fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb)
                             : -INFINITY;
         m = fmaxf(m, sv[j]);
@@ -353,7 +353,7 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
       const float ml = (mn == -INFINITY ? 0.f : mn) * LOG2E;  // exp2(-inf) = 0 for empty lanes
       float se = run_se[r] * __builtin_amdgcn_exp2f(fmaf(run_m[r], LOG2E, -ml));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) se += __builtin_amdgcn_exp2f(fmaf(sv[j], LOG2E, -ml));
+      for (int j = 0; j < J; ++j) se += __builtin_amdgcn_exp2f(fmaf(sv[j], LOG2E, -ml));
       run_m[r] = mn;
       run_se[r] = se;
     }
@@ -364,12 +364,13 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
       const float t = qi[r] < p.B ? p.thr[qi[r]] : INFINITY;
       float cnt = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < J; ++j)
         if (ni[j] < p.N)
           cnt += fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb) > t ? 1.f : 0.f;
       run_se[r] += cnt;  // an exact integer (< 2^24 per lane)
     }
-  } else {  // MODE 2: CE backward coefficients
+  } else {  // MODE 2: CE backward coefficients (8-wave workgroups only: J = 4, SN-candidate tiles)
+    static_assert(MODE != 2 || J == 4, "the CE backward runs the 8-wave shape");
     const int nblk = (p.N + SN - 1) / SN;
     const float c = p.c, m2c = -2.f * c;
     float cs[4][3];
@@ -433,24 +434,46 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
 // candidate tiles x + 8 (k + S i), S = stripes per XCD.  The nbq workgroups of one stripe walk
 // the same tiles in step, so a tile comes from HBM into its XCD's L2 once.
 constexpr int SQ2 = 128, SW2 = SQ2 / 16, KB_MAX = 16;  // d <= 256
+//
+// Workgroup shape NW (waves): 8 = 128 queries x 64-candidate tiles, one workgroup per CU (its
+// 111 KB of LDS); 4 = 64 queries x 32-candidate tiles at 56 KB, two workgroups per CU.  With 8
+// waves the one barrier per tile keeps both waves of a SIMD in the same phase -- both multiply,
+// then both run the epilogue while the matrix core idles; two 4-wave workgroups have no common
+// barrier, so one's epilogue issues beside the other's MFMAs.  Queries per workgroup 16 NW,
+// candidates per tile 8 NW (8 staging threads per candidate row), NW / 2 accumulators per wave.
 
 __host__ __device__ inline int score_lds_stride(int d) { return ((d + 15) & ~15) + 8; }
 
-// grid = 8 XCDs x query tiles x stripes (about one workgroup per CU when B is small).
+// grid = 8 XCDs x query tiles x stripes (about one 8-wave workgroup, or two 4-wave ones, per CU
+// when B is small); at most 32 stripes: the 8 x stripes partials of a query fit
+// ce_partial_slots(N) (>= 256 and >= the candidate tiles)
+template <int NW = 8>
 inline int score_f32_stripes(int B, int nbn) {
-  const int nbq = (B + SQ2 - 1) / SQ2;
-  return std::max(1, std::min(32 / nbq, (nbn + 7) / 8));
+  const int nbq = (B + 16 * NW - 1) / (16 * NW);
+  return std::max(1, std::min(std::min(256 / NW / nbq, 32), (nbn + 7) / 8));
 }
+template <int NW = 8>
 inline unsigned score_f32_grid(int B, int nbn) {
-  return (unsigned)(8L * ((B + SQ2 - 1) / SQ2) * score_f32_stripes(B, nbn));
+  return (unsigned)(8L * ((B + 16 * NW - 1) / (16 * NW)) * score_f32_stripes<NW>(B, nbn));
 }
-inline size_t score_f32_lds(int d) { return (size_t)2 * SN * (score_lds_stride(d) + 1) * 4; }
+template <int NW = 8>
+inline size_t score_f32_lds(int d) { return (size_t)2 * 8 * NW * (score_lds_stride(d) + 1) * 4; }
+// REGCN_SCORE_NW: the workgroup shape of the proxy-score kernels (the CE backward keeps 8)
+static int score_nw() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("REGCN_SCORE_NW");
+    v = (e && atoi(e) == 4) ? 4 : 8;
+  }
+  return v;
+}
 
 // One workgroup's work: `blk` of `nblk` workgroups of this job (the XCD of blk is blk % 8:
 // a job's first workgroup must sit at a multiple of 8 in the launch).
-template <int MODE>
+template <int MODE, int NW>
 __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const int nblk) {
-  extern __shared__ float Es[];  // 2 x SN x SE candidate rows, zero past N and d
+  constexpr int SQW = 16 * NW, SNW = 8 * NW, J = SNW / 16;  // queries, candidates per tile; accumulators
+  extern __shared__ float Es[];  // 2 x SNW x SE candidate rows, zero past N and d
   p.scale = p.scale_p ? *p.scale_p : 1.f;
   if (p.scale_raw && p.scale_p)  // softplus(raw) + 1e-6 (hyperbolic_decoder.py:717; torch threshold 20)
     p.scale = (p.scale > 20.f ? p.scale : log1pf(expf(p.scale))) + 1e-6f;
@@ -462,12 +485,12 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   };
   stamp(0);
   const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
-  const int nbn = p.n_rng ? p.rng_total : (p.N + SN - 1) / SN, nbq = (p.B + SQ2 - 1) / SQ2;
+  const int nbn = p.n_rng ? p.rng_total : (p.N + SNW - 1) / SNW, nbq = (p.B + SQW - 1) / SQW;
   // candidate tile t -> its first row and valid rows (row ranges: a tile never spans two)
   auto tile_rows = [&](int t, int& row0, int& nvalid) {
     if (!p.n_rng) {
-      row0 = t * SN;
-      nvalid = min(SN, p.N - row0);
+      row0 = t * SNW;
+      nvalid = min(SNW, p.N - row0);
       return;
     }
     // static indices only (a dynamic index would put the argument struct in scratch)
@@ -475,16 +498,16 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
 #pragma unroll
     for (int r = 1; r < SCORE_MAX_RANGES; ++r)
       if (r < p.n_rng && t >= p.rng_tile[r]) st = p.rng_start[r], tb = p.rng_tile[r], ln = p.rng_len[r];
-    const int off = (t - tb) * SN;
+    const int off = (t - tb) * SNW;
     row0 = st + off;
-    nvalid = min(SN, ln - off);
+    nvalid = min(SNW, ln - off);
   };
   const int S = nblk / (8 * nbq);
   const int xcd = blk & 7, rk = blk >> 3;
   const int bq = rk % nbq, stripe = rk / nbq;
   auto tile_of = [&](int i) { return xcd + 8 * (stripe + S * i); };
   int bn = tile_of(0);
-  const int q0 = bq * SQ2;
+  const int q0 = bq * SQW;
   const int g4 = 4 * (lane >> 4);
   // cross entropy: per-lane running (max, sum exp) over every tile of the strip, reduced over the
   // 16 lanes of each query row and written once, as partial xcd + 8 stripe of the query
@@ -543,7 +566,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     qi[r] = q0 + 16 * wv + li;
   }
   // staging map: thread tid stages candidate row tid / 8, float4 units tid % 8 + 8 it
-  static_assert(64 * SW2 == 8 * SN, "staging map: 8 threads per candidate row");
+  static_assert(64 * NW == 8 * SNW, "staging map: 8 threads per candidate row");
   constexpr int IT = KB_MAX * 4 / 8;
   const int sr = tid >> 3, sub = tid & 7, per_row = 4 * KB;
   f4 v[IT];
@@ -555,12 +578,12 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     for (int it = 0; it < IT; ++it) v[it] = *reinterpret_cast<const f4*>(erow + min((sub + 8 * it) * 4, d - 4));
   };
   // |e|^2 of each staged row, summed over its 8 staging lanes (xor 1, 2, 4), next to the tile
-  float* e2s = Es + 2 * SN * SE;  // [2][SN]
+  float* e2s = Es + 2 * SNW * SE;  // [2][SNW]
   auto stash = [&](int buf, int t) {
     int row0, nv;
     tile_rows(t, row0, nv);
     const bool row_ok = sr < nv;
-    float* lrow = Es + buf * SN * SE + sr * SE;
+    float* lrow = Es + buf * SNW * SE + sr * SE;
     float ss = 0.f;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -572,7 +595,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     ss += __shfl_xor(ss, 1);
     ss += __shfl_xor(ss, 2);
     ss += __shfl_xor(ss, 4);
-    if (sub == 0) e2s[buf * SN + sr] = ss;
+    if (sub == 0) e2s[buf * SNW + sr] = ss;
   };
   fetch(bn);
   stash(0, bn);
@@ -585,37 +608,39 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     // next tile's rows in flight under this tile's MFMAs (MODE 2: after its epilogue, whose
     // live registers would otherwise spill)
     if (MODE != 2) fetch(min(bn_next, nbn - 1));
-    const float* brow = Es + cur * SN * SE + (lane & 15) * SE + g4;
-    f4 acc[4] = {z4, z4, z4, z4};
+    const float* brow = Es + cur * SNW * SE + (lane & 15) * SE + g4;
+    f4 acc[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = z4;
     // B fragments of block b + 1 are read while block b's MFMAs run (register double buffer;
     // the read past the last block is clamped, never used)
-    f4 bb[2][4];  // ping-pong by block parity (static after unrolling: no copies)
+    f4 bb[2][J];  // ping-pong by block parity (static after unrolling: no copies)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bb[0][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE);
+    for (int j = 0; j < J; ++j) bb[0][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE);
 #pragma unroll
     for (int b = 0; b < KB_MAX; ++b) {
       if (b < KB) {  // wave-uniform
         const int bnx = min(b + 1, KB - 1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bb[(b + 1) & 1][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE + 16 * bnx);
+        for (int j = 0; j < J; ++j) bb[(b + 1) & 1][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE + 16 * bnx);
         __builtin_amdgcn_sched_barrier(0);  // keep block b + 1's reads ahead of block b's MFMAs
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < J; ++j)
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[b][e], bb[b & 1][j][e], acc[j], 0, 0, 0);
       }
     }
-    float y2[4], bn_[4];
-    int ni[4], row0, nv;
+    float y2[J], bn_[J];
+    int ni[J], row0, nv;
     tile_rows(bn, row0, nv);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < J; ++j) {
       ni[j] = 16 * j + (lane & 15) < nv ? row0 + 16 * j + (lane & 15) : 0x7fffffff;  // invalid: >= N
-      y2[j] = e2s[cur * SN + 16 * j + (lane & 15)];
+      y2[j] = e2s[cur * SNW + 16 * j + (lane & 15)];
       bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
     }
-    score_epilogue_fast<MODE>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se);
+    score_epilogue_fast<MODE, J>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se);
     if (!more) break;
     if (MODE == 2) fetch(bn_next);
     stash(cur ^ 1, bn_next);  // that buffer's readers passed the last barrier
@@ -839,7 +864,7 @@ __device__ __forceinline__ void score_ws_body(ScoreArgs p, const int blk, const 
   auto epilogue = [&]() {
 #pragma unroll
     for (int g = 0; g < 2; ++g)
-      score_epilogue_fast<MODE>(p, acc[g], x2[g], y2, bn_, qi[g], ni, lane, prev_bn, run_m[g], run_se[g]);
+      score_epilogue_fast<MODE, 4>(p, acc[g], x2[g], y2, bn_, qi[g], ni, lane, prev_bn, run_m[g], run_se[g]);
   };
   for (int i = 0;; ++i) {
     const int bn_next = tile_of(i + 1), bn_next2 = tile_of(i + 2);
@@ -872,19 +897,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   else score_ws_body<0>(p1, blockIdx.x - g0, gridDim.x - g0);
 }
 
-template <int MODE>
-__global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32(ScoreArgs p) {
-  score_f32_body<MODE>(p, blockIdx.x, gridDim.x);
+template <int MODE, int NW = 8>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32(ScoreArgs p) {
+  score_f32_body<MODE, NW>(p, blockIdx.x, gridDim.x);
 }
 
 // Two independent score jobs in one launch (a predict's entity and relation scores): job 1's
 // workgroups follow job 0's in dispatch order, so they take the CUs that job 0's shorter
 // strips free instead of running as a second serial launch.
-__global__ __launch_bounds__(64 * SW2) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32_jobs(ScoreArgs p0,
-                                                                                                      ScoreArgs p1,
-                                                                                                      int g0) {
-  if ((int)blockIdx.x < g0) score_f32_body<0>(p0, blockIdx.x, g0);
-  else score_f32_body<0>(p1, blockIdx.x - g0, gridDim.x - g0);
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32_jobs(ScoreArgs p0,
+                                                                                                     ScoreArgs p1,
+                                                                                                     int g0) {
+  if ((int)blockIdx.x < g0) score_f32_body<0, NW>(p0, blockIdx.x, g0);
+  else score_f32_body<0, NW>(p1, blockIdx.x - g0, gridDim.x - g0);
 }
 
 // Combine per-tile (max, sumexp) into per-query loss = lse - target logit (one wave per query).
@@ -1005,9 +1031,14 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   const dim3 g2(score_f32_grid(a.B, nbn)), b2(64 * SW2);
   const size_t lds2 = score_f32_lds(a.d);
   const bool ws = fast && score_ws() && score_ws_lds(a.d) <= SCORE_LDS_MAX;
+  const bool nw4 = fast && !ws && score_nw() == 4;
+  const int nbn4 = (a.N + 31) / 32;
+  const dim3 g4(score_f32_grid<4>(a.B, nbn4)), b4(256);
+  const size_t lds4 = score_f32_lds<4>(a.d);
   if (mode == 0) {
     if (!a.out) return set_error(REGCN_EINVAL, "null output");
     if (ws) hipLaunchKernelGGL((k_score_ws<0>), g2, dim3(512), score_ws_lds(a.d), st, a);
+    else if (nw4) hipLaunchKernelGGL((k_score_f32<0, 4>), g4, b4, lds4, st, a);
     else if (fast) hipLaunchKernelGGL((k_score_f32<0>), g2, b2, lds2, st, a);
     else if (a.use_dist) hipLaunchKernelGGL((k_score<0, true>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_score<0, false>), g, b, 0, st, a);
@@ -1015,12 +1046,14 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   }
   if (!a.target || !a.part || !a.tgt_logit || !loss) return set_error(REGCN_EINVAL, "CE needs target/workspace/loss");
   if (ws) hipLaunchKernelGGL((k_score_ws<1>), g2, dim3(512), score_ws_lds(a.d), st, a);
+  else if (nw4) hipLaunchKernelGGL((k_score_f32<1, 4>), g4, b4, lds4, st, a);
   else if (fast) hipLaunchKernelGGL((k_score_f32<1>), g2, b2, lds2, st, a);
   else if (a.use_dist) hipLaunchKernelGGL((k_score<1, true>), g, b, 0, st, a);
   else hipLaunchKernelGGL((k_score<1, false>), g, b, 0, st, a);
   int rc = check_launch("k_score_ce");
   if (rc) return rc;
-  const int nparts = fast ? 8 * score_f32_stripes(a.B, nbn) : nbn;  // <= ce_partial_slots(N)
+  const int nparts = nw4 ? 8 * score_f32_stripes<4>(a.B, nbn4)
+                         : fast ? 8 * score_f32_stripes(a.B, nbn) : nbn;  // <= ce_partial_slots(N)
   hipLaunchKernelGGL(k_ce_combine, dim3((a.B + 3) / 4), b, 0, st, a.part, a.tgt_logit, a.B, nparts, loss, a.lse_out);
   return check_launch("k_ce_combine");
 }
@@ -1040,10 +1073,14 @@ int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st) {
     return 0;
   }
   const unsigned g0 = score_f32_grid(a0.B, (a0.N + SN - 1) / SN), g1 = score_f32_grid(a1.B, (a1.N + SN - 1) / SN);
-  if (score_ws() && score_ws_lds(a0.d) <= SCORE_LDS_MAX)
+  if (score_ws() && score_ws_lds(a0.d) <= SCORE_LDS_MAX) {
     hipLaunchKernelGGL(k_score_ws_jobs, dim3(g0 + g1), dim3(512), score_ws_lds(a0.d), st, a0, a1, (int)g0);
-  else
-    hipLaunchKernelGGL(k_score_f32_jobs, dim3(g0 + g1), dim3(64 * SW2), score_f32_lds(a0.d), st, a0, a1, (int)g0);
+  } else if (score_nw() == 4) {
+    const unsigned h0 = score_f32_grid<4>(a0.B, (a0.N + 31) / 32), h1 = score_f32_grid<4>(a1.B, (a1.N + 31) / 32);
+    hipLaunchKernelGGL(k_score_f32_jobs<4>, dim3(h0 + h1), dim3(256), score_f32_lds<4>(a0.d), st, a0, a1, (int)h0);
+  } else {
+    hipLaunchKernelGGL(k_score_f32_jobs<8>, dim3(g0 + g1), dim3(64 * SW2), score_f32_lds(a0.d), st, a0, a1, (int)g0);
+  }
   return check_launch("k_score_f32_jobs");
 }
 
@@ -1076,7 +1113,17 @@ int rank_fused(ScoreArgs& a, int accumulate, int* counts, hipStream_t st) {
   if (a.B > 0 && (!a.q || !a.thr || !counts || !a.part)) return set_error(REGCN_EINVAL, "null pointer");
   if (a.B > 0 && a.N > 0 && !a.e) return set_error(REGCN_EINVAL, "null candidates");
   if (a.B == 0) return 0;
-  const int nbn = a.n_rng ? a.rng_total : (a.N + SN - 1) / SN;
+  const int nw = score_nw(), snw = 8 * nw;
+  if (a.n_rng) {  // the ranges' candidate tiles at this shape's tile size (a tile never spans two)
+    int tiles = 0;
+    for (int r = 0; r < SCORE_MAX_RANGES && r < a.n_rng; ++r) {
+      a.rng_tile[r] = tiles;
+      tiles += (a.rng_len[r] + snw - 1) / snw;
+    }
+    a.rng_tile[a.n_rng] = tiles;
+    a.rng_total = tiles;
+  }
+  const int nbn = a.n_rng ? a.rng_total : (a.N + snw - 1) / snw;
   if (nbn == 0) {  // nothing to count: counts stay (accumulate) or become 0
     if (!accumulate) {
       hipLaunchKernelGGL(k_count_combine, dim3((a.B + 3) / 4), dim3(256), 0, st, a.part, a.B, 0, 0, counts);
@@ -1085,11 +1132,12 @@ int rank_fused(ScoreArgs& a, int accumulate, int* counts, hipStream_t st) {
     return 0;
   }
   a.trace = g_trace;
-  hipLaunchKernelGGL((k_score_f32<3>), dim3(score_f32_grid(a.B, nbn)), dim3(64 * SW2), score_f32_lds(a.d), st, a);
+  if (nw == 4) hipLaunchKernelGGL((k_score_f32<3, 4>), dim3(score_f32_grid<4>(a.B, nbn)), dim3(256), score_f32_lds<4>(a.d), st, a);
+  else hipLaunchKernelGGL((k_score_f32<3>), dim3(score_f32_grid(a.B, nbn)), dim3(64 * SW2), score_f32_lds(a.d), st, a);
   const int rc = check_launch("k_score_f32<3>");
   if (rc) return rc;
-  hipLaunchKernelGGL(k_count_combine, dim3((a.B + 3) / 4), dim3(256), 0, st, a.part, a.B,
-                     8 * score_f32_stripes(a.B, nbn), accumulate, counts);
+  const int np = nw == 4 ? 8 * score_f32_stripes<4>(a.B, nbn) : 8 * score_f32_stripes(a.B, nbn);
+  hipLaunchKernelGGL(k_count_combine, dim3((a.B + 3) / 4), dim3(256), 0, st, a.part, a.B, np, accumulate, counts);
   return check_launch("k_count_combine");
 }
 

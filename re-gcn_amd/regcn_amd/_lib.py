@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REGCN_HIP_LIB") or os.path.join(_HERE, "libregcn_hip.so")  # override: A/B builds
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -134,6 +134,7 @@ class LayerDesc(ctypes.Structure):
         ("step_x_out", P), ("step_r_out", P), ("trace", P), ("item_src_runs", _c_int),
         ("gate_w", P), ("gate_out", P), ("step_tw", P),
         ("crel_tiles", _c_int), ("crel_item_src", P), ("crel_item_tl", P), ("rel_t", P), ("n_types", _c_int),
+        ("send_lo", ctypes.c_int64), ("send_n", _c_int), ("send_ptr", P), ("send_pos", P), ("send_x", P), ("send_r", P),
     ]
 
 

@@ -238,20 +238,21 @@ def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_
 
 
 def run_layer_chunked(mode, g, tail_views, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c, euclid, step, out,
-                      gate, after):
+                      gate, after, send=None):
     """The large-snapshot layer over a rank's rows in pipeline chunks (parallel.ShardedGraph,
     owner partition): the hub pass and the gather run once over `g` (all of the rank's rows),
     then each tail view's 64-row tail, `after(j)` following chunk j's tail (its rows' x and |h|
-    are final: the caller all-gathers them while the next chunk's tail runs)."""
+    are final: the caller all-gathers them while the next chunk's tail runs).  send(j): None or
+    the send block chunk j's tail writes as well (parallel.ExchangePlan.send_block)."""
     agg = _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c)
     if g.n_pos == 0:
         mode = _lib.AGG_NONE
     return _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c, euclid, step, agg, out, gate,
-                        int(g.work()["rows"].shape[0]), tail_views=tail_views, after=after)
+                        int(g.work()["rows"].shape[0]), tail_views=tail_views, after=after, send=send)
 
 
 def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c, euclid, step, agg, out, gate,
-                 n_rows, tail_views=None, after=None):
+                 n_rows, tail_views=None, after=None, send=None):
     """regcn_layer_rowtail_f32: the inline in-edge rows gathered into `agg` (which holds the hub
     rows already), then the 64-row tail over all rows (csrc/rowtail.hip)."""
     wk = g.work()
@@ -338,6 +339,14 @@ def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c,
             with torch.cuda.stream(lanes[j % len(lanes)]):
                 tw = tv.work()
                 nr = int(tw["rows"].shape[0])
+                sb = send(j) if (send is not None and nr) else None
+                if sb is not None:  # the tail also fills chunk j's send block of the halo exchange
+                    lo, n, ptr, pos, xs, r1 = sb
+                    desc.send_lo, desc.send_n = int(lo), int(n)
+                    desc.send_ptr, desc.send_pos = a(ptr, torch.int32), a(pos, torch.int32)
+                    desc.send_x, desc.send_r = a(xs), a(r1)
+                else:
+                    desc.send_lo, desc.send_n, desc.send_ptr, desc.send_pos, desc.send_x, desc.send_r = 0, 0, None, None, None, None
                 if nr:
                     keep.append(tw["rows"])
                     desc.rows, desc.n_pos, desc.V = a(tw["rows"], torch.int32), tv.n_pos, nr

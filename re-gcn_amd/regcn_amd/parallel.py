@@ -295,6 +295,36 @@ class ExchangePlan:
     def rows_received(self):
         return sum(sum(c[3]) for c in self.chunks)
 
+    def send_slots(self, j, lo, n):
+        """Chunk j's send block as seen from its rows (the tail writes it, regcn_layer_desc
+        send_*): (ptr, pos) int32 with row id lo + i going to block slots pos[ptr[i] .. ptr[i + 1])
+        -- the positions of id lo + i in chunk j's send list (one per receiver that reads it).
+        None when the chunk sends nothing or an id falls outside [lo, lo + n)."""
+        cache = self.__dict__.setdefault("_send_slots", {})
+        key = (j, lo, n)
+        if key not in cache:
+            send = self.chunks[j][0]
+            out = None
+            if send.numel() and int(send.min()) >= lo and int(send.max()) < lo + n:
+                order = torch.argsort(send, stable=True)
+                ptr = torch.zeros(n + 1, device=send.device, dtype=torch.int64)
+                ptr[1:] = torch.cumsum(torch.bincount(send - lo, minlength=n), 0)
+                out = (ptr.int(), order.int())
+            cache[key] = out
+        return cache[key]
+
+    def send_block(self, j, lo, n, d):
+        """(send descriptor for the chunk-j tail, (x block, |h| vector)) or None: fresh buffers
+        of chunk j's send list the tail fills (see send_slots)."""
+        sl = self.send_slots(j, lo, n)
+        if sl is None:
+            return None
+        m = self.chunks[j][0].numel()
+        dev = self.chunks[j][0].device
+        xs = torch.empty(m, d, device=dev, dtype=torch.float32)
+        r1 = torch.empty(m, device=dev, dtype=torch.float32)
+        return (lo, n, sl[0], sl[1], xs, r1), (xs, r1)
+
     def link_rows(self, j):
         """The largest per-peer row count of chunk j's exchange, either direction (each peer
         pair has its own xGMI link, so the exchange takes max over links)."""
@@ -332,6 +362,9 @@ def exchange_rows(chunk, xn, rn, group=None, pack=pack_rows, unpack=unpack_rows)
 # chunk, x rows and |h|, no receive-side scatter); 0: one all_to_all of pack_rows' (d + 4)-float
 # records scattered into the global rows by unpack_rows (round 4)
 HALO = os.environ.get("REGCN_HALO", "1") != "0"
+# The large-snapshot tails write the send block themselves (regcn_layer_desc send_*); 0: a gather
+# kernel after each chunk's tail (regcn_gather_rows_f32)
+SEND_FROM_TAIL = os.environ.get("REGCN_SEND_FROM_TAIL", "1") != "0"
 
 
 def record_bytes(plan, d):
@@ -732,18 +765,20 @@ class ShardedGraph:
         return agg
 
     def _rank_launches(self, mode, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                       drop_mask, c, euclid, step, out, gate, exchange, views=None):
+                       drop_mask, c, euclid, step, out, gate, exchange, views=None, send=None):
         """This rank's launches of one layer into `out`, exchange(j) after chunk j's rows are
         final.  Large snapshots: the hub pass and the gather once over all of the rank's rows,
         then each chunk's tail (full-size launches but the tails); otherwise each chunk's whole
         layer launch.  views: (whole-rows view, chunk views) to read x / r through (the halo
-        views when the input came through the halo exchange; default the plain views)."""
+        views when the input came through the halo exchange; default the plain views).  send(j):
+        chunk j's send-block descriptor for its tail (ExchangePlan.send_block) or None; only the
+        large-snapshot tails take it (exchange(j) gathers the rows otherwise)."""
         from .hyperbolic_layers import _use_rowtail, run_layer, run_layer_chunked
         V, d = x.shape
         rv, cvs = views if views is not None else (self.rank_view, [v for _, v in self.views])
         if rv is not None and _use_rowtail(V, int(rv.fw.host["rows"].shape[0]), d, prev_t, drop_mask, False):
             run_layer_chunked(mode, rv, cvs, x, r, rel, w_rel, nb, gamma, w_n, w_loop,
-                              w_evolve, c, euclid, step, out, gate, exchange)
+                              w_evolve, c, euclid, step, out, gate, exchange, send=send)
             return
         for j, view in enumerate(cvs):
             run_layer(mode, view, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
@@ -791,9 +826,26 @@ class ShardedGraph:
             _all_gather_into(xn[a:b], xn[k:k + cr], self.group)
             _all_gather_into(rn[a:b], rn[k:k + cr], self.group)
 
+        sent = {}  # chunk j -> its send block, written by chunk j's tail
+
+        def send(j):
+            if not (halo_out and SEND_FROM_TAIL):
+                return None
+            lo, hi = lay.ranges(self.rank)[j]
+            sb = plan.send_block(j, lo, hi - lo, d)
+            if sb is None:
+                return None
+            sent[j] = sb[1]
+            return sb[0]
+
         def gather_needed(j):  # the rows the consumer reads
             if halo_out:  # straight into the consumer's halo rows
-                exchange_halo(plan, j, xn, rn, lay.Vp, self.group)
+                blk = sent.pop(j, None)
+                if blk is not None and x.is_cuda:  # written on the tail's stream, read on this one
+                    for t in blk:
+                        t.record_stream(torch.cuda.current_stream(x.device))
+                exchange_halo(plan, j, xn, rn, lay.Vp, self.group,
+                              gather=(lambda *_: blk) if blk is not None else None)
             else:
                 exchange_rows(plan.chunks[j], xn, rn, self.group)
 
@@ -812,7 +864,8 @@ class ShardedGraph:
                 fn(j)
 
         self._rank_launches(mode, xin, rin, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                            drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, exchange, views=views)
+                            drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, exchange, views=views,
+                            send=send if self.collective else None)
         if comm is not None:
             cur.wait_stream(comm)
             for t in (xn, rn):
@@ -928,6 +981,8 @@ class RankSimulation(ShardedGraph):
         self.times = [[] for _ in range(world)]
         self.chunk_marks = [[] for _ in range(world)]  # per rank: (chunk-end events, link bytes) per layer
         self.delivery = []  # event pairs around the simulated halo deliveries (the all_to_alls' data)
+        # tests: ((x block, |h|), xn, rn, send ids) of every tail-written send block
+        self.keep_sends, self.sends = False, []
 
     def _timed(self, k, fn):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -966,9 +1021,24 @@ class RankSimulation(ShardedGraph):
         rn = torch.empty(xn.shape[0], device=x.device, dtype=torch.float32)
 
         def rank_launches(k, sg, plan, marks):
+            sent = {}
+
+            def send(j):  # chunk j's send block, written by its tail
+                if not (plan and halo_out and SEND_FROM_TAIL):
+                    return None
+                lo, hi = lay.ranges(k)[j]
+                sb = plan.send_block(j, lo, hi - lo, d)
+                if sb is None:
+                    return None
+                sent[j] = sb[1]
+                if self.keep_sends:
+                    self.sends.append((sb[1], xn, rn, plan.chunks[j][0]))
+                return sb[0]
+
             def after(j):  # chunk j's rows final: the rank's send-side kernel(s) of its exchange
                 if plan and halo_out:  # its send block (delivered into the halos below)
-                    gather_rows(xn, rn, plan.chunks[j][0])
+                    if sent.pop(j, None) is None:
+                        gather_rows(xn, rn, plan.chunks[j][0])
                 elif plan:  # the records, and the received records scattered (into scratch rows
                     sidx, _, ridx, _ = plan.chunks[j]  # here: the simulated rows hold their
                     send = pack_rows(xn, rn, sidx)      # values already)
@@ -980,7 +1050,8 @@ class RankSimulation(ShardedGraph):
                 marks.append(e)
             views = sg.halo_views(self.plan_for(k), in_bases[k]) if halo_in else None
             sg._rank_launches(mode, xin, rin, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip,
-                              drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, after, views=views)
+                              drop_mask, c, euclid, step, (h[:V], xn[:V], rn[:V]), gate, after, views=views,
+                              send=send)
         scratch = None
         if not halo_out:
             scratch = self.__dict__.get("_scratch")

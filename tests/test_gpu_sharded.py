@@ -95,7 +95,9 @@ def test_rank_simulation_matches_unsharded(golden, tag, world, chunks, rowtail, 
     (1e-4 * max(1, |ref|)) and relation states; a balanced relabel of the entities
     (EntityRelabel) changes nothing but the row order.  rowtail: the large-snapshot layer path
     (threshold lowered), where a rank's hub pass and gather run once over all of its rows and
-    only the tails per chunk (hyperbolic_layers.run_layer_chunked)."""
+    only the tails per chunk (hyperbolic_layers.run_layer_chunked), and each chunk's tail also
+    writes the send block of its halo exchange (regcn_layer_desc send_*): equal bit for bit to
+    gathering the rows after it (regcn_gather_rows_f32)."""
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     if rowtail:
@@ -113,8 +115,14 @@ def test_rank_simulation_matches_unsharded(golden, tag, world, chunks, rowtail, 
         embs, _, h0, _, _ = m.forward(glist, None, True)
         ref = embs[-1].clone()
         sims = [RankSimulation(g, world, chunks) for g in glist]
+        for sm in sims:
+            sm.keep_sends = True
         e2, _, h02, _, _ = m.forward(sims, None, True)
         assert_close(e2[-1], ref, what="simulated ranks")
+        sends = [s for sm in sims for s in sm.sends]
+        assert bool(sends) == rowtail
+        for (xs, r1), xn, rn, ids in sends:
+            assert torch.equal(xs, xn.index_select(0, ids)) and torch.equal(r1, rn.index_select(0, ids))
         assert_close(h02, h0, 1e-5, "relation state")
         assert all(len(t) for sm in sims for t in sm.times)
         snaps = [z["snap%d" % t] for t in range(T)]
