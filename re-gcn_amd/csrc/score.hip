@@ -328,14 +328,16 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
   for (int j = 0; j < J; ++j) ck[j] = col_k(y2[j], bn_[j], p);
   const float mx2 = p.mx * p.mx;
   if (MODE == 0) {
+    // the lane's candidates are ni[0] + 16 j (each valid one): one row address per query row,
+    // the 16 j steps as immediate store offsets
+    const int64_t n0 = ni[0] < p.N ? ni[0] : 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (qi[r] >= p.B) continue;
+      float* orow = p.out + (int64_t)qi[r] * p.N + n0;
 #pragma unroll
       for (int j = 0; j < J; ++j)
-        if (ni[j] < p.N)
-          p.out[(int64_t)qi[r] * p.N + ni[j]] =
-              fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb);
+        if (ni[j] < p.N) orow[16 * j] = fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb);
     }
   } else if (MODE == 1) {  // this lane's running (max, sum exp) per query row, across tiles
 #pragma unroll
