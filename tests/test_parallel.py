@@ -445,3 +445,30 @@ def test_entity_relabel_permutes_every_entity_tensor(decoder):
     per_entity = {k for k, v in before.items() if v.dim() >= 1 and v.shape[0] == V}
     assert per_entity == moved, per_entity ^ moved
     assert ("decoder_ob.b" in moved) == (decoder == "hyperbolic_convtranse")
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 1), (3, 3), (4, 2)])
+def test_send_slots_cover_the_send_list(world, chunks):
+    """ExchangePlan.send_slots / send_block (the send block a chunk's tail writes itself,
+    regcn_layer_desc.send_*): scattering every row of chunk j to its slots reproduces chunk j's
+    send list gathered in order (one slot per receiver that reads the row), for every rank."""
+    g = _snapshot(V=400, T=3000, seed=world)
+    V, d = g.number_of_nodes(), 5
+    ref = torch.arange(V * d, dtype=torch.float32).view(V, d) + 0.25
+    lay = P.OwnerLayout(V, world, chunks)
+    for rank in range(world):
+        plan = P.ExchangePlan(g, lay, rank)
+        for j, (lo, hi) in enumerate(lay.ranges(rank)):
+            sidx = plan.chunks[j][0]
+            sb = plan.send_block(j, lo, hi - lo, d)
+            if sb is None:
+                assert sidx.numel() == 0
+                continue
+            (lo_, n, ptr, pos, xs, r1), blk = sb
+            assert (lo_, n) == (lo, hi - lo) and blk[0] is xs and blk[1] is r1
+            assert ptr.dtype == torch.int32 and pos.dtype == torch.int32 and int(ptr[-1]) == sidx.numel()
+            rows = lo + torch.repeat_interleave(torch.arange(n), (ptr[1:] - ptr[:-1]).long())
+            xs[pos.long()] = ref[rows]
+            r1[pos.long()] = -ref[rows, 0]
+            assert torch.equal(xs, ref[sidx]) and torch.equal(r1, -ref[sidx, 0])
+            assert sorted(pos.tolist()) == list(range(sidx.numel()))
