@@ -506,12 +506,11 @@ __device__ __forceinline__ void rt_store(const RAcc<NT>& a, float* __restrict__ 
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     if (4 * (lane >> 4) + r >= n_valid) continue;
-    const int64_t base = (int64_t)crow[r] * d;
+    // one row address per row; the column tiles are immediate offsets (16 t floats)
+    float* row = M + (int64_t)crow[r] * d + (lane & 15);
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int col = 16 * t + (lane & 15);
-      if (col < d) M[base + col] = a.t[t][r];
-    }
+    for (int t = 0; t < NT; ++t)  // NT = ceil(d / 16): only the last tile has pad columns
+      if (t < NT - 1 || 16 * t + (lane & 15) < d) row[16 * t] = a.t[t][r];
   }
 }
 
@@ -571,12 +570,10 @@ __device__ __forceinline__ void rt_send_rows(const RAcc<NT>& a, const LayerArgs&
     int s0, s1;
     rt_send_span(p, crow[r], s0, s1);
     for (int sl = s0; sl < s1; ++sl) {
-      float* dst = p.send_x + (int64_t)p.send_pos[sl] * d;
+      float* dst = p.send_x + (int64_t)p.send_pos[sl] * d + (lane & 15);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        const int col = 16 * t + (lane & 15);
-        if (col < d) dst[col] = a.t[t][r];
-      }
+      for (int t = 0; t < NT; ++t)
+        if (t < NT - 1 || 16 * t + (lane & 15) < d) dst[16 * t] = a.t[t][r];
     }
   }
 }
@@ -746,7 +743,9 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
         const f4 c4 = clamp4(v.t[t], -10.f, 10.f);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const bool ok = (4 * q + r < n_valid) & (col < d);
+          // rows past n_valid were staged as zeros (and are never stored); only the last tile's
+          // pad columns (cl clamped onto a real column) need the select
+          const bool ok = t < NT - 1 || col < d;
           const float xp = xs[(4 * q + r) * ncols + cl];
           const float zt = zs[(4 * q + r) * ncols + cl];
           const float pr = fminf(fmaxf(ok ? xp : 0.f, -10.f), 10.f);

@@ -319,7 +319,8 @@ constexpr float LOG2E = 1.4426950408889634f;
 template <int MODE, int J>
 __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4* acc, const float* x2,
                                                     const float* y2, const float* bn_, const int* qi, const int* ni,
-                                                    int lane, int bn, float* run_m, float* run_se) {
+                                                    int lane, int bn, float* run_m, float* run_se,
+                                                    bool full = false) {
   RowK rk[4];
   ColK ck[J];
 #pragma unroll
@@ -331,6 +332,16 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
     // the lane's candidates are ni[0] + 16 j (each valid one): one row address per query row,
     // the 16 j steps as immediate store offsets
     const int64_t n0 = ni[0] < p.N ? ni[0] : 0;
+    if (full) {  // every query row and candidate of the tile valid (wave-uniform): no store masks
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float* orow = p.out + (int64_t)qi[r] * p.N + n0;
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          orow[16 * j] = fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb);
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (qi[r] >= p.B) continue;
@@ -642,7 +653,8 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
       y2[j] = e2s[cur * SNW + 16 * j + (lane & 15)];
       bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
     }
-    score_epilogue_fast<MODE, J>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se);
+    score_epilogue_fast<MODE, J>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se,
+                                 MODE == 0 && nv == SNW && q0 + SQW <= p.B);
     if (!more) break;
     if (MODE == 2) fetch(bn_next);
     stash(cur ^ 1, bn_next);  // that buffer's readers passed the last barrier
