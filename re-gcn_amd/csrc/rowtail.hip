@@ -659,7 +659,7 @@ __device__ __forceinline__ void rt_store_staged(const RAcc<NT>& a, float* __rest
 #pragma unroll
     for (int t = stage * RT_SC_TILES; t < min(NT, (stage + 1) * RT_SC_TILES); ++t) {
       const int cl = 16 * t + (lane & 15) - c0;
-      if (cl < ncols) {
+      if (t < NT - 1 || cl < ncols) {  // only the last column tile reaches past d
 #pragma unroll
         for (int r = 0; r < 4; ++r) st[(4 * q + r) * ncols + cl] = a.t[t][r];
       }
