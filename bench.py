@@ -695,7 +695,8 @@ SCALE_KERNEL = {  # library call -> its main kernel (rocprof / PMC name)
     "regcn_segment_mean_f32": "k_gather_sum<1>",
     "regcn_layer_f32": "k_layer<0, 1, false>",
     "regcn_layer_f32(step)": "k_layer<0, 1, true>",
-    "regcn_layer_rowtail_f32(gather)": "k_gather_agg<0, 1>",
+    # one call = the crel gather over the big tiles + the plain gather over the rest
+    "regcn_layer_rowtail_f32(gather)": "k_gather_crel<0, 32> + k_gather_agg<0, 1>",
     "regcn_layer_rowtail_f32": "k_rowtail2<13, 1>",
     "regcn_layer_rowtail_f32(step)": "k_rowtail3<13, 3>",
     "regcn_timestep_phase_f32(A)": "k_phase_a",
@@ -801,11 +802,12 @@ def pmc_for(kernel, config, d):
         pm = json.load(f)
     if pm.get("config") != config or int(pm.get("d", -1)) != d:
         return None, None
-    k = pm["kernels"].get(kernel)
-    if k is None:
+    names = kernel.split(" + ")  # a call of several kernels: their bytes per launch summed
+    ks = [pm["kernels"].get(n) for n in names]
+    if any(k is None for k in ks):
         return None, None
-    return k["hbm_bytes"], "profiles/pmc_traffic_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, %d launches)" % (
-        config, k["launches"])
+    return sum(k["hbm_bytes"] for k in ks), "profiles/pmc_traffic_%s.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, %s launches)" % (
+        config, " + ".join(str(k["launches"]) for k in ks))
 
 
 L2_GATHER_CEILING_TBPS = 16.8  # rows gathered from the XCD's L2, chip-wide (MI355X_MICROARCH.md, lower end)
