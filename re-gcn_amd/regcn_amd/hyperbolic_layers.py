@@ -37,6 +37,11 @@ ROWTAIL_CHUNKS = int(os.environ.get("REGCN_ROWTAIL_CHUNKS", "1"))
 # tile (regcn_layer_desc.crel_tiles, csrc/rowtail.hip k_gather_crel); 0 disables.  Config-5 sweep
 # (profiles/r5_crel_sweep.log, gather call ms): off 1.623, 512 1.657, 1024 1.596, 2048 1.580, 4096 1.667
 CREL_MIN_ITEMS = int(os.environ.get("REGCN_CREL_MIN_ITEMS", "2048"))
+# ... when at least this many tiles qualify: a crel workgroup is one tile's long chain, so a launch
+# of fewer big tiles than the chip's crel slots (3 per CU) lasts one chain while most CUs idle --
+# a rank's view of an owner-partitioned config-5 snapshot has ~220 (profiles/r5_owner_sim_kernels_*)
+# (8-rank simulation: predicted 8.19 -> 8.13 ms with 768, profiles/r5_crel_min_tiles_sim.txt)
+CREL_MIN_TILES = int(os.environ.get("REGCN_CREL_MIN_TILES", "768"))
 # A rank's pipeline-chunk tails (owner partition) on this many streams (1: one after another)
 CHUNK_TAIL_STREAMS = int(os.environ.get("REGCN_CHUNK_TAIL_STREAMS", "2"))
 
@@ -416,13 +421,13 @@ def _crel(g, mode, rel):
         if torch.cuda.is_current_stream_capturing():
             return None  # no host copy inside a capture: this launch gathers per item
         big = np.diff(g.work()["item_ptr"][:g.n_pos_tiles + 1].cpu().numpy()) >= CREL_MIN_ITEMS
-        k = 0
+        k, first = 0, 0
         if big.any():  # the big tiles follow the hub rows' tiles (no inline items: skipped in-kernel)
             first = int(np.argmax(big))
             rest = np.nonzero(~big[first:])[0]
             k = first + (int(rest[0]) if len(rest) else len(big) - first)
-        hit = g.__dict__["_crel_tiles"] = (CREL_MIN_ITEMS, k)
-    if hit[1] == 0:
+        hit = g.__dict__["_crel_tiles"] = (CREL_MIN_ITEMS, k, first)
+    if hit[1] == 0 or hit[1] - hit[2] < CREL_MIN_TILES:
         return None
     return hit[1], g.item_type_cols(), _rel_t(rel)
 

@@ -831,6 +831,8 @@ def test_crel_gather_matches_per_item(skew, euclid, monkeypatch):
     mode = _lib.AGG_EUCLID if euclid else _lib.AGG_UNION
     w = torch.randn(d, d, device=DEV, generator=gen) * 0.05
 
+    monkeypatch.setattr(HL, "CREL_MIN_TILES", 0)  # this snapshot has a handful of big tiles
+
     def gather(min_items):
         monkeypatch.setattr(HL, "CREL_MIN_ITEMS", min_items)
         g.__dict__.pop("_crel_tiles", None)
