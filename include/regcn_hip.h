@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define REGCN_ABI_VERSION 12
+#define REGCN_ABI_VERSION 13
 #define REGCN_EINVAL (-1)
 #define REGCN_ENOTSUP (-2)
 
@@ -79,6 +79,14 @@ int regcn_ln_roundtrip_f32(const float* x, int64_t rows, int32_t d, float c, flo
  * also emits x = log0(h) and r = |h| for the first timestep (x_out/r_out may be NULL). */
 int regcn_init_entities_f32(const float* dyn, const float* r_static, int64_t rows, int32_t d, float c,
                             int32_t layer_norm, float* h_out, float* x_out, float* r_out, void* stream);
+/* The same map over a row list (owner partition: a rank's own rows and the halo rows its first
+ * layer reads, parallel.ShardedGraph.initial_rows): row src[i] of dyn / r_static -> row dst[i]
+ * of h_out, x_out, r_out (row i when dst is NULL); h_out may be NULL (halo rows need x and |h|
+ * only).  Replaces the same hyperbolic_model.py:779-782 state as regcn_init_entities_f32,
+ * computed only where the rank reads it. */
+int regcn_init_entity_rows_f32(const float* dyn, const float* r_static, const int32_t* src, const int32_t* dst,
+                               int64_t n, int32_t d, float c, int32_t layer_norm, float* h_out, float* x_out,
+                               float* r_out, void* stream);
 
 /* ---- a2/a4/a5/a6: CSR gather + segment reduce --------------------------------------- */
 /* Union aggregation (HyperbolicUnionRGCNLayer msg/reduce/apply, hyperbolic_layers.py:222-240,

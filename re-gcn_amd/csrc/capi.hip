@@ -76,6 +76,11 @@ int regcn_init_entities_f32(const float* dyn, const float* r_static, int64_t row
                             int32_t layer_norm, float* h_out, float* x_out, float* r_out, void* s) {
   return rowmap(layer_norm ? 12 : 11, dyn, nullptr, r_static, rows, d, c, h_out, x_out, r_out, ST(s));
 }
+int regcn_init_entity_rows_f32(const float* dyn, const float* r_static, const int32_t* src, const int32_t* dst,
+                               int64_t n, int32_t d, float c, int32_t layer_norm, float* h_out, float* x_out,
+                               float* r_out, void* s) {
+  return init_rows(dyn, r_static, src, dst, n, d, c, layer_norm, h_out, x_out, r_out, ST(s));
+}
 
 int regcn_union_aggregate_f32(const float* x, const float* radius, const float* rel, const int32_t* col_src,
                               const int32_t* col_type, const float* norm, const int32_t* chunks, int32_t n_chunks,

@@ -29,6 +29,8 @@ inline Curv make_curv(double c) {
 // rowwise.hip
 int rowmap(int op, const float* a, const float* b, const float* vec, int64_t rows, int d, float c,
            float* out, float* out2, float* out3, hipStream_t st);
+int init_rows(const float* dyn, const float* r_static, const int32_t* src, const int32_t* dst, int64_t n, int d,
+              float c, int layer_norm, float* h, float* x, float* r, hipStream_t st);
 
 // aggregate.hip
 int gather_sum(int mode, const float* x, const float* radius, const float* rel, const int* col_src,

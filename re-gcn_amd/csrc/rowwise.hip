@@ -64,10 +64,15 @@ template <int EPL, int OP>
 __global__ __launch_bounds__(256) void k_rowmap(const float* __restrict__ a, const float* __restrict__ b,
                                                 const float* __restrict__ vec, int64_t rows, int d,
                                                 Curv k, float* __restrict__ out, float* __restrict__ out2,
-                                                float* __restrict__ out3) {
+                                                float* __restrict__ out3, const int32_t* __restrict__ src,
+                                                const int32_t* __restrict__ dst) {
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
-  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += nwaves) {
+  for (int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < rows; i += nwaves) {
+    // OP_INIT / OP_INIT_LN over a row list (regcn_init_entity_rows_f32): input row src[i],
+    // output row dst[i] (i without dst); the other ops run rows in place (src = dst = NULL)
+    const int64_t r = src ? (int64_t)src[i] : i;
+    const int64_t t = dst ? (int64_t)dst[i] : (src ? i : r);
     Frag<EPL> x;
     if (OP == OP_TO_POINCARE) {
       x.load(a + r * (d + 1), d, lane, 1);
@@ -119,12 +124,12 @@ __global__ __launch_bounds__(256) void k_rowmap(const float* __restrict__ a, con
 #pragma unroll
         for (int j = 0; j < EPL; ++j) x.v[j] = (x.v[j] / n) * rr;
       }
-      x.store(out + r * d, d, lane);
+      if (out) x.store(out + t * d, d, lane);
       const float h2 = x.sumsq();
-      if (lane == 0 && out3) out3[r] = fmaxf(sqrtf(h2), REGCN_EPS);
+      if (lane == 0 && out3) out3[t] = fmaxf(sqrtf(h2), REGCN_EPS);
       if (out2) {
         x.scale(log0_factor(h2, k));
-        x.store(out2 + r * d, d, lane);
+        x.store(out2 + t * d, d, lane);
       }
     } else if (OP == OP_MOBIUS_ADD) {                                   // hyperbolic_ops.py:118-143
       Frag<EPL> y;
@@ -149,17 +154,18 @@ __global__ __launch_bounds__(256) void k_rowmap(const float* __restrict__ a, con
 
 template <int OP>
 static int launch_rowmap(const float* a, const float* b, const float* vec, int64_t rows, int d,
-                         const Curv& k, float* out, float* out2, float* out3, hipStream_t st) {
+                         const Curv& k, float* out, float* out2, float* out3, hipStream_t st,
+                         const int32_t* src = nullptr, const int32_t* dst = nullptr) {
   if (rows == 0) return 0;
   int64_t blocks = (rows + 3) / 4;
   if (blocks > 8192) blocks = 8192;                      // grid-stride beyond 8 blocks/CU
   dim3 g((unsigned)blocks), blk(256);
   int epl = (d + 63) / 64;
-  if (epl <= 1) hipLaunchKernelGGL((k_rowmap<1, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3);
-  else if (epl <= 2) hipLaunchKernelGGL((k_rowmap<2, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3);
-  else if (epl <= 4) hipLaunchKernelGGL((k_rowmap<4, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3);
-  else if (epl <= 8) hipLaunchKernelGGL((k_rowmap<8, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3);
-  else if (epl <= 16) hipLaunchKernelGGL((k_rowmap<16, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3);
+  if (epl <= 1) hipLaunchKernelGGL((k_rowmap<1, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3, src, dst);
+  else if (epl <= 2) hipLaunchKernelGGL((k_rowmap<2, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3, src, dst);
+  else if (epl <= 4) hipLaunchKernelGGL((k_rowmap<4, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3, src, dst);
+  else if (epl <= 8) hipLaunchKernelGGL((k_rowmap<8, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3, src, dst);
+  else if (epl <= 16) hipLaunchKernelGGL((k_rowmap<16, OP>), g, blk, 0, st, a, b, vec, rows, d, k, out, out2, out3, src, dst);
   else return set_error(REGCN_EINVAL, "row width d=%d exceeds 1024", d);
   return check_launch("k_rowmap");
 }
@@ -194,6 +200,17 @@ int rowmap(int op, const float* a, const float* b, const float* vec, int64_t row
       return launch_rowmap<OP_INIT_LN>(a, b, vec, rows, d, k, out, out2, out3, st);
   }
   return set_error(REGCN_EINVAL, "unknown row op %d", op);
+}
+
+int init_rows(const float* dyn, const float* r_static, const int32_t* src, const int32_t* dst, int64_t n, int d,
+              float c, int layer_norm, float* h, float* x, float* r, hipStream_t st) {
+  if (d <= 0) return set_error(REGCN_EINVAL, "d must be positive");
+  if (n < 0) return set_error(REGCN_EINVAL, "negative row count");
+  if (n == 0) return 0;
+  if (!dyn || !r_static || !src || !x || !r) return set_error(REGCN_EINVAL, "null pointer");
+  Curv k = make_curv(c);
+  if (layer_norm) return launch_rowmap<OP_INIT_LN>(dyn, nullptr, r_static, n, d, k, h, x, r, st, src, dst);
+  return launch_rowmap<OP_INIT>(dyn, nullptr, r_static, n, d, k, h, x, r, st, src, dst);
 }
 
 

@@ -15,7 +15,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("REGCN_HIP_LIB") or os.path.join(_HERE, "libregcn_hip.so")  # override: A/B builds
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _c_int, _c_i64, _c_f, _c_vp, _c_sz = ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 P = _c_vp
@@ -37,6 +37,7 @@ _SIGS = {
     "regcn_prologue_f32": [P, _c_i64, _c_int, _c_f, P, P, P],
     "regcn_ln_roundtrip_f32": [P, _c_i64, _c_int, _c_f, P, P],
     "regcn_init_entities_f32": [P, P, _c_i64, _c_int, _c_f, _c_int, P, P, P, P],
+    "regcn_init_entity_rows_f32": [P, P, P, P, _c_i64, _c_int, _c_f, _c_int, P, P, P, P],
     "regcn_union_aggregate_f32": [P, P, P, P, P, P, P, _c_int, P, _c_int, _c_f, _c_int, P, _c_int, P, P],
     "regcn_euclid_aggregate_f32": [P, P, P, P, P, P, _c_int, P, _c_int, _c_int, P, _c_int, P, P],
     "regcn_union_aggregate_src_runs_f32": [P, P, P, P, P, P, P, P, _c_int, P, _c_int, _c_f, _c_int, _c_int, P, _c_int,

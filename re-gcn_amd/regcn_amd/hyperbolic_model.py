@@ -111,6 +111,8 @@ def relation_context(x, g, num_rels2):
 # the owner partition's exchange: the rows the next layer reads (parallel.ExchangePlan); 0: every
 # row after every layer (in-place all-gathers)
 SPARSE_EXCHANGE = os.environ.get("REGCN_SPARSE_EXCHANGE", "1") != "0"
+# ... and each rank maps only the initial rows it reads (ShardedGraph.initial_state); 0: all V
+OWNER_INIT = os.environ.get("REGCN_OWNER_INIT", "1") != "0"
 
 REL_INLINE_MAX_SPAN = 64  # longer r_to_e spans are averaged by the chunked segment-mean kernel first
 
@@ -367,13 +369,21 @@ class HyperbolicRecurrentRGCN(nn.Module):
         c_val = self._c_float()
         dev = self.dynamic_emb.device
         V, d = self.dynamic_emb.shape
+        fused_step = len(self.rgcn.layers) > 0 and not self.run_analysis
+        g_list = list(g_list)
+        if g_list:
+            g_list[0] = g_list[0].to(dev)
+        g0 = g_list[0] if g_list else None
+        # owner partition with the sparse halo exchange: each rank maps only the initial rows it
+        # reads (its own + the first snapshot's halo) instead of all V (ShardedGraph.initial_state)
+        owner0 = (fused_step and SPARSE_EXCHANGE and OWNER_INIT and isinstance(g0, ShardedGraph) and g0.halo_initial_state())
         scope = self.__dict__.get("_scope")
         if scope is not None and scope["c"] == c_val:  # a batch's shared parameter-only states
             r_static = scope["r_static"]
             h, x, r = scope["init"]
         else:
             r_static = self._static_radius(c_val).contiguous()
-            h, x, r = self._initial_state(c_val, r_static)
+            h, x, r = self._initial_state(c_val, r_static, g0 if owner0 else None)
         attach(h, x, r, c_val)
         self.h = h
         R2 = self.num_rels * 2
@@ -386,7 +396,6 @@ class HyperbolicRecurrentRGCN(nn.Module):
         if ana and self.training:  # hyperbolic_model.py:791-792
             _ana.log_embedding(self, h, "init_embeddings", c_val)
         gate_list, gate_means = [], []
-        fused_step = len(self.rgcn.layers) > 0 and not self.run_analysis
         for i, g in enumerate(g_list):
             g = g.to(dev)
             if isinstance(g, ShardedGraph) and g.partition == "owner":
@@ -450,27 +459,31 @@ class HyperbolicRecurrentRGCN(nn.Module):
                              torch.stack(gate_means) if gate_means else [])
         return history_embs, None, self.h_0, gate_list, []
 
-    def _initial_state(self, c_val, r_static):
+    def _initial_state(self, c_val, r_static, owner=None):
         """(h, x, r) of the initial entity state (hyperbolic_model.py:775-782): a function of
         parameters only, computed once per parameter version (param_caches) and reused by every
         predict (the kernels read it, none writes it), so a captured predict graph holds no init
-        launch."""
+        launch.  owner: the first snapshot of an owner partition -- only the rows this rank
+        reads (ShardedGraph.initial_state)."""
         pe = self.dynamic_emb
         V, d = pe.shape
         key = (pe.data_ptr(), pe._version, self.radius_static.data_ptr(), self.radius_static._version,
-               float(c_val), bool(self.layer_norm), float(self.radius_min), float(self.radius_max))
+               float(c_val), bool(self.layer_norm), float(self.radius_min), float(self.radius_max), id(owner))
         hit = self.__dict__.get("_init_cache")
-        if hit is not None and hit[0] == key and self.param_caches:
+        if hit is not None and hit[0] == key and hit[2] is owner and self.param_caches:
             return hit[1]
         dyn = pe.detach().contiguous()
-        h = torch.empty_like(dyn)
-        x = torch.empty_like(dyn)
-        r = torch.empty(V, device=pe.device, dtype=torch.float32)
-        _lib.call("regcn_init_entities_f32", _lib.fptr(dyn, "dynamic_emb"), _lib.fptr(r_static), V, d, c_val,
-                  int(bool(self.layer_norm)), _lib.fptr(h), _lib.fptr(x), _lib.fptr(r), _lib.stream())
+        if owner is not None:
+            h, x, r = owner.initial_state(dyn, r_static, c_val, self.layer_norm)
+        else:
+            h = torch.empty_like(dyn)
+            x = torch.empty_like(dyn)
+            r = torch.empty(V, device=pe.device, dtype=torch.float32)
+            _lib.call("regcn_init_entities_f32", _lib.fptr(dyn, "dynamic_emb"), _lib.fptr(r_static), V, d, c_val,
+                      int(bool(self.layer_norm)), _lib.fptr(h), _lib.fptr(x), _lib.fptr(r), _lib.stream())
         if self.param_caches and not torch.cuda.is_current_stream_capturing():
             _lib.publish()
-            self.__dict__["_init_cache"] = (key, (h, x, r))
+            self.__dict__["_init_cache"] = (key, (h, x, r), owner)
         return h, x, r
 
     def _step_tensors(self):

@@ -687,6 +687,51 @@ class ShardedGraph:
             cache[base] = (rv, [HaloView(v, remap) for _, v in self.views])
         return cache[base]
 
+    def init_rows(self, k=None):
+        """(own ids, halo ids), int32 on the device: the rows of the initial entity state rank k
+        (default this rank) reads -- its own rows, and this snapshot's halo (the sources of its
+        edges that other ranks own: all its first layer reads besides its own rows)."""
+        k = self.rank if k is None else k
+        cache = self.__dict__.setdefault("_init_rows", {})
+        if k not in cache:
+            dev = self.g.device
+            own = [torch.arange(a, b, device=dev, dtype=torch.int32) for a, b in self.layout.ranges(k) if b > a]
+            own = torch.cat(own) if own else torch.zeros(0, device=dev, dtype=torch.int32)
+            cache[k] = (own, self.plan_for(k).halo.to(dev, torch.int32))
+        return cache[k]
+
+    def halo_initial_state(self):
+        """Whether initial_state applies: the owner partition of > 1 ranks with the halo
+        exchange (the first layer then reads its sources through the halo views)."""
+        return self.partition == "owner" and self.world > 1 and HALO
+
+    @staticmethod
+    def _init_launch(dyn, r_static, src, dst, h, x, r, c, layer_norm):
+        if src.numel():
+            _lib.call("regcn_init_entity_rows_f32", _lib.fptr(dyn, "dynamic_emb"), _lib.fptr(r_static),
+                      _lib.iptr(src), _lib.iptr(dst) if dst is not None else None, src.numel(), dyn.shape[1],
+                      float(c), int(bool(layer_norm)), _lib.fptr(h) if h is not None else None, _lib.fptr(x),
+                      _lib.fptr(r), _lib.stream())
+
+    def initial_state(self, dyn, r_static, c, layer_norm):
+        """The initial entity state (h, x = log0 h, |h|; regcn_init_entities_f32's map,
+        hyperbolic_model.py:779-782) only where this rank reads it: its own rows at their ids and
+        this snapshot's halo at rows Vp.. (x and |h|), x tagged for the halo views as a layer's
+        output is, so the first layer reads its sources there.  Replaces every rank mapping all
+        V rows (config 5 at 8 ranks: 0.6 ms per step on every rank).  Rows outside are unset."""
+        lay = self.layout
+        V, d = dyn.shape
+        own, halo = self.init_rows()
+        H = halo.numel()
+        h = torch.empty(lay.Vp, d, device=dyn.device, dtype=torch.float32)
+        x = torch.empty(lay.Vp + H, d, device=dyn.device, dtype=torch.float32)
+        r = torch.empty(lay.Vp + H, device=dyn.device, dtype=torch.float32)
+        self._init_launch(dyn, r_static, own, own, h, x, r, c, layer_norm)
+        self._init_launch(dyn, r_static, halo, None, None, x[lay.Vp:], r[lay.Vp:], c, layer_norm)
+        xv = x[:V]
+        xv._regcn_halo = (self, x, r)
+        return h[:V], xv, r[:V]
+
     def link_bytes(self, plan, j, d):
         """Bytes on the busiest peer link in chunk j's exchange (the all-gather: one chunk of
         rows from every peer)."""
@@ -1081,6 +1126,26 @@ class RankSimulation(ShardedGraph):
             self.delivery.append((e0, e1))
             xv._regcn_halo = (target, xn, rn)
         return h[:V], xv, rn[:V]
+
+    def initial_state(self, dyn, r_static, c, layer_norm):
+        """Every simulated rank's initial rows (ShardedGraph.initial_state), each rank's
+        launches timed as its own: own rows at their ids, its halo at rows halo_bases()[k].."""
+        lay = self.layout
+        V, d = dyn.shape
+        bases = self.halo_bases()
+        h = torch.empty(lay.Vp, d, device=dyn.device, dtype=torch.float32)
+        x = torch.empty(bases[-1], d, device=dyn.device, dtype=torch.float32)
+        r = torch.empty(bases[-1], device=dyn.device, dtype=torch.float32)
+        for k in range(self.world):
+            own, halo = self.init_rows(k)
+
+            def launches(k=k, own=own, halo=halo):
+                self._init_launch(dyn, r_static, own, own, h, x, r, c, layer_norm)
+                self._init_launch(dyn, r_static, halo, None, None, x[bases[k]:], r[bases[k]:], c, layer_norm)
+            self._timed(k, launches)
+        xv = x[:V]
+        xv._regcn_halo = (self, x, r)
+        return h[:V], xv, r[:V]
 
     def exposed_exchange_ms(self, link_gbs=153.0):
         """Per rank: the exchange time no compute hides, summed over the layers run since

@@ -173,3 +173,36 @@ def test_gather_rows_matches_index_select(n, d):
     xs, r1 = P.gather_rows(x, r, ids)
     torch.cuda.synchronize()
     assert torch.equal(xs, x.index_select(0, ids)) and torch.equal(r1, r.index_select(0, ids))
+
+
+@pytest.mark.parametrize("ln,d", [(0, 200), (1, 200), (0, 37)])
+def test_init_entity_rows_match_the_full_map(ln, d):
+    """regcn_init_entity_rows_f32 (the owner partition's initial rows: a rank's own rows at
+    their ids, its halo compacted at rows Vp..): every listed row equal bit for bit to the same
+    row of regcn_init_entities_f32 over all rows; unlisted rows untouched; h may be skipped."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from regcn_amd import _lib
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(d + ln)
+    V, c = 5003, 0.7
+    dyn = (0.3 * torch.randn(V, d, generator=g)).to(dev)
+    rs = (0.2 + torch.rand(V, generator=g)).to(dev)
+    f, i = _lib.fptr, _lib.iptr
+    h, x, r = torch.empty(V, d, device=dev), torch.empty(V, d, device=dev), torch.empty(V, device=dev)
+    _lib.call("regcn_init_entities_f32", f(dyn), f(rs), V, d, c, ln, f(h), f(x), f(r), _lib.stream())
+    ids = torch.randperm(V, generator=g)[:1777].to(torch.int32).to(dev)
+    h2, x2 = torch.full_like(h, float("nan")), torch.full_like(x, float("nan"))
+    r2 = torch.full_like(r, float("nan"))
+    _lib.call("regcn_init_entity_rows_f32", f(dyn), f(rs), i(ids), i(ids), ids.numel(), d, c, ln, f(h2), f(x2),
+              f(r2), _lib.stream())
+    xc, rc = torch.empty(ids.numel(), d, device=dev), torch.empty(ids.numel(), device=dev)
+    _lib.call("regcn_init_entity_rows_f32", f(dyn), f(rs), i(ids), None, ids.numel(), d, c, ln, None, f(xc),
+              f(rc), _lib.stream())
+    torch.cuda.synchronize()
+    li = ids.long()
+    assert torch.equal(h2[li], h[li]) and torch.equal(x2[li], x[li]) and torch.equal(r2[li], r[li])
+    rest = torch.ones(V, dtype=torch.bool, device=dev)
+    rest[li] = False
+    assert bool(torch.isnan(h2[rest]).all() and torch.isnan(x2[rest]).all() and torch.isnan(r2[rest]).all())
+    assert torch.equal(xc, x[li]) and torch.equal(rc, r[li])
