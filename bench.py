@@ -900,7 +900,7 @@ def owner_simulation(args, cfg, device, world):
     relation GRU, queries, target scores, relation decoder), the all-gather volume, and the
     step a rank would take with the exchange hidden under its compute."""
     from regcn_amd.graph import hub_block_work  # noqa: F401
-    from regcn_amd.parallel import CandidateShard, EntityRelabel, RankSimulation
+    from regcn_amd.parallel import SIM_MARKERS, CandidateShard, EntityRelabel, RankSimulation
     from regcn_amd.synthetic import snapshot_series
     d, T, V, R = args.d, cfg["T"], cfg["V"], cfg["R"]
     snaps = snapshot_series(100, V, R, T + 1, cfg["per_snap"])
@@ -936,9 +936,13 @@ def owner_simulation(args, cfg, device, world):
         ts = shards[0].target_scores(q, emb, None, at[:, 2], dec.c, **kw)
         for k, sh in enumerate(shards):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if SIM_MARKERS:
+                torch.cuda._sleep(1)
             a.record()
             sh.range_ranks(q, emb, None, dec.c, ts, **kw)
             b.record()
+            if SIM_MARKERS:
+                torch.cuda._sleep(1)
             dec_times[k].append((a, b))
         model.rdecoder.forward(emb, r_emb, at, mode="test")
 

@@ -923,28 +923,42 @@ class ShardedGraph:
         return hv, xv, rn[:V]
 
     # ---- owner partition: the rows other ranks computed, when a consumer needs them
-    def relation_means(self, x, R2):
+    def relation_means(self, x, R2, sums_only=False):
         """Relation-context means (hyperbolic_model.relation_context) with the pairs
         partitioned like the rows: this rank sums the x rows of its own entities in every
         forward relation's r_to_e span (one sub-span per pipeline chunk), ONE all_reduce of the
-        R x d sums, then / count; inverse relations copy their forward row."""
+        R x d sums, then / count; inverse relations copy their forward row.  sums_only: the
+        rank's sums (no all_reduce, no division)."""
         R = R2 // 2
         V, d = x.shape
         wk = self.g.work()
         if self._rel is None:
-            self._rel = self._relation_lists(R)
-        ch, fx, ns, nq = self._rel
+            # (chunks, fixups, slots, ranges, unit weights, clamped counts): per snapshot
+            ch, fx, ns, nq = self._relation_lists(R)
+            self._rel = (ch, fx, ns, nq, torch.ones(R * nq, device=x.device, dtype=torch.float32),
+                         wk["rel_count"][:R].clamp(min=1.0).unsqueeze(1).contiguous())
+        ch, fx, ns, nq, ones, cnt = self._rel
         out = torch.zeros(R * nq, d, device=x.device, dtype=torch.float32)
         part = torch.empty(max(ns, 1), d, device=x.device, dtype=torch.float32)
-        ones = torch.ones(R * nq, device=x.device, dtype=torch.float32)
         _lib.call("regcn_segment_mean_f32", _lib.fptr(x, "x"), _lib.iptr(wk["rel_idx"]), _lib.fptr(ones),
                   _lib.iptr(ch), ch.shape[0], _lib.iptr(fx), fx.shape[0], d, _lib.fptr(part), d, _lib.fptr(out),
                   _lib.stream())
         sums = out.view(R, nq, d).sum(1) if nq > 1 else out
+        if sums_only:
+            return sums
         if self.collective:
             allreduce_partials(sums, self.group)
-        mean = torch.zeros(R2, d, device=x.device, dtype=torch.float32)
-        cnt = wk["rel_count"][:R].clamp(min=1.0).unsqueeze(1)
+        return self._relation_finish(sums, R2)
+
+    def _relation_sums(self, x, R):
+        """This rank's part of relation_means before the all_reduce: the R x d sums."""
+        return ShardedGraph.relation_means(self, x, 2 * R, sums_only=True)  # not a subclass's
+
+    def _relation_finish(self, sums, R2):
+        """Means from the (all-reduced) sums; inverse relations copy their forward row."""
+        R = R2 // 2
+        cnt = self._rel[5]
+        mean = torch.empty(R2, sums.shape[1], device=sums.device, dtype=torch.float32)  # both halves written
         torch.div(sums, cnt, out=mean[:R])
         mean[R:].copy_(mean[:R])
         return mean
@@ -1010,6 +1024,9 @@ def exposed_after(chunk_end_ms, xchg_ms):
     return max(0.0, end - chunk_end_ms[-1]) if chunk_end_ms else 0.0
 
 
+SIM_MARKERS = os.environ.get("REGCN_SIM_MARKERS", "0") != "0"
+
+
 class RankSimulation(ShardedGraph):
     """All `world` ranks of the owner partition run one after another on ONE device, for
     measurement (bench.py owner_simulation): every layer runs rank 0's chunk launches, then
@@ -1031,9 +1048,13 @@ class RankSimulation(ShardedGraph):
 
     def _timed(self, k, fn):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if SIM_MARKERS:  # profiling: a 1-cycle spin kernel around each rank's launches, so a
+            torch.cuda._sleep(1)  # kernel trace tells rank work from the rest (tools/sim_replicated.py)
         a.record()
         out = fn()
         b.record()
+        if SIM_MARKERS:
+            torch.cuda._sleep(1)
         self.times[k].append((a, b))
         return out
 
@@ -1165,10 +1186,9 @@ class RankSimulation(ShardedGraph):
 
 
     def relation_means(self, x, R2):
-        means = [self._timed(k, lambda: ShardedGraph.relation_means(sg, x, R2)) for k, sg in enumerate(self.ranks)]
-        cnt = self.g.work()["rel_count"].clamp(min=1.0).unsqueeze(1)
-        tot = sum(m * cnt for m in means)  # each rank's sums (mean x count), added as the all_reduce would
-        return tot / cnt
+        sums = [self._timed(k, lambda: ShardedGraph._relation_sums(sg, x, R2 // 2)) for k, sg in enumerate(self.ranks)]
+        tot = torch.stack(sums).sum(0)  # the all_reduce of the ranks' R x d sums (one small collective)
+        return ShardedGraph._relation_finish(self.ranks[0], tot, R2)
 
     def per_rank_ms(self):
         return [sum(a.elapsed_time(b) for a, b in t) for t in self.times]
