@@ -152,6 +152,82 @@ __global__ __launch_bounds__(256) void k_rowmap(const float* __restrict__ a, con
   }
 }
 
+// The initial entity state (OP_INIT / OP_INIT_LN) with the next row's loads in flight: HBM-bound
+// (2.4 KB per row) with one row per wave the loads of a wave's next row wait on the current
+// row's reduction chain; here row i + nwaves is fetched (EPL + 1 registers) before row i is
+// mapped, so a wave keeps two rows of loads outstanding.  The same arithmetic as k_rowmap's
+// OP_INIT branch, so the same bits.
+template <int EPL, int OP>
+__global__ __launch_bounds__(256) void k_init_rows(const float* __restrict__ a, const float* __restrict__ vec,
+                                                   int64_t rows, int d, Curv k, float* __restrict__ out,
+                                                   float* __restrict__ out2, float* __restrict__ out3,
+                                                   const int32_t* __restrict__ src, const int32_t* __restrict__ dst) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (i >= rows) return;
+  Frag<EPL> nx;
+  float nv;
+  {
+    const int64_t r = src ? (int64_t)src[i] : i;
+    nx.load(a + r * d, d, lane);
+    nv = vec[r];
+  }
+  for (; i < rows; i += nwaves) {
+    Frag<EPL> x = nx;
+    const float rv = nv;
+    const int64_t nxt = i + nwaves;
+    if (nxt < rows) {
+      const int64_t r = src ? (int64_t)src[nxt] : nxt;
+      nx.load(a + r * d, d, lane);
+      nv = vec[r];
+    }
+    const int64_t t = dst ? (int64_t)dst[i] : i;
+    float n2 = x.sumsq();
+    if (OP == OP_INIT_LN) {
+      x.scale(1.0f / fmaxf(sqrtf(n2), 1e-12f));
+      n2 = x.sumsq();
+    }
+    x.scale(exp0_factor(n2, k));
+    {
+      const float n = fmaxf(sqrtf(x.sumsq()), REGCN_EPS);
+      const float rr = fminf(fmaxf(rv, REGCN_EPS), k.rmax);
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) x.v[j] = (x.v[j] / n) * rr;
+    }
+    if (out) x.store(out + t * d, d, lane);
+    const float h2 = x.sumsq();
+    if (lane == 0 && out3) out3[t] = fmaxf(sqrtf(h2), REGCN_EPS);
+    if (out2) {
+      x.scale(log0_factor(h2, k));
+      x.store(out2 + t * d, d, lane);
+    }
+  }
+}
+
+template <int OP>
+static int launch_init(const float* a, const float* vec, int64_t rows, int d, const Curv& k, float* out,
+                       float* out2, float* out3, hipStream_t st, const int32_t* src, const int32_t* dst) {
+  if (rows == 0) return 0;
+  int64_t blocks = (rows + 3) / 4;
+  if (blocks > 8192) blocks = 8192;
+  dim3 g((unsigned)blocks), blk(256);
+  int epl = (d + 63) / 64;
+  if (epl <= 1) hipLaunchKernelGGL((k_init_rows<1, OP>), g, blk, 0, st, a, vec, rows, d, k, out, out2, out3, src, dst);
+  else if (epl <= 2) hipLaunchKernelGGL((k_init_rows<2, OP>), g, blk, 0, st, a, vec, rows, d, k, out, out2, out3, src, dst);
+  else if (epl <= 4) hipLaunchKernelGGL((k_init_rows<4, OP>), g, blk, 0, st, a, vec, rows, d, k, out, out2, out3, src, dst);
+  else if (epl <= 8) hipLaunchKernelGGL((k_init_rows<8, OP>), g, blk, 0, st, a, vec, rows, d, k, out, out2, out3, src, dst);
+  else if (epl <= 16) hipLaunchKernelGGL((k_init_rows<16, OP>), g, blk, 0, st, a, vec, rows, d, k, out, out2, out3, src, dst);
+  else return set_error(REGCN_EINVAL, "row width d=%d exceeds 1024", d);
+  return check_launch("k_init_rows");
+}
+
+// REGCN_INIT_PLAIN=1: the initial state through k_rowmap (no prefetch), for A/B measurements
+static bool init_plain() {
+  static const bool v = [] { const char* e = getenv("REGCN_INIT_PLAIN"); return e && e[0] == '1'; }();
+  return v;
+}
+
 template <int OP>
 static int launch_rowmap(const float* a, const float* b, const float* vec, int64_t rows, int d,
                          const Curv& k, float* out, float* out2, float* out3, hipStream_t st,
@@ -196,6 +272,10 @@ int rowmap(int op, const float* a, const float* b, const float* vec, int64_t row
     case OP_INIT:
     case OP_INIT_LN:
       if (!vec) return set_error(REGCN_EINVAL, "init needs the static radius");
+      if (!init_plain()) {
+        if (op == OP_INIT) return launch_init<OP_INIT>(a, vec, rows, d, k, out, out2, out3, st, nullptr, nullptr);
+        return launch_init<OP_INIT_LN>(a, vec, rows, d, k, out, out2, out3, st, nullptr, nullptr);
+      }
       if (op == OP_INIT) return launch_rowmap<OP_INIT>(a, b, vec, rows, d, k, out, out2, out3, st);
       return launch_rowmap<OP_INIT_LN>(a, b, vec, rows, d, k, out, out2, out3, st);
   }
@@ -209,8 +289,12 @@ int init_rows(const float* dyn, const float* r_static, const int32_t* src, const
   if (n == 0) return 0;
   if (!dyn || !r_static || !src || !x || !r) return set_error(REGCN_EINVAL, "null pointer");
   Curv k = make_curv(c);
-  if (layer_norm) return launch_rowmap<OP_INIT_LN>(dyn, nullptr, r_static, n, d, k, h, x, r, st, src, dst);
-  return launch_rowmap<OP_INIT>(dyn, nullptr, r_static, n, d, k, h, x, r, st, src, dst);
+  if (init_plain()) {
+    if (layer_norm) return launch_rowmap<OP_INIT_LN>(dyn, nullptr, r_static, n, d, k, h, x, r, st, src, dst);
+    return launch_rowmap<OP_INIT>(dyn, nullptr, r_static, n, d, k, h, x, r, st, src, dst);
+  }
+  if (layer_norm) return launch_init<OP_INIT_LN>(dyn, r_static, n, d, k, h, x, r, st, src, dst);
+  return launch_init<OP_INIT>(dyn, r_static, n, d, k, h, x, r, st, src, dst);
 }
 
 
