@@ -205,6 +205,67 @@ __global__ __launch_bounds__(256) void k_init_rows(const float* __restrict__ a, 
   }
 }
 
+// The same map with 16-B accesses: lane l holds elements 4l .. 4l + 3 of the row (d % 4 == 0,
+// d <= 256, 16-B aligned rows), so a row moves in one dwordx4 load and one dwordx4 store per
+// output instead of ceil(d / 64) dword ones; the next row's load is in flight as above.  The
+// row sums run in a different order than k_rowmap's (4 consecutive elements per lane), so the
+// last bits may differ from it.
+__device__ __forceinline__ float sq4(const float4& v) { return v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w; }
+__device__ __forceinline__ void scale4(float4& v, float f) { v.x *= f; v.y *= f; v.z *= f; v.w *= f; }
+
+template <int OP>
+__global__ __launch_bounds__(256) void k_init_rows4(const float* __restrict__ a, const float* __restrict__ vec,
+                                                    int64_t rows, int d, Curv k, float* __restrict__ out,
+                                                    float* __restrict__ out2, float* __restrict__ out3,
+                                                    const int32_t* __restrict__ src, const int32_t* __restrict__ dst) {
+  const int lane = threadIdx.x & 63;
+  const bool on = lane < (d >> 2);
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (i >= rows) return;
+  float4 nx = make_float4(0.f, 0.f, 0.f, 0.f);
+  float nv;
+  {
+    const int64_t r = src ? (int64_t)src[i] : i;
+    if (on) nx = reinterpret_cast<const float4*>(a + r * d)[lane];
+    nv = vec[r];
+  }
+  for (; i < rows; i += nwaves) {
+    float4 x = nx;
+    const float rv = nv;
+    const int64_t nxt = i + nwaves;
+    if (nxt < rows) {
+      const int64_t r = src ? (int64_t)src[nxt] : nxt;
+      if (on) nx = reinterpret_cast<const float4*>(a + r * d)[lane];
+      nv = vec[r];
+    }
+    const int64_t t = dst ? (int64_t)dst[i] : i;
+    float n2 = wave_sum(sq4(x));
+    if (OP == OP_INIT_LN) {
+      scale4(x, 1.0f / fmaxf(sqrtf(n2), 1e-12f));
+      n2 = wave_sum(sq4(x));
+    }
+    scale4(x, exp0_factor(n2, k));
+    {
+      const float n = fmaxf(sqrtf(wave_sum(sq4(x))), REGCN_EPS);
+      const float rr = fminf(fmaxf(rv, REGCN_EPS), k.rmax);
+      x.x = (x.x / n) * rr;
+      x.y = (x.y / n) * rr;
+      x.z = (x.z / n) * rr;
+      x.w = (x.w / n) * rr;
+    }
+    if (out && on) reinterpret_cast<float4*>(out + t * d)[lane] = x;
+    const float h2 = wave_sum(sq4(x));
+    if (lane == 0 && out3) out3[t] = fmaxf(sqrtf(h2), REGCN_EPS);
+    if (out2) {
+      scale4(x, log0_factor(h2, k));
+      if (on) reinterpret_cast<float4*>(out2 + t * d)[lane] = x;
+    }
+  }
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 template <int OP>
 static int launch_init(const float* a, const float* vec, int64_t rows, int d, const Curv& k, float* out,
                        float* out2, float* out3, hipStream_t st, const int32_t* src, const int32_t* dst) {
@@ -212,6 +273,10 @@ static int launch_init(const float* a, const float* vec, int64_t rows, int d, co
   int64_t blocks = (rows + 3) / 4;
   if (blocks > 8192) blocks = 8192;
   dim3 g((unsigned)blocks), blk(256);
+  if (d % 4 == 0 && d <= 256 && aligned16(a) && (!out || aligned16(out)) && (!out2 || aligned16(out2))) {
+    hipLaunchKernelGGL((k_init_rows4<OP>), g, blk, 0, st, a, vec, rows, d, k, out, out2, out3, src, dst);
+    return check_launch("k_init_rows4");
+  }
   int epl = (d + 63) / 64;
   if (epl <= 1) hipLaunchKernelGGL((k_init_rows<1, OP>), g, blk, 0, st, a, vec, rows, d, k, out, out2, out3, src, dst);
   else if (epl <= 2) hipLaunchKernelGGL((k_init_rows<2, OP>), g, blk, 0, st, a, vec, rows, d, k, out, out2, out3, src, dst);

@@ -2,7 +2,7 @@
 tools/simprobe.py / bench.py: the dispatches from the `--from`-th launch of the marker kernel
 (default: the initial-state kernel, one per step; the first is the warm-up step) to the end.
 
-  python tools/simprof_summary.py <results.db> [--marker k_init_rows<4, 11>] [--from 1] [--steps 3]
+  python tools/simprof_summary.py <results.db> [--marker k_init_rows4<11>] [--from 1] [--steps 3]
 """
 import argparse
 import sqlite3
@@ -11,7 +11,7 @@ import sqlite3
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
-    ap.add_argument("--marker", default="k_init_rows<4, 11>")
+    ap.add_argument("--marker", default="k_init_rows4<11>")
     ap.add_argument("--from", dest="start", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--top", type=int, default=45)
