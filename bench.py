@@ -707,7 +707,7 @@ SCALE_KERNEL = {  # library call -> its main kernel (rocprof / PMC name)
     "regcn_roth_queries_f32": "k_queries4",
     "regcn_relation_gru_x_f32": "k_rel_gru_x",
     "regcn_relation_gru_pre_f32": "k_rel_gru_pre",
-    "regcn_init_entities_f32": "k_init_entities",
+    "regcn_init_entities_f32": "k_init_rows4<11>",
 }
 
 
