@@ -689,6 +689,240 @@ def run_small(args, cfg, world, rank, device, backend, extras=True):
     return out
 
 
+def run_regcn(args, cfg, world, rank, device, backend):
+    """BASELINE.json configs[0]: the Euclidean RE-GCN (`RecurrentRGCN` + ConvTransE / ConvTransR,
+    src/rrgcn.py:142-194, src/decoder.py:10-100) at ICEWS14s' shape (|V| = 7,128, R = 230, 246
+    triples per snapshot, history 3, d = 200, the reference's ICEWS14s command: self-loop, layer
+    norm).  A step is one `predict`; a pool of 16 independent predicts is captured into one HIP
+    graph and whole pool passes are timed.  The CPU baseline is the oracle's `euclid_predict`
+    (oracle/model.py:330) on the host cores, and the MRR of both on the same sample is compared."""
+    from regcn_amd import graph as G
+    from regcn_amd.rrgcn import RecurrentRGCN
+    from regcn_amd.synthetic import snapshot_series
+    d, V, R, T = args.d, cfg["V"], cfg["R"], cfg["T"]
+    pool_n = args.pool or 16
+    torch.manual_seed(1234)
+    model = RecurrentRGCN("convtranse", "uvrgcn", V, R, 0, 0, d, "sub", T, num_bases=cfg["n_bases"],
+                          num_basis=cfg["n_bases"], num_hidden_layers=2, dropout=0.2, self_loop=True,
+                          layer_norm=True, input_dropout=0.2, hidden_dropout=0.2, feat_dropout=0.2,
+                          entity_prediction=True, relation_prediction=True, use_cuda=True, gpu=0)
+    model = model.to(device).eval()
+    snaps = snapshot_series(100 + 7919 * rank, V, R, T + pool_n, cfg["per_snap"])
+    samples = []
+    for i in range(pool_n):
+        glist = [G.build_sub_graph(V, R, s, True, device) for s in snaps[i:i + T]]
+        samples.append((snaps[i:i + T], glist, torch.from_numpy(snaps[i + T]).to(device), snaps[i + T]))
+
+    def eager(i):
+        _, glist, test, _ = samples[i]
+        return model.predict(glist, R, None, test, True)
+
+    cap = torch.cuda.Stream(device)
+    with torch.no_grad():
+        for i in range(len(samples)):
+            eager(i)
+        torch.cuda.synchronize()
+        pool_graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(cap):
+            for i in range(len(samples)):
+                eager(i)  # warm the capture stream's allocator pool
+            torch.cuda.synchronize()
+            with torch.cuda.graph(pool_graph, stream=cap):
+                for i in range(len(samples)):
+                    eager(i)
+    pool_graph.replay()
+    torch.cuda.synchronize()
+    steps = -(-args.steps // len(samples)) * len(samples)
+    epw = [edges_per_step(s[1]) for s in samples]
+    edges_local = sum(epw) * (steps // len(samples))
+
+    def run_steps():
+        for _ in range(steps // len(samples)):
+            pool_graph.replay()
+
+    elapsed, edges_total = _timed(world, device, backend, run_steps, edges_local)
+    value = edges_total / elapsed / 1e6
+    out = None
+    if rank == 0:
+        cpu = mrr = None
+        if not args.no_cpu_baseline and world == 1:
+            sys.path.insert(0, REPO)
+            from oracle import graph as OG
+            from oracle import model as OM
+            torch.set_num_threads(cpu_threads())
+            hist, glist, test, test_np = samples[0]
+            sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+            og = [OG.build_sub_graph(V, R, s) for s in hist]
+            times = []
+            t_end = time.time() + args.cpu_budget
+            with torch.no_grad():
+                while True:
+                    t0 = time.time()
+                    o_tr, o_score, o_score_rel = OM.euclid_predict(sd, dict(layer_norm=True, n_layers=2), og,
+                                                                    torch.from_numpy(test_np))[:3]
+                    times.append(time.time() - t0)
+                    if time.time() > t_end or len(times) >= 5:
+                        break
+                _, score, score_rel = model.predict(glist, R, None, test, True)
+            per = float(np.mean(times))
+            cpu = dict(value=epw[0] / per / 1e6, unit="M edges/s", cores=torch.get_num_threads(), kind="port",
+                       **cpu_info(), sample="%d x oracle euclid_predict (%s, history %d, %d queries); %.3f s each"
+                       % (len(times), cfg["label"], T, 2 * len(test_np), per))
+            mrr = {}
+            for name, got, ref, rel in (("entity", score, o_score, False), ("relation", score_rel, o_score_rel, True)):
+                ans = OM.answers_for_filter(test_np, R, rel_p=rel)
+                f_g, r_g = OM.total_rank(o_tr, got.float().cpu(), ans, rel)[:2]
+                f_o, r_o = OM.total_rank(o_tr, ref.float(), ans, rel)[:2]
+                mrr[name] = {"raw_hip": round(r_g, 6), "raw_oracle": round(r_o, 6), "filtered_hip": round(f_g, 6),
+                             "filtered_oracle": round(f_o, 6),
+                             "max_abs_delta": round(max(abs(r_g - r_o), abs(f_g - f_o)), 6)}
+            mrr["tolerance"] = 0.002
+        out = {"metric": METRIC, "value": round(value, 3), "unit": "M edges/s", "n_gpus": world, "steps": steps,
+               "warmup": args.warmup, "ms_per_step": round(elapsed / steps * 1e3, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic (ICEWS14s-shaped snapshots, random-init weights)",
+               "config": {"workload": cfg["label"] + " (BASELINE.json configs[0]): RecurrentRGCN.predict, "
+                          "layer norm, self-loop, ConvTransE + ConvTransR", "V": V, "R": R,
+                          "triples_per_snapshot": cfg["per_snap"], "history_len": T, "n_layers": 2, "d": d,
+                          "edges_per_step": int(np.mean(epw)), "queries_per_step": 2 * cfg["per_snap"],
+                          "hip_graph": True, "steps_per_graph_launch": len(samples),
+                          "parallelism": "replicas x%d" % world},
+               "cpu_baseline": cpu, "mrr_parity": mrr}
+    del pool_graph, samples, model
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+# ------------------------------------------------------------------------ the printed line
+LINE_LIMIT = 8192  # bytes: the driver parses the last stdout line from a bounded tail
+
+
+def _rnd(x, n=4):
+    return None if x is None else round(float(x), n)
+
+
+def _cpu_short(c):
+    if not c:
+        return None
+    return {"value": _rnd(c["value"], 6), "unit": c["unit"], "cores": c["cores"], "kind": c["kind"],
+            "sample": c["sample"][:160], "cpu_model": c.get("cpu_model")}
+
+
+def _roof_short(r, kernels=None):
+    if not r:
+        return None
+    keep = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic", "traffic_GBps", "traffic_frac",
+            "avg_launch_us", "launches_per_step", "algorithmic_bytes_per_launch", "flops_per_launch")
+    s = {k: r[k] for k in keep if r.get(k) is not None}
+    for k in ("algorithmic_bytes_per_launch", "flops_per_launch"):
+        if k in s:
+            s[k] = float("%.4g" % s[k])
+    if s.get("traffic"):
+        s["traffic_unit"] = "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, %s)" % (
+            (r.get("traffic_source") or "profiles/").split(" ")[0])
+    l2 = (kernels or {}).get(r.get("call"), {}).get("l2_request_stream")
+    if l2:
+        s["l2_request_stream"] = {"requests_per_launch": float("%.4g" % l2["requests_per_launch"]),
+                                  "achieved_TBps": l2["achieved_TBps"], "ceiling_TBps": l2["ceiling_TBps"],
+                                  "frac": l2["frac"]}
+    return s
+
+
+def _leg_short(r):
+    s = {k: r.get(k) for k in ("value", "ms_per_step", "latency_ms_per_predict") if r.get(k) is not None}
+    rf = r.get("roofline")
+    if rf:
+        s["roofline"] = {k: rf.get(k) for k in ("kernel", "bound", "frac", "avg_launch_us")}
+    c = r.get("cpu_baseline")
+    if c:
+        s["cpu_baseline"] = {"value": _rnd(c["value"], 7), "cores": c["cores"], "kind": c["kind"]}
+    m = r.get("mrr_parity")
+    if m:
+        s["mrr_max_abs_delta"] = max(m[k]["max_abs_delta"] for k in ("entity", "relation") if k in m)
+    return s
+
+
+def compact_line(out, detail_path=None):
+    """The bench line the driver parses (<= LINE_LIMIT bytes): the contract keys, the headline's
+    roofline and cpu_baseline, a one-line owner simulation, each dataset leg's value, roofline
+    fraction and cpu_baseline.  The full record (per-call kernels, rooflines at scale, per-rank
+    arrays) goes to `detail_path`."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    line = {k: out.get(k) for k in keep}
+    cfg = {k: v for k, v in (out.get("config") or {}).items() if k != "snapshot_stats"}
+    if isinstance(cfg.get("workload"), str):
+        cfg["workload"] = cfg["workload"][:220]
+    line["config"] = cfg
+    line["roofline"] = _roof_short(out.get("roofline"), out.get("kernels"))
+    line["cpu_baseline"] = _cpu_short(out.get("cpu_baseline"))
+    if out.get("latency_ms_per_predict") is not None:
+        line["latency_ms_per_predict"] = out["latency_ms_per_predict"]
+    b = out.get("breakdown") or {}
+    if "encoder_ms_per_step" in b:
+        line["breakdown"] = {"encoder_ms_per_step": b["encoder_ms_per_step"],
+                             "decoder_ms_per_step": b.get("decoder_ms_per_step")}
+    kern = out.get("kernels") or {}
+    if kern and "avg_us" in next(iter(kern.values())):
+        top = sorted(kern.items(), key=lambda kv: -kv[1]["avg_us"] * kv[1].get("per_step", 1))[:6]
+        line["top_calls_us"] = {k: [v["avg_us"], v.get("per_step"), v.get("frac")] for k, v in top}
+    sim = out.get("owner_simulation")
+    if sim:
+        line["owner_simulation"] = {
+            "world": sim["world"], "predicted_step_ms": sim["predicted_step_ms"],
+            "speedup_vs_headline": sim.get("predicted_speedup_vs_headline"), "max_rank_ms": sim["max_rank_ms"],
+            "mean_rank_ms": sim["mean_rank_ms"], "sum_rank_ms": round(sim["mean_rank_ms"] * sim["world"], 3),
+            "exposed_exchange_ms": sim["exposed_exchange_ms_per_step"], "replicated_ms": sim["replicated_ms"],
+            "halo_delivery_ms_excluded": sim.get("halo_delivery_ms_excluded"), "blocker_margin_ms": sim.get("blocker_margin_ms")}
+    ag = out.get("aggregation_roofline")
+    if ag:
+        u = ag.get("uniform_src", {}).get("union_aggregate", {})
+        z = ag.get("zipf_src", {}).get("union_aggregate", {})
+        line["aggregation_roofline"] = {"union_uniform_src": {"frac": u.get("frac"), "traffic_frac": u.get("traffic_frac"),
+                                                              "avg_launch_us": u.get("avg_launch_us")},
+                                        "union_zipf_src": {"frac": z.get("frac"), "traffic_frac": z.get("traffic_frac"),
+                                                           "avg_launch_us": z.get("avg_launch_us")}}
+    dr = out.get("decoder_roofline")
+    if dr:
+        line["decoder_roofline"] = {"score_frac": dr["score"]["frac"], "ce_frac": dr["cross_entropy"]["frac"],
+                                    "score_us": dr["score"]["avg_launch_us"]}
+    for k in ("replicas", "edge_partition"):
+        if out.get(k):
+            line[k] = {kk: out[k][kk] for kk in ("value", "ms_per_step", "scaling", "parallelism") if kk in out[k]}
+    if out.get("mrr_parity"):
+        m = out["mrr_parity"]
+        line["mrr_parity"] = {"max_abs_delta": max(m[k]["max_abs_delta"] for k in ("entity", "relation") if k in m),
+                              "tolerance": m.get("tolerance"), "workload": (m.get("workload") or "")[:60]}
+    legs = {k: _leg_short(out[k]) for k in LEGS if isinstance(out.get(k), dict)}
+    if legs:
+        line["legs"] = legs
+    if detail_path:
+        line["detail"] = detail_path
+    s = json.dumps(line, separators=(",", ":"))
+    for drop in ("top_calls_us", "aggregation_roofline", "decoder_roofline", "breakdown"):
+        if len(s) <= LINE_LIMIT:
+            break
+        line.pop(drop, None)
+        s = json.dumps(line, separators=(",", ":"))
+    return s
+
+
+def write_detail(out):
+    """The full record beside the line (BENCH_DETAIL, default gpurun_out/bench_detail.json)."""
+    path = os.environ.get("BENCH_DETAIL", os.path.join("gpurun_out", "bench_detail.json"))
+    try:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "w") as fh:
+            json.dump(out, fh)
+        return path
+    except OSError:
+        return None
+
+
+LEGS = ("icews14s", "icews14s_regcn", "icews18", "gdelt", "gdelt_lgcn")
+
+
 # --------------------------------------------------------------------------- config 5
 SCALE_KERNEL = {  # library call -> its main kernel (rocprof / PMC name)
     "regcn_union_aggregate_f32": "k_union_runs<false, false>",
@@ -1257,13 +1491,19 @@ def main():
         if world == 1 and not args.no_extras:
             # the dataset configs (BASELINE.json configs[1..3]) as legs of the N = 1 line; GDELT
             # (configs[3], history 7) for both encoders, each with its CPU baseline
-            for key, name, enc in (("icews14s", "icews14s_lgcn_roth", None), ("icews18", "icews18_roth", None),
+            for key, name, enc in (("icews14s", "icews14s_lgcn_roth", None),
+                                   ("icews14s_regcn", "icews14s_uvrgcn_convtranse", None),
+                                   ("icews18", "icews18_roth", None),
                                    ("gdelt", "gdelt", None), ("gdelt_lgcn", "gdelt", "lgcn")):
-                sub = parse(["--config", name, "--steps", "64", "--warmup", "4", "--cpu-budget", "10"]
-                            + (["--no-cpu-baseline"] if name == "icews18_roth" else []))
+                sub = parse(["--config", name, "--steps", "64", "--warmup", "4", "--cpu-budget", "10"])
                 c = dict(CONFIGS[name])
                 if enc:
                     c.update(encoder=enc, label=c["label"] + ", encoder=" + enc)
+                if key == "icews14s_regcn":
+                    r = run_regcn(sub, c, world, rank, device, backend)
+                    if rank == 0:
+                        out[key] = r
+                    continue
                 r = run_small(sub, c, world, rank, device, backend)
                 if rank == 0:
                     out[key] = {k: r[k] for k in ("value", "unit", "ms_per_step", "latency_ms_per_predict",
@@ -1276,6 +1516,8 @@ def main():
                             out["mrr_parity"] = mp
                         else:
                             out[key]["mrr_parity"] = mp
+    elif cfg["decoder"] == "convtranse":
+        out = run_regcn(args, cfg, world, rank, device, backend)
     else:
         out = run_small(args, cfg, world, rank, device, backend)
         if world > 1 and args.shard == "replica" and not args.no_extras:
@@ -1292,7 +1534,7 @@ def main():
             out["aggregation_roofline"] = aggregation_at_scale(device)
             out["decoder_roofline"] = decoder_at_scale()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(compact_line(out, write_detail(out)), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()

@@ -95,14 +95,13 @@ __device__ __forceinline__ void gru_pre_block(const RelGru2Args& p, int bx, int 
   f4* red = reinterpret_cast<f4*>(lds + TM * lda);  // [PRE_WAVES][3][64]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (w >= PRE_WAVES) {  // waves beyond the part's four (a wider phase launch) only meet its barriers
-    __syncthreads();
-    __syncthreads();
-    return;
-  }
+  // Every wave of the workgroup runs this whole body and so meets every one of its barriers;
+  // waves beyond the part's four (an 8-wave phase launch hosting it) only skip the work
+  // between them (`act` is wave-uniform).
+  const bool act = w < PRE_WAVES;
   const int r0 = bx * TM, jt = by;
   const int n_valid = min(TM, p.R2 - r0);
-  {  // [emb_rel | h_prev] rows as float4s, every load issued before the first LDS store
+  if (act) {  // [emb_rel | h_prev] rows as float4s, every load issued before the first LDS store
     constexpr int IT = TM * 2 * (MAX_D / 4) / (64 * PRE_WAVES);
     const int q4 = d >> 2, n = TM * 2 * q4;
     f4 v[IT];
@@ -133,19 +132,22 @@ __device__ __forceinline__ void gru_pre_block(const RelGru2Args& p, int bx, int 
     }
   }
   __syncthreads();
-  const bool hh = w >= PRE_WAVES / 2;
-  const int wi = hh ? w - PRE_WAVES / 2 : w;
-  const int NB = dp >> 4, NT = dp >> 4;
-  const int beg = (NB * wi) / (PRE_WAVES / 2), end = (NB * (wi + 1)) / (PRE_WAVES / 2);
-  const f4* bb = reinterpret_cast<const f4*>(hh ? p.w_hh : p.w_ih_e) + (int64_t)jt * 64 + lane;
-  const int64_t gs = (int64_t)NB * NT * 64;
-  f4 ar = {0.f, 0.f, 0.f, 0.f}, az = ar, an = ar;
-  const float* arow = A + (lane & 15) * lda + 4 * (lane >> 4) + (hh ? dp : 0);
-  if (beg < end) gru_mfma(arow, bb, gs, NT, beg, end, ar, az, an);
-  red[(w * 3 + 0) * 64 + lane] = ar;
-  red[(w * 3 + 1) * 64 + lane] = az;
-  red[(w * 3 + 2) * 64 + lane] = an;
+  if (act) {
+    const bool hh = w >= PRE_WAVES / 2;
+    const int wi = hh ? w - PRE_WAVES / 2 : w;
+    const int NB = dp >> 4, NT = dp >> 4;
+    const int beg = (NB * wi) / (PRE_WAVES / 2), end = (NB * (wi + 1)) / (PRE_WAVES / 2);
+    const f4* bb = reinterpret_cast<const f4*>(hh ? p.w_hh : p.w_ih_e) + (int64_t)jt * 64 + lane;
+    const int64_t gs = (int64_t)NB * NT * 64;
+    f4 ar = {0.f, 0.f, 0.f, 0.f}, az = ar, an = ar;
+    const float* arow = A + (lane & 15) * lda + 4 * (lane >> 4) + (hh ? dp : 0);
+    if (beg < end) gru_mfma(arow, bb, gs, NT, beg, end, ar, az, an);
+    red[(w * 3 + 0) * 64 + lane] = ar;
+    red[(w * 3 + 1) * 64 + lane] = az;
+    red[(w * 3 + 2) * 64 + lane] = an;
+  }
   __syncthreads();
+  if (!act) return;  // past the last barrier
   const int q = w;  // PRE_WAVES == 4: wave q finishes C register q (row 4 (lane >> 4) + q)
   float sr = 0.f, sz = 0.f, sn_i = 0.f, sn_h = 0.f;
 #pragma unroll
@@ -170,8 +172,9 @@ __device__ __forceinline__ void gru_pre_block(const RelGru2Args& p, int bx, int 
 // The tile's r_to_e items are flattened (row-sorted) and split into contiguous ranges per
 // wave; each wave keeps 8 row loads in flight and reduces segment-wise into partial slot
 // (row + wave); partials are combined in wave order (deterministic), then / count.
+// Every wave calls it (its one barrier); waves with !act only meet the barrier.
 __device__ __forceinline__ void stage_rel_means(const RelGru2Args& p, float* A, int lda, float* part, int* tmask,
-                                                int r0, int n_valid) {
+                                                int r0, int n_valid, bool act) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int d = p.d, col = lane * 4, colc = min(col, d - 4);
   const bool active = col < d;
@@ -185,7 +188,7 @@ __device__ __forceinline__ void stage_rel_means(const RelGru2Args& p, float* A, 
     off[i] = total;
     total += __builtin_amdgcn_readlane(cnt_l, i);
   }
-  const int ib = (total * w) / X_WAVES, ie = (total * (w + 1)) / X_WAVES;
+  const int ib = act ? (total * w) / X_WAVES : 0, ie = act ? (total * (w + 1)) / X_WAVES : 0;
   const f4 zero = {0.f, 0.f, 0.f, 0.f};
   int cur = -1;
   unsigned mask = 0;
@@ -231,8 +234,9 @@ __device__ __forceinline__ void stage_rel_means(const RelGru2Args& p, float* A, 
     }
   }
   flush();
-  if (lane == 0) tmask[w] = (int)mask;
+  if (act && lane == 0) tmask[w] = (int)mask;
   __syncthreads();
+  if (!act) return;
   for (int i = w; i < TM; i += X_WAVES) {
     f4 s = zero;
 #pragma unroll
@@ -258,45 +262,46 @@ __device__ __forceinline__ void gru_x_block(const RelGru2Args& p, int bx, int by
   int* tmask = reinterpret_cast<int*>(red + X_WAVES * 3 * 64);
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (w >= X_WAVES) {  // as in gru_pre_block: three barriers on either staging path
-    __syncthreads();
-    __syncthreads();
-    __syncthreads();
-    return;
-  }
+  // as in gru_pre_block: every wave meets every barrier, waves past the part's four skip the work
+  const bool act = w < X_WAVES;
   const int r0 = bx * TM, jt = by;
   const int n_valid = min(TM, p.R2 - r0);
   const int NB = dp >> 4, NT = dp >> 4;
   const int beg = (NB * w) / X_WAVES, end = (NB * (w + 1)) / X_WAVES;
   const int ei = 4 * (lane >> 4) + w;  // this lane's output element (wave w finishes C register w)
   const int en = 16 * jt + (lane & 15);
-  const bool eok = ei < n_valid && en < d;
+  const bool eok = act && ei < n_valid && en < d;
   const int64_t erow = (int64_t)(r0 + (eok ? ei : 0));
   const int ecol = eok ? en : 0;
   const float* pr = p.pre + erow * 4 * d;
   const float pre0 = pr[ecol], pre1 = pr[d + ecol], pre2 = pr[2 * d + ecol], pre3 = pr[3 * d + ecol];
   const float hprev = p.h_prev[erow * d + ecol];
   // zero A (padding columns and absent relations stay 0), then the means
-  for (int t = threadIdx.x; t < TM * lda; t += 64 * X_WAVES) A[t] = 0.f;
+  if (act)
+    for (int t = threadIdx.x; t < TM * lda; t += 64 * X_WAVES) A[t] = 0.f;
   if (p.x_mean) {
     __syncthreads();
-    for (int t = threadIdx.x; t < n_valid * d; t += 64 * X_WAVES) {
-      const int i = t / d, k = t - i * d;
-      A[i * lda + k] = p.x_mean[(int64_t)(r0 + i) * d + k];
-    }
+    if (act)
+      for (int t = threadIdx.x; t < n_valid * d; t += 64 * X_WAVES) {
+        const int i = t / d, k = t - i * d;
+        A[i * lda + k] = p.x_mean[(int64_t)(r0 + i) * d + k];
+      }
   } else {
-    stage_rel_means(p, A, lda, part, tmask, r0, n_valid);
+    stage_rel_means(p, A, lda, part, tmask, r0, n_valid, act);
   }
   __syncthreads();
-  const f4* bb = reinterpret_cast<const f4*>(p.w_ih_x) + (int64_t)jt * 64 + lane;
-  const int64_t gs = (int64_t)NB * NT * 64;
-  f4 ar = {0.f, 0.f, 0.f, 0.f}, az = ar, an = ar;
-  const float* arow = A + (lane & 15) * lda + 4 * (lane >> 4);
-  if (beg < end) gru_mfma(arow, bb, gs, NT, beg, end, ar, az, an);
-  red[(w * 3 + 0) * 64 + lane] = ar;
-  red[(w * 3 + 1) * 64 + lane] = az;
-  red[(w * 3 + 2) * 64 + lane] = an;
+  if (act) {
+    const f4* bb = reinterpret_cast<const f4*>(p.w_ih_x) + (int64_t)jt * 64 + lane;
+    const int64_t gs = (int64_t)NB * NT * 64;
+    f4 ar = {0.f, 0.f, 0.f, 0.f}, az = ar, an = ar;
+    const float* arow = A + (lane & 15) * lda + 4 * (lane >> 4);
+    if (beg < end) gru_mfma(arow, bb, gs, NT, beg, end, ar, az, an);
+    red[(w * 3 + 0) * 64 + lane] = ar;
+    red[(w * 3 + 1) * 64 + lane] = az;
+    red[(w * 3 + 2) * 64 + lane] = an;
+  }
   __syncthreads();
+  if (!act) return;  // past the last barrier
   const int q = w;  // X_WAVES == 4: wave q finishes C register q
   float v[3];
 #pragma unroll

@@ -509,8 +509,8 @@ __device__ __forceinline__ void rt_store(const RAcc<NT>& a, float* __restrict__ 
     // one row address per row; the column tiles are immediate offsets (16 t floats)
     float* row = M + (int64_t)crow[r] * d + (lane & 15);
 #pragma unroll
-    for (int t = 0; t < NT; ++t)  // NT = ceil(d / 16): only the last tile has pad columns
-      if (t < NT - 1 || 16 * t + (lane & 15) < d) row[16 * t] = a.t[t][r];
+    for (int t = 0; t < NT; ++t)  // a tile wholly inside d stores unmasked (a wave-uniform test)
+      if (16 * t + 15 < d || 16 * t + (lane & 15) < d) row[16 * t] = a.t[t][r];
   }
 }
 
@@ -573,7 +573,7 @@ __device__ __forceinline__ void rt_send_rows(const RAcc<NT>& a, const LayerArgs&
       float* dst = p.send_x + (int64_t)p.send_pos[sl] * d + (lane & 15);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-        if (t < NT - 1 || 16 * t + (lane & 15) < d) dst[16 * t] = a.t[t][r];
+        if (16 * t + 15 < d || 16 * t + (lane & 15) < d) dst[16 * t] = a.t[t][r];
     }
   }
 }
@@ -659,7 +659,7 @@ __device__ __forceinline__ void rt_store_staged(const RAcc<NT>& a, float* __rest
 #pragma unroll
     for (int t = stage * RT_SC_TILES; t < min(NT, (stage + 1) * RT_SC_TILES); ++t) {
       const int cl = 16 * t + (lane & 15) - c0;
-      if (t < NT - 1 || cl < ncols) {  // only the last column tile reaches past d
+      if (16 * t + 15 - c0 < ncols || cl < ncols) {  // tiles reaching past d are masked per lane
 #pragma unroll
         for (int r = 0; r < 4; ++r) st[(4 * q + r) * ncols + cl] = a.t[t][r];
       }
@@ -739,13 +739,13 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stage's copies have landed
         }
         const int col = 16 * t + (lane & 15);
-        const int ncols = min(RT_SC_COLS, d - RT_SC_COLS * stage), cl = min(col - RT_SC_COLS * stage, ncols - 1);
+        const int ncols = min(RT_SC_COLS, d - RT_SC_COLS * stage), cl = max(0, min(col - RT_SC_COLS * stage, ncols - 1));
         const f4 c4 = clamp4(v.t[t], -10.f, 10.f);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          // rows past n_valid were staged as zeros (and are never stored); only the last tile's
-          // pad columns (cl clamped onto a real column) need the select
-          const bool ok = t < NT - 1 || col < d;
+          // rows past n_valid were staged as zeros (and are never stored); only the pad columns
+          // of a tile reaching past d (cl clamped onto a real column) need the select
+          const bool ok = 16 * t + 15 < d || col < d;
           const float xp = xs[(4 * q + r) * ncols + cl];
           const float zt = zs[(4 * q + r) * ncols + cl];
           const float pr = fminf(fmaxf(ok ? xp : 0.f, -10.f), 10.f);

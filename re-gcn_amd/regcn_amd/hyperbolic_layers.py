@@ -113,11 +113,11 @@ def _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c):
     stride = d + 4
     part = torch.empty(max(g.heavy_slots, 1), stride, device=x.device, dtype=torch.float32)
     f, i = _lib.fptr, _lib.iptr
-    halo = getattr(g, "gather_cols", None)  # a rank's HaloView: remote sources read from its halo rows
+    halo = getattr(g, "hub_cols", None)  # a rank's HaloView: remote sources read from its halo rows
     if mode == _lib.AGG_LORENTZ:  # hub rows: edges in type order, same-type runs reuse rel/W from L1
         cs, ct = g.row_type_cols()
         if halo is not None:
-            cs = halo(cs, g.row_src_cols())[0]
+            cs, ct, _, hc = halo(cs, ct, None, hc)
         _lib.call("regcn_lorentz_aggregate_f32", f(x), f(rel), f(w_rel), i(cs), i(ct), i(hc),
                   hc.shape[0], i(hf), hf.shape[0], nb, float(c), d, f(part), stride, f(agg), _lib.stream())
     else:  # union / Euclid: relation half over type runs, source half over source runs
@@ -130,7 +130,7 @@ def _heavy_aggregate(mode, g, x, r, rel, w_rel, nb, gamma, c):
             hc, hf, n_slots = hb
             part = torch.empty(n_slots, stride, device=x.device, dtype=torch.float32)
         if halo is not None:
-            cs, ss = halo(cs, ss)
+            cs, ct, ss, hc = halo(cs, ct, ss, hc)
         _lib.call("regcn_union_aggregate_src_runs_f32", f(x), None if euclid else f(r), f(rel), i(cs), i(ct), i(ss),
                   f(wk["norm"]), i(hc), hc.shape[0], i(hf), hf.shape[0], float(gamma), int(euclid), d, f(part), stride,
                   f(agg), _lib.stream())

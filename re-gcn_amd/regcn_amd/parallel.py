@@ -187,13 +187,13 @@ class HaloView:
     lists that another rank owns is replaced by the index of its row in the rank's halo (the
     rows after the Vp owned ids, where the sparse exchange's all_to_alls land the received x
     and |h| rows in place: no scatter on the receiving side).  Owned ids are unchanged.  The
-    hub pass keeps the base view's chunk lists (positions, cut at the ORIGINAL source blocks:
-    `hub_owner`) and reads the remapped row/type and row/source columns (`gather_cols`)."""
+    hub pass keeps the base view's chunk lists (cut at the ORIGINAL source blocks: `hub_owner`),
+    rebased onto compacted, remapped copies of its hub rows' spans (`hub_cols`)."""
 
     def __init__(self, view, remap):
         self.v, self.remap = view, remap
         self.hub_owner = view
-        self._work = self._cols = None
+        self._work = None
 
     def __getattr__(self, name):
         return getattr(self.__dict__["v"], name)
@@ -216,13 +216,39 @@ class HaloView:
             t = self.__dict__["_item_type"] = (src, tl)
         return t
 
-    def gather_cols(self, cs, ss):
-        """(row/type order sources, row/source order sources) remapped (full-length copies;
-        the hub pass reads its rows' spans of them)."""
-        if self._cols is None:
-            self._cols = (self.remap[cs.long()].to(torch.int32), self.remap[ss.long()].to(torch.int32))
-            _lib.publish()
-        return self._cols
+    def hub_cols(self, cs, ct, ss, hc):
+        """The hub pass's columns for this view: only the spans of the hub rows that chunk list
+        `hc` names (the rank's own hub rows, a fraction of the snapshot's edges), compacted --
+        row/type order sources remapped to halo rows, their types, row/source order sources
+        remapped (ss may be None) -- and `hc` with its positions rebased onto the compacted
+        arrays.  Cached per chunk list; int64 temporaries are hub-edge sized, not E sized."""
+        cache = self.__dict__.setdefault("_hub_cols", {})
+        key = (hc.data_ptr(), ss is None)
+        hit = cache.get(key)
+        if hit is not None:
+            return hit
+        if not hc.numel():
+            out = cache[key] = (cs[:0], ct[:0], None if ss is None else ss[:0], hc)
+            return out
+        rowptr = self.v.g.work()["rowptr"]
+        rows = hc[:, 0].long()
+        urows = torch.unique(rows)
+        st = rowptr[urows].long()
+        ln = rowptr[urows + 1].long() - st
+        off = torch.cumsum(ln, 0) - ln
+        n = int(ln.sum())
+        pos = torch.repeat_interleave(st - off, ln) + torch.arange(n, device=st.device)  # global position of slot i
+        cs_c = self.remap[cs[pos].long()].to(torch.int32)
+        ct_c = ct[pos].contiguous()
+        ss_c = None if ss is None else self.remap[ss[pos].long()].to(torch.int32)
+        shift = (off - st)[torch.searchsorted(urows, rows)].to(torch.int32)
+        hc2 = hc.clone()
+        hc2[:, 1] += shift
+        hc2[:, 2] += shift
+        del pos
+        _lib.publish()
+        out = cache[key] = (cs_c, ct_c, ss_c, hc2)
+        return out
 
 
 # ------------------------------------------------------------------ sparse exchange

@@ -3,8 +3,9 @@ own synthetic snapshot) pinned against the oracle row by row.
 
 The whole-graph oracle does not fit this size in a test, so ~4.1k rows are pinned: the largest
 hubs (4.5M, 2.5M in-edges: the hub pass of k_union_runs / the heavy-row reduction), hubs of
-rank 10 / 100 / 1000, 4,000 random rows with in-edges (the inline tiles) and 64 rows without
-(W_evolve).  Their oracle outputs come from oracle.graph.row_subgraph (the rows' in-edges with
+rank 10 / 100 / 1000, 4,000 random rows with in-edges (the inline tiles), the rows of 24 random
+crel tiles (>= 2,048 inline items each: the rowtail gather's k_gather_crel, asserted to run) and
+64 rows without (W_evolve).  Their oracle outputs come from oracle.graph.row_subgraph (the rows' in-edges with
 the full graph's in-degrees) through oracle.layers.union_layer / lorentz_layer in float64, the
 messages materialised 2^18 edges at a time.  Both device paths are checked: the 64-row tail
 (regcn_layer_rowtail_f32, the default at this size) and the fused 16-row kernel
@@ -33,9 +34,20 @@ def case():
     deg = np.bincount(snap[:, 2], minlength=V) + np.bincount(snap[:, 0], minlength=V)
     order = np.argsort(-deg, kind="stable")
     rng = np.random.default_rng(5)
+    # rows of the crel gather's tiles (>= CREL_MIN_ITEMS inline items per tile, k_gather_crel:
+    # the relation half as one MFMA product per tile), which the rowtail path takes by default
+    from regcn_amd import hyperbolic_layers as HL
+    wk = g.work()
+    tiles = wk["tiles"][:g.n_pos_tiles].cpu().numpy()
+    big = np.flatnonzero(np.diff(wk["item_ptr"][:g.n_pos_tiles + 1].cpu().numpy()) >= HL.CREL_MIN_ITEMS)
+    assert len(big) >= HL.CREL_MIN_TILES
+    prow = wk["rows"].cpu().numpy()
+    crel_rows = np.concatenate([prow[tiles[t, 0]:tiles[t, 0] + tiles[t, 1]]
+                                for t in rng.choice(big, 24, replace=False)])
     rows = np.unique(np.concatenate([order[[0, 1, 10, 100, 1000]],
                                      rng.choice(np.flatnonzero(deg > 0), 4000, replace=False),
-                                     rng.choice(np.flatnonzero(deg == 0), 64, replace=False)]))
+                                     rng.choice(np.flatnonzero(deg == 0), 64, replace=False), crel_rows]))
+    assert len(np.intersect1d(rows, crel_rows)) >= 64
     gen = torch.Generator().manual_seed(6)
     # points at hyperbolic radii spread over [0.2, 3] (|x| < 1/sqrt(c) = 10)
     u = torch.randn(V, D, generator=gen)
@@ -87,4 +99,8 @@ def test_config5_rows_vs_oracle(case, kind, monkeypatch):
         finally:
             _lib.EVENT_TRACE = None
         assert entry in {n for n, _ in calls}, (path, calls)
+        if path == "rowtail" and kind == "union":  # the crel gather ran over the big tiles
+            hit = g.__dict__.get("_crel_tiles")
+            assert hit is not None and hit[1] - hit[2] >= HL.CREL_MIN_TILES, hit
+            assert HL._crel(g, _lib.AGG_UNION, case["rel"]) is not None
         assert_close(out[rows], ref, what="config-5 %s rows (%s)" % (kind, path))

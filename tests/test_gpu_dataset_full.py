@@ -73,3 +73,65 @@ def test_dataset_full_shape_vs_oracle(name, encoder):
         assert abs(mrr["hip_" + k] - mrr["or_" + k]) <= 0.002, (k, mrr)
     print(name, encoder or cfg["encoder"], {k: round(v, 5) for k, v in mrr.items()},
           "rank flips at near ties: %d of %d" % (int((diff > 0).sum()), diff.numel()))
+
+
+def test_regcn_icews14s_full_shape_vs_oracle():
+    """BASELINE.json configs[0] at its real shape: the Euclidean RE-GCN (RecurrentRGCN +
+    ConvTransE / ConvTransR, src/rrgcn.py:142-194, src/decoder.py:10-100) with the reference's
+    ICEWS14s command (d = 200, 2 layers, self-loop, layer norm, history 3) on ICEWS14s-shaped
+    snapshots (|V| = 7,128, R = 230, 246 triples each) against oracle.model.euclid_predict on the
+    same random-init weights: every history embedding, h_0 and both decoders' scores within
+    1e-4 * max(1, |ref|); entity ranks equal up to near ties; MRRs within 0.002."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from oracle import graph as OG
+    from oracle import model as OM
+    from regcn_amd import graph as G
+    from regcn_amd.rrgcn import RecurrentRGCN
+    from regcn_amd.synthetic import CONFIGS, snapshot_series
+    cfg = CONFIGS["icews14s_uvrgcn_convtranse"]
+    V, R, T, d = cfg["V"], cfg["R"], cfg["T"], 200
+    dev = torch.device("cuda", 0)
+    snaps = snapshot_series(23, V, R, T + 1, cfg["per_snap"])
+    torch.manual_seed(4)
+    m = RecurrentRGCN("convtranse", "uvrgcn", V, R, 0, 0, d, "sub", T, num_bases=100, num_basis=100,
+                      num_hidden_layers=2, dropout=0.2, self_loop=True, layer_norm=True, input_dropout=0.2,
+                      hidden_dropout=0.2, feat_dropout=0.2, entity_prediction=True, relation_prediction=True,
+                      use_cuda=True, gpu=0)
+    with torch.no_grad():  # non-trivial batch-norm statistics for the eval-mode decoders
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm1d):
+                mod.running_mean.uniform_(-0.1, 0.1)
+                mod.running_var.uniform_(0.5, 1.5)
+    m = m.to(dev).eval()
+    test = snaps[T]
+    with torch.no_grad():
+        glist = [G.build_sub_graph(V, R, s, True, dev) for s in snaps[:T]]
+        assert glist[0].number_of_edges() == 2 * cfg["per_snap"]
+        embs, _, h0, _, _ = m.forward(glist, None, True)
+        all_tr, score, score_rel = m.predict(glist, R, None, torch.from_numpy(test).to(dev), True)
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    og = [OG.build_sub_graph(V, R, s) for s in snaps[:T]]
+    o_tr, o_score, o_score_rel, o_embs, o_h0 = OM.euclid_predict(sd, dict(layer_norm=True, n_layers=2), og,
+                                                                  torch.from_numpy(test))
+    assert torch.equal(all_tr.cpu(), o_tr)
+    for t in range(T):
+        assert_close(embs[t].cpu(), o_embs[t], what="history embedding %d" % t)
+    assert_close(h0.cpu(), o_h0, what="h_0")
+    assert_close(score.cpu(), o_score, what="ConvTransE scores")
+    assert_close(score_rel.cpu(), o_score_rel, what="ConvTransR scores")
+    ans_e = OM.answers_for_filter(test, R)
+    ans_r = OM.answers_for_filter(test, R, True)
+    mrr, ranks = {}, {}
+    for pre, sc, sr in (("hip", score.float().cpu(), score_rel.float().cpu()), ("or", o_score, o_score_rel)):
+        _, _, r_e, f_e = OM.total_rank(o_tr, sc, ans_e)
+        _, _, r_r, f_r = OM.total_rank(o_tr, sr, ans_r, True)
+        ranks[pre] = r_e
+        for k, v in (("re", r_e), ("fe", f_e), ("rr", r_r), ("fr", f_r)):
+            mrr[pre + "_" + k] = float(torch.mean(1.0 / v.float()))
+    diff = (ranks["hip"] - ranks["or"]).abs()
+    tgt = o_score.gather(1, o_tr[:, 2:3].long())
+    close = ((o_score - tgt).abs() <= 1e-4 * torch.clamp(tgt.abs(), min=1.0)).sum(1) - 1
+    assert bool((diff <= close).all()), "entity rank differences without a near tie"
+    for k in ("re", "fe", "rr", "fr"):
+        assert abs(mrr["hip_" + k] - mrr["or_" + k]) <= 0.002, (k, mrr)

@@ -212,6 +212,43 @@ def test_phase_pipeline_bitwise(encoder, layers, skip, self_loop, ln):
             assert torch.equal(a, b), mode
 
 
+@pytest.mark.parametrize("R,d,means_first", [(13, 200, False), (13, 72, True), (50, 200, True), (64, 100, False)])
+def test_phase_gru_parts_on_eight_waves(R, d, means_first, monkeypatch):
+    """The relation-GRU parts (csrc/gru_parts.h, written for 4 waves) hosted by the 8-wave phase
+    workgroups (timestep.hip, -DREGCN_ROWTILE_WAVES=8): waves 4-7 run the same barrier
+    sequence with their work predicated off.  R2 = 26 / 100 / 128 relation rows (a last GRU row
+    tile of 10 / 4 / 16 rows), the relation means inline in the x-part (stage_rel_means, its
+    own barrier) or precomputed (x_mean, the other staging path); phase launches equal the
+    per-layer launches bit for bit, and two runs of the phases equal each other.  (Round 5's
+    hang and "memo" mismatches were waves 4-7 leaving the GRU parts early, so the workgroup's
+    barriers no longer paired up.)"""
+    from regcn_amd import graph as G
+    from regcn_amd import hyperbolic_model as HM
+    from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
+    from regcn_amd.synthetic import snapshot_series
+    monkeypatch.setattr(HM, "REL_INLINE_MAX_SPAN", -1 if means_first else 1 << 30)
+    V, T = 2000, 3
+    snaps = snapshot_series(11, V, R, T, 400)
+    torch.manual_seed(2)
+    m = HyperbolicRecurrentRGCN("roth", "hyperbolic_uvrgcn", V, R, 0, 0, d, "sub", T, num_bases=d // 2,
+                                num_hidden_layers=2, dropout=0.2, c=C, self_loop=True, layer_norm=False,
+                                entity_prediction=True, relation_prediction=True, use_cuda=True,
+                                radius_msg_gamma=0.15).to(DEV).eval()
+    m.param_caches = m.memo_pristine = False
+    glist = [G.build_sub_graph(V, R, s, True, DEV) for s in snaps]
+    assert all(HM._means_first(g) == means_first for g in glist)
+    res = {}
+    for mode in ("phases", "phases_again", "layers"):
+        m.use_phases = mode != "layers"
+        with torch.no_grad():
+            embs, _, h0, _, _ = m.forward(glist, None, True)
+        torch.cuda.synchronize()
+        res[mode] = [e.clone() for e in embs] + [h0.clone()]
+    for mode in ("phases", "phases_again"):
+        for a, b in zip(res[mode], res["layers"]):
+            assert torch.equal(a, b), mode
+
+
 @pytest.mark.parametrize("encoder,ln", [("lgcn", False), ("hyperbolic_uvrgcn", True)])
 def test_shared_parameter_states_bitwise(encoder, ln):
     """A batch of independent predicts inside HyperbolicRecurrentRGCN.shared_parameter_states

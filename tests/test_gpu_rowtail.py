@@ -62,18 +62,24 @@ def _zipf_snapshot(V, R, n, seed):
     return zipf_triples(rng, V, R, n)
 
 
-@pytest.mark.parametrize("encoder,residual,ln", [("hyperbolic_uvrgcn", True, False), ("lgcn", True, True),
-                                                 ("hyperbolic_uvrgcn", False, True)])
-def test_rowtail_matches_fused_layers(encoder, residual, ln):
+@pytest.mark.parametrize("encoder,residual,ln,d", [("hyperbolic_uvrgcn", True, False, 200), ("lgcn", True, True, 200),
+                                                   ("hyperbolic_uvrgcn", False, True, 200),
+                                                   # column-tile buckets wider than ceil(d / 16): NT = 8 at d = 96 /
+                                                   # 100, NT = 4 at d = 32 (the tiles past d must not be stored)
+                                                   ("hyperbolic_uvrgcn", True, False, 96),
+                                                   ("hyperbolic_uvrgcn", True, True, 100), ("lgcn", True, False, 32)])
+def test_rowtail_matches_fused_layers(encoder, residual, ln, d):
     """A 70k-row snapshot window (> ROWTAIL_MIN_ROWS): the per-layer forward with the 64-row
     tail equals the fused 16-row kernel's within 1e-4 * max(1, |ref|) (the products sum in
-    another k order), and so does the step layer computing its own time gate."""
+    another k order), and so does the step layer computing its own time gate.  The widths
+    below 200 run the tail with more column tiles than d fills (csrc/rowtail.hip launch_tail's
+    NT buckets): a store past column d would land in the next row."""
     from regcn_amd import graph as G
     from regcn_amd import hyperbolic_layers as HL
     from regcn_amd.hyperbolic_model import HyperbolicRecurrentRGCN
-    V, R, d, T = 70_000, 64, 200, 2
+    V, R, T = 70_000, 64, 2
     torch.manual_seed(7)
-    m = HyperbolicRecurrentRGCN("roth", encoder, V, R, 0, 0, d, "sub", T, num_bases=100, num_hidden_layers=2,
+    m = HyperbolicRecurrentRGCN("roth", encoder, V, R, 0, 0, d, "sub", T, num_bases=d // 2, num_hidden_layers=2,
                                 dropout=0.0, c=C, self_loop=True, layer_norm=ln, entity_prediction=True,
                                 relation_prediction=True, use_cuda=True, gpu=0, use_residual_evolution=residual,
                                 radius_msg_gamma=0.15).to(DEV).eval()
