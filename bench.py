@@ -58,6 +58,14 @@ SIM_BLOCKER_CYCLES = int(os.environ.get("BENCH_SIM_BLOCKER_CYCLES", str(1_200_00
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix peak (MI355X_MICROARCH.md)
 
 
+_T0 = time.time()
+
+
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print("[bench %6.1f s] %s" % (time.time() - _T0, msg), file=sys.stderr, flush=True)
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -400,8 +408,12 @@ def aggregation_at_scale(device):
     return out
 
 
+CPU_MAX_TRIPLES = 256
+
+
 def cpu_baseline(cfg, d, model, sample, budget):
     """Time the CPU oracle (restatement of the reference op sequence) on one sample."""
+    log("  cpu baseline (%s)" % cfg["label"])
     sys.path.insert(0, REPO)
     from oracle import graph as OG
     from oracle import model as OM
@@ -413,6 +425,10 @@ def cpu_baseline(cfg, d, model, sample, budget):
                 radius_anchor_beta=1.0, radius_msg_gamma=0.15, use_residual_evolution=True, layer_norm=False,
                 encoder=cfg["encoder"], decoder=cfg["decoder"])
     og = [OG.build_sub_graph(V, R, s) for s in hist]
+    # a bounded sample: the full encoder over the window, the decoders on at most 256 test
+    # triples (512 queries; ICEWS18's 3,080 queries x 23k candidates take the per-pair oracle
+    # minutes), the same queries for the MRR parity below
+    test_np = test_np[:CPU_MAX_TRIPLES]
     test = torch.from_numpy(test_np)
     times = []
     t_end = time.time() + budget
@@ -718,18 +734,32 @@ def run_regcn(args, cfg, world, rank, device, backend):
         return model.predict(glist, R, None, test, True)
 
     cap = torch.cuda.Stream(device)
+    conc = max(1, min(args.concurrent, len(samples)))
+    lanes = [torch.cuda.Stream(device) for _ in range(conc)] if conc > 1 else []
+
+    def pool_pass(origin):  # sample i on lane i % conc, forked from and joined back into origin
+        if not lanes:
+            for i in range(len(samples)):
+                eager(i)
+            return
+        for ln in lanes:
+            ln.wait_stream(origin)
+        for i in range(len(samples)):
+            with torch.cuda.stream(lanes[i % conc]):
+                eager(i)
+        for ln in lanes:
+            origin.wait_stream(ln)
+
     with torch.no_grad():
         for i in range(len(samples)):
             eager(i)
         torch.cuda.synchronize()
         pool_graph = torch.cuda.CUDAGraph()
         with torch.cuda.stream(cap):
-            for i in range(len(samples)):
-                eager(i)  # warm the capture stream's allocator pool
+            pool_pass(cap)  # warm the capture streams' allocator pools
             torch.cuda.synchronize()
             with torch.cuda.graph(pool_graph, stream=cap):
-                for i in range(len(samples)):
-                    eager(i)
+                pool_pass(cap)
     pool_graph.replay()
     torch.cuda.synchronize()
     steps = -(-args.steps // len(samples)) * len(samples)
@@ -746,6 +776,7 @@ def run_regcn(args, cfg, world, rank, device, backend):
     if rank == 0:
         cpu = mrr = None
         if not args.no_cpu_baseline and world == 1:
+            log("  cpu baseline (%s)" % cfg["label"])
             sys.path.insert(0, REPO)
             from oracle import graph as OG
             from oracle import model as OM
@@ -785,7 +816,7 @@ def run_regcn(args, cfg, world, rank, device, backend):
                           "layer norm, self-loop, ConvTransE + ConvTransR", "V": V, "R": R,
                           "triples_per_snapshot": cfg["per_snap"], "history_len": T, "n_layers": 2, "d": d,
                           "edges_per_step": int(np.mean(epw)), "queries_per_step": 2 * cfg["per_snap"],
-                          "hip_graph": True, "steps_per_graph_launch": len(samples),
+                          "hip_graph": True, "steps_per_graph_launch": len(samples), "concurrent_samples": conc,
                           "parallelism": "replicas x%d" % world},
                "cpu_baseline": cpu, "mrr_parity": mrr}
     del pool_graph, samples, model
@@ -1467,7 +1498,10 @@ def main():
     if args.encoder_launches == "auto":
         args.encoder_launches = "layers" if cfg.get("scale") else "phases"
     if cfg.get("scale"):
+        log("config 5: %d steps" % args.steps)
         out = run_scale(args, cfg, world, rank, device, backend)
+        if rank == 0:
+            log("config 5 done: %.1f M edges/s" % out["value"])
         if world > 1 and args.shard != "replica" and not args.no_extras:
             # the replica mode beside the partitioned headline (independent windows per rank)
             rep_args = parse(["--shard", "replica", "--steps", str(max(4, args.steps // 2)), "--warmup", "1",
@@ -1477,6 +1511,7 @@ def main():
                 out["replicas"] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps", "scaling")}
                 out["replicas"]["parallelism"] = r["config"]["parallelism"]
         if rank == 0 and world == 1 and args.sim_ranks > 1 and not args.no_extras:
+            log("owner simulation, %d ranks" % args.sim_ranks)
             sim = owner_simulation(args, cfg, device, args.sim_ranks)
             # against this run's measured one-GPU step (the simulation's own sum of the ranks'
             # launches is larger: many short launches)
@@ -1484,8 +1519,10 @@ def main():
             out["owner_simulation"] = sim
         if rank == 0 and world == 1:
             if not args.no_cpu_baseline:
+                log("cpu baseline")
                 out["cpu_baseline"] = cpu_baseline_scale(cfg, args.d, args.cpu_budget)
             if not args.no_scale:
+                log("aggregation and decoder rooflines")
                 out["aggregation_roofline"] = aggregation_at_scale(device)
                 out["decoder_roofline"] = decoder_at_scale()
         if world == 1 and not args.no_extras:
@@ -1499,6 +1536,7 @@ def main():
                 c = dict(CONFIGS[name])
                 if enc:
                     c.update(encoder=enc, label=c["label"] + ", encoder=" + enc)
+                log("leg %s" % key)
                 if key == "icews14s_regcn":
                     r = run_regcn(sub, c, world, rank, device, backend)
                     if rank == 0:

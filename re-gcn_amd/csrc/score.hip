@@ -667,6 +667,231 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   stamp(2);
 }
 
+// ---- 32 x 32 x 2 fp32 scorer (MODE 0 scores, MODE 3 fused rank count) ----------------------
+// v_mfma_f32_32x32x2_f32: a wave owns 32 queries x a 64-candidate tile as two 32 x 32
+// accumulators, so every B fragment read from LDS feeds a 32 x 32 block (twice the MACs of a
+// 16 x 16 x 4 fragment) and the k loop issues half the LDS reads per flop.  K order: 8-deep
+// block b, MFMA step e: lane half h = lane >> 5 carries k = 8 b + 4 h + e for both operands, so
+// a lane's A operand of a block is one float4 of its query row (columns 8 b + 4 h ..) and its B
+// operand one ds_read_b128 of its candidate row -- conflict-free with a row stride of 4 x odd
+// floats (each 16-lane b128 group's rows are distinct mod 16).  d = 200 is 25 blocks (no
+// padded k).  C layout: candidate 32 jb + (lane & 31), query (r & 3) + 8 (r >> 2) + 4 h.
+// A workgroup = 8 waves = 256 queries; the strip walk, XCD order, candidate staging (8 threads
+// per row, |e|^2 beside it) and one barrier per tile are k_score_f32's.  Scores and counts
+// equal each other bit for bit (the same kernel computes both); they differ from the 16 x 16
+// kernel's in the last bits (another k association).
+constexpr int S32_QW = 32, S32_SQ = 8 * S32_QW, S32_SN = 64;
+__host__ __device__ inline int score32_stride(int d) {
+  int s = ((d + 7) & ~7) / 4;
+  return 4 * (s | 1);
+}
+inline size_t score32_lds(int d) { return (size_t)2 * S32_SN * score32_stride(d) * 4; }
+__device__ const f4 kZeroF4[1] = {{0.f, 0.f, 0.f, 0.f}};
+inline int score32_stripes(int B, int nbn) {
+  const int nbq = (B + S32_SQ - 1) / S32_SQ;
+  return std::max(1, std::min(std::min(32 / nbq, 32), (nbn + 7) / 8));
+}
+inline unsigned score32_grid(int B, int nbn) {
+  return (unsigned)(8L * ((B + S32_SQ - 1) / S32_SQ) * score32_stripes(B, nbn));
+}
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float lanes32_sum(float v) {  // over the 32 lanes of a half-wave
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  v += __shfl_xor(v, 16);
+  return v;
+}
+
+template <int MODE, int KBM>
+__device__ __forceinline__ void score32_body(ScoreArgs p, const int blk, const int nblk) {
+  static_assert(MODE == 0 || MODE == 3, "the 32 x 32 scorer writes scores or rank counts");
+  extern __shared__ float Es[];  // 2 x S32_SN x SE candidate rows (zero past N and d)
+  p.scale = p.scale_p ? *p.scale_p : 1.f;
+  if (p.scale_raw && p.scale_p)  // softplus(raw) + 1e-6 (hyperbolic_decoder.py:717; torch threshold 20)
+    p.scale = (p.scale > 20.f ? p.scale : log1pf(expf(p.scale))) + 1e-6f;
+  p.margin = p.margin_p ? *p.margin_p : 0.f;
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int d = p.d, KB = (d + 7) >> 3, SE = score32_stride(d), SE4 = SE >> 2;
+  const int nbn = p.n_rng ? p.rng_total : (p.N + S32_SN - 1) / S32_SN, nbq = (p.B + S32_SQ - 1) / S32_SQ;
+  auto tile_rows = [&](int t, int& row0, int& nvalid) {
+    if (!p.n_rng) {
+      row0 = t * S32_SN;
+      nvalid = min(S32_SN, p.N - row0);
+      return;
+    }
+    int st = p.rng_start[0], tb = p.rng_tile[0], ln = p.rng_len[0];
+#pragma unroll
+    for (int r = 1; r < SCORE_MAX_RANGES; ++r)
+      if (r < p.n_rng && t >= p.rng_tile[r]) st = p.rng_start[r], tb = p.rng_tile[r], ln = p.rng_len[r];
+    const int off = (t - tb) * S32_SN;
+    row0 = st + off;
+    nvalid = min(S32_SN, ln - off);
+  };
+  const int S = nblk / (8 * nbq);
+  const int xcd = blk & 7, rk = blk >> 3;
+  const int bq = rk % nbq, stripe = rk / nbq;
+  auto tile_of = [&](int i) { return xcd + 8 * (stripe + S * i); };
+  int bn = tile_of(0);
+  const int q0 = bq * S32_SQ + S32_QW * wv;  // this wave's first query
+  const int qrow_of_r0 = 4 * h;               // C row of register r: (r & 3) + 8 (r >> 2) + 4 h
+  float run_c[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) run_c[r] = 0.f;
+  auto count_flush = [&]() {  // MODE 3: a query row's 32 lanes summed, partial xcd + 8 stripe
+    const int np = 8 * S, pidx = xcd + 8 * stripe;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int q = q0 + (r & 3) + 8 * (r >> 2) + qrow_of_r0;
+      const float cnt = lanes32_sum(run_c[r]);
+      if (l32 == 0 && q < p.B) p.part[(int64_t)q * np + pidx] = cnt;
+    }
+  };
+  if (bn >= nbn) {  // no work for this stripe (whole workgroup, before any barrier)
+    if (MODE == 3) count_flush();
+    return;
+  }
+  const f4 z4 = {0.f, 0.f, 0.f, 0.f};
+  // this wave's query rows: lane (l32, h) holds columns 8 b + 4 h .. + 3 of query q0 + l32
+  const int qr = q0 + l32;
+  const bool q_ok = qr < p.B;
+  const float* qrow = p.q + (int64_t)min(qr, p.B - 1) * d;
+  f4 a[KBM];
+  float xs = 0.f;
+#pragma unroll
+  for (int b = 0; b < KBM; ++b) {
+    const int c = 8 * b + 4 * h;
+    const f4 v = *reinterpret_cast<const f4*>(qrow + min(c, d - 4));
+    a[b] = (q_ok & (b < KB) & (c < d)) ? v : z4;
+    xs += dot4(a[b], a[b]);
+  }
+  xs += __shfl_xor(xs, 32);  // |q|^2 of query q0 + l32 (both halves)
+  // candidate tile staging by DMA (global_load_lds, 16 B per lane, no registers): the tile is
+  // S32_SN x SE4 float4 pieces in row-major LDS order; wave-instruction j of wave w covers pieces
+  // 64 (w + 8 j) + lane; pieces past column d or rows past the tile's end copy a zero row
+  const float* zrow = reinterpret_cast<const float*>(kZeroF4);
+  const int npieces = S32_SN * SE4, nins = (npieces + 511) / 512;
+  auto dma = [&](int buf, int t) {
+    int row0, nv;
+    tile_rows(t, row0, nv);
+    char* base = reinterpret_cast<char*>(Es + buf * S32_SN * SE);
+    for (int j = 0; j < nins; ++j) {
+      const int pc = 64 * (wv + 8 * j) + lane;
+      const int r = pc / SE4, c4 = pc - r * SE4;
+      const bool ok = (r < nv) & (4 * c4 < d);
+      const float* src = ok ? p.e + (int64_t)(row0 + r) * d + 4 * c4 : zrow;
+      if (64 * (wv + 8 * j) < npieces)  // wave-uniform
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(base + (size_t)64 * 16 * (wv + 8 * j)),
+                                         16, 0, 0);
+    }
+  };
+  dma(0, bn);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int cur = 0;
+  for (int i = 0;; ++i) {
+    const int bn_next = tile_of(i + 1);
+    const bool more = bn_next < nbn;  // workgroup-uniform
+    if (more) dma(cur ^ 1, bn_next);  // that buffer's readers passed the last barrier
+    const float* brow = Es + cur * S32_SN * SE + l32 * SE + 4 * h;
+    f16v acc[2];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[jb][r] = 0.f;
+    float ss[2] = {0.f, 0.f};  // |e|^2 halves of the lane's two candidates, from the B fragments
+    f4 bb[2][2];               // [block parity][jb]
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) bb[0][jb] = *reinterpret_cast<const f4*>(brow + 32 * jb * SE);
+#pragma unroll
+    for (int b = 0; b < KBM; ++b) {
+      if (b < KB) {  // wave-uniform
+        const int bnx = min(b + 1, KB - 1);
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) bb[(b + 1) & 1][jb] = *reinterpret_cast<const f4*>(brow + 32 * jb * SE + 8 * bnx);
+        __builtin_amdgcn_sched_barrier(0);  // keep block b + 1's reads ahead of block b's MFMAs
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int jb = 0; jb < 2; ++jb)
+            acc[jb] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[b][e], bb[b & 1][jb][e], acc[jb], 0, 0, 0);
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) ss[jb] += dot4(bb[b & 1][jb], bb[b & 1][jb]);
+      }
+    }
+    // epilogue: lane holds candidates row0 + 32 jb + l32, queries q0 + (r & 3) + 8 (r >> 2) + 4 h
+    int row0, nv;
+    tile_rows(bn, row0, nv);
+    ColK ck[2];
+    int ni[2];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb) {
+      const int li = 32 * jb + l32;
+      ni[jb] = li < nv ? row0 + li : 0x7fffffff;  // invalid: >= N
+      const float bias = (ni[jb] < p.N && p.bias) ? p.bias[ni[jb]] : 0.f;
+      ck[jb] = col_k(ss[jb] + __shfl_xor(ss[jb], 32), bias, p);
+    }
+    const bool full = MODE == 0 && nv == S32_SN && bq * S32_SQ + S32_SQ <= p.B;  // workgroup-uniform
+    const int64_t n0 = ni[0] < p.N ? ni[0] : 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = (r & 3) + 8 * (r >> 2) + qrow_of_r0;
+      const int q = q0 + qi;
+      const RowK rkq = row_k(__shfl(xs, qi), p);
+      if (MODE == 0) {
+        float* orow = p.out + (int64_t)min(q, p.B - 1) * p.N + n0;
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb) {
+          const float sc = fmaf(-p.scale, pair_n2(acc[jb][r], rkq, ck[jb], p, nullptr, nullptr, nullptr), ck[jb].sb);
+          if (full || (q < p.B && ni[jb] < p.N)) orow[32 * jb] = sc;
+        }
+      } else {
+        const float t = q < p.B ? p.thr[q] : INFINITY;
+        float cnt = 0.f;
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+          if (ni[jb] < p.N)
+            cnt += fmaf(-p.scale, pair_n2(acc[jb][r], rkq, ck[jb], p, nullptr, nullptr, nullptr), ck[jb].sb) > t ? 1.f : 0.f;
+        run_c[r] += cnt;  // an exact integer (< 2^24 per lane)
+      }
+    }
+    if (!more) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of the next tile have landed
+    __syncthreads();                                    // ... and every wave's; this tile's readers are done
+    cur ^= 1;
+    bn = bn_next;
+  }
+  if (MODE == 3) count_flush();
+}
+
+template <int MODE, int KBM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_score32(ScoreArgs p) {
+  score32_body<MODE, KBM>(p, blockIdx.x, gridDim.x);
+}
+
+template <int KBM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_score32_jobs(ScoreArgs p0, ScoreArgs p1,
+                                                                                            int g0) {
+  if ((int)blockIdx.x < g0) score32_body<0, KBM>(p0, blockIdx.x, g0);
+  else score32_body<0, KBM>(p1, blockIdx.x - g0, gridDim.x - g0);
+}
+
+// REGCN_SCORE32=1 selects the 32 x 32 x 2 kernel for the scores and rank counts (opt-in: measured
+// slower than the 16 x 16 x 4 kernel, 4.48 vs 4.33 ms at config 5 and 28 vs 26 us at the ICEWS14s
+// decoder shape, profiles/r6_score32_ab.jsonl)
+static bool score32_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("REGCN_SCORE32");
+    v = e ? atoi(e) : 0;
+  }
+  return v != 0;
+}
+
 // Wave-specialised fp32 scorer: the same workgroup tile (128 queries, strips of 64-candidate
 // tiles, XCD-aware order) with the roles split so the epilogue never holds the matrix core.
 // Waves 0-3 (one per SIMD) are MFMA waves: wave w keeps queries [32w, 32w + 32) in registers
@@ -1051,6 +1276,12 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   const size_t lds4 = score_f32_lds<4>(a.d);
   if (mode == 0) {
     if (!a.out) return set_error(REGCN_EINVAL, "null output");
+    if (fast && score32_on()) {
+      const dim3 g32(score32_grid(a.B, (a.N + S32_SN - 1) / S32_SN));
+      if ((a.d + 7) / 8 <= 25) hipLaunchKernelGGL((k_score32<0, 25>), g32, dim3(512), score32_lds(a.d), st, a);
+      else hipLaunchKernelGGL((k_score32<0, 32>), g32, dim3(512), score32_lds(a.d), st, a);
+      return check_launch("k_score32");
+    }
     if (ws) hipLaunchKernelGGL((k_score_ws<0>), g2, dim3(512), score_ws_lds(a.d), st, a);
     else if (nw4) hipLaunchKernelGGL((k_score_f32<0, 4>), g4, b4, lds4, st, a);
     else if (fast) hipLaunchKernelGGL((k_score_f32<0>), g2, b2, lds2, st, a);
@@ -1087,7 +1318,12 @@ int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st) {
     return 0;
   }
   const unsigned g0 = score_f32_grid(a0.B, (a0.N + SN - 1) / SN), g1 = score_f32_grid(a1.B, (a1.N + SN - 1) / SN);
-  if (score_ws() && score_ws_lds(a0.d) <= SCORE_LDS_MAX) {
+  if (score32_on()) {
+    const unsigned h0 = score32_grid(a0.B, (a0.N + S32_SN - 1) / S32_SN);
+    const unsigned h1 = score32_grid(a1.B, (a1.N + S32_SN - 1) / S32_SN);
+    if ((a0.d + 7) / 8 <= 25) hipLaunchKernelGGL(k_score32_jobs<25>, dim3(h0 + h1), dim3(512), score32_lds(a0.d), st, a0, a1, (int)h0);
+    else hipLaunchKernelGGL(k_score32_jobs<32>, dim3(h0 + h1), dim3(512), score32_lds(a0.d), st, a0, a1, (int)h0);
+  } else if (score_ws() && score_ws_lds(a0.d) <= SCORE_LDS_MAX) {
     hipLaunchKernelGGL(k_score_ws_jobs, dim3(g0 + g1), dim3(512), score_ws_lds(a0.d), st, a0, a1, (int)g0);
   } else if (score_nw() == 4) {
     const unsigned h0 = score_f32_grid<4>(a0.B, (a0.N + 31) / 32), h1 = score_f32_grid<4>(a1.B, (a1.N + 31) / 32);
@@ -1127,7 +1363,8 @@ int rank_fused(ScoreArgs& a, int accumulate, int* counts, hipStream_t st) {
   if (a.B > 0 && (!a.q || !a.thr || !counts || !a.part)) return set_error(REGCN_EINVAL, "null pointer");
   if (a.B > 0 && a.N > 0 && !a.e) return set_error(REGCN_EINVAL, "null candidates");
   if (a.B == 0) return 0;
-  const int nw = score_nw(), snw = 8 * nw;
+  const bool s32 = score32_on();
+  const int nw = score_nw(), snw = s32 ? S32_SN : 8 * nw;
   if (a.n_rng) {  // the ranges' candidate tiles at this shape's tile size (a tile never spans two)
     int tiles = 0;
     for (int r = 0; r < SCORE_MAX_RANGES && r < a.n_rng; ++r) {
@@ -1146,11 +1383,18 @@ int rank_fused(ScoreArgs& a, int accumulate, int* counts, hipStream_t st) {
     return 0;
   }
   a.trace = g_trace;
-  if (nw == 4) hipLaunchKernelGGL((k_score_f32<3, 4>), dim3(score_f32_grid<4>(a.B, nbn)), dim3(256), score_f32_lds<4>(a.d), st, a);
-  else hipLaunchKernelGGL((k_score_f32<3>), dim3(score_f32_grid(a.B, nbn)), dim3(64 * SW2), score_f32_lds(a.d), st, a);
+  if (s32) {
+    if ((a.d + 7) / 8 <= 25) hipLaunchKernelGGL((k_score32<3, 25>), dim3(score32_grid(a.B, nbn)), dim3(512), score32_lds(a.d), st, a);
+    else hipLaunchKernelGGL((k_score32<3, 32>), dim3(score32_grid(a.B, nbn)), dim3(512), score32_lds(a.d), st, a);
+  } else if (nw == 4) {
+    hipLaunchKernelGGL((k_score_f32<3, 4>), dim3(score_f32_grid<4>(a.B, nbn)), dim3(256), score_f32_lds<4>(a.d), st, a);
+  } else {
+    hipLaunchKernelGGL((k_score_f32<3>), dim3(score_f32_grid(a.B, nbn)), dim3(64 * SW2), score_f32_lds(a.d), st, a);
+  }
   const int rc = check_launch("k_score_f32<3>");
   if (rc) return rc;
-  const int np = nw == 4 ? 8 * score_f32_stripes<4>(a.B, nbn) : 8 * score_f32_stripes(a.B, nbn);
+  const int np = s32 ? 8 * score32_stripes(a.B, nbn)
+                     : nw == 4 ? 8 * score_f32_stripes<4>(a.B, nbn) : 8 * score_f32_stripes(a.B, nbn);
   hipLaunchKernelGGL(k_count_combine, dim3((a.B + 3) / 4), dim3(256), 0, st, a.part, a.B, np, accumulate, counts);
   return check_launch("k_count_combine");
 }

@@ -8,7 +8,10 @@
 #   prof         kernel trace + stats of the short headline command
 #   prof:<cfg>   kernel trace + stats of `bench.py --config <cfg>` (dataset sizes)
 #   pmc          SQ / GRBM + L2-request / FETCH_SIZE / WRITE_SIZE passes of the short headline
+#   agg[:uniform] the config-5 aggregation benchmark: kernel trace + FETCH / WRITE passes
+#   simprof      kernel trace of the 8-rank owner-partition simulation (tools/simprobe.py)
 #   py:<script>  python <script> (commas for spaces)         -> gpurun_out/$TAG.<n>.log
+#   sh:<script>  bash <script> (commas for spaces)           -> gpurun_out/$TAG.<n>.log
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -41,6 +44,20 @@ for job in $JOBS; do
       timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/$TAG.pmc_fetch -o run -- $SHORT > $R/$TAG.pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; exit 1; }
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/$TAG.pmc_write -o run -- $SHORT > $R/$TAG.pmc_write.log 2>&1 || { echo "pmc write failed"; exit 1; }
       python3 tools/pmc_summary.py $R/$TAG.pmc_sq $R/$TAG.pmc_grbm $R/$TAG.pmc_fetch $R/$TAG.pmc_write --match=k_rowtail,k_gather_agg,k_gather_crel,k_union_runs,k_score,k_gather_sum,k_init > $R/$TAG.pmc_summary.txt ;;
+    agg|agg:uniform)
+      # the config-5 aggregation benchmark: kernel trace + FETCH_SIZE / WRITE_SIZE (Zipf or uniform sources)
+      u=""; t=agg; [ "$job" = agg:uniform ] && { u="--uniform-src"; t=agg_uniform; }
+      A="python3 $GRAFT_REPO_ROOT/tools/aggbench.py --reps 2 --which union_aggregate,union_aggregate_src_runs,lorentz_aggregate $u"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$TAG.${t}_prof -o run -- $A > $R/$TAG.${t}_prof.log 2>&1 || { echo "agg rocprof failed"; exit 1; }
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/$TAG.${t}_fetch -o run -- $A > $R/$TAG.${t}_fetch.log 2>&1 || { echo "agg pmc fetch failed"; exit 1; }
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $R/$TAG.${t}_write -o run -- $A > $R/$TAG.${t}_write.log 2>&1 || { echo "agg pmc write failed"; exit 1; } ;;
+    simprof)
+      # kernel trace of the 8-rank owner-partition simulation, chunk tails on one stream (exclusive kernel times)
+      REGCN_CHUNK_TAIL_STREAMS=1 timeout -k 10 420 rocprofv3 --kernel-trace -d $R/$TAG.simprof -o sim -- python3 $GRAFT_REPO_ROOT/tools/simprobe.py --world 8 > $R/$TAG.simprof.log 2>&1 || { echo "simprobe failed"; tail -20 $R/$TAG.simprof.log; exit 1; }
+      python3 tools/simprof_summary.py $R/$TAG.simprof/sim_results.db --steps 6 --top 40 > $R/$TAG.simprof_summary.txt && rm -f $R/$TAG.simprof/sim_results.db ;;
+    sh:*)
+      timeout -k 10 900 bash $arg > $R/$TAG.$n.log 2>&1 || { echo "bash $arg failed"; tail -20 $R/$TAG.$n.log; exit 1; }
+      tail -30 $R/$TAG.$n.log ;;
     py:*)
       timeout -k 10 600 python -u $arg > $R/$TAG.$n.log 2>&1 || { echo "python $arg failed"; tail -20 $R/$TAG.$n.log; exit 1; }
       tail -5 $R/$TAG.$n.log ;;
