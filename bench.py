@@ -16,16 +16,18 @@ fragment packing); the snapshot graphs are built once, in HBM, before the timed 
 metric = million directed message edges aggregated per second (edges after inverse
 doubling x GCN layers x history snapshots = 300M per step), whole job:
 K steps timed exactly, between barriers + device synchronisation, max over ranks.
-Multi-GPU: one process per GPU.  At config 5 with --gpus > 1 the default is the owner
-partition (SURVEY.md §8(e) partitioning 2, strong scaling): the entity ids are relabelled so
-each rank's rows carry an equal share of the edges (parallel.EntityRelabel), every rank runs
-its rows of every layer and all-gathers their tangent rows and radii (804 B per row) on a
-side stream while its next row chunk computes, the relation means are partitioned (one
-all_reduce of R x d), and the step ends in the candidate-sharded decoder (predict_ranks: each
-rank scores its own rows as candidates, one all_reduce of the 2B rank counts).  The replica
-mode (independent windows per rank, weak scaling) rides along as the `replicas` key.  At N = 1
-the line carries `owner_simulation`: the 8 ranks' launches run one after another on the one
-GPU, each rank's device time measured, plus the replicated work and the exchange volume.
+Multi-GPU: one process per GPU.  The default (--gpus > 1) is replicas: independent predicts are
+the data-parallel unit (hyperbolic_main.py's test loop predicts every test snapshot from its own
+window), so each rank runs its own windows with no data-path collective (weak scaling; value =
+all ranks' edges over the max-over-ranks time).  `--shard owner` (or `--owner-leg` beside the
+replicas) partitions every snapshot instead (SURVEY.md §8(e) partitioning 2, strong scaling of one
+predict): the entity ids are relabelled so each rank's rows carry an equal share of the edges
+(parallel.EntityRelabel), every rank runs its rows of every layer and sends the rows the other
+ranks read (halo all_to_all, 804 B per row) on a side stream while its next row chunk computes,
+the relation means are partitioned (one all_reduce of R x d), and the step ends in the
+candidate-sharded decoder (predict_ranks).  At N = 1 the line carries `owner_simulation`: the 8
+ranks' launches run one after another on the one GPU, each rank's device time measured, plus the
+replicated work and the exchange volume.
 
 Per-call device times come from HIP events recorded on the launching stream after every
 library call during the timed steps (`_lib.EVENT_TRACE`); `roofline` reports the call
@@ -33,10 +35,12 @@ with the largest time per step against its algorithmic bytes (or flops), with th
 traffic of its kernel from the committed rocprofv3 PMC passes (profiles/).
 `cpu_baseline` times the CPU oracle's encoder forward on a bounded sample on rank 0.
 
-The dataset-sized configs (ICEWS14s lgcn+roth, ICEWS18 roth, GDELT) run with `--config`
-(latency-bound, pools of independent predicts in one HIP graph, whole pool passes timed);
-the headline line carries ICEWS14s and ICEWS18 results (and the MRR parity of the HIP
-predict against the oracle) as extra keys.
+The dataset-sized configs (ICEWS14s lgcn+roth, ICEWS14s RE-GCN uvrgcn+convtranse, ICEWS18 roth,
+GDELT for both encoders) run with `--config` (latency-bound: pools of 48 independent predicts, 24
+in flight, in one HIP graph, whole pool passes timed); the headline line carries them as `legs`
+(value, roofline fraction, CPU baseline, MRR parity of the HIP predict against the oracle).
+The printed line is compact (<= 8 KB, compact_line); the full record goes to BENCH_DETAIL
+(default gpurun_out/bench_detail.json).
 """
 import argparse
 import contextlib
@@ -73,7 +77,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="synthetic_1m")
     ap.add_argument("--pool", type=int, default=0,
-                    help="distinct samples cycled through the timed steps (default: 2 windows at config 5; 16 "
+                    help="distinct samples cycled through the timed steps (default: 2 windows at config 5; 48 "
                          "for the dataset configs, where one pool pass is one batch of independent predicts)")
     ap.add_argument("--queries", type=int, default=1024,
                     help="config 5: queries per step (half test triples, half their inverses)")
@@ -87,10 +91,12 @@ def parse(argv=None):
     ap.add_argument("--graph-steps", type=int, default=0,
                     help="steps captured per HIP graph (default: the whole pool, replayed as one launch; "
                          "1 = one graph per step)")
-    ap.add_argument("--concurrent", type=int, default=4,
+    ap.add_argument("--concurrent", type=int, default=24,
                     help="independent samples in flight together (one stream each inside the pool's HIP "
                          "graph): predicts of different test snapshots are independent (hyperbolic_main.py "
-                         ":100-149 without --multi-step), so a server may overlap them")
+                         ":100-149 without --multi-step), so a server may overlap them.  Default 16 with "
+                         "pools of 48 (profiles/r6_concurrency_sweep.txt: ICEWS14s 27.9 -> 31.7, GDELT "
+                         "65.6 -> 69.6, ICEWS18 31.7 -> 34.4 M edges/s against 4 with pools of 16)")
     ap.add_argument("--per-layer", action="store_true", help=argparse.SUPPRESS)  # = --encoder-launches layers
     ap.add_argument("--serving-cache", action="store_true",
                     help="keep parameter-only states across steps (initial entity state, timestep 0's GRU "
@@ -107,10 +113,12 @@ def parse(argv=None):
     ap.add_argument("--no-scale", action="store_true",
                     help="skip the config-5 aggregation and decoder rooflines (N=1 only)")
     ap.add_argument("--shard", default="auto", choices=["auto", "replica", "edge", "owner"],
-                    help="multi-GPU: independent samples per rank (weak scaling), or every snapshot "
-                         "partitioned across the ranks by edges (all-reduce) / destination owner "
-                         "(all-gather) (strong scaling, SURVEY.md §8(e)); auto: owner at config 5 with "
-                         "--gpus > 1 (+ a replica leg), replica for the dataset configs")
+                    help="multi-GPU: independent samples per rank (weak scaling, no data-path collective), "
+                         "or every snapshot partitioned across the ranks by edges (all-reduce) / destination "
+                         "owner (halo all_to_all) (strong scaling, SURVEY.md §8(e)); auto: replica")
+    ap.add_argument("--owner-leg", action="store_true",
+                    help="config 5, N > 1: also run the owner partition (every snapshot split across the "
+                         "ranks by destination rows, halo exchange over RCCL) beside the replica headline")
     ap.add_argument("--sim-ranks", type=int, default=8,
                     help="config 5 at N = 1: ranks of the one-GPU owner-partition simulation (0: skip)")
     a = ap.parse_args(argv)
@@ -539,7 +547,7 @@ def run_small(args, cfg, world, rank, device, backend, extras=True):
     Whole pool passes are timed (steps rounded up to a multiple of the pool when the pool
     runs as one HIP graph), so the value does not depend on the step count."""
     d = args.d
-    pool_n = args.pool or 16
+    pool_n = args.pool or 48
     model = build_model(cfg, d, device, seed=1234)          # same weights on every rank
     model.use_phases = args.encoder_launches != "layers"
     model.memo_pristine = model.param_caches = args.serving_cache
@@ -716,7 +724,7 @@ def run_regcn(args, cfg, world, rank, device, backend):
     from regcn_amd.rrgcn import RecurrentRGCN
     from regcn_amd.synthetic import snapshot_series
     d, V, R, T = args.d, cfg["V"], cfg["R"], cfg["T"]
-    pool_n = args.pool or 16
+    pool_n = args.pool or 48
     torch.manual_seed(1234)
     model = RecurrentRGCN("convtranse", "uvrgcn", V, R, 0, 0, d, "sub", T, num_bases=cfg["n_bases"],
                           num_basis=cfg["n_bases"], num_hidden_layers=2, dropout=0.2, self_loop=True,
@@ -918,7 +926,7 @@ def compact_line(out, detail_path=None):
     if dr:
         line["decoder_roofline"] = {"score_frac": dr["score"]["frac"], "ce_frac": dr["cross_entropy"]["frac"],
                                     "score_us": dr["score"]["avg_launch_us"]}
-    for k in ("replicas", "edge_partition"):
+    for k in ("owner_partition", "edge_partition"):
         if out.get(k):
             line[k] = {kk: out[k][kk] for kk in ("value", "ms_per_step", "scaling", "parallelism") if kk in out[k]}
     if out.get("mrr_parity"):
@@ -1494,7 +1502,10 @@ def main():
     from regcn_amd.synthetic import CONFIGS
     cfg = CONFIGS[args.config]
     if args.shard == "auto":
-        args.shard = "owner" if cfg.get("scale") and world > 1 else "replica"
+        # independent predicts (windows) are the data-parallel unit: one per rank, no data-path
+        # collective, weak scaling; --shard owner|edge partitions every snapshot across the
+        # ranks instead (strong scaling of one predict; --owner-leg runs it beside the replicas)
+        args.shard = "replica"
     if args.encoder_launches == "auto":
         args.encoder_launches = "layers" if cfg.get("scale") else "phases"
     if cfg.get("scale"):
@@ -1502,14 +1513,17 @@ def main():
         out = run_scale(args, cfg, world, rank, device, backend)
         if rank == 0:
             log("config 5 done: %.1f M edges/s" % out["value"])
-        if world > 1 and args.shard != "replica" and not args.no_extras:
-            # the replica mode beside the partitioned headline (independent windows per rank)
-            rep_args = parse(["--shard", "replica", "--steps", str(max(4, args.steps // 2)), "--warmup", "1",
+        if world > 1 and args.shard == "replica" and args.owner_leg:
+            # the owner partition beside the replicas: every rank the same windows, its rows of
+            # every snapshot (strong scaling of one predict, SURVEY.md §8(e) partitioning 2)
+            log("owner-partition leg")
+            own_args = parse(["--shard", "owner", "--steps", str(max(4, args.steps // 2)), "--warmup", "1",
                               "--no-extras"])
-            r = run_scale(rep_args, cfg, world, rank, device, backend)
+            r = run_scale(own_args, cfg, world, rank, device, backend)
             if rank == 0:
-                out["replicas"] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps", "scaling")}
-                out["replicas"]["parallelism"] = r["config"]["parallelism"]
+                out["owner_partition"] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps", "scaling")}
+                out["owner_partition"]["parallelism"] = r["config"]["parallelism"]
+                out["owner_partition"]["exchange_gb_per_step_rank0"] = r.get("exchange_gb_per_step_rank0")
         if rank == 0 and world == 1 and args.sim_ranks > 1 and not args.no_extras:
             log("owner simulation, %d ranks" % args.sim_ranks)
             sim = owner_simulation(args, cfg, device, args.sim_ranks)

@@ -179,6 +179,8 @@ struct ScoreArgs {
   // rng_len[r]) of e, tiled range by range (range r's tiles [rng_tile[r], rng_tile[r + 1])),
   // so one launch covers a rank's owner ranges; n_rng == 0: rows [0, N)
   int n_rng, rng_total;  // rng_total = rng_tile[n_rng] (device code indexes the arrays statically only)
+  int bal;               // MODE 0, > 0: balanced grid, query tile blk % nbq takes candidate tiles
+                         // blk / nbq + bal i (set by the launcher for small candidate sets)
   int rng_start[8], rng_len[8], rng_tile[9];
 };
 

@@ -337,8 +337,9 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
       for (int r = 0; r < 4; ++r) {
         float* orow = p.out + (int64_t)qi[r] * p.N + n0;
 #pragma unroll
-        for (int j = 0; j < J; ++j)
+        for (int j = 0; j < J; ++j) {
           orow[16 * j] = fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb);
+        }
       }
       return;
     }
@@ -517,8 +518,12 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   };
   const int S = nblk / (8 * nbq);
   const int xcd = blk & 7, rk = blk >> 3;
-  const int bq = rk % nbq, stripe = rk / nbq;
-  auto tile_of = [&](int i) { return xcd + 8 * (stripe + S * i); };
+  // balanced grid (MODE 0, small candidate sets): workgroup blk takes query tile blk % nbq and
+  // every p.bal-th candidate tile from blk / nbq, so the grid fills the CUs whatever nbq is;
+  // striped grid: XCD-aware strips (see above)
+  const bool bal = MODE == 0 && p.bal > 0;
+  const int bq = bal ? blk % nbq : rk % nbq, stripe = rk / nbq, g0b = blk / nbq;
+  auto tile_of = [&](int i) { return bal ? g0b + p.bal * i : xcd + 8 * (stripe + S * i); };
   int bn = tile_of(0);
   const int q0 = bq * SQW;
   const int g4 = 4 * (lane >> 4);
@@ -878,6 +883,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
                                                                                             int g0) {
   if ((int)blockIdx.x < g0) score32_body<0, KBM>(p0, blockIdx.x, g0);
   else score32_body<0, KBM>(p1, blockIdx.x - g0, gridDim.x - g0);
+}
+
+// The balanced grid for small candidate sets (MODE 0): the striped grid's 8 x nbq x stripes
+// workgroups under-fill the chip when nbq does not divide 32 (ICEWS18: 25 query tiles -> 200
+// workgroups, GDELT: 13 -> 208) and deals few tiles per workgroup unevenly; there the grid is
+// nbq x bal with bal ~ 256 / nbq candidate-tile strides (one 8-wave workgroup per CU).  Large
+// candidate sets (>= 64 tiles per strip: config 5) keep the XCD-aware strips.  REGCN_SCORE_BAL=0
+// disables it.
+static int score_bal_on() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("REGCN_SCORE_BAL");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+static int score_bal(int B, int nbn) {
+  const int nbq = (B + SQ2 - 1) / SQ2;
+  if (!score_bal_on() || nbn / (8 * score_f32_stripes(B, nbn)) >= 64) return 0;
+  return std::max(1, std::min(nbn, 256 / nbq));
 }
 
 // REGCN_SCORE32=1 selects the 32 x 32 x 2 kernel for the scores and rank counts (opt-in: measured
@@ -1284,7 +1309,11 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
     }
     if (ws) hipLaunchKernelGGL((k_score_ws<0>), g2, dim3(512), score_ws_lds(a.d), st, a);
     else if (nw4) hipLaunchKernelGGL((k_score_f32<0, 4>), g4, b4, lds4, st, a);
-    else if (fast) hipLaunchKernelGGL((k_score_f32<0>), g2, b2, lds2, st, a);
+    else if (fast) {
+      a.bal = score_bal(a.B, nbn);
+      const dim3 gb(a.bal ? (unsigned)(((a.B + SQ2 - 1) / SQ2) * a.bal) : g2.x);
+      hipLaunchKernelGGL((k_score_f32<0>), gb, b2, lds2, st, a);
+    }
     else if (a.use_dist) hipLaunchKernelGGL((k_score<0, true>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_score<0, false>), g, b, 0, st, a);
     return check_launch("k_score");
@@ -1329,7 +1358,14 @@ int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st) {
     const unsigned h0 = score_f32_grid<4>(a0.B, (a0.N + 31) / 32), h1 = score_f32_grid<4>(a1.B, (a1.N + 31) / 32);
     hipLaunchKernelGGL(k_score_f32_jobs<4>, dim3(h0 + h1), dim3(256), score_f32_lds<4>(a0.d), st, a0, a1, (int)h0);
   } else {
-    hipLaunchKernelGGL(k_score_f32_jobs<8>, dim3(g0 + g1), dim3(64 * SW2), score_f32_lds(a0.d), st, a0, a1, (int)g0);
+    unsigned h[2];
+    int j = 0;
+    for (ScoreArgs* a : {&a0, &a1}) {
+      const int nbn = (a->N + SN - 1) / SN;
+      a->bal = score_bal(a->B, nbn);
+      h[j++] = a->bal ? (unsigned)(((a->B + SQ2 - 1) / SQ2) * a->bal) : score_f32_grid(a->B, nbn);
+    }
+    hipLaunchKernelGGL(k_score_f32_jobs<8>, dim3(h[0] + h[1]), dim3(64 * SW2), score_f32_lds(a0.d), st, a0, a1, (int)h[0]);
   }
   return check_launch("k_score_f32_jobs");
 }
