@@ -58,6 +58,8 @@ sys.path.insert(0, os.path.join(REPO, "re-gcn_amd"))
 
 METRIC = "million edges aggregated/sec at d=200 history_len=3; MRR parity vs ref"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_COPY_GBS = 6300.0          # measured device copy rate (uniform-source aggregation)
+LINK_DERATE = 0.8              # owner simulation: the peer links at 80 % of nominal (the derated prediction)
 SIM_BLOCKER_CYCLES = int(os.environ.get("BENCH_SIM_BLOCKER_CYCLES", str(1_200_000_000)))  # ~0.5 s device wait
 FP32_MFMA_PEAK_TFLOPS = 157.3  # dense fp32 matrix peak (MI355X_MICROARCH.md)
 
@@ -913,7 +915,9 @@ def compact_line(out, detail_path=None):
             "speedup_vs_headline": sim.get("predicted_speedup_vs_headline"), "max_rank_ms": sim["max_rank_ms"],
             "mean_rank_ms": sim["mean_rank_ms"], "sum_rank_ms": round(sim["mean_rank_ms"] * sim["world"], 3),
             "exposed_exchange_ms": sim["exposed_exchange_ms_per_step"], "replicated_ms": sim["replicated_ms"],
-            "halo_delivery_ms_excluded": sim.get("halo_delivery_ms_excluded"), "blocker_margin_ms": sim.get("blocker_margin_ms")}
+            "receive_ms_max": max(sim.get("receive_ms_per_rank") or [0.0]),
+            "predicted_step_ms_links_derated": sim.get("predicted_step_ms_links_derated"),
+            "blocker_margin_ms": sim.get("blocker_margin_ms")}
     ag = out.get("aggregation_roofline")
     if ag:
         u = ag.get("uniform_src", {}).get("union_aggregate", {})
@@ -1293,8 +1297,16 @@ def owner_simulation(args, cfg, device, world):
     # per rank: chunk j's exchange starts when chunk j's rows are final and the link is free;
     # the next layer waits for the last one (RankSimulation.exposed_exchange_ms)
     exp_k = np.sum([sm.exposed_exchange_ms(link_gbs) for sm in sims], axis=0) / reps
-    exposed = float(exp_k[int(np.argmax(per_rank + exp_k))])
-    pred = float((per_rank + exp_k).max()) + replicated
+    # the receive side on a real node: RCCL's copy kernels land each received row in a FIFO in
+    # the receiver's HBM and copy it to the halo rows (a read + a write of the bytes through HBM),
+    # charged to the receiving rank at the measured 6.3 TB/s copy rate as if serialised with its
+    # compute (an upper bound: the copies run on a few CUs beside the layer kernels)
+    recv_ms = 2.0 * recv / (HBM_COPY_GBS * 1e9) * 1e3
+    exposed = float(exp_k[int(np.argmax(per_rank + exp_k + recv_ms))])
+    pred = float((per_rank + exp_k + recv_ms).max()) + replicated
+    # the same with the peer links derated to LINK_DERATE of their nominal 153 GB/s
+    exp_d = np.sum([sm.exposed_exchange_ms(link_gbs * LINK_DERATE) for sm in sims], axis=0) / reps
+    pred_derated = float((per_rank + exp_d + recv_ms).max()) + replicated
     return {
         "world": world, "chunks_per_rank": lay.chunks, "rows_per_chunk": lay.cr,
         "per_rank_ms": [round(float(x), 3) for x in per_rank],
@@ -1308,9 +1320,12 @@ def owner_simulation(args, cfg, device, world):
         "exposed_exchange_ms_per_rank": [round(float(x), 3) for x in exp_k],
         "exposed_exchange_ms_per_step": round(exposed, 3),
         "edge_loads_per_rank": loads, "edge_loads_contiguous_ids": loads_plain,
+        "receive_ms_per_rank": [round(float(x), 3) for x in recv_ms],
         "predicted_step_ms": round(pred, 3),
         "predicted_M_edges_per_s": round(edges / pred / 1e3, 1),
-        "halo_delivery_ms_excluded": round(delivery, 3),
+        "predicted_step_ms_links_derated": round(pred_derated, 3),
+        "link_derate": LINK_DERATE,
+        "halo_delivery_ms_simulated": round(delivery, 3),
         "blocker_margin_ms": round(margin[0], 1),  # > 0: every timed step was enqueued before its wait ended
         "as_issued": {"host_ms_per_step": round(host_issued_ms, 3),
                       "max_rank_ms": round(float((issued_rank + issued_dec).max()), 3),
@@ -1327,7 +1342,10 @@ def owner_simulation(args, cfg, device, world):
                 "its exposed exchange) + replicated.  Exchange: per chunk two all_to_alls (x rows, |h|) of "
                 "the rows the next layer reads (ExchangePlan) into the receivers' halo rows, its time = the "
                 "busiest peer link's bytes at the nominal 153 GB/s, starting when the chunk's rows are final "
-                "and the previous chunk's exchange is done; a layer exposes what runs past its last chunk",
+                "and the previous chunk's exchange is done; a layer exposes what runs past its last chunk.  "
+                "Receive side: each rank's received bytes cross its HBM twice (RCCL's FIFO, then the halo "
+                "rows) at the 6.3 TB/s copy rate, added to the rank as serialised time; the simulation's "
+                "own delivery copies (one GPU scattering all 8 ranks' halos) are reported, not used",
     }
 
 

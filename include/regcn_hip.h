@@ -76,7 +76,8 @@ int regcn_prologue_f32(const float* h, int64_t rows, int32_t d, float c, float* 
 /* exp0(normalize(log0(x))): layer-norm round trip, hyperbolic_model.py:832-835, :926-929 */
 int regcn_ln_roundtrip_f32(const float* x, int64_t rows, int32_t d, float c, float* out, void* stream);
 /* Initial entity state, hyperbolic_model.py:779-782: h = apply_radius(exp0([normalize]dyn), r_static);
- * also emits x = log0(h) and r = |h| for the first timestep (x_out/r_out may be NULL). */
+ * also emits x = log0(h) and r = |h| for the first timestep (x_out/r_out may be NULL; h_out may be
+ * NULL when x_out is not: the fused timestep reads x and |h| only). */
 int regcn_init_entities_f32(const float* dyn, const float* r_static, int64_t rows, int32_t d, float c,
                             int32_t layer_norm, float* h_out, float* x_out, float* r_out, void* stream);
 /* The same map over a row list (owner partition: a rank's own rows and the halo rows its first
@@ -311,7 +312,9 @@ int regcn_layer_f32(const regcn_layer_desc* desc, void* stream);
  *      same epilogue / timestep as regcn_layer_f32.
  * desc->w_n / w_loop / w_evolve / step_w_g are packed by regcn_pack_weight_kp_f32 for this
  * call (a k-permuted fragment order the tail's direct global A loads need).  No skip gate, no
- * dropout mask.  Values equal regcn_layer_f32's up to the fp32 order of the products' sums. */
+ * dropout mask.  Values equal regcn_layer_f32's up to the fp32 order of the products' sums.
+ * A layer without the timestep may pass h_out = NULL when x_next is set (a cell's inner layer:
+ * the next layer reads x_next and r_next only). */
 int regcn_layer_rowtail_f32(const regcn_layer_desc* desc, float* agg, void* stream);
 /* One part of regcn_layer_rowtail_f32, so a caller can pipeline row chunks on two streams
  * (the gather of chunk i + 1 beside the tail of chunk i): which = 1: the gather of tiles

@@ -705,7 +705,7 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
   if constexpr (!STEP) {
     // (element stores: staging them as in the step layer made the two-group first layer's
     // tail 2.5 % slower at config 5)
-    rt_store<NT>(v, p.h_out, crow, n_valid, d);
+    if (p.h_out) rt_store<NT>(v, p.h_out, crow, n_valid, d);
     if (p.r_next) rt_store_radius(n2, p.r_next, crow, n_valid);
     if (p.send_x) rt_send_radius(p, n2, crow, n_valid);
     if (p.x_next) {
@@ -970,7 +970,8 @@ int layer_rowtail(const LayerArgs& a, float* agg, hipStream_t st) {
 int layer_rowtail_part(const LayerArgs& a, float* agg, int which, int lo, int hi, hipStream_t st) {
   const int mode = a.agg_mode;
   if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "rowtail needs d %% 4 == 0, d <= 256");
-  if (!a.x || !a.rows || (!a.h_out && !a.fuse_step)) return set_error(REGCN_EINVAL, "null pointer");
+  // a non-step layer may skip h (h_out NULL) when its consumer reads x_next and r_next only
+  if (!a.x || !a.rows || (!a.h_out && !a.fuse_step && !a.x_next)) return set_error(REGCN_EINVAL, "null pointer");
   if ((a.w_loop == nullptr) != (a.w_evolve == nullptr)) return set_error(REGCN_EINVAL, "self-loop weights must come in pairs");
   if (a.prev_t || a.drop_mask) return set_error(REGCN_EINVAL, "rowtail has no skip gate / dropout mask (use regcn_layer_f32)");
   if (a.n_pos < 0 || a.n_pos > a.V) return set_error(REGCN_EINVAL, "bad n_pos");

@@ -314,7 +314,9 @@ static int launch_rowmap(const float* a, const float* b, const float* vec, int64
 int rowmap(int op, const float* a, const float* b, const float* vec, int64_t rows, int d, float c,
            float* out, float* out2, float* out3, hipStream_t st) {
   if (d <= 0) return set_error(REGCN_EINVAL, "d must be positive");
-  if (!a || !out) return set_error(REGCN_EINVAL, "null pointer");
+  // the initial state may skip h (out) when x is written (its consumers read x and |h| only)
+  const bool init_op = op == OP_INIT || op == OP_INIT_LN;
+  if (!a || (!out && !(init_op && out2))) return set_error(REGCN_EINVAL, "null pointer");
   Curv k = make_curv(c);
   switch (op) {
     case OP_LOG0: return launch_rowmap<OP_LOG0>(a, b, vec, rows, d, k, out, out2, out3, st);

@@ -44,6 +44,9 @@ CREL_MIN_ITEMS = int(os.environ.get("REGCN_CREL_MIN_ITEMS", "2048"))
 CREL_MIN_TILES = int(os.environ.get("REGCN_CREL_MIN_TILES", "768"))
 # A rank's pipeline-chunk tails (owner partition) on this many streams (1: one after another)
 CHUNK_TAIL_STREAMS = int(os.environ.get("REGCN_CHUNK_TAIL_STREAMS", "2"))
+# a fused-step cell's inner layer on the 64-row tail skips its Poincare rows h (the next layer
+# reads x = log0 h and |h| only): 800 MB less written per timestep at config 5
+INNER_SKIP_H = os.environ.get("REGCN_INNER_SKIP_H", "1") != "0"
 
 
 def _rowtail_chunks(g, k):
@@ -159,7 +162,7 @@ def _use_rowtail(V, n_rows, d, prev_t, drop_mask, pos_only):
 
 
 def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_t, w_skip, b_skip, drop_mask, c,
-              euclid=False, step=None, agg=None, out=None, pos_only=False, gate=None):
+              euclid=False, step=None, agg=None, out=None, pos_only=False, gate=None, need_h=True):
     """One fused layer launch (regcn_layer_f32): inline gather + GEMMs + epilogue, or with
     `step` the timestep too.  Returns (h, x_next, r_next) of the layer (or of the step).
     `g` may be a rank's view of a snapshot (parallel.py): the launch covers its rows only,
@@ -187,7 +190,7 @@ def run_layer(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, prev_
         mode = _lib.AGG_NONE
     if rowtail:
         return _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c, euclid, step, agg, out,
-                            gate, n_rows)
+                            gate, n_rows, need_h=need_h)
     if out is None:
         h = torch.empty_like(x)
         xn = torch.empty_like(x)
@@ -257,9 +260,10 @@ def run_layer_chunked(mode, g, tail_views, x, r, rel, w_rel, nb, gamma, w_n, w_l
 
 
 def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c, euclid, step, agg, out, gate,
-                 n_rows, tail_views=None, after=None, send=None):
+                 n_rows, tail_views=None, after=None, send=None, need_h=True):
     """regcn_layer_rowtail_f32: the inline in-edge rows gathered into `agg` (which holds the hub
-    rows already), then the 64-row tail over all rows (csrc/rowtail.hip)."""
+    rows already), then the 64-row tail over all rows (csrc/rowtail.hip).  need_h=False (a
+    cell's inner layer, whose consumer reads x_next and r_next only): h is not written."""
     wk = g.work()
     V, d = x.shape
     a = _lib.addr
@@ -305,7 +309,7 @@ def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c,
         desc.rel_t = a(cr[2])
         keep.append(cr[2])
     if step is None:
-        desc.h_out, desc.x_next, desc.r_next = a(h), a(xn), a(rn)
+        desc.h_out, desc.x_next, desc.r_next = a(h) if (need_h or not INNER_SKIP_H) else None, a(xn), a(rn)
         if gate is not None and gate.w_g_param is not None:
             if gate.tw is None:
                 gate.tw = torch.empty_like(x)
@@ -466,9 +470,10 @@ class HyperbolicUnionRGCNLayer(nn.Module):
             self.skip_bias = nn.Parameter(torch.zeros(out_feat))
         self.dropout = nn.Dropout(dropout) if dropout > 0 else None
 
-    def forward(self, g, h_hyper, rel_emb, prev_h=None, step=None, pos_only=False, out=None, gate=None):
+    def forward(self, g, h_hyper, rel_emb, prev_h=None, step=None, pos_only=False, out=None, gate=None,
+                need_h=True):
         """hyperbolic_layers.py:242-323 (one fused launch; `step` fuses the timestep;
-        pos_only/out/gate: see run_layer)."""
+        pos_only/out/gate/need_h: see run_layer)."""
         if self.activation is None:
             raise NotImplementedError("the fused tail applies rrelu; activation=None is not supported")
         self.rel_emb = rel_emb
@@ -483,7 +488,8 @@ class HyperbolicUnionRGCNLayer(nn.Module):
                               self.weight_neighbor, wl, we, prev_t,
                               self.skip_weight if prev_t is not None else None,
                               self.skip_bias.detach() if prev_t is not None else None,
-                              _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only, gate=gate)
+                              _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only, gate=gate,
+                              need_h=need_h)
         return attach(h, xn, rn, c)
 
 
@@ -518,9 +524,10 @@ class LorentzRGCNLayer(nn.Module):
         self.dropout = nn.Dropout(dropout) if dropout > 0 else None
         self.rel_emb = None
 
-    def forward(self, g, h_hyper, rel_emb=None, prev_h=None, step=None, pos_only=False, out=None, gate=None):
+    def forward(self, g, h_hyper, rel_emb=None, prev_h=None, step=None, pos_only=False, out=None, gate=None,
+                need_h=True):
         """hyperbolic_layers.py:627-694 (one fused launch; `step` fuses the timestep;
-        pos_only/out/gate: see run_layer)."""
+        pos_only/out/gate/need_h: see run_layer)."""
         if self.activation is None:
             raise NotImplementedError("the fused tail applies rrelu; activation=None is not supported")
         if self.submat_in * self.num_bases != self.in_feat:
@@ -544,7 +551,8 @@ class LorentzRGCNLayer(nn.Module):
                               None, wl, we, prev_t,
                               self.skip_weight if prev_t is not None else None,
                               self.skip_bias.detach() if prev_t is not None else None,
-                              _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only, gate=gate)
+                              _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only, gate=gate,
+                              need_h=need_h)
         return attach(h, xn, rn, c)
 
 
@@ -573,7 +581,8 @@ class LorentzRGCNCell(nn.Module):
         for i, layer in enumerate(self.layers):
             last = i == n - 1
             h_new = layer(g, h, rel_embs[i], prev_h=prev_h, step=step if last else None, pos_only=pos_only,
-                          out=out if last else None, gate=step if (i == 0 and not last) else None)
+                          out=out if last else None, gate=step if (i == 0 and not last) else None,
+                          need_h=last or step is None)
             prev_h = h
             h = h_new
         return h

@@ -80,7 +80,8 @@ class HyperbolicRGCNCell(HyperbolicBaseRGCN):
             # prev_h is never passed (hyperbolic_model.py:152)
             last = i == n - 1
             h = layer(g, h, rel_embs[i], step=step if last else None, pos_only=pos_only, out=out if last else None,
-                      gate=step if (i == 0 and not last) else None)
+                      gate=step if (i == 0 and not last) else None,
+                      need_h=last or step is None)  # a fused-step cell's inner h: read as x, |h| only
         return h
 
 
@@ -114,6 +115,7 @@ SPARSE_EXCHANGE = os.environ.get("REGCN_SPARSE_EXCHANGE", "1") != "0"
 # ... and each rank maps only the initial rows it reads (ShardedGraph.initial_state); 0: all V
 OWNER_INIT = os.environ.get("REGCN_OWNER_INIT", "1") != "0"
 
+INIT_SKIP_H = os.environ.get("REGCN_INIT_SKIP_H", "1") != "0"  # see HyperbolicRecurrentRGCN._initial_state
 REL_INLINE_MAX_SPAN = 64  # longer r_to_e spans are averaged by the chunked segment-mean kernel first
 
 
@@ -383,7 +385,10 @@ class HyperbolicRecurrentRGCN(nn.Module):
             h, x, r = scope["init"]
         else:
             r_static = self._static_radius(c_val).contiguous()
-            h, x, r = self._initial_state(c_val, r_static, g0 if owner0 else None)
+            # the fused per-layer path (config 5) reads the initial state's x and |h| only; the
+            # phase launches and the unfused timestep may read h itself
+            need_h = not (fused_step and not self._phases_ok(g_list) and INIT_SKIP_H)
+            h, x, r = self._initial_state(c_val, r_static, g0 if owner0 else None, need_h=need_h)
         attach(h, x, r, c_val)
         self.h = h
         R2 = self.num_rels * 2
@@ -459,16 +464,19 @@ class HyperbolicRecurrentRGCN(nn.Module):
                              torch.stack(gate_means) if gate_means else [])
         return history_embs, None, self.h_0, gate_list, []
 
-    def _initial_state(self, c_val, r_static, owner=None):
+    def _initial_state(self, c_val, r_static, owner=None, need_h=True):
         """(h, x, r) of the initial entity state (hyperbolic_model.py:775-782): a function of
         parameters only, computed once per parameter version (param_caches) and reused by every
         predict (the kernels read it, none writes it), so a captured predict graph holds no init
         launch.  owner: the first snapshot of an owner partition -- only the rows this rank
-        reads (ShardedGraph.initial_state)."""
+        reads (ShardedGraph.initial_state).  need_h=False: the Poincare rows h are not written
+        (the fused timestep path reads x = log0 h and |h| only: 800 MB less per predict at
+        config 5); h is then an unwritten buffer carrying x and |h| (tangent.attach)."""
         pe = self.dynamic_emb
         V, d = pe.shape
         key = (pe.data_ptr(), pe._version, self.radius_static.data_ptr(), self.radius_static._version,
-               float(c_val), bool(self.layer_norm), float(self.radius_min), float(self.radius_max), id(owner))
+               float(c_val), bool(self.layer_norm), float(self.radius_min), float(self.radius_max), id(owner),
+               bool(need_h))
         hit = self.__dict__.get("_init_cache")
         if hit is not None and hit[0] == key and hit[2] is owner and self.param_caches:
             return hit[1]
@@ -480,7 +488,8 @@ class HyperbolicRecurrentRGCN(nn.Module):
             x = torch.empty_like(dyn)
             r = torch.empty(V, device=pe.device, dtype=torch.float32)
             _lib.call("regcn_init_entities_f32", _lib.fptr(dyn, "dynamic_emb"), _lib.fptr(r_static), V, d, c_val,
-                      int(bool(self.layer_norm)), _lib.fptr(h), _lib.fptr(x), _lib.fptr(r), _lib.stream())
+                      int(bool(self.layer_norm)), _lib.fptr(h) if need_h else None, _lib.fptr(x), _lib.fptr(r),
+                      _lib.stream())
         if self.param_caches and not torch.cuda.is_current_stream_capturing():
             _lib.publish()
             self.__dict__["_init_cache"] = (key, (h, x, r), owner)
