@@ -794,7 +794,7 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     float f[4];
     spread_rows(fminf(fmaxf(newr, REGCN_EPS), kr.rmax) / fmaxf(sqrtf(n2o), REGCN_EPS), f);
     rt_scale_known<NT>(v, n2, f);
-    rt_store_staged<NT>(v, s.h_out, R, d, lds, p, false);
+    if (s.h_out) rt_store_staged<NT>(v, s.h_out, R, d, lds, p, false);
     if (s.r_out) rt_store_radius(n2, s.r_out, crow, n_valid);
     if (p.send_x) rt_send_radius(p, n2, crow, n_valid);
     if (s.x_out) {
@@ -987,7 +987,9 @@ int layer_rowtail_part(const LayerArgs& a, float* agg, int which, int lo, int hi
   if (a.fuse_step) {
     const StepArgs& s = a.step;
     if (a.euclid) return set_error(REGCN_EINVAL, "the fused timestep is hyperbolic only");
-    if (!s.x_prev || !s.w_g || !s.b_g || !s.r_static || !s.h_out) return set_error(REGCN_EINVAL, "null timestep pointer");
+    // the timestep may skip h (h_out NULL) when x_out is written (predict's earlier timesteps)
+    if (!s.x_prev || !s.w_g || !s.b_g || !s.r_static || (!s.h_out && !s.x_out))
+      return set_error(REGCN_EINVAL, "null timestep pointer");
     if (s.residual && (!s.w_r || !s.b_r)) return set_error(REGCN_EINVAL, "residual radius needs w_r and b_r");
   }
   if (a.V == 0) return 0;

@@ -152,6 +152,7 @@ class StepSpec:
         self.w_r, self.b_r, self.eps_r, self.beta = w_r, b_r, eps_r, beta
         self.layer_norm, self.residual, self.c_radius = layer_norm, residual, c_radius
         self.w_g_param, self.tw = w_g_param, None
+        self.need_h = True  # False: the timestep's Poincare rows h are not written (x, |h| are)
 
 
 def _use_rowtail(V, n_rows, d, prev_t, drop_mask, pos_only):
@@ -325,7 +326,8 @@ def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c,
         desc.step_eps_r, desc.step_beta = float(step.eps_r), float(step.beta)
         desc.step_layer_norm, desc.step_residual = int(bool(step.layer_norm)), int(bool(step.residual))
         desc.step_c_radius = float(step.c_radius)
-        desc.step_h_out, desc.step_x_out, desc.step_r_out = a(h), a(xn), a(rn)
+        skip = not step.need_h and INNER_SKIP_H
+        desc.step_h_out, desc.step_x_out, desc.step_r_out = None if skip else a(h), a(xn), a(rn)
         if step.tw is not None:
             desc.step_tw = a(step.tw)
             keep.append(step.tw)

@@ -420,6 +420,8 @@ class HyperbolicRecurrentRGCN(nn.Module):
                 step = StepSpec(x_prev, wg, bg, r_static, w_r, b_r, trev.epsilon, trev.anchor_beta,
                                 self.layer_norm, self.use_residual_evolution, trev.c,
                                 w_g_param=self.time_gate_weight)
+                # predict reads the last state's h only; the next timestep reads x and |h|
+                step.need_h = i == len(g_list) - 1 or not self.__dict__.get("_last_h_only")
                 self.h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0], step=step)
             else:
                 # the timestep kernel reads every row of current_h (and recomputes x, |h| from
@@ -817,6 +819,16 @@ class HyperbolicRecurrentRGCN(nn.Module):
             return HyperbolicOps.layer_norm_roundtrip(emb, c_val)  # :926-929 / :992-995
         return emb
 
+    def _forward_last_h(self, test_graph, static_graph, use_cuda):
+        """forward for predict: only the last history state's Poincare rows are read, so the
+        earlier timesteps' h need not be written (the fused per-layer path skips them; their x
+        and |h| are written as always).  The history list's earlier entries are not valid h."""
+        self.__dict__["_last_h_only"] = True
+        try:
+            return self.forward(test_graph, static_graph, use_cuda)
+        finally:
+            self.__dict__.pop("_last_h_only", None)
+
     def predict(self, test_graph, num_rels, static_graph, test_triplets, use_cuda):
         """hyperbolic_model.py:892-939."""
         with torch.no_grad():
@@ -826,7 +838,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
                     roth_pair_fusable(self.decoder_ob, self.rdecoder, self.dynamic_emb):
                 # one stream end to end: encoder, then the two-launch RotH/RotHRel front
                 # (queries + candidates + all_triples, then both scores in one launch)
-                evolve_embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
+                evolve_embs, _, r_emb, _, _ = self._forward_last_h(test_graph, static_graph, use_cuda)
                 last = evolve_embs[-1]
                 if getattr(last, "_regcn_owner", None) is not None:  # owner partition: rank-local rows
                     last._regcn_owner[0].complete_rows(last)
@@ -847,7 +859,7 @@ class HyperbolicRecurrentRGCN(nn.Module):
             if side is not None:
                 built = torch.cuda.Event()
                 built.record(side)
-            evolve_embs, _, r_emb, _, _ = self.forward(test_graph, static_graph, use_cuda)
+            evolve_embs, _, r_emb, _, _ = self._forward_last_h(test_graph, static_graph, use_cuda)
             if side is not None:
                 torch.cuda.current_stream(dev).wait_event(built)
                 all_triples.record_stream(torch.cuda.current_stream(dev))
