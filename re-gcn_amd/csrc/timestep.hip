@@ -466,21 +466,31 @@ __global__ __launch_bounds__(NTHR) void k_phase_a(PhaseArgs p) {
   extern __shared__ float lds[];
   PhaseStamp stamp(p);
   int b = blockIdx.x;
-  // every block of A is on the timestep's critical path
+  // every block of A is on the timestep's critical path; the dispatcher hands blocks out in
+  // order, so the longest go first: rows without in-edges (layer 0, ~11 us at GDELT's late
+  // timesteps), the relation GRU x-half (~10 us), the in-edge rows' GEMMs (~8 us), the memo
+  // copy (~4 us).  (GDELT timestep 6 with the zero rows last: they started at 8.4 us behind
+  // the GRU blocks and set the 25 us span, profiles/r6_phasetrace_gdelt.log.)
   __builtin_amdgcn_s_setprio(2);
-  if (b < 2 * p.n_pos_rt) {
-    if ((b & 1) == 0 && !p.L[0].w_loop) return;  // no self loop: the gate GEMM only
-    return a_pos_rows(p, b, lds);
+  // (the zero-row segment is padded to a multiple of 8 blocks, so the GRU blocks' XCD grouping
+  // -- blocks g and g + 8 on one XCD -- holds; the pads return at once)
+  const int zpad = gru_blocks_padded(p.n_zero_rt);
+  if (b < zpad) {
+    if (b < p.n_zero_rt) a_zero_rows(p, b, lds);
+    return;
   }
-  b -= 2 * p.n_pos_rt;
+  b -= zpad;
   if (b < gru_blocks_padded(p.n_gru)) {
     int bx, by;
     if (gru_block_xcd(b, p.n_gru, p.gru_rt, bx, by)) gru_x_block(p.gru, bx, by, lds);
     return;
   }
   b -= gru_blocks_padded(p.n_gru);
-  if (b < p.n_zero_rt) return a_zero_rows(p, b, lds);
-  copy_block(p, b - p.n_zero_rt);
+  if (b < 2 * p.n_pos_rt) {
+    if ((b & 1) == 0 && !p.L[0].w_loop) return;  // no self loop: the gate GEMM only
+    return a_pos_rows(p, b, lds);
+  }
+  copy_block(p, b - 2 * p.n_pos_rt);
 }
 
 template <int AGG, int S>
@@ -564,7 +574,7 @@ int timestep_phase(PhaseArgs a, int phase, hipStream_t st) {
     a.n_gru = a.gru.h_out ? gru_blocks : 0;
     if (a.n_gru && (!a.gru.h_prev || !a.gru.w_ih_x || !a.gru.pre || (!a.gru.x_mean && !a.gru.rel_start)))
       return set_error(REGCN_EINVAL, "GRU x-phase operands missing");
-    grid = (unsigned)(2 * a.n_pos_rt + gru_blocks_padded(a.n_gru) + n_zero_rt + a.n_copy);
+    grid = (unsigned)(gru_blocks_padded(n_zero_rt) + gru_blocks_padded(a.n_gru) + 2 * a.n_pos_rt + a.n_copy);
     lds = std::max({2 * tile + TM * 4, tile + small, a.n_gru ? gru_x_lds_bytes(d) : 0});
     if (grid) hipLaunchKernelGGL(k_phase_a, dim3(grid), dim3(NTHR), lds, st, a);
     return grid ? check_launch("k_phase_a") : 0;

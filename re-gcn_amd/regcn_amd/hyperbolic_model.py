@@ -651,7 +651,9 @@ class HyperbolicRecurrentRGCN(nn.Module):
             n_zero = ((sum(desc.prev_n_pos[i] for i in range(desc.n_prev)) if desc.memo_h else
                        0 if desc.skip_zero_rows else V - desc.n_pos) + 15) // 16
             n_copy = min(128, (V * d // 4 + 2047) // 2048) if desc.memo_h else 0  # timestep.hip launcher
-            kinds = ([("pos_rows", 2 * ((desc.n_pos + 15) // 16)), ("gru_x", n_gru), ("zero", n_zero), ("copy", n_copy)]
+            pad8 = lambda n: (n + 7) // 8 * 8  # noqa: E731  (segments padded for the XCD grouping)
+            kinds = ([("zero", pad8(n_zero)), ("gru_x", pad8(n_gru)), ("pos_rows", 2 * ((desc.n_pos + 15) // 16)),
+                      ("copy", n_copy)]
                      if phase == 0 else
                      [("pos_tiles", desc.n_pos_tiles), ("zero", n_zero)]
                      + ([("gru_pre", n_gru)] if phase == 1 and desc.gru_pre else []))

@@ -19,9 +19,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--var", default="REGCN_SCORE32")
     ap.add_argument("--shapes", default="1024x1000000,492x7128",
-                    help="B x N pairs (ICEWS18: 3080x23033, GDELT: 1540x7691)")
+                    help="B x N pairs, comma- or plus-separated (ICEWS18: 3080x23033, GDELT: 1540x7691)")
     a = ap.parse_args()
-    for shp in a.shapes.split(","):
+    for shp in a.shapes.replace("+", ",").split(","):
         B, N = (int(v) for v in shp.split("x"))
         reps = 5 if N >= 100_000 else 200
         for rnd in range(a.rounds):
