@@ -62,8 +62,16 @@ __device__ __forceinline__ void gru_mfma(const float* arow, const f4* bb, int64_
   }
 }
 
-constexpr int PRE_WAVES = 4;  // 2 on W_ih^e (emb columns), 2 on W_hh
-constexpr int X_WAVES = 4;    // K = d split 4 ways
+// Every wave of the unit's workgroup (NWAVE, rowtile.h: 8 in the dataset-size kernels and the
+// standalone relgru.hip launches, 4 otherwise) takes part in the products: the pre-phase puts
+// half of them on W_ih^e (emb columns) and half on W_hh, the x-phase splits K = d over all of
+// them, each wave a 1/NWAVE share of the k-blocks (at 8 waves the GRU blocks' MFMA chains are
+// half as long as at 4, and no wave of an 8-wave phase workgroup idles through them).  The C
+// registers are finished by waves 0-3 (wave q: C register q), summing every wave's partial in
+// wave order.
+constexpr int PRE_WAVES = NWAVE;
+constexpr int X_WAVES = NWAVE;
+static_assert(NWAVE >= 4 && NWAVE % 2 == 0, "the GRU parts need >= 4 waves (one per C register)");
 
 __host__ __device__ inline int gru_dpad(int d) { return (d + 15) & ~15; }
 // A tile stride for `parts` d-wide operand blocks, each zero padded to a multiple of 16 and
@@ -86,13 +94,17 @@ __device__ __forceinline__ bool gru_block_xcd(int g, int n, int rt, int& bx, int
   return w < n;
 }
 
-inline size_t gru_pre_lds_bytes(int d) { return (size_t)TM * gru2_lda(d, 2) * 4 + (size_t)PRE_WAVES * 3 * 64 * 16; }
+// the waves' gate partials (PRE_WAVES x 3 x 64 float4) reuse the A tile's LDS once every wave's
+// products have read it (one barrier between)
+inline size_t gru_pre_lds_bytes(int d) {
+  return std::max((size_t)TM * gru2_lda(d, 2) * 4, (size_t)PRE_WAVES * 3 * 64 * 16);
+}
 
 // Workgroup (bx, by) of the pre-phase: relation rows 16 bx.., output column tile by.
 __device__ __forceinline__ void gru_pre_block(const RelGru2Args& p, int bx, int by, float* lds) {
   const int d = p.d, dp = gru_dpad(d), lda = gru2_lda(d, 2);
   float* A = lds;  // TM x lda: [emb_rel | 0 pad | h_prev | 0 pad]
-  f4* red = reinterpret_cast<f4*>(lds + TM * lda);  // [PRE_WAVES][3][64]
+  f4* red = reinterpret_cast<f4*>(lds);  // [PRE_WAVES][3][64], over A after the products
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // Every wave of the workgroup runs this whole body and so meets every one of its barriers;
@@ -132,6 +144,7 @@ __device__ __forceinline__ void gru_pre_block(const RelGru2Args& p, int bx, int 
     }
   }
   __syncthreads();
+  f4 ar = {0.f, 0.f, 0.f, 0.f}, az = ar, an = ar;
   if (act) {
     const bool hh = w >= PRE_WAVES / 2;
     const int wi = hh ? w - PRE_WAVES / 2 : w;
@@ -139,16 +152,18 @@ __device__ __forceinline__ void gru_pre_block(const RelGru2Args& p, int bx, int 
     const int beg = (NB * wi) / (PRE_WAVES / 2), end = (NB * (wi + 1)) / (PRE_WAVES / 2);
     const f4* bb = reinterpret_cast<const f4*>(hh ? p.w_hh : p.w_ih_e) + (int64_t)jt * 64 + lane;
     const int64_t gs = (int64_t)NB * NT * 64;
-    f4 ar = {0.f, 0.f, 0.f, 0.f}, az = ar, an = ar;
     const float* arow = A + (lane & 15) * lda + 4 * (lane >> 4) + (hh ? dp : 0);
     if (beg < end) gru_mfma(arow, bb, gs, NT, beg, end, ar, az, an);
+  }
+  __syncthreads();  // every wave's products have read A: its LDS takes the partials
+  if (act) {
     red[(w * 3 + 0) * 64 + lane] = ar;
     red[(w * 3 + 1) * 64 + lane] = az;
     red[(w * 3 + 2) * 64 + lane] = an;
   }
   __syncthreads();
-  if (!act) return;  // past the last barrier
-  const int q = w;  // PRE_WAVES == 4: wave q finishes C register q (row 4 (lane >> 4) + q)
+  if (!act || w >= 4) return;  // past the last barrier; waves 0-3 finish the C registers
+  const int q = w;  // wave q finishes C register q (row 4 (lane >> 4) + q)
   float sr = 0.f, sz = 0.f, sn_i = 0.f, sn_h = 0.f;
 #pragma unroll
   for (int w2 = 0; w2 < PRE_WAVES; ++w2) {
@@ -248,9 +263,13 @@ __device__ __forceinline__ void stage_rel_means(const RelGru2Args& p, float* A, 
   }
 }
 
-inline size_t gru_x_lds_bytes(int d) {
-  return (size_t)(TM + TM + X_WAVES - 1) * gru2_lda(d, 1) * 4 + (size_t)X_WAVES * 3 * 64 * 16 + 16 * 4;
+// A (TM x lda) | the partial rows of the relation means ((TM + X_WAVES - 1) x lda), whose LDS the
+// waves' gate partials (X_WAVES x 3 x 64 float4) reuse after the means are staged | tmask
+__host__ __device__ inline int gru_x_part_floats(int d) {
+  const int rows = (TM + X_WAVES - 1) * gru2_lda(d, 1), red = X_WAVES * 3 * 64 * 4;
+  return rows > red ? rows : red;
 }
+inline size_t gru_x_lds_bytes(int d) { return ((size_t)TM * gru2_lda(d, 1) + gru_x_part_floats(d)) * 4 + 16 * 4; }
 
 // Workgroup (bx, by) of the x-phase.  The gate partials and h_prev are loaded at entry
 // (they depend on nothing here), so their latency hides under the relation-mean gather.
@@ -258,8 +277,8 @@ __device__ __forceinline__ void gru_x_block(const RelGru2Args& p, int bx, int by
   const int d = p.d, dp = gru_dpad(d), lda = gru2_lda(d, 1);
   float* A = lds;                                         // TM x lda: x_mean | 0 pad
   float* part = lds + TM * lda;                           // (TM + X_WAVES - 1) x lda partial rows
-  f4* red = reinterpret_cast<f4*>(part + (TM + X_WAVES - 1) * lda);  // [X_WAVES][3][64]
-  int* tmask = reinterpret_cast<int*>(red + X_WAVES * 3 * 64);
+  f4* red = reinterpret_cast<f4*>(part);                  // [X_WAVES][3][64], over part after staging
+  int* tmask = reinterpret_cast<int*>(part + gru_x_part_floats(d));
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // as in gru_pre_block: every wave meets every barrier, waves past the part's four skip the work
@@ -268,9 +287,9 @@ __device__ __forceinline__ void gru_x_block(const RelGru2Args& p, int bx, int by
   const int n_valid = min(TM, p.R2 - r0);
   const int NB = dp >> 4, NT = dp >> 4;
   const int beg = (NB * w) / X_WAVES, end = (NB * (w + 1)) / X_WAVES;
-  const int ei = 4 * (lane >> 4) + w;  // this lane's output element (wave w finishes C register w)
+  const int ei = 4 * (lane >> 4) + w;  // this lane's output element (wave w < 4 finishes C register w)
   const int en = 16 * jt + (lane & 15);
-  const bool eok = act && ei < n_valid && en < d;
+  const bool eok = act && w < 4 && ei < n_valid && en < d;
   const int64_t erow = (int64_t)(r0 + (eok ? ei : 0));
   const int ecol = eok ? en : 0;
   const float* pr = p.pre + erow * 4 * d;
@@ -301,8 +320,8 @@ __device__ __forceinline__ void gru_x_block(const RelGru2Args& p, int bx, int by
     red[(w * 3 + 2) * 64 + lane] = an;
   }
   __syncthreads();
-  if (!act) return;  // past the last barrier
-  const int q = w;  // X_WAVES == 4: wave q finishes C register q
+  if (!act || w >= 4) return;  // past the last barrier; waves 0-3 finish the C registers
+  const int q = w;  // wave q < 4 finishes C register q
   float v[3];
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
