@@ -31,12 +31,16 @@ namespace regcn {
 
 // ------------------------------------------------------------------------------ packing
 // Wp[s][jq][lane][e] = W[16 (s / 4) + 4 (lane / 16) + s % 4][16 (4 jq + e) + lane % 16], zero
-// outside d_in x d_out; s < 4 * ceil(d_in / 16).
+// outside d_in x d_out; s < 4 * ceil(d_in / 16).  The last 16-deep block is transposed:
+// W[16 (s / 4) + 4 (s % 4) + lane / 16][...], so its k-steps past d_in hold only zero rows and
+// rt_mm skips them (d = 200: 2 of the block's 4 steps, 50 k-steps per product instead of 52).
 __global__ void k_pack_weight_kp(const float* __restrict__ W, int d_in, int d_out, int S, float* __restrict__ Wp) {
   const int total = S * 4 * 64 * 4;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
     const int e = idx & 3, lane = (idx >> 2) & 63, jq = (idx >> 8) & 3, s = idx >> 10;
-    const int k = 16 * (s >> 2) + 4 * (lane >> 4) + (s & 3), n = 16 * (4 * jq + e) + (lane & 15);
+    const bool last = (s >> 2) == (S >> 2) - 1;
+    const int k = 16 * (s >> 2) + (last ? 4 * (s & 3) + (lane >> 4) : 4 * (lane >> 4) + (s & 3));
+    const int n = 16 * (4 * jq + e) + (lane & 15);
     Wp[idx] = (k < d_in && n < d_out) ? W[(int64_t)k * d_out + n] : 0.f;
   }
 }
@@ -342,6 +346,51 @@ constexpr int RT_A_RING = 3;
 // A ring (3 k-blocks x 4 waves x RG groups x 1 KB)
 __host__ __device__ constexpr size_t rt_lds_bytes(int RG) { return 2 * RT_KB_BYTES + RT_A_RING * 4 * RG * 1024; }
 
+// One 16-deep k-block of rt_mm: acc[g] += A_g[.., block] @ W[block, ..].  A fragments from the
+// wave's ring slot `aslot` (lane l: row l % 16, columns 4 (l / 16) .. + 3 of the block), B
+// fragments from the LDS weight buffer `buf` (this lane's first).  LAST: the transposed last
+// block (k_pack_weight_kp) -- k-step e, lane group q takes column 4 e + q, i.e. element q of the
+// piece lane 16 e + l % 16 copied -- and only its first `ns` k-steps (the others hold columns
+// >= d only).
+template <int NT, int RG, bool CLAMP>
+__device__ __forceinline__ void rt_block(RAcc<NT> (&acc)[RG], const char* aslot, const f4* buf, bool LAST, int ns) {
+  const int lane = threadIdx.x & 63;
+  f4 a[RG];
+#pragma unroll
+  for (int g = 0; g < RG; ++g) {
+    if (!LAST) {
+      a[g] = *reinterpret_cast<const f4*>(aslot + g * 1024 + lane * 16);
+    } else {
+      const float* t = reinterpret_cast<const float*>(aslot + g * 1024 + (lane & 15) * 16) + (lane >> 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[g][e] = t[64 * e];
+    }
+  }
+  constexpr int JQ = (NT + 3) / 4;  // fragment quads a k-step reads
+  f4 b[2][4];
+#pragma unroll
+  for (int jq = 0; jq < JQ; ++jq) b[0][jq] = buf[jq * 64];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (s >= ns) break;  // wave-uniform
+    if (s + 1 < ns) {
+#pragma unroll
+      for (int jq = 0; jq < JQ; ++jq) b[(s + 1) & 1][jq] = buf[((s + 1) * 4 + jq) * 64];
+    }
+    // k-step s + 1's fragment reads stay ahead of k-step s's MFMAs (the scheduler would
+    // otherwise sink each read to its first use and wait for it there)
+    __builtin_amdgcn_sched_barrier(0);
+    float as[RG];
+#pragma unroll
+    for (int g = 0; g < RG; ++g) as[g] = CLAMP ? fminf(fmaxf(a[g][s], -10.f), 10.f) : a[g][s];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g = 0; g < RG; ++g)
+        acc[g].t[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(as[g], b[s & 1][t >> 2][t & 3], acc[g].t[t], 0, 0, 0);
+  }
+}
+
 // acc[g] += A_g[16 rows x K] @ W for the wave's RG row groups: A row of lane l in group g =
 // arow[g] (row l % 16 of the group), columns >= d and rows with !aok[g] read as 0, CLAMP: A
 // clamped to +-10 (the time gate's operand); Wp packed by k_pack_weight_kp.  Both operands
@@ -351,7 +400,8 @@ __host__ __device__ constexpr size_t rt_lds_bytes(int RG) { return 2 * RT_KB_BYT
 // in flight while k-block kb's MFMAs run; every B fragment read feeds RG MFMAs.  Masked A
 // lanes DMA from a zero row.  One raw barrier per k-block after a counted vmcnt (the A block
 // two ahead may stay in flight across it; __syncthreads would drain it).  Every wave of the
-// workgroup must call this with the same Wp and KB.
+// workgroup must call this with the same Wp and KB.  The last k-block runs only its k-steps
+// that hold columns < d (rt_block).
 template <int NT, int RG, bool CLAMP>
 __device__ __forceinline__ void rt_mm(RAcc<NT> (&acc)[RG], const float* const (&arow)[RG], const bool (&aok)[RG],
                                       const float* __restrict__ Wp, int d, int KB, char* lds) {
@@ -361,6 +411,7 @@ __device__ __forceinline__ void rt_mm(RAcc<NT> (&acc)[RG], const float* const (&
   char* abuf = lds + 2 * RT_KB_BYTES + w * RG * 1024;
   const char* wsrc = reinterpret_cast<const char*>(Wp);
   const float* zrow = reinterpret_cast<const float*>(kZeroRow);
+  const int nlast = (d - 16 * (KB - 1) + 3) >> 2;  // k-steps of the last block with columns < d
   auto dma_w = [&](int kb) {  // this wave's quarter of k-block kb into buffer kb & 1
     char* dst = wbuf + (kb & 1) * RT_KB_BYTES + w * (RT_KB_BYTES / 4);
     const char* src = wsrc + (int64_t)kb * RT_KB_BYTES + w * (RT_KB_BYTES / 4) + lane * 16;
@@ -393,33 +444,10 @@ __device__ __forceinline__ void rt_mm(RAcc<NT> (&acc)[RG], const float* const (&
     }
     if (kb + 1 < KB) dma_w(kb + 1);
     if (kb + 2 < KB) dma_a(kb + 2);
-    f4 a[RG];
-#pragma unroll
-    for (int g = 0; g < RG; ++g)
-      a[g] = *reinterpret_cast<const f4*>(abuf + (kb % RT_A_RING) * A_SLOT + g * 1024 + lane * 16);
+    const char* aslot = abuf + (kb % RT_A_RING) * A_SLOT;
     const f4* buf = reinterpret_cast<const f4*>(wbuf + (kb & 1) * RT_KB_BYTES) + lane;
-    constexpr int JQ = (NT + 3) / 4;  // fragment quads a k-step reads
-    f4 b[2][4];
-#pragma unroll
-    for (int jq = 0; jq < JQ; ++jq) b[0][jq] = buf[jq * 64];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      if (s + 1 < 4) {
-#pragma unroll
-        for (int jq = 0; jq < JQ; ++jq) b[(s + 1) & 1][jq] = buf[((s + 1) * 4 + jq) * 64];
-      }
-      // k-step s + 1's fragment reads stay ahead of k-step s's MFMAs (the scheduler would
-      // otherwise sink each read to its first use and wait for it there)
-      __builtin_amdgcn_sched_barrier(0);
-      float as[RG];
-#pragma unroll
-      for (int g = 0; g < RG; ++g) as[g] = CLAMP ? fminf(fmaxf(a[g][s], -10.f), 10.f) : a[g][s];
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int g = 0; g < RG; ++g)
-          acc[g].t[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(as[g], b[s & 1][t >> 2][t & 3], acc[g].t[t], 0, 0, 0);
-    }
+    const bool last = kb + 1 == KB;
+    rt_block<NT, RG, CLAMP>(acc, aslot, buf, last, last ? nlast : 4);
   }
   // every wave has read the last buffers before a following call refills them
   asm volatile("s_barrier" ::: "memory");
@@ -445,40 +473,34 @@ __device__ __forceinline__ void rt_scale(RAcc<NT>& a, const float f[4]) {
     for (int r = 0; r < 4; ++r) a.t[t][r] *= f[r];
 }
 
+// Row maps with the scaling deferred: m2 = |row|^2 and pf = the factor not yet multiplied into
+// the row's elements, both for the lane's own row (own_row: lane l holds row l & 3 of its
+// quarter).  A chain of maps (exp0 + project, project, log0, F.normalize, the radius) updates
+// the two scalars only; rt_apply then multiplies the product of the chain's factors in, one
+// pass over the row's elements instead of one per map (the step tail's chains of 6 and 4).
+struct RtLazy {
+  float m2, pf;
+};
+__device__ __forceinline__ void lz_scale(RtLazy& z, float f) {
+  z.pf *= f;
+  z.m2 *= f * f;
+}
+__device__ __forceinline__ void lz_project(RtLazy& z, const Curv& k) { lz_scale(z, project_factor(z.m2, k)); }
+__device__ __forceinline__ void lz_log0(RtLazy& z, const Curv& k) { lz_scale(z, log0_factor(z.m2, k)); }
+__device__ __forceinline__ void lz_exp0(RtLazy& z, const Curv& k) {  // exp0 + project
+  float o;
+  z.pf *= exp0_factor(z.m2, k, &o);
+  z.m2 = o;
+}
+__device__ __forceinline__ void lz_normalize(RtLazy& z) {  // F.normalize, eps 1e-12
+  lz_scale(z, 1.0f / fmaxf(sqrtf(z.m2), 1e-12f));
+}
 template <int NT>
-__device__ __forceinline__ void rt_scale_known(RAcc<NT>& a, float n2[4], const float f[4]) {
+__device__ __forceinline__ void rt_apply(RAcc<NT>& a, RtLazy& z) {
+  float f[4];
+  spread_rows(z.pf, f);
   rt_scale(a, f);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) n2[r] *= f[r] * f[r];
-}
-
-template <int NT>
-__device__ __forceinline__ void rt_project(RAcc<NT>& a, float n2[4], const Curv& k) {
-  float f[4];
-  spread_rows(project_factor(own_row(n2), k), f);
-  rt_scale_known(a, n2, f);
-}
-
-template <int NT>
-__device__ __forceinline__ void rt_log0(RAcc<NT>& a, float n2[4], const Curv& k) {
-  float f[4];
-  spread_rows(log0_factor(own_row(n2), k), f);
-  rt_scale_known(a, n2, f);
-}
-
-template <int NT>
-__device__ __forceinline__ void rt_exp0(RAcc<NT>& a, float n2[4], const Curv& k) {  // exp0 + project
-  float f[4], o;
-  spread_rows(exp0_factor(own_row(n2), k, &o), f);
-  rt_scale(a, f);
-  spread_rows(o, n2);
-}
-
-template <int NT>
-__device__ __forceinline__ void rt_normalize(RAcc<NT>& a, float n2[4]) {  // F.normalize, eps 1e-12
-  float f[4];
-  spread_rows(1.0f / fmaxf(sqrtf(own_row(n2)), 1e-12f), f);
-  rt_scale_known(a, n2, f);
+  z.pf = 1.f;
 }
 
 // C-layout rows of a row-major matrix (columns >= d and rows past n_valid read 0)
@@ -699,30 +721,42 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     v.t[t] = leaky4(v.t[t]);
   }
   float n2[4];
-  if (!p.euclid || p.r_next) rt_sumsq<NT>(v, n2);
-  if (!p.euclid) rt_exp0<NT>(v, n2, p.k);
+  RtLazy z{0.f, 1.f};
+  if (!p.euclid || p.r_next) {
+    rt_sumsq<NT>(v, n2);
+    z.m2 = own_row(n2);
+  }
+  if (!p.euclid) lz_exp0(z, p.k);
 
   if constexpr (!STEP) {
     // (element stores: staging them as in the step layer made the two-group first layer's
     // tail 2.5 % slower at config 5)
-    if (p.h_out) rt_store<NT>(v, p.h_out, crow, n_valid, d);
+    if (p.h_out) {
+      if (!p.euclid) rt_apply<NT>(v, z);
+      rt_store<NT>(v, p.h_out, crow, n_valid, d);
+    }
+    spread_rows(z.m2, n2);
     if (p.r_next) rt_store_radius(n2, p.r_next, crow, n_valid);
     if (p.send_x) rt_send_radius(p, n2, crow, n_valid);
     if (p.x_next) {
-      if (!p.euclid) rt_log0<NT>(v, n2, p.k);
+      if (!p.euclid) {
+        lz_log0(z, p.k);
+        rt_apply<NT>(v, z);
+      }
       rt_store<NT>(v, p.x_next, crow, n_valid, d);
       if (p.send_x) rt_send_rows<NT>(v, p, crow, n_valid, d);
     }
   } else {
     const StepArgs& s = p.step;
     const Curv k = s.k;
-    rt_project<NT>(v, n2, k);
+    lz_project(z, k);
     if (s.layer_norm) {
-      rt_log0<NT>(v, n2, k);
-      rt_normalize<NT>(v, n2);
-      rt_exp0<NT>(v, n2, k);
+      lz_log0(z, k);
+      lz_normalize(z);
+      lz_exp0(z, k);
     }
-    rt_log0<NT>(v, n2, k);
+    lz_log0(z, k);
+    rt_apply<NT>(v, z);
     float bg[NT];
     rt_col<NT>(bg, s.b_g, d);
     if constexpr (MODE == RT_STEP_PRE) {
@@ -769,16 +803,18 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
       }
     }
     rt_sumsq<NT>(v, n2);
-    rt_exp0<NT>(v, n2, k);
-    rt_project<NT>(v, n2, k);  // hyperbolic_model.py:860
+    z.m2 = own_row(n2);
+    lz_exp0(z, k);
+    lz_project(z, k);  // hyperbolic_model.py:860
     // radius: per-row scalars once per lane, for its own row r = lane & 3 (own_row)
     const float rs = s.r_static[own_int(crow)];
-    const float n2o = own_row(n2);
+    const float n2o = z.m2;
     float newr = rs;
     if (s.residual) {
       float wr[NT], lf[4], dl[4];
       rt_col<NT>(wr, s.w_r, d);
-      spread_rows(log0_factor(n2o, s.k_rad), lf);
+      // log0 of the row v pf (its factor still pending): one factor per row
+      spread_rows(z.pf * log0_factor(n2o, s.k_rad), lf);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float acc = 0.f;
@@ -791,14 +827,17 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
       newr = (s.beta * rs + (1.f - s.beta) * dyn) + delta;
     }
     const Curv kr = s.residual ? s.k_rad : s.k;
-    float f[4];
-    spread_rows(fminf(fmaxf(newr, REGCN_EPS), kr.rmax) / fmaxf(sqrtf(n2o), REGCN_EPS), f);
-    rt_scale_known<NT>(v, n2, f);
-    if (s.h_out) rt_store_staged<NT>(v, s.h_out, R, d, lds, p, false);
+    lz_scale(z, fminf(fmaxf(newr, REGCN_EPS), kr.rmax) / fmaxf(sqrtf(n2o), REGCN_EPS));
+    if (s.h_out) {
+      rt_apply<NT>(v, z);
+      rt_store_staged<NT>(v, s.h_out, R, d, lds, p, false);
+    }
+    spread_rows(z.m2, n2);
     if (s.r_out) rt_store_radius(n2, s.r_out, crow, n_valid);
     if (p.send_x) rt_send_radius(p, n2, crow, n_valid);
     if (s.x_out) {
-      rt_log0<NT>(v, n2, k);
+      lz_log0(z, k);
+      rt_apply<NT>(v, z);
       rt_store_staged<NT>(v, s.x_out, R, d, lds, p, p.send_x != nullptr);
     }
   }
@@ -936,6 +975,16 @@ static int rt_rg2_min_rows() {
   return v;
 }
 
+// REGCN_STEP_RG=2: the step layer's tail with two row groups per wave too (A/B; default one)
+static int step_rg() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("REGCN_STEP_RG");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
 template <int NT>
 static int launch_tail(const LayerArgs& a, int r0, int r1, hipStream_t st) {
   // two groups only when the launch still fills the chip with 128-row workgroups (a rank's
@@ -943,7 +992,9 @@ static int launch_tail(const LayerArgs& a, int r0, int r1, hipStream_t st) {
   const int rg = (NT > 8 && rowtail_rg() == 2 && r1 - r0 >= rt_rg2_min_rows()) ? 2 : 1;
   const unsigned grid = (unsigned)((r1 - r0 + RT_ROWS * rg - 1) / (RT_ROWS * rg));
   const size_t lds = rt_lds_bytes(rg);
-  if (a.fuse_step && a.step.tw) {
+  if (a.fuse_step && a.step.tw && rg == 2 && step_rg() == 2) {
+    hipLaunchKernelGGL((k_rowtail2<NT, RT_STEP_PRE>), dim3(grid), dim3(NTHR), lds, st, a, r0);
+  } else if (a.fuse_step && a.step.tw) {
     hipLaunchKernelGGL((k_rowtail3<NT, RT_STEP_PRE>), dim3((r1 - r0 + RT_ROWS - 1) / RT_ROWS), dim3(NTHR),
                        rt_lds_bytes(1), st, a, r0);
   } else if (a.fuse_step) {

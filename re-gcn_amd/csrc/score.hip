@@ -484,8 +484,12 @@ static int score_nw() {
 
 // One workgroup's work: `blk` of `nblk` workgroups of this job (the XCD of blk is blk % 8:
 // a job's first workgroup must sit at a multiple of 8 in the launch).
-template <int MODE, int NW>
+// KBT: the number of 16-deep k-blocks when known at compile time (13: 192 < d <= 208, every
+// configuration's d = 200), so the query registers and staging loads are sized to it; 0 = any
+// d <= 256.
+template <int MODE, int NW, int KBT = 0>
 __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const int nblk) {
+  constexpr int KBA = KBT ? KBT : KB_MAX;
   constexpr int SQW = 16 * NW, SNW = 8 * NW, J = SNW / 16;  // queries, candidates per tile; accumulators
   extern __shared__ float Es[];  // 2 x SNW x SE candidate rows, zero past N and d
   p.scale = p.scale_p ? *p.scale_p : 1.f;
@@ -498,7 +502,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     if (p.trace && tid == 0) p.trace[(int64_t)blk * 16 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  const int d = p.d, KB = (d + 15) >> 4, SE = score_lds_stride(d);
+  const int d = p.d, KB = KBT ? KBT : (d + 15) >> 4, SE = score_lds_stride(d);
   const int nbn = p.n_rng ? p.rng_total : (p.N + SNW - 1) / SNW, nbq = (p.B + SQW - 1) / SQW;
   // candidate tile t -> its first row and valid rows (row ranges: a tile never spans two)
   auto tile_rows = [&](int t, int& row0, int& nvalid) {
@@ -564,14 +568,25 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   const int qr = q0 + 16 * wv + (lane & 15);
   const bool q_ok = qr < p.B;
   const float* qrow = p.q + (int64_t)min(qr, p.B - 1) * d;
-  f4 a[KB_MAX];
+  // The last k-block is transposed in both operands (stash below): MFMA step e, lane group q
+  // takes column 16 b + 4 e + q, so its steps past d hold pad columns only and are skipped
+  // (d = 200: 50 k-steps per tile instead of 52).
+  const int nlast = (d - 16 * (KB - 1) + 3) >> 2;
+  f4 a[KBA - 1], alast;  // blocks 0 .. KB - 2; the last block, transposed
   float xs = 0.f;
 #pragma unroll
-  for (int b = 0; b < KB_MAX; ++b) {
+  for (int b = 0; b < KBA - 1; ++b) {
     const f4 v = *reinterpret_cast<const f4*>(qrow + min(16 * b + g4, d - 4));
-    a[b] = (q_ok & (b < KB) & (16 * b + g4 < d)) ? v : z4;
+    a[b] = (q_ok & (b < KB - 1) & (16 * b + g4 < d)) ? v : z4;
     xs += dot4(a[b], a[b]);
   }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int col = 16 * (KB - 1) + 4 * e + (lane >> 4);
+    const float v = qrow[min(col, d - 1)];
+    alast[e] = (q_ok & (col < d)) ? v : 0.f;
+  }
+  xs += dot4(alast, alast);
   // |q|^2 of query (lane & 15): sum the 4 k-quarters; the C rows of this lane
   xs += __shfl_xor(xs, 16);
   xs += __shfl_xor(xs, 32);
@@ -585,7 +600,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   }
   // staging map: thread tid stages candidate row tid / 8, float4 units tid % 8 + 8 it
   static_assert(64 * NW == 8 * SNW, "staging map: 8 threads per candidate row");
-  constexpr int IT = KB_MAX * 4 / 8;
+  constexpr int IT = (KBA * 4 + 7) / 8;
   const int sr = tid >> 3, sub = tid & 7, per_row = 4 * KB;
   f4 v[IT];
   auto fetch = [&](int t) {  // unconditional clamped loads (a conditional load drains vmcnt)
@@ -608,7 +623,17 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
       const int u = sub + 8 * it;
       const f4 w = (row_ok & (4 * u < d)) ? v[it] : z4;
       ss += dot4(w, w);
-      if (u < per_row) *reinterpret_cast<f4*>(lrow + 4 * u) = w;
+      if (u < per_row) {
+        if (u >= per_row - 4) {  // the transposed last block: column 16 b + 4 e + i at 4 i + e
+          float* bl = lrow + (per_row - 4) * 4 + (u - (per_row - 4));
+          bl[0] = w.x;
+          bl[4] = w.y;
+          bl[8] = w.z;
+          bl[12] = w.w;
+        } else {
+          *reinterpret_cast<f4*>(lrow + 4 * u) = w;
+        }
+      }
     }
     ss += __shfl_xor(ss, 1);
     ss += __shfl_xor(ss, 2);
@@ -631,16 +656,20 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[j] = z4;
     // B fragments of block b + 1 are read while block b's MFMAs run (register double buffer;
-    // the read past the last block is clamped, never used)
-    f4 bb[2][J];  // ping-pong by block parity (static after unrolling: no copies)
+    // the last block's into blast)
+    f4 bb[2][J], blast[J];  // ping-pong by block parity (static after unrolling: no copies)
 #pragma unroll
     for (int j = 0; j < J; ++j) bb[0][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE);
 #pragma unroll
-    for (int b = 0; b < KB_MAX; ++b) {
-      if (b < KB) {  // wave-uniform
-        const int bnx = min(b + 1, KB - 1);
+    for (int b = 0; b < KBA - 1; ++b) {
+      if (b < KB - 1) {  // wave-uniform
+        if (b + 1 < KB - 1) {
 #pragma unroll
-        for (int j = 0; j < J; ++j) bb[(b + 1) & 1][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE + 16 * bnx);
+          for (int j = 0; j < J; ++j) bb[(b + 1) & 1][j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE + 16 * (b + 1));
+        } else {
+#pragma unroll
+          for (int j = 0; j < J; ++j) blast[j] = *reinterpret_cast<const f4*>(brow + 16 * j * SE + 16 * (b + 1));
+        }
         __builtin_amdgcn_sched_barrier(0);  // keep block b + 1's reads ahead of block b's MFMAs
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -648,6 +677,17 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
           for (int j = 0; j < J; ++j)
             acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[b][e], bb[b & 1][j][e], acc[j], 0, 0, 0);
       }
+    }
+    if (KB == 1) {
+#pragma unroll
+      for (int j = 0; j < J; ++j) blast[j] = bb[0][j];
+    }
+    // the last block: its k-steps holding columns < d only
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (e > 0 && e >= nlast) break;  // wave-uniform
+#pragma unroll
+      for (int j = 0; j < J; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(alast[e], blast[j][e], acc[j], 0, 0, 0);
     }
     float y2[J], bn_[J];
     int ni[J], row0, nv;
@@ -1161,20 +1201,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   else score_ws_body<0>(p1, blockIdx.x - g0, gridDim.x - g0);
 }
 
-template <int MODE, int NW = 8>
+template <int MODE, int NW = 8, int KBT = 0>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32(ScoreArgs p) {
-  score_f32_body<MODE, NW>(p, blockIdx.x, gridDim.x);
+  score_f32_body<MODE, NW, KBT>(p, blockIdx.x, gridDim.x);
+}
+// the 8-wave kernel of mode M, specialised for 13 k-blocks when d allows
+template <int M>
+static auto score_f32_kernel(int d) {
+  return (d + 15) / 16 == 13 ? k_score_f32<M, 8, 13> : k_score_f32<M, 8, 0>;
 }
 
 // Two independent score jobs in one launch (a predict's entity and relation scores): job 1's
 // workgroups follow job 0's in dispatch order, so they take the CUs that job 0's shorter
 // strips free instead of running as a second serial launch.
-template <int NW>
+template <int NW, int KBT = 0>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) void k_score_f32_jobs(ScoreArgs p0,
                                                                                                      ScoreArgs p1,
                                                                                                      int g0) {
-  if ((int)blockIdx.x < g0) score_f32_body<0, NW>(p0, blockIdx.x, g0);
-  else score_f32_body<0, NW>(p1, blockIdx.x - g0, gridDim.x - g0);
+  if ((int)blockIdx.x < g0) score_f32_body<0, NW, KBT>(p0, blockIdx.x, g0);
+  else score_f32_body<0, NW, KBT>(p1, blockIdx.x - g0, gridDim.x - g0);
 }
 
 // Combine per-tile (max, sumexp) into per-query loss = lse - target logit (one wave per query).
@@ -1312,7 +1357,7 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
     else if (fast) {
       a.bal = score_bal(a.B, nbn);
       const dim3 gb(a.bal ? (unsigned)(((a.B + SQ2 - 1) / SQ2) * a.bal) : g2.x);
-      hipLaunchKernelGGL((k_score_f32<0>), gb, b2, lds2, st, a);
+      hipLaunchKernelGGL(score_f32_kernel<0>(a.d), gb, b2, lds2, st, a);
     }
     else if (a.use_dist) hipLaunchKernelGGL((k_score<0, true>), g, b, 0, st, a);
     else hipLaunchKernelGGL((k_score<0, false>), g, b, 0, st, a);
@@ -1321,7 +1366,7 @@ int score(ScoreArgs& a, int mode, float* loss, hipStream_t st) {
   if (!a.target || !a.part || !a.tgt_logit || !loss) return set_error(REGCN_EINVAL, "CE needs target/workspace/loss");
   if (ws) hipLaunchKernelGGL((k_score_ws<1>), g2, dim3(512), score_ws_lds(a.d), st, a);
   else if (nw4) hipLaunchKernelGGL((k_score_f32<1, 4>), g4, b4, lds4, st, a);
-  else if (fast) hipLaunchKernelGGL((k_score_f32<1>), g2, b2, lds2, st, a);
+  else if (fast) hipLaunchKernelGGL(score_f32_kernel<1>(a.d), g2, b2, lds2, st, a);
   else if (a.use_dist) hipLaunchKernelGGL((k_score<1, true>), g, b, 0, st, a);
   else hipLaunchKernelGGL((k_score<1, false>), g, b, 0, st, a);
   int rc = check_launch("k_score_ce");
@@ -1365,7 +1410,8 @@ int score_jobs(ScoreArgs& a0, ScoreArgs& a1, hipStream_t st) {
       a->bal = score_bal(a->B, nbn);
       h[j++] = a->bal ? (unsigned)(((a->B + SQ2 - 1) / SQ2) * a->bal) : score_f32_grid(a->B, nbn);
     }
-    hipLaunchKernelGGL(k_score_f32_jobs<8>, dim3(h[0] + h[1]), dim3(64 * SW2), score_f32_lds(a0.d), st, a0, a1, (int)h[0]);
+    auto kern = (a0.d + 15) / 16 == 13 ? k_score_f32_jobs<8, 13> : k_score_f32_jobs<8, 0>;
+    hipLaunchKernelGGL(kern, dim3(h[0] + h[1]), dim3(64 * SW2), score_f32_lds(a0.d), st, a0, a1, (int)h[0]);
   }
   return check_launch("k_score_f32_jobs");
 }
@@ -1384,7 +1430,7 @@ int score_ce_bwd(ScoreArgs& a, hipStream_t st) {
   const size_t lds2 = score_f32_lds(a.d);
   // (the uniform-wave kernel: the backward epilogue's registers beside the wave-specialised
   // kernel's two A groups would spill)
-  hipLaunchKernelGGL((k_score_f32<2>), g2, b2, lds2, st, a);
+  hipLaunchKernelGGL(score_f32_kernel<2>(a.d), g2, b2, lds2, st, a);
   return check_launch("k_score_ce_bwd");
 }
 
@@ -1425,7 +1471,7 @@ int rank_fused(ScoreArgs& a, int accumulate, int* counts, hipStream_t st) {
   } else if (nw == 4) {
     hipLaunchKernelGGL((k_score_f32<3, 4>), dim3(score_f32_grid<4>(a.B, nbn)), dim3(256), score_f32_lds<4>(a.d), st, a);
   } else {
-    hipLaunchKernelGGL((k_score_f32<3>), dim3(score_f32_grid(a.B, nbn)), dim3(64 * SW2), score_f32_lds(a.d), st, a);
+    hipLaunchKernelGGL(score_f32_kernel<3>(a.d), dim3(score_f32_grid(a.B, nbn)), dim3(64 * SW2), score_f32_lds(a.d), st, a);
   }
   const int rc = check_launch("k_score_f32<3>");
   if (rc) return rc;
