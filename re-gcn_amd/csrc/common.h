@@ -76,29 +76,69 @@ __device__ __forceinline__ f4 leaky4(f4 v) { return f4{leaky(v.x), leaky(v.y), l
 // v_exp + v_rcp (<= 2 ulp): the IEEE expf and division cost ~30 VALU ops per element.
 __device__ __forceinline__ float sigmoidf(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
+// ---- factor math in a few VALU --------------------------------------------------------------
+// The row maps' per-row scalars (norms, tanh / atanh of them, their ratios) sit in the MFMA
+// kernels' epilogues, and on gfx950 the fp32 MFMA and the VALU share the SIMD's issue (the two
+// do not overlap: tools/probe/overlap_probe.hip), so every VALU instruction there
+// costs time.  The IEEE sqrtf / division / tanhf / atanhf sequences are 18 / 12 / ~60 / ~130 VALU;
+// these are 1 / 2 / ~16 / ~16 on the 1-ulp v_sqrt / v_rcp / v_exp / v_log instructions, within
+// 6 ulp of the exact function (<= 3.5e-7 relative over the whole range, checked against float64
+// in tests/test_fastmath.py's restatement), against the 1e-4 parity tolerance.
+constexpr float FM_LOG2E = 1.4426950408889634f, FM_LN2 = 0.6931471805599453f;
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fdiv(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+// tanh(x), x >= 0: odd Taylor polynomial to x^9 below 0.25 (truncation < 1e-8 relative), else
+// (1 - e) / (1 + e) with e = exp(-2x) <= 0.61 (no cancellation)
+__device__ __forceinline__ float ftanh_pos(float x) {
+  const float x2 = x * x;
+  float p = fmaf(x2, 62.f / 2835.f, -17.f / 315.f);
+  p = fmaf(x2, p, 2.f / 15.f);
+  p = fmaf(x2, p, -1.f / 3.f);
+  p = fmaf(x * x2, p, x);
+  const float e = __builtin_amdgcn_exp2f(x * (-2.f * FM_LOG2E));
+  const float q = (1.f - e) * frcp(1.f + e);
+  return x < 0.25f ? p : q;
+}
+__device__ __forceinline__ float ftanh(float x) { return copysignf(ftanh_pos(fabsf(x)), x); }
+// atanh(s), 0 <= s < 1: odd Taylor polynomial to s^11 below 0.25 (truncation < 5e-9 relative),
+// else ln((1 + s) / (1 - s)) / 2 with the ratio >= 1.67
+__device__ __forceinline__ float fatanh_pos(float s) {
+  const float s2 = s * s;
+  float p = fmaf(s2, 1.f / 11.f, 1.f / 9.f);
+  p = fmaf(s2, p, 1.f / 7.f);
+  p = fmaf(s2, p, 1.f / 5.f);
+  p = fmaf(s2, p, 1.f / 3.f);
+  p = fmaf(s * s2, p, s);
+  const float q = (0.5f * FM_LN2) * __builtin_amdgcn_logf((1.f + s) * frcp(1.f - s));
+  return s < 0.25f ? p : q;
+}
+// |row| from its squared norm, clamped (the stored radius, apply_radius's norm)
+__device__ __forceinline__ float row_radius(float n2) { return fmaxf(fsqrt(n2), REGCN_EPS); }
+
 // ---- scalar factors of the row maps, given the row's squared norm n2 ------------------
 
 // log0: x * atanh(min(sqrt_c |x|, 1-eps)) / (sqrt_c |x|), |x| clamped to eps
 // (hyperbolic_ops.py:97-116).
 __device__ __forceinline__ float log0_factor(float n2, const Curv& k) {
-  float n = fmaxf(sqrtf(n2), REGCN_EPS);
+  float n = row_radius(n2);
   float s = fminf(k.sqrt_c * n, k.atanh_mx);
-  return atanhf(s) / (k.sqrt_c * n);
+  return fdiv(fatanh_pos(s), k.sqrt_c * n);
 }
 
 // project_to_ball factor (hyperbolic_ops.py:37-74): min(|x|c, mx)/|x|c, |x|c = max(|x|, eps).
 __device__ __forceinline__ float project_factor(float n2, const Curv& k) {
-  float n = fmaxf(sqrtf(n2), REGCN_EPS);
-  return fminf(n, k.mx) / n;
+  float n = row_radius(n2);
+  return fdiv(fminf(n, k.mx), n);
 }
 
 // exp0 then project (hyperbolic_ops.py:76-95).  Returns the factor f with
 // exp0(v) = f * v; *out_n2 receives |exp0(v)|^2 (analytic).
 __device__ __forceinline__ float exp0_factor(float n2, const Curv& k, float* out_n2 = nullptr) {
-  float rn = sqrtf(n2);
+  float rn = fsqrt(n2);
   float n = fmaxf(rn, REGCN_EPS);
-  float t = tanhf(k.sqrt_c * n);
-  float f = t / (n * k.sqrt_c);
+  float t = ftanh_pos(k.sqrt_c * n);
+  float f = fdiv(t, n * k.sqrt_c);
   float pn = f * rn;                 // |tanh(..) v / (n sqrt_c)|
   float pf = project_factor(pn * pn, k);
   if (out_n2) {
@@ -115,9 +155,9 @@ __device__ __forceinline__ f4 row_project(f4 v, const Curv& k) { return v * proj
 
 // apply_radius (hyperbolic_ops.py:208-233): direction * clamp(r, eps, rmax).
 __device__ __forceinline__ f4 row_apply_radius(f4 v, float r, const Curv& k) {
-  float n = fmaxf(sqrtf(wave_sum(dot4(v, v))), REGCN_EPS);
+  float n = row_radius(wave_sum(dot4(v, v)));
   float rr = fminf(fmaxf(r, REGCN_EPS), k.rmax);
-  return (v / n) * rr;
+  return v * fdiv(rr, n);
 }
 
 __device__ __forceinline__ f4 load4(const float* p, int col, int d) {

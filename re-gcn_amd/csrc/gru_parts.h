@@ -334,7 +334,7 @@ __device__ __forceinline__ void gru_x_block(const RelGru2Args& p, int bx, int by
   if (eok) {
     const float r = sigmoidf(pre0 + v[0]);
     const float z = sigmoidf(pre1 + v[1]);
-    const float nn = tanhf(pre2 + v[2] + r * pre3);
+    const float nn = ftanh(pre2 + v[2] + r * pre3);
     p.h_out[erow * d + en] = (1.f - z) * nn + z * hprev;
   }
 }

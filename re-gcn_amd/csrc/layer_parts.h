@@ -118,7 +118,7 @@ __device__ __forceinline__ void step_epilogue_out(RowRed& rr, Frag& ct, float n2
     }
     rr.allreduce(dl);
     const float delta = fminf(fmaxf(own_row(dl) + *p.b_r, -p.eps_r), p.eps_r);
-    const float dyn = fmaxf(sqrtf(n2o), REGCN_EPS);
+    const float dyn = row_radius(n2o);
     newr = (p.beta * rs + (1.f - p.beta) * dyn) + delta;
     if constexpr (ANA) {
       if (p.stat_out && (threadIdx.x & 15) < 4 && wave_id() == 0 && ri < n_valid) {
@@ -131,7 +131,7 @@ __device__ __forceinline__ void step_epilogue_out(RowRed& rr, Frag& ct, float n2
   }
   const Curv kr = p.residual ? p.k_rad : p.k;  // by value: a pointer select would pin a local StepArgs in scratch
   float f[4];
-  spread_rows(fminf(fmaxf(newr, REGCN_EPS), kr.rmax) / fmaxf(sqrtf(n2o), REGCN_EPS), f);
+  spread_rows(fdiv(fminf(fmaxf(newr, REGCN_EPS), kr.rmax), row_radius(n2o)), f);
   scale_known(ct, n2, f);
   frag_store(ct, h_out, trow, n_valid, p.d);
   if (r_out) store_radius(n2, r_out, trow, n_valid);

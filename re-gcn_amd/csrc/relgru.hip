@@ -181,7 +181,7 @@ __global__ __launch_bounds__(GTHR) void k_rel_gru(RelGruArgs p) {
   if (i < n_valid && n < d) {
     const float r = sigmoidf(v[0] + p.b_ih[n] + p.b_hh[n]);
     const float z = sigmoidf(v[1] + p.b_ih[d + n] + p.b_hh[d + n]);
-    const float nn = tanhf(v[2] + p.b_ih[2 * d + n] + r * (v[3] + p.b_hh[2 * d + n]));
+    const float nn = ftanh(v[2] + p.b_ih[2 * d + n] + r * (v[3] + p.b_hh[2 * d + n]));
     const float h = A[i * lda + 2 * d + n];
     p.h_out[(int64_t)(r0 + i) * d + n] = (1.f - z) * nn + z * h;
   }

@@ -493,7 +493,7 @@ __device__ __forceinline__ void lz_exp0(RtLazy& z, const Curv& k) {  // exp0 + p
   z.m2 = o;
 }
 __device__ __forceinline__ void lz_normalize(RtLazy& z) {  // F.normalize, eps 1e-12
-  lz_scale(z, 1.0f / fmaxf(sqrtf(z.m2), 1e-12f));
+  lz_scale(z, frcp(fmaxf(fsqrt(z.m2), 1e-12f)));
 }
 template <int NT>
 __device__ __forceinline__ void rt_apply(RAcc<NT>& a, RtLazy& z) {
@@ -553,7 +553,7 @@ __device__ __forceinline__ void rt_store_radius(const float n2[4], float* __rest
   if ((lane & 15) == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (4 * (lane >> 4) + r < n_valid) rad[crow[r]] = fmaxf(sqrtf(n2[r]), REGCN_EPS);
+      if (4 * (lane >> 4) + r < n_valid) rad[crow[r]] = row_radius(n2[r]);
   }
 }
 
@@ -576,7 +576,7 @@ __device__ __forceinline__ void rt_send_radius(const LayerArgs& p, const float n
       if (4 * (lane >> 4) + r >= n_valid) continue;
       int s0, s1;
       rt_send_span(p, crow[r], s0, s1);
-      const float v = fmaxf(sqrtf(n2[r]), REGCN_EPS);  // = rt_store_radius's value
+      const float v = row_radius(n2[r]);  // = rt_store_radius's value
       for (int sl = s0; sl < s1; ++sl) p.send_r[p.send_pos[sl]] = v;
     }
   }
@@ -645,16 +645,19 @@ __device__ __forceinline__ RtRows rt_rows(const LayerArgs& p, int base) {
 constexpr int RT_SC_COLS = 80, RT_SC_TILES = RT_SC_COLS / 16, RT_SC_BYTES = 16 * RT_SC_COLS * 4;
 static_assert(4 * 2 * RT_SC_BYTES <= rt_lds_bytes(1), "blend staging must fit the tail's LDS");
 
-__device__ __forceinline__ void rt_stage_blend(const StepArgs& s, const RtRows& R, int d, int stage, char* lds) {
+__device__ __forceinline__ void rt_stage_blend(const StepArgs& s, const RtRows& R, int d, int dpad, int stage,
+                                               char* lds) {
   const int lane = threadIdx.x & 63, w = wave_id();
-  const int c0 = RT_SC_COLS * stage, ncols = min(RT_SC_COLS, d - c0), f4pr = ncols >> 2;
+  // the stage spans the padded width (16 NT columns): columns >= d are staged as zeros, so the
+  // blend reads every column of its tiles unmasked
+  const int c0 = RT_SC_COLS * stage, ncols = min(RT_SC_COLS, dpad - c0), f4pr = ncols >> 2;
   const float* zrow = reinterpret_cast<const float*>(kZeroRow);
   char* base = lds + w * 2 * RT_SC_BYTES;
 #pragma unroll
   for (int i = 0; i < RT_SC_BYTES / 1024; ++i) {
     const int slot = 64 * i + lane, sr = slot / max(f4pr, 1), sc = slot - sr * f4pr;
     const int rid = __shfl(R.arow_id, min(sr, 15));
-    const bool ok = (slot < 16 * f4pr) & (sr < R.n_valid);
+    const bool ok = (slot < 16 * f4pr) & (sr < R.n_valid) & (c0 + 4 * sc < d);
     const int64_t off = (int64_t)rid * d + c0 + 4 * sc;
     __builtin_amdgcn_global_load_lds((const void*)(ok ? s.x_prev + off : zrow),
                                      (__attribute__((address_space(3))) void*)(base + i * 1024), 16, 0, 0);
@@ -714,7 +717,7 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
   const int* crow = R.crow;
   const int n_valid = R.n_valid;
   // the first blend stage's copies fly under the epilogue's row maps
-  if constexpr (MODE == RT_STEP_PRE) rt_stage_blend(p.step, R, d, 0, lds);
+  if constexpr (MODE == RT_STEP_PRE) rt_stage_blend(p.step, R, d, 16 * NT, 0, lds);
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     if (!p.euclid) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
@@ -762,29 +765,32 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     if constexpr (MODE == RT_STEP_PRE) {
       const float* xs = reinterpret_cast<const float*>(lds + wave_id() * 2 * RT_SC_BYTES);
       const float* zs = xs + RT_SC_BYTES / 4;
+      // sigmoid(z + b) = 1 / (1 + 2^(z (-log2 e) + b (-log2 e)))
+      float nbg[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) nbg[t] = bg[t] * -FM_LOG2E;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int stage = t / RT_SC_TILES;
         if (t % RT_SC_TILES == 0) {
           if (stage > 0) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the last stage
-            rt_stage_blend(s, R, d, stage, lds);
+            rt_stage_blend(s, R, d, 16 * NT, stage, lds);
           }
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stage's copies have landed
         }
-        const int col = 16 * t + (lane & 15);
-        const int ncols = min(RT_SC_COLS, d - RT_SC_COLS * stage), cl = max(0, min(col - RT_SC_COLS * stage, ncols - 1));
+        // rows past n_valid and columns >= d were staged as zeros (pad columns: v, x_prev and the
+        // gate row all 0 there, so the blend keeps them 0; such rows are never stored)
+        const int ncols = min(RT_SC_COLS, 16 * NT - RT_SC_COLS * stage);
+        const int cl = 16 * t + (lane & 15) - RT_SC_COLS * stage;
         const f4 c4 = clamp4(v.t[t], -10.f, 10.f);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          // rows past n_valid were staged as zeros (and are never stored); only the pad columns
-          // of a tile reaching past d (cl clamped onto a real column) need the select
-          const bool ok = 16 * t + 15 < d || col < d;
           const float xp = xs[(4 * q + r) * ncols + cl];
           const float zt = zs[(4 * q + r) * ncols + cl];
-          const float pr = fminf(fmaxf(ok ? xp : 0.f, -10.f), 10.f);
-          const float gg = sigmoidf((ok ? zt : 0.f) + bg[t]);
-          v.t[t][r] = gg * c4[r] + (1.f - gg) * pr;
+          const float pr = fminf(fmaxf(xp, -10.f), 10.f);
+          const float gg = frcp(1.f + __builtin_amdgcn_exp2f(fmaf(zt, -FM_LOG2E, nbg[t])));
+          v.t[t][r] = fmaf(gg, c4[r] - pr, pr);  // gg c4 + (1 - gg) pr
         }
       }
     } else {
@@ -813,21 +819,21 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     if (s.residual) {
       float wr[NT], lf[4], dl[4];
       rt_col<NT>(wr, s.w_r, d);
-      // log0 of the row v pf (its factor still pending): one factor per row
+      // w_r . log0(v pf) = (pf log0 factor) (w_r . v): the row's factor applied to the dot
       spread_rows(z.pf * log0_factor(n2o, s.k_rad), lf);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float acc = 0.f;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) acc += wr[t] * (v.t[t][r] * lf[r]);
-        dl[r] = row16_sum(acc);
+        for (int t = 0; t < NT; ++t) acc = fmaf(wr[t], v.t[t][r], acc);
+        dl[r] = row16_sum(acc) * lf[r];
       }
       const float delta = fminf(fmaxf(own_row(dl) + *s.b_r, -s.eps_r), s.eps_r);
-      const float dyn = fmaxf(sqrtf(n2o), REGCN_EPS);
+      const float dyn = row_radius(n2o);
       newr = (s.beta * rs + (1.f - s.beta) * dyn) + delta;
     }
     const Curv kr = s.residual ? s.k_rad : s.k;
-    lz_scale(z, fminf(fmaxf(newr, REGCN_EPS), kr.rmax) / fmaxf(sqrtf(n2o), REGCN_EPS));
+    lz_scale(z, fdiv(fminf(fmaxf(newr, REGCN_EPS), kr.rmax), row_radius(n2o)));
     if (s.h_out) {
       rt_apply<NT>(v, z);
       rt_store_staged<NT>(v, s.h_out, R, d, lds, p, false);

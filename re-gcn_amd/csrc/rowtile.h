@@ -351,7 +351,7 @@ __device__ __forceinline__ void exp0_known(Frag& a, float n2[4], const Curv& k) 
 
 __device__ __forceinline__ void normalize_known(Frag& a, float n2[4]) {  // F.normalize, eps 1e-12
   float f[4];
-  spread_rows(1.0f / fmaxf(sqrtf(own_row(n2)), 1e-12f), f);
+  spread_rows(frcp(fmaxf(fsqrt(own_row(n2)), 1e-12f)), f);
   scale_known(a, n2, f);
 }
 
@@ -422,7 +422,7 @@ __device__ __forceinline__ void store_radius(const float n2[4], float* __restric
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = frag_row(r);
-      if (i < n_valid) rad[rows[i]] = fmaxf(sqrtf(n2[r]), REGCN_EPS);
+      if (i < n_valid) rad[rows[i]] = row_radius(n2[r]);
     }
   }
 }

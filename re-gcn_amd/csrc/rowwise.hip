@@ -87,7 +87,7 @@ __global__ __launch_bounds__(256) void k_rowmap(const float* __restrict__ a, con
       x.scale(log0_factor(n2, k));
       x.store(out + r * d, d, lane);
     } else if (OP == OP_PROLOGUE) {
-      float rad = fmaxf(sqrtf(n2), REGCN_EPS);
+      float rad = row_radius(n2);
       x.scale(log0_factor(n2, k));
       x.store(out + r * d, d, lane);
       if (lane == 0) out2[r] = rad;
@@ -98,35 +98,35 @@ __global__ __launch_bounds__(256) void k_rowmap(const float* __restrict__ a, con
       x.scale(project_factor(n2, k));
       x.store(out + r * d, d, lane);
     } else if (OP == OP_APPLY_RADIUS) {
-      float n = fmaxf(sqrtf(n2), REGCN_EPS);
+      float n = row_radius(n2);
       float rr = fminf(fmaxf(vec[r], REGCN_EPS), k.rmax);
 #pragma unroll
-      for (int j = 0; j < EPL; ++j) x.v[j] = (x.v[j] / n) * rr;
+      for (int j = 0; j < EPL; ++j) x.v[j] = x.v[j] * fdiv(rr, n);
       x.store(out + r * d, d, lane);
     } else if (OP == OP_RADIUS) {
-      if (lane == 0) out[r] = fmaxf(sqrtf(n2), REGCN_EPS);
+      if (lane == 0) out[r] = row_radius(n2);
     } else if (OP == OP_SUMSQ) {
       if (lane == 0) out[r] = n2;
     } else if (OP == OP_LN_ROUNDTRIP) {
       x.scale(log0_factor(n2, k));
-      x.scale(1.0f / fmaxf(sqrtf(x.sumsq()), 1e-12f));
+      x.scale(frcp(fmaxf(fsqrt(x.sumsq()), 1e-12f)));
       x.scale(exp0_factor(x.sumsq(), k));
       x.store(out + r * d, d, lane);
     } else if (OP == OP_INIT || OP == OP_INIT_LN) {
       if (OP == OP_INIT_LN) {
-        x.scale(1.0f / fmaxf(sqrtf(n2), 1e-12f));
+        x.scale(frcp(fmaxf(fsqrt(n2), 1e-12f)));
         n2 = x.sumsq();
       }
       x.scale(exp0_factor(n2, k));
       {
-        const float n = fmaxf(sqrtf(x.sumsq()), REGCN_EPS);
+        const float n = row_radius(x.sumsq());
         const float rr = fminf(fmaxf(vec[r], REGCN_EPS), k.rmax);
 #pragma unroll
-        for (int j = 0; j < EPL; ++j) x.v[j] = (x.v[j] / n) * rr;
+        for (int j = 0; j < EPL; ++j) x.v[j] = x.v[j] * fdiv(rr, n);
       }
       if (out) x.store(out + t * d, d, lane);
       const float h2 = x.sumsq();
-      if (lane == 0 && out3) out3[t] = fmaxf(sqrtf(h2), REGCN_EPS);
+      if (lane == 0 && out3) out3[t] = row_radius(h2);
       if (out2) {
         x.scale(log0_factor(h2, k));
         x.store(out2 + t * d, d, lane);
@@ -185,19 +185,19 @@ __global__ __launch_bounds__(256) void k_init_rows(const float* __restrict__ a, 
     const int64_t t = dst ? (int64_t)dst[i] : i;
     float n2 = x.sumsq();
     if (OP == OP_INIT_LN) {
-      x.scale(1.0f / fmaxf(sqrtf(n2), 1e-12f));
+      x.scale(frcp(fmaxf(fsqrt(n2), 1e-12f)));
       n2 = x.sumsq();
     }
     x.scale(exp0_factor(n2, k));
     {
-      const float n = fmaxf(sqrtf(x.sumsq()), REGCN_EPS);
+      const float n = row_radius(x.sumsq());
       const float rr = fminf(fmaxf(rv, REGCN_EPS), k.rmax);
 #pragma unroll
-      for (int j = 0; j < EPL; ++j) x.v[j] = (x.v[j] / n) * rr;
+      for (int j = 0; j < EPL; ++j) x.v[j] = x.v[j] * fdiv(rr, n);
     }
     if (out) x.store(out + t * d, d, lane);
     const float h2 = x.sumsq();
-    if (lane == 0 && out3) out3[t] = fmaxf(sqrtf(h2), REGCN_EPS);
+    if (lane == 0 && out3) out3[t] = row_radius(h2);
     if (out2) {
       x.scale(log0_factor(h2, k));
       x.store(out2 + t * d, d, lane);
@@ -242,21 +242,18 @@ __global__ __launch_bounds__(256) void k_init_rows4(const float* __restrict__ a,
     const int64_t t = dst ? (int64_t)dst[i] : i;
     float n2 = wave_sum(sq4(x));
     if (OP == OP_INIT_LN) {
-      scale4(x, 1.0f / fmaxf(sqrtf(n2), 1e-12f));
+      scale4(x, frcp(fmaxf(fsqrt(n2), 1e-12f)));
       n2 = wave_sum(sq4(x));
     }
     scale4(x, exp0_factor(n2, k));
     {
-      const float n = fmaxf(sqrtf(wave_sum(sq4(x))), REGCN_EPS);
+      const float n = row_radius(wave_sum(sq4(x)));
       const float rr = fminf(fmaxf(rv, REGCN_EPS), k.rmax);
-      x.x = (x.x / n) * rr;
-      x.y = (x.y / n) * rr;
-      x.z = (x.z / n) * rr;
-      x.w = (x.w / n) * rr;
+      x = x * fdiv(rr, n);
     }
     if (out && on) reinterpret_cast<float4*>(out + t * d)[lane] = x;
     const float h2 = wave_sum(sq4(x));
-    if (lane == 0 && out3) out3[t] = fmaxf(sqrtf(h2), REGCN_EPS);
+    if (lane == 0 && out3) out3[t] = row_radius(h2);
     if (out2) {
       scale4(x, log0_factor(h2, k));
       if (on) reinterpret_cast<float4*>(out2 + t * d)[lane] = x;

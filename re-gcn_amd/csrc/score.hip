@@ -503,6 +503,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   };
   stamp(0);
   const int d = p.d, KB = KBT ? KBT : (d + 15) >> 4, SE = score_lds_stride(d);
+  if constexpr (KBT > 0) __builtin_assume(d > 16 * (KBT - 1) && d <= 16 * KBT);
   const int nbn = p.n_rng ? p.rng_total : (p.N + SNW - 1) / SNW, nbq = (p.B + SQW - 1) / SQW;
   // candidate tile t -> its first row and valid rows (row ranges: a tile never spans two)
   auto tile_rows = [&](int t, int& row0, int& nvalid) {
@@ -612,16 +613,15 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   };
   // |e|^2 of each staged row, summed over its 8 staging lanes (xor 1, 2, 4), next to the tile
   float* e2s = Es + 2 * SNW * SE;  // [2][SNW]
-  auto stash = [&](int buf, int t) {
-    int row0, nv;
-    tile_rows(t, row0, nv);
-    const bool row_ok = sr < nv;
+  auto stash = [&](int buf) {
+    // rows past the tile's valid rows hold a copy of its last row (fetch clamps): finite, and
+    // their scores are never written or counted, so only the columns >= d need zeros
     float* lrow = Es + buf * SNW * SE + sr * SE;
     float ss = 0.f;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       const int u = sub + 8 * it;
-      const f4 w = (row_ok & (4 * u < d)) ? v[it] : z4;
+      const f4 w = (4 * u < d) ? v[it] : z4;
       ss += dot4(w, w);
       if (u < per_row) {
         if (u >= per_row - 4) {  // the transposed last block: column 16 b + 4 e + i at 4 i + e
@@ -641,7 +641,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     if (sub == 0) e2s[buf * SNW + sr] = ss;
   };
   fetch(bn);
-  stash(0, bn);
+  stash(0);
   __syncthreads();
   stamp(1);
   int cur = 0;
@@ -702,7 +702,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
                                  MODE == 0 && nv == SNW && q0 + SQW <= p.B);
     if (!more) break;
     if (MODE == 2) fetch(bn_next);
-    stash(cur ^ 1, bn_next);  // that buffer's readers passed the last barrier
+    stash(cur ^ 1);  // that buffer's readers passed the last barrier
     __syncthreads();
     cur ^= 1;
     bn = bn_next;

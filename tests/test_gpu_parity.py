@@ -891,3 +891,34 @@ def test_crel_gather_matches_per_item(skew, euclid, monkeypatch):
     assert torch.equal(a1, a2) and torch.equal(h1, h2)
     assert not torch.equal(a1[rows], ref)  # the product path ran (another fp32 association)
     assert float((h1 - h_ref).abs().max()) <= 1e-4
+
+
+@pytest.mark.parametrize("c", [0.01, 0.05, 1.0])
+def test_row_maps_fast_factor_math(c):
+    """The row maps' factor math (common.h: v_sqrt / v_rcp / v_exp / v_log based tanh, atanh,
+    norms and ratios) against float64 over row norms 1e-5 .. 30: within 2e-6 relative of the
+    exact maps (the IEEE-library versions they replaced were within ~3e-7; parity needs 1e-4)."""
+    from regcn_amd.hyperbolic_ops import HyperbolicOps as H
+    g = torch.Generator().manual_seed(7)
+    d = 200
+    dirs = torch.nn.functional.normalize(torch.randn(4096, d, generator=g, dtype=torch.float64))
+    norms = torch.logspace(-5, 1.5, 4096, dtype=torch.float64)[:, None]
+    x = dirs * norms
+    sc = c ** 0.5
+    n = x.norm(dim=1, keepdim=True).clamp_min(1e-6)
+    mx = 1 / sc - 2e-6  # project_to_ball's bound (hyperbolic_ops.py:37-74, eps twice)
+
+    def project(y):
+        ny = y.norm(dim=1, keepdim=True).clamp_min(1e-6)
+        return y * torch.clamp(ny, max=mx) / ny
+
+    exp_ref = project(torch.tanh(sc * n) * x / (sc * n))
+    got = H.exp_map_zero(x.float().to(DEV), c).double().cpu()
+    rel = ((got - exp_ref).norm(dim=1) / exp_ref.norm(dim=1)).max().item()
+    assert rel <= 2e-6, "exp0 relative error %.3g" % rel
+    xb = project(x * (0.9 / sc) / n.clamp_min(0.9 / sc))  # inside the ball
+    nb = xb.norm(dim=1, keepdim=True).clamp_min(1e-6)
+    log_ref = torch.atanh(torch.clamp(sc * nb, max=1 - 1e-6)) * xb / (sc * nb)
+    got = H.log_map_zero(xb.float().to(DEV), c).double().cpu()
+    rel = ((got - log_ref).norm(dim=1) / log_ref.norm(dim=1)).max().item()
+    assert rel <= 2e-6, "log0 relative error %.3g" % rel
