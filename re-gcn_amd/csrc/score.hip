@@ -448,6 +448,10 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
 // candidate tiles x + 8 (k + S i), S = stripes per XCD.  The nbq workgroups of one stripe walk
 // the same tiles in step, so a tile comes from HBM into its XCD's L2 once.
 constexpr int SQ2 = 128, SW2 = SQ2 / 16, KB_MAX = 16;  // d <= 256
+#ifndef REGCN_SCORE_STAMPS
+#define REGCN_SCORE_STAMPS 0
+#endif
+constexpr bool kScoreStamps = REGCN_SCORE_STAMPS != 0;  // diagnostic build: per-phase cycle sums
 //
 // Workgroup shape NW (waves): 8 = 128 queries x 64-candidate tiles, one workgroup per CU (its
 // 111 KB of LDS); 4 = 64 queries x 32-candidate tiles at 56 KB, two workgroups per CU.  With 8
@@ -644,6 +648,16 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   stash(0);
   __syncthreads();
   stamp(1);
+  // diagnostic build only (-DREGCN_SCORE_STAMPS=1, tools/scorebench.py --stamps): wave 0's
+  // s_memtime cycles per tile phase, summed -- products, epilogue, staging, barrier
+  int64_t ph[4] = {0, 0, 0, 0}, t_ph = kScoreStamps ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
+  auto phase = [&](int k) {
+    if constexpr (kScoreStamps) {
+      const int64_t t = (int64_t)__builtin_amdgcn_s_memtime();
+      ph[k] += t - t_ph;
+      t_ph = t;
+    }
+  };
   int cur = 0;
   for (int i = 0;; ++i) {
     const int bn_next = tile_of(i + 1);
@@ -689,6 +703,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
 #pragma unroll
       for (int j = 0; j < J; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(alast[e], blast[j][e], acc[j], 0, 0, 0);
     }
+    phase(0);
     float y2[J], bn_[J];
     int ni[J], row0, nv;
     tile_rows(bn, row0, nv);
@@ -700,16 +715,25 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     }
     score_epilogue_fast<MODE, J>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se,
                                  MODE == 0 && nv == SNW && q0 + SQW <= p.B);
+    phase(1);
     if (!more) break;
     if (MODE == 2) fetch(bn_next);
     stash(cur ^ 1);  // that buffer's readers passed the last barrier
+    phase(2);
     __syncthreads();
+    phase(3);
     cur ^= 1;
     bn = bn_next;
   }
   if (MODE == 1) ce_flush();
   if (MODE == 3) count_flush();
   stamp(2);
+  if constexpr (kScoreStamps) {
+    if (p.trace && tid == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p.trace[(int64_t)blk * 16 + 4 + k] = ph[k];
+    }
+  }
 }
 
 // ---- 32 x 32 x 2 fp32 scorer (MODE 0 scores, MODE 3 fused rank count) ----------------------

@@ -78,6 +78,41 @@ def measure(B=1024, N=1_000_000, d=200, reps=5, modes="score,ce,ce_bwd", verbose
     return out
 
 
+def stamps(B=1024, N=1_000_000, d=200):
+    """Per-phase cycle sums of the proxy scorer's workgroups (a library built with
+    -DREGCN_SCORE_STAMPS=1, passed as REGCN_HIP_LIB): wave 0's s_memtime cycles in the products,
+    the epilogue, the next tile's staging and the barrier, summed over its tiles; printed as the
+    mean over workgroups and as fractions of their sum."""
+    from regcn_amd import _lib
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    q = torch.randn(B, d, device=dev, generator=g) * 0.05
+    e = torch.randn(N, d, device=dev, generator=g) * 0.05
+    bias = torch.randn(N, device=dev, generator=g) * 0.1
+    scale = torch.tensor([1.3], device=dev)
+    margin = torch.tensor([0.7], device=dev)
+    S = torch.empty(B, N, device=dev)
+    f = _lib.fptr
+    buf = torch.zeros(65536 * 16, dtype=torch.int64, device=dev)
+    run = lambda: _lib.call("regcn_hyp_score_f32", f(q), f(e), f(bias), None, f(scale), f(margin), B, N, d, 0.01, 0,
+                            f(S), _lib.stream())
+    run()
+    torch.cuda.synchronize()
+    _lib.call("regcn_set_trace", _lib.addr(buf, torch.int64))
+    run()
+    torch.cuda.synchronize()
+    _lib.call("regcn_set_trace", None)
+    t = buf.view(-1, 16).cpu()
+    used = t[:, 0] != 0
+    ph = t[used][:, 4:8].double()
+    names = ["products", "epilogue", "staging", "barrier"]
+    mean = ph.mean(0)
+    res = {"workgroups": int(used.sum()), "cycles_mean": {n: round(float(v)) for n, v in zip(names, mean)},
+           "frac": {n: round(float(v / mean.sum()), 4) for n, v in zip(names, mean)},
+           "span_us_mean": round(float((t[used][:, 2] - t[used][:, 0]).double().mean()) / 100.0, 1)}
+    print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=1024)
@@ -85,7 +120,11 @@ def main():
     ap.add_argument("--d", type=int, default=200)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--modes", default="score,ce,ce_bwd")
+    ap.add_argument("--stamps", action="store_true", help="phase cycle sums (REGCN_SCORE_STAMPS build)")
     a = ap.parse_args()
+    if a.stamps:
+        stamps(a.B, a.N, a.d)
+        return
     print(json.dumps(measure(a.B, a.N, a.d, a.reps, a.modes)), flush=True)
 
 
