@@ -276,7 +276,8 @@ typedef struct regcn_layer_desc {
                             source order (regcn_snapshot_item_src_order_i32), so a row's k items
                             from one source gather that source row once, k * w_e * x[src]
                             (the relation rows still per item) */
-  /* regcn_layer_rowtail_f32 only (NULL elsewhere): */
+  /* regcn_layer_rowtail_f32 only (NULL elsewhere); its products address the x / agg /
+   * step_x_prev rows with 32-bit byte offsets: row id * d * 4 < 4 GB - 64 KB */
   const float* gate_w;   /* a cell's first layer: also the timestep's time-gate pre-activation */
   float* gate_out;       /*   clamp(x) @ gate_w (kp-packed W_g) of every row -> gate_out (V x d) */
   const float* step_tw;  /* the step layer: those rows (else the gate product runs in-kernel) */

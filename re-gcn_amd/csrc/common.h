@@ -60,15 +60,19 @@ __device__ __forceinline__ float dot4(f4 a, f4 b) {
   return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }
 
+// clamp(x, lo, hi) as one v_med3_f32 (fminf(fmaxf()) adds a NaN-quieting v_max per element;
+// the same value for every non-NaN x)
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 __device__ __forceinline__ f4 clamp4(f4 v, float lo, float hi) {
-  return f4{fminf(fmaxf(v.x, lo), hi), fminf(fmaxf(v.y, lo), hi), fminf(fmaxf(v.z, lo), hi),
-            fminf(fmaxf(v.w, lo), hi)};
+  return f4{clampf(v.x, lo, hi), clampf(v.y, lo, hi), clampf(v.z, lo, hi), clampf(v.w, lo, hi)};
 }
 
-// F.rrelu(x) with training=False: slope (1/8 + 1/3) / 2 = 11/48.
+// F.rrelu(x) with training=False: slope (1/8 + 1/3) / 2 = 11/48.  For 0 < slope < 1 it is
+// max(x, slope x) = med3(x, slope x, +inf): two VALU, no compare / select, the same bits as
+// x >= 0 ? x : slope x.
 __device__ __forceinline__ float leaky(float x) {
   const float slope = (1.0f / 8.0f + 1.0f / 3.0f) * 0.5f;
-  return x >= 0.f ? x : x * slope;
+  return __builtin_amdgcn_fmed3f(x, x * slope, __builtin_inff());
 }
 
 __device__ __forceinline__ f4 leaky4(f4 v) { return f4{leaky(v.x), leaky(v.y), leaky(v.z), leaky(v.w)}; }

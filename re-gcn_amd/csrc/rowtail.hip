@@ -331,13 +331,9 @@ struct RAcc {
   }
 };
 
-// acc += A[16 rows x K] @ W for the wave's rows: A row of lane l = arow (row l % 16 of the
-// wave), columns >= d and rows with !aok read as 0 (clamped loads, then a select), CLAMP:
-// A clamped to +-10 (the time gate's operand); Wp packed by k_pack_weight_kp.  B fragments of
-// the next P k-steps are in flight while a k-step's NT MFMAs issue.
-// Masked A lanes (rows !aok, columns >= d) load from this zero row instead of their row: the
-// loaded value then needs no select, which would make the compiler wait for the load right
-// where it is issued (an s_waitcnt vmcnt(0) per k-block, no prefetch).
+// Masked lanes of the blend staging (rows past the group, columns >= d) DMA from this zero
+// row instead of their row: no select on the loaded value, which would make the compiler wait
+// for the load right where it is issued.
 __device__ const f4 kZeroRow[1] = {{0.f, 0.f, 0.f, 0.f}};
 
 constexpr int RT_KB_BYTES = 4 * 4 * 64 * 16;  // one 16-deep k-block of a packed weight: 16 KB
@@ -382,7 +378,7 @@ __device__ __forceinline__ void rt_block(RAcc<NT> (&acc)[RG], const char* aslot,
     __builtin_amdgcn_sched_barrier(0);
     float as[RG];
 #pragma unroll
-    for (int g = 0; g < RG; ++g) as[g] = CLAMP ? fminf(fmaxf(a[g][s], -10.f), 10.f) : a[g][s];
+    for (int g = 0; g < RG; ++g) as[g] = CLAMP ? clampf(a[g][s], -10.f, 10.f) : a[g][s];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -392,43 +388,48 @@ __device__ __forceinline__ void rt_block(RAcc<NT> (&acc)[RG], const char* aslot,
 }
 
 // acc[g] += A_g[16 rows x K] @ W for the wave's RG row groups: A row of lane l in group g =
-// arow[g] (row l % 16 of the group), columns >= d and rows with !aok[g] read as 0, CLAMP: A
-// clamped to +-10 (the time gate's operand); Wp packed by k_pack_weight_kp.  Both operands
-// stream through LDS by DMA (global_load_lds), nothing through registers: k-block kb + 1 of
-// the weight (16 KB, a quarter per wave, double-buffered) and k-block kb + 2 of the wave's own
-// A fragments (1 KB per group, each lane DMAs the 16 bytes it later reads: a 3-deep ring) are
-// in flight while k-block kb's MFMAs run; every B fragment read feeds RG MFMAs.  Masked A
-// lanes DMA from a zero row.  One raw barrier per k-block after a counted vmcnt (the A block
-// two ahead may stay in flight across it; __syncthreads would drain it).  Every wave of the
-// workgroup must call this with the same Wp and KB.  The last k-block runs only its k-steps
-// that hold columns < d (rt_block).
+// row arow[g] of the row-major matrix A (row l % 16 of the group), rows with !aok[g] read as 0,
+// CLAMP: A clamped to +-10 (the time gate's operand); Wp packed by k_pack_weight_kp.  Both
+// operands stream through LDS by DMA (buffer_load ... lds), nothing through registers: k-block
+// kb + 1 of the weight (16 KB, a quarter per wave, double-buffered) and k-block kb + 2 of the
+// wave's own A fragments (1 KB per group, each lane DMAs the 16 bytes it later reads: a 3-deep
+// ring) are in flight while k-block kb's MFMAs run; every B fragment read feeds RG MFMAs.  The
+// per-lane byte offsets are fixed for the whole product and the k-block advances the scalar
+// offset only (no per-k-block address VALU); a masked row gets an offset past the resource's
+// records, which the hardware reads as zeros.  Columns >= d of the last block read the next
+// row's floats, which no k-step uses (the transposed last block: rt_block).  One raw barrier per
+// k-block after a counted vmcnt (the A block two ahead may stay in flight across it;
+// __syncthreads would drain it).  Every wave of the workgroup must call this with the same Wp
+// and KB.  The last k-block runs only its k-steps that hold columns < d (rt_block).
+constexpr uint32_t RT_OOB = 0xFFFF0000u;  // A offset of a masked row (+ any k-block: still past)
+// one 16-B piece per lane, buffer -> LDS at `dst` (wave-uniform) + 16 lane
+__device__ __forceinline__ void rt_dma16(__amdgpu_buffer_rsrc_t r, char* dst, uint32_t voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, voff, soff, 0, 0);
+}
 template <int NT, int RG, bool CLAMP>
-__device__ __forceinline__ void rt_mm(RAcc<NT> (&acc)[RG], const float* const (&arow)[RG], const bool (&aok)[RG],
+__device__ __forceinline__ void rt_mm(RAcc<NT> (&acc)[RG], const float* A, const int (&arow)[RG], const bool (&aok)[RG],
                                       const float* __restrict__ Wp, int d, int KB, char* lds) {
   const int lane = threadIdx.x & 63, q = lane >> 4, w = wave_id();
   constexpr int A_SLOT = 4 * RG * 1024;
   char* wbuf = lds;
   char* abuf = lds + 2 * RT_KB_BYTES + w * RG * 1024;
-  const char* wsrc = reinterpret_cast<const char*>(Wp);
-  const float* zrow = reinterpret_cast<const float*>(kZeroRow);
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Wp), (short)0, KB * RT_KB_BYTES, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(A), (short)0, (int)RT_OOB,
+                                                                      0x00020000);
+  const uint32_t wo = (uint32_t)(w * (RT_KB_BYTES / 4) + lane * 16);
+  uint32_t ao[RG];
+#pragma unroll
+  for (int g = 0; g < RG; ++g) ao[g] = aok[g] ? ((uint32_t)arow[g] * (uint32_t)d + 4u * q) * 4u : RT_OOB;
   const int nlast = (d - 16 * (KB - 1) + 3) >> 2;  // k-steps of the last block with columns < d
   auto dma_w = [&](int kb) {  // this wave's quarter of k-block kb into buffer kb & 1
     char* dst = wbuf + (kb & 1) * RT_KB_BYTES + w * (RT_KB_BYTES / 4);
-    const char* src = wsrc + (int64_t)kb * RT_KB_BYTES + w * (RT_KB_BYTES / 4) + lane * 16;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(src + i * 1024),
-                                       (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 0);
+    for (int i = 0; i < 4; ++i) rt_dma16(wr, dst + i * 1024, wo + i * 1024, kb * RT_KB_BYTES);
   };
   auto dma_a = [&](int kb) {  // lane l: A_g[row l % 16][16 kb + 4 (l / 16) ...] into ring slot kb % 3
-    const int col = 16 * kb + 4 * q;
 #pragma unroll
-    for (int g = 0; g < RG; ++g) {
-      const float* src = (aok[g] & (col < d)) ? arow[g] + col : zrow;
-      __builtin_amdgcn_global_load_lds(
-          (const void*)src, (__attribute__((address_space(3))) void*)(abuf + (kb % RT_A_RING) * A_SLOT + g * 1024), 16,
-          0, 0);
-    }
+    for (int g = 0; g < RG; ++g) rt_dma16(ar, abuf + (kb % RT_A_RING) * A_SLOT + g * 1024, ao[g], kb * 64);
   };
   dma_a(0);
   dma_w(0);
@@ -525,10 +526,21 @@ template <int NT>
 __device__ __forceinline__ void rt_store(const RAcc<NT>& a, float* __restrict__ M, const int crow[4], int n_valid,
                                          int d) {
   const int lane = threadIdx.x & 63;
+  if (n_valid == 16 && d > 16 * (NT - 1)) {
+    // (wave-uniform) all 16 rows valid and every tile but the last inside d: no masks, one row
+    // address per row and the column tiles as immediate offsets (16 t floats)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float* row = M + (int64_t)crow[r] * d + (lane & 15);
+#pragma unroll
+      for (int t = 0; t < NT - 1; ++t) row[16 * t] = a.t[t][r];
+      if (16 * (NT - 1) + (lane & 15) < d) row[16 * (NT - 1)] = a.t[NT - 1][r];
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     if (4 * (lane >> 4) + r >= n_valid) continue;
-    // one row address per row; the column tiles are immediate offsets (16 t floats)
     float* row = M + (int64_t)crow[r] * d + (lane & 15);
 #pragma unroll
     for (int t = 0; t < NT; ++t)  // a tile wholly inside d stores unmasked (a wave-uniform test)
@@ -788,7 +800,7 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
         for (int r = 0; r < 4; ++r) {
           const float xp = xs[(4 * q + r) * ncols + cl];
           const float zt = zs[(4 * q + r) * ncols + cl];
-          const float pr = fminf(fmaxf(xp, -10.f), 10.f);
+          const float pr = clampf(xp, -10.f, 10.f);
           const float gg = frcp(1.f + __builtin_amdgcn_exp2f(fmaf(zt, -FM_LOG2E, nbg[t])));
           v.t[t][r] = fmaf(gg, c4[r] - pr, pr);  // gg c4 + (1 - gg) pr
         }
@@ -870,16 +882,16 @@ __device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
   // the passes are the workgroup's (every wave takes part in each weight's LDS stream)
   const int n_wg = min(RT_ROWS * RG, p.V - wg0);
   const int npos_wg = min(max(p.n_pos - wg0, 0), n_wg);
-  const float* xrow[RG];
+  int arow[RG];
   bool valid[RG];
 #pragma unroll
-  for (int g = 0; g < RG; ++g) xrow[g] = p.x + (int64_t)R[g].arow_id * d, valid[g] = R[g].a_valid;
+  for (int g = 0; g < RG; ++g) arow[g] = R[g].arow_id, valid[g] = R[g].a_valid;
 
   RAcc<NT> v[RG];
   if constexpr (MODE == RT_GATE) {  // the timestep's gate pre-activation, stored as is
 #pragma unroll
     for (int g = 0; g < RG; ++g) v[g].zero();
-    rt_mm<NT, RG, true>(v, xrow, valid, p.w_gate, d, KB, rt_lds);
+    rt_mm<NT, RG, true>(v, p.x, arow, valid, p.w_gate, d, KB, rt_lds);
 #pragma unroll
     for (int g = 0; g < RG; ++g) rt_store<NT>(v[g], p.gate_out, R[g].crow, R[g].n_valid, d);
   }
@@ -903,15 +915,12 @@ __device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) v[g].t[t] = clamp4(v[g].t[t], -10.f, 10.f);
     }
-    const float* arow[RG];
     bool ok[RG];
 #pragma unroll
-    for (int g = 0; g < RG; ++g) {
-      arow[g] = pass == 0 ? p.agg + (int64_t)R[g].arow_id * d : xrow[g];
+    for (int g = 0; g < RG; ++g)
       ok[g] = pass == 0 ? R[g].a_pos : (mixed ? (pass == 1 ? R[g].a_pos : R[g].a_valid & !R[g].a_pos) : R[g].a_valid);
-    }
     const float* W = pass == 0 ? p.w_n : (pass == 1 && npos_wg > 0 ? p.w_loop : p.w_evolve);
-    rt_mm<NT, RG, false>(v, arow, ok, W, d, KB, rt_lds);
+    rt_mm<NT, RG, false>(v, pass == 0 ? p.agg : p.x, arow, ok, W, d, KB, rt_lds);
   }
   if (((first == 0 && last == 1) || (first == 1 && last == 1 && p1)) && !p.euclid) {
     // agg @ W_n without a self loop, or Lorentz rows without one
@@ -923,9 +932,9 @@ __device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
   if constexpr (MODE == RT_STEP) {  // the time gate pre-activation clamp(x_prev) @ W_g
     RAcc<NT> gt[1];
     gt[0].zero();
-    const float* xp[1] = {p.step.x_prev + (int64_t)R[0].arow_id * d};
+    const int xr[1] = {R[0].arow_id};
     const bool okp[1] = {R[0].a_valid};
-    rt_mm<NT, 1, true>(gt, xp, okp, p.step.w_g, d, KB, rt_lds);
+    rt_mm<NT, 1, true>(gt, p.step.x_prev, xr, okp, p.step.w_g, d, KB, rt_lds);
     rt_finish<NT, MODE>(p, v[0], R[0], &gt[0], rt_lds);
   } else {
 #pragma unroll
@@ -1027,6 +1036,8 @@ int layer_rowtail(const LayerArgs& a, float* agg, hipStream_t st) {
 int layer_rowtail_part(const LayerArgs& a, float* agg, int which, int lo, int hi, hipStream_t st) {
   const int mode = a.agg_mode;
   if (a.d <= 0 || a.d > MAX_D || (a.d & 3)) return set_error(REGCN_EINVAL, "rowtail needs d %% 4 == 0, d <= 256");
+  // the products read x / agg / x_prev rows through 32-bit buffer offsets (rt_mm)
+  if ((int64_t)a.V * a.d * 4 >= (int64_t)RT_OOB) return set_error(REGCN_ENOTSUP, "rowtail tables must stay under 4 GB");
   // a non-step layer may skip h (h_out NULL) when its consumer reads x_next and r_next only
   if (!a.x || !a.rows || (!a.h_out && !a.fuse_step && !a.x_next)) return set_error(REGCN_EINVAL, "null pointer");
   if ((a.w_loop == nullptr) != (a.w_evolve == nullptr)) return set_error(REGCN_EINVAL, "self-loop weights must come in pairs");

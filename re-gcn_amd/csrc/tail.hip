@@ -25,7 +25,7 @@ namespace {
 
 constexpr int TAIL_THR = 256;
 
-__device__ __forceinline__ float clamp10(float x) { return fminf(fmaxf(x, -10.f), 10.f); }
+__device__ __forceinline__ float clamp10(float x) { return clampf(x, -10.f, 10.f); }
 __device__ __forceinline__ bool in10(float x) { return x >= -10.f && x <= 10.f; }
 
 template <bool BWD>
