@@ -337,6 +337,32 @@ struct RAcc {
 __device__ const f4 kZeroRow[1] = {{0.f, 0.f, 0.f, 0.f}};
 
 constexpr int RT_KB_BYTES = 4 * 4 * 64 * 16;  // one 16-deep k-block of a packed weight: 16 KB
+// Diagnostic build only (-DREGCN_RT_STAMPS=1, tools/c5probe.py --rt-stamps): the step tail's
+// wave 0 s_memtime cycles per phase into trace[16 b + 8 ..]: products, row maps, blend-stage
+// waits, blend, the row maps after it (radius included), the radius stores, the x stores.
+#ifndef REGCN_RT_STAMPS
+#define REGCN_RT_STAMPS 0
+#endif
+constexpr bool kRtStamps = REGCN_RT_STAMPS != 0;
+struct RtStamps {
+  int64_t ph[7] = {0, 0, 0, 0, 0, 0, 0}, t = 0;
+  __device__ __forceinline__ void start() {
+    if constexpr (kRtStamps) t = (int64_t)__builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void mark(int k) {
+    if constexpr (kRtStamps) {
+      const int64_t u = (int64_t)__builtin_amdgcn_s_memtime();
+      ph[k] += u - t;
+      t = u;
+    }
+  }
+  __device__ __forceinline__ void write(int64_t* trace) {
+    if constexpr (kRtStamps) {
+      if (trace && threadIdx.x == 0)
+        for (int k = 0; k < 7; ++k) trace[(int64_t)blockIdx.x * 16 + 8 + k] = ph[k];
+    }
+  }
+};
 constexpr int RT_A_RING = 3;
 // LDS of a workgroup whose waves hold RG 16-row groups each: the weight double buffer and the
 // A ring (3 k-blocks x 4 waves x RG groups x 1 KB)
@@ -723,7 +749,7 @@ __device__ __forceinline__ void rt_store_staged(const RAcc<NT>& a, float* __rest
 // layer's x / |h| or the timestep.  `g` (RT_STEP) holds the in-kernel gate product.
 template <int NT, int MODE>
 __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const RtRows& R, const RAcc<NT>* g,
-                                          char* lds) {
+                                          char* lds, RtStamps* sp = nullptr) {
   constexpr bool STEP = MODE >= RT_STEP;
   const int lane = threadIdx.x & 63, q = lane >> 4, d = p.d;
   const int* crow = R.crow;
@@ -764,6 +790,12 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
   } else {
     const StepArgs& s = p.step;
     const Curv k = s.k;
+    // the radius step's operands, loaded now: their latency (r_static is an HBM row read) would
+    // otherwise sit between the blend and the stores
+    const float rs = s.r_static[own_int(crow)];
+    const float br = s.residual ? *s.b_r : 0.f;
+    float wr[NT];
+    if (s.residual) rt_col<NT>(wr, s.w_r, d);
     lz_project(z, k);
     if (s.layer_norm) {
       lz_log0(z, k);
@@ -774,6 +806,7 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     rt_apply<NT>(v, z);
     float bg[NT];
     rt_col<NT>(bg, s.b_g, d);
+    if (sp) sp->mark(1);
     if constexpr (MODE == RT_STEP_PRE) {
       const float* xs = reinterpret_cast<const float*>(lds + wave_id() * 2 * RT_SC_BYTES);
       const float* zs = xs + RT_SC_BYTES / 4;
@@ -789,7 +822,9 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the last stage
             rt_stage_blend(s, R, d, 16 * NT, stage, lds);
           }
+          if (sp) sp->mark(3);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stage's copies have landed
+          if (sp) sp->mark(2);
         }
         // rows past n_valid and columns >= d were staged as zeros (pad columns: v, x_prev and the
         // gate row all 0 there, so the blend keeps them 0; such rows are never stored)
@@ -820,17 +855,16 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
         }
       }
     }
+    if (sp) sp->mark(3);
     rt_sumsq<NT>(v, n2);
     z.m2 = own_row(n2);
     lz_exp0(z, k);
     lz_project(z, k);  // hyperbolic_model.py:860
     // radius: per-row scalars once per lane, for its own row r = lane & 3 (own_row)
-    const float rs = s.r_static[own_int(crow)];
     const float n2o = z.m2;
     float newr = rs;
     if (s.residual) {
-      float wr[NT], lf[4], dl[4];
-      rt_col<NT>(wr, s.w_r, d);
+      float lf[4], dl[4];
       // w_r . log0(v pf) = (pf log0 factor) (w_r . v): the row's factor applied to the dot
       spread_rows(z.pf * log0_factor(n2o, s.k_rad), lf);
 #pragma unroll
@@ -840,12 +874,13 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
         for (int t = 0; t < NT; ++t) acc = fmaf(wr[t], v.t[t][r], acc);
         dl[r] = row16_sum(acc) * lf[r];
       }
-      const float delta = fminf(fmaxf(own_row(dl) + *s.b_r, -s.eps_r), s.eps_r);
+      const float delta = fminf(fmaxf(own_row(dl) + br, -s.eps_r), s.eps_r);
       const float dyn = row_radius(n2o);
       newr = (s.beta * rs + (1.f - s.beta) * dyn) + delta;
     }
     const Curv kr = s.residual ? s.k_rad : s.k;
     lz_scale(z, fdiv(fminf(fmaxf(newr, REGCN_EPS), kr.rmax), row_radius(n2o)));
+    if (sp) sp->mark(4);
     if (s.h_out) {
       rt_apply<NT>(v, z);
       rt_store_staged<NT>(v, s.h_out, R, d, lds, p, false);
@@ -853,11 +888,13 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     spread_rows(z.m2, n2);
     if (s.r_out) rt_store_radius(n2, s.r_out, crow, n_valid);
     if (p.send_x) rt_send_radius(p, n2, crow, n_valid);
+    if (sp) sp->mark(5);
     if (s.x_out) {
       lz_log0(z, k);
       rt_apply<NT>(v, z);
       rt_store_staged<NT>(v, s.x_out, R, d, lds, p, p.send_x != nullptr);
     }
+    if (sp) sp->mark(6);
   }
 }
 
@@ -873,6 +910,8 @@ template <int NT, int MODE, int RG>
 __device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
   static_assert(MODE != RT_STEP || RG == 1, "the in-kernel gate product runs on one row group");
   extern __shared__ char rt_lds[];
+  RtStamps st;
+  st.start();
   const int w = wave_id();
   const int wg0 = row0 + blockIdx.x * RT_ROWS * RG;
   const int d = p.d, KB = (d + 15) >> 4;
@@ -937,8 +976,11 @@ __device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
     rt_mm<NT, 1, true>(gt, p.step.x_prev, xr, okp, p.step.w_g, d, KB, rt_lds);
     rt_finish<NT, MODE>(p, v[0], R[0], &gt[0], rt_lds);
   } else {
+    st.mark(0);
 #pragma unroll
-    for (int g = 0; g < RG; ++g) rt_finish<NT, MODE>(p, v[g], R[g], nullptr, rt_lds);
+    for (int g = 0; g < RG; ++g)
+      rt_finish<NT, MODE>(p, v[g], R[g], nullptr, rt_lds, (kRtStamps && MODE == RT_STEP_PRE) ? &st : nullptr);
+    if constexpr (MODE == RT_STEP_PRE) st.write(p.trace);
   }
 }
 
@@ -1007,6 +1049,7 @@ static int launch_tail(const LayerArgs& a, int r0, int r1, hipStream_t st) {
   const int rg = (NT > 8 && rowtail_rg() == 2 && r1 - r0 >= rt_rg2_min_rows()) ? 2 : 1;
   const unsigned grid = (unsigned)((r1 - r0 + RT_ROWS * rg - 1) / (RT_ROWS * rg));
   const size_t lds = rt_lds_bytes(rg);
+  if (kRtStamps && a.fuse_step && a.step.tw) const_cast<LayerArgs&>(a).trace = g_trace;
   if (a.fuse_step && a.step.tw && rg == 2 && step_rg() == 2) {
     hipLaunchKernelGGL((k_rowtail2<NT, RT_STEP_PRE>), dim3(grid), dim3(NTHR), lds, st, a, r0);
   } else if (a.fuse_step && a.step.tw) {

@@ -5,6 +5,7 @@ launches vs per-layer launches, wall time per predict and peak memory.
   python tools/c5probe.py [--V 1000000] [--triples 25000000] [--reps 5] [--modes phases,layers]
 """
 import argparse
+import json
 import os
 import sys
 import time
@@ -27,6 +28,8 @@ def main():
     ap.add_argument("--modes", default="phases,layers")
     ap.add_argument("--encoder", default="hyperbolic_uvrgcn")
     ap.add_argument("--budgets", default="0", help="fused-layer edge budgets to compare (0: the default)")
+    ap.add_argument("--rt-stamps", action="store_true",
+                    help="step-tail phase cycles (a library built with -DREGCN_RT_STAMPS=1 as REGCN_HIP_LIB)")
     ap.add_argument("--streams", type=int, default=1,
                     help="independent predicts in flight on this many streams (two windows alternate)")
     a = ap.parse_args()
@@ -56,6 +59,9 @@ def run(a, cfg, snaps, dev, budget):
     test = torch.from_numpy(snaps[cfg["T"]][:512]).to(dev)
     edges = 2 * sum(g.number_of_edges() for g in glist)
     outs = {}
+    if a.rt_stamps:
+        rt_stamps(model, glist, cfg, test, dev)
+        return
     for mode in a.modes.split(","):
         model.use_phases = mode == "phases"
         with torch.no_grad():
@@ -81,6 +87,30 @@ def run(a, cfg, snaps, dev, budget):
         for name, x, y in (("score", p[1], l[1]), ("score_rel", p[2], l[2])):
             print("%s equal=%s max|d|=%.3g finite=%s" % (name, bool(torch.equal(x, y)), float((x - y).abs().max()),
                                                         bool(torch.isfinite(x).all())), flush=True)
+
+
+def rt_stamps(model, glist, cfg, test, dev):
+    """Wave 0's s_memtime cycles per phase of the last step-tail launch (k_rowtail3, the
+    diagnostic build's trace[16 b + 8 ..]): products, row maps, blend-stage waits, blend, the
+    maps after it, the radius stores, the x stores;
+    mean over its workgroups and fractions."""
+    from regcn_amd import _lib
+    model.use_phases = False
+    with torch.no_grad():
+        for _ in range(2):
+            model.predict(glist, cfg["R"], None, test, True)
+        torch.cuda.synchronize()
+        buf = torch.zeros(1 << 20, 16, dtype=torch.int64, device=dev)
+        _lib.call("regcn_set_trace", _lib.addr(buf, torch.int64))
+        model.predict(glist, cfg["R"], None, test, True)
+        torch.cuda.synchronize()
+        _lib.call("regcn_set_trace", None)
+    ph = buf[:, 8:15].double().cpu()
+    used = ph.sum(1) > 0
+    mean = ph[used].mean(0)
+    names = ["products", "row_maps", "stage_waits", "blend", "maps_after", "radius_stores", "x_stores"]
+    print(json.dumps({"workgroups": int(used.sum()), "cycles_mean": {n: round(float(v)) for n, v in zip(names, mean)},
+                      "frac": {n: round(float(v / mean.sum()), 4) for n, v in zip(names, mean)}}), flush=True)
 
 
 def run_streams(a, cfg, snaps, dev, glist):
