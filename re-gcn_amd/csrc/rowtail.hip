@@ -620,24 +620,6 @@ __device__ __forceinline__ void rt_send_radius(const LayerArgs& p, const float n
   }
 }
 
-template <int NT>
-__device__ __forceinline__ void rt_send_rows(const RAcc<NT>& a, const LayerArgs& p, const int crow[4], int n_valid,
-                                             int d) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if (4 * (lane >> 4) + r >= n_valid) continue;
-    int s0, s1;
-    rt_send_span(p, crow[r], s0, s1);
-    for (int sl = s0; sl < s1; ++sl) {
-      float* dst = p.send_x + (int64_t)p.send_pos[sl] * d + (lane & 15);
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-        if (16 * t + 15 < d || 16 * t + (lane & 15) < d) dst[16 * t] = a.t[t][r];
-    }
-  }
-}
-
 __device__ __forceinline__ int own_int(const int v[4]) {
   const bool b0 = threadIdx.x & 1, b1 = threadIdx.x & 2;
   const int lo = b0 ? v[1] : v[0], hi = b0 ? v[3] : v[2];
@@ -654,10 +636,25 @@ __device__ __forceinline__ int own_int(const int v[4]) {
 // blend reads them per column tile: no second accumulator set, half the registers).
 enum { RT_LAYER = 0, RT_GATE = 1, RT_STEP = 2, RT_STEP_PRE = 3 };
 
-// One 16-row group of a wave: its row ids (C layout), counts and A-operand row.
+// Stage layout of the step layer's blend operands and of the staged row stores: per column
+// stage of RT_SC_COLS (80) and array, 16-B piece sc of row `row` sits at float
+// 256 (sc >> 2) + 16 pi(row) + 4 (sc & 3), pi(row) = (row >> 2) + 4 (row & 3).  Lane l of the
+// i-th 1-KB copy moves piece 4 i + (l & 3) of row rt_stage_row(l) (pi of it = l >> 2), so a
+// copy is contiguous in LDS (global_load_lds puts lane l's 16 B at 16 l), a lane's row id is
+// one shuffle per kernel, and the C-layout element (row 4 q + r, stage column 16 t + c) sits at
+// 256 t + 64 r + 16 q + c = 256 t + 64 r + lane: conflict-free element reads and writes.  (A
+// row-major stage divided the slot by the row width per piece -- ~20 VALU and a shuffle + LDS
+// round trip per 16 B -- and its element accesses, rows 320 B apart, hit one bank 4 ways.)
+__device__ __forceinline__ int rt_stage_row(int lane) {
+  const int p = lane >> 2;
+  return 4 * (p & 3) + (p >> 2);
+}
+
+// One 16-row group of a wave: its row ids (C layout), counts and A-operand row; stage_rid /
+// stage_ok: the row this lane moves in the stage copies (rt_stage_row).
 struct RtRows {
-  int base, n_valid, arow_id, npos_w;
-  bool a_valid, a_pos;
+  int base, n_valid, arow_id, npos_w, stage_rid;
+  bool a_valid, a_pos, stage_ok;
   int crow[4];
 };
 
@@ -672,16 +669,19 @@ __device__ __forceinline__ RtRows rt_rows(const LayerArgs& p, int base) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) R.crow[r] = __shfl(R.arow_id, 4 * q + r);
   R.npos_w = min(max(p.n_pos - base, 0), R.n_valid);
+  R.stage_rid = __shfl(R.arow_id, rt_stage_row(lane));
+  R.stage_ok = rt_stage_row(lane) < R.n_valid;
   return R;
 }
 
 // The step layer's blend operands (x_prev and the gate rows) in column stages of RT_SC_COLS:
 // each wave DMAs its 16 rows' columns [RT_SC_COLS s, ...) of both arrays into its own LDS
-// region (row stride = the stage's width; 16-B pieces, global_load_lds, 5 instructions per
-// array), then reads them in C layout -- instead of 2 x NT x 4 scattered 4-B loads per lane.
-// The region is the products' LDS (free after rt_mm's final barrier): 4 waves x 2 arrays x 5 KB.
+// region (the stage layout above; 16-B pieces, global_load_lds, <= 5 instructions per array),
+// then reads them in C layout -- instead of 2 x NT x 4 scattered 4-B loads per lane.  The
+// region is the products' LDS (free after rt_mm's final barrier): 4 waves x 2 arrays x 5 KB.
 constexpr int RT_SC_COLS = 80, RT_SC_TILES = RT_SC_COLS / 16, RT_SC_BYTES = 16 * RT_SC_COLS * 4;
 static_assert(4 * 2 * RT_SC_BYTES <= rt_lds_bytes(1), "blend staging must fit the tail's LDS");
+static_assert(RT_SC_BYTES == RT_SC_TILES * 1024, "a stage is RT_SC_TILES 1-KB copies per array");
 
 __device__ __forceinline__ void rt_stage_blend(const StepArgs& s, const RtRows& R, int d, int dpad, int stage,
                                                char* lds) {
@@ -691,55 +691,54 @@ __device__ __forceinline__ void rt_stage_blend(const StepArgs& s, const RtRows& 
   const int c0 = RT_SC_COLS * stage, ncols = min(RT_SC_COLS, dpad - c0), f4pr = ncols >> 2;
   const float* zrow = reinterpret_cast<const float*>(kZeroRow);
   char* base = lds + w * 2 * RT_SC_BYTES;
+  const int64_t off = (int64_t)R.stage_rid * d + c0 + 4 * (lane & 3);
 #pragma unroll
-  for (int i = 0; i < RT_SC_BYTES / 1024; ++i) {
-    const int slot = 64 * i + lane, sr = slot / max(f4pr, 1), sc = slot - sr * f4pr;
-    const int rid = __shfl(R.arow_id, min(sr, 15));
-    const bool ok = (slot < 16 * f4pr) & (sr < R.n_valid) & (c0 + 4 * sc < d);
-    const int64_t off = (int64_t)rid * d + c0 + 4 * sc;
-    __builtin_amdgcn_global_load_lds((const void*)(ok ? s.x_prev + off : zrow),
+  for (int i = 0; i < RT_SC_TILES; ++i) {
+    if (4 * i >= f4pr) break;  // (dpad and stage are compile-time: the stage's copies)
+    const int sc = 4 * i + (lane & 3);
+    const bool ok = R.stage_ok & (sc < f4pr) & (c0 + 4 * sc < d);
+    __builtin_amdgcn_global_load_lds((const void*)(ok ? s.x_prev + off + 16 * i : zrow),
                                      (__attribute__((address_space(3))) void*)(base + i * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(ok ? s.tw + off : zrow),
+    __builtin_amdgcn_global_load_lds((const void*)(ok ? s.tw + off + 16 * i : zrow),
                                      (__attribute__((address_space(3))) void*)(base + RT_SC_BYTES + i * 1024), 16, 0, 0);
   }
 }
 
-// C-layout rows stored through the wave's LDS region in the same 80-column stages: written
-// there per element, read back as 16-B row pieces, stored as whole 16-B vectors (5 per lane per
-// stage) instead of NT x 4 scattered 4-B stores.  In-order LDS within the wave: no barrier.
-// send: also into p's send block (as rt_send_rows)
+// C-layout rows stored through the wave's LDS region in the same 80-column stages (the stage
+// layout): written there per element, read back as 16-B row pieces (one contiguous
+// ds_read_b128 per copy), stored as whole 16-B vectors instead of NT x 4 scattered 4-B stores.
+// In-order LDS within the wave: no barrier.  Pad columns are written (never stored).
+// send: also into p's send block (every slot of the row, rt_send_span)
 template <int NT>
 __device__ __forceinline__ void rt_store_staged(const RAcc<NT>& a, float* __restrict__ M, const RtRows& R, int d,
                                                 char* lds, const LayerArgs& p, bool send) {
-  const int lane = threadIdx.x & 63, q = lane >> 4;
+  const int lane = threadIdx.x & 63;
   float* st = reinterpret_cast<float*>(lds + wave_id() * 2 * RT_SC_BYTES);
   constexpr int NS = (NT + RT_SC_TILES - 1) / RT_SC_TILES;
+  float* mrow = M + (int64_t)R.stage_rid * d + 4 * (lane & 3);
+  int s0 = 0, s1 = 0;
+  if (send) rt_send_span(p, R.stage_rid, s0, s1);
 #pragma unroll
   for (int stage = 0; stage < NS; ++stage) {
     const int c0 = RT_SC_COLS * stage;
     if (c0 >= d) break;
-    const int ncols = min(RT_SC_COLS, d - c0), f4pr = ncols >> 2;
+    const int f4pr = min(RT_SC_COLS, d - c0) >> 2;
+    const int t0 = stage * RT_SC_TILES;
 #pragma unroll
-    for (int t = stage * RT_SC_TILES; t < min(NT, (stage + 1) * RT_SC_TILES); ++t) {
-      const int cl = 16 * t + (lane & 15) - c0;
-      if (16 * t + 15 - c0 < ncols || cl < ncols) {  // tiles reaching past d are masked per lane
+    for (int t = t0; t < min(NT, t0 + RT_SC_TILES); ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) st[(4 * q + r) * ncols + cl] = a.t[t][r];
-      }
-    }
+      for (int r = 0; r < 4; ++r) st[256 * (t - t0) + 64 * r + lane] = a.t[t][r];
+    constexpr int NI = RT_SC_TILES;
+    f4 val[NI];
 #pragma unroll
-    for (int i = 0; i < RT_SC_BYTES / 1024; ++i) {
-      const int slot = 64 * i + lane, sr = slot / f4pr, sc = slot - sr * f4pr;
-      const int rid = __shfl(R.arow_id, min(sr, 15));
-      if (slot < 16 * f4pr && sr < R.n_valid) {
-        const f4 val = *reinterpret_cast<const f4*>(st + 4 * slot);
-        *reinterpret_cast<f4*>(M + (int64_t)rid * d + c0 + 4 * sc) = val;
-        if (send) {
-          int s0, s1;
-          rt_send_span(p, rid, s0, s1);
-          for (int sl = s0; sl < s1; ++sl)
-            *reinterpret_cast<f4*>(p.send_x + (int64_t)p.send_pos[sl] * d + c0 + 4 * sc) = val;
-        }
+    for (int i = 0; i < NI; ++i)
+      if (t0 + i < NT) val[i] = *reinterpret_cast<const f4*>(st + 256 * i + 4 * lane);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      if (t0 + i < NT && R.stage_ok && 4 * i + (lane & 3) < f4pr) {
+        *reinterpret_cast<f4*>(mrow + c0 + 16 * i) = val[i];
+        for (int sl = s0; sl < s1; ++sl)
+          *reinterpret_cast<f4*>(p.send_x + (int64_t)p.send_pos[sl] * d + c0 + 16 * i + 4 * (lane & 3)) = val[i];
       }
     }
   }
@@ -756,11 +755,10 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
   const int n_valid = R.n_valid;
   // the first blend stage's copies fly under the epilogue's row maps
   if constexpr (MODE == RT_STEP_PRE) rt_stage_blend(p.step, R, d, 16 * NT, 0, lds);
+  // the clamp as bounds (+-inf: none, Euclid) -- a runtime test per element would be a select
+  const float cb = p.euclid ? __builtin_inff() : 10.f;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    if (!p.euclid) v.t[t] = clamp4(v.t[t], -10.f, 10.f);
-    v.t[t] = leaky4(v.t[t]);
-  }
+  for (int t = 0; t < NT; ++t) v.t[t] = leaky4(clamp4(v.t[t], -cb, cb));
   float n2[4];
   RtLazy z{0.f, 1.f};
   if (!p.euclid || p.r_next) {
@@ -770,8 +768,6 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
   if (!p.euclid) lz_exp0(z, p.k);
 
   if constexpr (!STEP) {
-    // (element stores: staging them as in the step layer made the two-group first layer's
-    // tail 2.5 % slower at config 5)
     if (p.h_out) {
       if (!p.euclid) rt_apply<NT>(v, z);
       rt_store<NT>(v, p.h_out, crow, n_valid, d);
@@ -784,8 +780,9 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
         lz_log0(z, p.k);
         rt_apply<NT>(v, z);
       }
-      rt_store<NT>(v, p.x_next, crow, n_valid, d);
-      if (p.send_x) rt_send_rows<NT>(v, p, crow, n_valid, d);
+      // staged like the step layer's rows (element stores: 2,062 vs 2,052 us at config 5,
+      // profiles/r6_stage_layout_ab.jsonl)
+      rt_store_staged<NT>(v, p.x_next, R, d, lds, p, p.send_x != nullptr);
     }
   } else {
     const StepArgs& s = p.step;
@@ -828,13 +825,12 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
         }
         // rows past n_valid and columns >= d were staged as zeros (pad columns: v, x_prev and the
         // gate row all 0 there, so the blend keeps them 0; such rows are never stored)
-        const int ncols = min(RT_SC_COLS, 16 * NT - RT_SC_COLS * stage);
-        const int cl = 16 * t + (lane & 15) - RT_SC_COLS * stage;
+        const int tt = t - RT_SC_TILES * stage;  // the stage layout: element at 256 tt + 64 r + lane
         const f4 c4 = clamp4(v.t[t], -10.f, 10.f);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float xp = xs[(4 * q + r) * ncols + cl];
-          const float zt = zs[(4 * q + r) * ncols + cl];
+          const float xp = xs[256 * tt + 64 * r + lane];
+          const float zt = zs[256 * tt + 64 * r + lane];
           const float pr = clampf(xp, -10.f, 10.f);
           const float gg = frcp(1.f + __builtin_amdgcn_exp2f(fmaf(zt, -FM_LOG2E, nbg[t])));
           v.t[t][r] = fmaf(gg, c4[r] - pr, pr);  // gg c4 + (1 - gg) pr

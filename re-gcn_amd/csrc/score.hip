@@ -275,17 +275,36 @@ __global__ __launch_bounds__(256) void k_score(ScoreArgs p) {
 // den = (1 + eps + c^2 x2 y2) - 2c xy.
 struct RowK {
   float x2, m2Bq, Bq2, c2x2;
+  float sx2, sm2Bq, sBq2;  // the same times scale (pair_score_fast)
 };
 struct ColK {
   float y2, A0, sb;
+  float lo;  // sb - scale mx^2: the score at the clamp
 };
 
 __device__ __forceinline__ RowK row_k(float x2, const ScoreArgs& p) {
   const float Bq = 1.f - p.c * x2;
-  return RowK{x2, -2.f * Bq, Bq * Bq, p.c * p.c * x2};
+  return RowK{x2, -2.f * Bq, Bq * Bq, p.c * p.c * x2, p.scale * x2, -2.f * p.scale * Bq, p.scale * (Bq * Bq)};
 }
 __device__ __forceinline__ ColK col_k(float y2, float bias, const ScoreArgs& p) {
-  return ColK{y2, 1.f + p.c * y2, p.scale * p.margin + bias};
+  const float sb = p.scale * p.margin + bias;
+  return ColK{y2, 1.f + p.c * y2, sb, fmaf(-p.scale, p.mx * p.mx, sb)};
+}
+
+// The proxy score of one pair in 11 VALU: S = sb - scale min(n2, mx^2) = med3(a, lo, sgn(scale) inf)
+// with a = sb - (scale |num|^2 / den) / den -- scale folded into the row factors, the clamp as
+// one med3 against the column's clamped score (max for scale >= 0, min below), |num|^2 not
+// clamped at 0 (>= 0 but for rounding, which moves S by ~1e-7 scale).  sgn_inf: +inf or -inf by
+// the sign of scale.  Every score, CE and count path uses it, so they agree bit for bit.
+__device__ __forceinline__ float pair_score_fast(float xy, const RowK& r, const ColK& q, const ScoreArgs& p,
+                                                 float sgn_inf) {
+  const float m2c = -2.f * p.c;
+  const float A = fmaf(m2c, xy, q.A0);
+  const float t = fmaf(A, r.sx2, r.sm2Bq * xy);
+  const float sn2 = fmaf(A, t, r.sBq2 * q.y2);
+  const float den = fmaf(m2c, xy, fmaf(r.c2x2, q.y2, 1.f + REGCN_EPS));
+  const float rd = __builtin_amdgcn_rcpf(den);
+  return __builtin_amdgcn_fmed3f(fmaf(-(sn2 * rd), rd, q.sb), q.lo, sgn_inf);
 }
 
 // n^2 of one pair (clamped to mx^2), and optionally num2 / den for the gradient.
@@ -316,7 +335,11 @@ __device__ __forceinline__ float row16_max(float v) {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
-template <int MODE, int J>
+// PERM: the lane's J candidates are consecutive (ni[j] = ni[0] + j: score_f32_body stages
+// candidate J i + j at tile row 16 j + i), so a query row's scores leave as one J-float vector
+// store per lane (`full` and vec-aligned), not J scattered 4-B stores; otherwise ni[j] =
+// ni[0] + 16 j.
+template <int MODE, int J, bool PERM = false>
 __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4* acc, const float* x2,
                                                     const float* y2, const float* bn_, const int* qi, const int* ni,
                                                     int lane, int bn, float* run_m, float* run_se,
@@ -328,17 +351,27 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
 #pragma unroll
   for (int j = 0; j < J; ++j) ck[j] = col_k(y2[j], bn_[j], p);
   const float mx2 = p.mx * p.mx;
+  const float sgn_inf = p.scale >= 0.f ? __builtin_inff() : -__builtin_inff();
   if (MODE == 0) {
-    // the lane's candidates are ni[0] + 16 j (each valid one): one row address per query row,
-    // the 16 j steps as immediate store offsets
+    // the lane's candidates are ni[0] + CS j (each valid one): one row address per query row,
+    // the j steps as immediate store offsets
+    constexpr int CS = PERM ? 1 : 16;
     const int64_t n0 = ni[0] < p.N ? ni[0] : 0;
     if (full) {  // every query row and candidate of the tile valid (wave-uniform): no store masks
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float* orow = p.out + (int64_t)qi[r] * p.N + n0;
+        float sv[J];
 #pragma unroll
-        for (int j = 0; j < J; ++j) {
-          orow[16 * j] = fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb);
+        for (int j = 0; j < J; ++j) sv[j] = pair_score_fast(acc[j][r], rk[r], ck[j], p, sgn_inf);
+        if constexpr (PERM && J == 4) {
+          *reinterpret_cast<f4*>(orow) = f4{sv[0], sv[1], sv[2], sv[3]};
+        } else if constexpr (PERM && J == 2) {
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          *reinterpret_cast<f2*>(orow) = f2{sv[0], sv[1]};
+        } else {
+#pragma unroll
+          for (int j = 0; j < J; ++j) orow[CS * j] = sv[j];
         }
       }
       return;
@@ -349,7 +382,7 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
       float* orow = p.out + (int64_t)qi[r] * p.N + n0;
 #pragma unroll
       for (int j = 0; j < J; ++j)
-        if (ni[j] < p.N) orow[16 * j] = fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb);
+        if (ni[j] < p.N) orow[CS * j] = pair_score_fast(acc[j][r], rk[r], ck[j], p, sgn_inf);
     }
   } else if (MODE == 1) {  // this lane's running (max, sum exp) per query row, across tiles
 #pragma unroll
@@ -358,7 +391,7 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
       const int t = qi[r] < p.B ? p.target[qi[r]] : -1;
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        sv[j] = ni[j] < p.N ? fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb)
+        sv[j] = ni[j] < p.N ? pair_score_fast(acc[j][r], rk[r], ck[j], p, sgn_inf)
                             : -INFINITY;
         m = fmaxf(m, sv[j]);
         if (ni[j] == t) p.tgt_logit[qi[r]] = sv[j];
@@ -380,7 +413,7 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
 #pragma unroll
       for (int j = 0; j < J; ++j)
         if (ni[j] < p.N)
-          cnt += fmaf(-p.scale, pair_n2(acc[j][r], rk[r], ck[j], p, nullptr, nullptr, nullptr), ck[j].sb) > t ? 1.f : 0.f;
+          cnt += pair_score_fast(acc[j][r], rk[r], ck[j], p, sgn_inf) > t ? 1.f : 0.f;
       run_se[r] += cnt;  // an exact integer (< 2^24 per lane)
     }
   } else {  // MODE 2: CE backward coefficients (8-wave workgroups only: J = 4, SN-candidate tiles)
@@ -403,7 +436,7 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
         const float xy = acc[j][r], Y2 = ck[j].y2;
         float num2, rd, A;
         const float n2 = pair_n2(xy, rk[r], ck[j], p, &num2, &rd, &A);
-        const float S = fmaf(-p.scale, n2, ck[j].sb);
+        const float S = pair_score_fast(xy, rk[r], ck[j], p, sgn_inf);  // the forward's bits
         const float G = gl * (__builtin_amdgcn_exp2f(fmaf(S, LOG2E, -lsel)) - (ni[j] == t ? 1.f : 0.f));
         float gxy = 0.f, gx2 = 0.f, gy2 = 0.f;
         if (num2 * rd * rd <= mx2) {  // not clamped: dn2/du = dnum2/du / den^2 - 2 num2 dden/du / den^3
@@ -506,7 +539,9 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     if (p.trace && tid == 0) p.trace[(int64_t)blk * 16 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  const int d = p.d, KB = KBT ? KBT : (d + 15) >> 4, SE = score_lds_stride(d);
+  // with KBT known the row stride is a constant (16 KBT + 8 = score_lds_stride(d) for every d of
+  // the bucket), so the B-fragment reads of a tile are immediate offsets of one address
+  const int d = p.d, KB = KBT ? KBT : (d + 15) >> 4, SE = KBT ? 16 * KBT + 8 : score_lds_stride(d);
   if constexpr (KBT > 0) __builtin_assume(d > 16 * (KBT - 1) && d <= 16 * KBT);
   const int nbn = p.n_rng ? p.rng_total : (p.N + SNW - 1) / SNW, nbq = (p.B + SQW - 1) / SQW;
   // candidate tile t -> its first row and valid rows (row ranges: a tile never spans two)
@@ -607,6 +642,9 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   static_assert(64 * NW == 8 * SNW, "staging map: 8 threads per candidate row");
   constexpr int IT = (KBA * 4 + 7) / 8;
   const int sr = tid >> 3, sub = tid & 7, per_row = 4 * KB;
+  // candidate sr of the tile sits at tile row 16 (sr % J) + sr / J, so accumulator j of lane l
+  // holds candidate J (l & 15) + j: a lane's J candidates are consecutive (vector score stores)
+  const int trow = 16 * (sr % J) + sr / J;
   f4 v[IT];
   auto fetch = [&](int t) {  // unconditional clamped loads (a conditional load drains vmcnt)
     int row0, nv;
@@ -620,7 +658,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   auto stash = [&](int buf) {
     // rows past the tile's valid rows hold a copy of its last row (fetch clamps): finite, and
     // their scores are never written or counted, so only the columns >= d need zeros
-    float* lrow = Es + buf * SNW * SE + sr * SE;
+    float* lrow = Es + buf * SNW * SE + trow * SE;
     float ss = 0.f;
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
@@ -642,7 +680,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     ss += __shfl_xor(ss, 1);
     ss += __shfl_xor(ss, 2);
     ss += __shfl_xor(ss, 4);
-    if (sub == 0) e2s[buf * SNW + sr] = ss;
+    if (sub == 0) e2s[buf * SNW + trow] = ss;
   };
   fetch(bn);
   stash(0);
@@ -709,12 +747,14 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     tile_rows(bn, row0, nv);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      ni[j] = 16 * j + (lane & 15) < nv ? row0 + 16 * j + (lane & 15) : 0x7fffffff;  // invalid: >= N
+      const int c = J * (lane & 15) + j;  // the candidate at tile row 16 j + (lane & 15)
+      ni[j] = c < nv ? row0 + c : 0x7fffffff;  // invalid: >= N
       y2[j] = e2s[cur * SNW + 16 * j + (lane & 15)];
       bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
     }
-    score_epilogue_fast<MODE, J>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se,
-                                 MODE == 0 && nv == SNW && q0 + SQW <= p.B);
+    // vector stores need the row start aligned to J floats (wave-uniform)
+    score_epilogue_fast<MODE, J, true>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se,
+                                       MODE == 0 && nv == SNW && q0 + SQW <= p.B && p.N % J == 0 && row0 % J == 0);
     phase(1);
     if (!more) break;
     if (MODE == 2) fetch(bn_next);
@@ -905,6 +945,7 @@ __device__ __forceinline__ void score32_body(ScoreArgs p, const int blk, const i
       ck[jb] = col_k(ss[jb] + __shfl_xor(ss[jb], 32), bias, p);
     }
     const bool full = MODE == 0 && nv == S32_SN && bq * S32_SQ + S32_SQ <= p.B;  // workgroup-uniform
+    const float sgn_inf = p.scale >= 0.f ? __builtin_inff() : -__builtin_inff();
     const int64_t n0 = ni[0] < p.N ? ni[0] : 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -915,7 +956,7 @@ __device__ __forceinline__ void score32_body(ScoreArgs p, const int blk, const i
         float* orow = p.out + (int64_t)min(q, p.B - 1) * p.N + n0;
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb) {
-          const float sc = fmaf(-p.scale, pair_n2(acc[jb][r], rkq, ck[jb], p, nullptr, nullptr, nullptr), ck[jb].sb);
+          const float sc = pair_score_fast(acc[jb][r], rkq, ck[jb], p, sgn_inf);
           if (full || (q < p.B && ni[jb] < p.N)) orow[32 * jb] = sc;
         }
       } else {
@@ -924,7 +965,7 @@ __device__ __forceinline__ void score32_body(ScoreArgs p, const int blk, const i
 #pragma unroll
         for (int jb = 0; jb < 2; ++jb)
           if (ni[jb] < p.N)
-            cnt += fmaf(-p.scale, pair_n2(acc[jb][r], rkq, ck[jb], p, nullptr, nullptr, nullptr), ck[jb].sb) > t ? 1.f : 0.f;
+            cnt += pair_score_fast(acc[jb][r], rkq, ck[jb], p, sgn_inf) > t ? 1.f : 0.f;
         run_c[r] += cnt;  // an exact integer (< 2^24 per lane)
       }
     }
