@@ -153,6 +153,9 @@ class StepSpec:
         self.layer_norm, self.residual, self.c_radius = layer_norm, residual, c_radius
         self.w_g_param, self.tw = w_g_param, None
         self.need_h = True  # False: the timestep's Poincare rows h are not written (x, |h| are)
+        # False: x = log0 h and |h| are not written (predict's last timestep, whose consumers read
+        # h only); the 64-row tail honours it and the returned h carries no tangent cache
+        self.need_xr = True
 
 
 def _use_rowtail(V, n_rows, d, prev_t, drop_mask, pos_only):
@@ -328,6 +331,9 @@ def _run_rowtail(mode, g, x, r, rel, w_rel, nb, gamma, w_n, w_loop, w_evolve, c,
         desc.step_c_radius = float(step.c_radius)
         skip = not step.need_h and INNER_SKIP_H
         desc.step_h_out, desc.step_x_out, desc.step_r_out = None if skip else a(h), a(xn), a(rn)
+        if not step.need_xr and not skip and send is None:
+            desc.step_x_out = desc.step_r_out = None
+            xn = rn = None
         if step.tw is not None:
             desc.step_tw = a(step.tw)
             keep.append(step.tw)
@@ -492,7 +498,7 @@ class HyperbolicUnionRGCNLayer(nn.Module):
                               self.skip_bias.detach() if prev_t is not None else None,
                               _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only, gate=gate,
                               need_h=need_h)
-        return attach(h, xn, rn, c)
+        return attach(h, xn, rn, c) if xn is not None else h  # xn None: StepSpec.need_xr
 
 
 class LorentzRGCNLayer(nn.Module):
@@ -555,7 +561,7 @@ class LorentzRGCNLayer(nn.Module):
                               self.skip_bias.detach() if prev_t is not None else None,
                               _drop_mask(self, x), c, step=step, out=out, pos_only=pos_only, gate=gate,
                               need_h=need_h)
-        return attach(h, xn, rn, c)
+        return attach(h, xn, rn, c) if xn is not None else h  # xn None: StepSpec.need_xr
 
 
 class LorentzRGCNCell(nn.Module):

@@ -116,6 +116,8 @@ SPARSE_EXCHANGE = os.environ.get("REGCN_SPARSE_EXCHANGE", "1") != "0"
 OWNER_INIT = os.environ.get("REGCN_OWNER_INIT", "1") != "0"
 
 INIT_SKIP_H = os.environ.get("REGCN_INIT_SKIP_H", "1") != "0"  # see HyperbolicRecurrentRGCN._initial_state
+# predict's last timestep on the 64-row tail writes h only (StepSpec.need_xr); 0: x and |h| too
+LAST_SKIP_XR = os.environ.get("REGCN_LAST_SKIP_XR", "1") != "0"
 REL_INLINE_MAX_SPAN = 64  # longer r_to_e spans are averaged by the chunked segment-mean kernel first
 
 
@@ -422,6 +424,10 @@ class HyperbolicRecurrentRGCN(nn.Module):
                                 w_g_param=self.time_gate_weight)
                 # predict reads the last state's h only; the next timestep reads x and |h|
                 step.need_h = i == len(g_list) - 1 or not self.__dict__.get("_last_h_only")
+                # ... and its x and |h| are dead (the decoders read h; nothing follows the last
+                # timestep), unless ranks still exchange them (owner partition)
+                step.need_xr = not (LAST_SKIP_XR and i == len(g_list) - 1 and self.__dict__.get("_last_h_only")
+                                    and not isinstance(g, ShardedGraph))
                 self.h = self.rgcn.forward(g, self.h, [self.h_0, self.h_0], step=step)
             else:
                 # the timestep kernel reads every row of current_h (and recomputes x, |h| from
