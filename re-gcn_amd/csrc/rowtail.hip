@@ -791,8 +791,9 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     // otherwise sit between the blend and the stores
     const float rs = s.r_static[own_int(crow)];
     const float br = s.residual ? *s.b_r : 0.f;
-    float wr[NT];
+    float wr[NT], bg[NT];
     if (s.residual) rt_col<NT>(wr, s.w_r, d);
+    rt_col<NT>(bg, s.b_g, d);  // (the blend's gate bias: in flight under the row maps too)
     lz_project(z, k);
     if (s.layer_norm) {
       lz_log0(z, k);
@@ -801,8 +802,6 @@ __device__ __forceinline__ void rt_finish(const LayerArgs& p, RAcc<NT>& v, const
     }
     lz_log0(z, k);
     rt_apply<NT>(v, z);
-    float bg[NT];
-    rt_col<NT>(bg, s.b_g, d);
     if (sp) sp->mark(1);
     if constexpr (MODE == RT_STEP_PRE) {
       const float* xs = reinterpret_cast<const float*>(lds + wave_id() * 2 * RT_SC_BYTES);
@@ -928,7 +927,8 @@ __device__ __forceinline__ void rowtail_body(const LayerArgs& p, int row0) {
     for (int g = 0; g < RG; ++g) v[g].zero();
     rt_mm<NT, RG, true>(v, p.x, arow, valid, p.w_gate, d, KB, rt_lds);
 #pragma unroll
-    for (int g = 0; g < RG; ++g) rt_store<NT>(v[g], p.gate_out, R[g].crow, R[g].n_valid, d);
+    for (int g = 0; g < RG; ++g) rt_store_staged<NT>(v[g], p.gate_out, R[g], d, rt_lds, p, false);
+    __syncthreads();  // the waves' staging regions overlap the next product's first copies
   }
 #pragma unroll
   for (int g = 0; g < RG; ++g) v[g].zero();

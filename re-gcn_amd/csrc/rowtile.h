@@ -314,7 +314,10 @@ __device__ __forceinline__ void scale_known(Frag& a, float n2[4], const float f[
 // r = l & 3 (own_row), and each lane then takes row r's result from lane r of its DPP row
 // (row_newbcast, one VALU op): a quarter of the transcendental work, bit-identical values.
 __device__ __forceinline__ float own_row(const float v[4]) {
-  // a two-level select tree (a select chain on r == k is turned into a scratch array)
+  // a two-level select tree (a select chain on r == k is turned into a scratch array; in the
+  // step tail's radius residual, once the vectoriser pairs v's elements, this tree becomes one
+  // too -- a 32-B scratch round trip there; a bit-mask select (v_bfi_b32) avoided it but made
+  // the first-layer tail ~1 % slower and the step tail no faster: profiles/r6_bias_own_row_ab.jsonl)
   const bool b0 = threadIdx.x & 1, b1 = threadIdx.x & 2;
   const float lo = b0 ? v[1] : v[0], hi = b0 ? v[3] : v[2];
   return b1 ? hi : lo;

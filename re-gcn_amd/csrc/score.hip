@@ -682,6 +682,21 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     ss += __shfl_xor(ss, 4);
     if (sub == 0) e2s[buf * SNW + trow] = ss;
   };
+  // the per-candidate biases of a tile, loaded before its products (unconditional clamped loads,
+  // as fetch): loaded in the epilogue they put a memory round trip (~0.5-1k cycles, both waves of
+  // a SIMD at once) into every tile
+  float bcur[J];
+  auto load_bias = [&](int t, float (&b)[J]) {
+    if (!p.bias) {  // (uniform)
+#pragma unroll
+      for (int j = 0; j < J; ++j) b[j] = 0.f;
+      return;
+    }
+    int r0, nv;
+    tile_rows(t, r0, nv);
+#pragma unroll
+    for (int j = 0; j < J; ++j) b[j] = p.bias[r0 + min(J * (lane & 15) + j, max(nv - 1, 0))];
+  };
   fetch(bn);
   stash(0);
   __syncthreads();
@@ -703,6 +718,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     // next tile's rows in flight under this tile's MFMAs (MODE 2: after its epilogue, whose
     // live registers would otherwise spill)
     if (MODE != 2) fetch(min(bn_next, nbn - 1));
+    load_bias(bn, bcur);
     const float* brow = Es + cur * SNW * SE + (lane & 15) * SE + g4;
     f4 acc[J];
 #pragma unroll
@@ -750,9 +766,11 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
       const int c = J * (lane & 15) + j;  // the candidate at tile row 16 j + (lane & 15)
       ni[j] = c < nv ? row0 + c : 0x7fffffff;  // invalid: >= N
       y2[j] = e2s[cur * SNW + 16 * j + (lane & 15)];
-      bn_[j] = (ni[j] < p.N && p.bias) ? p.bias[ni[j]] : 0.f;
+      bn_[j] = bcur[j];  // (an invalid candidate's bias is never used)
     }
-    // vector stores need the row start aligned to J floats (wave-uniform)
+    // vector stores need the row start aligned to J floats (wave-uniform).  (Holding a full
+    // tile's scores in registers and storing them after the tile's barrier, off the next stash's
+    // vmcnt wait, was 7 % slower: profiles/r6_score_hold_ab.jsonl.)
     score_epilogue_fast<MODE, J, true>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se,
                                        MODE == 0 && nv == SNW && q0 + SQW <= p.B && p.N % J == 0 && row0 % J == 0);
     phase(1);
