@@ -71,11 +71,18 @@ __device__ __forceinline__ f4 clamp4(f4 v, float lo, float hi) {
 // max(x, slope x) = med3(x, slope x, +inf): two VALU, no compare / select, the same bits as
 // x >= 0 ? x : slope x.  Written as the instruction itself: the compiler folds the builtin into
 // maxnum(x, slope x) and, not knowing x canonical, quiets it first (v_max x, x): three VALU.
+#ifndef REGCN_LEAKY_ASM
+#define REGCN_LEAKY_ASM 1
+#endif
 __device__ __forceinline__ float leaky(float x) {
   const float slope = (1.0f / 8.0f + 1.0f / 3.0f) * 0.5f;
+#if REGCN_LEAKY_ASM
   float r;
   asm("v_med3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(x * slope), "s"(__builtin_inff()));
   return r;
+#else
+  return __builtin_amdgcn_fmed3f(x, x * slope, __builtin_inff());
+#endif
 }
 
 __device__ __forceinline__ f4 leaky4(f4 v) { return f4{leaky(v.x), leaky(v.y), leaky(v.z), leaky(v.w)}; }

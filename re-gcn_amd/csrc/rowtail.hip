@@ -60,8 +60,11 @@ int pack_weight_kp(const float* W, int d_in, int d_out, float* Wp, hipStream_t s
 // The inline in-edge rows of every in-degree > 0 tile (the tiles / items of the fused kernel),
 // finished (norm-scaled sum, or Lorentz centroid -> log0) and written to out[row]; rows over
 // the budget are skipped (out already holds them).
+#ifndef REGCN_GATHER_WAVES
+#define REGCN_GATHER_WAVES 5  // waves per SIMD the gather is compiled for (89 VGPRs: 5)
+#endif
 template <int AGG, int S>
-__global__ __launch_bounds__(NTHR) void k_gather_agg(LayerArgs p, float* __restrict__ out, int tile0) {
+__global__ __launch_bounds__(NTHR) __attribute__((amdgpu_waves_per_eu(REGCN_GATHER_WAVES))) void k_gather_agg(LayerArgs p, float* __restrict__ out, int tile0) {
   extern __shared__ float lds[];
   const int tile = tile0 + blockIdx.x;
   const int lda = tile_lda(p.d);

@@ -335,15 +335,16 @@ __device__ __forceinline__ float row16_max(float v) {
 
 constexpr float LOG2E = 1.4426950408889634f;
 
-// PERM: the lane's J candidates are consecutive (ni[j] = ni[0] + j: score_f32_body stages
-// candidate J i + j at tile row 16 j + i), so a query row's scores leave as one J-float vector
-// store per lane (`full` and vec-aligned), not J scattered 4-B stores; otherwise ni[j] =
-// ni[0] + 16 j.
-template <int MODE, int J, bool PERM = false>
+// perm: the lane's J candidates are consecutive (ni[j] = ni[0] + j: score_f32_body stages
+// candidate J i + j at tile row 16 j + i when N % J == 0), so a full tile's query row leaves as
+// one J-float vector store per lane, not J scattered 4-B stores; otherwise ni[j] = ni[0] + 16 j
+// (16 lanes store 64 contiguous bytes per instruction: with N % J != 0 the permuted order's
+// scalar stores, 16 B apart per lane, cost the dataset decoders 3-14 %).
+template <int MODE, int J>
 __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4* acc, const float* x2,
                                                     const float* y2, const float* bn_, const int* qi, const int* ni,
                                                     int lane, int bn, float* run_m, float* run_se,
-                                                    bool full = false) {
+                                                    bool full = false, bool perm = false) {
   RowK rk[4];
   ColK ck[J];
 #pragma unroll
@@ -353,9 +354,8 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
   const float mx2 = p.mx * p.mx;
   const float sgn_inf = p.scale >= 0.f ? __builtin_inff() : -__builtin_inff();
   if (MODE == 0) {
-    // the lane's candidates are ni[0] + CS j (each valid one): one row address per query row,
-    // the j steps as immediate store offsets
-    constexpr int CS = PERM ? 1 : 16;
+    // the lane's candidates are ni[0] + j (perm) or ni[0] + 16 j (each valid one): one row
+    // address per query row, the j steps as immediate store offsets
     const int64_t n0 = ni[0] < p.N ? ni[0] : 0;
     if (full) {  // every query row and candidate of the tile valid (wave-uniform): no store masks
 #pragma unroll
@@ -364,14 +364,19 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
         float sv[J];
 #pragma unroll
         for (int j = 0; j < J; ++j) sv[j] = pair_score_fast(acc[j][r], rk[r], ck[j], p, sgn_inf);
-        if constexpr (PERM && J == 4) {
-          *reinterpret_cast<f4*>(orow) = f4{sv[0], sv[1], sv[2], sv[3]};
-        } else if constexpr (PERM && J == 2) {
-          typedef float f2 __attribute__((ext_vector_type(2)));
-          *reinterpret_cast<f2*>(orow) = f2{sv[0], sv[1]};
+        if (perm) {  // (uniform)
+          if constexpr (J == 4) {
+            *reinterpret_cast<f4*>(orow) = f4{sv[0], sv[1], sv[2], sv[3]};
+          } else if constexpr (J == 2) {
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<f2*>(orow) = f2{sv[0], sv[1]};
+          } else {
+#pragma unroll
+            for (int j = 0; j < J; ++j) orow[j] = sv[j];
+          }
         } else {
 #pragma unroll
-          for (int j = 0; j < J; ++j) orow[CS * j] = sv[j];
+          for (int j = 0; j < J; ++j) orow[16 * j] = sv[j];
         }
       }
       return;
@@ -380,9 +385,15 @@ __device__ __forceinline__ void score_epilogue_fast(const ScoreArgs& p, const f4
     for (int r = 0; r < 4; ++r) {
       if (qi[r] >= p.B) continue;
       float* orow = p.out + (int64_t)qi[r] * p.N + n0;
+      if (perm) {
 #pragma unroll
-      for (int j = 0; j < J; ++j)
-        if (ni[j] < p.N) orow[CS * j] = pair_score_fast(acc[j][r], rk[r], ck[j], p, sgn_inf);
+        for (int j = 0; j < J; ++j)
+          if (ni[j] < p.N) orow[j] = pair_score_fast(acc[j][r], rk[r], ck[j], p, sgn_inf);
+      } else {
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+          if (ni[j] < p.N) orow[16 * j] = pair_score_fast(acc[j][r], rk[r], ck[j], p, sgn_inf);
+      }
     }
   } else if (MODE == 1) {  // this lane's running (max, sum exp) per query row, across tiles
 #pragma unroll
@@ -642,9 +653,11 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
   static_assert(64 * NW == 8 * SNW, "staging map: 8 threads per candidate row");
   constexpr int IT = (KBA * 4 + 7) / 8;
   const int sr = tid >> 3, sub = tid & 7, per_row = 4 * KB;
-  // candidate sr of the tile sits at tile row 16 (sr % J) + sr / J, so accumulator j of lane l
-  // holds candidate J (l & 15) + j: a lane's J candidates are consecutive (vector score stores)
-  const int trow = 16 * (sr % J) + sr / J;
+  // perm: candidate sr of the tile sits at tile row 16 (sr % J) + sr / J, so accumulator j of
+  // lane l holds candidate J (l & 15) + j: a lane's J candidates are consecutive (vector score
+  // stores); otherwise at tile row sr (lane l, accumulator j: candidate 16 j + (l & 15))
+  const bool perm = p.N % J == 0 && p.n_rng == 0;  // (uniform) see score_epilogue_fast
+  const int trow = perm ? 16 * (sr % J) + sr / J : sr;
   f4 v[IT];
   auto fetch = [&](int t) {  // unconditional clamped loads (a conditional load drains vmcnt)
     int row0, nv;
@@ -695,7 +708,7 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     int r0, nv;
     tile_rows(t, r0, nv);
 #pragma unroll
-    for (int j = 0; j < J; ++j) b[j] = p.bias[r0 + min(J * (lane & 15) + j, max(nv - 1, 0))];
+    for (int j = 0; j < J; ++j) b[j] = p.bias[r0 + min(perm ? J * (lane & 15) + j : 16 * j + (lane & 15), max(nv - 1, 0))];
   };
   fetch(bn);
   stash(0);
@@ -763,16 +776,16 @@ __device__ __forceinline__ void score_f32_body(ScoreArgs p, const int blk, const
     tile_rows(bn, row0, nv);
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const int c = J * (lane & 15) + j;  // the candidate at tile row 16 j + (lane & 15)
+      const int c = perm ? J * (lane & 15) + j : 16 * j + (lane & 15);  // at tile row 16 j + (lane & 15)
       ni[j] = c < nv ? row0 + c : 0x7fffffff;  // invalid: >= N
       y2[j] = e2s[cur * SNW + 16 * j + (lane & 15)];
       bn_[j] = bcur[j];  // (an invalid candidate's bias is never used)
     }
-    // vector stores need the row start aligned to J floats (wave-uniform).  (Holding a full
+    // (perm: every row start is aligned to J floats).  (Holding a full
     // tile's scores in registers and storing them after the tile's barrier, off the next stash's
     // vmcnt wait, was 7 % slower: profiles/r6_score_hold_ab.jsonl.)
-    score_epilogue_fast<MODE, J, true>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se,
-                                       MODE == 0 && nv == SNW && q0 + SQW <= p.B && p.N % J == 0 && row0 % J == 0);
+    score_epilogue_fast<MODE, J>(p, acc, x2, y2, bn_, qi, ni, lane, bn, run_m, run_se,
+                                 MODE == 0 && nv == SNW && q0 + SQW <= p.B, perm);
     phase(1);
     if (!more) break;
     if (MODE == 2) fetch(bn_next);
