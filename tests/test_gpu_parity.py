@@ -381,7 +381,11 @@ def test_score_and_ce_vs_golden(golden):
                  what="ce crel")
 
 
-@pytest.mark.parametrize("B,N,d", [(1, 1, 4), (5, 7, 12), (130, 1000, 200), (64, 64, 256)])
+# N % 4 == 0 stages the candidates permuted (a lane's four consecutive, one vector store per
+# query row); other N keep the plain order (score.hip score_f32_body `perm`): both, with
+# partial query and candidate tiles
+@pytest.mark.parametrize("B,N,d", [(1, 1, 4), (5, 7, 12), (130, 1000, 200), (64, 64, 256), (160, 2048, 200),
+                                   (300, 4099, 200), (129, 4160, 196)])
 def test_score_shapes_vs_oracle(B, N, d):
     from oracle import model as OM
     from oracle import ops as O
