@@ -676,3 +676,14 @@ def givens_rotation(x, angles, reflect=False):
             and x.shape[1] % 2 == 0):
         return _Givens.apply(x, angles, reflect)
     return None
+
+
+def batch_norm(bn, x):
+    """bn(x) (src/decoder.py's BatchNorm1d).  In eval mode through torch's native batch-norm
+    kernel instead of MIOpen's: MIOpenBatchNormFwdInferSpatialEst took ~140 us per call at the
+    ConvTransE / ConvTransR shapes, a third of the RE-GCN leg's kernel time
+    (profiles/r6_regcn_leg_kernel_stats.csv); the native kernel computes the same
+    (x - mean) / sqrt(var + eps) * weight + bias."""
+    if bn.training or torch.is_grad_enabled() or not x.is_cuda:
+        return bn(x)
+    return torch.native_batch_norm(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, False, 0.0, bn.eps)[0]

@@ -572,10 +572,10 @@ class HyperbolicConvTransE(nn.Module):
         et = 0.9 * torch.tanh(et) + 0.1 * et
         B = len(triplets)
         x = torch.cat([et[triplets[:, 0]].unsqueeze(1), rel_embedding[triplets[:, 1]].unsqueeze(1)], 1)
-        x = self.feature_map_drop(F.relu(self.bn1(self.conv1(self.inp_drop(self.bn0(x))))))
+        x = self.feature_map_drop(F.relu(_ag.batch_norm(self.bn1, self.conv1(self.inp_drop(_ag.batch_norm(self.bn0, x))))))
         x = self.hidden_drop(_ag.linear(self.fc, x.view(B, -1)))
         if B > 1:
-            x = self.bn2(x)
+            x = _ag.batch_norm(self.bn2, x)
         return torch.mm(F.relu(x), et.transpose(1, 0)) + self.b
 
 
@@ -601,6 +601,6 @@ class HyperbolicConvTransR(nn.Module):
         et = 0.9 * torch.tanh(et) + 0.1 * et
         B = len(triplets)
         x = torch.cat([et[triplets[:, 0]].unsqueeze(1), et[triplets[:, 2]].unsqueeze(1)], 1)
-        x = self.feature_map_drop(F.relu(self.bn1(self.conv1(self.inp_drop(self.bn0(x))))))
-        x = self.bn2(self.hidden_drop(_ag.linear(self.fc, x.view(B, -1))))
+        x = self.feature_map_drop(F.relu(_ag.batch_norm(self.bn1, self.conv1(self.inp_drop(_ag.batch_norm(self.bn0, x))))))
+        x = _ag.batch_norm(self.bn2, self.hidden_drop(_ag.linear(self.fc, x.view(B, -1))))
         return torch.mm(F.relu(x), rel_embedding.transpose(1, 0)) + self.b

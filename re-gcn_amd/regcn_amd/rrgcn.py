@@ -78,10 +78,10 @@ class ConvTransE(nn.Module):
         e_all = torch.tanh(embedding)
         B = len(triplets)
         x = torch.cat([e_all[triplets[:, 0]].unsqueeze(1), emb_rel[triplets[:, 1]].unsqueeze(1)], 1)
-        x = self.feature_map_drop(F.relu(self.bn1(self.conv1(self.inp_drop(self.bn0(x))))))
+        x = self.feature_map_drop(F.relu(_ag.batch_norm(self.bn1, self.conv1(self.inp_drop(_ag.batch_norm(self.bn0, x))))))
         x = self.hidden_drop(_ag.linear(self.fc, x.view(B, -1)))
         if B > 1:
-            x = self.bn2(x)
+            x = _ag.batch_norm(self.bn2, x)
         x = F.relu(x)
         return torch.mm(x, (e_all if partial_embeding is None else partial_embeding).transpose(1, 0))
 
@@ -109,8 +109,8 @@ class ConvTransR(nn.Module):
         e_all = torch.tanh(embedding)
         B = len(triplets)
         x = torch.cat([e_all[triplets[:, 0]].unsqueeze(1), e_all[triplets[:, 2]].unsqueeze(1)], 1)
-        x = self.feature_map_drop(F.relu(self.bn1(self.conv1(self.inp_drop(self.bn0(x))))))
-        x = self.bn2(self.hidden_drop(_ag.linear(self.fc, x.view(B, -1))))
+        x = self.feature_map_drop(F.relu(_ag.batch_norm(self.bn1, self.conv1(self.inp_drop(_ag.batch_norm(self.bn0, x))))))
+        x = _ag.batch_norm(self.bn2, self.hidden_drop(_ag.linear(self.fc, x.view(B, -1))))
         return torch.mm(F.relu(x), emb_rel.transpose(1, 0))
 
 
