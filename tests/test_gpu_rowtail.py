@@ -107,3 +107,25 @@ def test_rowtail_matches_fused_layers(encoder, residual, ln, d):
                 assert_close(a, b, what="rowtail (in-kernel gate) vs fused")
         finally:
             HL.ROWTAIL_MIN_ROWS = old
+
+
+def test_predict_last_step_writes_h_only(golden, rowtail_everywhere, monkeypatch):
+    """predict's last timestep on the 64-row tail writes h only (StepSpec.need_xr: its x and |h|
+    are read by nothing): the scores are bit for bit those of the run that writes them, and the
+    last state carries no tangent cache (a later tangent_of recomputes it instead of reading
+    unwritten rows)."""
+    from regcn_amd import hyperbolic_model as HM
+    z = golden("model_uvrgcn_roth_r512_d200.npz")
+    m, glist, (V, R, d, T) = build_hyperbolic_model(z, "uvrgcn_roth_r512_d200", DEV)
+    m.use_phases = False
+    test = torch.from_numpy(z["test"]).to(DEV)
+    outs = {}
+    for skip in (False, True):
+        monkeypatch.setattr(HM, "LAST_SKIP_XR", skip)
+        with torch.no_grad():
+            outs[skip] = [t.clone() for t in m.predict(glist, R, None, test, True)[1:]]
+            last = m._forward_last_h(glist, None, True)[0][-1]
+        assert (getattr(last, "_regcn_xr", None) is None) == skip, "tangent cache on the last state"
+    for a, b in zip(outs[False], outs[True]):
+        assert torch.equal(a, b)
+    assert_close(outs[True][0], z["score"], what="entity score")
