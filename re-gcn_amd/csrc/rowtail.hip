@@ -577,15 +577,15 @@ __device__ __forceinline__ void rt_store(const RAcc<NT>& a, float* __restrict__ 
   }
 }
 
+// lane l: column 16 t + (l & 15) of the d-vector v for each column tile t, through a buffer
+// resource of d floats: the tile is an immediate offset and columns >= d read 0 (no clamped
+// address or select per load)
 template <int NT>
 __device__ __forceinline__ void rt_col(float out[NT], const float* __restrict__ v, int d) {
-  const int lane = threadIdx.x & 63;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(v), (short)0, d * 4, 0x00020000);
+  const int vo = (int)(threadIdx.x & 15) * 4;
 #pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int col = 16 * t + (lane & 15);
-    const float x = v[min(col, d - 1)];
-    out[t] = col < d ? x : 0.f;
-  }
+  for (int t = 0; t < NT; ++t) out[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo + 64 * t, 0, 0));
 }
 
 __device__ __forceinline__ void rt_store_radius(const float n2[4], float* __restrict__ rad, const int crow[4],
